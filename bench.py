@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""BASELINE metric: rows/s of filter -> hash-join -> group-by over 1e9 fact rows.
+
+    SELECT d.g, SUM(f.v), COUNT(f.v) FROM fact f JOIN dim d ON f.k = d.k
+    WHERE f.x > 49 GROUP BY d.g
+
+fact: x Int64 in [0,100), k Int64 uniform in [0,1e7), v Float64 in [0,1)
+dim : k = a permutation of [0,1e7), g Int64 in [0,1024)        
+
+One step = one execution of the query over device-resident synthetic columns
+(data generated in HBM by the counter-based generator before timing): build
+the dim hash table, probe + filter + aggregate every fact row, finalize the
+groups, and for N>1 the partial->final aggregate exchange over RCCL.
+
+Multi-GPU (torchrun, one rank per GPU): every rank holds its own 1e9-row fact
+shard (weak scaling, BASELINE config 4) and the replicated dim (broadcast
+join: each rank generates it, no data-path collective); the partial
+per-group states are all-gathered over RCCL and merged on the device by a
+second HashAggregate (the reference's partial/final aggregate stage shape,
+crates/query-distributed/src/planner.rs:200-249).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "query-engine_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 0x5EED
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=1_000_000_000, help="fact rows per GPU")
+    ap.add_argument("--dim", type=int, default=10_000_000)
+    ap.add_argument("--groups", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=50_000_000, help="fact rows for the CPU baseline (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per launch of the probe kernel (tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement of the reference executor semantics) on a bounded
+    sample: the full dim table and the first `cpu-sample` fact rows, 1 thread."""
+    if args.cpu_sample <= 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit
+    n = args.cpu_sample
+    x = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, args.dim)
+    v = ob.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ob.generate(abi.GEN_PERMUTATION, SEED, 0, args.dim, args.dim)
+    dg = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 5, args.dim, args.groups)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    t0 = time.perf_counter()
+    ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, pred, ob.HostCol(dk),
+                             [ob.HostCol(dg)], [(AF.Sum, 2), (AF.Count, 2)])
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate, 1 thread, {n} fact rows x {args.dim} dim rows "
+                      f"(build included), {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    import torch
+    if dist:
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import qe_hip
+    from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit
+
+    torch.cuda.set_device(local)
+    stream = torch.cuda.Stream(local)
+    torch.cuda.set_stream(stream)  # a real stream handle: library kernels, copies and RCCL are ordered on it
+    ctx = qe_hip.Context(local)
+    ctx.set_stream(stream.cuda_stream)
+
+    n, nd = args.rows, args.dim
+    row0 = rank * n
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100, row0=row0)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd, row0=row0)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n, row0=row0)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, args.groups)
+    ctx.sync()
+    pred = binop(col(0, "f.x"), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
+
+    def step():
+        gk, ga, g = ctx.join_filter_aggregate([x, k, v], 1, pred, dk, [dg], aggs)
+        if not dist:
+            return gk, ga, g
+        # partial -> final: all-gather the partial (g, sum, count) rows (padded
+        # to the largest rank's group count) and merge them with a device
+        # HashAggregate(SUM, SUM) filtered on count > 0 (drops the padding).
+        gmax = torch.tensor([g], device="cuda", dtype=torch.int64)
+        tdist.all_reduce(gmax, op=tdist.ReduceOp.MAX)
+        m = int(gmax.item())
+        part = torch.zeros((3, m), device="cuda", dtype=torch.int64)
+        for i, c in enumerate([gk[0], ga[0], ga[1]]):
+            if g:
+                ctx.copy_d2d(part[i].data_ptr(), c.c.values, 8 * g)
+        allp = torch.empty((world, 3, m), device="cuda", dtype=torch.int64)
+        tdist.all_gather_into_tensor(allp, part)
+        allp = allp.permute(1, 0, 2).contiguous().view(3, world * m)
+        cols = [ctx.wrap_device(abi.DT_INT64, allp[0].data_ptr(), world * m),
+                ctx.wrap_device(abi.DT_FLOAT64, allp[1].data_ptr(), world * m),
+                ctx.wrap_device(abi.DT_INT64, allp[2].data_ptr(), world * m)]
+        fk, fa, fg = ctx.filter_aggregate(cols, binop(col(2), BinaryOp.Greater, lit(0)), [0],
+                                          [(AF.Sum, 1), (AF.Sum, 2)])
+        keep = (allp,)
+        return fk, fa, fg
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # timed region: K steps bracketed by barrier + synchronize
+    ctx.timing(True)
+    ctx.timing_reset()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    probe_ms, probe_launches = ctx.kernel_time("join_filter_aggregate")
+    build_ms, _ = ctx.kernel_time("join_build")
+    ctx.timing(False)
+
+    if dist:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity on the result: every selected row landed in exactly one group
+    gk, ga, g = res
+    counts, _ = ga[1].to_numpy()
+    total_rows = n * world
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = total_rows * args.steps / elapsed
+    avg_probe_ms = probe_ms / max(probe_launches, 1)
+    alg_bytes = 24.0 * n  # x, k, v read once per fact row
+    achieved = alg_bytes / (avg_probe_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("rows") == n and tj.get("kernel") == "join_filter_aggregate":
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = cpu_baseline(args)
+        line = {
+            "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic (counter-based splitmix64, generated in HBM; BASELINE.md §2)",
+            "config": {
+                "workload": "filter->hash-join->group-by (BASELINE metric query): SELECT d.g, SUM(f.v), COUNT(f.v) "
+                            "FROM fact f JOIN dim d ON f.k = d.k WHERE f.x > 49 GROUP BY d.g",
+                "fact_rows_per_gpu": n,
+                "dim_rows": nd,
+                "groups": args.groups,
+                "parallelism": f"fact sharded x{world}, dim replicated (broadcast join)"
+                               + (", RCCL partial->final aggregate" if dist else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_agg_rows<GM_JOIN,PM_TERMS,LDS> (qeh timer 'join_filter_aggregate')",
+                "kernel_ms": avg_probe_ms,
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "build_ms_per_step": build_ms / args.steps,
+            "result_groups": int(g),
+            "result_rows_counted": int(counts.sum()),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

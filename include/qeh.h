@@ -1,0 +1,263 @@
+/*
+ * qeh.h — C ABI of the MI355X (gfx950) physical-execution backend for
+ * AarambhDevHub/query-engine's `crates/query-executor`.
+ *
+ * Boundary (SURVEY.md §8 row b): the reference executes a closed enum
+ *   `PhysicalPlan` (crates/query-executor/src/physical_plan.rs:13-72) through
+ *   `QueryExecutor::execute(&self, &PhysicalPlan) -> Result<Vec<RecordBatch>>`
+ *   (crates/query-executor/src/executor.rs:19-21).  There is no operator trait,
+ *   so the drop-in is "same enum, same signature": a Rust `HipQueryExecutor`
+ *    walks the enum and calls the operator entry points
+ *   below, or hands the whole plan to `qeh_execute_plan`.
+ *
+ * Conventions
+ *   - Every function returns an `int` status (enum qeh_status).  On failure the
+ *     calling thread's message is available from qeh_last_error(); status codes
+ *     map onto `query_core::QueryError` (crates/query-core/src/error.rs:4-57):
+ *     QEH_E_OVERFLOW / QEH_E_DIV0 -> QueryError::ArrowError (arrow's
+ *     ArithmeticOverflow / DivideByZero), everything else -> ExecutionError.
+ *   - Column buffers passed to operator entry points are DEVICE pointers
+ *     (HBM-resident).  qeh_column mirrors an Arrow primitive array:
+ *     values + optional LSB-first validity bitmap + element offset.  Booleans
+ *     are bit-packed exactly as in Arrow.
+ *   - Output columns are allocated by the library from its device pool; the
+ *     caller releases them with qeh_column_release().  Input buffers are never
+ *     written or retained.
+ *   - A context is bound to one device and one HIP stream; all work is
+ *     enqueued on that stream.  Use one context per host thread.
+ */
+#ifndef QEH_H
+#define QEH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QEH_ABI_VERSION 1
+
+/* ---- status -------------------------------------------------------------- */
+enum qeh_status {
+    QEH_OK = 0,
+    QEH_E_INVALID = 1,     /* bad argument / shape                          */
+    QEH_E_OVERFLOW = 2,    /* checked integer arithmetic overflow           */
+    QEH_E_DIV0 = 3,        /* integer division by zero                      */
+    QEH_E_OOM = 4,         /* device allocation failed                      */
+    QEH_E_UNSUPPORTED = 5, /* operator / type not implemented on device     */
+    QEH_E_HIP = 6,         /* HIP runtime error                              */
+    QEH_E_TYPE = 7,        /* expression type error (reference error text)  */
+    QEH_E_INTERNAL = 8     /* kernel-side protocol failure (bounded spin)   */
+};
+
+/* ---- data types (subset of query_core::DataType, types.rs:5-40) ---------- */
+enum qeh_dtype {
+    QEH_DT_NULL = 0,
+    QEH_DT_BOOL = 1,
+    QEH_DT_INT32 = 2,
+    QEH_DT_INT64 = 3,
+    QEH_DT_FLOAT32 = 4,
+    QEH_DT_FLOAT64 = 5,
+    QEH_DT_UTF8 = 6,   /* values = byte buffer, offsets = int32[length+1] */
+    QEH_DT_UINT32 = 7  /* internal: row indices / permutations          */
+};
+
+/* An Arrow-layout column.  All pointers are device pointers. */
+typedef struct qeh_column {
+    int32_t dtype;            /* enum qeh_dtype                               */
+    int32_t owned;            /* 1 if allocated by the library (release it)   */
+    int64_t length;           /* logical rows                                 */
+    int64_t offset;           /* element offset into values/validity (Arrow)  */
+    int64_t null_count;       /* -1 = unknown                                 */
+    void *values;             /* element buffer (bit-packed for BOOL)         */
+    uint8_t *validity;        /* LSB-first bitmap, NULL = all valid           */
+    int32_t *offsets;         /* UTF8 only                                    */
+    int64_t values_bytes;     /* UTF8 only: size of the byte buffer           */
+} qeh_column;
+
+/* ---- expressions: postfix encoding of PhysicalExpr ------------------------
+ * physical_plan.rs:74-142.  Only the variants the converters emit
+ * (crates/query-pgwire/src/backend.rs:727-756) are representable:
+ * Column{index}, Literal(ScalarValue), BinaryExpr, UnaryExpr.  Children come
+ * before parents (post-order); the last node is the root.  Type coercion is
+ * NOT encoded: the library applies the reference's rules
+ * (operators.rs:616-709) itself.                                             */
+enum qeh_expr_kind {
+    QEH_EX_COLUMN = 1,
+    QEH_EX_LITERAL = 2,
+    QEH_EX_BINARY = 3,
+    QEH_EX_UNARY = 4
+};
+/* Same order as `BinaryOp` (physical_plan.rs:119-136; TsMatch excluded). */
+enum qeh_binop {
+    QEH_OP_ADD = 0, QEH_OP_SUB = 1, QEH_OP_MUL = 2, QEH_OP_DIV = 3, QEH_OP_MOD = 4,
+    QEH_OP_EQ = 5, QEH_OP_NEQ = 6, QEH_OP_LT = 7, QEH_OP_LTE = 8, QEH_OP_GT = 9,
+    QEH_OP_GTE = 10, QEH_OP_AND = 11, QEH_OP_OR = 12
+};
+/* `UnaryOp` (physical_plan.rs:138-142). */
+enum qeh_unop { QEH_UOP_NOT = 0, QEH_UOP_MINUS = 1 };
+
+typedef struct qeh_expr_node {
+    int32_t kind;        /* enum qeh_expr_kind                              */
+    int32_t op;          /* qeh_binop / qeh_unop                            */
+    int32_t index;       /* COLUMN: input column index                      */
+    int32_t lit_dtype;   /* LITERAL: enum qeh_dtype (NULL = ScalarValue::Null) */
+    int32_t lit_is_null; /* LITERAL: typed None (e.g. Int64(None))         */
+    int32_t _pad;
+    int64_t lit_i64;     /* BOOL/INT32/INT64 literal                        */
+    double lit_f64;      /* FLOAT32/FLOAT64 literal                         */
+} qeh_expr_node;
+
+typedef struct qeh_expr {
+    const qeh_expr_node *nodes;
+    int32_t n_nodes;
+} qeh_expr;
+
+/* ---- aggregates: `AggregateFunction` (physical_plan.rs:150-157) ---------- */
+enum qeh_agg_func {
+    QEH_AGG_COUNT = 0, QEH_AGG_SUM = 1, QEH_AGG_AVG = 2, QEH_AGG_MIN = 3, QEH_AGG_MAX = 4
+};
+typedef struct qeh_agg {
+    int32_t func;        /* enum qeh_agg_func                                */
+    int32_t column;      /* index into the aggregate-input column list       */
+} qeh_agg;
+
+/* ---- context / runtime --------------------------------------------------- */
+typedef struct qeh_ctx qeh_ctx;
+
+int qeh_abi_version(void);
+/* Thread-local message for the last failing call on this thread. */
+const char *qeh_last_error(void);
+
+int qeh_init(int device, qeh_ctx **out);
+int qeh_shutdown(qeh_ctx *ctx);
+/* Run on a caller-owned hipStream_t (e.g. torch's current stream); NULL =
+ * the context's own stream. */
+int qeh_set_stream(qeh_ctx *ctx, void *hip_stream);
+void *qeh_get_stream(qeh_ctx *ctx);
+int qeh_synchronize(qeh_ctx *ctx);
+
+/* Device memory through the context's caching pool (no hipMalloc on the hot
+ * path after warm-up). */
+int qeh_device_alloc(qeh_ctx *ctx, size_t bytes, void **out);
+int qeh_device_free(qeh_ctx *ctx, void *ptr);
+/* Return every cached block to the driver. */
+int qeh_pool_trim(qeh_ctx *ctx);
+int qeh_memcpy_h2d(qeh_ctx *ctx, void *dst, const void *src, size_t bytes);
+int qeh_memcpy_d2h(qeh_ctx *ctx, void *dst, const void *src, size_t bytes);
+int qeh_memcpy_d2d(qeh_ctx *ctx, void *dst, const void *src, size_t bytes); /* async */
+int qeh_memset(qeh_ctx *ctx, void *dst, int value, size_t bytes);
+int qeh_column_release(qeh_ctx *ctx, qeh_column *col);
+
+/* Per-kernel device timing (HIP events on the context stream).  When enabled
+ * every launch is bracketed by events; qeh_kernel_time() synchronises and
+ * returns total milliseconds and launch count for kernels whose name equals
+ * `name` since the last qeh_timing_reset(). */
+int qeh_timing_enable(qeh_ctx *ctx, int enable);
+int qeh_timing_reset(qeh_ctx *ctx);
+int qeh_kernel_time(qeh_ctx *ctx, const char *name, double *total_ms, int64_t *launches);
+
+/* ---- synthetic data (counter-based; identical on host: oracle/qe_oracle.c)
+ * value(row) = splitmix64((seed ^ (col_id << 56)) + row), then per kind:
+ *   UNIFORM_MOD : (int64)(u % modulus) + lo
+ *   UNIT_F64    : (double)(u >> 11) * 2^-53            in [0,1)
+ *   PERMUTATION : (row * 0x9E3779B1 + col_id) % modulus  (bijection when
+ *                 gcd(0x9E3779B1, modulus) == 1)                            */
+enum qeh_gen_kind { QEH_GEN_UNIFORM_MOD = 0, QEH_GEN_UNIT_F64 = 1, QEH_GEN_PERMUTATION = 2 };
+int qeh_generate(qeh_ctx *ctx, int kind, uint64_t seed, uint64_t col_id, int64_t row0,
+                 int64_t n, int64_t modulus, int64_t lo, void *out_values);
+
+/* ---- operators (each cites the reference operator it replaces) ----------- */
+
+/* Filter: executor.rs:131-155 (+ arrow filter_record_batch).  Evaluates
+ * `predicate` over `cols`, keeps rows where it is TRUE (NULL -> dropped),
+ * order-preserving, and gathers columns `out_idx[0..n_out)` into `out`.
+ * Non-boolean predicate -> QEH_E_TYPE "Filter predicate must return boolean". */
+int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+               const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows);
+
+/* Projection expression: operators.rs:13-62 evaluate_expr over one input.
+ * Column references are returned zero-copy (owned = 0). */
+int qeh_eval(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *expr,
+             int64_t n_rows, qeh_column *out);
+
+/* Result type of `expr` over inputs of the given dtypes (no device work).
+ * Mirrors the reference's typing; errors with the reference's message. */
+int qeh_expr_type(const int32_t *col_dtypes, int n_cols, const qeh_expr *expr, int32_t *out_dtype);
+
+/* HashAggregate: executor.rs:157-190, operators.rs:745-848.
+ * n_keys == 0: global aggregate -> one row (or zero rows when `input_batches`
+ * is 0, matching the reference's "no batches -> no row" quirk, executor.rs:178).
+ * n_keys >= 1: one row per distinct key tuple (NULL keys form one group);
+ * out_keys[n_keys], out_aggs[n_aggs] are filled; row order unspecified.
+ * Result types follow operators.rs:745-848 (COUNT Int64; SUM int->Int64,
+ * float->Float64; AVG Float64; MIN/MAX keep the input type).              */
+int qeh_hash_aggregate(qeh_ctx *ctx, const qeh_column *keys, int n_keys,
+                       const qeh_column *agg_inputs, int n_inputs, const qeh_agg *aggs,
+                       int n_aggs, int64_t input_batches, qeh_column *out_keys,
+                       qeh_column *out_aggs, int64_t *out_groups);
+
+/* Fused HashAggregate(Filter(input)): executor.rs:38-49 composed without
+ * materialising the filtered batch.  `predicate` (may be NULL) and the key /
+ * aggregate column indexes all refer to `cols`.  Output as qeh_hash_aggregate. */
+int qeh_filter_aggregate(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                         const int32_t *key_idx, int n_keys, const qeh_agg *aggs, int n_aggs,
+                         int64_t input_batches, qeh_column *out_keys, qeh_column *out_aggs,
+                         int64_t *out_groups);
+
+/* Inner equi-join: the intended semantics of executor.rs:363-381 (the
+ * reference ignores `on`).  Builds a hash table on
+ * `build_key`, probes with `probe_key` (NULL keys never match), and emits the
+ * matching (probe row, build row) pairs with probe payload columns first
+ * (left ++ right, executor.rs:532-537).  Row order unspecified.              */
+int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, const qeh_column *probe_cols,
+                        int n_probe_cols, const qeh_column *build_key,
+                        const qeh_column *build_cols, int n_build_cols, qeh_column *out_probe,
+                        qeh_column *out_build, int64_t *out_rows);
+
+/* Fused filter -> hash-join -> group-by (the BASELINE metric path):
+ *   SELECT <build group keys>, AGG(probe cols)... FROM probe JOIN build
+ *   ON probe.key = build.key WHERE <predicate over probe cols> GROUP BY <build keys>
+ * = HashAggregate(Filter(HashJoin(Scan probe, Scan build))) with the filter
+ * referring only to probe-side columns (physical_plan.rs:28-39; the planner's
+ * operator order, planner.rs:114-166).  `predicate` may be NULL.
+ * Group keys are build-side columns; aggregate inputs are probe-side columns.
+ * Output exactly as qeh_hash_aggregate over the joined+filtered rows.     */
+int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                              int probe_key_idx, const qeh_expr *predicate,
+                              const qeh_column *build_key, const qeh_column *build_group_keys,
+                              int n_group_keys, const qeh_agg *aggs, int n_aggs,
+                              qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups);
+
+/* Stable lexicographic sort -> permutation (UINT32 row ids) of the input.
+ * Intended semantics of `Sort` (physical_plan.rs:40-44; executor.rs:290-297
+ * is the identity): per-key ascending flag, NULLs first, floats totalOrder. */
+int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending,
+                     qeh_column *out_perm);
+
+/* Gather rows `indices` (UINT32 or INT64 device column) of `col`. */
+int qeh_take(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out);
+
+/* ROW_NUMBER() OVER (PARTITION BY part_keys ORDER BY order_keys): Int64 column
+ * aligned to input order; 1-based within each partition, ties broken by input
+ * position (docs/WINDOW_FUNCTIONS.md:44-65; `WindowFunctionType::RowNumber`,
+ * physical_plan.rs:160-179). */
+int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_part,
+                   const qeh_column *order_keys, int n_order, const int8_t *ascending,
+                   qeh_column *out_rn);
+
+/* Hash partitioning for multi-GPU exchange (model: Partitioner::partition_by_hash,
+ * crates/query-distributed/src/partition.rs:151-212; the hash function is not
+ * observable in results, §8 row a15).  Writes `counts[n_parts]` and a
+ * partition-major permutation (UINT32) so that rows of partition p are
+ * perm[offsets[p] .. offsets[p]+counts[p]), stable within a partition.
+ * NULL keys go to partition 0 (reference skips them when hashing,
+ * partition.rs:292-316, i.e. they hash like an empty key). */
+int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
+                       qeh_column *out_perm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QEH_H */

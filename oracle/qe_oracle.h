@@ -1,0 +1,67 @@
+/*
+ * qe_oracle.h — CPU ORACLE (test infrastructure only; never linked into the
+ * product).  A plain-C restatement of the reference executor's semantics for
+ * the hot path, used by tests/ as the checker and by bench.py as the timed
+ * CPU baseline ("port").  See qe_oracle.c for per-function citations.
+ *
+ * Parity pinning (DESIGN.md "Oracle"): the reference cannot be built here (no
+ * cargo/rustc, arrow-rs 53.4.1 not vendored) and its own tests pin almost
+ * nothing on this path, so this oracle is pinned by (a) the reference's known
+ * answers (config 1 on data/employees.csv, the sorted-merge and partition-
+ * conservation tests) and (b) golden vectors produced in the build container
+ * by Arrow C++ (pyarrow 25) for the arrow-rs kernel semantics the reference
+ * calls (tests/golden/, tools/gen_golden.py).  Join / group-by / sort /
+ * ROW_NUMBER follow the intended semantics of SURVEY.md §8.0 because the
+ * reference's implementations are stubs: for those, parity is against this
+ * restatement, not against reference output.
+ */
+#ifndef QE_ORACLE_H
+#define QE_ORACLE_H
+#include <stdint.h>
+
+/* dtypes and expression nodes share the numbering of include/qeh.h */
+#include "../include/qeh.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* host column: booleans/validity one byte per row (1 = true / valid) */
+typedef struct qo_col {
+    int32_t dtype;
+    int32_t _pad;
+    int64_t length;
+    void *values;   /* int32/int64/float/double/uint8(bool)/uint32 */
+    uint8_t *valid; /* NULL = all valid */
+} qo_col;
+
+const char *qo_last_error(void);
+void qo_free(void *p);
+void qo_col_free(qo_col *c);
+
+void qo_generate(int kind, uint64_t seed, uint64_t col_id, int64_t row0, int64_t n, int64_t modulus,
+                 int64_t lo, void *out);
+
+int qo_eval(const qo_col *cols, int n_cols, int64_t n_rows, const qeh_expr_node *nodes, int n_nodes,
+            qo_col *out);
+int qo_filter(const qo_col *cols, int n_cols, const qeh_expr_node *nodes, int n_nodes,
+              const int32_t *out_idx, int n_out, qo_col *out, int64_t *out_rows);
+int qo_hash_aggregate(const qo_col *keys, int n_keys, const qo_col *inputs, int n_inputs,
+                      const qeh_agg *aggs, int n_aggs, int64_t input_batches, qo_col *out_keys,
+                      qo_col *out_aggs, int64_t *out_groups);
+int qo_hash_join_inner(const qo_col *probe_key, const qo_col *probe_cols, int n_probe,
+                       const qo_col *build_key, const qo_col *build_cols, int n_build,
+                       qo_col *out_probe, qo_col *out_build, int64_t *out_rows);
+int qo_join_filter_aggregate(const qo_col *probe_cols, int n_probe, int probe_key_idx,
+                             const qeh_expr_node *pred, int n_pred, const qo_col *build_key,
+                             const qo_col *build_group_keys, int n_group_keys, const qeh_agg *aggs,
+                             int n_aggs, qo_col *out_keys, qo_col *out_aggs, int64_t *out_groups);
+int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int64_t n_rows,
+                    uint32_t *out_perm);
+int qo_row_number(const qo_col *part, int n_part, const qo_col *order, int n_order,
+                  const int8_t *ascending, int64_t n_rows, int64_t *out_rn);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+// Join hash tables in HBM (build side of HashJoinExec).
+//
+// Three layouts, chosen per build from the build keys' min/max:
+//   DIRECT  key range <= 4*n: uint32 array indexed by key-kmin, entry = payload+1
+//           (a "perfect hash": one 4-B read per probe, table <= 16 B/build row)
+//   PACKED  range < 2^(64-pbits): one uint64 per slot, entry = (key-kmin+1)<<pbits | payload,
+//           linear probing, load <= 0.6 -> one 8-B read per probe (same line almost always)
+//   WIDE    otherwise: int64 keys[] + uint32 payload[] + uint32 state[]
+// Payload = build row id (materialising join) or dense group id (fused
+// join->aggregate).  Tables are rebuilt per query (they live for one
+// HashJoin execution, like the reference's per-query Vec<RecordBatch>).
+#pragma once
+
+#include "device_common.h"
+
+namespace qeh {
+
+enum TableKind : int32_t { TK_DIRECT = 0, TK_PACKED = 1, TK_WIDE = 2 };
+
+struct HashTable {
+    int32_t kind;
+    int32_t pbits;       // PACKED: payload bits
+    int32_t unique;      // every build key distinct -> stop at first match
+    int32_t _pad;
+    uint64_t mask;       // PACKED/WIDE: capacity - 1
+    int64_t kmin;        // DIRECT/PACKED key base
+    int64_t kmax;
+    uint64_t range;      // DIRECT: entries
+    uint64_t *slots;     // PACKED entries / WIDE keys
+    uint32_t *payload;   // DIRECT entries / WIDE payloads
+    uint32_t *state;     // WIDE occupancy
+};
+
+// Probe `key`; calls f(payload) for every match (first match only when
+// unique).  Returns number of matches.
+template <class F>
+__device__ __forceinline__ int table_probe(const HashTable &t, int64_t key, F &&f) {
+    if (key < t.kmin || key > t.kmax) return 0;
+    if (t.kind == TK_DIRECT) {
+        uint32_t e = t.payload[(uint64_t)key - (uint64_t)t.kmin];
+        if (e == 0) return 0;
+        f(e - 1u);
+        return 1;
+    }
+    uint64_t h = hash64((uint64_t)key) & t.mask;
+    int found = 0;
+    if (t.kind == TK_PACKED) {
+        const uint64_t want = (uint64_t)key - (uint64_t)t.kmin + 1ull;
+        const uint64_t pm = (1ull << t.pbits) - 1ull;
+        for (uint64_t i = 0; i <= t.mask; ++i) {
+            uint64_t e = t.slots[h];
+            if (e == 0) break;
+            if ((e >> t.pbits) == want) {
+                f((uint32_t)(e & pm));
+                ++found;
+                if (t.unique) break;
+            }
+            h = (h + 1) & t.mask;
+        }
+        return found;
+    }
+    for (uint64_t i = 0; i <= t.mask; ++i) {
+        if (t.state[h] == 0) break;
+        if ((int64_t)t.slots[h] == key) {
+            f(t.payload[h]);
+            ++found;
+            if (t.unique) break;
+        }
+        h = (h + 1) & t.mask;
+    }
+    return found;
+}
+
+}  // namespace qeh

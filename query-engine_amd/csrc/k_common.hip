@@ -1,0 +1,228 @@
+// Shared kernels and host helpers: column views, device-wide scan, gather.
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "device_common.h"
+#include "ops.h"
+
+namespace qeh {
+
+ColRef make_colref(const qeh_column &c) {
+    ColRef r{};
+    r.dtype = c.dtype;
+    r.validity = c.validity;
+    r.vbit0 = c.offset;
+    size_t es = dtype_size(c.dtype);
+    if (c.dtype == QEH_DT_BOOL || c.dtype == QEH_DT_UTF8 || es == 0)
+        r.values = c.values;  // bit-addressed (BOOL) or offsets-addressed (UTF8)
+    else
+        r.values = (const char *)c.values + (size_t)c.offset * es;
+    return r;
+}
+
+int check_column(const qeh_column &c, const char *what) {
+    if (c.length < 0) return fail(QEH_E_INVALID, std::string(what) + ": negative length");
+    if (c.length > 0 && !c.values) return fail(QEH_E_INVALID, std::string(what) + ": null values pointer");
+    if (c.length >= (int64_t)0xFFFFFFFFll)
+        return fail(QEH_E_UNSUPPORTED, std::string(what) + ": more than 2^32-1 rows per column");
+    switch (c.dtype) {
+        case QEH_DT_BOOL: case QEH_DT_INT32: case QEH_DT_INT64: case QEH_DT_FLOAT32:
+        case QEH_DT_FLOAT64: case QEH_DT_UINT32:
+            return QEH_OK;
+        case QEH_DT_UTF8:
+            return QEH_OK;
+        default:
+            return fail(QEH_E_UNSUPPORTED, std::string(what) + ": unsupported column type");
+    }
+}
+
+int make_colset(const qeh_column *cols, int n, ColSet *out) {
+    if (n > kMaxCols)
+        return fail(QEH_E_UNSUPPORTED, "too many columns for one device operator (max " +
+                                           std::to_string(kMaxCols) + ")");
+    std::memset(out, 0, sizeof(*out));
+    out->n = n;
+    for (int i = 0; i < n; ++i) {
+        QEH_TRY(check_column(cols[i], "column"));
+        out->c[i] = make_colref(cols[i]);
+    }
+    return QEH_OK;
+}
+
+int kernel_error_status(uint32_t err, const char *op) {
+    if (err & kErrDiv0) return fail(QEH_E_DIV0, "Arrow error: Divide by zero error");
+    if (err & kErrModOverflow)
+        return fail(QEH_E_OVERFLOW, "attempt to calculate the remainder with overflow (the reference aborts here, operators.rs:720)");
+    if (err & kErrOverflow) return fail(QEH_E_OVERFLOW, "Arrow error: Arithmetic overflow");
+    if (err & kErrSpin) return fail(QEH_E_INTERNAL, std::string(op) + ": device protocol timeout");
+    return QEH_OK;
+}
+
+int forced_table_kind() {
+    const char *e = std::getenv("QEH_FORCE_TABLE");
+    if (!e) return -1;
+    if (!std::strcmp(e, "direct")) return TK_DIRECT;
+    if (!std::strcmp(e, "packed")) return TK_PACKED;
+    if (!std::strcmp(e, "wide")) return TK_WIDE;
+    return -1;
+}
+
+// ---- exclusive scan --------------------------------------------------------------
+constexpr int kScanItems = 4;                    // per thread
+constexpr int kScanTile = kBlock * kScanItems;   // 1024 per block
+
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *lds_wave, uint64_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+    }
+    if (lane == 63) lds_wave[w] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+    for (int i = 0; i < kBlock / 64; ++i) {
+        if (i < w) base += lds_wave[i];
+        tot += lds_wave[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+__global__ void k_scan_partials(const uint32_t *__restrict__ in, int64_t n, uint64_t *__restrict__ partial) {
+    __shared__ uint64_t lw[kBlock / 64];
+    int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i)
+        if (base + i < n) s += in[base + i];
+    uint64_t tot;
+    block_excl_scan_u64(s, lw, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of partial[0..nb) in place, total -> *total
+__global__ void k_scan_top(uint64_t *partial, int64_t nb, uint64_t *total) {
+    __shared__ uint64_t lw[kBlock / 64];
+    uint64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += kBlock) {
+        int64_t i = b0 + threadIdx.x;
+        uint64_t v = i < nb ? partial[i] : 0;
+        uint64_t tot;
+        uint64_t ex = block_excl_scan_u64(v, lw, &tot);
+        if (i < nb) partial[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void k_scan_apply(const uint32_t *__restrict__ in, int64_t n, const uint64_t *__restrict__ partial,
+                             uint64_t *__restrict__ out) {
+    __shared__ uint64_t lw[kBlock / 64];
+    int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        v[i] = base + i < n ? in[base + i] : 0;
+        s += v[i];
+    }
+    uint64_t tot;
+    uint64_t ex = block_excl_scan_u64(s, lw, &tot) + partial[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        if (base + i < n) out[base + i] = ex;
+        ex += v[i];
+    }
+}
+
+int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total) {
+    if (n <= 0) {
+        if (total) *total = 0;
+        return QEH_OK;
+    }
+    int64_t nb = (n + kScanTile - 1) / kScanTile;
+    DevBuf part, tot;
+    QEH_TRY(part.alloc(ctx, (size_t)nb * 8));
+    QEH_TRY(tot.alloc(ctx, 8));
+    {
+        KernelTimer kt(ctx, "scan");
+        hipLaunchKernelGGL(k_scan_partials, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, in, n, part.as<uint64_t>());
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, ctx->stream, part.as<uint64_t>(), nb, tot.as<uint64_t>());
+        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, in, n, part.as<uint64_t>(), out);
+    }
+    QEH_HIP(hipGetLastError());
+    if (total) QEH_TRY(read_small(ctx, total, tot.p, 8));
+    return QEH_OK;
+}
+
+// ---- gather --------------------------------------------------------------------
+// out[i] = src[idx[i]]; one wave writes 64 consecutive rows so that the
+// validity / boolean words are produced by a single ballot.
+template <typename T>
+__global__ void k_gather(ColRef src, const uint32_t *__restrict__ idx, int64_t m, T *__restrict__ out,
+                         uint64_t *__restrict__ out_valid) {
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w * 64 < m; w += nwaves) {
+        int64_t i = w * 64 + lane;
+        bool live = i < m;
+        uint32_t j = live ? idx[i] : 0;
+        bool valid = live && col_valid(src, j);
+        if (live) out[i] = ((const T *)src.values)[j];
+        if (out_valid) {
+            uint64_t b = __ballot(valid);
+            if (lane == 0) out_valid[w] = b;
+        }
+    }
+}
+
+__global__ void k_gather_bool(ColRef src, const uint32_t *__restrict__ idx, int64_t m, uint64_t *__restrict__ out,
+                              uint64_t *__restrict__ out_valid) {
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w * 64 < m; w += nwaves) {
+        int64_t i = w * 64 + lane;
+        bool live = i < m;
+        uint32_t j = live ? idx[i] : 0;
+        bool v = live && bit_at((const uint8_t *)src.values, src.vbit0 + j);
+        bool valid = live && col_valid(src, j);
+        uint64_t bv = __ballot(v), bn = __ballot(valid);
+        if (lane == 0) {
+            out[w] = bv;
+            if (out_valid) out_valid[w] = bn;
+        }
+    }
+}
+
+int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out) {
+    QEH_TRY(check_column(src, "gather"));
+    if (src.dtype == QEH_DT_UTF8) return fail(QEH_E_UNSUPPORTED, "gather of Utf8 columns is not implemented on the device");
+    bool with_valid = src.validity != nullptr;
+    QEH_TRY(alloc_column(ctx, src.dtype, m, with_valid, out));
+    if (m == 0) return QEH_OK;
+    ColRef s = make_colref(src);
+    int grid = grid_for(ctx, (m + 63) / 64, kBlock / 64, 8);
+    KernelTimer kt(ctx, "gather");
+    switch (src.dtype) {
+        case QEH_DT_BOOL:
+            hipLaunchKernelGGL(k_gather_bool, dim3(grid), dim3(kBlock), 0, ctx->stream, s, idx, m,
+                               (uint64_t *)out->values, (uint64_t *)out->validity);
+            break;
+        case QEH_DT_INT32: case QEH_DT_FLOAT32: case QEH_DT_UINT32:
+            hipLaunchKernelGGL(k_gather<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, s, idx, m,
+                               (uint32_t *)out->values, (uint64_t *)out->validity);
+            break;
+        default:
+            hipLaunchKernelGGL(k_gather<uint64_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, s, idx, m,
+                               (uint64_t *)out->values, (uint64_t *)out->validity);
+            break;
+    }
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+}  // namespace qeh

@@ -1,0 +1,55 @@
+// Host-side helpers shared between operator translation units.
+#pragma once
+
+#include "expr.h"
+#include "grouptable.h"
+#include "hashtable.h"
+#include "qeh_internal.h"
+
+namespace qeh {
+
+// qeh_column -> kernel view.  Validation of dtype/length happens in callers.
+ColRef make_colref(const qeh_column &c);
+int check_column(const qeh_column &c, const char *what);
+int make_colset(const qeh_column *cols, int n, ColSet *out);
+
+// Device-wide exclusive scan of uint32 counts into uint64 offsets; returns
+// the total through *total (synchronous read).  `out` may alias nothing.
+int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total);
+
+// Join hash table built over `key` with payload either row ids
+// (row_payload == nullptr) or row_payload[row].
+struct BuiltTable {
+    HashTable t{};
+    DevBuf slots, payload, state;
+    int64_t n_inserted = 0;
+};
+int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload,
+                     uint64_t payload_max, BuiltTable *out, int force_kind = -1);
+
+// Group table over key tuples: slots hold a representative row id; dense ids
+// 0..G-1 follow slot order.  rep_row[g] = a row carrying group g's key.
+struct GroupTable {
+    KeyCols keys{};
+    DevBuf slots;    // uint32[cap], EMPTY = 0xFFFFFFFF
+    DevBuf dense;    // uint64[cap] dense id per occupied slot
+    DevBuf rep_row;  // uint32[G]
+    uint64_t cap = 0;
+    int64_t groups = 0;
+};
+int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *out,
+                      uint32_t *slot_of_row /* optional, device uint32[n_rows] */);
+// build_group_table + per-row dense ids (uint32[n_rows]).
+int assign_group_ids(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
+                     DevBuf *gid_of_row);
+
+// Gather rows `idx[0..m)` of a column into a new owned column.
+int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out);
+
+// Error word -> status.
+int kernel_error_status(uint32_t err, const char *op);
+
+// Environment knob for forcing a table layout in tests ("direct"/"packed"/"wide").
+int forced_table_kind();
+
+}  // namespace qeh

@@ -1,0 +1,157 @@
+// Internal host-side runtime of the qeh backend: context, caching device pool,
+// per-thread error string, launch/timing helpers.  Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/qeh.h"
+
+namespace qeh {
+
+// ---- errors ----------------------------------------------------------------
+void set_error(const std::string &msg);
+int fail(int status, const std::string &msg);
+
+#define QEH_HIP(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return ::qeh::fail(QEH_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define QEH_TRY(expr)               \
+    do {                            \
+        int _s = (expr);            \
+        if (_s != QEH_OK) return _s; \
+    } while (0)
+
+// ---- caching device pool ----------------------------------------------------
+// Size-class free lists (powers of two >= 256 B, exact size above 1 GiB).
+// Freed blocks are kept for reuse so steady-state queries never call
+// hipMalloc / hipFree (which would also serialise the device).
+class DevicePool {
+  public:
+    explicit DevicePool(int device) : device_(device) {}
+    int device() const { return device_; }
+    ~DevicePool();
+    int alloc(size_t bytes, void **out);
+    int free(void *p);
+    void trim();
+    size_t bytes_in_use() const { return in_use_; }
+
+  private:
+    static size_t size_class(size_t bytes);
+    int device_;
+    std::mutex mu_;
+    std::multimap<size_t, void *> free_;        // class size -> block
+    std::unordered_map<void *, size_t> live_;   // block -> class size
+    size_t in_use_ = 0;
+};
+
+// ---- per-kernel timing --------------------------------------------------------
+struct TimingRecord {
+    std::string name;
+    hipEvent_t start, stop;
+};
+
+}  // namespace qeh
+
+struct qeh_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    qeh::DevicePool *pool = nullptr;
+    hipDeviceProp_t props{};
+    // small scratch (status words, counters, flags), zeroed per call
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // pinned host staging for small device->host results
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
+    // timing
+    bool timing = false;
+    std::vector<qeh::TimingRecord> timing_pending;
+    std::vector<hipEvent_t> event_free;
+    std::map<std::string, std::pair<double, int64_t>> timing_done;
+};
+
+namespace qeh {
+
+// Scoped device selection for every entry point.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// RAII device buffer from the pool.
+struct DevBuf {
+    qeh_ctx *ctx = nullptr;
+    void *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { reset(); }
+    int alloc(qeh_ctx *c, size_t bytes) {
+        reset();
+        ctx = c;
+        n = bytes;
+        return c->pool->alloc(bytes ? bytes : 1, &p);
+    }
+    void reset() {
+        if (p && ctx) ctx->pool->free(p);
+        p = nullptr;
+        n = 0;
+    }
+    void *release() {
+        void *r = p;
+        p = nullptr;
+        return r;
+    }
+    template <class T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+// Event bracketing for named kernels (only when ctx->timing).
+struct KernelTimer {
+    qeh_ctx *ctx;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(qeh_ctx *c, const char *n);
+    ~KernelTimer();
+};
+
+// Pinned staging for small D2H results.
+int read_small(qeh_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes);
+// Zeroed scratch words (status / counters) valid until the next call.
+int scratch_zeroed(qeh_ctx *ctx, size_t bytes, void **out);
+
+// Grid sizing: persistent-ish grids of `per_cu` blocks per CU.
+inline int grid_for(qeh_ctx *ctx, int64_t work_items, int items_per_block, int per_cu = 8) {
+    int64_t want = (work_items + items_per_block - 1) / items_per_block;
+    int64_t cap = (int64_t)ctx->props.multiProcessorCount * per_cu;
+    if (want > cap) want = cap;
+    if (want < 1) want = 1;
+    return (int)want;
+}
+
+size_t dtype_size(int dt);
+int alloc_column(qeh_ctx *ctx, int dtype, int64_t length, bool with_validity, qeh_column *out);
+
+}  // namespace qeh

@@ -1,0 +1,10 @@
+"""qe_hip — Python binding of the MI355X qeh backend (C ABI: include/qeh.h).
+
+Import with the package directory on sys.path:
+    sys.path.insert(0, "<repo>/query-engine_amd"); import qe_hip
+"""
+from . import abi  # noqa: F401
+from .abi import QehError, load  # noqa: F401
+from .device import Context, DeviceColumn, agg  # noqa: F401
+from .expr import (AggregateExpr, AggregateFunction, BinaryExpr, BinaryOp, Column,  # noqa: F401
+                   Literal, PhysicalExpr, ScalarValue, UnaryExpr, UnaryOp, binop, col, lit)

@@ -1,0 +1,323 @@
+"""Device context and column handles over the qeh C ABI.
+
+Host data enters as numpy arrays (values + optional boolean validity) laid out
+exactly like Arrow primitive arrays once on the device (bit-packed booleans and
+LSB-first validity bitmaps).  Every operator wrapper calls one C entry point of
+include/qeh.h; nothing here computes results on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .expr import AggregateExpr, PhysicalExpr
+
+NP_OF = {abi.DT_INT32: np.int32, abi.DT_INT64: np.int64, abi.DT_FLOAT32: np.float32,
+         abi.DT_FLOAT64: np.float64, abi.DT_UINT32: np.uint32}
+DT_OF = {np.dtype(np.int32): abi.DT_INT32, np.dtype(np.int64): abi.DT_INT64,
+         np.dtype(np.float32): abi.DT_FLOAT32, np.dtype(np.float64): abi.DT_FLOAT64,
+         np.dtype(np.uint32): abi.DT_UINT32, np.dtype(np.bool_): abi.DT_BOOL}
+
+
+def pack_bits(b: np.ndarray) -> np.ndarray:
+    """bool[n] -> Arrow LSB-first bitmap bytes, padded to 8 bytes."""
+    bits = np.packbits(np.asarray(b, dtype=bool), bitorder="little")
+    pad = (-len(bits)) % 8
+    return np.concatenate([bits, np.zeros(pad + (8 if len(bits) == 0 else 0), np.uint8)])
+
+
+def unpack_bits(buf: np.ndarray, n: int, offset: int = 0) -> np.ndarray:
+    return np.unpackbits(buf, bitorder="little")[offset:offset + n].astype(bool)
+
+
+class DeviceColumn:
+    """An Arrow-layout column in HBM.  `owned` columns came from the library
+    pool (released with qeh_column_release); uploaded columns are owned by
+    this handle's context allocations."""
+
+    def __init__(self, ctx: "Context", c: abi.QehColumn, bufs: Sequence[int] = ()):
+        self.ctx = ctx
+        self.c = c
+        self._bufs = list(bufs)  # pool buffers this handle allocated itself
+
+    @property
+    def dtype(self) -> int:
+        return self.c.dtype
+
+    def __len__(self) -> int:
+        return self.c.length
+
+    def release(self) -> None:
+        if self.ctx is None:
+            return
+        if self.c.owned:
+            abi.check(self.ctx.lib.qeh_column_release(self.ctx.h, C.byref(self.c)))
+        for b in self._bufs:
+            self.ctx.free(b)
+        self._bufs = []
+        self.ctx = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+    def to_numpy(self) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """(values, validity-or-None) copied to the host."""
+        n, off = self.c.length, self.c.offset
+        ctx = self.ctx
+        valid = None
+        if self.c.validity and n > 0:
+            nbytes = (off + n + 7) // 8
+            vb = np.empty(nbytes, np.uint8)
+            ctx.d2h(vb, self.c.validity, nbytes)
+            valid = unpack_bits(vb, n, off)
+        elif self.c.validity:
+            valid = np.zeros(0, bool)
+        if self.c.dtype == abi.DT_BOOL:
+            nbytes = (off + n + 7) // 8
+            vb = np.empty(max(nbytes, 1), np.uint8)
+            if n > 0:
+                ctx.d2h(vb, self.c.values, nbytes)
+            return unpack_bits(vb, n, off), valid
+        npdt = NP_OF[self.c.dtype]
+        out = np.empty(n, npdt)
+        if n > 0:
+            ctx.d2h(out, self.c.values + off * out.itemsize, n * out.itemsize)
+        return out, valid
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.lib = abi.load()
+        h = C.c_void_p()
+        abi.check(self.lib.qeh_init(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            abi.check(self.lib.qeh_shutdown(self.h))
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- memory ----------------------------------------------------------
+    def alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        abi.check(self.lib.qeh_device_alloc(self.h, max(int(nbytes), 8), C.byref(p)))
+        return p.value
+
+    def free(self, p: int) -> None:
+        abi.check(self.lib.qeh_device_free(self.h, p))
+
+    def h2d(self, dst: int, src: np.ndarray) -> None:
+        src = np.ascontiguousarray(src)
+        abi.check(self.lib.qeh_memcpy_h2d(self.h, dst, src.ctypes.data, src.nbytes))
+
+    def d2h(self, dst: np.ndarray, src: int, nbytes: int) -> None:
+        abi.check(self.lib.qeh_memcpy_d2h(self.h, dst.ctypes.data, src, nbytes))
+
+    def sync(self) -> None:
+        abi.check(self.lib.qeh_synchronize(self.h))
+
+    def set_stream(self, stream_handle: int) -> None:
+        abi.check(self.lib.qeh_set_stream(self.h, stream_handle))
+
+    # ---- timing ----------------------------------------------------------
+    def timing(self, on: bool) -> None:
+        abi.check(self.lib.qeh_timing_enable(self.h, 1 if on else 0))
+
+    def timing_reset(self) -> None:
+        abi.check(self.lib.qeh_timing_reset(self.h))
+
+    def kernel_time(self, name: str) -> Tuple[float, int]:
+        ms, n = C.c_double(), C.c_int64()
+        abi.check(self.lib.qeh_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    # ---- columns ---------------------------------------------------------
+    def upload(self, values: np.ndarray, valid: Optional[np.ndarray] = None, offset: int = 0) -> DeviceColumn:
+        """numpy -> Arrow-layout device column.  `offset` prepends that many
+        padding rows and records them as the Arrow array offset (exercises
+        non-zero offsets)."""
+        values = np.asarray(values)
+        dt = DT_OF.get(values.dtype)
+        if dt is None:
+            raise TypeError(f"unsupported dtype {values.dtype}")
+        n = len(values)
+        c = abi.QehColumn(dtype=dt, owned=0, length=n, offset=offset, null_count=0)
+        bufs = []
+        if dt == abi.DT_BOOL:
+            host = pack_bits(np.concatenate([np.zeros(offset, bool), values]))
+        else:
+            host = np.concatenate([np.zeros(offset, values.dtype), values])
+        p = self.alloc(max(host.nbytes, 8))
+        bufs.append(p)
+        if host.nbytes:
+            self.h2d(p, host)
+        c.values = p
+        if valid is not None:
+            valid = np.asarray(valid, bool)
+            vb = pack_bits(np.concatenate([np.zeros(offset, bool), valid]))
+            q = self.alloc(max(vb.nbytes, 8))
+            bufs.append(q)
+            self.h2d(q, vb)
+            c.validity = q
+            c.null_count = int(n - valid.sum())
+        return DeviceColumn(self, c, bufs)
+
+    def empty(self, dtype: int, n: int) -> DeviceColumn:
+        """Uninitialised device column (no validity) from the pool."""
+        item = np.dtype(NP_OF[dtype]).itemsize
+        p = self.alloc(max(n * item, 8))
+        c = abi.QehColumn(dtype=dtype, owned=0, length=n, offset=0, null_count=0, values=p)
+        return DeviceColumn(self, c, [p])
+
+    def generate(self, kind: int, seed: int, col_id: int, n: int, modulus: int = 0, lo: int = 0,
+                 row0: int = 0) -> DeviceColumn:
+        dt = abi.DT_FLOAT64 if kind == abi.GEN_UNIT_F64 else abi.DT_INT64
+        col = self.empty(dt, n)
+        abi.check(self.lib.qeh_generate(self.h, kind, seed, col_id, row0, n, modulus, lo, col.c.values))
+        return col
+
+    def _wrap(self, c: abi.QehColumn) -> DeviceColumn:
+        return DeviceColumn(self, c)
+
+    @staticmethod
+    def _cols(cols: Sequence[DeviceColumn]):
+        arr = (abi.QehColumn * max(len(cols), 1))(*[x.c for x in cols])
+        return arr
+
+    # ---- operators -------------------------------------------------------
+    def filter(self, cols: Sequence[DeviceColumn], predicate: PhysicalExpr,
+               out_idx: Optional[Sequence[int]] = None) -> Tuple[List[DeviceColumn], int]:
+        out_idx = list(range(len(cols))) if out_idx is None else list(out_idx)
+        e, keep = predicate.to_c()
+        cin = self._cols(cols)
+        oi = (C.c_int32 * max(len(out_idx), 1))(*out_idx)
+        cout = (abi.QehColumn * max(len(out_idx), 1))()
+        rows = C.c_int64()
+        abi.check(self.lib.qeh_filter(self.h, cin, len(cols), C.byref(e), oi, len(out_idx), cout, C.byref(rows)))
+        return [self._wrap(cout[i]) for i in range(len(out_idx))], rows.value
+
+    def eval(self, cols: Sequence[DeviceColumn], expr: PhysicalExpr, n_rows: Optional[int] = None) -> DeviceColumn:
+        e, keep = expr.to_c()
+        cin = self._cols(cols)
+        out = abi.QehColumn()
+        n = n_rows if n_rows is not None else (len(cols[0]) if cols else 0)
+        abi.check(self.lib.qeh_eval(self.h, cin, len(cols), C.byref(e), n, C.byref(out)))
+        if not out.owned:  # zero-copy column reference: keep the source alive
+            src = cols[expr.index]
+            return DeviceColumn(self, out, []), src
+        return self._wrap(out)
+
+    def hash_aggregate(self, keys: Sequence[DeviceColumn], inputs: Sequence[DeviceColumn],
+                       aggs: Sequence[Tuple[int, int]], input_batches: int = 1):
+        ck, ci = self._cols(keys), self._cols(inputs)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        ok = (abi.QehColumn * max(len(keys), 1))()
+        oa = (abi.QehColumn * max(len(aggs), 1))()
+        g = C.c_int64()
+        abi.check(self.lib.qeh_hash_aggregate(self.h, ck, len(keys), ci, len(inputs), ca, len(aggs),
+                                              input_batches, ok, oa, C.byref(g)))
+        if g.value == 0 and not ok[0].values and not oa[0].values:
+            return [], [], 0
+        return [self._wrap(ok[i]) for i in range(len(keys))], [self._wrap(oa[i]) for i in range(len(aggs))], g.value
+
+    def filter_aggregate(self, cols: Sequence[DeviceColumn], predicate: Optional[PhysicalExpr],
+                         key_idx: Sequence[int], aggs: Sequence[Tuple[int, int]], input_batches: int = 1):
+        cc = self._cols(cols)
+        ki = (C.c_int32 * max(len(key_idx), 1))(*key_idx)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        ok = (abi.QehColumn * max(len(key_idx), 1))()
+        oa = (abi.QehColumn * max(len(aggs), 1))()
+        g = C.c_int64()
+        if predicate is not None:
+            e, keep = predicate.to_c()
+            ep = C.byref(e)
+        else:
+            ep = None
+        abi.check(self.lib.qeh_filter_aggregate(self.h, cc, len(cols), ep, ki, len(key_idx), ca, len(aggs),
+                                                input_batches, ok, oa, C.byref(g)))
+        if g.value == 0 and not oa[0].values:
+            return [], [], 0
+        return [self._wrap(ok[i]) for i in range(len(key_idx))], [self._wrap(oa[i]) for i in range(len(aggs))], g.value
+
+    def copy_d2d(self, dst: int, src: int, nbytes: int) -> None:
+        abi.check(self.lib.qeh_memcpy_d2d(self.h, dst, src, nbytes))
+
+    def wrap_device(self, dtype: int, ptr: int, n: int, validity: int = 0) -> DeviceColumn:
+        """View caller-owned device memory (e.g. a torch tensor) as a column."""
+        c = abi.QehColumn(dtype=dtype, owned=0, length=n, offset=0, null_count=0 if not validity else -1,
+                          values=ptr, validity=validity or None)
+        return DeviceColumn(self, c, [])
+
+    def hash_join_inner(self, probe_key: DeviceColumn, probe_cols: Sequence[DeviceColumn],
+                        build_key: DeviceColumn, build_cols: Sequence[DeviceColumn]):
+        cp, cb = self._cols(probe_cols), self._cols(build_cols)
+        op = (abi.QehColumn * max(len(probe_cols), 1))()
+        ob = (abi.QehColumn * max(len(build_cols), 1))()
+        rows = C.c_int64()
+        abi.check(self.lib.qeh_hash_join_inner(self.h, C.byref(probe_key.c), cp, len(probe_cols),
+                                               C.byref(build_key.c), cb, len(build_cols), op, ob, C.byref(rows)))
+        return ([self._wrap(op[i]) for i in range(len(probe_cols))],
+                [self._wrap(ob[i]) for i in range(len(build_cols))], rows.value)
+
+    def join_filter_aggregate(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                              predicate: Optional[PhysicalExpr], build_key: DeviceColumn,
+                              build_group_keys: Sequence[DeviceColumn], aggs: Sequence[Tuple[int, int]]):
+        cp = self._cols(probe_cols)
+        cg = self._cols(build_group_keys)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        ok = (abi.QehColumn * max(len(build_group_keys), 1))()
+        oa = (abi.QehColumn * max(len(aggs), 1))()
+        g = C.c_int64()
+        if predicate is not None:
+            e, keep = predicate.to_c()
+            ep = C.byref(e)
+        else:
+            ep = None
+        abi.check(self.lib.qeh_join_filter_aggregate(self.h, cp, len(probe_cols), probe_key_idx, ep,
+                                                     C.byref(build_key.c), cg, len(build_group_keys), ca,
+                                                     len(aggs), ok, oa, C.byref(g)))
+        return ([self._wrap(ok[i]) for i in range(len(build_group_keys))],
+                [self._wrap(oa[i]) for i in range(len(aggs))], g.value)
+
+    def sort_indices(self, keys: Sequence[DeviceColumn], ascending: Sequence[bool]) -> DeviceColumn:
+        ck = self._cols(keys)
+        asc = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in ascending])
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_sort_indices(self.h, ck, len(keys), asc, C.byref(out)))
+        return self._wrap(out)
+
+    def take(self, col: DeviceColumn, indices: DeviceColumn) -> DeviceColumn:
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_take(self.h, C.byref(col.c), C.byref(indices.c), C.byref(out)))
+        return self._wrap(out)
+
+    def row_number(self, part: Sequence[DeviceColumn], order: Sequence[DeviceColumn],
+                   ascending: Sequence[bool]) -> DeviceColumn:
+        cp, co = self._cols(part), self._cols(order)
+        asc = (C.c_int8 * max(len(order), 1))(*[1 if a else 0 for a in ascending])
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_row_number(self.h, cp, len(part), co, len(order), asc, C.byref(out)))
+        return self._wrap(out)
+
+    def hash_partition(self, key: DeviceColumn, n_parts: int):
+        counts = (C.c_int64 * n_parts)()
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_hash_partition(self.h, C.byref(key.c), n_parts, counts, C.byref(out)))
+        return np.array(counts[:], dtype=np.int64), self._wrap(out)
+
+
+def agg(func: int, column: int) -> Tuple[int, int]:
+    return (func, column)
