@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="fact rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000_000)
     ap.add_argument("--groups", type=int, default=1024)
+    ap.add_argument("--threshold", type=int, default=49, help="WHERE f.x > threshold (49 = the BASELINE query)")
     ap.add_argument("--cpu-sample", type=int, default=50_000_000, help="fact rows for the CPU baseline (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch of the probe kernel (tools/pmc_traffic.py)")
@@ -103,7 +104,7 @@ def main():
     dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
     dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, args.groups)
     ctx.sync()
-    pred = binop(col(0, "f.x"), BinaryOp.Greater, lit(49))
+    pred = binop(col(0, "f.x"), BinaryOp.Greater, lit(args.threshold))
     aggs = [(AF.Sum, 2), (AF.Count, 2)]
 
     def step():

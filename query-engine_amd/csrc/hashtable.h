@@ -1,7 +1,8 @@
 // Join hash tables in HBM (build side of HashJoinExec).
 //
 // Three layouts, chosen per build from the build keys' min/max:
-//   DIRECT  key range <= 4*n: uint32 array indexed by key-kmin, entry = payload+1
+//   DIRECT  key range <= 4*n: uint32 (or uint16 when payloads < 65535) array indexed by
+//           key-kmin, entry = payload+1
 //           (a "perfect hash": one 4-B read per probe, table <= 16 B/build row)
 //   PACKED  range < 2^(64-pbits): one uint64 per slot, entry = (key-kmin+1)<<pbits | payload,
 //           linear probing, load <= 0.6 -> one 8-B read per probe (same line almost always)
@@ -29,6 +30,7 @@ struct HashTable {
     uint64_t *slots;     // PACKED entries / WIDE keys
     uint32_t *payload;   // DIRECT entries / WIDE payloads
     uint32_t *state;     // WIDE occupancy
+    uint16_t *payload16; // DIRECT with payloads < 65535: 2-B entries (half the cache footprint)
 };
 
 // Probe `key`; calls f(payload) for every match (first match only when
@@ -37,7 +39,8 @@ template <class F>
 __device__ __forceinline__ int table_probe(const HashTable &t, int64_t key, F &&f) {
     if (key < t.kmin || key > t.kmax) return 0;
     if (t.kind == TK_DIRECT) {
-        uint32_t e = t.payload[(uint64_t)key - (uint64_t)t.kmin];
+        const uint64_t i = (uint64_t)key - (uint64_t)t.kmin;
+        uint32_t e = t.payload16 ? (uint32_t)t.payload16[i] : t.payload[i];
         if (e == 0) return 0;
         f(e - 1u);
         return 1;

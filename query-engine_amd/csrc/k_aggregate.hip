@@ -14,6 +14,7 @@
 // states do not fit the LDS budget.  A finalize pass compacts non-empty
 // groups and converts states to the reference's result types.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -124,6 +125,314 @@ __global__ __launch_bounds__(kBlock) void k_agg_rows(ColSet cols, int64_t n, Pre
                     agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * stride_slot + g],
                                      lds[(int64_t)sp.val_slot * stride_slot + g]);
             }
+        }
+    }
+}
+
+// ---- fast fused probe: no-null 8-byte columns, unique DIRECT/PACKED table ------------
+// Each lane owns 8 rows as four 16-byte pairs (every load instruction of a
+// wave reads 1 KiB contiguous); all column loads of a tile are issued before
+// the predicate is evaluated, all table probes before any LDS update, so a
+// wave keeps 4 * (1 + terms + agg columns) HBM loads and 8 probes in flight.
+constexpr int kFastPairs = 4;
+constexpr int kFastR = 2 * kFastPairs;
+constexpr int kFastTile = kBlock * kFastR;  // 2048 rows per workgroup iteration
+
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
+
+struct FastIn {
+    const int64_t *key;
+    const int64_t *term[2];
+    int32_t term_dt[2];
+    const int64_t *acol[2];
+    int32_t agg_colslot[kMaxAggs];  // which acol an aggregate reads (-1: COUNT of a no-null column)
+};
+
+template <bool NT>
+__device__ __forceinline__ v2i64 ld2(const int64_t *p) {
+    if (NT) return __builtin_nontemporal_load((const v2i64 *)p);
+    return *(const v2i64 *)p;
+}
+
+__device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, uint32_t &gid) {
+    if (key < t.kmin || key > t.kmax) return false;
+    if (t.kind == TK_DIRECT) {
+        const uint64_t i = (uint64_t)key - (uint64_t)t.kmin;
+        uint32_t e = t.payload16 ? (uint32_t)t.payload16[i] : t.payload[i];
+        gid = e - 1u;
+        return e != 0;
+    }
+    uint64_t h = hash64((uint64_t)key) & t.mask;
+    const uint64_t want = (uint64_t)key - (uint64_t)t.kmin + 1ull;
+    for (uint64_t i = 0; i <= t.mask; ++i) {
+        uint64_t e = t.slots[h];
+        if (e == 0) return false;
+        if ((e >> t.pbits) == want) {
+            gid = (uint32_t)(e & ((1ull << t.pbits) - 1ull));
+            return true;
+        }
+        h = (h + 1) & t.mask;
+    }
+    return false;
+}
+
+template <int NTERMS, int NACOL, bool NT>
+__global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, HashTable t,
+                                                          int64_t G, int64_t n_tiles, uint64_t *__restrict__ gstates) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    {
+        const int64_t words = (int64_t)specs.n_slots * G;
+        for (int64_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = 0;
+        __syncthreads();
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind == AK_MIN || sp.kind == AK_MAX)
+                for (int64_t g = threadIdx.x; g < G; g += blockDim.x) lds[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t base = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
+        v2i64 key[kFastPairs], tc[NTERMS > 0 ? NTERMS : 1][kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
+#pragma unroll
+        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
+#pragma unroll
+        for (int c = 0; c < NACOL; ++c)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
+
+        uint32_t sel = (1u << kFastR) - 1u;
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i) {
+            const PredTerm pt = terms.t[i];
+            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+            uint32_t tr = 0;
+#pragma unroll
+            for (int r = 0; r < kFastR; ++r) {
+                int64_t v = tc[i][r >> 1][r & 1];
+                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
+                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            }
+            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
+            else sel &= tr;
+        }
+        uint32_t gid[kFastR];
+        uint32_t hit = 0;
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            gid[r] = 0;
+            if ((sel >> r) & 1)
+                if (probe_unique(t, key[r >> 1][r & 1], gid[r])) hit |= 1u << r;
+        }
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            if (!((hit >> r) & 1)) continue;
+            const uint32_t g = gid[r];
+            atomicAdd((unsigned long long *)&lds[g], 1ull);
+            for (int a = 0; a < specs.n; ++a) {
+                const AggSpec sp = specs.a[a];
+                if (sp.kind == AK_COUNT) continue;
+                const int cs = in.agg_colslot[a];
+                int64_t x = (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
+                x = agg_input(sp.kind, sp.in_type, x);
+                agg_apply<true>(sp.kind, &lds[(int64_t)sp.val_slot * G + g], x);
+            }
+        }
+    }
+    __syncthreads();
+    for (int64_t g = threadIdx.x; g < G; g += blockDim.x) {
+        uint64_t rows = lds[g];
+        if (!rows) continue;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lds[(int64_t)sp.val_slot * G + g]);
+        }
+    }
+}
+
+// ---- XCD-partitioned probe (tables larger than one XCD's L2) -----------------------
+// Phase A streams the probe columns once, filters, and appends each selected
+// row's (key, aggregate inputs) to one of 8 partitions = 8 contiguous slices
+// of the table.  Phase B's workgroups read their XCD id and drain the
+// partition of the same index first (stealing the others' leftovers), so each
+// XCD's 4 MiB L2 only ever holds 1/8 of the table.  Placement only affects
+// speed: every item is processed exactly once whatever the XCD mapping.
+constexpr int kParts = 8;
+constexpr int kPartBatch = 8192;
+
+struct PartBufs {
+    void *key[kParts];             // uint32 key offsets (DIRECT) or int64 keys (PACKED)
+    int64_t *val[2][kParts];
+    unsigned long long *cursor;    // [0..8): fill cursors (phase A), [8..16): batch cursors (phase B)
+    uint64_t cap;                  // items per partition
+    float scale;                   // DIRECT: partition = key offset * scale
+    int32_t shift;                 // PACKED: partition = slot >> shift
+    uint32_t *overflow;
+};
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+
+template <int NTERMS, int NACOL, bool KEY64, bool NT>
+__global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms terms, HashTable t, int64_t n_tiles,
+                                                           PartBufs pb) {
+    __shared__ uint32_t cnt[kParts];
+    __shared__ unsigned long long base[kParts];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        if (threadIdx.x < kParts) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const int64_t b0 = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
+        v2i64 key[kFastPairs], tc[NTERMS > 0 ? NTERMS : 1][kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
+#pragma unroll
+        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + b0 + j * 128);
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + b0 + j * 128);
+#pragma unroll
+        for (int c = 0; c < NACOL; ++c)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + b0 + j * 128);
+        uint32_t sel = (1u << kFastR) - 1u;
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i) {
+            const PredTerm pt = terms.t[i];
+            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+            uint32_t tr = 0;
+#pragma unroll
+            for (int r = 0; r < kFastR; ++r) {
+                int64_t v = tc[i][r >> 1][r & 1];
+                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
+                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            }
+            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
+            else sel &= tr;
+        }
+        uint32_t part[kFastR], pos[kFastR];
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            part[r] = 0;
+            pos[r] = 0;
+            if (!((sel >> r) & 1)) continue;
+            const int64_t k = key[r >> 1][r & 1];
+            if (k < t.kmin || k > t.kmax) {  // cannot match: drop here
+                sel &= ~(1u << r);
+                continue;
+            }
+            uint32_t p;
+            if (KEY64) {
+                p = (uint32_t)((hash64((uint64_t)k) & t.mask) >> pb.shift);
+            } else {
+                p = (uint32_t)((float)((uint64_t)k - (uint64_t)t.kmin) * pb.scale);
+                p = p > kParts - 1 ? kParts - 1 : p;
+            }
+            part[r] = p;
+            pos[r] = atomicAdd(&cnt[p], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < kParts) {
+            const uint32_t c = cnt[threadIdx.x];
+            base[threadIdx.x] = c ? atomicAdd(&pb.cursor[threadIdx.x], (unsigned long long)c) : 0ull;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            if (!((sel >> r) & 1)) continue;
+            const uint32_t p = part[r];
+            const uint64_t idx = base[p] + pos[r];
+            if (idx >= pb.cap) {
+                *pb.overflow = 1u;
+                continue;
+            }
+            const int64_t k = key[r >> 1][r & 1];
+            if (KEY64) ((int64_t *)pb.key[p])[idx] = k;
+            else ((uint32_t *)pb.key[p])[idx] = (uint32_t)((uint64_t)k - (uint64_t)t.kmin);
+#pragma unroll
+            for (int c = 0; c < NACOL; ++c) pb.val[c][p][idx] = ac[c][r >> 1][r & 1];
+        }
+    }
+}
+
+template <int NACOL, bool KEY64>
+__global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn in, HashTable t, AggSpecs specs,
+                                                             int64_t G, uint64_t *__restrict__ gstates) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int64_t words = (int64_t)specs.n_slots * G;
+    unsigned long long *grab = (unsigned long long *)&lds[words];
+    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+    for (int a = 0; a < specs.n; ++a) {
+        const AggSpec sp = specs.a[a];
+        if (sp.kind == AK_MIN || sp.kind == AK_MAX)
+            for (int64_t g = threadIdx.x; g < G; g += blockDim.x) lds[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
+    }
+    __syncthreads();
+    const uint32_t x = xcc_id();
+    for (int k = 0; k < kParts; ++k) {
+        const uint32_t p = (x + k) & (kParts - 1);
+        unsigned long long filled = __hip_atomic_load(&pb.cursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t n_p = filled < pb.cap ? filled : pb.cap;
+        for (;;) {
+            if (threadIdx.x == 0) *grab = atomicAdd(&pb.cursor[kParts + p], (unsigned long long)kPartBatch);
+            __syncthreads();
+            const uint64_t b = *grab;
+            __syncthreads();
+            if (b >= n_p) break;
+            const uint64_t e = b + kPartBatch < n_p ? b + kPartBatch : n_p;
+            for (uint64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * kBlock) {
+                int64_t kk[4];
+                int64_t vv[NACOL > 0 ? NACOL : 1][4];
+                bool live[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * kBlock;
+                    live[u] = i < e;
+                    const uint64_t ii = live[u] ? i : b;
+                    kk[u] = KEY64 ? ((const int64_t *)pb.key[p])[ii]
+                                  : (int64_t)((uint64_t)t.kmin + ((const uint32_t *)pb.key[p])[ii]);
+#pragma unroll
+                    for (int c = 0; c < NACOL; ++c) vv[c][u] = __builtin_nontemporal_load(&pb.val[c][p][ii]);
+                }
+                uint32_t gid[4];
+                bool hit[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) hit[u] = live[u] && probe_unique(t, kk[u], gid[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (!hit[u]) continue;
+                    const uint32_t g = gid[u];
+                    atomicAdd((unsigned long long *)&lds[g], 1ull);
+                    for (int a = 0; a < specs.n; ++a) {
+                        const AggSpec sp = specs.a[a];
+                        if (sp.kind == AK_COUNT) continue;
+                        const int cs = in.agg_colslot[a];
+                        int64_t v = (NACOL > 1 && cs == 1) ? vv[NACOL > 1 ? 1 : 0][u] : vv[0][u];
+                        agg_apply<true>(sp.kind, &lds[(int64_t)sp.val_slot * G + g], agg_input(sp.kind, sp.in_type, v));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int64_t g = threadIdx.x; g < G; g += blockDim.x) {
+        uint64_t rows = lds[g];
+        if (!rows) continue;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lds[(int64_t)sp.val_slot * G + g]);
         }
     }
 }
@@ -296,6 +605,194 @@ static void launch_agg_rows(qeh_ctx *ctx, int pm, bool lds, int grid, size_t shm
 #undef QEH_LAUNCH
 }
 
+static ColRef advance(ColRef c, int64_t rows) {
+    size_t es = dtype_size(c.dtype);
+    if (c.dtype != QEH_DT_BOOL && es) c.values = (const char *)c.values + (size_t)rows * es;
+    c.vbit0 += rows;
+    return c;
+}
+
+static bool fast_col_ok(const ColRef &c) {
+    return (c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_FLOAT64) && c.validity == nullptr &&
+           ((uintptr_t)c.values & 15) == 0;
+}
+
+static int fast_nt_mode() {
+    static int m = -1;
+    if (m < 0) {
+        const char *e = std::getenv("QEH_NT_LOADS");
+        m = (e && e[0] == '1') ? 1 : 0;
+    }
+    return m;
+}
+
+// The fused probe's fast path: returns true when it launched (full tiles by
+// k_join_agg_fast, the ragged tail by the generic kernel).
+// Eligibility of the specialised probe kernels; fills the kernel's view.
+static bool fast_eligible(const ColSet &cols, const PredPlan &pp, const GidSource &src, const AggSpecs &specs,
+                          FastIn *inp, int *nterms_out, int *nacol_out) {
+    if (pp.mode == PM_PROG || (pp.mode == PM_TERMS && pp.terms.n > 2)) return false;
+    if (!src.jt.unique || (src.jt.kind != TK_DIRECT && src.jt.kind != TK_PACKED)) return false;
+    if (!fast_col_ok(cols.c[src.key_col]) || cols.c[src.key_col].dtype != QEH_DT_INT64) return false;
+    FastIn &in = *inp;
+    in = FastIn{};
+    in.key = (const int64_t *)cols.c[src.key_col].values;
+    const int nterms = pp.mode == PM_TERMS ? pp.terms.n : 0;
+    for (int i = 0; i < nterms; ++i) {
+        const ColRef &c = cols.c[pp.terms.t[i].col];
+        if (!fast_col_ok(c)) return false;
+        in.term[i] = (const int64_t *)c.values;
+        in.term_dt[i] = c.dtype;
+    }
+    int nacol = 0;
+    int acol_idx[2] = {-1, -1};
+    for (int a = 0; a < specs.n; ++a) {
+        const AggSpec &sp = specs.a[a];
+        if (sp.cnt_slot != 0) return false;
+        in.agg_colslot[a] = -1;
+        if (sp.kind == AK_COUNT) continue;
+        int slot = -1;
+        for (int c = 0; c < nacol; ++c)
+            if (acol_idx[c] == sp.col) slot = c;
+        if (slot < 0) {
+            if (nacol == 2) return false;
+            if (!fast_col_ok(cols.c[sp.col])) return false;
+            acol_idx[nacol] = sp.col;
+            in.acol[nacol] = (const int64_t *)cols.c[sp.col].values;
+            slot = nacol++;
+        }
+        in.agg_colslot[a] = slot;
+    }
+    *nterms_out = nterms;
+    *nacol_out = nacol;
+    return true;
+}
+
+static void launch_tail(qeh_ctx *ctx, const ColSet &cols, int64_t n, int64_t done, const PredPlan &pp,
+                        const GidSource &src, const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err,
+                        size_t lds_bytes) {
+    if (done >= n) return;
+    ColSet tail = cols;
+    for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);
+    launch_agg_rows<GM_JOIN>(ctx, pp.mode, true, 1, lds_bytes, tail, n - done, pp, src, specs, G, states, err);
+}
+
+static bool try_fast_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
+                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes,
+                          int per_cu) {
+    if (std::getenv("QEH_NO_FAST")) return false;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol)) return false;
+    const int64_t n_tiles = n / kFastTile;
+    if (n_tiles > 0) {
+        const int grid = grid_for(ctx, n_tiles * kFastTile, kFastTile, per_cu);
+        const bool nt = fast_nt_mode() == 1;
+#define QEH_FAST(NTV, NAV, NTB)                                                                                    \
+    hipLaunchKernelGGL((k_join_agg_fast<NTV, NAV, NTB>), dim3(grid), dim3(kBlock), lds_bytes, ctx->stream, in, pp.terms, \
+                       specs, src.jt, G, n_tiles, states)
+#define QEH_FAST_NA(NTV, NTB)                       \
+    if (nacol == 0) QEH_FAST(NTV, 0, NTB);          \
+    else if (nacol == 1) QEH_FAST(NTV, 1, NTB);     \
+    else QEH_FAST(NTV, 2, NTB);
+#define QEH_FAST_NT(NTB)                            \
+    if (nterms == 0) { QEH_FAST_NA(0, NTB) }        \
+    else if (nterms == 1) { QEH_FAST_NA(1, NTB) }   \
+    else { QEH_FAST_NA(2, NTB) }
+        if (nt) { QEH_FAST_NT(true) } else { QEH_FAST_NT(false) }
+#undef QEH_FAST_NT
+#undef QEH_FAST_NA
+#undef QEH_FAST
+    }
+    launch_tail(ctx, cols, n, n_tiles * kFastTile, pp, src, specs, G, states, err, lds_bytes);
+    return true;
+}
+
+static uint64_t table_bytes(const HashTable &t) {
+    if (t.kind == TK_DIRECT) return t.range * (t.payload16 ? 2 : 4);
+    if (t.kind == TK_PACKED) return (t.mask + 1) * 8;
+    return (t.mask + 1) * 16;
+}
+
+// XCD-partitioned probe (phase A + phase B).  Returns 1 when it ran, 0 when
+// not eligible, and falls back (re-initialising the states) on partition
+// overflow (heavily skewed keys).
+static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp,
+                                const GidSource &src, const AggSpecs &specs, int64_t G, uint64_t *states,
+                                uint32_t *err, size_t lds_bytes, int per_cu, bool *overflowed) {
+    *overflowed = false;
+    if (std::getenv("QEH_NO_PART")) return 0;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol)) return 0;
+    const HashTable &t = src.jt;
+    const uint64_t min_bytes = std::getenv("QEH_PART_MIN_BYTES") ? std::strtoull(std::getenv("QEH_PART_MIN_BYTES"), nullptr, 10)
+                                                                 : UINT64_MAX;  // opt-in until it beats the single pass
+    if (table_bytes(t) < min_bytes) return 0;  // fits one XCD's L2 well enough: single pass
+    const int64_t n_tiles = n / kFastTile;
+    if (n_tiles == 0) return 0;
+    const int64_t rows = n_tiles * kFastTile;
+    const bool key64 = t.kind == TK_PACKED;
+    PartBufs pb{};
+    pb.cap = (uint64_t)(rows / kParts) + (uint64_t)(rows / kParts) / 4 + 65536;
+    const size_t kb = key64 ? 8 : 4;
+    DevBuf kbuf, vbuf, cur, ovf;
+    if (kbuf.alloc(ctx, pb.cap * kb * kParts) != QEH_OK) return 0;
+    if (nacol && vbuf.alloc(ctx, pb.cap * 8 * kParts * nacol) != QEH_OK) return 0;
+    if (cur.alloc(ctx, 2 * kParts * 8 + 64) != QEH_OK) return 0;
+    for (int p = 0; p < kParts; ++p) {
+        pb.key[p] = (char *)kbuf.p + (size_t)p * pb.cap * kb;
+        for (int c = 0; c < nacol; ++c) pb.val[c][p] = (int64_t *)vbuf.p + ((size_t)c * kParts + p) * pb.cap;
+    }
+    pb.cursor = cur.as<unsigned long long>();
+    pb.overflow = (uint32_t *)(cur.as<char>() + 2 * kParts * 8);
+    pb.scale = (float)kParts / (float)(t.range ? t.range : 1);
+    int lg = 0;
+    while ((1ull << lg) < t.mask + 1) ++lg;
+    pb.shift = lg > 3 ? lg - 3 : 0;
+    if (hipMemsetAsync(cur.p, 0, 2 * kParts * 8 + 64, ctx->stream) != hipSuccess) return 0;
+    const bool nt = fast_nt_mode() == 1;
+    {
+        KernelTimer kt(ctx, "join_partition");
+        const int grid = grid_for(ctx, rows, kFastTile, 8);
+#define QEH_PA(NTV, NAV, K64, NTB) \
+    hipLaunchKernelGGL((k_join_partition<NTV, NAV, K64, NTB>), dim3(grid), dim3(kBlock), 0, ctx->stream, in, pp.terms, t, n_tiles, pb)
+#define QEH_PA_NA(NTV, K64, NTB)                         \
+    if (nacol == 0) QEH_PA(NTV, 0, K64, NTB);            \
+    else if (nacol == 1) QEH_PA(NTV, 1, K64, NTB);       \
+    else QEH_PA(NTV, 2, K64, NTB);
+#define QEH_PA_NT(K64, NTB)                              \
+    if (nterms == 0) { QEH_PA_NA(0, K64, NTB) }          \
+    else if (nterms == 1) { QEH_PA_NA(1, K64, NTB) }     \
+    else { QEH_PA_NA(2, K64, NTB) }
+        if (key64) { if (nt) { QEH_PA_NT(true, true) } else { QEH_PA_NT(true, false) } }
+        else { if (nt) { QEH_PA_NT(false, true) } else { QEH_PA_NT(false, false) } }
+#undef QEH_PA_NT
+#undef QEH_PA_NA
+#undef QEH_PA
+    }
+    {
+        KernelTimer kt(ctx, "join_probe_parts");
+        const size_t shm = lds_bytes + 16;
+        const int grid = ctx->props.multiProcessorCount * std::max(1, per_cu);
+#define QEH_PB(NAV, K64) \
+    hipLaunchKernelGGL((k_join_probe_parts<NAV, K64>), dim3(grid), dim3(kBlock), shm, ctx->stream, pb, in, t, specs, G, states)
+        if (key64) { if (nacol == 0) QEH_PB(0, true); else if (nacol == 1) QEH_PB(1, true); else QEH_PB(2, true); }
+        else { if (nacol == 0) QEH_PB(0, false); else if (nacol == 1) QEH_PB(1, false); else QEH_PB(2, false); }
+#undef QEH_PB
+    }
+    launch_tail(ctx, cols, n, rows, pp, src, specs, G, states, err, lds_bytes);
+    uint32_t of = 0;
+    if (read_small(ctx, &of, pb.overflow, 4) != QEH_OK) return 0;
+    if (of) {
+        *overflowed = true;
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
+                           ctx->stream, states, G, specs);
+        return 0;
+    }
+    return 1;
+}
+
 // Run the row-aggregation kernel and finalize into owned output columns.
 static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, const PredPlan &pp,
                           const GidSource &src, const AggSpecs &specs, int64_t G, const KeyCols &out_keys_src,
@@ -317,7 +814,15 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         int grid = grid_for(ctx, n, kAggTile, per_cu);
         KernelTimer kt(ctx, kname);
         if (gm == GM_ZERO) launch_agg_rows<GM_ZERO>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
-        else if (gm == GM_JOIN) launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
+        else if (gm == GM_JOIN) {
+            bool ovf = false;
+            if (lds && try_partitioned_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
+                                            lds_bytes, per_cu, &ovf) == 1) {
+            } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
+                                       lds_bytes, per_cu)))
+                launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
+                                         states.as<uint64_t>(), errw.as<uint32_t>());
+        }
         else launch_agg_rows<GM_GROUP>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
     }
     QEH_HIP(hipGetLastError());

@@ -6,6 +6,7 @@
 // table over the right (build) input; probing lives with the consumers
 // (k_join.hip, k_pipeline.hip).
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "device_common.h"
@@ -104,6 +105,11 @@ __global__ void k_insert_wide(ColRef key, int64_t n, const uint32_t *row_payload
     }
 }
 
+__global__ void k_narrow_direct(const uint32_t *__restrict__ in, uint64_t n, uint16_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint16_t)in[i];
+}
+
 // Duplicate detection for WIDE tables (separate launch: all slots are final).
 __global__ void k_wide_dups(ColRef key, int64_t n, HashTable t, uint32_t *dup) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -190,6 +196,18 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_pa
         QEH_TRY(read_small(ctx, &dup, flag.p, 4));
         if (!dup) {
             t.unique = 1;
+            if (payload_max < 0xFFFFull && !std::getenv("QEH_NO_U16")) {  // entries fit 16 bits: halve the table's cache footprint
+                QEH_TRY(out->payload16.alloc(ctx, range * 2));
+                {
+                    KernelTimer kt(ctx, "join_build");
+                    hipLaunchKernelGGL(k_narrow_direct, dim3(grid_for(ctx, (int64_t)range, kBlock * 8, 8)), dim3(kBlock), 0,
+                                       ctx->stream, t.payload, range, out->payload16.as<uint16_t>());
+                }
+                QEH_HIP(hipGetLastError());
+                t.payload16 = out->payload16.as<uint16_t>();
+                t.payload = nullptr;
+                out->payload.reset();
+            }
             return QEH_OK;
         }
         // duplicate build keys: a perfect-hash slot holds one row; rebuild hashed

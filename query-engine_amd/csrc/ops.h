@@ -21,7 +21,7 @@ int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t 
 // (row_payload == nullptr) or row_payload[row].
 struct BuiltTable {
     HashTable t{};
-    DevBuf slots, payload, state;
+    DevBuf slots, payload, state, payload16;
     int64_t n_inserted = 0;
 };
 int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload,

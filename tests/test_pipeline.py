@@ -139,3 +139,33 @@ def test_no_predicate_and_empty_inputs(ctx):
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
     gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (e, None), [(e, None)], AGGS)
     assert len(gk[0][0]) == 0 and len(wk[0][0]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("table", ["direct", "packed"])
+def test_xcd_partitioned_probe(ctx, monkeypatch, table):
+    """Phase A (filter + partition by table slice) / phase B (XCD-affine probe)
+    forced on small tables; ragged tail handled by the generic kernel."""
+    monkeypatch.setenv("QEH_PART_MIN_BYTES", "0")
+    monkeypatch.setenv("QEH_FORCE_TABLE", table)
+    x, k, v, dk, dg = metric_data(1_000_003, 100_000, 1024)
+    probe = [(x, None), (k, None), (v, None)]
+    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Avg, 2), (AF.Min, 0), (AF.Max, 2), (AF.Sum, 0)]
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0, 2])
+
+
+@pytest.mark.gpu
+def test_xcd_partition_overflow_falls_back(ctx, monkeypatch):
+    """Every probe key in one table slice overflows its partition: the
+    operator must re-run on the single-pass kernel and stay exact."""
+    monkeypatch.setenv("QEH_PART_MIN_BYTES", "0")
+    rng = np.random.default_rng(5)
+    n, nd = 600_000, 80_000
+    dk = rng.permutation(nd).astype(np.int64)
+    dg = rng.integers(0, 100, nd)
+    k = rng.integers(0, nd // 16, n)  # all in partition 0
+    x = np.full(n, 99, np.int64)
+    v = rng.random(n)
+    gk, ga, wk, wa = run_both(ctx, [(x, None), (k, None), (v, None)], 1, PRED, (dk, None), [(dg, None)], AGGS)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
