@@ -1,0 +1,362 @@
+// FilterExec and ProjectionExec expressions.
+//
+// Reference: execute_filter (crates/query-executor/src/executor.rs:131-155)
+// evaluates the predicate with evaluate_expr (operators.rs:13-62) and calls
+// arrow's filter_record_batch (NULL -> dropped, order preserved) on every
+// column; execute_projection (executor.rs:93-129) evaluates each expression
+// (column references are Arc clones, operators.rs:15-23).
+//
+// Filter on the device is ONE pass: every workgroup takes a 2048-row tile in
+// dispatch order (atomic ticket), evaluates the predicate (wave-uniform
+// interpreter, expr_device.h), ranks the surviving rows with ballot+mbcnt,
+// publishes its count, learns the rows before it by a decoupled look-back
+// over 8-byte {flag, value} status words (agent-scope relaxed atomics: the
+// status word is the only data handed between workgroups), and writes the
+// selected rows of every output column to their final, order-preserving
+// positions.  Inputs are read once, outputs written once.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "expr_device.h"
+#include "lookback.h"
+#include "ops.h"
+
+namespace qeh {
+
+constexpr int kFR = 8;                       // rows per thread
+constexpr int kFTile = kBlock * kFR;         // 2048 rows per tile
+struct OutSpec {
+    const void *src_values;     // ColRef.values of the source column
+    const uint8_t *src_valid;
+    int64_t src_vbit0;
+    int32_t dtype;
+    int32_t _pad;
+    void *dst_values;
+    uint32_t *dst_valid;        // nullptr when the source has no validity
+};
+struct OutSpecs {
+    OutSpec o[kMaxCols];
+    int32_t n;
+};
+
+template <int PM>
+__global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64_t n_tiles, PredTerms terms,
+                                                   DevProgram prog, OutSpecs outs, uint64_t *__restrict__ status,
+                                                   unsigned long long *__restrict__ ticket, uint32_t *__restrict__ errp,
+                                                   uint64_t *__restrict__ total_out) {
+    __shared__ uint32_t wave_cnt[kFR][kBlock / 64];
+    __shared__ uint32_t wave_off[kFR][kBlock / 64];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_total;
+    __shared__ uint32_t vbits[kMaxCols + 1][kFTile / 32 + 2];  // row kMaxCols: validity staging
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t err = 0;
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1ull);
+        __syncthreads();
+        const int64_t tile = s_tile;
+        if (tile >= n_tiles) break;
+        const int64_t row0 = tile * kFTile + threadIdx.x;  // rows row0 + r*256
+        uint32_t sel;
+        if (PM == 1) {
+            sel = eval_terms<kFR>(terms, cols, row0, kBlock, n);
+        } else {
+            ExprRegs<kFR> X;
+            run_program<kFR>(prog, cols, row0, kBlock, n, X, err);
+            sel = program_true_mask<kFR>(X);
+        }
+        uint32_t rank[kFR];
+#pragma unroll
+        for (int r = 0; r < kFR; ++r) {
+            const uint64_t b = __ballot((sel >> r) & 1);
+            rank[r] = mbcnt(b);
+            if (lane == 0) wave_cnt[r][wave] = (uint32_t)popc64(b);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int r = 0; r < kFR; ++r)
+                for (int w = 0; w < kBlock / 64; ++w) {
+                    wave_off[r][w] = acc;
+                    acc += wave_cnt[r][w];
+                }
+            s_total = acc;
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        if (wave == 0) {
+            uint64_t prefix = 0;
+            if (tile == 0) {
+                if (lane == 0) st_agent(&status[0], kFlagIncl | total);
+            } else {
+                if (lane == 0) st_agent(&status[tile], kFlagAgg | total);
+                prefix = lookback(status, tile, total, errp);
+                if (lane == 0) st_agent(&status[tile], kFlagIncl | (prefix + total));
+            }
+            if (lane == 0) {
+                s_prefix = prefix;
+                if (tile == n_tiles - 1) *total_out = prefix + total;
+            }
+        }
+        // stage validity / boolean bits of this tile's output range in LDS
+        for (int i = threadIdx.x; i < outs.n * (kFTile / 32 + 2); i += blockDim.x) (&vbits[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t prefix = s_prefix;
+        const uint32_t shift = (uint32_t)(prefix & 31);  // bit offset of the tile's first row in its word
+#pragma unroll
+        for (int r = 0; r < kFR; ++r) {
+            if (!((sel >> r) & 1)) continue;
+            const int64_t row = row0 + (int64_t)r * kBlock;
+            const uint32_t local = wave_off[r][wave] + rank[r];
+            const uint64_t pos = prefix + local;
+            for (int c = 0; c < outs.n; ++c) {
+                const OutSpec &o = outs.o[c];
+                switch (o.dtype) {
+                    case QEH_DT_BOOL: {
+                        if (bit_at((const uint8_t *)o.src_values, o.src_vbit0 + row)) {
+                            const uint32_t b = local + shift;
+                            atomicOr(&vbits[c][b >> 5], 1u << (b & 31));
+                        }
+                        break;
+                    }
+                    case QEH_DT_INT32: case QEH_DT_FLOAT32: case QEH_DT_UINT32:
+                        ((uint32_t *)o.dst_values)[pos] = ((const uint32_t *)o.src_values)[row];
+                        break;
+                    default:
+                        ((uint64_t *)o.dst_values)[pos] = ((const uint64_t *)o.src_values)[row];
+                        break;
+                }
+            }
+        }
+        __syncthreads();
+        // validity (and boolean values) words: interior words are owned by this
+        // tile; the first and last word may be shared with neighbours -> atomicOr
+        const uint32_t nwords = (shift + total + 31) / 32;
+        for (int c = 0; c < outs.n; ++c) {
+            const OutSpec &o = outs.o[c];
+            const bool bool_vals = o.dtype == QEH_DT_BOOL;
+            if (!o.dst_valid && !bool_vals) continue;
+            // validity bits need their own staging pass
+            if (o.dst_valid) {
+                __syncthreads();
+                for (int i = threadIdx.x; i < kFTile / 32 + 2; i += blockDim.x) vbits[kMaxCols][i] = 0;
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < kFR; ++r) {
+                    if (!((sel >> r) & 1)) continue;
+                    const int64_t row = row0 + (int64_t)r * kBlock;
+                    if (!o.src_valid || bit_at(o.src_valid, o.src_vbit0 + row)) {
+                        const uint32_t b = wave_off[r][wave] + rank[r] + shift;
+                        atomicOr(&vbits[kMaxCols][b >> 5], 1u << (b & 31));
+                    }
+                }
+                __syncthreads();
+                for (uint32_t w = threadIdx.x; w < nwords; w += blockDim.x) {
+                    uint32_t *dst = &o.dst_valid[(prefix >> 5) + w];
+                    const uint32_t v = vbits[kMaxCols][w];
+                    if (w == 0 || w == nwords - 1) atomicOr(dst, v);
+                    else *dst = v;
+                }
+            }
+            if (bool_vals) {
+                for (uint32_t w = threadIdx.x; w < nwords; w += blockDim.x) {
+                    uint32_t *dst = &((uint32_t *)o.dst_values)[(prefix >> 5) + w];
+                    const uint32_t v = vbits[c][w];
+                    if (w == 0 || w == nwords - 1) atomicOr(dst, v);
+                    else *dst = v;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (err) atomicOr(errp, err);
+}
+
+// ---- projection expression -------------------------------------------------------------
+constexpr int kER = 4;
+template <int RT>  // result dtype class: 0 = 8-byte, 1 = 4-byte int, 2 = float32, 3 = bool
+__global__ __launch_bounds__(kBlock) void k_eval(ColSet cols, int64_t n, DevProgram prog, void *__restrict__ out,
+                                                 uint64_t *__restrict__ out_valid, uint32_t *__restrict__ errp) {
+    const int lane = threadIdx.x & 63;
+    uint32_t err = 0;
+    const int64_t nchunks = (n + 64 * kER - 1) / (64 * kER);
+    const int64_t wstride = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nchunks; w += wstride) {
+        const int64_t base = w * 64 * kER;
+        ExprRegs<kER> X;
+        run_program<kER>(prog, cols, base + lane, 64, n, X, err);
+#pragma unroll
+        for (int r = 0; r < kER; ++r) {
+            const int64_t row = base + r * 64 + lane;
+            const bool live = row < n;
+            const bool valid = live && ((X.valid[0] >> r) & 1);
+            const uint64_t vb = __ballot(valid);
+            if (RT == 3) {
+                const uint64_t bb = __ballot(live && (X.v[0][r] & 1));
+                if (lane == 0) ((uint64_t *)out)[(base + r * 64) >> 6] = bb;
+            } else if (live) {
+                if (RT == 0) ((int64_t *)out)[row] = X.v[0][r];
+                else if (RT == 1) ((int32_t *)out)[row] = (int32_t)X.v[0][r];
+                else ((float *)out)[row] = (float)as_f64(X.v[0][r]);
+            }
+            if (lane == 0) out_valid[(base + r * 64) >> 6] = vb;
+        }
+    }
+    if (err) atomicOr(errp, err);
+}
+
+}  // namespace qeh
+
+using namespace qeh;
+
+extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                          const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows) {
+    if (!ctx || !out_rows || (n_out > 0 && (!out || !out_idx))) return fail(QEH_E_INVALID, "qeh_filter: bad argument");
+    *out_rows = 0;
+    if (n_out > kMaxCols) return fail(QEH_E_UNSUPPORTED, "too many output columns for one filter (max 12)");
+    DeviceGuard dg(ctx->device);
+    ColSet cs;
+    QEH_TRY(make_colset(cols, n_cols, &cs));
+    const int64_t n = n_cols > 0 ? cols[0].length : 0;
+    for (int i = 0; i < n_cols; ++i)
+        if (cols[i].length != n) return fail(QEH_E_INVALID, "filter columns have different lengths");
+    std::vector<int32_t> dts(n_cols);
+    for (int i = 0; i < n_cols; ++i) dts[i] = cols[i].dtype;
+    DevProgram prog;
+    QEH_TRY(compile_expr(predicate, dts.data(), n_cols, &prog));
+    if (prog.result_type != QEH_DT_BOOL) return fail(QEH_E_TYPE, "Filter predicate must return boolean");
+    PredTerms terms{};
+    const bool fast = lower_to_terms(predicate, dts.data(), n_cols, &terms);
+    OutSpecs os{};
+    os.n = n_out;
+    int made = 0;
+    for (int j = 0; j < n_out; ++j) {
+        if (out_idx[j] < 0 || out_idx[j] >= n_cols) {
+            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            return fail(QEH_E_INVALID, "filter output column index out of range");
+        }
+        const qeh_column &src = cols[out_idx[j]];
+        if (src.dtype == QEH_DT_UTF8) {
+            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            return fail(QEH_E_UNSUPPORTED, "Utf8 filter outputs are not compacted on the device");
+        }
+        int s = alloc_column(ctx, src.dtype, n, src.validity != nullptr, &out[j]);
+        if (s != QEH_OK) {
+            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            return s;
+        }
+        ++made;
+        const size_t words = ((size_t)(n + 63) / 64) * 8;
+        if (src.validity) QEH_HIP(hipMemsetAsync(out[j].validity, 0, words ? words : 8, ctx->stream));
+        if (src.dtype == QEH_DT_BOOL) QEH_HIP(hipMemsetAsync(out[j].values, 0, words ? words : 8, ctx->stream));
+        const ColRef cr = make_colref(src);
+        OutSpec &o = os.o[j];
+        o.src_values = cr.values;
+        o.src_valid = cr.validity;
+        o.src_vbit0 = cr.vbit0;
+        o.dtype = src.dtype;
+        o.dst_values = out[j].values;
+        o.dst_valid = (uint32_t *)out[j].validity;
+    }
+    const int64_t n_tiles = (n + kFTile - 1) / kFTile;
+    uint64_t total = 0;
+    if (n_tiles > 0) {
+        void *scr = nullptr;
+        const size_t hdr = 64;
+        QEH_TRY(scratch_zeroed(ctx, hdr + (size_t)n_tiles * 8, &scr));
+        unsigned long long *ticket = (unsigned long long *)scr;
+        uint32_t *err = (uint32_t *)((char *)scr + 8);
+        uint64_t *tot = (uint64_t *)((char *)scr + 16);
+        uint64_t *status = (uint64_t *)((char *)scr + hdr);
+        const int grid = grid_for(ctx, n, kFTile, 4);
+        {
+            KernelTimer kt(ctx, "filter");
+            if (fast)
+                hipLaunchKernelGGL(k_filter<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n, n_tiles, terms, prog, os,
+                                   status, ticket, err, tot);
+            else
+                hipLaunchKernelGGL(k_filter<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n, n_tiles, terms, prog, os,
+                                   status, ticket, err, tot);
+        }
+        QEH_HIP(hipGetLastError());
+        uint64_t hdrv[3];
+        int s = read_small(ctx, hdrv, scr, 24);
+        if (s == QEH_OK) s = kernel_error_status((uint32_t)hdrv[1], "filter");
+        if (s != QEH_OK) {
+            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            return s;
+        }
+        total = hdrv[2];
+    }
+    for (int j = 0; j < n_out; ++j) {
+        out[j].length = (int64_t)total;
+        out[j].null_count = out[j].validity ? -1 : 0;
+    }
+    *out_rows = (int64_t)total;
+    return QEH_OK;
+}
+
+extern "C" int qeh_eval(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *expr, int64_t n_rows,
+                        qeh_column *out) {
+    if (!ctx || !out || !expr) return fail(QEH_E_INVALID, "qeh_eval: bad argument");
+    std::memset(out, 0, sizeof(*out));
+    DeviceGuard dg(ctx->device);
+    for (int i = 0; i < n_cols; ++i)
+        if (cols[i].length != n_rows) return fail(QEH_E_INVALID, "eval columns have different lengths");
+    const int ci = expr_as_column(expr);
+    if (ci >= 0) {  // zero-copy column reference (operators.rs:15-23)
+        if (ci >= n_cols) return fail(QEH_E_INVALID, "Column index " + std::to_string(ci) + " out of bounds");
+        *out = cols[ci];
+        out->owned = 0;
+        return QEH_OK;
+    }
+    ColSet cs;
+    QEH_TRY(make_colset(cols, n_cols, &cs));
+    std::vector<int32_t> dts(n_cols);
+    for (int i = 0; i < n_cols; ++i) dts[i] = cols[i].dtype;
+    DevProgram prog;
+    QEH_TRY(compile_expr(expr, dts.data(), n_cols, &prog));
+    int rt = prog.result_type;
+    if (rt == QEH_DT_NULL) rt = QEH_DT_INT64;  // NullArray: all-null column, typed Int64 here
+    QEH_TRY(alloc_column(ctx, rt, n_rows, true, out));
+    if (n_rows == 0) return QEH_OK;
+    void *scr = nullptr;
+    int s = scratch_zeroed(ctx, 64, &scr);
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out);
+        return s;
+    }
+    const int grid = grid_for(ctx, n_rows, kBlock * kER, 8);
+    {
+        KernelTimer kt(ctx, "eval");
+        uint32_t *err = (uint32_t *)scr;
+        uint64_t *ov = (uint64_t *)out->validity;
+        switch (rt) {
+            case QEH_DT_BOOL:
+                hipLaunchKernelGGL(k_eval<3>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n_rows, prog, out->values, ov, err);
+                break;
+            case QEH_DT_INT32:
+                hipLaunchKernelGGL(k_eval<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n_rows, prog, out->values, ov, err);
+                break;
+            case QEH_DT_FLOAT32:
+                hipLaunchKernelGGL(k_eval<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n_rows, prog, out->values, ov, err);
+                break;
+            default:
+                hipLaunchKernelGGL(k_eval<0>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n_rows, prog, out->values, ov, err);
+                break;
+        }
+    }
+    QEH_HIP(hipGetLastError());
+    uint32_t e = 0;
+    s = read_small(ctx, &e, scr, 4);
+    if (s == QEH_OK) s = kernel_error_status(e, "eval");
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out);
+        return s;
+    }
+    out->null_count = -1;
+    return QEH_OK;
+}

@@ -1,0 +1,471 @@
+// SortExec, ROW_NUMBER() window and hash partitioning: LSD radix sort with
+// LDS histograms producing a stable permutation.
+//
+// Reference: execute_sort is the identity (crates/query-executor/src/executor.rs:290-297)
+// and the Window arm passes its input through (executor.rs:76-80), so the
+// semantics are the intended ones of SURVEY.md §8.0: stable lexicographic sort
+// by `exprs` with a per-key ascending flag, NULLs first (arrow SortOptions
+// default; the only explicit null ordering in the tree is
+// distributed/operators.rs:97-104), floats by totalOrder; ROW_NUMBER numbers
+// rows 1.. within each PARTITION BY group in ORDER BY order, ties by input
+// position (docs/WINDOW_FUNCTIONS.md:44-65), output aligned to input order.
+// Hash partitioning follows Partitioner::partition_by_hash
+// (crates/query-distributed/src/partition.rs:151-212) with a device hash.
+//
+// Key encoding: each key column becomes an unsigned integer in [0, 2^bits):
+// NULL -> 0, value -> (ordered(x) - min + 1) ascending or (max - ordered(x) + 1)
+// descending, where ordered() is sign-flip for ints and totalOrder for floats
+// and min/max come from one reduction.  Only `bits` = bit length of the range
+// are sorted (e.g. 21 bits for k in [0, 2^20)), 8 bits per pass; keys are
+// processed last column first, each column's passes reading its encoding
+// through the current permutation, so the result is lexicographic and stable.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device_common.h"
+#include "ops.h"
+
+namespace qeh {
+
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;
+
+struct KeyStats {
+    int64_t mn, mx;
+};
+
+__device__ __forceinline__ int64_t ordered_key(const ColRef &c, int64_t row) {
+    const int64_t x = load_i64(c, row);
+    if (c.dtype == QEH_DT_FLOAT32 || c.dtype == QEH_DT_FLOAT64) return f64_order_key(as_f64(x));
+    return x;
+}
+
+__global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t n, KeyStats *out) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = perm ? perm[i] : i;
+        if (!col_valid(c, r)) continue;
+        const int64_t k = ordered_key(c, r);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin((long long *)&out->mn, (long long)mn);
+        atomicMax((long long *)&out->mx, (long long)mx);
+    }
+}
+
+__global__ void k_stats_init(KeyStats *s) {
+    s->mn = INT64_MAX;
+    s->mx = INT64_MIN;
+}
+
+// encoded key of row perm[i] (or i) -> keys[i]; perm_out[i] = perm[i] (or i)
+// mode 0: value encoding (NULL -> 0, values biased by `bias`); mode 1: null flag only
+__global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n, int64_t mn, int64_t mx, int asc,
+                         uint64_t bias, int mode, uint64_t *__restrict__ keys, uint32_t *__restrict__ perm_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = perm ? perm[i] : i;
+        uint64_t k = 0;
+        if (col_valid(c, r)) {
+            if (mode == 1) {
+                k = 1;
+            } else {
+                const int64_t x = ordered_key(c, r);
+                k = asc ? (uint64_t)x - (uint64_t)mn + bias : (uint64_t)mx - (uint64_t)x + bias;
+            }
+        }
+        keys[i] = k;
+        perm_out[i] = (uint32_t)r;
+    }
+}
+
+// ---- one LSD pass ----------------------------------------------------------------------
+// block b owns elements [b*seg, (b+1)*seg); hist is digit-major [kRadix][nblocks]
+__global__ __launch_bounds__(kBlock) void k_rs_hist(const uint64_t *__restrict__ keys, int64_t n, int64_t seg,
+                                                    int shift, uint32_t *__restrict__ hist, int nblocks) {
+    __shared__ uint32_t h[kRadix];
+    for (int i = threadIdx.x; i < kRadix; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&h[(keys[i] >> shift) & (kRadix - 1)], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < kRadix; d += blockDim.x) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
+}
+
+__global__ __launch_bounds__(kBlock) void k_rs_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                       int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
+                                                       int nblocks, uint64_t *__restrict__ keys_out,
+                                                       uint32_t *__restrict__ vals_out) {
+    constexpr int W = kBlock / 64;
+    __shared__ uint32_t wave_hist[W][kRadix];
+    __shared__ uint64_t wave_pos[W][kRadix];
+    __shared__ uint64_t run[kRadix];  // next output position of each digit for this block
+    const int wave = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < kRadix; d += blockDim.x) run[d] = offs[(int64_t)d * nblocks + blockIdx.x];
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    for (int64_t c0 = lo; c0 < hi; c0 += kBlock) {
+        for (int i = threadIdx.x; i < W * kRadix; i += blockDim.x) (&wave_hist[0][0])[i] = 0;
+        __syncthreads();
+        const int64_t i = c0 + threadIdx.x;
+        const bool live = i < hi;
+        const uint64_t k = live ? keys[i] : 0;
+        const uint32_t v = live ? vals[i] : 0;
+        const uint32_t dg = (uint32_t)((k >> shift) & (kRadix - 1));
+        // lanes of this wave holding the same digit: 8 ballots (wave64 has no match_any)
+        uint64_t peers = __ballot(live);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; ++b) {
+            const uint64_t m = __ballot((dg >> b) & 1);
+            peers &= ((dg >> b) & 1) ? m : ~m;
+        }
+        const uint32_t rank = mbcnt(peers);
+        if (live && rank == 0) wave_hist[wave][dg] = (uint32_t)popc64(peers);
+        __syncthreads();
+        for (int d = threadIdx.x; d < kRadix; d += blockDim.x) {
+            uint64_t acc = run[d];
+            for (int w = 0; w < W; ++w) {
+                wave_pos[w][d] = acc;
+                acc += wave_hist[w][d];
+            }
+            run[d] = acc;
+        }
+        __syncthreads();
+        if (live) {  // stable: element order = (chunk, wave, lane)
+            const uint64_t pos = wave_pos[wave][dg] + rank;
+            keys_out[pos] = k;
+            vals_out[pos] = v;
+        }
+    }
+}
+
+// Sort state: encoded keys + permutation, double-buffered.
+struct RadixState {
+    DevBuf k[2], v[2];
+    int cur = 0;
+    int64_t n = 0;
+};
+
+// Stable LSD passes over the low `bits` of the encoded keys in rs.
+static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
+    const int64_t n = rs.n;
+    if (n <= 1 || bits <= 0) return QEH_OK;
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + 4095) / 4096, 1), (int64_t)ctx->props.multiProcessorCount * 4);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    DevBuf hist, offs;
+    QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
+    QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    for (int shift = 0; shift < bits; shift += kRadixBits) {
+        KernelTimer kt(ctx, "radix_pass");
+        const int c = rs.cur;
+        hipLaunchKernelGGL(k_rs_hist, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<uint64_t>(), n, seg, shift,
+                           hist.as<uint32_t>(), nblocks);
+        QEH_HIP(hipGetLastError());
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<uint64_t>(),
+                           rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<uint64_t>(),
+                           rs.v[1 - c].as<uint32_t>());
+        QEH_HIP(hipGetLastError());
+        rs.cur = 1 - c;
+    }
+    return QEH_OK;
+}
+
+static int bit_length(uint64_t x) {
+    int b = 0;
+    while (b < 64 && (x >> b) != 0) ++b;
+    return b;
+}
+
+// Encode key column `c` through the current permutation (or identity) and
+// sort by it.  Returns the key range bits used.
+static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, bool asc, bool first) {
+    const ColRef c = make_colref(col);
+    const int64_t n = rs.n;
+    DevBuf st;
+    QEH_TRY(st.alloc(ctx, sizeof(KeyStats)));
+    KeyStats ks{};
+    const uint32_t *perm = first ? nullptr : rs.v[rs.cur].as<uint32_t>();
+    {
+        KernelTimer kt(ctx, "sort_encode");
+        hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, st.as<KeyStats>());
+        hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, c, perm, n,
+                           st.as<KeyStats>());
+    }
+    QEH_HIP(hipGetLastError());
+    QEH_TRY(read_small(ctx, &ks, st.p, sizeof ks));
+    const bool nullable = col.validity != nullptr && col.null_count != 0;
+    int bits = 1;  // all NULL (or empty)
+    uint64_t bias = nullable ? 1 : 0;
+    bool null_pass = false;
+    if (ks.mn <= ks.mx) {
+        const uint64_t span = (uint64_t)ks.mx - (uint64_t)ks.mn;  // values map to bias .. span+bias
+        if (nullable && span == UINT64_MAX) {  // 2^64 values + NULL: 65 bits -> separate null-flag pass
+            bias = 0;
+            null_pass = true;
+        }
+        bits = bit_length(span + bias);
+        if (bits == 0) bits = 1;
+    }
+    for (int pass = 0; pass < (null_pass ? 2 : 1); ++pass) {
+        const uint32_t *pm = (first && pass == 0) ? nullptr : rs.v[rs.cur].as<uint32_t>();
+        const int o = 1 - rs.cur;  // encode into the spare buffers, then swap
+        {
+            KernelTimer kt(ctx, "sort_encode");
+            hipLaunchKernelGGL(k_encode, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, c, pm, n,
+                               ks.mn, ks.mx, asc ? 1 : 0, bias, pass, rs.k[o].as<uint64_t>(), rs.v[o].as<uint32_t>());
+        }
+        QEH_HIP(hipGetLastError());
+        rs.cur = o;
+        QEH_TRY(radix_passes(ctx, rs, pass == 0 ? bits : 1));
+    }
+    return QEH_OK;
+}
+
+// Stable lexicographic permutation by keys (last key sorted first).
+static int sort_perm(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending, int64_t n,
+                     RadixState &rs) {
+    rs.n = n;
+    for (int b = 0; b < 2; ++b) {
+        QEH_TRY(rs.k[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 8));
+        QEH_TRY(rs.v[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4));
+    }
+    rs.cur = 0;
+    if (n == 0) return QEH_OK;
+    for (int j = n_keys - 1; j >= 0; --j)
+        QEH_TRY(sort_by_column(ctx, rs, keys[j], ascending ? ascending[j] != 0 : true, j == n_keys - 1));
+    return QEH_OK;
+}
+
+static int check_sort_keys(const qeh_column *keys, int n_keys, int64_t *n) {
+    if (n_keys < 1) return fail(QEH_E_INVALID, "sort needs at least one key");
+    *n = keys[0].length;
+    for (int j = 0; j < n_keys; ++j) {
+        QEH_TRY(check_column(keys[j], "sort key"));
+        if (keys[j].dtype == QEH_DT_UTF8) return fail(QEH_E_UNSUPPORTED, "Utf8 sort keys are not supported on the device");
+        if (keys[j].length != *n) return fail(QEH_E_INVALID, "sort keys have different lengths");
+    }
+    return QEH_OK;
+}
+
+// ---- ROW_NUMBER ----------------------------------------------------------------------------
+// flags[i] = 1 when sorted row i starts a new partition (partition columns differ from row i-1)
+__global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, int64_t n, uint32_t *__restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t f = 1;
+        if (i > 0) {
+            const int64_t a = perm[i - 1], b = perm[i];
+            f = 0;
+            for (int c = 0; c < part.n; ++c) {
+                const bool va = col_valid(part.c[c], a), vb = col_valid(part.c[c], b);
+                if (va != vb || (va && load_i64(part.c[c], a) != load_i64(part.c[c], b))) {
+                    f = 1;
+                    break;
+                }
+            }
+        }
+        flags[i] = f;
+    }
+}
+
+// seg_excl[i] = number of partition starts before i; start_of[seg] = sorted index of its first row
+__global__ void k_part_starts(const uint32_t *__restrict__ flags, const uint64_t *__restrict__ seg_excl, int64_t n,
+                              uint64_t *__restrict__ start_of) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (flags[i]) start_of[seg_excl[i]] = (uint64_t)i;
+}
+
+__global__ void k_row_numbers(const uint32_t *__restrict__ flags, const uint64_t *__restrict__ seg_excl,
+                              const uint64_t *__restrict__ start_of, const uint32_t *__restrict__ perm, int64_t n,
+                              int64_t *__restrict__ rn) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t seg = seg_excl[i] + flags[i] - 1;  // inclusive count - 1
+        rn[perm[i]] = (int64_t)((uint64_t)i - start_of[seg] + 1);
+    }
+}
+
+// ---- hash partition ---------------------------------------------------------------------------
+__global__ void k_partition_ids(ColRef key, int64_t n, uint32_t parts, uint64_t *__restrict__ keys,
+                                uint32_t *__restrict__ idx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t p = 0;  // NULL keys hash like an empty key (partition.rs:292-316 skips them)
+        if (col_valid(key, i)) p = (uint32_t)(hash64((uint64_t)load_i64(key, i)) % parts);
+        keys[i] = p;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+__global__ void k_count_parts(const uint64_t *__restrict__ ids, int64_t n, int parts, unsigned long long *__restrict__ counts) {
+    __shared__ uint32_t h[kRadix];
+    for (int i = threadIdx.x; i < kRadix; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[ids[i]], 1u);
+    __syncthreads();
+    for (int p = threadIdx.x; p < parts; p += blockDim.x)
+        if (h[p]) atomicAdd(&counts[p], (unsigned long long)h[p]);
+}
+
+__global__ void k_u64_to_u32_idx(const int64_t *__restrict__ in, int64_t n, int64_t limit, uint32_t *__restrict__ out,
+                                 uint32_t *__restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = in[i];
+        if (v < 0 || v >= limit) *bad = 1u;
+        out[i] = (uint32_t)(v < 0 || v >= limit ? 0 : v);
+    }
+}
+
+}  // namespace qeh
+
+using namespace qeh;
+
+extern "C" int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending,
+                                qeh_column *out_perm) {
+    if (!ctx || !keys || !out_perm) return fail(QEH_E_INVALID, "qeh_sort_indices: bad argument");
+    DeviceGuard dg(ctx->device);
+    int64_t n;
+    QEH_TRY(check_sort_keys(keys, n_keys, &n));
+    RadixState rs;
+    QEH_TRY(sort_perm(ctx, keys, n_keys, ascending, n, rs));
+    QEH_TRY(alloc_column(ctx, QEH_DT_UINT32, n, false, out_perm));
+    if (n > 0) QEH_HIP(hipMemcpyAsync(out_perm->values, rs.v[rs.cur].p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+extern "C" int qeh_take(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out) {
+    if (!ctx || !col || !indices || !out) return fail(QEH_E_INVALID, "qeh_take: bad argument");
+    DeviceGuard dg(ctx->device);
+    if (indices->validity) return fail(QEH_E_UNSUPPORTED, "take: nullable indices");
+    const int64_t m = indices->length;
+    if (indices->dtype == QEH_DT_UINT32) {
+        const uint32_t *idx = (const uint32_t *)indices->values + indices->offset;
+        QEH_TRY(gather_column(ctx, *col, idx, m, out));
+        QEH_HIP(hipStreamSynchronize(ctx->stream));
+        return QEH_OK;
+    }
+    if (indices->dtype != QEH_DT_INT64) return fail(QEH_E_INVALID, "take: indices must be UInt32 or Int64");
+    DevBuf idx, bad;
+    QEH_TRY(idx.alloc(ctx, (size_t)std::max<int64_t>(m, 1) * 4));
+    QEH_TRY(bad.alloc(ctx, 8));
+    QEH_HIP(hipMemsetAsync(bad.p, 0, 8, ctx->stream));
+    if (m > 0)
+        hipLaunchKernelGGL(k_u64_to_u32_idx, dim3(grid_for(ctx, m, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                           (const int64_t *)indices->values + indices->offset, m, col->length, idx.as<uint32_t>(),
+                           bad.as<uint32_t>());
+    uint32_t b = 0;
+    QEH_TRY(read_small(ctx, &b, bad.p, 4));
+    if (b) return fail(QEH_E_INVALID, "take: index out of bounds");
+    QEH_TRY(gather_column(ctx, *col, idx.as<uint32_t>(), m, out));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_part, const qeh_column *order_keys,
+                              int n_order, const int8_t *ascending, qeh_column *out_rn) {
+    if (!ctx || !out_rn || (n_part + n_order) < 1) return fail(QEH_E_INVALID, "qeh_row_number: bad argument");
+    if (n_part > kMaxGroupKeys) return fail(QEH_E_UNSUPPORTED, "at most 4 PARTITION BY keys on the device");
+    DeviceGuard dg(ctx->device);
+    std::vector<qeh_column> all;
+    std::vector<int8_t> asc;
+    for (int j = 0; j < n_part; ++j) {
+        all.push_back(part_keys[j]);
+        asc.push_back(1);
+    }
+    for (int j = 0; j < n_order; ++j) {
+        all.push_back(order_keys[j]);
+        asc.push_back(ascending ? ascending[j] : 1);
+    }
+    int64_t n;
+    QEH_TRY(check_sort_keys(all.data(), (int)all.size(), &n));
+    RadixState rs;
+    QEH_TRY(sort_perm(ctx, all.data(), (int)all.size(), asc.data(), n, rs));
+    QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out_rn));
+    if (n == 0) return QEH_OK;
+    const uint32_t *perm = rs.v[rs.cur].as<uint32_t>();
+    DevBuf flags, seg, starts;
+    int s = flags.alloc(ctx, (size_t)n * 4);
+    if (s == QEH_OK) s = seg.alloc(ctx, (size_t)n * 8);
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out_rn);
+        return s;
+    }
+    KeyCols pk{};
+    pk.n = n_part;
+    for (int j = 0; j < n_part; ++j) pk.c[j] = make_colref(part_keys[j]);
+    const int grid = grid_for(ctx, n, kBlock * 8, 8);
+    {
+        KernelTimer kt(ctx, "row_number");
+        hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
+    }
+    uint64_t nseg = 0;
+    s = exclusive_scan_u32(ctx, flags.as<uint32_t>(), seg.as<uint64_t>(), n, &nseg);
+    if (s == QEH_OK) s = starts.alloc(ctx, (size_t)std::max<uint64_t>(nseg, 1) * 8);
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out_rn);
+        return s;
+    }
+    {
+        KernelTimer kt(ctx, "row_number");
+        hipLaunchKernelGGL(k_part_starts, dim3(grid), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<uint64_t>(), n,
+                           starts.as<uint64_t>());
+        hipLaunchKernelGGL(k_row_numbers, dim3(grid), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<uint64_t>(),
+                           starts.as<uint64_t>(), perm, n, (int64_t *)out_rn->values);
+    }
+    QEH_HIP(hipGetLastError());
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+extern "C" int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
+                                  qeh_column *out_perm) {
+    if (!ctx || !key || !counts || !out_perm || n_parts < 1 || n_parts > kRadix)
+        return fail(QEH_E_INVALID, "qeh_hash_partition: bad argument (1..256 partitions)");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*key, "partition key"));
+    if (key->dtype != QEH_DT_INT64 && key->dtype != QEH_DT_INT32)
+        return fail(QEH_E_UNSUPPORTED, "partition keys must be Int32/Int64 on the device");
+    const int64_t n = key->length;
+    RadixState rs;
+    rs.n = n;
+    for (int b = 0; b < 2; ++b) {
+        QEH_TRY(rs.k[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 8));
+        QEH_TRY(rs.v[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4));
+    }
+    std::fill(counts, counts + n_parts, 0);
+    if (n > 0) {
+        {
+            KernelTimer kt(ctx, "hash_partition");
+            hipLaunchKernelGGL(k_partition_ids, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                               make_colref(*key), n, (uint32_t)n_parts, rs.k[0].as<uint64_t>(), rs.v[0].as<uint32_t>());
+        }
+        QEH_HIP(hipGetLastError());
+        QEH_TRY(radix_passes(ctx, rs, n_parts > 1 ? bit_length((uint64_t)n_parts - 1) : 0));
+    }
+    QEH_TRY(alloc_column(ctx, QEH_DT_UINT32, n, false, out_perm));
+    if (n > 0) {
+        QEH_HIP(hipMemcpyAsync(out_perm->values, rs.v[rs.cur].p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        DevBuf cnt;
+        int s = cnt.alloc(ctx, (size_t)n_parts * 8);
+        if (s == QEH_OK) {
+            QEH_HIP(hipMemsetAsync(cnt.p, 0, (size_t)n_parts * 8, ctx->stream));
+            hipLaunchKernelGGL(k_count_parts, dim3(grid_for(ctx, n, kBlock * 16, 4)), dim3(kBlock), 0, ctx->stream,
+                               rs.k[rs.cur].as<uint64_t>(), n, n_parts, cnt.as<unsigned long long>());
+            s = read_small(ctx, counts, cnt.p, (size_t)n_parts * 8);
+        }
+        if (s != QEH_OK) {
+            qeh_column_release(ctx, out_perm);
+            return s;
+        }
+    }
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}

@@ -105,7 +105,8 @@ def eval_expr(cols: Sequence[HostCol], expr, n_rows: int):
     na = (abi.QehExprNode * len(nodes))(*nodes)
     out = QoCol()
     _check(lib().qo_eval(_arr(cols), len(cols), C.c_int64(n_rows), na, len(nodes), C.byref(out)))
-    return _take(out), out.dtype
+    dt = out.dtype
+    return _take(out), dt
 
 
 def filter(cols: Sequence[HostCol], pred, out_idx: Optional[Sequence[int]] = None):

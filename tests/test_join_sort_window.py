@@ -1,0 +1,161 @@
+"""HashJoin (INNER, materialising), Sort, ROW_NUMBER and hash partitioning:
+device through the C ABI vs the CPU oracle (intended semantics).
+Integer/index results bit-exact.  Join output is compared as a multiset, and
+additionally in order when the build keys are unique (left-row order = the
+order of the reference's filtered Cartesian product, executor.rs:500-540)."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from helpers import rows_of, sorted_rows
+
+
+def col_pair(c):
+    return c.to_numpy()
+
+
+def join_both(ctx, pk, pcols, bk, bcols):
+    dp = [ctx.upload(*c) for c in pcols]
+    db = [ctx.upload(*c) for c in bcols]
+    op, obd, rows = ctx.hash_join_inner(ctx.upload(*pk), dp, ctx.upload(*bk), db)
+    got = [c.to_numpy() for c in op] + [c.to_numpy() for c in obd]
+    wp, wb, wrows = ob.hash_join_inner(ob.HostCol(*pk), [ob.HostCol(*c) for c in pcols], ob.HostCol(*bk),
+                                       [ob.HostCol(*c) for c in bcols])
+    assert rows == wrows
+    return got, wp + wb
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_probe,n_build", [(0, 10), (10, 0), (1, 1), (5000, 100), (1_000_000, 100_000)])
+def test_join_unique_build_in_order(ctx, n_probe, n_build):
+    r = np.random.default_rng(n_probe + n_build)
+    bk = r.permutation(max(n_build, 1))[:n_build].astype(np.int64) * 3
+    ba = r.integers(-5, 5, n_build).astype(np.int64)
+    pk = r.integers(0, 3 * max(n_build, 1), n_probe).astype(np.int64)
+    pv = r.random(n_probe)
+    got, want = join_both(ctx, (pk, None), [(pv, None), (pk, None)], (bk, None), [(ba, None), (bk, None)])
+    assert rows_of(got) == rows_of(want)  # same order
+
+
+@pytest.mark.gpu
+def test_join_duplicates_nulls_int32_keys(ctx):
+    r = np.random.default_rng(9)
+    bk = r.integers(0, 500, 3000).astype(np.int32)
+    bkv = r.random(3000) > 0.1
+    ba = r.random(3000)
+    pk = r.integers(0, 600, 40_000).astype(np.int64)
+    pkv = r.random(40_000) > 0.05
+    pb = r.random(40_000) > 0.5
+    got, want = join_both(ctx, (pk, pkv), [(pk, pkv), (pb, None)], (bk, bkv), [(ba, bkv), (bk, bkv)])
+    assert sorted_rows(got) == sorted_rows(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("table", ["direct", "packed", "wide"])
+def test_join_table_layouts(ctx, monkeypatch, table):
+    monkeypatch.setenv("QEH_FORCE_TABLE", table)
+    r = np.random.default_rng(2)
+    bk = r.integers(-(2 ** 20), 2 ** 20, 20_000).astype(np.int64)
+    pk = bk[r.integers(0, len(bk), 100_000)]
+    got, want = join_both(ctx, (pk, None), [(pk, None)], (bk, None), [(bk, None)])
+    assert sorted_rows(got) == sorted_rows(want)
+
+
+def sort_both(ctx, keys, asc):
+    perm = ctx.sort_indices([ctx.upload(*k) for k in keys], asc).to_numpy()[0]
+    want = ob.sort_indices([ob.HostCol(*k) for k in keys], asc)
+    return perm, want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 100_000, 2_000_000])
+def test_sort_single_int64_stable(ctx, n):
+    r = np.random.default_rng(n)
+    k = r.integers(-1000, 1000, n).astype(np.int64)  # many ties -> stability matters
+    perm, want = sort_both(ctx, [(k, None)], [True])
+    assert np.array_equal(perm, want)
+
+
+@pytest.mark.gpu
+def test_sort_multi_key_mixed_types_nulls_desc(ctx):
+    r = np.random.default_rng(4)
+    n = 300_000
+    a = r.integers(0, 20, n).astype(np.int32)
+    av = r.random(n) > 0.05
+    b = np.round(r.standard_normal(n), 2)
+    bv = r.random(n) > 0.1
+    c = r.integers(-(2 ** 62), 2 ** 62, n).astype(np.int64)
+    d = r.random(n) > 0.5
+    for asc in ([True, False, True, True], [False, True, False, False]):
+        perm, want = sort_both(ctx, [(a, av), (b, bv), (c, None), (d, None)], asc)
+        assert np.array_equal(perm, want)
+
+
+@pytest.mark.gpu
+def test_sort_full_range_int64_and_negative_zero(ctx):
+    k = np.array([2 ** 63 - 1, -(2 ** 63), 0, -1, 1, 2 ** 63 - 1, -(2 ** 63)], np.int64)
+    perm, want = sort_both(ctx, [(k, None)], [True])
+    assert np.array_equal(perm, want)
+    f = np.array([0.0, -0.0, 1.5, -1.5, np.inf, -np.inf, 0.0], np.float64)  # totalOrder: -0.0 < +0.0
+    perm, want = sort_both(ctx, [(f, None)], [True])
+    assert np.array_equal(perm, want)
+
+
+@pytest.mark.gpu
+def test_take_gather(ctx):
+    r = np.random.default_rng(8)
+    v = r.random(10_000)
+    m = r.random(10_000) > 0.3
+    idx = r.integers(0, 10_000, 5000).astype(np.uint32)
+    out = ctx.take(ctx.upload(v, m), ctx.upload(idx))
+    gv, gm = out.to_numpy()
+    assert np.array_equal(gm, m[idx])
+    assert np.array_equal(gv[gm], v[idx][m[idx]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", [(0, 4), (1, 1), (10_000, 7), (1_000_000, 1024)])
+def test_row_number(ctx, n, parts):
+    r = np.random.default_rng(n)
+    k = r.integers(0, parts, n).astype(np.int64)
+    v = r.integers(-50, 50, n).astype(np.int64)  # ties inside partitions: broken by input position
+    rn = ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [True]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k)], [ob.HostCol(v)], [True])
+    assert np.array_equal(rn, want)
+
+
+@pytest.mark.gpu
+def test_row_number_nulls_desc_two_order_keys(ctx):
+    r = np.random.default_rng(12)
+    n = 50_000
+    k = r.integers(0, 30, n).astype(np.int32)
+    kv = r.random(n) > 0.1
+    v = r.random(n)
+    vv = r.random(n) > 0.2
+    w = r.integers(0, 3, n).astype(np.int64)
+    rn = ctx.row_number([ctx.upload(k, kv)], [ctx.upload(v, vv), ctx.upload(w)], [False, True]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k, kv)], [ob.HostCol(v, vv), ob.HostCol(w)], [False, True])
+    assert np.array_equal(rn, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [1, 2, 8, 256])
+def test_hash_partition_conserves_rows(ctx, parts):
+    """partition.rs:400-415 pins row conservation; we also pin determinism,
+    stability within a partition and key -> single partition."""
+    r = np.random.default_rng(parts)
+    k = r.integers(0, 5000, 200_000).astype(np.int64)
+    kv = r.random(200_000) > 0.01
+    counts, perm = ctx.hash_partition(ctx.upload(k, kv), parts)
+    p = perm.to_numpy()[0]
+    assert counts.sum() == len(k)
+    assert np.array_equal(np.sort(p), np.arange(len(k), dtype=np.uint32))  # a permutation
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    seen = {}
+    for q in range(parts):
+        rows = p[offs[q]:offs[q + 1]]
+        assert np.all(np.diff(rows.astype(np.int64)) > 0)  # stable within a partition
+        for key in np.unique(np.where(kv[rows], k[rows], -1)):
+            assert seen.setdefault(int(key), q) == q  # one partition per key
+    counts2, perm2 = ctx.hash_partition(ctx.upload(k, kv), parts)
+    assert np.array_equal(counts, counts2) and np.array_equal(perm2.to_numpy()[0], p)
