@@ -1,0 +1,810 @@
+// QueryExecutor on the device: walks the reference's PhysicalPlan enum
+// (crates/query-executor/src/physical_plan.rs:13-72, flattened by
+// include/qeh_plan.h) the way QueryExecutor::execute_plan does
+// (crates/query-executor/src/executor.rs:23-91): post-order, every child
+// fully materialised — but the materialised tables stay in HBM, and the
+// patterns the reference's planner emits for the hot path are fused:
+//   HashAggregate(Filter(HashJoin(L, R)))  -> qeh_join_filter_aggregate
+//   HashAggregate(HashJoin(L, R))          -> qeh_join_filter_aggregate (no predicate)
+//   HashAggregate(Filter(X)), grouped      -> qeh_filter_aggregate
+// Semantics per node: Scan uploads DataSource batches;
+// Filter drops NULL-predicate rows and empty batches (executor.rs:131-155);
+// Projection uses the planner schema's names (executor.rs:93-129); global
+// aggregates keep the "no input batch -> no row" quirk (executor.rs:157-190);
+// GROUP BY, INNER equi-join, Sort and ROW_NUMBER follow the intended
+// semantics; Limit slices (executor.rs:299-341); SubqueryScan and IndexScan
+// behave as in the reference (executor.rs:72-88).
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/qeh_plan.h"
+#include "ops.h"
+
+namespace qeh {
+int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const qeh_column *agg_inputs,
+                            int n_inputs, const qeh_agg *aggs, int n_aggs, const qeh_column *pred_cols,
+                            int n_pred_cols, const qeh_expr *predicate, int64_t input_batches,
+                            qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups);
+}
+
+namespace {
+
+using namespace qeh;
+
+struct Holder {
+    qeh_ctx *ctx = nullptr;
+    qeh_column c{};
+    ~Holder() {
+        if (c.owned) qeh_column_release(ctx, &c);
+    }
+};
+
+struct Col {
+    qeh_column c{};                  // view (offset/length may differ from the owner's)
+    std::shared_ptr<Holder> owner;   // keeps the buffers alive
+};
+
+struct Field {
+    std::string name;
+    int dtype;
+    bool nullable;
+};
+
+struct Table {
+    std::vector<Field> fields;
+    std::vector<Col> cols;
+    int64_t rows = 0;
+    int64_t batches = 0;  // >0 iff the reference would hold at least one batch here
+};
+
+Col own(qeh_ctx *ctx, const qeh_column &c) {
+    Col r;
+    r.c = c;
+    auto h = std::make_shared<Holder>();  // constructed in place: exactly one releasing owner
+    h->ctx = ctx;
+    h->c = c;
+    r.owner = h;
+    return r;
+}
+
+// ---- Arrow import ----------------------------------------------------------------------
+int dtype_of_format(const char *f, int *dt) {
+    if (!f) return fail(QEH_E_INVALID, "arrow schema without format");
+    if (!std::strcmp(f, "l")) *dt = QEH_DT_INT64;
+    else if (!std::strcmp(f, "i")) *dt = QEH_DT_INT32;
+    else if (!std::strcmp(f, "g")) *dt = QEH_DT_FLOAT64;
+    else if (!std::strcmp(f, "f")) *dt = QEH_DT_FLOAT32;
+    else if (!std::strcmp(f, "b")) *dt = QEH_DT_BOOL;
+    else if (!std::strcmp(f, "u")) *dt = QEH_DT_UTF8;
+    else return fail(QEH_E_UNSUPPORTED, std::string("arrow type '") + f + "' is not supported on the device");
+    return QEH_OK;
+}
+
+const char *format_of_dtype(int dt) {
+    switch (dt) {
+        case QEH_DT_INT64: return "l";
+        case QEH_DT_INT32: return "i";
+        case QEH_DT_FLOAT64: return "g";
+        case QEH_DT_FLOAT32: return "f";
+        case QEH_DT_BOOL: return "b";
+        case QEH_DT_UTF8: return "u";
+        case QEH_DT_UINT32: return "I";
+        default: return "n";
+    }
+}
+
+inline bool get_bit(const uint8_t *b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
+inline void set_bit(uint8_t *b, int64_t i, bool v) {
+    if (v) b[i >> 3] |= (uint8_t)(1u << (i & 7));
+    else b[i >> 3] &= (uint8_t)~(1u << (i & 7));
+}
+
+int upload_host(qeh_ctx *ctx, void **dst, const void *src, size_t bytes) {
+    QEH_TRY(ctx->pool->alloc(bytes ? bytes : 8, dst));
+    if (bytes) QEH_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return QEH_OK;
+}
+
+// Concatenate column `ci` of every batch into one device column.
+int import_column(qeh_ctx *ctx, const qeh_source &src, int ci, int dt, Col *out) {
+    int64_t total = 0;
+    bool any_nulls = false;
+    for (int64_t b = 0; b < src.n_batches; ++b) {
+        const ArrowArray *batch = src.batches[b];
+        if (ci >= batch->n_children) return fail(QEH_E_INVALID, "record batch has fewer columns than its schema");
+        const ArrowArray *ch = batch->children[ci];
+        total += batch->length;
+        if (ch->null_count != 0 && ch->buffers[0]) any_nulls = true;
+    }
+    qeh_column c{};
+    c.dtype = dt;
+    c.owned = 1;
+    c.length = total;
+    c.null_count = 0;
+    const size_t vbytes = (size_t)((total + 63) / 64) * 8 + 8;
+    std::vector<uint8_t> valid;
+    if (any_nulls) valid.assign(vbytes, 0);
+    std::vector<uint8_t> vals;
+    std::vector<int32_t> offs;
+    std::vector<uint8_t> data;
+    const size_t es = dtype_size(dt);
+    if (dt == QEH_DT_BOOL) vals.assign(vbytes, 0);
+    else if (dt == QEH_DT_UTF8) offs.assign((size_t)total + 1, 0);
+    else vals.resize((size_t)total * es);
+    int64_t pos = 0;
+    int64_t nulls = 0;
+    for (int64_t b = 0; b < src.n_batches; ++b) {
+        const ArrowArray *batch = src.batches[b];
+        const ArrowArray *ch = batch->children[ci];
+        const int64_t len = batch->length, off = batch->offset + ch->offset;
+        const uint8_t *vb = (const uint8_t *)ch->buffers[0];
+        for (int64_t i = 0; i < len; ++i) {
+            const bool v = !(ch->null_count != 0 && vb) || get_bit(vb, off + i);
+            if (any_nulls) set_bit(valid.data(), pos + i, v);
+            nulls += !v;
+        }
+        if (dt == QEH_DT_BOOL) {
+            const uint8_t *bits = (const uint8_t *)ch->buffers[1];
+            for (int64_t i = 0; i < len; ++i) set_bit(vals.data(), pos + i, get_bit(bits, off + i));
+        } else if (dt == QEH_DT_UTF8) {
+            const int32_t *so = (const int32_t *)ch->buffers[1];
+            const uint8_t *sd = (const uint8_t *)ch->buffers[2];
+            const int32_t base = (int32_t)data.size();
+            data.insert(data.end(), sd + so[off], sd + so[off + len]);
+            for (int64_t i = 0; i < len; ++i) offs[(size_t)(pos + i + 1)] = base + (so[off + i + 1] - so[off]);
+        } else if (len) {
+            std::memcpy(vals.data() + (size_t)pos * es, (const uint8_t *)ch->buffers[1] + (size_t)off * es, (size_t)len * es);
+        }
+        pos += len;
+    }
+    c.null_count = nulls;
+    void *p = nullptr;
+    if (dt == QEH_DT_UTF8) {
+        QEH_TRY(upload_host(ctx, &p, offs.data(), offs.size() * 4));
+        c.offsets = (int32_t *)p;
+        QEH_TRY(upload_host(ctx, &p, data.data(), data.size()));
+        c.values = p;
+        c.values_bytes = (int64_t)data.size();
+    } else {
+        QEH_TRY(upload_host(ctx, &p, vals.data(), vals.size()));
+        c.values = p;
+    }
+    if (any_nulls && nulls > 0) {
+        QEH_TRY(upload_host(ctx, &p, valid.data(), valid.size()));
+        c.validity = (uint8_t *)p;
+    }
+    QEH_HIP(hipStreamSynchronize(ctx->stream));  // host staging buffers die here
+    *out = own(ctx, c);
+    return QEH_OK;
+}
+
+int import_source(qeh_ctx *ctx, const qeh_source &src, Table *t) {
+    if (!src.schema) return fail(QEH_E_INVALID, "source without schema");
+    t->fields.clear();
+    t->cols.clear();
+    for (int64_t i = 0; i < src.schema->n_children; ++i) {
+        const ArrowSchema *f = src.schema->children[i];
+        int dt;
+        QEH_TRY(dtype_of_format(f->format, &dt));
+        t->fields.push_back({f->name ? f->name : "", dt, (f->flags & ARROW_FLAG_NULLABLE) != 0});
+        Col c;
+        QEH_TRY(import_column(ctx, src, (int)i, dt, &c));
+        t->cols.push_back(c);
+    }
+    t->rows = 0;
+    for (int64_t b = 0; b < src.n_batches; ++b) t->rows += src.batches[b]->length;
+    t->batches = src.n_batches;
+    return QEH_OK;
+}
+
+// ---- Arrow export ----------------------------------------------------------------------
+struct ExportArray {
+    std::vector<std::vector<uint8_t>> bufs;
+    std::vector<const void *> ptrs;
+    std::vector<ArrowArray *> children;
+};
+struct ExportSchema {
+    std::string format, name;
+    std::vector<ArrowSchema *> children;
+};
+
+void release_array(ArrowArray *a) {
+    if (!a || !a->release) return;
+    for (int64_t i = 0; i < a->n_children; ++i) {
+        if (a->children[i]->release) a->children[i]->release(a->children[i]);
+        delete a->children[i];
+    }
+    delete (ExportArray *)a->private_data;
+    a->release = nullptr;
+}
+
+void release_schema(ArrowSchema *s) {
+    if (!s || !s->release) return;
+    for (int64_t i = 0; i < s->n_children; ++i) {
+        if (s->children[i]->release) s->children[i]->release(s->children[i]);
+        delete s->children[i];
+    }
+    delete (ExportSchema *)s->private_data;
+    s->release = nullptr;
+}
+
+int download(qeh_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return QEH_OK;
+    QEH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return QEH_OK;
+}
+
+int export_column(qeh_ctx *ctx, const Col &col, ArrowArray *out) {
+    const qeh_column &c = col.c;
+    const int64_t n = c.length, off = c.offset;
+    auto *ex = new ExportArray();
+    ex->bufs.resize(3);
+    std::vector<uint8_t> tmp;
+    const size_t bitbytes = (size_t)(n + 7) / 8 + 8;
+    int64_t nulls = 0;
+    int s = QEH_OK;
+    if (c.validity) {
+        const size_t src_bytes = (size_t)(off + n + 7) / 8;
+        tmp.resize(src_bytes + 8);
+        s = download(ctx, tmp.data(), c.validity, src_bytes);
+    }
+    std::vector<uint8_t> raw;
+    if (s == QEH_OK) {
+        if (c.dtype == QEH_DT_BOOL) {
+            raw.resize((size_t)(off + n + 7) / 8 + 8);
+            s = download(ctx, raw.data(), c.values, (size_t)(off + n + 7) / 8);
+        } else if (c.dtype == QEH_DT_UTF8) {
+            ex->bufs[1].resize((size_t)(n + 1) * 4);
+            s = download(ctx, ex->bufs[1].data(), c.offsets + off, (size_t)(n + 1) * 4);
+        } else {
+            const size_t es = dtype_size(c.dtype);
+            ex->bufs[1].resize((size_t)n * es + 8);
+            s = download(ctx, ex->bufs[1].data(), (const char *)c.values + (size_t)off * es, (size_t)n * es);
+        }
+    }
+    if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "export: stream sync failed");
+    if (s != QEH_OK) {
+        delete ex;
+        return s;
+    }
+    if (c.validity) {
+        ex->bufs[0].assign(bitbytes, 0);
+        for (int64_t i = 0; i < n; ++i) {
+            const bool v = get_bit(tmp.data(), off + i);
+            set_bit(ex->bufs[0].data(), i, v);
+            nulls += !v;
+        }
+    }
+    if (c.dtype == QEH_DT_BOOL) {
+        ex->bufs[1].assign(bitbytes, 0);
+        for (int64_t i = 0; i < n; ++i) set_bit(ex->bufs[1].data(), i, get_bit(raw.data(), off + i));
+    }
+    int nbuf = 2;
+    if (c.dtype == QEH_DT_UTF8) {
+        int32_t *o = (int32_t *)ex->bufs[1].data();
+        const int32_t b0 = o[0];
+        const int32_t b1 = o[n];
+        ex->bufs[2].resize((size_t)(b1 - b0) + 8);
+        if (b1 > b0) {
+            if (download(ctx, ex->bufs[2].data(), (const uint8_t *)c.values + b0, (size_t)(b1 - b0)) != QEH_OK ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess) {
+                delete ex;
+                return fail(QEH_E_HIP, "export: utf8 download failed");
+            }
+        }
+        for (int64_t i = 0; i <= n; ++i) o[i] -= b0;
+        nbuf = 3;
+    }
+    ex->ptrs.resize(nbuf);
+    ex->ptrs[0] = c.validity ? ex->bufs[0].data() : nullptr;
+    for (int i = 1; i < nbuf; ++i) ex->ptrs[i] = ex->bufs[i].data();
+    std::memset(out, 0, sizeof(*out));
+    out->length = n;
+    out->null_count = nulls;
+    out->offset = 0;
+    out->n_buffers = nbuf;
+    out->buffers = ex->ptrs.data();
+    out->release = release_array;
+    out->private_data = ex;
+    return QEH_OK;
+}
+
+int export_table(qeh_ctx *ctx, const Table &t, ArrowSchema *os, ArrowArray *oa) {
+    auto *ea = new ExportArray();
+    auto *es = new ExportSchema();
+    es->format = "+s";
+    std::memset(oa, 0, sizeof(*oa));
+    std::memset(os, 0, sizeof(*os));
+    oa->length = t.rows;
+    oa->n_buffers = 1;
+    ea->ptrs.push_back(nullptr);
+    oa->buffers = ea->ptrs.data();
+    oa->release = release_array;
+    oa->private_data = ea;
+    os->format = es->format.c_str();
+    os->name = "";
+    os->release = release_schema;
+    os->private_data = es;
+    for (size_t i = 0; i < t.cols.size(); ++i) {
+        auto *ca = new ArrowArray();
+        int s = export_column(ctx, t.cols[i], ca);
+        if (s != QEH_OK) {
+            delete ca;
+            oa->n_children = (int64_t)ea->children.size();
+            oa->children = ea->children.data();
+            release_array(oa);
+            os->n_children = (int64_t)es->children.size();
+            os->children = es->children.data();
+            release_schema(os);
+            return s;
+        }
+        ea->children.push_back(ca);
+        auto *cs = new ArrowSchema();
+        auto *ces = new ExportSchema();
+        ces->format = format_of_dtype(t.fields[i].dtype);
+        ces->name = t.fields[i].name;
+        std::memset(cs, 0, sizeof(*cs));
+        cs->format = ces->format.c_str();
+        cs->name = ces->name.c_str();
+        cs->flags = t.fields[i].nullable ? ARROW_FLAG_NULLABLE : 0;
+        cs->release = release_schema;
+        cs->private_data = ces;
+        es->children.push_back(cs);
+    }
+    oa->n_children = (int64_t)ea->children.size();
+    oa->children = ea->children.data();
+    os->n_children = (int64_t)es->children.size();
+    os->children = es->children.data();
+    return QEH_OK;
+}
+
+// ---- cross join index generation -------------------------------------------------------
+__global__ void k_cross_indices(int64_t nl, int64_t nr, uint32_t *li, uint32_t *ri) {
+    const int64_t m = nl * nr;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        li[i] = (uint32_t)(i / nr);  // left row-major (executor.rs:437-498)
+        ri[i] = (uint32_t)(i % nr);
+    }
+}
+
+// ---- the executor ------------------------------------------------------------------------
+class Executor {
+  public:
+    Executor(qeh_ctx *ctx, const qeh_plan *plan, const qeh_source *src, int n_src)
+        : ctx_(ctx), plan_(plan), src_(src), n_src_(n_src) {}
+
+    int run(int node, Table *out, int depth = 0) {
+        if (node < 0 || node >= plan_->n_nodes) return fail(QEH_E_INVALID, "plan node index out of range");
+        if (depth > 256) return fail(QEH_E_INVALID, "plan too deep (cycle?)");
+        const qeh_plan_node &nd = plan_->nodes[node];
+        switch (nd.kind) {
+            case QEH_PLAN_SCAN:
+            case QEH_PLAN_INDEX_SCAN:  // executor.rs:81-88: IndexScan falls back to a full scan
+                if (nd.source < 0 || nd.source >= n_src_) return fail(QEH_E_INVALID, "scan source index out of range");
+                return import_source(ctx_, src_[nd.source], out);
+            case QEH_PLAN_SUBQUERY_SCAN: return run(nd.input, out, depth + 1);
+            case QEH_PLAN_FILTER: return filter(nd, out, depth);
+            case QEH_PLAN_PROJECTION: return projection(nd, out, depth);
+            case QEH_PLAN_HASH_AGGREGATE: return aggregate(nd, out, depth);
+            case QEH_PLAN_HASH_JOIN: return join(nd, out, depth);
+            case QEH_PLAN_SORT: return sort(nd, out, depth);
+            case QEH_PLAN_LIMIT: return limit(nd, out, depth);
+            case QEH_PLAN_WINDOW: return window(nd, out, depth);
+            default: return fail(QEH_E_INVALID, "unknown plan node kind");
+        }
+    }
+
+  private:
+    qeh_ctx *ctx_;
+    const qeh_plan *plan_;
+    const qeh_source *src_;
+    int n_src_;
+
+    static std::vector<qeh_column> raw(const Table &t) {
+        std::vector<qeh_column> v;
+        for (auto &c : t.cols) v.push_back(c.c);
+        return v;
+    }
+
+    int eval(const Table &t, const qeh_expr &e, Col *out) {
+        const int ci = expr_as_column(&e);
+        if (ci >= 0) {
+            if (ci >= (int)t.cols.size())
+                return fail(QEH_E_INVALID, "Column index " + std::to_string(ci) + " out of bounds");
+            *out = t.cols[ci];
+            return QEH_OK;
+        }
+        auto cols = raw(t);
+        qeh_column r{};
+        QEH_TRY(qeh_eval(ctx_, cols.data(), (int)cols.size(), &e, t.rows, &r));
+        *out = own(ctx_, r);
+        return QEH_OK;
+    }
+
+    int filter(const qeh_plan_node &nd, Table *out, int depth) {
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        return filter_table(in, nd.predicate, out);
+    }
+
+    int filter_table(const Table &in, const qeh_expr &pred, Table *out) {
+        out->fields = in.fields;
+        out->cols.clear();
+        auto cols = raw(in);
+        std::vector<int32_t> idx(cols.size());
+        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+        std::vector<qeh_column> res(std::max<size_t>(cols.size(), 1));
+        int64_t rows = 0;
+        if (cols.empty()) return fail(QEH_E_UNSUPPORTED, "filter over a batch without columns");
+        QEH_TRY(qeh_filter(ctx_, cols.data(), (int)cols.size(), &pred, idx.data(), (int)idx.size(), res.data(), &rows));
+        for (size_t i = 0; i < cols.size(); ++i) out->cols.push_back(own(ctx_, res[i]));
+        out->rows = rows;
+        out->batches = (in.batches > 0 && rows > 0) ? 1 : 0;  // empty batches are dropped (executor.rs:149-151)
+        return QEH_OK;
+    }
+
+    int projection(const qeh_plan_node &nd, Table *out, int depth) {
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        out->fields.clear();
+        out->cols.clear();
+        for (int i = 0; i < nd.n_exprs; ++i) {
+            Col c;
+            QEH_TRY(eval(in, nd.exprs[i], &c));
+            std::string name = (nd.field_names && i < nd.n_fields && nd.field_names[i]) ? nd.field_names[i]
+                                                                                        : "col_" + std::to_string(i);
+            out->fields.push_back({name, c.c.dtype, true});
+            out->cols.push_back(c);
+        }
+        out->rows = in.rows;
+        out->batches = nd.n_exprs == 0 ? 0 : in.batches;  // executor.rs:109-111
+        return QEH_OK;
+    }
+
+    // `on` = Column(a) = Column(b) with one side in each input
+    static bool equi_keys(const qeh_expr &on, int n_left, int *lk, int *rk) {
+        if (on.n_nodes != 3) return false;
+        const qeh_expr_node *n = on.nodes;
+        if (n[0].kind != QEH_EX_COLUMN || n[1].kind != QEH_EX_COLUMN || n[2].kind != QEH_EX_BINARY || n[2].op != QEH_OP_EQ)
+            return false;
+        int a = n[0].index, b = n[1].index;
+        if (a >= n_left && b < n_left) std::swap(a, b);
+        if (!(a < n_left && b >= n_left)) return false;
+        *lk = a;
+        *rk = b - n_left;
+        return true;
+    }
+
+    int join(const qeh_plan_node &nd, Table *out, int depth) {
+        Table l, r;
+        QEH_TRY(run(nd.left, &l, depth + 1));
+        QEH_TRY(run(nd.right, &r, depth + 1));
+        return join_tables(nd, l, r, out);
+    }
+
+    int join_tables(const qeh_plan_node &nd, const Table &l, const Table &r, Table *out) {
+        out->fields = l.fields;
+        out->fields.insert(out->fields.end(), r.fields.begin(), r.fields.end());
+        out->cols.clear();
+        out->rows = 0;
+        out->batches = 0;
+        if (l.batches == 0 || r.batches == 0) {  // executor.rs:350-352
+            for (auto &f : out->fields) {
+                qeh_column c{};
+                QEH_TRY(alloc_column(ctx_, f.dtype == QEH_DT_UTF8 ? QEH_DT_INT64 : f.dtype, 0, false, &c));
+                c.dtype = f.dtype;
+                out->cols.push_back(own(ctx_, c));
+            }
+            return QEH_OK;
+        }
+        std::vector<qeh_column> lo(l.cols.size()), ro(r.cols.size());
+        int64_t rows = 0;
+        auto lc = raw(l), rc = raw(r);
+        if (nd.join_type == QEH_JOIN_CROSS || (nd.join_type == QEH_JOIN_INNER && !nd.has_predicate)) {
+            const int64_t m = l.rows * r.rows;
+            if (m >= (int64_t)0xFFFFFFFF) return fail(QEH_E_UNSUPPORTED, "cross join output beyond 2^32 rows");
+            DevBuf li, ri;
+            QEH_TRY(li.alloc(ctx_, (size_t)std::max<int64_t>(m, 1) * 4));
+            QEH_TRY(ri.alloc(ctx_, (size_t)std::max<int64_t>(m, 1) * 4));
+            if (m > 0)
+                hipLaunchKernelGGL(k_cross_indices, dim3(grid_for(ctx_, m, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream,
+                                   l.rows, r.rows, li.as<uint32_t>(), ri.as<uint32_t>());
+            for (size_t i = 0; i < lc.size(); ++i) {
+                QEH_TRY(gather_column(ctx_, lc[i], li.as<uint32_t>(), m, &lo[i]));
+                out->cols.push_back(own(ctx_, lo[i]));
+            }
+            for (size_t i = 0; i < rc.size(); ++i) {
+                QEH_TRY(gather_column(ctx_, rc[i], ri.as<uint32_t>(), m, &ro[i]));
+                out->cols.push_back(own(ctx_, ro[i]));
+            }
+            QEH_HIP(hipStreamSynchronize(ctx_->stream));
+            rows = m;
+        } else {
+            if (nd.join_type != QEH_JOIN_INNER)
+                return fail(QEH_E_UNSUPPORTED, "LEFT/RIGHT/FULL joins are not implemented on the device (SURVEY.md §8 f3)");
+            int lk, rk;
+            if (!equi_keys(nd.predicate, (int)l.cols.size(), &lk, &rk))
+                return fail(QEH_E_UNSUPPORTED, "only single-column equi-joins (l.k = r.k) run on the device");
+            QEH_TRY(qeh_hash_join_inner(ctx_, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(), (int)rc.size(),
+                                        lo.data(), ro.data(), &rows));
+            for (auto &c : lo) out->cols.push_back(own(ctx_, c));
+            for (auto &c : ro) out->cols.push_back(own(ctx_, c));
+        }
+        out->rows = rows;
+        out->batches = rows > 0 ? 1 : 0;  // executor.rs:374-376 keeps non-empty joins only
+        return QEH_OK;
+    }
+
+    static bool all_columns(const qeh_expr *e, int n, int lo, int hi) {
+        for (int i = 0; i < n; ++i) {
+            int c = expr_as_column(&e[i]);
+            if (c < lo || c >= hi) return false;
+        }
+        return true;
+    }
+
+    int aggregate(const qeh_plan_node &nd, Table *out, int depth) {
+        out->fields.clear();
+        out->cols.clear();
+        out->rows = 0;
+        out->batches = 0;
+        if (nd.n_aggs == 0) {  // executor.rs:163-165
+            Table in;
+            QEH_TRY(run(nd.input, &in, depth + 1));
+            return QEH_OK;
+        }
+        const qeh_plan_node &child = plan_->nodes[nd.input];
+        const bool grouped = nd.n_exprs > 0;
+        std::vector<qeh_agg_expr> aggs(nd.aggs, nd.aggs + nd.n_aggs);
+        std::vector<qeh_expr> aexprs(nd.n_aggs);
+        for (int i = 0; i < nd.n_aggs; ++i) aexprs[i] = aggs[i].expr;
+
+        // fused: HashAggregate([Filter](HashJoin(L, R) on L.k = R.k)), grouped by R columns, aggregating L columns
+        const qeh_plan_node *jn = nullptr;
+        const qeh_expr *pred = nullptr;
+        if (grouped && !std::getenv("QEH_NO_FUSION")) {
+            if (child.kind == QEH_PLAN_HASH_JOIN) jn = &child;
+            else if (child.kind == QEH_PLAN_FILTER && plan_->nodes[child.input].kind == QEH_PLAN_HASH_JOIN) {
+                jn = &plan_->nodes[child.input];
+                pred = &child.predicate;
+            }
+            if (jn && !(jn->join_type == QEH_JOIN_INNER && jn->has_predicate)) jn = nullptr;
+        }
+        if (jn) {
+            Table l, r;
+            QEH_TRY(run(jn->left, &l, depth + 2));
+            QEH_TRY(run(jn->right, &r, depth + 2));
+            const int nl = (int)l.cols.size(), nr = (int)r.cols.size();
+            int lk, rk;
+            const bool keys_ok = equi_keys(jn->predicate, nl, &lk, &rk);
+            const bool pred_left = !pred || (expr_columns(pred) >> nl) == 0;
+            if (keys_ok && pred_left && all_columns(nd.exprs, nd.n_exprs, nl, nl + nr) &&
+                all_columns(aexprs.data(), nd.n_aggs, 0, nl) && l.batches > 0 && r.batches > 0) {
+                auto lc = raw(l), rc = raw(r);
+                std::vector<qeh_column> gk;
+                for (int i = 0; i < nd.n_exprs; ++i) gk.push_back(rc[expr_as_column(&nd.exprs[i]) - nl]);
+                std::vector<qeh_agg> qa(nd.n_aggs);
+                for (int i = 0; i < nd.n_aggs; ++i) qa[i] = {aggs[i].func, expr_as_column(&aexprs[i])};
+                std::vector<qeh_column> ok(gk.size()), oa(qa.size());
+                int64_t g = 0;
+                QEH_TRY(qeh_join_filter_aggregate(ctx_, lc.data(), nl, lk, pred, &rc[rk], gk.data(), (int)gk.size(),
+                                                  qa.data(), (int)qa.size(), ok.data(), oa.data(), &g));
+                for (int i = 0; i < nd.n_exprs; ++i) {
+                    const Field &f = r.fields[expr_as_column(&nd.exprs[i]) - nl];
+                    out->fields.push_back({f.name, f.dtype, true});
+                    out->cols.push_back(own(ctx_, ok[i]));
+                }
+                for (int i = 0; i < nd.n_aggs; ++i) {
+                    out->fields.push_back({"col_" + std::to_string(i), oa[i].dtype, true});
+                    out->cols.push_back(own(ctx_, oa[i]));
+                }
+                out->rows = g;
+                out->batches = g > 0 ? 1 : 0;
+                return QEH_OK;
+            }
+            // not fusable: materialise join (and filter) then aggregate
+            Table joined;
+            QEH_TRY(join_tables(*jn, l, r, &joined));
+            if (pred) {
+                Table f;
+                QEH_TRY(filter_table(joined, *pred, &f));
+                return aggregate_table(nd, f, out);
+            }
+            return aggregate_table(nd, joined, out);
+        }
+        // fused HashAggregate(Filter(X)) for GROUP BY
+        if (grouped && child.kind == QEH_PLAN_FILTER && !std::getenv("QEH_NO_FUSION")) {
+            Table in;
+            QEH_TRY(run(child.input, &in, depth + 2));
+            const int n = (int)in.cols.size();
+            if (all_columns(nd.exprs, nd.n_exprs, 0, n) && all_columns(aexprs.data(), nd.n_aggs, 0, n) && in.batches > 0) {
+                auto cols = raw(in);
+                std::vector<qeh_column> keys;
+                for (int i = 0; i < nd.n_exprs; ++i) keys.push_back(cols[expr_as_column(&nd.exprs[i])]);
+                std::vector<qeh_agg> qa(nd.n_aggs);
+                for (int i = 0; i < nd.n_aggs; ++i) qa[i] = {aggs[i].func, expr_as_column(&aexprs[i])};
+                std::vector<qeh_column> ok(keys.size()), oa(qa.size());
+                int64_t g = 0;
+                QEH_TRY(hash_aggregate_filtered(ctx_, keys.data(), (int)keys.size(), cols.data(), n, qa.data(),
+                                                (int)qa.size(), cols.data(), n, &child.predicate, in.batches, ok.data(),
+                                                oa.data(), &g));
+                for (int i = 0; i < nd.n_exprs; ++i) {
+                    const Field &f = in.fields[expr_as_column(&nd.exprs[i])];
+                    out->fields.push_back({f.name, f.dtype, true});
+                    out->cols.push_back(own(ctx_, ok[i]));
+                }
+                for (int i = 0; i < nd.n_aggs; ++i) {
+                    out->fields.push_back({"col_" + std::to_string(i), oa[i].dtype, true});
+                    out->cols.push_back(own(ctx_, oa[i]));
+                }
+                out->rows = g;
+                out->batches = g > 0 ? 1 : 0;
+                return QEH_OK;
+            }
+            Table f;
+            QEH_TRY(filter_table(in, child.predicate, &f));
+            return aggregate_table(nd, f, out);
+        }
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        return aggregate_table(nd, in, out);
+    }
+
+    int aggregate_table(const qeh_plan_node &nd, const Table &in, Table *out) {
+        out->fields.clear();
+        out->cols.clear();
+        std::vector<Col> keys, inputs;
+        for (int i = 0; i < nd.n_exprs; ++i) {
+            Col c;
+            QEH_TRY(eval(in, nd.exprs[i], &c));
+            keys.push_back(c);
+        }
+        for (int i = 0; i < nd.n_aggs; ++i) {
+            Col c;
+            QEH_TRY(eval(in, nd.aggs[i].expr, &c));
+            inputs.push_back(c);
+        }
+        std::vector<qeh_column> kc, ic;
+        for (auto &c : keys) kc.push_back(c.c);
+        for (auto &c : inputs) ic.push_back(c.c);
+        std::vector<qeh_agg> qa(nd.n_aggs);
+        for (int i = 0; i < nd.n_aggs; ++i) qa[i] = {nd.aggs[i].func, i};
+        std::vector<qeh_column> ok(std::max<size_t>(kc.size(), 1)), oa(qa.size());
+        int64_t g = 0;
+        QEH_TRY(qeh_hash_aggregate(ctx_, kc.data(), (int)kc.size(), ic.data(), (int)ic.size(), qa.data(), (int)qa.size(),
+                                   in.batches, ok.data(), oa.data(), &g));
+        if (nd.n_exprs == 0 && in.batches == 0) {  // executor.rs:178-186 / 196-198
+            out->rows = 0;
+            out->batches = 0;
+            return QEH_OK;
+        }
+        for (int i = 0; i < nd.n_exprs; ++i) {
+            const int ci = expr_as_column(&nd.exprs[i]);
+            std::string name = ci >= 0 ? in.fields[ci].name : "group_" + std::to_string(i);
+            out->fields.push_back({name, ok[i].dtype, true});
+            out->cols.push_back(own(ctx_, ok[i]));
+        }
+        for (int i = 0; i < nd.n_aggs; ++i) {
+            out->fields.push_back({"col_" + std::to_string(i), oa[i].dtype, true});  // executor.rs:203-207
+            out->cols.push_back(own(ctx_, oa[i]));
+        }
+        out->rows = g;
+        out->batches = g > 0 || nd.n_exprs == 0 ? 1 : 0;
+        return QEH_OK;
+    }
+
+    int sort(const qeh_plan_node &nd, Table *out, int depth) {
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        if (nd.n_exprs == 0 || in.rows == 0) {
+            *out = in;
+            return QEH_OK;
+        }
+        std::vector<Col> keys;
+        for (int i = 0; i < nd.n_exprs; ++i) {
+            Col c;
+            QEH_TRY(eval(in, nd.exprs[i], &c));
+            keys.push_back(c);
+        }
+        std::vector<qeh_column> kc;
+        for (auto &c : keys) kc.push_back(c.c);
+        std::vector<int8_t> asc(nd.n_exprs, 1);
+        for (int i = 0; i < nd.n_exprs; ++i)
+            if (nd.ascending) asc[i] = nd.ascending[i];
+        qeh_column perm{};
+        QEH_TRY(qeh_sort_indices(ctx_, kc.data(), (int)kc.size(), asc.data(), &perm));
+        Col p = own(ctx_, perm);
+        out->fields = in.fields;
+        out->cols.clear();
+        for (auto &c : in.cols) {
+            qeh_column g{};
+            QEH_TRY(qeh_take(ctx_, &c.c, &p.c, &g));
+            out->cols.push_back(own(ctx_, g));
+        }
+        out->rows = in.rows;
+        out->batches = in.batches;
+        return QEH_OK;
+    }
+
+    int limit(const qeh_plan_node &nd, Table *out, int depth) {
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        const int64_t start = std::min<int64_t>(std::max<int64_t>(nd.skip, 0), in.rows);
+        int64_t end = in.rows;
+        if (nd.fetch >= 0) end = std::min<int64_t>(end, start + nd.fetch);
+        *out = in;
+        for (auto &c : out->cols) {  // zero-copy slice (RecordBatch::slice)
+            c.c.offset += start;
+            c.c.length = end - start;
+            c.c.null_count = c.c.validity ? -1 : 0;
+        }
+        out->rows = end - start;
+        out->batches = (in.batches > 0 && out->rows > 0) ? 1 : 0;
+        return QEH_OK;
+    }
+
+    int window(const qeh_plan_node &nd, Table *out, int depth) {
+        Table in;
+        QEH_TRY(run(nd.input, &in, depth + 1));
+        *out = in;
+        for (int w = 0; w < nd.n_window; ++w) {
+            const qeh_window_expr &we = nd.window[w];
+            if (we.func != QEH_WIN_ROW_NUMBER)
+                return fail(QEH_E_UNSUPPORTED, "only ROW_NUMBER() runs on the device");
+            std::vector<Col> pk, okc;
+            for (int i = 0; i < we.n_partition; ++i) {
+                Col c;
+                QEH_TRY(eval(in, we.partition_by[i], &c));
+                pk.push_back(c);
+            }
+            for (int i = 0; i < we.n_order; ++i) {
+                Col c;
+                QEH_TRY(eval(in, we.order_by[i], &c));
+                okc.push_back(c);
+            }
+            std::vector<qeh_column> pc, oc;
+            for (auto &c : pk) pc.push_back(c.c);
+            for (auto &c : okc) oc.push_back(c.c);
+            std::vector<int8_t> asc(std::max(we.n_order, 1), 1);
+            qeh_column rn{};
+            if (pc.empty() && oc.empty()) {
+                // ROW_NUMBER() OVER (): 1..n in input order
+                qeh_column iota{};
+                QEH_TRY(alloc_column(ctx_, QEH_DT_INT64, in.rows, false, &iota));
+                std::vector<int64_t> h((size_t)in.rows);
+                for (int64_t i = 0; i < in.rows; ++i) h[(size_t)i] = i + 1;
+                QEH_HIP(hipMemcpyAsync(iota.values, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx_->stream));
+                QEH_HIP(hipStreamSynchronize(ctx_->stream));
+                rn = iota;
+            } else {
+                QEH_TRY(qeh_row_number(ctx_, pc.data(), (int)pc.size(), oc.data(), (int)oc.size(), asc.data(), &rn));
+            }
+            const size_t idx = out->cols.size();
+            std::string name = (nd.field_names && (int)idx < nd.n_fields && nd.field_names[idx]) ? nd.field_names[idx]
+                                                                                                : "row_number";
+            out->fields.push_back({name, QEH_DT_INT64, true});  // planner.rs:767-770 types it Int64
+            out->cols.push_back(own(ctx_, rn));
+        }
+        return QEH_OK;
+    }
+};
+
+}  // namespace
+
+extern "C" int qeh_execute_plan(qeh_ctx *ctx, const qeh_plan *plan, const qeh_source *sources, int n_sources,
+                                ArrowSchema *out_schema, ArrowArray *out_batch, int64_t *out_n_batches) {
+    if (!ctx || !plan || !out_n_batches || !out_schema || !out_batch)
+        return fail(QEH_E_INVALID, "qeh_execute_plan: bad argument");
+    *out_n_batches = 0;
+    DeviceGuard dg(ctx->device);
+    Executor ex(ctx, plan, sources, n_sources);
+    Table t;
+    QEH_TRY(ex.run(plan->root, &t));
+    if (t.batches == 0) return QEH_OK;
+    QEH_TRY(export_table(ctx, t, out_schema, out_batch));
+    *out_n_batches = 1;
+    return QEH_OK;
+}

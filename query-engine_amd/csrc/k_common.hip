@@ -1,4 +1,5 @@
 // Shared kernels and host helpers: column views, device-wide scan, gather.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -198,9 +199,86 @@ __global__ void k_gather_bool(ColRef src, const uint32_t *__restrict__ idx, int6
     }
 }
 
+// ---- Utf8 gather: lengths -> scan -> offsets -> byte copy --------------------------
+__global__ void k_utf8_lengths(const int32_t *__restrict__ offs, int64_t off0, const uint32_t *__restrict__ idx, int64_t m,
+                               uint32_t *__restrict__ len) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = off0 + idx[i];
+        len[i] = (uint32_t)(offs[r + 1] - offs[r]);
+    }
+}
+
+__global__ void k_utf8_offsets(const uint64_t *__restrict__ excl, int64_t m, uint64_t total, int32_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= m; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (int32_t)(i < m ? excl[i] : total);
+}
+
+// one wave per row: lanes copy the row's bytes
+__global__ void k_utf8_copy(const int32_t *__restrict__ offs, int64_t off0, const uint8_t *__restrict__ data,
+                            const uint32_t *__restrict__ idx, int64_t m, const int32_t *__restrict__ out_offs,
+                            uint8_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < m; w += nw) {
+        const int64_t r = off0 + idx[w];
+        const int32_t s = offs[r], e = offs[r + 1], d = out_offs[w];
+        for (int32_t b = lane; b < e - s; b += 64) out[d + b] = data[s + b];
+    }
+}
+
+static int gather_utf8(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out) {
+    std::memset(out, 0, sizeof(*out));
+    out->dtype = QEH_DT_UTF8;
+    out->owned = 1;
+    out->length = m;
+    DevBuf len, excl;
+    QEH_TRY(len.alloc(ctx, (size_t)std::max<int64_t>(m, 1) * 4));
+    QEH_TRY(excl.alloc(ctx, (size_t)std::max<int64_t>(m, 1) * 8));
+    const int grid = grid_for(ctx, m + 1, kBlock * 4, 8);
+    if (m > 0)
+        hipLaunchKernelGGL(k_utf8_lengths, dim3(grid), dim3(kBlock), 0, ctx->stream, src.offsets, src.offset, idx, m,
+                           len.as<uint32_t>());
+    uint64_t total = 0;
+    QEH_TRY(exclusive_scan_u32(ctx, len.as<uint32_t>(), excl.as<uint64_t>(), m, &total));
+    if (total > 0x7FFFFFFFull) return fail(QEH_E_UNSUPPORTED, "Utf8 output larger than 2 GiB (Arrow Utf8 uses int32 offsets)");
+    void *o = nullptr, *d = nullptr;
+    QEH_TRY(ctx->pool->alloc((size_t)(m + 1) * 4, &o));
+    int s = ctx->pool->alloc(std::max<size_t>(total, 8), &d);
+    if (s != QEH_OK) {
+        ctx->pool->free(o);
+        return s;
+    }
+    out->offsets = (int32_t *)o;
+    out->values = d;
+    out->values_bytes = (int64_t)total;
+    hipLaunchKernelGGL(k_utf8_offsets, dim3(grid), dim3(kBlock), 0, ctx->stream, excl.as<uint64_t>(), m, total, out->offsets);
+    if (m > 0)
+        hipLaunchKernelGGL(k_utf8_copy, dim3(grid_for(ctx, m, kBlock / 64, 8)), dim3(kBlock), 0, ctx->stream, src.offsets,
+                           src.offset, (const uint8_t *)src.values, idx, m, out->offsets, (uint8_t *)out->values);
+    if (src.validity) {
+        void *v = nullptr;
+        const size_t vb = std::max<size_t>(((size_t)(m + 63) / 64) * 8, 8);
+        QEH_TRY(ctx->pool->alloc(vb, &v));
+        out->validity = (uint8_t *)v;
+        out->null_count = -1;
+        ColRef sr = make_colref(src);
+        sr.dtype = QEH_DT_BOOL;  // only validity is read (values pointer unused for bits)
+        sr.values = src.validity;
+        // reuse the boolean gather: values = validity bits, validity = none
+        ColRef vr = sr;
+        vr.validity = nullptr;
+        hipLaunchKernelGGL(k_gather_bool, dim3(grid_for(ctx, (m + 63) / 64, kBlock / 64, 8)), dim3(kBlock), 0, ctx->stream,
+                           vr, idx, m, (uint64_t *)out->validity, (uint64_t *)nullptr);
+    } else {
+        out->null_count = 0;
+    }
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
 int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out) {
     QEH_TRY(check_column(src, "gather"));
-    if (src.dtype == QEH_DT_UTF8) return fail(QEH_E_UNSUPPORTED, "gather of Utf8 columns is not implemented on the device");
+    if (src.dtype == QEH_DT_UTF8) return gather_utf8(ctx, src, idx, m, out);
     bool with_valid = src.validity != nullptr;
     QEH_TRY(alloc_column(ctx, src.dtype, m, with_valid, out));
     if (m == 0) return QEH_OK;

@@ -212,11 +212,15 @@ __global__ __launch_bounds__(kBlock) void k_eval(ColSet cols, int64_t n, DevProg
 
 using namespace qeh;
 
+__global__ void k_iota_u32(uint32_t *out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)i;
+}
+
 extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
                           const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows) {
     if (!ctx || !out_rows || (n_out > 0 && (!out || !out_idx))) return fail(QEH_E_INVALID, "qeh_filter: bad argument");
     *out_rows = 0;
-    if (n_out > kMaxCols) return fail(QEH_E_UNSUPPORTED, "too many output columns for one filter (max 12)");
     DeviceGuard dg(ctx->device);
     ColSet cs;
     QEH_TRY(make_colset(cols, n_cols, &cs));
@@ -230,30 +234,36 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     if (prog.result_type != QEH_DT_BOOL) return fail(QEH_E_TYPE, "Filter predicate must return boolean");
     PredTerms terms{};
     const bool fast = lower_to_terms(predicate, dts.data(), n_cols, &terms);
+    for (int j = 0; j < n_out; ++j)
+        if (out_idx[j] < 0 || out_idx[j] >= n_cols) return fail(QEH_E_INVALID, "filter output column index out of range");
+    // fixed-width outputs are compacted by the kernel; Utf8 outputs are
+    // gathered afterwards through the selected-row ids (an extra UINT32 output)
+    std::vector<int> fixed, utf8;
+    for (int j = 0; j < n_out; ++j) (cols[out_idx[j]].dtype == QEH_DT_UTF8 ? utf8 : fixed).push_back(j);
+    const int n_kernel_out = (int)fixed.size() + (utf8.empty() ? 0 : 1);
+    if (n_kernel_out > kMaxCols) return fail(QEH_E_UNSUPPORTED, "too many output columns for one filter (max 12)");
+    std::vector<char> made(n_out, 0);
+    auto cleanup = [&]() {
+        for (int j = 0; j < n_out; ++j)
+            if (made[j]) qeh_column_release(ctx, &out[j]);
+    };
     OutSpecs os{};
-    os.n = n_out;
-    int made = 0;
-    for (int j = 0; j < n_out; ++j) {
-        if (out_idx[j] < 0 || out_idx[j] >= n_cols) {
-            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
-            return fail(QEH_E_INVALID, "filter output column index out of range");
-        }
+    os.n = n_kernel_out;
+    DevBuf iota, rowids;
+    for (size_t q = 0; q < fixed.size(); ++q) {
+        const int j = fixed[q];
         const qeh_column &src = cols[out_idx[j]];
-        if (src.dtype == QEH_DT_UTF8) {
-            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
-            return fail(QEH_E_UNSUPPORTED, "Utf8 filter outputs are not compacted on the device");
-        }
         int s = alloc_column(ctx, src.dtype, n, src.validity != nullptr, &out[j]);
         if (s != QEH_OK) {
-            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            cleanup();
             return s;
         }
-        ++made;
+        made[j] = 1;
         const size_t words = ((size_t)(n + 63) / 64) * 8;
         if (src.validity) QEH_HIP(hipMemsetAsync(out[j].validity, 0, words ? words : 8, ctx->stream));
         if (src.dtype == QEH_DT_BOOL) QEH_HIP(hipMemsetAsync(out[j].values, 0, words ? words : 8, ctx->stream));
         const ColRef cr = make_colref(src);
-        OutSpec &o = os.o[j];
+        OutSpec &o = os.o[q];
         o.src_values = cr.values;
         o.src_valid = cr.validity;
         o.src_vbit0 = cr.vbit0;
@@ -261,12 +271,31 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
         o.dst_values = out[j].values;
         o.dst_valid = (uint32_t *)out[j].validity;
     }
+    if (!utf8.empty()) {
+        int s = iota.alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4);
+        if (s == QEH_OK) s = rowids.alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4);
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
+        if (n > 0)
+            hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                               iota.as<uint32_t>(), n);
+        OutSpec &o = os.o[fixed.size()];
+        o.src_values = iota.p;
+        o.dtype = QEH_DT_UINT32;
+        o.dst_values = rowids.p;
+    }
     const int64_t n_tiles = (n + kFTile - 1) / kFTile;
     uint64_t total = 0;
     if (n_tiles > 0) {
         void *scr = nullptr;
         const size_t hdr = 64;
-        QEH_TRY(scratch_zeroed(ctx, hdr + (size_t)n_tiles * 8, &scr));
+        int s = scratch_zeroed(ctx, hdr + (size_t)n_tiles * 8, &scr);
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
         unsigned long long *ticket = (unsigned long long *)scr;
         uint32_t *err = (uint32_t *)((char *)scr + 8);
         uint64_t *tot = (uint64_t *)((char *)scr + 16);
@@ -283,17 +312,26 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
         }
         QEH_HIP(hipGetLastError());
         uint64_t hdrv[3];
-        int s = read_small(ctx, hdrv, scr, 24);
+        s = read_small(ctx, hdrv, scr, 24);
         if (s == QEH_OK) s = kernel_error_status((uint32_t)hdrv[1], "filter");
         if (s != QEH_OK) {
-            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out[i]);
+            cleanup();
             return s;
         }
         total = hdrv[2];
     }
+    for (int j : utf8) {
+        int s = gather_column(ctx, cols[out_idx[j]], rowids.as<uint32_t>(), (int64_t)total, &out[j]);
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
+        made[j] = 1;
+    }
+    if (!utf8.empty()) QEH_HIP(hipStreamSynchronize(ctx->stream));
     for (int j = 0; j < n_out; ++j) {
         out[j].length = (int64_t)total;
-        out[j].null_count = out[j].validity ? -1 : 0;
+        if (out[j].dtype != QEH_DT_UTF8) out[j].null_count = out[j].validity ? -1 : 0;
     }
     *out_rows = (int64_t)total;
     return QEH_OK;

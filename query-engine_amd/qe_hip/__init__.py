@@ -8,3 +8,6 @@ from .abi import QehError, load  # noqa: F401
 from .device import Context, DeviceColumn, agg  # noqa: F401
 from .expr import (AggregateExpr, AggregateFunction, BinaryExpr, BinaryOp, Column,  # noqa: F401
                    Literal, PhysicalExpr, ScalarValue, UnaryExpr, UnaryOp, binop, col, lit)
+from .plan import (DataSource, Filter, HashAggregate, HashJoin, IndexScan, JoinType, Limit,  # noqa: F401
+                   MemoryDataSource, Projection, QueryExecutor, Scan, Sort, SubqueryScan, Window, WindowExpr,
+                   WindowFunctionType)

@@ -78,6 +78,16 @@ class DeviceColumn:
             valid = unpack_bits(vb, n, off)
         elif self.c.validity:
             valid = np.zeros(0, bool)
+        if self.c.dtype == abi.DT_UTF8:
+            offs = np.empty(n + 1, np.int32)
+            ctx.d2h(offs, self.c.offsets + 4 * off, 4 * (n + 1))
+            nb = int(offs[-1]) if n else 0
+            data = np.empty(max(nb, 1), np.uint8)
+            if nb:
+                ctx.d2h(data, self.c.values, nb)
+            raw = data.tobytes()
+            out = np.array([raw[offs[i]:offs[i + 1]].decode() for i in range(n)], dtype=object)
+            return out, valid
         if self.c.dtype == abi.DT_BOOL:
             nbytes = (off + n + 7) // 8
             vb = np.empty(max(nbytes, 1), np.uint8)
@@ -149,6 +159,8 @@ class Context:
         """numpy -> Arrow-layout device column.  `offset` prepends that many
         padding rows and records them as the Arrow array offset (exercises
         non-zero offsets)."""
+        if isinstance(values, (list, tuple)) or (isinstance(values, np.ndarray) and values.dtype == object):
+            return self._upload_utf8(list(values), valid)
         values = np.asarray(values)
         dt = DT_OF.get(values.dtype)
         if dt is None:
@@ -173,6 +185,28 @@ class Context:
             self.h2d(q, vb)
             c.validity = q
             c.null_count = int(n - valid.sum())
+        return DeviceColumn(self, c, bufs)
+
+    def _upload_utf8(self, strs, valid=None) -> DeviceColumn:
+        n = len(strs)
+        if valid is None:
+            valid = np.array([x is not None for x in strs], bool)
+        enc = [(x or "").encode() if v else b"" for x, v in zip(strs, valid)]
+        offs = np.zeros(n + 1, np.int32)
+        offs[1:] = np.cumsum([len(b) for b in enc]) if n else []
+        data = np.frombuffer(b"".join(enc), np.uint8) if offs[-1] else np.zeros(8, np.uint8)
+        po, pd = self.alloc(offs.nbytes), self.alloc(max(data.nbytes, 8))
+        self.h2d(po, offs)
+        self.h2d(pd, data)
+        c = abi.QehColumn(dtype=abi.DT_UTF8, owned=0, length=n, offset=0, null_count=int(n - valid.sum()),
+                          values=pd, offsets=po, values_bytes=int(offs[-1]))
+        bufs = [po, pd]
+        if not valid.all():
+            vb = pack_bits(valid)
+            q = self.alloc(vb.nbytes)
+            self.h2d(q, vb)
+            c.validity = q
+            bufs.append(q)
         return DeviceColumn(self, c, bufs)
 
     def empty(self, dtype: int, n: int) -> DeviceColumn:

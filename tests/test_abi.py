@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    src = open(os.path.join(ROOT, "include", "qeh.h")).read()
+    src = open(os.path.join(ROOT, "include", "qeh.h")).read() + open(os.path.join(ROOT, "include", "qeh_plan.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:int|const char \*|void \*)\s*(qeh_\w+)\s*\(", src, flags=re.M)))
 
@@ -23,7 +23,7 @@ def test_header_declares_the_operator_surface():
     names = declared_functions()
     for required in ["qeh_init", "qeh_filter", "qeh_eval", "qeh_hash_aggregate", "qeh_filter_aggregate",
                      "qeh_hash_join_inner", "qeh_join_filter_aggregate", "qeh_sort_indices", "qeh_take",
-                     "qeh_row_number", "qeh_hash_partition", "qeh_last_error"]:
+                     "qeh_row_number", "qeh_hash_partition", "qeh_last_error", "qeh_execute_plan"]:
         assert required in names
 
 

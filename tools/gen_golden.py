@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/* fixtures (run in the build container only).
+
+The reference (Rust + arrow-rs 53.4.1) cannot be built here, so golden outputs
+for the arrow kernels the reference calls come from Arrow C++ (pyarrow 25),
+which implements the same Arrow semantics for these kernels:
+  cmp::{eq,neq,lt,lt_eq,gt,gt_eq}  -> pc.equal/.../greater_equal (null-propagating)
+  compute::{and,or,not}            -> pc.and_/pc.or_/pc.invert   (non-Kleene)
+  numeric::{add,sub,mul,div} ints  -> pc.add_checked/subtract_checked/multiply_checked/divide_checked
+  filter_record_batch              -> pc.filter(null_selection_behavior="drop")
+  compute::{sum,min,max}, count    -> pc.sum/min/max/count (non-overflowing data: pyarrow
+                                      widens Int32 sums, arrow-rs wraps them)
+Intended-semantics operators are pinned the same way:
+  GROUP BY -> Table.group_by().aggregate();  INNER JOIN -> Table.join("inner");
+  Sort     -> pc.sort_indices(null_placement="at_start") (stable);
+  ROW_NUMBER -> numpy lexsort (no Arrow kernel; documented as numpy-pinned).
+Config 1's known answer comes from the reference's own data/employees.csv
+(SURVEY.md §8 row c), copied here as a data fixture.
+Every fixture is an .npz written with allow_pickle=False.
+"""
+import json
+import os
+import shutil
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import pyarrow.csv as pacsv
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden")
+N = 4096
+
+
+def col_arrays(arr: pa.Array):
+    """values (nulls filled with 0) + validity."""
+    valid = ~np.asarray(arr.is_null().to_numpy(zero_copy_only=False), bool)
+    t = arr.type
+    if pa.types.is_boolean(t):
+        vals = np.asarray(arr.fill_null(False).to_numpy(zero_copy_only=False), bool)
+    else:
+        vals = np.asarray(arr.fill_null(0).to_numpy(zero_copy_only=False))
+    return vals, valid
+
+
+def base_table(seed=20251226):
+    r = np.random.default_rng(seed)
+    def nulls(p):
+        return r.random(N) < p
+    x = pa.array(r.integers(0, 100, N), pa.int64(), mask=nulls(0.1))
+    i = pa.array(r.integers(-1000, 1000, N).astype(np.int32), pa.int32(), mask=nulls(0.15))
+    v = pa.array(np.round(r.random(N), 6), pa.float64(), mask=nulls(0.12))
+    f = pa.array(r.random(N).astype(np.float32), pa.float32(), mask=nulls(0.05))
+    b = pa.array(r.random(N) > 0.5, pa.bool_(), mask=nulls(0.1))
+    k = pa.array(r.integers(0, 37, N), pa.int64(), mask=nulls(0.05))
+    return pa.table({"x": x, "i": i, "v": v, "f": f, "b": b, "k": k})
+
+
+def save(name, **arrays):
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
+
+
+def put_table(prefix, t: pa.Table, d: dict):
+    for name in t.column_names:
+        vals, valid = col_arrays(t.column(name).combine_chunks())
+        d[f"{prefix}{name}"] = vals
+        d[f"{prefix}{name}__valid"] = valid
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    manifest = {"generator": "tools/gen_golden.py", "pyarrow": pa.__version__, "fixtures": {}}
+    t = base_table()
+
+    # ---- filter predicates (expression encodings are rebuilt by the tests from these names)
+    preds = {
+        "x_gt_49": pc.greater(t["x"], 49),
+        "v_le_half": pc.less_equal(t["v"], 0.5),
+        "i_lt_f64": pc.less(pc.cast(t["i"], pa.float64()), 12.5),
+        "f_ge_v": pc.greater_equal(pc.cast(t["f"], pa.float64()), t["v"]),
+        "and_or": pc.or_(pc.and_(pc.greater(t["x"], 20), pc.less(t["v"], 0.5)), pc.equal(t["i"], 7)),
+        "not_b": pc.invert(t["b"]),
+        "x_plus_x_gt_50": pc.greater(pc.add_checked(t["x"], t["x"]), 50),
+        "x_times_3_ne_i": pc.not_equal(pc.multiply_checked(t["x"], 3), pc.cast(t["i"], pa.int64())),
+    }
+    d = {}
+    put_table("in_", t, d)
+    for name, mask in preds.items():
+        ft = t.filter(mask, null_selection_behavior="drop")
+        put_table(f"{name}__", ft, d)
+        d[f"{name}__rows"] = np.array([ft.num_rows])
+    save("filter", **d)
+    manifest["fixtures"]["filter"] = {"rows": N, "predicates": list(preds)}
+
+    # ---- global aggregates (evaluate_aggregate): non-overflowing data
+    d = {}
+    put_table("in_", t, d)
+    for c in ["x", "v", "f", "i"]:
+        a = t[c]
+        d[f"{c}__count"] = np.array([pc.count(a).as_py()])
+        d[f"{c}__sum"] = np.array([pc.sum(a).as_py()], dtype=np.float64 if c in ("v", "f") else np.int64)
+        d[f"{c}__avg"] = np.array([pc.mean(a).as_py()])
+        d[f"{c}__min"] = np.array([pc.min(a).as_py()])
+        d[f"{c}__max"] = np.array([pc.max(a).as_py()])
+    save("global_agg", **d)
+    manifest["fixtures"]["global_agg"] = {"columns": ["x", "v", "f", "i"]}
+
+    # ---- grouped aggregate (intended semantics)
+    g = t.group_by(["k"], use_threads=False).aggregate(
+        [("v", "sum"), ("v", "count"), ("v", "mean"), ("x", "min"), ("x", "max"), ("x", "sum")])
+    d = {}
+    put_table("in_", t, d)
+    put_table("out_", g, d)
+    save("group_agg", **d)
+    manifest["fixtures"]["group_agg"] = {"groups": g.num_rows, "columns": g.column_names}
+
+    # ---- inner join (intended semantics)
+    r = np.random.default_rng(7)
+    left = pa.table({"lk": pa.array(r.integers(0, 300, 3000), pa.int64(), mask=r.random(3000) < 0.05),
+                     "lv": pa.array(r.random(3000))})
+    right = pa.table({"rk": pa.array(r.integers(0, 250, 400), pa.int64(), mask=r.random(400) < 0.05),
+                      "ra": pa.array(r.integers(-9, 9, 400), pa.int64())})
+    j = left.join(right, keys="lk", right_keys="rk", join_type="inner", use_threads=False)
+    j = j.select(["lk", "lv", "ra"])
+    d = {}
+    put_table("left_", left, d)
+    put_table("right_", right, d)
+    put_table("out_", j, d)
+    save("join", **d)
+    manifest["fixtures"]["join"] = {"rows": j.num_rows}
+
+    # ---- stable multi-key sort, nulls first
+    keys = [("k", "ascending"), ("v", "descending"), ("x", "ascending")]
+    idx = pc.sort_indices(t, sort_keys=keys, null_placement="at_start")
+    d = {}
+    put_table("in_", t, d)
+    d["perm"] = np.asarray(idx.to_numpy(), np.uint32)
+    save("sort", **d)
+    manifest["fixtures"]["sort"] = {"keys": keys}
+
+    # ---- ROW_NUMBER() OVER (PARTITION BY k ORDER BY x) (numpy-pinned)
+    kk, kv = col_arrays(t["k"].combine_chunks())
+    xx, xv = col_arrays(t["x"].combine_chunks())
+    # lexsort: last key primary. nulls first -> sort by valid flag before value
+    order = np.lexsort((np.arange(N), xx, xv, kk, kv))
+    rn = np.zeros(N, np.int64)
+    prev = None
+    cnt = 0
+    for pos in order:
+        key = (bool(kv[pos]), int(kk[pos]) if kv[pos] else 0)
+        cnt = cnt + 1 if key == prev else 1
+        prev = key
+        rn[pos] = cnt
+    d = {}
+    put_table("in_", t, d)
+    d["rn"] = rn
+    save("row_number", **d)
+    manifest["fixtures"]["row_number"] = {"partition_by": "k", "order_by": "x"}
+
+    # ---- config 1: the reference's data/employees.csv and its known answer
+    src = "/root/reference/data/employees.csv"
+    dst = os.path.join(OUT, "employees.csv")
+    if os.path.exists(src):
+        shutil.copyfile(src, dst)
+    emp = pacsv.read_csv(dst)
+    ans = emp.filter(pc.greater(emp["age"], 25)).select(["name", "age"])
+    manifest["fixtures"]["employees"] = {
+        "query": "SELECT name,age FROM employees WHERE age>25",
+        "schema": ["employees.name: Utf8", "employees.age: Int64"],
+        "rows": [[n, a] for n, a in zip(ans["name"].to_pylist(), ans["age"].to_pylist())],
+    }
+    json.dump(manifest, open(os.path.join(OUT, "manifest.json"), "w"), indent=1)
+    print(json.dumps(manifest["fixtures"]["employees"]))
+
+
+if __name__ == "__main__":
+    main()
