@@ -107,30 +107,17 @@ def main():
     pred = binop(col(0, "f.x"), BinaryOp.Greater, lit(args.threshold))
     aggs = [(AF.Sum, 2), (AF.Count, 2)]
 
+    dx = None
+    if dist:
+        from qe_hip.distributed import DistributedExecutor
+        dx = DistributedExecutor(ctx)
+
     def step():
-        gk, ga, g = ctx.join_filter_aggregate([x, k, v], 1, pred, dk, [dg], aggs)
         if not dist:
-            return gk, ga, g
-        # partial -> final: all-gather the partial (g, sum, count) rows (padded
-        # to the largest rank's group count) and merge them with a device
-        # HashAggregate(SUM, SUM) filtered on count > 0 (drops the padding).
-        gmax = torch.tensor([g], device="cuda", dtype=torch.int64)
-        tdist.all_reduce(gmax, op=tdist.ReduceOp.MAX)
-        m = int(gmax.item())
-        part = torch.zeros((3, m), device="cuda", dtype=torch.int64)
-        for i, c in enumerate([gk[0], ga[0], ga[1]]):
-            if g:
-                ctx.copy_d2d(part[i].data_ptr(), c.c.values, 8 * g)
-        allp = torch.empty((world, 3, m), device="cuda", dtype=torch.int64)
-        tdist.all_gather_into_tensor(allp, part)
-        allp = allp.permute(1, 0, 2).contiguous().view(3, world * m)
-        cols = [ctx.wrap_device(abi.DT_INT64, allp[0].data_ptr(), world * m),
-                ctx.wrap_device(abi.DT_FLOAT64, allp[1].data_ptr(), world * m),
-                ctx.wrap_device(abi.DT_INT64, allp[2].data_ptr(), world * m)]
-        fk, fa, fg = ctx.filter_aggregate(cols, binop(col(2), BinaryOp.Greater, lit(0)), [0],
-                                          [(AF.Sum, 1), (AF.Sum, 2)])
-        keep = (allp,)
-        return fk, fa, fg
+            return ctx.join_filter_aggregate([x, k, v], 1, pred, dk, [dg], aggs)
+        # broadcast join (dim replicated), partial states shuffled by group key
+        # over RCCL all-to-all, final aggregate on the owning rank
+        return dx.join_filter_aggregate_broadcast([x, k, v], 1, pred, dk, [dg], aggs)
 
     for _ in range(args.warmup):
         step()
@@ -161,6 +148,12 @@ def main():
     # sanity on the result: every selected row landed in exactly one group
     gk, ga, g = res
     counts, _ = ga[1].to_numpy()
+    counted = int(counts.sum())
+    groups = int(g)
+    if dist:
+        t = torch.tensor([counted, groups], device="cuda", dtype=torch.int64)
+        tdist.all_reduce(t)
+        counted, groups = int(t[0].item()), int(t[1].item())
     total_rows = n * world
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_rows * args.steps / elapsed
@@ -198,7 +191,7 @@ def main():
                 "dim_rows": nd,
                 "groups": args.groups,
                 "parallelism": f"fact sharded x{world}, dim replicated (broadcast join)"
-                               + (", RCCL partial->final aggregate" if dist else ""),
+                               + (", partial states shuffled by RCCL all-to-all, final aggregate per owner rank" if dist else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -212,8 +205,8 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "build_ms_per_step": build_ms / args.steps,
-            "result_groups": int(g),
-            "result_rows_counted": int(counts.sum()),
+            "result_groups": groups,
+            "result_rows_counted": counted,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -257,6 +257,12 @@ int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_part,
 int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
                        qeh_column *out_perm);
 
+/* Validity bitmap <-> one byte per row (1 = valid), for moving nullable
+ * columns through byte-addressed collectives (RCCL all-to-all splits are
+ * row counts, not bit offsets).  Buffers are device pointers. */
+int qeh_validity_to_bytes(qeh_ctx *ctx, const qeh_column *col, uint8_t *out_bytes);
+int qeh_bytes_to_validity(qeh_ctx *ctx, const uint8_t *bytes, int64_t n, uint8_t *out_bitmap);
+
 #ifdef __cplusplus
 }
 #endif

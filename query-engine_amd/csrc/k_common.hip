@@ -304,3 +304,42 @@ int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int6
 }
 
 }  // namespace qeh
+
+namespace qeh {
+__global__ void k_valid_bytes(ColRef c, int64_t n, uint8_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = col_valid(c, i) ? 1 : 0;
+}
+
+__global__ void k_bytes_valid(const uint8_t *__restrict__ in, int64_t n, uint64_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w * 64 < n; w += nw) {
+        const int64_t i = w * 64 + lane;
+        const uint64_t b = __ballot(i < n && in[i] != 0);
+        if (lane == 0) out[w] = b;
+    }
+}
+}  // namespace qeh
+
+extern "C" int qeh_validity_to_bytes(qeh_ctx *ctx, const qeh_column *col, uint8_t *out_bytes) {
+    using namespace qeh;
+    if (!ctx || !col || (col->length > 0 && !out_bytes)) return fail(QEH_E_INVALID, "qeh_validity_to_bytes: bad argument");
+    DeviceGuard dg(ctx->device);
+    if (col->length == 0) return QEH_OK;
+    hipLaunchKernelGGL(k_valid_bytes, dim3(grid_for(ctx, col->length, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                       make_colref(*col), col->length, out_bytes);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+extern "C" int qeh_bytes_to_validity(qeh_ctx *ctx, const uint8_t *bytes, int64_t n, uint8_t *out_bitmap) {
+    using namespace qeh;
+    if (!ctx || (n > 0 && (!bytes || !out_bitmap))) return fail(QEH_E_INVALID, "qeh_bytes_to_validity: bad argument");
+    DeviceGuard dg(ctx->device);
+    if (n == 0) return QEH_OK;
+    hipLaunchKernelGGL(k_bytes_valid, dim3(grid_for(ctx, (n + 63) / 64, kBlock / 64, 8)), dim3(kBlock), 0, ctx->stream,
+                       bytes, n, (uint64_t *)out_bitmap);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}

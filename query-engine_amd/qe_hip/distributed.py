@@ -1,0 +1,182 @@
+"""Multi-GPU execution: one process per GPU, torch.distributed over RCCL/xGMI.
+
+Reference model (SURVEY.md §8 row e): the reference only simulates
+distribution — hash partitioning (crates/query-distributed/src/partition.rs:151-212),
+Exchange (operators.rs:15-73) and partial/final aggregate and shuffle-join stage
+shapes (planner.rs:200-249) — and never executes workers.  Here the same
+stages run for real:
+
+  * shuffle(key, cols): device hash partition (qeh_hash_partition) -> device
+    gather into partition-major order -> ONE all_to_all per column over RCCL
+    (counts first, so every rank knows its receive splits).
+  * hash_join_inner: shuffle both sides by the join key, local device join.
+  * group_by: local partial aggregate -> shuffle partial states by the first
+    group key -> final aggregate on the owning rank (partial/final stages).
+  * join_filter_aggregate_broadcast (the BASELINE metric path): the dimension
+    is replicated (broadcast join), every rank runs the fused kernel on its
+    fact shard, then the partial states are shuffled by group key and merged.
+
+The collectives carry device tensors under the "nccl" backend (RCCL on ROCm)
+and host tensors under "gloo" (CPU rehearsal of the same code path).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import abi
+from .device import NP_OF, Context, DeviceColumn
+from .expr import AggregateFunction as AF
+
+TORCH_OF = {abi.DT_INT64: torch.int64, abi.DT_FLOAT64: torch.float64, abi.DT_INT32: torch.int32,
+            abi.DT_FLOAT32: torch.float32, abi.DT_UINT32: torch.int32}
+
+
+def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=None
+             ) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """All-to-all of partition-major payloads.  send_counts[r] rows of every
+    payload go to rank r.  Returns (recv_counts, received payloads)."""
+    world = dist.get_world_size(group)
+    send_counts = send_counts.to(torch.int64)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    ins = [int(x) for x in send_counts.tolist()]
+    outs = [int(x) for x in recv_counts.tolist()]
+    assert len(ins) == world
+    received = []
+    for p in payloads:
+        out = torch.empty((sum(outs),) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
+        dist.all_to_all_single(out, p.contiguous(), output_split_sizes=outs, input_split_sizes=ins, group=group)
+        received.append(out)
+    return recv_counts, received
+
+
+# partial -> final aggregate decomposition (distributed/planner.rs:200-249 stage shape)
+FINAL_OF = {AF.Count: AF.Sum, AF.Sum: AF.Sum, AF.Min: AF.Min, AF.Max: AF.Max}
+
+
+class DistributedExecutor:
+    def __init__(self, ctx: Context, group=None):
+        self.ctx = ctx
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        self._keep: list = []  # tensors backing wrapped columns
+
+    # ---- column <-> tensor ------------------------------------------------------
+    def _to_tensors(self, col: DeviceColumn) -> List[torch.Tensor]:
+        n = len(col)
+        if col.dtype == abi.DT_UTF8 or col.dtype == abi.DT_BOOL:
+            raise NotImplementedError("Utf8/Boolean columns are not exchanged between GPUs yet")
+        tdt = TORCH_OF[col.dtype]
+        if self.device == "cuda":
+            vals = torch.empty(n, dtype=tdt, device="cuda")
+            if n:
+                item = vals.element_size()
+                self.ctx.copy_d2d(vals.data_ptr(), col.c.values + col.c.offset * item, n * item)
+            out = [vals]
+            if col.c.validity:
+                vb = torch.empty(n, dtype=torch.uint8, device="cuda")
+                abi.check(self.ctx.lib.qeh_validity_to_bytes(self.ctx.h, col.c, vb.data_ptr()))
+                out.append(vb)
+            return out
+        v, m = col.to_numpy()
+        out = [torch.from_numpy(np.ascontiguousarray(v))]
+        if col.c.validity:
+            out.append(torch.from_numpy(m.astype(np.uint8)))
+        return out
+
+    def _from_tensors(self, dtype: int, vals: torch.Tensor, valid: Optional[torch.Tensor]) -> DeviceColumn:
+        n = vals.shape[0]
+        if self.device == "cuda":
+            bitmap = 0
+            if valid is not None:
+                bm = torch.zeros(((n + 63) // 64) * 8 + 8, dtype=torch.uint8, device="cuda")
+                abi.check(self.ctx.lib.qeh_bytes_to_validity(self.ctx.h, valid.data_ptr(), n, bm.data_ptr()))
+                self._keep.append(bm)
+                bitmap = bm.data_ptr()
+            self._keep.append(vals)
+            return self.ctx.wrap_device(dtype, vals.data_ptr(), n, bitmap)
+        v = vals.numpy().astype(NP_OF[dtype], copy=False)
+        m = None if valid is None else valid.numpy().astype(bool)
+        return self.ctx.upload(v, m)
+
+    def _sync(self):
+        if self.device == "cuda":
+            self.ctx.sync()
+
+    # ---- shuffle -----------------------------------------------------------------
+    def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
+        """Route every row to rank hash(key) % world (partition.rs:151-212)."""
+        counts, perm = self.ctx.hash_partition(key, self.world)
+        taken = [self.ctx.take(c, perm) for c in cols]
+        payloads, shape = [], []
+        for t in taken:
+            ts = self._to_tensors(t)
+            shape.append((t.dtype, len(ts) == 2))
+            payloads.extend(ts)
+        self._sync()
+        _, recv = exchange(torch.tensor(counts, dtype=torch.int64, device=self.device), payloads, self.group)
+        out, i = [], 0
+        for dtype, nullable in shape:
+            vals = recv[i]
+            valid = recv[i + 1] if nullable else None
+            i += 2 if nullable else 1
+            out.append(self._from_tensors(dtype, vals, valid))
+        return out
+
+    # ---- operators -----------------------------------------------------------------
+    def hash_join_inner(self, probe_key_idx: int, probe_cols: Sequence[DeviceColumn], build_key_idx: int,
+                        build_cols: Sequence[DeviceColumn]):
+        """Shuffle join: both sides hash-partitioned by the key, local device join."""
+        p = self.shuffle(probe_cols[probe_key_idx], probe_cols)
+        b = self.shuffle(build_cols[build_key_idx], build_cols)
+        return self.ctx.hash_join_inner(p[probe_key_idx], p, b[build_key_idx], b)
+
+    def _final(self, keys: Sequence[DeviceColumn], partials: Sequence[DeviceColumn], aggs: Sequence[Tuple[int, int]]):
+        shuffled = self.shuffle(keys[0], list(keys) + list(partials))
+        nk = len(keys)
+        fk, fa, g = self.ctx.hash_aggregate(shuffled[:nk], shuffled[nk:],
+                                            [(FINAL_OF[f], i) for i, (f, _) in enumerate(aggs)])
+        return fk, fa, g
+
+    def group_by(self, keys: Sequence[DeviceColumn], inputs: Sequence[DeviceColumn], aggs: Sequence[Tuple[int, int]]):
+        """Partial aggregate locally, shuffle partial states by the first key,
+        final aggregate on the owning rank.  Each rank returns the groups it owns."""
+        for f, _ in aggs:
+            if f not in FINAL_OF:
+                raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        pk, pa_, g = self.ctx.hash_aggregate(keys, inputs, aggs)
+        if g == 0 and not pk:
+            pk = [self.ctx.empty(k.dtype, 0) for k in keys]
+            pa_ = [self.ctx.empty(abi.DT_INT64, 0) for _ in aggs]
+        return self._final(pk, pa_, aggs)
+
+    def join_filter_aggregate_broadcast(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
+                                        aggs):
+        """Broadcast join: `build_*` replicated on every rank, `probe_cols` = this
+        rank's shard.  Fused local pipeline, then partial/final merge."""
+        for f, _ in aggs:
+            if f not in FINAL_OF:
+                raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
+                                                    build_group_keys, aggs)
+        return self._final(pk, pa_, aggs)
+
+    def gather_to_root(self, cols: Sequence[DeviceColumn]) -> Optional[List[Tuple[np.ndarray, Optional[np.ndarray]]]]:
+        """Collect every rank's result rows on rank 0 (host arrays)."""
+        local = [c.to_numpy() for c in cols]
+        objs = [None] * self.world
+        dist.all_gather_object(objs, local, group=self.group)
+        if self.rank != 0:
+            return None
+        out = []
+        for j in range(len(cols)):
+            vals = np.concatenate([o[j][0] for o in objs])
+            masks = [o[j][1] if o[j][1] is not None else np.ones(len(o[j][0]), bool) for o in objs]
+            out.append((vals, np.concatenate(masks)))
+        return out

@@ -1,0 +1,122 @@
+"""One rank of a multi-process rehearsal of qe_hip.distributed (launched by
+tests/test_distributed.py as separate processes; RANK/WORLD_SIZE/MASTER_* in
+the environment).  mode "exchange": CPU-only gloo all-to-all of partition-major
+rows.  mode "gpu": every rank computes on cuda:0, collectives over gloo (host
+tensors) — the one-GPU rehearsal of the RCCL path."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "query-engine_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def rows_for(rank, n=5000):
+    r = np.random.default_rng(100 + rank)
+    k = r.integers(0, 997, n).astype(np.int64)
+    v = r.random(n)
+    return k, v
+
+
+def mode_exchange(rank, world):
+    from qe_hip.distributed import exchange
+    k, v = rows_for(rank)
+    part = k % world  # stand-in partition function (the device hash is tested on the GPU)
+    order = np.argsort(part, kind="stable")
+    counts = np.bincount(part, minlength=world)
+    recv_counts, (rk, rv) = exchange(torch.tensor(counts), [torch.from_numpy(k[order]), torch.from_numpy(v[order])])
+    all_k = np.concatenate([rows_for(r)[0] for r in range(world)])
+    all_v = np.concatenate([rows_for(r)[1] for r in range(world)])
+    mine = all_k % world == rank
+    assert int(recv_counts.sum()) == int(mine.sum())
+    got = sorted(zip(rk.numpy().tolist(), rv.numpy().tolist()))
+    want = sorted(zip(all_k[mine].tolist(), all_v[mine].tolist()))
+    assert got == want
+
+
+def mode_gpu(rank, world):
+    import qe_hip
+    import oracle_bind as ob
+    from helpers import assert_grouped_equal, sorted_rows
+    from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit
+    from qe_hip.distributed import DistributedExecutor
+    ctx = qe_hip.Context(0)
+    dx = DistributedExecutor(ctx)
+    # --- shuffle join: fact shard per rank x dim shard per rank
+    def fact(r):
+        g = np.random.default_rng(10 + r)
+        return g.integers(0, 3000, 40_000).astype(np.int64), g.random(40_000)
+    def dim(r):
+        keys = np.arange(r, 3000, world, dtype=np.int64)  # disjoint shards of a unique key set
+        return keys, keys * 7
+    fk, fv = fact(rank)
+    dk, da = dim(rank)
+    op, obd, rows = dx.hash_join_inner(0, [ctx.upload(fk), ctx.upload(fv)], 0, [ctx.upload(dk), ctx.upload(da)])
+    res = dx.gather_to_root(op + obd)
+    if rank == 0:
+        FK = np.concatenate([fact(r)[0] for r in range(world)])
+        FV = np.concatenate([fact(r)[1] for r in range(world)])
+        DK = np.concatenate([dim(r)[0] for r in range(world)])
+        DA = np.concatenate([dim(r)[1] for r in range(world)])
+        wp, wb, wrows = ob.hash_join_inner(ob.HostCol(FK), [ob.HostCol(FK), ob.HostCol(FV)], ob.HostCol(DK),
+                                           [ob.HostCol(DK), ob.HostCol(DA)])
+        assert sorted_rows(res) == sorted_rows(wp + wb)
+    # --- distributed group by (partial/final)
+    g = np.random.default_rng(50 + rank)
+    k = g.integers(0, 300, 30_000).astype(np.int64)
+    v = g.integers(-1000, 1000, 30_000).astype(np.int64)
+    keys, aggs_out, ng = dx.group_by([ctx.upload(k)], [ctx.upload(v)], [(AF.Sum, 0), (AF.Count, 0), (AF.Min, 0),
+                                                                        (AF.Max, 0)])
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        K = np.concatenate([np.random.default_rng(50 + r).integers(0, 300, 30_000) for r in range(world)])
+        V = np.concatenate([np.random.default_rng(50 + r).integers(-1000, 1000, 30_000) for r in range(world)])
+        # regenerate exactly as the ranks did (same two draws per rank)
+        K, V = [], []
+        for r in range(world):
+            gg = np.random.default_rng(50 + r)
+            K.append(gg.integers(0, 300, 30_000))
+            V.append(gg.integers(-1000, 1000, 30_000))
+        K, V = np.concatenate(K).astype(np.int64), np.concatenate(V).astype(np.int64)
+        wk, wa, wg, _ = ob.hash_aggregate([ob.HostCol(K)], [ob.HostCol(V)], [(AF.Sum, 0), (AF.Count, 0), (AF.Min, 0),
+                                                                               (AF.Max, 0)])
+        assert_grouped_equal(res[:1], res[1:], wk, wa)
+    # --- the BASELINE metric path: broadcast dim, sharded fact
+    n, nd = 200_000, 20_000
+    x = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 1, n, 100, row0=rank * n)
+    kk = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 2, n, nd, row0=rank * n)
+    vv = ob.generate(abi.GEN_UNIT_F64, 0x5EED, 3, n, row0=rank * n)
+    dkk = ob.generate(abi.GEN_PERMUTATION, 0x5EED, 0, nd, nd)
+    dg = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 5, nd, 256)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast([ctx.upload(x), ctx.upload(kk), ctx.upload(vv)], 1, pred,
+                                                            ctx.upload(dkk), [ctx.upload(dg)], [(AF.Sum, 2), (AF.Count, 2)])
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        X = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 1, n * world, 100)
+        KK = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 2, n * world, nd)
+        VV = ob.generate(abi.GEN_UNIT_F64, 0x5EED, 3, n * world)
+        wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred, ob.HostCol(dkk),
+                                              [ob.HostCol(dg)], [(AF.Sum, 2), (AF.Count, 2)])
+        assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    ctx.close()
+
+
+def main():
+    mode = sys.argv[1]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        {"exchange": mode_exchange, "gpu": mode_gpu}[mode](rank, world)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+    print(f"rank {rank} ok")
+
+
+if __name__ == "__main__":
+    main()
