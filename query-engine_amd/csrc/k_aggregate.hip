@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "agg.h"
 #include "expr_device.h"
@@ -265,7 +266,8 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
 // XCD's 4 MiB L2 only ever holds 1/8 of the table.  Placement only affects
 // speed: every item is processed exactly once whatever the XCD mapping.
 constexpr int kParts = 8;
-constexpr int kPartBatch = 8192;
+constexpr int kPartBatch = 16384;
+constexpr int kPartUnroll = 16;  // phase B items in flight per lane
 
 struct PartBufs {
     void *key[kParts];             // uint32 key offsets (DIRECT) or int64 keys (PACKED)
@@ -286,8 +288,12 @@ __device__ __forceinline__ uint32_t xcc_id() {
 template <int NTERMS, int NACOL, bool KEY64, bool NT>
 __global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms terms, HashTable t, int64_t n_tiles,
                                                            PartBufs pb) {
-    __shared__ uint32_t cnt[kParts];
+    typedef typename std::conditional<KEY64, int64_t, uint32_t>::type KeyT;
+    __shared__ uint32_t cnt[kParts], lofs[kParts];
+    __shared__ uint32_t s_total;
     __shared__ unsigned long long base[kParts];
+    __shared__ KeyT skey[kFastTile];
+    __shared__ int64_t sval[NACOL > 0 ? NACOL : 1][kFastTile];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         if (threadIdx.x < kParts) cnt[threadIdx.x] = 0;
@@ -341,26 +347,47 @@ __global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms 
             pos[r] = atomicAdd(&cnt[p], 1u);
         }
         __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int p = 0; p < kParts; ++p) {
+                lofs[p] = acc;
+                acc += cnt[p];
+            }
+            s_total = acc;
+        }
         if (threadIdx.x < kParts) {
             const uint32_t c = cnt[threadIdx.x];
             base[threadIdx.x] = c ? atomicAdd(&pb.cursor[threadIdx.x], (unsigned long long)c) : 0ull;
         }
         __syncthreads();
+        // stage the tile's rows in LDS grouped by partition ...
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
             if (!((sel >> r) & 1)) continue;
-            const uint32_t p = part[r];
-            const uint64_t idx = base[p] + pos[r];
-            if (idx >= pb.cap) {
+            const uint32_t s = lofs[part[r]] + pos[r];
+            const int64_t k = key[r >> 1][r & 1];
+            skey[s] = KEY64 ? (KeyT)k : (KeyT)((uint64_t)k - (uint64_t)t.kmin);
+#pragma unroll
+            for (int c = 0; c < NACOL; ++c) sval[c][s] = ac[c][r >> 1][r & 1];
+        }
+        __syncthreads();
+        // ... and copy them out: consecutive lanes write consecutive slots, so
+        // every partition's rows leave as contiguous, coalesced runs
+        const uint32_t total = s_total;
+        for (uint32_t i = threadIdx.x; i < total; i += kBlock) {
+            uint32_t p = 0;
+#pragma unroll
+            for (int q = 1; q < kParts; ++q) p += lofs[q] <= i ? 1u : 0u;  // last partition starting at or before i
+            const uint64_t dst = base[p] + (i - lofs[p]);
+            if (dst >= pb.cap) {
                 *pb.overflow = 1u;
                 continue;
             }
-            const int64_t k = key[r >> 1][r & 1];
-            if (KEY64) ((int64_t *)pb.key[p])[idx] = k;
-            else ((uint32_t *)pb.key[p])[idx] = (uint32_t)((uint64_t)k - (uint64_t)t.kmin);
+            ((KeyT *)pb.key[p])[dst] = skey[i];
 #pragma unroll
-            for (int c = 0; c < NACOL; ++c) pb.val[c][p][idx] = ac[c][r >> 1][r & 1];
+            for (int c = 0; c < NACOL; ++c) pb.val[c][p][dst] = sval[c][i];
         }
+        __syncthreads();
     }
 }
 
@@ -390,27 +417,31 @@ __global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn
             __syncthreads();
             if (b >= n_p) break;
             const uint64_t e = b + kPartBatch < n_p ? b + kPartBatch : n_p;
-            for (uint64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * kBlock) {
-                int64_t kk[4];
-                int64_t vv[NACOL > 0 ? NACOL : 1][4];
-                bool live[4];
+            constexpr int U = kPartUnroll;
+            for (uint64_t i0 = b + threadIdx.x; i0 < e; i0 += U * kBlock) {
+                int64_t kk[U];
+                int64_t vv[NACOL > 0 ? NACOL : 1][U];
+                uint32_t live = 0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < U; ++u) {
                     const uint64_t i = i0 + (uint64_t)u * kBlock;
-                    live[u] = i < e;
-                    const uint64_t ii = live[u] ? i : b;
+                    if (i < e) live |= 1u << u;
+                    const uint64_t ii = i < e ? i : b;
                     kk[u] = KEY64 ? ((const int64_t *)pb.key[p])[ii]
                                   : (int64_t)((uint64_t)t.kmin + ((const uint32_t *)pb.key[p])[ii]);
 #pragma unroll
                     for (int c = 0; c < NACOL; ++c) vv[c][u] = __builtin_nontemporal_load(&pb.val[c][p][ii]);
                 }
-                uint32_t gid[4];
-                bool hit[4];
+                uint32_t gid[U];
+                uint32_t hit = 0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) hit[u] = live[u] && probe_unique(t, kk[u], gid[u]);
+                for (int u = 0; u < U; ++u) {
+                    gid[u] = 0;
+                    if (((live >> u) & 1) && probe_unique(t, kk[u], gid[u])) hit |= 1u << u;
+                }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (!hit[u]) continue;
+                for (int u = 0; u < U; ++u) {
+                    if (!((hit >> u) & 1)) continue;
                     const uint32_t g = gid[u];
                     atomicAdd((unsigned long long *)&lds[g], 1ull);
                     for (int a = 0; a < specs.n; ++a) {

@@ -108,6 +108,15 @@ def load(path: str | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    # One HIP runtime per process: torch's wheel bundles its own libamdhip64
+    # (same soname, libamdhip64.so.7).  If libqeh.so loaded /opt/rocm's copy
+    # first, a later `import torch` would load a second runtime that finds no
+    # device.  Importing torch first makes libqeh bind to the copy already
+    # mapped, so torch streams/collectives and qeh kernels share one runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise RuntimeError(f"libqeh.so not found at {p}: build it with `make -C query-engine_amd` "
                            "(there is no CPU fallback)")
