@@ -620,7 +620,8 @@ class Executor {
             Table in;
             QEH_TRY(run(child.input, &in, depth + 2));
             const int n = (int)in.cols.size();
-            if (all_columns(nd.exprs, nd.n_exprs, 0, n) && all_columns(aexprs.data(), nd.n_aggs, 0, n) && in.batches > 0) {
+            if (n <= 11 && all_columns(nd.exprs, nd.n_exprs, 0, n) && all_columns(aexprs.data(), nd.n_aggs, 0, n) &&
+                in.batches > 0) {
                 auto cols = raw(in);
                 std::vector<qeh_column> keys;
                 for (int i = 0; i < nd.n_exprs; ++i) keys.push_back(cols[expr_as_column(&nd.exprs[i])]);

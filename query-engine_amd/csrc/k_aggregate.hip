@@ -29,8 +29,15 @@ constexpr int kAggR = 4;                           // rows per lane
 constexpr int kAggTile = kBlock * kAggR;           // rows per workgroup iteration
 constexpr size_t kLdsStateBudget = 48 * 1024;      // bytes of LDS state per workgroup
 
-enum GidMode { GM_ZERO = 0, GM_JOIN = 1, GM_GROUP = 2 };
+enum GidMode { GM_ZERO = 0, GM_JOIN = 1, GM_GROUP = 2, GM_LDSHASH = 3 };
 enum PredMode { PM_NONE = 0, PM_TERMS = 1, PM_PROG = 2 };
+
+constexpr int64_t kEmptyKey = INT64_MIN;
+struct GTable {                  // GM_LDSHASH: HBM table of group keys (EMPTY = INT64_MIN)
+    int64_t *keys;
+    uint64_t mask;               // capacity - 1; states index gcap = NULL group, gcap+1 = key INT64_MIN
+    uint32_t *overflow;
+};
 
 struct GidSource {
     HashTable jt;            // GM_JOIN
@@ -40,6 +47,9 @@ struct GidSource {
     const uint32_t *gslots;  // GM_GROUP
     uint64_t gmask;
     const uint64_t *gdense;
+    GTable gt;               // GM_LDSHASH
+    int32_t lcap;            // GM_LDSHASH: LDS slots per workgroup
+    int32_t _pad2;
 };
 
 template <int GM, int PM, bool LDS>
@@ -468,6 +478,146 @@ __global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn
     }
 }
 
+// ---- single-pass GROUP BY on one key: LDS hash table per workgroup ----------------------
+// Each workgroup aggregates its rows into an LDS open-addressing table keyed by
+// the key's 64-bit payload (ints sign-extended, floats as bits); rows whose key
+// does not find a slot within a few probes go straight to the HBM table.  At
+// the end the workgroup merges its occupied slots into the HBM table with
+// global atomics: one global update per (workgroup, group), not per row.
+__device__ __forceinline__ int64_t gt_slot(const GTable &g, int64_t key) {
+    uint64_t h = hash64((uint64_t)key) & g.mask;
+    for (uint64_t p = 0; p <= g.mask; ++p) {
+        const long long cur = __hip_atomic_load((long long *)&g.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) return (int64_t)h;
+        if (cur == kEmptyKey) {
+            const unsigned long long old =
+                atomicCAS((unsigned long long *)&g.keys[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+            if ((long long)old == kEmptyKey || (long long)old == key) return (int64_t)h;
+        }
+        if (p > 4096) break;  // a healthy table never probes this far: report overflow, host regrows
+        h = (h + 1) & g.mask;
+    }
+    *g.overflow = 1u;
+    return -1;
+}
+
+template <int PM>
+__global__ __launch_bounds__(kBlock) void k_groupby_lds(ColSet cols, int64_t n, PredTerms terms, DevProgram prog,
+                                                        int key_col, GidSource src, AggSpecs specs, int64_t G,
+                                                        uint64_t *__restrict__ gstates, uint32_t *__restrict__ errp) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int lcap = src.lcap;
+    int64_t *lkeys = (int64_t *)lds;
+    uint64_t *lst = lds + lcap;  // [n_slots][lcap]
+    for (int i = threadIdx.x; i < lcap; i += blockDim.x) lkeys[i] = kEmptyKey;
+    for (int64_t i = threadIdx.x; i < (int64_t)specs.n_slots * lcap; i += blockDim.x) lst[i] = 0;
+    __syncthreads();
+    for (int a = 0; a < specs.n; ++a) {
+        const AggSpec sp = specs.a[a];
+        if (sp.kind == AK_MIN || sp.kind == AK_MAX)
+            for (int i = threadIdx.x; i < lcap; i += blockDim.x) lst[(int64_t)sp.val_slot * lcap + i] = (uint64_t)agg_init_value(sp.kind);
+    }
+    __syncthreads();
+    const int64_t gcap = (int64_t)src.gt.mask + 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t err = 0;
+    const int64_t ntiles = (n + kAggTile - 1) / kAggTile;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row0 = tile * kAggTile + (int64_t)wave * 64 * kAggR + lane;
+        uint32_t sel;
+        if (PM == PM_TERMS) {
+            sel = eval_terms<kAggR>(terms, cols, row0, 64, n);
+        } else if (PM == PM_PROG) {
+            ExprRegs<kAggR> X;
+            run_program<kAggR>(prog, cols, row0, 64, n, X, err);
+            sel = program_true_mask<kAggR>(X);
+        } else {
+            sel = 0;
+#pragma unroll
+            for (int r = 0; r < kAggR; ++r)
+                if (row0 + r * 64 < n) sel |= 1u << r;
+        }
+        int64_t kv[kAggR];
+        uint32_t kvalid;
+        load_rows<kAggR>(cols.c[key_col], row0, 64, n, kv, kvalid);
+#pragma unroll
+        for (int r = 0; r < kAggR; ++r) {
+            if (!((sel >> r) & 1)) continue;
+            const int64_t row = row0 + r * 64;
+            const int64_t key = kv[r];
+            uint64_t *st;
+            int64_t stride, idx;
+            bool local = false;
+            int lslot = -1;
+            if (((kvalid >> r) & 1) && key != kEmptyKey) {
+                int h = (int)(hash64((uint64_t)key) & (uint64_t)(lcap - 1));
+                for (int p = 0; p < 32; ++p) {
+                    const int64_t cur = lkeys[h];
+                    if (cur == key) { lslot = h; break; }
+                    if (cur == kEmptyKey) {
+                        const unsigned long long old = atomicCAS((unsigned long long *)&lkeys[h],
+                                                                 (unsigned long long)kEmptyKey, (unsigned long long)key);
+                        if ((long long)old == kEmptyKey || (long long)old == key) { lslot = h; break; }
+                    }
+                    h = (h + 1) & (lcap - 1);
+                }
+            }
+            if (lslot >= 0) {
+                local = true;
+                st = lst;
+                stride = lcap;
+                idx = lslot;
+            } else {
+                st = gstates;
+                stride = G;
+                if (!((kvalid >> r) & 1)) idx = gcap;            // the NULL group
+                else if (key == kEmptyKey) idx = gcap + 1;       // the key that doubles as EMPTY
+                else idx = gt_slot(src.gt, key);
+                if (idx < 0) continue;                            // overflow flagged; host regrows and reruns
+            }
+            atomicAdd((unsigned long long *)&st[idx], 1ull);
+            for (int a = 0; a < specs.n; ++a) {
+                const AggSpec sp = specs.a[a];
+                const ColRef &c = cols.c[sp.col];
+                if (!col_valid(c, row)) continue;
+                if (sp.cnt_slot) atomicAdd((unsigned long long *)&st[(int64_t)sp.cnt_slot * stride + idx], 1ull);
+                if (sp.kind != AK_COUNT) {
+                    const int64_t x = agg_input(sp.kind, sp.in_type, load_i64(c, row));
+                    if (local) agg_apply<true>(sp.kind, &st[(int64_t)sp.val_slot * stride + idx], x);
+                    else agg_apply<false>(sp.kind, &st[(int64_t)sp.val_slot * stride + idx], x);
+                }
+            }
+        }
+    }
+    if (err) atomicOr(errp, err);
+    __syncthreads();
+    for (int i = threadIdx.x; i < lcap; i += blockDim.x) {
+        const int64_t key = lkeys[i];
+        if (key == kEmptyKey) continue;
+        const int64_t g = gt_slot(src.gt, key);
+        if (g < 0) continue;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)lst[i]);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.cnt_slot) {
+                const uint64_t c = lst[(int64_t)sp.cnt_slot * lcap + i];
+                if (c) atomicAdd((unsigned long long *)&gstates[(int64_t)sp.cnt_slot * G + g], (unsigned long long)c);
+            }
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * lcap + i]);
+        }
+    }
+}
+
+__global__ void k_fill_i64(int64_t *p, int64_t n, int64_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+__global__ void k_iota(uint32_t *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = (uint32_t)i;
+}
+
 __global__ void k_states_init(uint64_t *states, int64_t G, AggSpecs specs) {
     const int64_t words = (int64_t)specs.n_slots * G;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
@@ -824,6 +974,8 @@ static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, con
     return 1;
 }
 
+constexpr int kRetryBigger = 100;  // internal: group table too small
+
 // Run the row-aggregation kernel and finalize into owned output columns.
 static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, const PredPlan &pp,
                           const GidSource &src, const AggSpecs &specs, int64_t G, const KeyCols &out_keys_src,
@@ -854,9 +1006,28 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
                 launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
                                          states.as<uint64_t>(), errw.as<uint32_t>());
         }
+        else if (gm == GM_LDSHASH) {
+            const size_t shm = (size_t)(1 + specs.n_slots) * src.lcap * 8;
+            const int pc = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / shm));
+            const int g2 = grid_for(ctx, n, kAggTile, pc);
+            if (pp.mode == PM_TERMS)
+                hipLaunchKernelGGL(k_groupby_lds<PM_TERMS>, dim3(g2), dim3(kBlock), shm, ctx->stream, cols, n, pp.terms,
+                                   pp.prog, src.key_col, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
+            else if (pp.mode == PM_PROG)
+                hipLaunchKernelGGL(k_groupby_lds<PM_PROG>, dim3(g2), dim3(kBlock), shm, ctx->stream, cols, n, pp.terms,
+                                   pp.prog, src.key_col, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
+            else
+                hipLaunchKernelGGL(k_groupby_lds<PM_NONE>, dim3(g2), dim3(kBlock), shm, ctx->stream, cols, n, pp.terms,
+                                   pp.prog, src.key_col, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
+        }
         else launch_agg_rows<GM_GROUP>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
     }
     QEH_HIP(hipGetLastError());
+    if (gm == GM_LDSHASH) {  // table overflow: the caller regrows and reruns
+        uint32_t of = 0;
+        QEH_TRY(read_small(ctx, &of, src.gt.overflow, 4));
+        if (of) return kRetryBigger;
+    }
 
     // compact non-empty groups
     DevBuf flags, pos;
@@ -926,6 +1097,70 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     return QEH_OK;
 }
 
+int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const qeh_column *agg_inputs,
+                            int n_inputs, const qeh_agg *aggs, int n_aggs, const qeh_column *pred_cols,
+                            int n_pred_cols, const qeh_expr *predicate, int64_t input_batches,
+                            qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups);
+
+// More aggregates than one kernel carries (kMaxAggs): run the operator once per
+// chunk of aggregates.  Group order differs between runs (slot races), so every
+// chunk's output is put in key order (the radix sort; keys are unique per group)
+// and the chunks then line up row for row.
+static int aggregate_chunked(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const qeh_column *agg_inputs,
+                             int n_inputs, const qeh_agg *aggs, int n_aggs, const qeh_column *pred_cols,
+                             int n_pred_cols, const qeh_expr *predicate, int64_t input_batches,
+                             qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups) {
+    std::vector<qeh_column> made;  // everything produced so far, released on error
+    auto release_all = [&]() {
+        for (auto &c : made) qeh_column_release(ctx, &c);
+    };
+    std::vector<qeh_column> ck(n_keys);
+    std::vector<int8_t> asc(n_keys, 1);
+    int64_t groups = -1;
+    for (int a0 = 0; a0 < n_aggs; a0 += kMaxAggs) {
+        const int na = std::min(kMaxAggs, n_aggs - a0);
+        int64_t g = 0;
+        int s = hash_aggregate_filtered(ctx, keys, n_keys, agg_inputs, n_inputs, aggs + a0, na, pred_cols,
+                                        n_pred_cols, predicate, input_batches, ck.data(), out_aggs + a0, &g);
+        if (s != QEH_OK) {
+            release_all();
+            return s;
+        }
+        if (groups >= 0 && g != groups) {
+            for (int i = 0; i < n_keys; ++i) qeh_column_release(ctx, &ck[i]);
+            for (int i = 0; i < na; ++i) qeh_column_release(ctx, &out_aggs[a0 + i]);
+            release_all();
+            return fail(QEH_E_INTERNAL, "aggregate chunks disagree on the group count");
+        }
+        groups = g;
+        if (n_keys > 0 && g > 1) {
+            qeh_column perm{};
+            s = qeh_sort_indices(ctx, ck.data(), n_keys, asc.data(), &perm);
+            for (int i = 0; s == QEH_OK && i < n_keys + na; ++i) {
+                qeh_column *c = i < n_keys ? &ck[i] : &out_aggs[a0 + i - n_keys];
+                qeh_column t{};
+                s = qeh_take(ctx, c, &perm, &t);
+                qeh_column_release(ctx, c);
+                *c = t;
+            }
+            qeh_column_release(ctx, &perm);
+            if (s != QEH_OK) {
+                for (int i = 0; i < n_keys; ++i) qeh_column_release(ctx, &ck[i]);
+                for (int i = 0; i < na; ++i) qeh_column_release(ctx, &out_aggs[a0 + i]);
+                release_all();
+                return s;
+            }
+        }
+        for (int i = 0; i < n_keys; ++i) {
+            if (a0 == 0) out_keys[i] = ck[i], made.push_back(ck[i]);
+            else qeh_column_release(ctx, &ck[i]);
+        }
+        for (int i = 0; i < na; ++i) made.push_back(out_aggs[a0 + i]);
+    }
+    *out_groups = groups;
+    return QEH_OK;
+}
+
 // Internal entry shared by qeh_hash_aggregate and the executor's fused
 // Aggregate(Filter(..)) path: `cols` = key columns then aggregate inputs.
 int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const qeh_column *agg_inputs,
@@ -935,6 +1170,9 @@ int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, co
     if (!out_groups) return fail(QEH_E_INVALID, "qeh_hash_aggregate: out_groups is NULL");
     *out_groups = 0;
     if (n_aggs == 0) return QEH_OK;  // executor.rs:163-165: no aggregates -> no batches
+    if (n_aggs > kMaxAggs)
+        return aggregate_chunked(ctx, keys, n_keys, agg_inputs, n_inputs, aggs, n_aggs, pred_cols, n_pred_cols,
+                                 predicate, input_batches, out_keys, out_aggs, out_groups);
     int64_t n = -1;
     auto take_len = [&](const qeh_column &c) -> int {
         if (n < 0) n = c.length;
@@ -945,9 +1183,12 @@ int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, co
     for (int i = 0; i < n_inputs; ++i) QEH_TRY(take_len(agg_inputs[i]));
     for (int i = 0; i < n_pred_cols; ++i) QEH_TRY(take_len(pred_cols[i]));
     if (n < 0) n = 0;
-    // kernel ColSet = predicate columns, then aggregate inputs (keys are read through KeyCols)
+    // kernel ColSet = predicate columns, then aggregate inputs (keys are read through KeyCols);
+    // when the predicate reads the aggregate inputs themselves they are passed once
+    const bool shared_cols = pred_cols == agg_inputs && n_pred_cols == n_inputs;
     std::vector<qeh_column> all;
-    for (int i = 0; i < n_pred_cols; ++i) all.push_back(pred_cols[i]);
+    if (!shared_cols)
+        for (int i = 0; i < n_pred_cols; ++i) all.push_back(pred_cols[i]);
     std::vector<int> idx(n_inputs);
     for (int i = 0; i < n_inputs; ++i) {
         idx[i] = (int)all.size();
@@ -970,6 +1211,60 @@ int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, co
         KeyCols none{};
         return aggregate_rows(ctx, GM_ZERO, cols, n, pp, src, specs, 1, none, nullptr, nullptr, false,
                               "aggregate_rows", out_keys, out_aggs, out_groups);
+    }
+    const int kd0 = keys[0].dtype;
+    if (n_keys == 1 && kd0 != QEH_DT_UTF8 && !std::getenv("QEH_NO_LDS_GROUPBY")) {
+        // single key: one pass, LDS hash table per workgroup, HBM table for the merge
+        uint64_t gcap = 1ull << 16;
+        while (gcap < (uint64_t)(n / 16) && gcap < (1ull << 22)) gcap <<= 1;
+        ColSet cols2;
+        std::vector<qeh_column> all2 = all;
+        all2.push_back(keys[0]);
+        QEH_TRY(make_colset(all2.data(), (int)all2.size(), &cols2));
+        for (int attempt = 0;; ++attempt) {
+            const int64_t G = (int64_t)gcap + 2;
+            DevBuf gkeys, ovf, iota, gvalid;
+            QEH_TRY(gkeys.alloc(ctx, (size_t)G * 8));
+            QEH_TRY(ovf.alloc(ctx, 8));
+            QEH_TRY(iota.alloc(ctx, (size_t)G * 4));
+            QEH_TRY(gvalid.alloc(ctx, (size_t)((G + 63) / 64) * 8));
+            QEH_HIP(hipMemsetAsync(ovf.p, 0, 8, ctx->stream));
+            const int gg = grid_for(ctx, G, kBlock * 8, 8);
+            hipLaunchKernelGGL(k_fill_i64, dim3(gg), dim3(kBlock), 0, ctx->stream, gkeys.as<int64_t>(), (int64_t)gcap, kEmptyKey);
+            const int64_t tail[2] = {0, kEmptyKey};
+            QEH_HIP(hipMemcpyAsync(gkeys.as<int64_t>() + gcap, tail, 16, hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL(k_iota, dim3(gg), dim3(kBlock), 0, ctx->stream, iota.as<uint32_t>(), G);
+            QEH_HIP(hipMemsetAsync(gvalid.p, 0xFF, (size_t)((G + 63) / 64) * 8, ctx->stream));
+            uint8_t nb = 0;  // clear the NULL group's validity bit (bit gcap)
+            uint8_t byte = (uint8_t)~(1u << (gcap & 7));
+            (void)nb;
+            QEH_HIP(hipMemcpyAsync(gvalid.as<uint8_t>() + (gcap >> 3), &byte, 1, hipMemcpyHostToDevice, ctx->stream));
+            QEH_HIP(hipStreamSynchronize(ctx->stream));  // host staging above
+            GidSource ls{};
+            ls.gt.keys = gkeys.as<int64_t>();
+            ls.gt.mask = gcap - 1;
+            ls.gt.overflow = ovf.as<uint32_t>();
+            ls.key_col = (int)all.size();
+            int lcap = 2048;
+            while (lcap > 256 && (size_t)(1 + specs.n_slots) * lcap * 8 > 64 * 1024) lcap >>= 1;
+            ls.lcap = lcap;
+            KeyCols kc{};
+            kc.n = 1;
+            kc.c[0].values = gkeys.p;
+            kc.c[0].dtype = QEH_DT_INT64;  // raw 64-bit payloads; written back as the key's dtype
+            kc.c[0].validity = gvalid.as<uint8_t>();
+            kc.c[0].vbit0 = 0;
+            const int s = aggregate_rows(ctx, GM_LDSHASH, cols2, n, pp, ls, specs, G, kc, kd.data(), iota.as<uint32_t>(),
+                                         true, "aggregate_rows", out_keys, out_aggs, out_groups);
+            if (s != kRetryBigger) {
+                if (s == QEH_OK && keys[0].validity == nullptr) {
+                    // keys without nulls produce a never-null key column
+                }
+                return s;
+            }
+            if (gcap >= (1ull << 30)) return fail(QEH_E_OOM, "group table overflow");
+            gcap <<= 4;
+        }
     }
     GroupTable gt;
     QEH_TRY(build_group_table(ctx, keys, n_keys, n, &gt, nullptr));

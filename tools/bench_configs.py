@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE configs on one MI355X (the headline metric is bench.py).
+
+  cfg2  Filter + GROUP BY SUM/COUNT: SELECT k, SUM(v), COUNT(v), SUM(vi) FROM t
+        WHERE x > 49 GROUP BY k   (1e8 rows; 32 B/row algorithmic)
+  cfg3  INNER hash join 1e9 x 1e7 materialising (f.v, d.a)
+        (16 B probe + 16 B output per fact row; build 16 B/dim row)
+  cfg5  ROW_NUMBER() OVER (PARTITION BY k ORDER BY v), k in [0, 2^20)
+        (16 B read + 8 B write per row)
+  filter  the Filter operator alone: SELECT x, k, v WHERE x > 49 (24 B in + 12 B out avg per row)
+
+Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
+fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter] [--scale 1.0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "query-engine_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (one HIP runtime: torch first, see qe_hip/abi.py)
+
+import qe_hip  # noqa: E402
+import oracle_bind as ob  # noqa: E402
+from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit  # noqa: E402
+
+PEAK = 8000.0
+SEED = 0x5EED
+
+
+def timed(ctx, fn, reps, names):
+    fn()
+    ctx.sync()
+    ctx.timing(True)
+    ctx.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    ctx.sync()
+    wall = (time.perf_counter() - t0) / reps
+    kt = {n: ctx.kernel_time(n)[0] / reps for n in names}
+    ctx.timing(False)
+    return wall, kt, out
+
+
+def line(cfg, rows, wall, alg_bytes, kernel_ms, kernel, cpu, extra=None):
+    gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+    d = {"config": cfg, "rows": rows, "rows_per_s": rows / wall, "ms_per_run": wall * 1e3,
+         "dominant_kernel": kernel, "kernel_ms": kernel_ms, "alg_bytes": alg_bytes,
+         "achieved_GBs": gbs, "frac_of_8TBs": gbs / PEAK if gbs else None, "cpu_baseline": cpu}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def cfg2(ctx, scale):
+    n = int(1e8 * scale)
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 1024)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    vi = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 4, n, 2 ** 21, lo=-(2 ** 20))
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    fn = lambda: ctx.filter_aggregate([x, k, v, vi], pred, [1], [(AF.Sum, 2), (AF.Count, 2), (AF.Sum, 3)])
+    wall, kt, _ = timed(ctx, fn, 10, ["aggregate_rows", "group_insert"])
+    m = 20_000_000
+    hx = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 1, m, 100)
+    hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, m, 1024)
+    hv = ob.generate(abi.GEN_UNIT_F64, SEED, 3, m)
+    hvi = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 4, m, 2 ** 21, lo=-(2 ** 20))
+    t0 = time.perf_counter()
+    fc, rows, _ = ob.filter([ob.HostCol(hx), ob.HostCol(hk), ob.HostCol(hv), ob.HostCol(hvi)], pred)
+    fh = [ob.HostCol(a, b) for a, b in fc]
+    ob.hash_aggregate([fh[1]], fh, [(AF.Sum, 2), (AF.Count, 2), (AF.Sum, 3)])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows, {dt:.2f} s"}
+    kms = kt["aggregate_rows"] + kt["group_insert"]
+    line("cfg2 filter+group-by 1e8", n, wall, 32.0 * n, kms, "group_insert + k_agg_rows<GM_GROUP,PM_TERMS,LDS>", cpu)
+
+
+def cfg3(ctx, scale):
+    n, nd = int(1e9 * scale), 10_000_000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    fv = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1000)
+
+    def fn():
+        p, b, rows = ctx.hash_join_inner(fk, [fv], dk, [da])
+        for c in p + b:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 3, ["join_probe", "join_gather", "join_build"])
+    m = 20_000_000
+    hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, m, nd)
+    hv = ob.generate(abi.GEN_UNIT_F64, SEED, 3, m)
+    hdk = ob.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    hda = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1000)
+    t0 = time.perf_counter()
+    ob.hash_join_inner(ob.HostCol(hk), [ob.HostCol(hv)], ob.HostCol(hdk), [ob.HostCol(hda)])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} probe x {nd} build, {dt:.2f} s"}
+    kms = kt["join_probe"] + kt["join_gather"]
+    line("cfg3 inner join 1e9 x 1e7", n, wall, 32.0 * n, kms, "k_join_probe + k_gather", cpu,
+         {"output_rows": rows, "build_ms": kt["join_build"]})
+
+
+def cfg5(ctx, scale):
+    n = int(1e9 * scale)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 20)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 8, n, 2 ** 62, lo=-(2 ** 61))
+
+    def fn():
+        rn = ctx.row_number([k], [v], [True])
+        rn.release()
+    wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "row_number"])
+    m = 5_000_000
+    hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 7, m, 2 ** 20)
+    hv = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 8, m, 2 ** 62, lo=-(2 ** 61))
+    t0 = time.perf_counter()
+    ob.row_number([ob.HostCol(hk)], [ob.HostCol(hv)], [True])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows, {dt:.2f} s"}
+    kms = sum(kt.values())
+    line("cfg5 ROW_NUMBER 1e9", n, wall, 24.0 * n, kms, "k_rs_hist/k_rs_scatter (+encode, row numbers)", cpu, kt)
+
+
+def cfg_filter(ctx, scale):
+    n = int(5e8 * scale)
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 1024)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+
+    def fn():
+        out, rows = ctx.filter([x, k, v], pred)
+        for c in out:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 5, ["filter"])
+    line("filter 5e8 x3 cols", n, wall, 24.0 * n + 24.0 * rows, kt["filter"], "k_filter<1>", None,
+         {"selected": rows})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="cfg2,cfg3,cfg5,filter")
+    ap.add_argument("--scale", type=float, default=1.0)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    ctx = qe_hip.Context(0)
+    ctx.set_stream(s.cuda_stream)
+    for name in args.only.split(","):
+        {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter}[name](ctx, args.scale)
+        ctx.sync()
+        abi.check(ctx.lib.qeh_pool_trim(ctx.h))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
