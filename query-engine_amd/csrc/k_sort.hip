@@ -89,61 +89,129 @@ __global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n,
 }
 
 // ---- one LSD pass ----------------------------------------------------------------------
-// block b owns elements [b*seg, (b+1)*seg); hist is digit-major [kRadix][nblocks]
+// Block b owns elements [b*seg, (b+1)*seg) and walks them in tiles of kRsTile;
+// inside a tile wave w owns the contiguous run [w*64*kRsIpt, (w+1)*64*kRsIpt)
+// and its item j is element w*64*kRsIpt + j*64 + lane, so (wave, j, lane) is
+// input order and every load is a full 512-byte wave line.  hist is digit-major
+// [kRadix][nblocks].
+constexpr int kRsIpt = 8;
+constexpr int kRsTile = kBlock * kRsIpt;
+static_assert(kBlock == kRadix, "one thread per digit in the tile bookkeeping");
+
+// lanes of this wave whose digit equals mine (wave64 has no match_any: 8 ballots)
+__device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
+    uint64_t peers = __ballot(live);
+#pragma unroll
+    for (int b = 0; b < kRadixBits; ++b) {
+        const uint64_t m = __ballot((dg >> b) & 1);
+        peers &= ((dg >> b) & 1) ? m : ~m;
+    }
+    return peers;
+}
+
 __global__ __launch_bounds__(kBlock) void k_rs_hist(const uint64_t *__restrict__ keys, int64_t n, int64_t seg,
                                                     int shift, uint32_t *__restrict__ hist, int nblocks) {
     __shared__ uint32_t h[kRadix];
-    for (int i = threadIdx.x; i < kRadix; i += blockDim.x) h[i] = 0;
+    h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&h[(keys[i] >> shift) & (kRadix - 1)], 1u);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t c0 = lo; c0 < hi; c0 += kRsTile) {
+        const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
+        uint64_t k[kRsIpt];
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            const int64_t i = base + j * 64;
+            k[j] = i < hi ? __builtin_nontemporal_load(&keys[i]) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            const bool live = base + j * 64 < hi;
+            const uint32_t dg = (uint32_t)((k[j] >> shift) & (kRadix - 1));
+            const uint64_t peers = digit_peers(dg, live);  // one LDS atomic per distinct digit per wave
+            if (live && mbcnt(peers) == 0) atomicAdd(&h[dg], (uint32_t)popc64(peers));
+        }
+    }
     __syncthreads();
-    for (int d = threadIdx.x; d < kRadix; d += blockDim.x) hist[(int64_t)d * nblocks + blockIdx.x] = h[d];
+    hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
+// Stable scatter: rank each tile by digit in registers/LDS, reorder it in LDS,
+// then write digit runs (≈ kRsTile/kRadix elements each) contiguously.
 __global__ __launch_bounds__(kBlock) void k_rs_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                        int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                        int nblocks, uint64_t *__restrict__ keys_out,
                                                        uint32_t *__restrict__ vals_out) {
     constexpr int W = kBlock / 64;
-    __shared__ uint32_t wave_hist[W][kRadix];
-    __shared__ uint64_t wave_pos[W][kRadix];
-    __shared__ uint64_t run[kRadix];  // next output position of each digit for this block
-    const int wave = threadIdx.x >> 6;
-    for (int d = threadIdx.x; d < kRadix; d += blockDim.x) run[d] = offs[(int64_t)d * nblocks + blockIdx.x];
+    __shared__ uint64_t s_keys[kRsTile];
+    __shared__ uint32_t s_vals[kRsTile];
+    __shared__ uint32_t wcnt[W][kRadix];  // per-wave digit counts, then per-wave start inside the digit
+    __shared__ uint32_t loc[kRadix];      // tile-local start of each digit
+    __shared__ uint32_t wsum[W];
+    __shared__ uint64_t run[kRadix];      // global position of the block's next element of each digit
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
-    for (int64_t c0 = lo; c0 < hi; c0 += kBlock) {
-        for (int i = threadIdx.x; i < W * kRadix; i += blockDim.x) (&wave_hist[0][0])[i] = 0;
-        __syncthreads();
-        const int64_t i = c0 + threadIdx.x;
-        const bool live = i < hi;
-        const uint64_t k = live ? keys[i] : 0;
-        const uint32_t v = live ? vals[i] : 0;
-        const uint32_t dg = (uint32_t)((k >> shift) & (kRadix - 1));
-        // lanes of this wave holding the same digit: 8 ballots (wave64 has no match_any)
-        uint64_t peers = __ballot(live);
+    for (int64_t c0 = lo; c0 < hi; c0 += kRsTile) {
 #pragma unroll
-        for (int b = 0; b < kRadixBits; ++b) {
-            const uint64_t m = __ballot((dg >> b) & 1);
-            peers &= ((dg >> b) & 1) ? m : ~m;
-        }
-        const uint32_t rank = mbcnt(peers);
-        if (live && rank == 0) wave_hist[wave][dg] = (uint32_t)popc64(peers);
+        for (int w = 0; w < W; ++w) wcnt[w][t] = 0;
         __syncthreads();
-        for (int d = threadIdx.x; d < kRadix; d += blockDim.x) {
-            uint64_t acc = run[d];
-            for (int w = 0; w < W; ++w) {
-                wave_pos[w][d] = acc;
-                acc += wave_hist[w][d];
+        const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
+        uint64_t k[kRsIpt];
+        uint32_t v[kRsIpt], rk[kRsIpt];
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            const int64_t i = base + j * 64;
+            const bool live = i < hi;
+            k[j] = live ? __builtin_nontemporal_load(&keys[i]) : 0;
+            v[j] = live ? __builtin_nontemporal_load(&vals[i]) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            const bool live = base + j * 64 < hi;
+            const uint32_t dg = (uint32_t)((k[j] >> shift) & (kRadix - 1));
+            const uint64_t peers = digit_peers(dg, live);
+            const uint32_t before = wcnt[wave][dg];
+            rk[j] = before + mbcnt(peers);
+            if (live && mbcnt(peers) == 0) wcnt[wave][dg] = before + (uint32_t)popc64(peers);
+        }
+        __syncthreads();
+        // thread t = digit t: wave starts inside the digit, tile total, block scan -> loc
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t c = wcnt[w][t];
+            wcnt[w][t] = tot;
+            tot += c;
+        }
+        const uint32_t incl = wave_incl_scan(tot);
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t wbase = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) wbase += w < wave ? wsum[w] : 0;
+        loc[t] = wbase + incl - tot;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            if (base + j * 64 < hi) {
+                const uint32_t dg = (uint32_t)((k[j] >> shift) & (kRadix - 1));
+                const uint32_t p = loc[dg] + wcnt[wave][dg] + rk[j];
+                s_keys[p] = k[j];
+                s_vals[p] = v[j];
             }
-            run[d] = acc;
         }
         __syncthreads();
-        if (live) {  // stable: element order = (chunk, wave, lane)
-            const uint64_t pos = wave_pos[wave][dg] + rank;
-            keys_out[pos] = k;
-            vals_out[pos] = v;
+        const int cnt = (int)(hi - c0 < kRsTile ? hi - c0 : kRsTile);
+        for (int p = t; p < cnt; p += kBlock) {
+            const uint64_t key = s_keys[p];
+            const uint32_t dg = (uint32_t)((key >> shift) & (kRadix - 1));
+            const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
+            keys_out[pos] = key;
+            vals_out[pos] = s_vals[p];
         }
+        __syncthreads();
+        run[t] += tot;
     }
 }
 
@@ -152,13 +220,14 @@ struct RadixState {
     DevBuf k[2], v[2];
     int cur = 0;
     int64_t n = 0;
+    bool enc_injective = false;  // k[cur] encodes the last-sorted column one-to-one (no null-flag pass)
 };
 
 // Stable LSD passes over the low `bits` of the encoded keys in rs.
 static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
     const int64_t n = rs.n;
     if (n <= 1 || bits <= 0) return QEH_OK;
-    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + 4095) / 4096, 1), (int64_t)ctx->props.multiProcessorCount * 4);
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsTile - 1) / kRsTile, 1), (int64_t)ctx->props.multiProcessorCount * 4);
     const int64_t seg = (n + nblocks - 1) / nblocks;
     DevBuf hist, offs;
     QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
@@ -227,6 +296,7 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
         rs.cur = o;
         QEH_TRY(radix_passes(ctx, rs, pass == 0 ? bits : 1));
     }
+    rs.enc_injective = !null_pass;
     return QEH_OK;
 }
 
@@ -274,6 +344,13 @@ __global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, in
         }
         flags[i] = f;
     }
+}
+
+// single partition key: compare the sorted encodings (coalesced) instead of
+// gathering the key column through the permutation
+__global__ void k_part_flags_enc(const uint64_t *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        flags[i] = i == 0 || enc[i] != enc[i - 1];
 }
 
 // seg_excl[i] = number of partition starts before i; start_of[seg] = sorted index of its first row
@@ -404,7 +481,11 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     const int grid = grid_for(ctx, n, kBlock * 8, 8);
     {
         KernelTimer kt(ctx, "row_number");
-        hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
+        if (n_part == 1 && rs.enc_injective)
+            hipLaunchKernelGGL(k_part_flags_enc, dim3(grid), dim3(kBlock), 0, ctx->stream, rs.k[rs.cur].as<uint64_t>(), n,
+                               flags.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
     }
     uint64_t nseg = 0;
     s = exclusive_scan_u32(ctx, flags.as<uint32_t>(), seg.as<uint64_t>(), n, &nseg);

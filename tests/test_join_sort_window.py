@@ -159,3 +159,28 @@ def test_hash_partition_conserves_rows(ctx, parts):
             assert seen.setdefault(int(key), q) == q  # one partition per key
     counts2, perm2 = ctx.hash_partition(ctx.upload(k, kv), parts)
     assert np.array_equal(counts, counts2) and np.array_equal(perm2.to_numpy()[0], p)
+
+
+@pytest.mark.gpu
+def test_sort_many_tiles_per_block_wide_keys(ctx):
+    """> 1024 blocks x 2048-row tiles: several tiles per block, 8 passes of 8 bits, low-entropy top digit."""
+    r = np.random.default_rng(21)
+    n = 6_000_001
+    k = r.integers(-(2 ** 62), 2 ** 62, n).astype(np.int64)
+    k[::7] = 5  # heavy duplicate run
+    perm, want = sort_both(ctx, [(k, None)], [False])
+    assert np.array_equal(perm, want)
+
+
+@pytest.mark.gpu
+def test_row_number_full_range_nullable_partition_key(ctx):
+    """Null-flag pass case (2^64 values + NULL): partition flags fall back to comparing the key column."""
+    r = np.random.default_rng(22)
+    n = 40_000
+    k = r.integers(0, 50, n).astype(np.int64)
+    k[0], k[1] = np.iinfo(np.int64).min, np.iinfo(np.int64).max
+    kv = r.random(n) > 0.1
+    v = r.integers(-9, 9, n).astype(np.int64)
+    rn = ctx.row_number([ctx.upload(k, kv)], [ctx.upload(v)], [True]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k, kv)], [ob.HostCol(v)], [True])
+    assert np.array_equal(rn, want)
