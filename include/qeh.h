@@ -257,6 +257,21 @@ int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_part,
 int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
                        qeh_column *out_perm);
 
+/* Range partition for distributed Sort / ORDER BY (SURVEY.md §8 row e):
+ * partition p holds the rows whose order key lies between splitters p-1 and p
+ * (`splitters` = host array of ascending order keys: the Int value itself, the
+ * IEEE totalOrder key of Float64 bits, Float32 widened to Float64 first);
+ * equal keys share a partition, NULLs go to partition 0 (NULLs first, as in
+ * qeh_sort_indices); `ascending` = 0 reverses the partition order.  Same
+ * counts / stable partition-major `out_perm` contract as qeh_hash_partition. */
+int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int ascending, const int64_t *splitters,
+                        int n_splitters, int64_t *counts, qeh_column *out_perm);
+
+/* out[indices[i]] = col[i] (inverse of qeh_take for a permutation): returns
+ * per-row results to their original positions after an exchange.  Non-null
+ * fixed-width columns; `indices` UINT32 of the same length. */
+int qeh_scatter(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out);
+
 /* Validity bitmap <-> one byte per row (1 = valid), for moving nullable
  * columns through byte-addressed collectives (RCCL all-to-all splits are
  * row counts, not bit offsets).  Buffers are device pointers. */

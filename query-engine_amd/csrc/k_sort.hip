@@ -380,6 +380,28 @@ __global__ void k_partition_ids(ColRef key, int64_t n, uint32_t parts, uint64_t 
     }
 }
 
+// range partition: NULL -> 0 (NULLs sort first); value -> number of splitters
+// strictly below (ascending) / above (descending) its order key, so equal keys
+// share a partition and partition p precedes p+1 in sort order
+__global__ void k_range_ids(ColRef key, int64_t n, const int64_t *__restrict__ split, int n_split, int asc,
+                            uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t p = 0;
+        if (col_valid(key, i)) {
+            const int64_t k = ordered_key(key, i);
+            for (int j = 0; j < n_split; ++j) p += asc ? split[j] < k : split[j] > k;
+        }
+        keys[i] = p;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+template <typename T>
+__global__ void k_scatter(const T *__restrict__ src, const uint32_t *__restrict__ idx, int64_t m, T *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        out[idx[i]] = src[i];
+}
+
 __global__ void k_count_parts(const uint64_t *__restrict__ ids, int64_t n, int parts, unsigned long long *__restrict__ counts) {
     __shared__ uint32_t h[kRadix];
     for (int i = threadIdx.x; i < kRadix; i += blockDim.x) h[i] = 0;
@@ -506,15 +528,10 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     return QEH_OK;
 }
 
-extern "C" int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
-                                  qeh_column *out_perm) {
-    if (!ctx || !key || !counts || !out_perm || n_parts < 1 || n_parts > kRadix)
-        return fail(QEH_E_INVALID, "qeh_hash_partition: bad argument (1..256 partitions)");
-    DeviceGuard dg(ctx->device);
-    QEH_TRY(check_column(*key, "partition key"));
-    if (key->dtype != QEH_DT_INT64 && key->dtype != QEH_DT_INT32)
-        return fail(QEH_E_UNSUPPORTED, "partition keys must be Int32/Int64 on the device");
-    const int64_t n = key->length;
+// Stable partition-major permutation from per-row partition ids written by `ids`.
+template <typename IdLaunch>
+static int partition_perm(qeh_ctx *ctx, int64_t n, int n_parts, IdLaunch ids, const char *timer, int64_t *counts,
+                          qeh_column *out_perm) {
     RadixState rs;
     rs.n = n;
     for (int b = 0; b < 2; ++b) {
@@ -524,9 +541,8 @@ extern "C" int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_par
     std::fill(counts, counts + n_parts, 0);
     if (n > 0) {
         {
-            KernelTimer kt(ctx, "hash_partition");
-            hipLaunchKernelGGL(k_partition_ids, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
-                               make_colref(*key), n, (uint32_t)n_parts, rs.k[0].as<uint64_t>(), rs.v[0].as<uint32_t>());
+            KernelTimer kt(ctx, timer);
+            ids(rs.k[0].as<uint64_t>(), rs.v[0].as<uint32_t>());
         }
         QEH_HIP(hipGetLastError());
         QEH_TRY(radix_passes(ctx, rs, n_parts > 1 ? bit_length((uint64_t)n_parts - 1) : 0));
@@ -547,6 +563,82 @@ extern "C" int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_par
             return s;
         }
     }
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+extern "C" int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t *counts,
+                                  qeh_column *out_perm) {
+    if (!ctx || !key || !counts || !out_perm || n_parts < 1 || n_parts > kRadix)
+        return fail(QEH_E_INVALID, "qeh_hash_partition: bad argument (1..256 partitions)");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*key, "partition key"));
+    if (key->dtype != QEH_DT_INT64 && key->dtype != QEH_DT_INT32)
+        return fail(QEH_E_UNSUPPORTED, "partition keys must be Int32/Int64 on the device");
+    const int64_t n = key->length;
+    const ColRef kc = make_colref(*key);
+    return partition_perm(
+        ctx, n, n_parts,
+        [&](uint64_t *ids, uint32_t *idx) {
+            hipLaunchKernelGGL(k_partition_ids, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, kc,
+                               n, (uint32_t)n_parts, ids, idx);
+        },
+        "hash_partition", counts, out_perm);
+}
+
+extern "C" int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int ascending, const int64_t *splitters,
+                                   int n_splitters, int64_t *counts, qeh_column *out_perm) {
+    if (!ctx || !key || !counts || !out_perm || n_splitters < 0 || n_splitters >= kRadix ||
+        (n_splitters > 0 && !splitters))
+        return fail(QEH_E_INVALID, "qeh_range_partition: bad argument (0..255 splitters)");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*key, "partition key"));
+    if (key->dtype == QEH_DT_UTF8) return fail(QEH_E_UNSUPPORTED, "Utf8 range partition keys are not supported on the device");
+    for (int j = 1; j < n_splitters; ++j)
+        if (splitters[j] < splitters[j - 1]) return fail(QEH_E_INVALID, "qeh_range_partition: splitters must be ascending");
+    const int64_t n = key->length;
+    DevBuf sp;
+    QEH_TRY(sp.alloc(ctx, (size_t)std::max(n_splitters, 1) * 8));
+    if (n_splitters > 0)
+        QEH_HIP(hipMemcpyAsync(sp.p, splitters, (size_t)n_splitters * 8, hipMemcpyHostToDevice, ctx->stream));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));  // host splitter array may go away
+    const ColRef kc = make_colref(*key);
+    return partition_perm(
+        ctx, n, n_splitters + 1,
+        [&](uint64_t *ids, uint32_t *idx) {
+            hipLaunchKernelGGL(k_range_ids, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, kc, n,
+                               sp.as<int64_t>(), n_splitters, ascending ? 1 : 0, ids, idx);
+        },
+        "range_partition", counts, out_perm);
+}
+
+extern "C" int qeh_scatter(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out) {
+    if (!ctx || !col || !indices || !out) return fail(QEH_E_INVALID, "qeh_scatter: bad argument");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*col, "scatter"));
+    if (indices->dtype != QEH_DT_UINT32 || indices->validity) return fail(QEH_E_INVALID, "scatter: indices must be non-null UInt32");
+    if (indices->length != col->length) return fail(QEH_E_INVALID, "scatter: indices and column lengths differ");
+    if (col->validity && col->null_count != 0) return fail(QEH_E_UNSUPPORTED, "scatter: nullable columns");
+    int w = 0;
+    switch (col->dtype) {
+        case QEH_DT_INT64: case QEH_DT_FLOAT64: w = 8; break;
+        case QEH_DT_INT32: case QEH_DT_FLOAT32: case QEH_DT_UINT32: w = 4; break;
+        default: return fail(QEH_E_UNSUPPORTED, "scatter: fixed-width numeric columns only");
+    }
+    const int64_t m = col->length;
+    QEH_TRY(alloc_column(ctx, col->dtype, m, false, out));
+    if (m > 0) {
+        KernelTimer kt(ctx, "scatter");
+        const uint32_t *idx = (const uint32_t *)indices->values + indices->offset;
+        const int grid = grid_for(ctx, m, kBlock * 8, 8);
+        if (w == 8)
+            hipLaunchKernelGGL(k_scatter<uint64_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                               (const uint64_t *)col->values + col->offset, idx, m, (uint64_t *)out->values);
+        else
+            hipLaunchKernelGGL(k_scatter<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                               (const uint32_t *)col->values + col->offset, idx, m, (uint32_t *)out->values);
+    }
+    QEH_HIP(hipGetLastError());
     QEH_HIP(hipStreamSynchronize(ctx->stream));
     return QEH_OK;
 }

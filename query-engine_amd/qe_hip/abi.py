@@ -84,6 +84,8 @@ SIGNATURES = {
     "qeh_take": (I, [P, COLP, COLP, COLP]),
     "qeh_row_number": (I, [P, COLP, I, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_hash_partition": (I, [P, COLP, I, C.POINTER(I64), COLP]),
+    "qeh_range_partition": (I, [P, COLP, I, C.POINTER(I64), I, C.POINTER(I64), COLP]),
+    "qeh_scatter": (I, [P, COLP, COLP, COLP]),
     "qeh_validity_to_bytes": (I, [P, COLP, P]),
     "qeh_bytes_to_validity": (I, [P, P, I64, P]),
     "qeh_execute_plan": (I, [P, P, P, I, P, P, C.POINTER(I64)]),  # include/qeh_plan.h; typed in plan.py

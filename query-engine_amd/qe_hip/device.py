@@ -352,6 +352,34 @@ class Context:
         abi.check(self.lib.qeh_hash_partition(self.h, C.byref(key.c), n_parts, counts, C.byref(out)))
         return np.array(counts[:], dtype=np.int64), self._wrap(out)
 
+    def range_partition(self, key: DeviceColumn, splitters, ascending: bool = True):
+        """Partition ids by order-key ranges (qeh_range_partition); splitters
+        are ascending order keys (see ``order_keys``)."""
+        sp = np.ascontiguousarray(np.asarray(splitters, dtype=np.int64))
+        n_parts = len(sp) + 1
+        counts = (C.c_int64 * n_parts)()
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_range_partition(self.h, C.byref(key.c), 1 if ascending else 0,
+                                               sp.ctypes.data_as(C.POINTER(C.c_int64)), len(sp), counts,
+                                               C.byref(out)))
+        return np.array(counts[:], dtype=np.int64), self._wrap(out)
+
+    def scatter(self, col: DeviceColumn, perm: DeviceColumn) -> DeviceColumn:
+        """out[perm[i]] = col[i] (qeh_scatter)."""
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_scatter(self.h, C.byref(col.c), C.byref(perm.c), C.byref(out)))
+        return self._wrap(out)
+
+
+def order_keys(values: np.ndarray) -> np.ndarray:
+    """Host twin of the device order key used by qeh_range_partition: ints as
+    Int64, floats widened to Float64 and mapped to IEEE totalOrder."""
+    v = np.asarray(values)
+    if v.dtype.kind == "f":
+        b = v.astype(np.float64).view(np.int64)
+        return b ^ ((b >> 63).astype(np.uint64) >> np.uint64(1)).astype(np.int64)
+    return v.astype(np.int64)
+
 
 def agg(func: int, column: int) -> Tuple[int, int]:
     return (func, column)

@@ -12,6 +12,9 @@ stages run for real:
   * hash_join_inner: shuffle both sides by the join key, local device join.
   * group_by: local partial aggregate -> shuffle partial states by the first
     group key -> final aggregate on the owning rank (partial/final stages).
+  * row_number: hash shuffle by the partition key, local ROW_NUMBER, reverse
+    all-to-all, scatter back into input order.
+  * sort: sample splitters, range partition, exchange, stable local sort.
   * join_filter_aggregate_broadcast (the BASELINE metric path): the dimension
     is replicated (broadcast join), every rank runs the fused kernel on its
     fact shard, then the partial states are shuffled by group key and merged.
@@ -28,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import abi
-from .device import NP_OF, Context, DeviceColumn
+from .device import NP_OF, Context, DeviceColumn, order_keys
 from .expr import AggregateFunction as AF
 
 TORCH_OF = {abi.DT_INT64: torch.int64, abi.DT_FLOAT64: torch.float64, abi.DT_INT32: torch.int32,
@@ -110,23 +113,28 @@ class DistributedExecutor:
             self.ctx.sync()
 
     # ---- shuffle -----------------------------------------------------------------
-    def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
-        """Route every row to rank hash(key) % world (partition.rs:151-212)."""
-        counts, perm = self.ctx.hash_partition(key, self.world)
-        taken = [self.ctx.take(c, perm) for c in cols]
+    def _exchange_columns(self, cols: Sequence[DeviceColumn], counts) -> Tuple[List[DeviceColumn], List[int]]:
+        """All-to-all of partition-major columns: counts[r] leading rows go to rank r."""
         payloads, shape = [], []
-        for t in taken:
+        for t in cols:
             ts = self._to_tensors(t)
             shape.append((t.dtype, len(ts) == 2))
             payloads.extend(ts)
         self._sync()
-        _, recv = exchange(torch.tensor(counts, dtype=torch.int64, device=self.device), payloads, self.group)
+        recv_counts, recv = exchange(torch.tensor(np.asarray(counts), dtype=torch.int64, device=self.device), payloads,
+                                     self.group)
         out, i = [], 0
         for dtype, nullable in shape:
             vals = recv[i]
             valid = recv[i + 1] if nullable else None
             i += 2 if nullable else 1
             out.append(self._from_tensors(dtype, vals, valid))
+        return out, [int(x) for x in recv_counts.tolist()]
+
+    def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
+        """Route every row to rank hash(key) % world (partition.rs:151-212)."""
+        counts, perm = self.ctx.hash_partition(key, self.world)
+        out, _ = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
         return out
 
     # ---- operators -----------------------------------------------------------------
@@ -166,6 +174,47 @@ class DistributedExecutor:
         pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
                                                     build_group_keys, aggs)
         return self._final(pk, pa_, aggs)
+
+    def row_number(self, part_keys: Sequence[DeviceColumn], order_keys: Sequence[DeviceColumn],
+                   ascending: Sequence[bool]) -> DeviceColumn:
+        """ROW_NUMBER() OVER (PARTITION BY .. ORDER BY ..) over rank-sharded rows
+        (global input order = rank-major).  Rows are hash-shuffled by the first
+        partition key, so each PARTITION BY group lives on one rank and is numbered
+        there (received order = source-rank-major, stable within a source, i.e. the
+        global input order that breaks ties); the numbers go back by the reverse
+        all-to-all and are scattered into this rank's input order."""
+        counts, perm = self.ctx.hash_partition(part_keys[0], self.world)
+        cols = list(part_keys) + list(order_keys)
+        recv, recv_counts = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
+        npk = len(part_keys)
+        rn = self.ctx.row_number(recv[:npk], recv[npk:], list(ascending))
+        back, _ = self._exchange_columns([rn], recv_counts)  # reverse: return what each source sent
+        return self.ctx.scatter(back[0], perm)
+
+    def sort(self, cols: Sequence[DeviceColumn], key_idx: Sequence[int], ascending: Sequence[bool],
+             samples_per_rank: int = 4096) -> List[DeviceColumn]:
+        """ORDER BY over rank-sharded rows: range-partition on the first sort key
+        with splitters from an all-gathered sample, then a stable local sort.  The
+        global result is rank 0's rows, then rank 1's, ...  Equal first keys share a
+        rank and arrive source-rank-major, so the result is stable."""
+        k0 = cols[key_idx[0]]
+        n = len(k0)
+        sample = np.empty(0, np.int64)
+        if n:
+            idx = np.unique(np.linspace(0, n - 1, min(n, samples_per_rank)).astype(np.uint32))
+            sv, sm = self.ctx.take(k0, self.ctx.upload(idx)).to_numpy()
+            sample = order_keys(sv if sm is None else sv[sm])
+        objs = [None] * self.world
+        dist.all_gather_object(objs, sample, group=self.group)
+        allk = np.sort(np.concatenate(objs)) if objs else np.empty(0, np.int64)
+        if len(allk):
+            splitters = allk[[(i + 1) * len(allk) // self.world for i in range(self.world - 1)]]
+        else:
+            splitters = np.zeros(self.world - 1, np.int64)
+        counts, perm = self.ctx.range_partition(k0, splitters, bool(ascending[0]))
+        recv, _ = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
+        p = self.ctx.sort_indices([recv[i] for i in key_idx], list(ascending))
+        return [self.ctx.take(c, p) for c in recv]
 
     def gather_to_root(self, cols: Sequence[DeviceColumn]) -> Optional[List[Tuple[np.ndarray, Optional[np.ndarray]]]]:
         """Collect every rank's result rows on rank 0 (host arrays)."""

@@ -103,6 +103,40 @@ def mode_gpu(rank, world):
         wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred, ob.HostCol(dkk),
                                               [ob.HostCol(dg)], [(AF.Sum, 2), (AF.Count, 2)])
         assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    # --- distributed ROW_NUMBER (hash shuffle by partition key, reverse exchange, scatter)
+    def win(r):
+        g = np.random.default_rng(70 + r)
+        kk = g.integers(0, 200, 25_000).astype(np.int64)
+        km = g.random(25_000) > 0.05
+        vv = g.integers(-30, 30, 25_000).astype(np.int64)
+        return kk, km, vv
+    wk_, wm_, wv_ = win(rank)
+    rn = dx.row_number([ctx.upload(wk_, wm_)], [ctx.upload(wv_)], [False])
+    res = dx.gather_to_root([rn])
+    if rank == 0:
+        K = np.concatenate([win(r)[0] for r in range(world)])
+        M = np.concatenate([win(r)[1] for r in range(world)])
+        V = np.concatenate([win(r)[2] for r in range(world)])
+        want = ob.row_number([ob.HostCol(K, M)], [ob.HostCol(V)], [False])
+        assert np.array_equal(res[0][0], want)
+    # --- distributed ORDER BY (sampled range partition, stable local sort)
+    def srt(r):
+        g = np.random.default_rng(90 + r)
+        a = np.round(g.standard_normal(30_000), 1)
+        am = g.random(30_000) > 0.1
+        b = g.integers(0, 5, 30_000).astype(np.int64)
+        return a, am, b
+    for asc in ([True, False], [False, True]):
+        a_, am_, b_ = srt(rank)
+        rid = (np.arange(30_000) + rank * 30_000).astype(np.int64)  # global input position
+        out = dx.sort([ctx.upload(a_, am_), ctx.upload(b_), ctx.upload(rid)], [0, 1], asc)
+        res = dx.gather_to_root(out)
+        if rank == 0:
+            A = np.concatenate([srt(r)[0] for r in range(world)])
+            AM = np.concatenate([srt(r)[1] for r in range(world)])
+            B = np.concatenate([srt(r)[2] for r in range(world)])
+            perm = ob.sort_indices([ob.HostCol(A, AM), ob.HostCol(B)], asc)
+            assert np.array_equal(res[2][0], perm.astype(np.int64))
     ctx.close()
 
 

@@ -184,3 +184,37 @@ def test_row_number_full_range_nullable_partition_key(ctx):
     rn = ctx.row_number([ctx.upload(k, kv)], [ctx.upload(v)], [True]).to_numpy()[0]
     want = ob.row_number([ob.HostCol(k, kv)], [ob.HostCol(v)], [True])
     assert np.array_equal(rn, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("asc", [True, False])
+def test_range_partition_orders_partitions(ctx, asc):
+    from qe_hip.device import order_keys
+    r = np.random.default_rng(23)
+    n = 100_000
+    v = np.round(r.standard_normal(n), 2)
+    m = r.random(n) > 0.05
+    split = np.sort(order_keys(np.array([-1.0, -0.0, 0.5, 1.25])))
+    counts, perm = ctx.range_partition(ctx.upload(v, m), split, asc)
+    p = perm.to_numpy()[0]
+    assert counts.sum() == n and np.array_equal(np.sort(p), np.arange(n, dtype=np.uint32))
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    ok = order_keys(v)
+    want_part = np.where(m, (split[None, :] < ok[:, None]).sum(1) if asc else (split[None, :] > ok[:, None]).sum(1), 0)
+    for q in range(len(counts)):
+        rows = p[offs[q]:offs[q + 1]]
+        assert np.all(np.diff(rows.astype(np.int64)) > 0)
+        assert np.all(want_part[rows] == q)
+
+
+@pytest.mark.gpu
+def test_scatter_inverts_take(ctx):
+    r = np.random.default_rng(24)
+    n = 300_001
+    v = r.integers(-(2 ** 62), 2 ** 62, n).astype(np.int64)
+    perm = r.permutation(n).astype(np.uint32)
+    dp = ctx.upload(perm)
+    back = ctx.scatter(ctx.take(ctx.upload(v), dp), dp).to_numpy()[0]
+    assert np.array_equal(back, v)
+    f = r.random(n).astype(np.float32)
+    assert np.array_equal(ctx.scatter(ctx.take(ctx.upload(f), dp), dp).to_numpy()[0], f)
