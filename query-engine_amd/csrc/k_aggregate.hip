@@ -187,6 +187,47 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
     return false;
 }
 
+// One 2048-row tile of the fast-path columns: every load (16-B pairs) issued
+// before the term predicate is evaluated.  Lane rows: base + j*128 + {0,1}.
+template <int NTERMS, int NACOL, bool NT>
+struct FastTile {
+    v2i64 key[kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
+    uint32_t sel;
+    __device__ __forceinline__ void load(const FastIn &in, const PredTerms &terms, int64_t base) {
+        v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
+#pragma unroll
+        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
+#pragma unroll
+        for (int c = 0; c < NACOL; ++c)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
+        sel = (1u << kFastR) - 1u;
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i) {
+            const PredTerm pt = terms.t[i];
+            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+            uint32_t tr = 0;
+#pragma unroll
+            for (int r = 0; r < kFastR; ++r) {
+                int64_t v = tc[i][r >> 1][r & 1];
+                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
+                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            }
+            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
+            else sel &= tr;
+        }
+    }
+    __device__ __forceinline__ int64_t k(int r) const { return key[r >> 1][r & 1]; }
+    // value of row r for aggregate input slot `cs` (0 or 1)
+    __device__ __forceinline__ int64_t a(int cs, int r) const {
+        return (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
+    }
+};
+
 template <int NTERMS, int NACOL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, HashTable t,
                                                           int64_t G, int64_t n_tiles, uint64_t *__restrict__ gstates) {
@@ -205,40 +246,16 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t base = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
-        v2i64 key[kFastPairs], tc[NTERMS > 0 ? NTERMS : 1][kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
-#pragma unroll
-        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
-#pragma unroll
-        for (int c = 0; c < NACOL; ++c)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
-
-        uint32_t sel = (1u << kFastR) - 1u;
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i) {
-            const PredTerm pt = terms.t[i];
-            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
-            uint32_t tr = 0;
-#pragma unroll
-            for (int r = 0; r < kFastR; ++r) {
-                int64_t v = tc[i][r >> 1][r & 1];
-                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
-                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
-            }
-            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
-            else sel &= tr;
-        }
+        FastTile<NTERMS, NACOL, NT> ft;
+        ft.load(in, terms, base);
+        const uint32_t sel = ft.sel;
         uint32_t gid[kFastR];
         uint32_t hit = 0;
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
             gid[r] = 0;
             if ((sel >> r) & 1)
-                if (probe_unique(t, key[r >> 1][r & 1], gid[r])) hit |= 1u << r;
+                if (probe_unique(t, ft.k(r), gid[r])) hit |= 1u << r;
         }
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
@@ -248,9 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
             for (int a = 0; a < specs.n; ++a) {
                 const AggSpec sp = specs.a[a];
                 if (sp.kind == AK_COUNT) continue;
-                const int cs = in.agg_colslot[a];
-                int64_t x = (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
-                x = agg_input(sp.kind, sp.in_type, x);
+                const int64_t x = agg_input(sp.kind, sp.in_type, ft.a(in.agg_colslot[a], r));
                 agg_apply<true>(sp.kind, &lds[(int64_t)sp.val_slot * G + g], x);
             }
         }
@@ -309,39 +324,16 @@ __global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms 
         if (threadIdx.x < kParts) cnt[threadIdx.x] = 0;
         __syncthreads();
         const int64_t b0 = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
-        v2i64 key[kFastPairs], tc[NTERMS > 0 ? NTERMS : 1][kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
-#pragma unroll
-        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + b0 + j * 128);
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + b0 + j * 128);
-#pragma unroll
-        for (int c = 0; c < NACOL; ++c)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + b0 + j * 128);
-        uint32_t sel = (1u << kFastR) - 1u;
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i) {
-            const PredTerm pt = terms.t[i];
-            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
-            uint32_t tr = 0;
-#pragma unroll
-            for (int r = 0; r < kFastR; ++r) {
-                int64_t v = tc[i][r >> 1][r & 1];
-                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
-                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
-            }
-            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
-            else sel &= tr;
-        }
+        FastTile<NTERMS, NACOL, NT> ft;
+        ft.load(in, terms, b0);
+        uint32_t sel = ft.sel;
         uint32_t part[kFastR], pos[kFastR];
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
             part[r] = 0;
             pos[r] = 0;
             if (!((sel >> r) & 1)) continue;
-            const int64_t k = key[r >> 1][r & 1];
+            const int64_t k = ft.k(r);
             if (k < t.kmin || k > t.kmax) {  // cannot match: drop here
                 sel &= ~(1u << r);
                 continue;
@@ -375,10 +367,10 @@ __global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms 
         for (int r = 0; r < kFastR; ++r) {
             if (!((sel >> r) & 1)) continue;
             const uint32_t s = lofs[part[r]] + pos[r];
-            const int64_t k = key[r >> 1][r & 1];
+            const int64_t k = ft.k(r);
             skey[s] = KEY64 ? (KeyT)k : (KeyT)((uint64_t)k - (uint64_t)t.kmin);
 #pragma unroll
-            for (int c = 0; c < NACOL; ++c) sval[c][s] = ac[c][r >> 1][r & 1];
+            for (int c = 0; c < NACOL; ++c) sval[c][s] = ft.ac[c][r >> 1][r & 1];
         }
         __syncthreads();
         // ... and copy them out: consecutive lanes write consecutive slots, so
@@ -437,8 +429,9 @@ __global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn
                     const uint64_t i = i0 + (uint64_t)u * kBlock;
                     if (i < e) live |= 1u << u;
                     const uint64_t ii = i < e ? i : b;
-                    kk[u] = KEY64 ? ((const int64_t *)pb.key[p])[ii]
-                                  : (int64_t)((uint64_t)t.kmin + ((const uint32_t *)pb.key[p])[ii]);
+                    kk[u] = KEY64 ? __builtin_nontemporal_load(&((const int64_t *)pb.key[p])[ii])
+                                  : (int64_t)((uint64_t)t.kmin +
+                                              __builtin_nontemporal_load(&((const uint32_t *)pb.key[p])[ii]));
 #pragma unroll
                     for (int c = 0; c < NACOL; ++c) vv[c][u] = __builtin_nontemporal_load(&pb.val[c][p][ii]);
                 }
@@ -603,6 +596,92 @@ __global__ __launch_bounds__(kBlock) void k_groupby_lds(ColSet cols, int64_t n, 
                 const uint64_t c = lst[(int64_t)sp.cnt_slot * lcap + i];
                 if (c) atomicAdd((unsigned long long *)&gstates[(int64_t)sp.cnt_slot * G + g], (unsigned long long)c);
             }
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * lcap + i]);
+        }
+    }
+}
+
+// Fast single-key GROUP BY: the FastTile loads of k_join_agg_fast with the
+// group slot found in a per-workgroup LDS hash of keys (linear probing, CAS
+// insert); keys that do not fit the LDS table (or INT64_MIN, the empty
+// marker) update the HBM table's states directly with global atomics.
+template <int NTERMS, int NACOL, bool NT>
+__global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, GTable gt,
+                                                           int lcap, int64_t G, int64_t n_tiles,
+                                                           uint64_t *__restrict__ gstates) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    int64_t *lkeys = (int64_t *)lds;
+    uint64_t *lst = lds + lcap;  // [n_slots][lcap]
+    for (int i = threadIdx.x; i < lcap; i += blockDim.x) lkeys[i] = kEmptyKey;
+    for (int64_t i = threadIdx.x; i < (int64_t)specs.n_slots * lcap; i += blockDim.x) lst[i] = 0;
+    __syncthreads();
+    for (int a = 0; a < specs.n; ++a) {
+        const AggSpec sp = specs.a[a];
+        if (sp.kind == AK_MIN || sp.kind == AK_MAX)
+            for (int i = threadIdx.x; i < lcap; i += blockDim.x) lst[(int64_t)sp.val_slot * lcap + i] = (uint64_t)agg_init_value(sp.kind);
+    }
+    __syncthreads();
+    const int64_t gcap = (int64_t)gt.mask + 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t base = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
+        FastTile<NTERMS, NACOL, NT> ft;
+        ft.load(in, terms, base);
+        const uint32_t sel = ft.sel;
+        int slot[kFastR];
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            slot[r] = -1;
+            const int64_t key = ft.k(r);
+            if (!((sel >> r) & 1) || key == kEmptyKey) continue;
+            int h = (int)(hash64((uint64_t)key) & (uint64_t)(lcap - 1));
+            for (int p = 0; p < 32; ++p) {
+                const int64_t cur = lkeys[h];
+                if (cur == key) { slot[r] = h; break; }
+                if (cur == kEmptyKey) {
+                    const unsigned long long old = atomicCAS((unsigned long long *)&lkeys[h], (unsigned long long)kEmptyKey,
+                                                             (unsigned long long)key);
+                    if ((long long)old == kEmptyKey || (long long)old == key) { slot[r] = h; break; }
+                }
+                h = (h + 1) & (lcap - 1);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            if (!((sel >> r) & 1)) continue;
+            if (slot[r] >= 0) {
+                const int h = slot[r];
+                atomicAdd((unsigned long long *)&lst[h], 1ull);
+                for (int a = 0; a < specs.n; ++a) {
+                    const AggSpec sp = specs.a[a];
+                    if (sp.kind == AK_COUNT) continue;
+                    agg_apply<true>(sp.kind, &lst[(int64_t)sp.val_slot * lcap + h],
+                                    agg_input(sp.kind, sp.in_type, ft.a(in.agg_colslot[a], r)));
+                }
+            } else {
+                const int64_t key = ft.k(r);
+                const int64_t g = key == kEmptyKey ? gcap + 1 : gt_slot(gt, key);
+                if (g < 0) continue;  // overflow flagged; host regrows and reruns
+                atomicAdd((unsigned long long *)&gstates[g], 1ull);
+                for (int a = 0; a < specs.n; ++a) {
+                    const AggSpec sp = specs.a[a];
+                    if (sp.kind == AK_COUNT) continue;
+                    agg_apply<false>(sp.kind, &gstates[(int64_t)sp.val_slot * G + g],
+                                     agg_input(sp.kind, sp.in_type, ft.a(in.agg_colslot[a], r)));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < lcap; i += blockDim.x) {
+        const int64_t key = lkeys[i];
+        if (key == kEmptyKey) continue;
+        const int64_t g = gt_slot(gt, key);
+        if (g < 0) continue;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)lst[i]);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
             if (sp.kind != AK_COUNT)
                 agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * lcap + i]);
         }
@@ -810,14 +889,14 @@ static int fast_nt_mode() {
 // The fused probe's fast path: returns true when it launched (full tiles by
 // k_join_agg_fast, the ragged tail by the generic kernel).
 // Eligibility of the specialised probe kernels; fills the kernel's view.
-static bool fast_eligible(const ColSet &cols, const PredPlan &pp, const GidSource &src, const AggSpecs &specs,
-                          FastIn *inp, int *nterms_out, int *nacol_out) {
+// `key_col`: the column read as FastIn::key (join probe key or group key).
+static bool fast_cols_eligible(const ColSet &cols, const PredPlan &pp, int key_col, const AggSpecs &specs,
+                               FastIn *inp, int *nterms_out, int *nacol_out) {
     if (pp.mode == PM_PROG || (pp.mode == PM_TERMS && pp.terms.n > 2)) return false;
-    if (!src.jt.unique || (src.jt.kind != TK_DIRECT && src.jt.kind != TK_PACKED)) return false;
-    if (!fast_col_ok(cols.c[src.key_col]) || cols.c[src.key_col].dtype != QEH_DT_INT64) return false;
+    if (!fast_col_ok(cols.c[key_col])) return false;
     FastIn &in = *inp;
     in = FastIn{};
-    in.key = (const int64_t *)cols.c[src.key_col].values;
+    in.key = (const int64_t *)cols.c[key_col].values;
     const int nterms = pp.mode == PM_TERMS ? pp.terms.n : 0;
     for (int i = 0; i < nterms; ++i) {
         const ColRef &c = cols.c[pp.terms.t[i].col];
@@ -847,6 +926,13 @@ static bool fast_eligible(const ColSet &cols, const PredPlan &pp, const GidSourc
     *nterms_out = nterms;
     *nacol_out = nacol;
     return true;
+}
+
+static bool fast_eligible(const ColSet &cols, const PredPlan &pp, const GidSource &src, const AggSpecs &specs,
+                          FastIn *inp, int *nterms_out, int *nacol_out) {
+    if (!src.jt.unique || (src.jt.kind != TK_DIRECT && src.jt.kind != TK_PACKED)) return false;
+    if (cols.c[src.key_col].dtype != QEH_DT_INT64) return false;
+    return fast_cols_eligible(cols, pp, src.key_col, specs, inp, nterms_out, nacol_out);
 }
 
 static void launch_tail(qeh_ctx *ctx, const ColSet &cols, int64_t n, int64_t done, const PredPlan &pp,
@@ -974,6 +1060,54 @@ static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, con
     return 1;
 }
 
+// Fast single-key GROUP BY (k_group_agg_fast) over the full tiles, generic
+// LDS-hash kernel over the ragged tail.  False when not eligible.
+static bool lds_group_fast(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
+                           const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err) {
+    if (std::getenv("QEH_NO_FAST")) return false;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_cols_eligible(cols, pp, src.key_col, specs, &in, &nterms, &nacol)) return false;
+    int lcap = 2048;
+    while (lcap > 256 && (size_t)(1 + specs.n_slots) * lcap * 8 > 64 * 1024) lcap >>= 1;
+    const size_t shm = (size_t)(1 + specs.n_slots) * lcap * 8;
+    if (shm > 64 * 1024) return false;
+    const int64_t n_tiles = n / kFastTile;
+    if (n_tiles > 0) {
+        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / shm));
+        const int grid = grid_for(ctx, n_tiles * kFastTile, kFastTile, per_cu);
+        const bool nt = fast_nt_mode() == 1;
+#define QEH_GF(NTV, NAV, NTB)                                                                                       \
+    hipLaunchKernelGGL((k_group_agg_fast<NTV, NAV, NTB>), dim3(grid), dim3(kBlock), shm, ctx->stream, in, pp.terms, \
+                       specs, src.gt, lcap, G, n_tiles, states)
+#define QEH_GF_NA(NTV, NTB)                       \
+    if (nacol == 0) QEH_GF(NTV, 0, NTB);          \
+    else if (nacol == 1) QEH_GF(NTV, 1, NTB);     \
+    else QEH_GF(NTV, 2, NTB);
+#define QEH_GF_NT(NTB)                            \
+    if (nterms == 0) { QEH_GF_NA(0, NTB) }        \
+    else if (nterms == 1) { QEH_GF_NA(1, NTB) }   \
+    else { QEH_GF_NA(2, NTB) }
+        if (nt) { QEH_GF_NT(true) } else { QEH_GF_NT(false) }
+#undef QEH_GF_NT
+#undef QEH_GF_NA
+#undef QEH_GF
+    }
+    const int64_t done = n_tiles * kFastTile;
+    if (done < n) {
+        ColSet tail = cols;
+        for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);
+        const size_t tshm = (size_t)(1 + specs.n_slots) * src.lcap * 8;
+        if (pp.mode == PM_TERMS)
+            hipLaunchKernelGGL(k_groupby_lds<PM_TERMS>, dim3(1), dim3(kBlock), tshm, ctx->stream, tail, n - done, pp.terms,
+                               pp.prog, src.key_col, src, specs, G, states, err);
+        else
+            hipLaunchKernelGGL(k_groupby_lds<PM_NONE>, dim3(1), dim3(kBlock), tshm, ctx->stream, tail, n - done, pp.terms,
+                               pp.prog, src.key_col, src, specs, G, states, err);
+    }
+    return true;
+}
+
 constexpr int kRetryBigger = 100;  // internal: group table too small
 
 // Run the row-aggregation kernel and finalize into owned output columns.
@@ -1005,6 +1139,9 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
                                        lds_bytes, per_cu)))
                 launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
                                          states.as<uint64_t>(), errw.as<uint32_t>());
+        }
+        else if (gm == GM_LDSHASH && lds_group_fast(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(),
+                                                      errw.as<uint32_t>())) {
         }
         else if (gm == GM_LDSHASH) {
             const size_t shm = (size_t)(1 + specs.n_slots) * src.lcap * 8;
@@ -1221,7 +1358,7 @@ int hash_aggregate_filtered(qeh_ctx *ctx, const qeh_column *keys, int n_keys, co
         std::vector<qeh_column> all2 = all;
         all2.push_back(keys[0]);
         QEH_TRY(make_colset(all2.data(), (int)all2.size(), &cols2));
-        for (int attempt = 0;; ++attempt) {
+        for (;;) {
             const int64_t G = (int64_t)gcap + 2;
             DevBuf gkeys, ovf, iota, gvalid;
             QEH_TRY(gkeys.alloc(ctx, (size_t)G * 8));

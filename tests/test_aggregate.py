@@ -127,3 +127,28 @@ def test_more_aggregates_than_one_kernel_carries(ctx, keys):
     aggs = [(AF.Sum, 1), (AF.Count, 1), (AF.Avg, 1), (AF.Min, 1), (AF.Max, 1), (AF.Sum, 2), (AF.Min, 2),
             (AF.Max, 2), (AF.Count, 0), (AF.Avg, 2), (AF.Count, 3), (AF.Sum, 3)]
     run(ctx, cols, keys, aggs, float_aggs=(0, 2, 9))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("groups", [7, 1024, 5000, 300_000])
+def test_group_by_fast_path_no_nulls(ctx, groups):
+    """Non-null 8-byte columns take k_group_agg_fast (LDS key hash); >2048 keys
+    per workgroup spill to the HBM table; ragged tail through the generic kernel."""
+    r = np.random.default_rng(groups)
+    n = 2_000_003
+    key = r.integers(0, groups, n).astype(np.int64) * 7919 - 3
+    key[::50_000] = np.iinfo(np.int64).min
+    cols = [(key, None), (r.random(n), None), (r.integers(-(2 ** 40), 2 ** 40, n).astype(np.int64), None),
+            (r.integers(0, 100, n).astype(np.int64), None)]
+    aggs = [(AF.Sum, 1), (AF.Count, 1), (AF.Min, 2), (AF.Max, 2), (AF.Sum, 2)]
+    run(ctx, cols, [0], aggs, pred=binop(col(3), BinaryOp.Greater, lit(49)), float_aggs=(0,))
+    run(ctx, cols, [0], aggs[:3], float_aggs=(0,))
+
+
+@pytest.mark.gpu
+def test_group_by_fast_path_float_key(ctx):
+    r = np.random.default_rng(31)
+    n = 500_000
+    key = np.round(r.standard_normal(n), 1)
+    cols = [(key, None), (r.integers(-9, 9, n).astype(np.int64), None)]
+    run(ctx, cols, [0], [(AF.Sum, 1), (AF.Count, 1), (AF.Avg, 1)], float_aggs=(2,))
