@@ -70,8 +70,9 @@ __global__ void k_stats_init(KeyStats *s) {
 
 // encoded key of row perm[i] (or i) -> keys[i]; perm_out[i] = perm[i] (or i)
 // mode 0: value encoding (NULL -> 0, values biased by `bias`); mode 1: null flag only
+template <typename KeyT>
 __global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n, int64_t mn, int64_t mx, int asc,
-                         uint64_t bias, int mode, uint64_t *__restrict__ keys, uint32_t *__restrict__ perm_out) {
+                         uint64_t bias, int mode, KeyT *__restrict__ keys, uint32_t *__restrict__ perm_out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = perm ? perm[i] : i;
         uint64_t k = 0;
@@ -83,7 +84,7 @@ __global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n,
                 k = asc ? (uint64_t)x - (uint64_t)mn + bias : (uint64_t)mx - (uint64_t)x + bias;
             }
         }
-        keys[i] = k;
+        keys[i] = (KeyT)k;
         perm_out[i] = (uint32_t)r;
     }
 }
@@ -109,7 +110,8 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
     return peers;
 }
 
-__global__ __launch_bounds__(kBlock) void k_rs_hist(const uint64_t *__restrict__ keys, int64_t n, int64_t seg,
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k_rs_hist(const KeyT *__restrict__ keys, int64_t n, int64_t seg,
                                                     int shift, uint32_t *__restrict__ hist, int nblocks) {
     __shared__ uint32_t h[kRadix];
     h[threadIdx.x] = 0;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const uint64_t *__restrict__
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t c0 = lo; c0 < hi; c0 += kRsTile) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
-        uint64_t k[kRsIpt];
+        KeyT k[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
@@ -138,12 +140,13 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const uint64_t *__restrict__
 
 // Stable scatter: rank each tile by digit in registers/LDS, reorder it in LDS,
 // then write digit runs (≈ kRsTile/kRadix elements each) contiguously.
-__global__ __launch_bounds__(kBlock) void k_rs_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+template <typename KeyT>
+__global__ __launch_bounds__(kBlock) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                        int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
-                                                       int nblocks, uint64_t *__restrict__ keys_out,
+                                                       int nblocks, KeyT *__restrict__ keys_out,
                                                        uint32_t *__restrict__ vals_out) {
     constexpr int W = kBlock / 64;
-    __shared__ uint64_t s_keys[kRsTile];
+    __shared__ KeyT s_keys[kRsTile];
     __shared__ uint32_t s_vals[kRsTile];
     __shared__ uint32_t wcnt[W][kRadix];  // per-wave digit counts, then per-wave start inside the digit
     __shared__ uint32_t loc[kRadix];      // tile-local start of each digit
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const uint64_t *__restric
         for (int w = 0; w < W; ++w) wcnt[w][t] = 0;
         __syncthreads();
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
-        uint64_t k[kRsIpt];
+        KeyT k[kRsIpt];
         uint32_t v[kRsIpt], rk[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const uint64_t *__restric
         __syncthreads();
         const int cnt = (int)(hi - c0 < kRsTile ? hi - c0 : kRsTile);
         for (int p = t; p < cnt; p += kBlock) {
-            const uint64_t key = s_keys[p];
+            const KeyT key = s_keys[p];
             const uint32_t dg = (uint32_t)((key >> shift) & (kRadix - 1));
             const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
             keys_out[pos] = key;
@@ -221,10 +224,12 @@ struct RadixState {
     int cur = 0;
     int64_t n = 0;
     bool enc_injective = false;  // k[cur] encodes the last-sorted column one-to-one (no null-flag pass)
+    bool key32 = false;          // k[] currently holds 32-bit keys (column range fits 32 bits)
 };
 
 // Stable LSD passes over the low `bits` of the encoded keys in rs.
-static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
+template <typename KeyT>
+static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
     const int64_t n = rs.n;
     if (n <= 1 || bits <= 0) return QEH_OK;
     const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsTile - 1) / kRsTile, 1), (int64_t)ctx->props.multiProcessorCount * 4);
@@ -235,17 +240,22 @@ static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
     for (int shift = 0; shift < bits; shift += kRadixBits) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = rs.cur;
-        hipLaunchKernelGGL(k_rs_hist, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<uint64_t>(), n, seg, shift,
+        hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
                            hist.as<uint32_t>(), nblocks);
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
-        hipLaunchKernelGGL(k_rs_scatter, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<uint64_t>(),
-                           rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<uint64_t>(),
+        hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<KeyT>(),
+                           rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
                            rs.v[1 - c].as<uint32_t>());
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
     return QEH_OK;
+}
+
+// Stable LSD passes over the low `bits` of the encoded keys in rs.
+static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
+    return rs.key32 ? radix_passes_t<uint32_t>(ctx, rs, bits) : radix_passes_t<uint64_t>(ctx, rs, bits);
 }
 
 static int bit_length(uint64_t x) {
@@ -262,11 +272,11 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
     DevBuf st;
     QEH_TRY(st.alloc(ctx, sizeof(KeyStats)));
     KeyStats ks{};
-    const uint32_t *perm = first ? nullptr : rs.v[rs.cur].as<uint32_t>();
     {
         KernelTimer kt(ctx, "sort_encode");
         hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, st.as<KeyStats>());
-        hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, c, perm, n,
+        // min/max do not depend on row order: read the column directly, not through the permutation
+        hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, c, nullptr, n,
                            st.as<KeyStats>());
     }
     QEH_HIP(hipGetLastError());
@@ -287,14 +297,21 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
     for (int pass = 0; pass < (null_pass ? 2 : 1); ++pass) {
         const uint32_t *pm = (first && pass == 0) ? nullptr : rs.v[rs.cur].as<uint32_t>();
         const int o = 1 - rs.cur;  // encode into the spare buffers, then swap
+        const int pbits = pass == 0 ? bits : 1;
+        rs.key32 = pbits <= 32;  // narrow keys halve the key traffic of every pass
         {
             KernelTimer kt(ctx, "sort_encode");
-            hipLaunchKernelGGL(k_encode, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, c, pm, n,
-                               ks.mn, ks.mx, asc ? 1 : 0, bias, pass, rs.k[o].as<uint64_t>(), rs.v[o].as<uint32_t>());
+            const int g = grid_for(ctx, n, kBlock * 8, 8);
+            if (rs.key32)
+                hipLaunchKernelGGL(k_encode<uint32_t>, dim3(g), dim3(kBlock), 0, ctx->stream, c, pm, n, ks.mn, ks.mx,
+                                   asc ? 1 : 0, bias, pass, rs.k[o].as<uint32_t>(), rs.v[o].as<uint32_t>());
+            else
+                hipLaunchKernelGGL(k_encode<uint64_t>, dim3(g), dim3(kBlock), 0, ctx->stream, c, pm, n, ks.mn, ks.mx,
+                                   asc ? 1 : 0, bias, pass, rs.k[o].as<uint64_t>(), rs.v[o].as<uint32_t>());
         }
         QEH_HIP(hipGetLastError());
         rs.cur = o;
-        QEH_TRY(radix_passes(ctx, rs, pass == 0 ? bits : 1));
+        QEH_TRY(radix_passes(ctx, rs, pbits));
     }
     rs.enc_injective = !null_pass;
     return QEH_OK;
@@ -348,7 +365,8 @@ __global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, in
 
 // single partition key: compare the sorted encodings (coalesced) instead of
 // gathering the key column through the permutation
-__global__ void k_part_flags_enc(const uint64_t *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags) {
+template <typename KeyT>
+__global__ void k_part_flags_enc(const KeyT *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         flags[i] = i == 0 || enc[i] != enc[i - 1];
 }
@@ -503,9 +521,12 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     const int grid = grid_for(ctx, n, kBlock * 8, 8);
     {
         KernelTimer kt(ctx, "row_number");
-        if (n_part == 1 && rs.enc_injective)
-            hipLaunchKernelGGL(k_part_flags_enc, dim3(grid), dim3(kBlock), 0, ctx->stream, rs.k[rs.cur].as<uint64_t>(), n,
-                               flags.as<uint32_t>());
+        if (n_part == 1 && rs.enc_injective && rs.key32)
+            hipLaunchKernelGGL(k_part_flags_enc<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                               rs.k[rs.cur].as<uint32_t>(), n, flags.as<uint32_t>());
+        else if (n_part == 1 && rs.enc_injective)
+            hipLaunchKernelGGL(k_part_flags_enc<uint64_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                               rs.k[rs.cur].as<uint64_t>(), n, flags.as<uint32_t>());
         else
             hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
     }
