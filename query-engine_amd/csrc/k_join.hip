@@ -15,7 +15,9 @@
 // requested payload columns (late materialisation).  Build keys with
 // duplicates take one extra counting pass to size the output.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -132,6 +134,154 @@ __global__ void k_join_count(ColRef key, int64_t n, HashTable t, unsigned long l
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(total, (unsigned long long)c);
 }
 
+// ---- fused materialising probe (unique DIRECT build, non-null 8-byte columns) ----------
+// The build side's payload columns are embedded in a key-offset-indexed record
+// array (one random 8*NB-byte read per match instead of table -> row -> column)
+// and key presence in a bitmap that stays L2-resident.  One pass per probe
+// tile: 16-byte loads of key + probe payloads, presence test, record loads,
+// ballot ranks, decoupled look-back for the output offset, then every output
+// column leaves through LDS as one contiguous, coalesced run.
+constexpr int kMatMaxP = 3, kMatMaxB = 3;
+constexpr int kMPairs = 4, kMR = 2 * kMPairs, kMTile = kBlock * kMR;
+typedef long long v2i64j __attribute__((ext_vector_type(2)));
+
+struct MatIn {
+    const int64_t *key;
+    const int64_t *pcol[kMatMaxP];
+    int64_t *pout[kMatMaxP];
+    int64_t *bout[kMatMaxB];
+    const int64_t *rec;        // [range][NB]
+    const uint32_t *present;   // bit per key offset
+    int64_t kmin, kmax;
+    int64_t n;
+};
+
+__global__ void k_embed_build(ColRef key, int64_t n, int64_t kmin, const int64_t *b0, const int64_t *b1,
+                              const int64_t *b2, int nb, int64_t *__restrict__ rec, uint32_t *__restrict__ present) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        const uint64_t off = (uint64_t)load_i64(key, i) - (uint64_t)kmin;
+        atomicOr(&present[off >> 5], 1u << (off & 31));
+        rec[off * nb] = b0[i];
+        if (nb > 1) rec[off * nb + 1] = b1[i];
+        if (nb > 2) rec[off * nb + 2] = b2[i];
+    }
+}
+
+__device__ __forceinline__ v2i64j ld_pair(const int64_t *p, int64_t row, int64_t n) {
+    if (row + 1 < n) return __builtin_nontemporal_load((const v2i64j *)(p + row));
+    v2i64j v = {0, 0};
+    if (row < n) v[0] = p[row];
+    return v;
+}
+
+template <int NP, int NB>
+__global__ __launch_bounds__(kBlock) void k_join_mat(MatIn in, int64_t n_tiles, uint64_t *__restrict__ status,
+                                                     unsigned long long *__restrict__ ticket, uint32_t *__restrict__ errp,
+                                                     uint64_t *__restrict__ total_out) {
+    constexpr int W = kBlock / 64;
+    __shared__ int64_t stage[kMTile];
+    __shared__ uint32_t cnt[W][kMPairs], offs[W][kMPairs];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_total;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1ull);
+        __syncthreads();
+        const int64_t tile = s_tile;
+        if (tile >= n_tiles) break;
+        const int64_t base = tile * kMTile + (int64_t)wave * (64 * kMR) + 2 * lane;
+        v2i64j key[kMPairs], pv[NP > 0 ? NP : 1][kMPairs];
+#pragma unroll
+        for (int j = 0; j < kMPairs; ++j) key[j] = ld_pair(in.key, base + j * 128, in.n);
+#pragma unroll
+        for (int c = 0; c < NP; ++c)
+#pragma unroll
+            for (int j = 0; j < kMPairs; ++j) pv[c][j] = ld_pair(in.pcol[c], base + j * 128, in.n);
+        uint32_t hit = 0;
+        uint64_t off[kMR];
+#pragma unroll
+        for (int r = 0; r < kMR; ++r) {
+            const int64_t row = base + (r >> 1) * 128 + (r & 1);
+            const int64_t k = key[r >> 1][r & 1];
+            off[r] = (uint64_t)k - (uint64_t)in.kmin;
+            if (row < in.n && k >= in.kmin && k <= in.kmax && ((in.present[off[r] >> 5] >> (off[r] & 31)) & 1))
+                hit |= 1u << r;
+        }
+        int64_t bv[NB][kMR];
+#pragma unroll
+        for (int r = 0; r < kMR; ++r)
+#pragma unroll
+            for (int c = 0; c < NB; ++c) bv[c][r] = ((hit >> r) & 1) ? in.rec[off[r] * NB + c] : 0;
+        // ranks in tile order (wave, pair j, lane, element)
+        uint32_t rank[kMR];
+#pragma unroll
+        for (int j = 0; j < kMPairs; ++j) {
+            const uint64_t m0 = __ballot((hit >> (2 * j)) & 1), m1 = __ballot((hit >> (2 * j + 1)) & 1);
+            const uint32_t below = mbcnt(m0) + mbcnt(m1);
+            rank[2 * j] = below;
+            rank[2 * j + 1] = below + ((hit >> (2 * j)) & 1);
+            if (lane == 0) cnt[wave][j] = (uint32_t)(popc64(m0) + popc64(m1));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int w = 0; w < W; ++w)
+                for (int j = 0; j < kMPairs; ++j) {
+                    offs[w][j] = acc;
+                    acc += cnt[w][j];
+                }
+            s_total = acc;
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        if (wave == 0) {
+            uint64_t prefix = 0;
+            if (tile == 0) {
+                if (lane == 0) st_agent(&status[0], kFlagIncl | total);
+            } else {
+                if (lane == 0) st_agent(&status[tile], kFlagAgg | total);
+                prefix = lookback(status, tile, total, errp);
+                if (lane == 0) st_agent(&status[tile], kFlagIncl | (prefix + total));
+            }
+            if (lane == 0) {
+                s_prefix = prefix;
+                if (tile == n_tiles - 1) *total_out = prefix + total;
+            }
+        }
+        __syncthreads();
+        const uint64_t prefix = s_prefix;
+        // every output column: scatter into LDS by local rank, then one coalesced run
+        // (columns expanded at compile time so the register arrays stay in VGPRs)
+        auto emit = [&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            if constexpr (c < NP + NB) {
+#pragma unroll
+                for (int r = 0; r < kMR; ++r) {
+                    if (!((hit >> r) & 1)) continue;
+                    int64_t v;
+                    if constexpr (c < NP) v = pv[c][r >> 1][r & 1];
+                    else v = bv[c - NP][r];
+                    stage[offs[wave][r >> 1] + rank[r]] = v;
+                }
+                __syncthreads();
+                int64_t *dst;
+                if constexpr (c < NP) dst = in.pout[c] + prefix;
+                else dst = in.bout[c - NP] + prefix;
+                for (uint32_t i = threadIdx.x; i < total; i += kBlock) __builtin_nontemporal_store(stage[i], &dst[i]);
+                __syncthreads();
+            }
+        };
+        emit(std::integral_constant<int, 0>{});
+        emit(std::integral_constant<int, 1>{});
+        emit(std::integral_constant<int, 2>{});
+        emit(std::integral_constant<int, 3>{});
+        emit(std::integral_constant<int, 4>{});
+        emit(std::integral_constant<int, 5>{});
+    }
+}
+
 int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt, DevBuf *probe_idx,
                  DevBuf *build_idx, int64_t *out_rows) {
     const int64_t n = probe_key.length;
@@ -180,6 +330,108 @@ int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt
     return QEH_OK;
 }
 
+static bool mat_col_ok(const qeh_column &c) {
+    return (c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_FLOAT64) && (!c.validity || c.null_count == 0) &&
+           (((uintptr_t)((const int64_t *)c.values + c.offset)) & 15) == 0;
+}
+
+constexpr int kNotEligible = -1;
+
+// Fused path of qeh_hash_join_inner; kNotEligible when the shapes do not fit.
+static int join_materialise_fused(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_column *probe_cols, int np,
+                                  const qeh_column &build_key, const qeh_column *build_cols, int nb, const BuiltTable &bt,
+                                  qeh_column *out_probe, qeh_column *out_build, int64_t *out_rows) {
+    if (std::getenv("QEH_NO_FUSED_JOIN")) return kNotEligible;
+    if (!bt.t.unique || bt.t.kind != TK_DIRECT || np > kMatMaxP || nb < 1 || nb > kMatMaxB) return kNotEligible;
+    if (!mat_col_ok(probe_key)) return kNotEligible;
+    for (int i = 0; i < np; ++i)
+        if (!mat_col_ok(probe_cols[i])) return kNotEligible;
+    for (int i = 0; i < nb; ++i)
+        if (!mat_col_ok(build_cols[i])) return kNotEligible;
+    const uint64_t range = bt.t.range;
+    if (range > (1ull << 31)) return kNotEligible;
+    const int64_t n = probe_key.length, nbuild = build_key.length;
+    DevBuf rec, present;
+    QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * nb, 1) * 8));
+    QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
+    QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+    auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
+    if (nbuild > 0) {
+        KernelTimer kt(ctx, "join_build");
+        hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                           make_colref(build_key), nbuild, bt.t.kmin, cptr(build_cols[0]),
+                           nb > 1 ? cptr(build_cols[1]) : nullptr, nb > 2 ? cptr(build_cols[2]) : nullptr, nb,
+                           rec.as<int64_t>(), present.as<uint32_t>());
+        QEH_HIP(hipGetLastError());
+    }
+    // outputs sized for every probe row (a unique build emits at most one row per probe row)
+    int made_p = 0, made_b = 0;
+    auto cleanup = [&]() {
+        for (int i = 0; i < made_p; ++i) qeh_column_release(ctx, &out_probe[i]);
+        for (int i = 0; i < made_b; ++i) qeh_column_release(ctx, &out_build[i]);
+    };
+    int s = QEH_OK;
+    for (int i = 0; i < np && s == QEH_OK; ++i)
+        if ((s = alloc_column(ctx, probe_cols[i].dtype, n, false, &out_probe[i])) == QEH_OK) ++made_p;
+    for (int i = 0; i < nb && s == QEH_OK; ++i)
+        if ((s = alloc_column(ctx, build_cols[i].dtype, n, false, &out_build[i])) == QEH_OK) ++made_b;
+    if (s != QEH_OK) {
+        cleanup();
+        return s;
+    }
+    uint64_t total = 0;
+    const int64_t n_tiles = (n + kMTile - 1) / kMTile;
+    if (n_tiles > 0) {
+        void *scr = nullptr;
+        s = scratch_zeroed(ctx, 64 + (size_t)n_tiles * 8, &scr);
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
+        MatIn in{};
+        in.key = cptr(probe_key);
+        for (int i = 0; i < np; ++i) {
+            in.pcol[i] = cptr(probe_cols[i]);
+            in.pout[i] = (int64_t *)out_probe[i].values;
+        }
+        for (int i = 0; i < nb; ++i) in.bout[i] = (int64_t *)out_build[i].values;
+        in.rec = rec.as<int64_t>();
+        in.present = present.as<uint32_t>();
+        in.kmin = bt.t.kmin;
+        in.kmax = bt.t.kmax;
+        in.n = n;
+        unsigned long long *ticket = (unsigned long long *)scr;
+        uint32_t *err = (uint32_t *)((char *)scr + 8);
+        uint64_t *tot = (uint64_t *)((char *)scr + 16);
+        uint64_t *status = (uint64_t *)((char *)scr + 64);
+        const int grid = grid_for(ctx, n, kMTile, 4);
+        {
+            KernelTimer kt(ctx, "join_probe");
+#define QEH_MAT(NPV, NBV) \
+    hipLaunchKernelGGL((k_join_mat<NPV, NBV>), dim3(grid), dim3(kBlock), 0, ctx->stream, in, n_tiles, status, ticket, err, tot)
+#define QEH_MAT_B(NPV)                     \
+    if (nb == 1) QEH_MAT(NPV, 1);          \
+    else if (nb == 2) QEH_MAT(NPV, 2);     \
+    else QEH_MAT(NPV, 3);
+            if (np == 0) { QEH_MAT_B(0) } else if (np == 1) { QEH_MAT_B(1) } else if (np == 2) { QEH_MAT_B(2) } else { QEH_MAT_B(3) }
+#undef QEH_MAT_B
+#undef QEH_MAT
+        }
+        uint64_t hdr[3];
+        s = hipGetLastError() == hipSuccess ? read_small(ctx, hdr, scr, 24) : fail(QEH_E_HIP, "join: probe launch failed");
+        if (s == QEH_OK) s = kernel_error_status((uint32_t)hdr[1], "hash join");
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
+        total = hdr[2];
+    }
+    for (int i = 0; i < np; ++i) out_probe[i].length = (int64_t)total;
+    for (int i = 0; i < nb; ++i) out_build[i].length = (int64_t)total;
+    *out_rows = (int64_t)total;
+    return QEH_OK;
+}
+
 }  // namespace qeh
 
 using namespace qeh;
@@ -199,6 +451,11 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
         if (build_cols[i].length != build_key->length) return fail(QEH_E_INVALID, "build columns have different lengths");
     BuiltTable bt;
     QEH_TRY(build_join_table(ctx, *build_key, nullptr, (uint64_t)std::max<int64_t>(build_key->length - 1, 0), &bt));
+    {
+        const int r = join_materialise_fused(ctx, *probe_key, probe_cols, n_probe_cols, *build_key, build_cols, n_build_cols,
+                                             bt, out_probe, out_build, out_rows);
+        if (r != kNotEligible) return r;
+    }
     DevBuf pidx, bidx;
     int64_t m = 0;
     QEH_TRY(join_indices(ctx, *probe_key, bt, &pidx, &bidx, &m));

@@ -218,3 +218,37 @@ def test_scatter_inverts_take(ctx):
     assert np.array_equal(back, v)
     f = r.random(n).astype(np.float32)
     assert np.array_equal(ctx.scatter(ctx.take(ctx.upload(f), dp), dp).to_numpy()[0], f)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("np_,nb", [(0, 1), (1, 1), (3, 3), (2, 2)])
+@pytest.mark.parametrize("n_probe", [2047, 2049, 300_001])
+def test_join_fused_materialise_matches_unfused(ctx, monkeypatch, np_, nb, n_probe):
+    """The fused probe (records embedded by key offset, LDS-staged output) against
+    the index-pair + gather path and the oracle, in probe-row order."""
+    r = np.random.default_rng(np_ * 10 + nb + n_probe)
+    n_build = 50_000
+    bk = (r.permutation(2 * n_build)[:n_build] - 7000).astype(np.int64)  # DIRECT, half the offsets absent
+    bcols = [(bk, None)] + [(r.integers(-(2 ** 62), 2 ** 62, n_build).astype(np.int64), None),
+                            (r.random(n_build), None)][: nb - 1]
+    pk = r.integers(-9000, 2 * n_build - 5000, n_probe).astype(np.int64)
+    pcols = [(r.random(n_probe), None), (pk, None), (r.integers(0, 9, n_probe).astype(np.int64), None)][:np_]
+    got, want = join_both(ctx, (pk, None), pcols, (bk, None), bcols)
+    assert rows_of(got) == rows_of(want)
+    monkeypatch.setenv("QEH_NO_FUSED_JOIN", "1")
+    got2, _ = join_both(ctx, (pk, None), pcols, (bk, None), bcols)
+    assert rows_of(got2) == rows_of(got)
+
+
+@pytest.mark.gpu
+def test_join_fused_with_array_offsets(ctx):
+    r = np.random.default_rng(77)
+    bk = r.permutation(10_000).astype(np.int64)
+    ba = r.integers(0, 100, 10_000).astype(np.int64)
+    pk = r.integers(0, 12_000, 100_000).astype(np.int64)
+    pv = r.random(100_000)
+    dp = [ctx.upload(pv, offset=2)]
+    op, obd, rows = ctx.hash_join_inner(ctx.upload(pk, offset=4), dp, ctx.upload(bk, offset=2), [ctx.upload(ba, offset=6)])
+    wp, wb, wrows = ob.hash_join_inner(ob.HostCol(pk), [ob.HostCol(pv)], ob.HostCol(bk), [ob.HostCol(ba)])
+    assert rows == wrows
+    assert rows_of([c.to_numpy() for c in op + obd]) == rows_of(wp + wb)
