@@ -602,6 +602,12 @@ __global__ __launch_bounds__(kBlock) void k_groupby_lds(ColSet cols, int64_t n, 
     }
 }
 
+// cheap multiplicative hash for the per-workgroup LDS table (the HBM table keeps hash64)
+__device__ __forceinline__ uint32_t lds_hash(int64_t key) {
+    const uint32_t x = (uint32_t)key ^ (uint32_t)((uint64_t)key >> 32);
+    return (x * 0x9E3779B1u) ^ ((x * 0x9E3779B1u) >> 15);
+}
+
 // Fast single-key GROUP BY: the FastTile loads of k_join_agg_fast with the
 // group slot found in a per-workgroup LDS hash of keys (linear probing, CAS
 // insert); keys that do not fit the LDS table (or INT64_MIN, the empty
@@ -629,13 +635,21 @@ __global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms 
         FastTile<NTERMS, NACOL, NT> ft;
         ft.load(in, terms, base);
         const uint32_t sel = ft.sel;
-        int slot[kFastR];
+        // first probe of all rows at once (a warm table answers nearly every row
+        // there), then the rest of the probe sequence for the few that need it
+        int slot[kFastR], h0[kFastR];
+        int64_t first[kFastR];
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
-            slot[r] = -1;
+            h0[r] = (int)(lds_hash(ft.k(r)) & (uint32_t)(lcap - 1));
+            first[r] = lkeys[h0[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
             const int64_t key = ft.k(r);
-            if (!((sel >> r) & 1) || key == kEmptyKey) continue;
-            int h = (int)(hash64((uint64_t)key) & (uint64_t)(lcap - 1));
+            slot[r] = (first[r] == key && key != kEmptyKey) ? h0[r] : -1;
+            if (slot[r] >= 0 || !((sel >> r) & 1) || key == kEmptyKey) continue;
+            int h = h0[r];
             for (int p = 0; p < 32; ++p) {
                 const int64_t cur = lkeys[h];
                 if (cur == key) { slot[r] = h; break; }

@@ -15,8 +15,10 @@
 // selected rows of every output column to their final, order-preserving
 // positions.  Inputs are read once, outputs written once.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "expr_device.h"
@@ -175,6 +177,138 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
     if (err) atomicOr(errp, err);
 }
 
+// ---- fast filter: non-null 8-byte columns, <= 2 terms ---------------------------------------
+// Every column the tile needs (outputs first, then predicate-only columns) is
+// loaded once as 16-byte pairs before anything else, the selected rows are
+// ranked with ballots, the tile's output offset comes from the same decoupled
+// look-back, and each output column leaves through LDS as one contiguous run
+// (full-line writes instead of one scattered 8-byte store per selected row).
+constexpr int kFFMaxCols = 4;
+constexpr int kFFPairs = 4, kFFR = 2 * kFFPairs;
+static_assert(kFFR * kBlock == kFTile, "fast filter tiles match the generic filter's");
+typedef long long v2i64f __attribute__((ext_vector_type(2)));
+
+struct FastFilterIn {
+    const int64_t *col[kFFMaxCols];   // slots: outputs first, then predicate-only columns
+    int64_t *out[kFFMaxCols];
+    int32_t n_out;
+    int32_t term_slot[2];
+    int32_t term_dt[2];
+    int32_t _pad;
+    int64_t n;
+};
+
+__device__ __forceinline__ v2i64f ff_pair(const int64_t *p, int64_t row, int64_t n) {
+    if (row + 1 < n) return __builtin_nontemporal_load((const v2i64f *)(p + row));
+    v2i64f v = {0, 0};
+    if (row < n) v[0] = p[row];
+    return v;
+}
+
+template <int NTERMS, int NC>
+__global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t n_tiles, PredTerms terms,
+                                                        uint64_t *__restrict__ status, unsigned long long *__restrict__ ticket,
+                                                        uint32_t *__restrict__ errp, uint64_t *__restrict__ total_out) {
+    constexpr int W = kBlock / 64;
+    __shared__ int64_t stage[kFTile];
+    __shared__ uint32_t cnt[W][kFFPairs], offs[W][kFFPairs];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_total;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1ull);
+        __syncthreads();
+        const int64_t tile = s_tile;
+        if (tile >= n_tiles) break;
+        const int64_t base = tile * kFTile + (int64_t)wave * (64 * kFFR) + 2 * lane;
+        v2i64f cv[NC][kFFPairs];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int j = 0; j < kFFPairs; ++j) cv[c][j] = ff_pair(in.col[c], base + j * 128, in.n);
+        uint32_t live = 0;
+#pragma unroll
+        for (int r = 0; r < kFFR; ++r)
+            if (base + (r >> 1) * 128 + (r & 1) < in.n) live |= 1u << r;
+        uint32_t acc = live;
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i) {
+            const PredTerm pt = terms.t[i];
+            const int slot = in.term_slot[i];
+            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+            uint32_t tr = 0;
+#pragma unroll
+            for (int r = 0; r < kFFR; ++r) {
+                int64_t v = 0;
+#pragma unroll
+                for (int c = 0; c < NC; ++c)  // wave-uniform select, constant register indices
+                    if (c == slot) v = cv[c][r >> 1][r & 1];
+                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
+                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            }
+            if (NTERMS > 1 && terms.is_or) acc = (i == 0) ? tr : (acc | tr);
+            else acc &= tr;
+        }
+        const uint32_t sel = acc & live;
+        uint32_t rank[kFFR];
+#pragma unroll
+        for (int j = 0; j < kFFPairs; ++j) {
+            const uint64_t m0 = __ballot((sel >> (2 * j)) & 1), m1 = __ballot((sel >> (2 * j + 1)) & 1);
+            const uint32_t below = mbcnt(m0) + mbcnt(m1);
+            rank[2 * j] = below;
+            rank[2 * j + 1] = below + ((sel >> (2 * j)) & 1);
+            if (lane == 0) cnt[wave][j] = (uint32_t)(popc64(m0) + popc64(m1));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int w = 0; w < W; ++w)
+                for (int j = 0; j < kFFPairs; ++j) {
+                    offs[w][j] = acc;
+                    acc += cnt[w][j];
+                }
+            s_total = acc;
+        }
+        __syncthreads();
+        const uint32_t total = s_total;
+        if (wave == 0) {
+            uint64_t prefix = 0;
+            if (tile == 0) {
+                if (lane == 0) st_agent(&status[0], kFlagIncl | total);
+            } else {
+                if (lane == 0) st_agent(&status[tile], kFlagAgg | total);
+                prefix = lookback(status, tile, total, errp);
+                if (lane == 0) st_agent(&status[tile], kFlagIncl | (prefix + total));
+            }
+            if (lane == 0) {
+                s_prefix = prefix;
+                if (tile == n_tiles - 1) *total_out = prefix + total;
+            }
+        }
+        __syncthreads();
+        const uint64_t prefix = s_prefix;
+        auto emit = [&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            if constexpr (c < NC) {
+                if (c < in.n_out) {  // wave-uniform
+#pragma unroll
+                    for (int r = 0; r < kFFR; ++r)
+                        if ((sel >> r) & 1) stage[offs[wave][r >> 1] + rank[r]] = cv[c][r >> 1][r & 1];
+                    __syncthreads();
+                    int64_t *dst = in.out[c] + prefix;
+                    for (uint32_t i = threadIdx.x; i < total; i += kBlock) __builtin_nontemporal_store(stage[i], &dst[i]);
+                    __syncthreads();
+                }
+            }
+        };
+        emit(std::integral_constant<int, 0>{});
+        emit(std::integral_constant<int, 1>{});
+        emit(std::integral_constant<int, 2>{});
+        emit(std::integral_constant<int, 3>{});
+    }
+}
+
 // ---- projection expression -------------------------------------------------------------
 constexpr int kER = 4;
 template <int RT>  // result dtype class: 0 = 8-byte, 1 = 4-byte int, 2 = float32, 3 = bool
@@ -286,6 +420,39 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
         o.dtype = QEH_DT_UINT32;
         o.dst_values = rowids.p;
     }
+    // fast path: every referenced column non-null 8-byte and 16-byte aligned, <= 2 terms,
+    // distinct output columns, <= 4 columns in all
+    FastFilterIn ffi{};
+    int ff_nc = 0;
+    bool ff = fast && terms.n <= 2 && utf8.empty() && !std::getenv("QEH_NO_FAST_FILTER");
+    auto ff_ok = [&](const qeh_column &c) {
+        return (c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_FLOAT64) && (!c.validity || c.null_count == 0) &&
+               ((uintptr_t)((const int64_t *)c.values + c.offset) & 15) == 0;
+    };
+    std::vector<int> slot_col;  // slot -> input column
+    for (int j = 0; ff && j < n_out; ++j) {
+        const int ci = out_idx[j];
+        if (!ff_ok(cols[ci]) || std::find(slot_col.begin(), slot_col.end(), ci) != slot_col.end()) ff = false;
+        else slot_col.push_back(ci);
+    }
+    for (int i = 0; ff && i < terms.n; ++i) {
+        const int ci = terms.t[i].col;
+        if (!ff_ok(cols[ci]) || (terms.t[i].ctype != QEH_DT_INT64 && terms.t[i].ctype != QEH_DT_FLOAT64)) ff = false;
+        auto it = std::find(slot_col.begin(), slot_col.end(), ci);
+        if (ff && it == slot_col.end()) slot_col.push_back(ci);
+    }
+    if (ff && ((int)slot_col.size() > kFFMaxCols || slot_col.empty())) ff = false;
+    if (ff) {
+        ff_nc = (int)slot_col.size();
+        for (int c = 0; c < ff_nc; ++c) ffi.col[c] = (const int64_t *)cols[slot_col[c]].values + cols[slot_col[c]].offset;
+        for (int j = 0; j < n_out; ++j) ffi.out[j] = (int64_t *)out[j].values;
+        ffi.n_out = n_out;
+        for (int i = 0; i < terms.n; ++i) {
+            ffi.term_slot[i] = (int)(std::find(slot_col.begin(), slot_col.end(), terms.t[i].col) - slot_col.begin());
+            ffi.term_dt[i] = cols[terms.t[i].col].dtype;
+        }
+        ffi.n = n;
+    }
     const int64_t n_tiles = (n + kFTile - 1) / kFTile;
     uint64_t total = 0;
     if (n_tiles > 0) {
@@ -303,7 +470,18 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
         const int grid = grid_for(ctx, n, kFTile, 4);
         {
             KernelTimer kt(ctx, "filter");
-            if (fast)
+            if (ff) {
+#define QEH_FF(NTV, NCV) \
+    hipLaunchKernelGGL((k_filter_fast<NTV, NCV>), dim3(grid), dim3(kBlock), 0, ctx->stream, ffi, n_tiles, terms, status, ticket, err, tot)
+#define QEH_FF_NC(NTV)                                    \
+    if (ff_nc == 1) QEH_FF(NTV, 1);                       \
+    else if (ff_nc == 2) QEH_FF(NTV, 2);                  \
+    else if (ff_nc == 3) QEH_FF(NTV, 3);                  \
+    else QEH_FF(NTV, 4);
+                if (terms.n == 0) { QEH_FF_NC(0) } else if (terms.n == 1) { QEH_FF_NC(1) } else { QEH_FF_NC(2) }
+#undef QEH_FF_NC
+#undef QEH_FF
+            } else if (fast)
                 hipLaunchKernelGGL(k_filter<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n, n_tiles, terms, prog, os,
                                    status, ticket, err, tot);
             else

@@ -138,37 +138,59 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const KeyT *__restrict__ key
     hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter: rank each tile by digit in registers/LDS, reorder it in LDS,
-// then write digit runs (≈ kRsTile/kRadix elements each) contiguously.
+// Stable scatter, one 1024-thread workgroup per CU: rank each 8192-element
+// tile by digit (ballot peers + per-wave counters), reorder it in LDS, then
+// write every digit's run (≈ 32 elements = whole 128-byte lines) contiguously.
+// Few, long-lived workgroups keep the open output lines of an XCD within its
+// L2 (32 workgroups × 256 digits × 2 arrays), and the next tile's loads are
+// issued before the current tile is ranked (LDS-only barriers below do not
+// wait for them).
+constexpr int kRsThreads = 1024;
+constexpr int kRsSTile = kRsThreads * kRsIpt;  // 8192
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
-                                                       int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
-                                                       int nblocks, KeyT *__restrict__ keys_out,
-                                                       uint32_t *__restrict__ vals_out) {
-    constexpr int W = kBlock / 64;
-    __shared__ KeyT s_keys[kRsTile];
-    __shared__ uint32_t s_vals[kRsTile];
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                           int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
+                                                           int nblocks, KeyT *__restrict__ keys_out,
+                                                           uint32_t *__restrict__ vals_out) {
+    constexpr int W = kRsThreads / 64;
+    constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
+    __shared__ KeyT s_keys[kRsSTile];
+    __shared__ uint32_t s_vals[kRsSTile];
     __shared__ uint32_t wcnt[W][kRadix];  // per-wave digit counts, then per-wave start inside the digit
     __shared__ uint32_t loc[kRadix];      // tile-local start of each digit
-    __shared__ uint32_t wsum[W];
+    __shared__ uint32_t tot_s[kRadix];
+    __shared__ uint32_t wsum[DW];
     __shared__ uint64_t run[kRadix];      // global position of the block's next element of each digit
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
+    if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
-    for (int64_t c0 = lo; c0 < hi; c0 += kRsTile) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) wcnt[w][t] = 0;
-        __syncthreads();
+    KeyT k[kRsIpt];
+    uint32_t v[kRsIpt];
+    auto load_tile = [&](int64_t c0, KeyT *kk, uint32_t *vv) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
-        KeyT k[kRsIpt];
-        uint32_t v[kRsIpt], rk[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
             const bool live = i < hi;
-            k[j] = live ? __builtin_nontemporal_load(&keys[i]) : 0;
-            v[j] = live ? __builtin_nontemporal_load(&vals[i]) : 0;
+            kk[j] = live ? __builtin_nontemporal_load(&keys[i]) : 0;
+            vv[j] = live ? __builtin_nontemporal_load(&vals[i]) : 0;
         }
+    };
+    if (lo < hi) load_tile(lo, k, v);
+    for (int64_t c0 = lo; c0 < hi; c0 += kRsSTile) {
+        for (int i = t; i < W * kRadix; i += kRsThreads) (&wcnt[0][0])[i] = 0;
+        KeyT kn[kRsIpt];
+        uint32_t vn[kRsIpt];
+        const int64_t c1 = c0 + kRsSTile;
+        if (c1 < hi) load_tile(c1, kn, vn);  // in flight while this tile is ranked and written
+        lds_barrier();
+        const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
+        uint32_t rk[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const bool live = base + j * 64 < hi;
@@ -178,23 +200,28 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const KeyT *__restrict__ 
             rk[j] = before + mbcnt(peers);
             if (live && mbcnt(peers) == 0) wcnt[wave][dg] = before + (uint32_t)popc64(peers);
         }
-        __syncthreads();
-        // thread t = digit t: wave starts inside the digit, tile total, block scan -> loc
-        uint32_t tot = 0;
+        lds_barrier();
+        // thread t < 256 = digit t: wave starts inside the digit, tile total, scan -> loc
+        uint32_t tot = 0, incl = 0;
+        if (t < kRadix) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint32_t c = wcnt[w][t];
-            wcnt[w][t] = tot;
-            tot += c;
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = wcnt[w][t];
+                wcnt[w][t] = tot;
+                tot += c;
+            }
+            tot_s[t] = tot;
+            incl = wave_incl_scan(tot);
+            if (lane == 63) wsum[wave] = incl;
         }
-        const uint32_t incl = wave_incl_scan(tot);
-        if (lane == 63) wsum[wave] = incl;
-        __syncthreads();
-        uint32_t wbase = 0;
+        lds_barrier();
+        if (t < kRadix) {
+            uint32_t wbase = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) wbase += w < wave ? wsum[w] : 0;
-        loc[t] = wbase + incl - tot;
-        __syncthreads();
+            for (int w = 0; w < DW; ++w) wbase += w < wave ? wsum[w] : 0;
+            loc[t] = wbase + incl - tot;
+        }
+        lds_barrier();
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             if (base + j * 64 < hi) {
@@ -204,17 +231,22 @@ __global__ __launch_bounds__(kBlock) void k_rs_scatter(const KeyT *__restrict__ 
                 s_vals[p] = v[j];
             }
         }
-        __syncthreads();
-        const int cnt = (int)(hi - c0 < kRsTile ? hi - c0 : kRsTile);
-        for (int p = t; p < cnt; p += kBlock) {
+        lds_barrier();
+        const int cnt = (int)(hi - c0 < kRsSTile ? hi - c0 : kRsSTile);
+        for (int p = t; p < cnt; p += kRsThreads) {
             const KeyT key = s_keys[p];
             const uint32_t dg = (uint32_t)((key >> shift) & (kRadix - 1));
             const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
             keys_out[pos] = key;
             vals_out[pos] = s_vals[p];
         }
-        __syncthreads();
-        run[t] += tot;
+        lds_barrier();
+        if (t < kRadix) run[t] += tot_s[t];
+#pragma unroll
+        for (int j = 0; j < kRsIpt; ++j) {
+            k[j] = kn[j];
+            v[j] = vn[j];
+        }
     }
 }
 
@@ -232,7 +264,8 @@ template <typename KeyT>
 static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
     const int64_t n = rs.n;
     if (n <= 1 || bits <= 0) return QEH_OK;
-    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsTile - 1) / kRsTile, 1), (int64_t)ctx->props.multiProcessorCount * 4);
+    // one long-lived scatter workgroup per CU (see k_rs_scatter); hist uses the same segments
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)ctx->props.multiProcessorCount);
     const int64_t seg = (n + nblocks - 1) / nblocks;
     DevBuf hist, offs;
     QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
@@ -244,7 +277,7 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
                            hist.as<uint32_t>(), nblocks);
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
-        hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<KeyT>(),
+        hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
                            rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
                            rs.v[1 - c].as<uint32_t>());
         QEH_HIP(hipGetLastError());

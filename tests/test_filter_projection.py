@@ -148,3 +148,40 @@ def test_projection_column_reference_is_zero_copy(ctx):
     dev = [ctx.upload(v, m) for v, m in t]
     view, src = ctx.eval(dev, col(2))
     assert view.c.values == dev[2].c.values and view.c.owned == 0
+
+
+FAST_PREDS = {
+    "gt_int": binop(col(0), BinaryOp.Greater, lit(49)),
+    "float_col_int_lit": binop(col(1), BinaryOp.LessEqual, lit(0)),
+    "int_col_float_lit": binop(col(0), BinaryOp.Less, lit(12.5)),
+    "and": binop(col(0), BinaryOp.Greater, lit(20)) & binop(col(1), BinaryOp.Less, lit(0.5)),
+    "or": binop(col(2), BinaryOp.Greater, lit(0)) | binop(col(1), BinaryOp.Less, lit(0.25)),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(FAST_PREDS))
+@pytest.mark.parametrize("n", [0, 1, 2047, 2049, 1_000_003])
+def test_fast_filter_non_null_8byte_columns(ctx, monkeypatch, name, n):
+    """All-8-byte, non-null inputs take k_filter_fast (register tiles + LDS-staged
+    runs); same rows, same order as the generic kernel and the oracle."""
+    r = np.random.default_rng(n + len(name))
+    cols = [(r.integers(0, 100, n).astype(np.int64), None), (r.random(n) - 0.25, None),
+            (r.integers(-(2 ** 40), 2 ** 40, n).astype(np.int64), None)]
+    rows = run_filter(ctx, cols, FAST_PREDS[name])
+    monkeypatch.setenv("QEH_NO_FAST_FILTER", "1")
+    assert run_filter(ctx, cols, FAST_PREDS[name]) == rows
+
+
+@pytest.mark.gpu
+def test_fast_filter_output_subset_and_aligned_offset(ctx):
+    r = np.random.default_rng(5)
+    n = 300_000
+    x = r.integers(0, 100, n).astype(np.int64)
+    v = r.random(n)
+    dev = [ctx.upload(x, offset=2), ctx.upload(v, offset=4)]
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    out, rows = ctx.filter(dev, pred, [1])
+    keep = x > 49
+    assert rows == int(keep.sum())
+    assert np.array_equal(out[0].to_numpy()[0], v[keep])
