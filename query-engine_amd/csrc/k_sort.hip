@@ -96,8 +96,8 @@ __global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n,
 // input order and every load is a full 512-byte wave line.  hist is digit-major
 // [kRadix][nblocks].
 constexpr int kRsIpt = 8;
-constexpr int kRsTile = kBlock * kRsIpt;
-static_assert(kBlock == kRadix, "one thread per digit in the tile bookkeeping");
+constexpr int kRsThreads = 1024;
+constexpr int kRsSTile = kRsThreads * kRsIpt;  // 8192
 
 // lanes of this wave whose digit equals mine (wave64 has no match_any: 8 ballots)
 __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
@@ -111,20 +111,20 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
 }
 
 template <typename KeyT>
-__global__ __launch_bounds__(kBlock) void k_rs_hist(const KeyT *__restrict__ keys, int64_t n, int64_t seg,
-                                                    int shift, uint32_t *__restrict__ hist, int nblocks) {
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__ keys, int64_t n, int64_t seg,
+                                                        int shift, uint32_t *__restrict__ hist, int nblocks) {
     __shared__ uint32_t h[kRadix];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int64_t c0 = lo; c0 < hi; c0 += kRsTile) {
+    for (int64_t c0 = lo; c0 < hi; c0 += kRsSTile) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
         KeyT k[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
-            k[j] = i < hi ? __builtin_nontemporal_load(&keys[i]) : 0;
+            k[j] = __builtin_nontemporal_load(&keys[i < hi ? i : hi - 1]);
         }
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const KeyT *__restrict__ key
         }
     }
     __syncthreads();
-    hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (threadIdx.x < kRadix) hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
 // Stable scatter, one 1024-thread workgroup per CU: rank each 8192-element
@@ -145,8 +145,6 @@ __global__ __launch_bounds__(kBlock) void k_rs_hist(const KeyT *__restrict__ key
 // L2 (32 workgroups × 256 digits × 2 arrays), and the next tile's loads are
 // issued before the current tile is ranked (LDS-only barriers below do not
 // wait for them).
-constexpr int kRsThreads = 1024;
-constexpr int kRsSTile = kRsThreads * kRsIpt;  // 8192
 
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -171,14 +169,17 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
     KeyT k[kRsIpt];
     uint32_t v[kRsIpt];
+    // loads are unconditional (indices clamped into [lo, hi)): no branches around
+    // them, so the compiler's wait counts stay exact and the prefetch really
+    // stays in flight across the ranking of the current tile
     auto load_tile = [&](int64_t c0, KeyT *kk, uint32_t *vv) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
-            const bool live = i < hi;
-            kk[j] = live ? __builtin_nontemporal_load(&keys[i]) : 0;
-            vv[j] = live ? __builtin_nontemporal_load(&vals[i]) : 0;
+            const int64_t ii = i < hi ? i : hi - 1;
+            kk[j] = __builtin_nontemporal_load(&keys[ii]);
+            vv[j] = __builtin_nontemporal_load(&vals[ii]);
         }
     };
     if (lo < hi) load_tile(lo, k, v);
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
         KeyT kn[kRsIpt];
         uint32_t vn[kRsIpt];
         const int64_t c1 = c0 + kRsSTile;
-        if (c1 < hi) load_tile(c1, kn, vn);  // in flight while this tile is ranked and written
+        load_tile(c1 < hi ? c1 : c0, kn, vn);  // in flight while this tile is ranked and written
         lds_barrier();
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
         uint32_t rk[kRsIpt];
@@ -273,7 +274,7 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
     for (int shift = 0; shift < bits; shift += kRadixBits) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = rs.cur;
-        hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kBlock), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
+        hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
                            hist.as<uint32_t>(), nblocks);
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
