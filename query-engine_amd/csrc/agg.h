@@ -39,6 +39,8 @@ struct AggSpec {
 struct AggSpecs {
     int32_t n;
     int32_t n_slots;   // 1 + value slots + count slots
+    int32_t shards;    // copies of the global states (>= 1), see shard_states
+    int32_t _pad;
     AggSpec a[kMaxAggs];
 };
 

@@ -52,10 +52,18 @@ struct GidSource {
     int32_t _pad2;
 };
 
+// Global states are kept in specs.shards copies ([shard][slot][G]); workgroup b
+// merges into copy b % shards, so thousands of workgroups do not all hit the
+// same few KB with atomics.  k_states_reduce folds the copies into copy 0.
+__device__ __forceinline__ uint64_t *shard_states(uint64_t *all, const AggSpecs &specs, int64_t G) {
+    return all + (uint64_t)(blockIdx.x % (unsigned)specs.shards) * (uint64_t)specs.n_slots * (uint64_t)G;
+}
+
 template <int GM, int PM, bool LDS>
 __global__ __launch_bounds__(kBlock) void k_agg_rows(ColSet cols, int64_t n, PredTerms terms, DevProgram prog,
                                                      GidSource src, AggSpecs specs, int64_t G,
-                                                     uint64_t *__restrict__ gstates, uint32_t *__restrict__ errp) {
+                                                     uint64_t *__restrict__ gstates_all, uint32_t *__restrict__ errp) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     uint64_t *st = LDS ? lds : gstates;
     const int64_t stride_slot = G;
@@ -230,7 +238,8 @@ struct FastTile {
 
 template <int NTERMS, int NACOL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, HashTable t,
-                                                          int64_t G, int64_t n_tiles, uint64_t *__restrict__ gstates) {
+                                                          int64_t G, int64_t n_tiles, uint64_t *__restrict__ gstates_all) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     {
         const int64_t words = (int64_t)specs.n_slots * G;
@@ -299,6 +308,7 @@ struct PartBufs {
     int64_t *val[2][kParts];
     unsigned long long *cursor;    // [0..8): fill cursors (phase A), [8..16): batch cursors (phase B)
     uint64_t cap;                  // items per partition
+    uint64_t batch;                // phase B items per grab
     float scale;                   // DIRECT: partition = key offset * scale
     int32_t shift;                 // PACKED: partition = slot >> shift
     uint32_t *overflow;
@@ -395,7 +405,8 @@ __global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms 
 
 template <int NACOL, bool KEY64>
 __global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn in, HashTable t, AggSpecs specs,
-                                                             int64_t G, uint64_t *__restrict__ gstates) {
+                                                             int64_t G, uint64_t *__restrict__ gstates_all) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const int64_t words = (int64_t)specs.n_slots * G;
     unsigned long long *grab = (unsigned long long *)&lds[words];
@@ -413,12 +424,12 @@ __global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn
         unsigned long long filled = __hip_atomic_load(&pb.cursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t n_p = filled < pb.cap ? filled : pb.cap;
         for (;;) {
-            if (threadIdx.x == 0) *grab = atomicAdd(&pb.cursor[kParts + p], (unsigned long long)kPartBatch);
+            if (threadIdx.x == 0) *grab = atomicAdd(&pb.cursor[kParts + p], (unsigned long long)pb.batch);
             __syncthreads();
             const uint64_t b = *grab;
             __syncthreads();
             if (b >= n_p) break;
-            const uint64_t e = b + kPartBatch < n_p ? b + kPartBatch : n_p;
+            const uint64_t e = b + pb.batch < n_p ? b + pb.batch : n_p;
             constexpr int U = kPartUnroll;
             for (uint64_t i0 = b + threadIdx.x; i0 < e; i0 += U * kBlock) {
                 int64_t kk[U];
@@ -497,7 +508,8 @@ __device__ __forceinline__ int64_t gt_slot(const GTable &g, int64_t key) {
 template <int PM>
 __global__ __launch_bounds__(kBlock) void k_groupby_lds(ColSet cols, int64_t n, PredTerms terms, DevProgram prog,
                                                         int key_col, GidSource src, AggSpecs specs, int64_t G,
-                                                        uint64_t *__restrict__ gstates, uint32_t *__restrict__ errp) {
+                                                        uint64_t *__restrict__ gstates_all, uint32_t *__restrict__ errp) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const int lcap = src.lcap;
     int64_t *lkeys = (int64_t *)lds;
@@ -615,7 +627,8 @@ __device__ __forceinline__ uint32_t lds_hash(int64_t key) {
 template <int NTERMS, int NACOL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, GTable gt,
                                                            int lcap, int64_t G, int64_t n_tiles,
-                                                           uint64_t *__restrict__ gstates) {
+                                                           uint64_t *__restrict__ gstates_all) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     int64_t *lkeys = (int64_t *)lds;
     uint64_t *lst = lds + lcap;  // [n_slots][lcap]
@@ -712,13 +725,36 @@ __global__ void k_iota(uint32_t *p, int64_t n) {
 }
 
 __global__ void k_states_init(uint64_t *states, int64_t G, AggSpecs specs) {
-    const int64_t words = (int64_t)specs.n_slots * G;
+    const int64_t words = (int64_t)specs.shards * specs.n_slots * G;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t slot = i / G;
+        int64_t slot = (i / G) % specs.n_slots;
         uint64_t v = 0;
         for (int a = 0; a < specs.n; ++a)
             if (specs.a[a].val_slot == slot) v = (uint64_t)agg_init_value(specs.a[a].kind);
         states[i] = v;
+    }
+}
+
+// Fold the shard copies into copy 0 (same merge as agg_merge_global, no atomics).
+__global__ void k_states_reduce(uint64_t *states, int64_t G, AggSpecs specs) {
+    const int64_t words = (int64_t)specs.n_slots * G;
+    const int64_t stride = words;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t slot = i / G;
+        int kind = -1;  // counts
+        for (int a = 0; a < specs.n; ++a)
+            if (specs.a[a].val_slot == slot) kind = specs.a[a].kind;
+        uint64_t acc = states[i];
+        for (int sh = 1; sh < specs.shards; ++sh) {
+            const uint64_t v = states[i + sh * stride];
+            switch (kind) {
+                case AK_SUM_F: acc = __builtin_bit_cast(uint64_t, as_f64(acc) + as_f64(v)); break;
+                case AK_MIN: acc = (int64_t)v < (int64_t)acc ? v : acc; break;
+                case AK_MAX: acc = (int64_t)v > (int64_t)acc ? v : acc; break;
+                default: acc += v; break;  // counts, wrapping int sums
+            }
+        }
+        states[i] = acc;
     }
 }
 
@@ -810,6 +846,7 @@ static int plan_aggs(const qeh_agg *aggs, int n_aggs, const qeh_column *inputs, 
     if (n_aggs > kMaxAggs) return fail(QEH_E_UNSUPPORTED, "too many aggregates for one device operator (max 8)");
     std::memset(out, 0, sizeof(*out));
     out->n = n_aggs;
+    out->shards = 1;
     int slot = 1;
     for (int i = 0; i < n_aggs; ++i) {
         const qeh_agg &a = aggs[i];
@@ -1014,30 +1051,74 @@ static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, con
     if (n_tiles == 0) return 0;
     const int64_t rows = n_tiles * kFastTile;
     const bool key64 = t.kind == TK_PACKED;
-    PartBufs pb{};
-    pb.cap = (uint64_t)(rows / kParts) + (uint64_t)(rows / kParts) / 4 + 65536;
-    const size_t kb = key64 ? 8 : 4;
-    DevBuf kbuf, vbuf, cur, ovf;
-    if (kbuf.alloc(ctx, pb.cap * kb * kParts) != QEH_OK) return 0;
-    if (nacol && vbuf.alloc(ctx, pb.cap * 8 * kParts * nacol) != QEH_OK) return 0;
-    if (cur.alloc(ctx, 2 * kParts * 8 + 64) != QEH_OK) return 0;
-    for (int p = 0; p < kParts; ++p) {
-        pb.key[p] = (char *)kbuf.p + (size_t)p * pb.cap * kb;
-        for (int c = 0; c < nacol; ++c) pb.val[c][p] = (int64_t *)vbuf.p + ((size_t)c * kParts + p) * pb.cap;
+    // QEH_PART_CHUNK = fact rows per pipeline chunk (0: one chunk).  Chunks run
+    // phase A on the main stream and phase B on the auxiliary stream, two
+    // partition-buffer slots in flight, so B(c) overlaps A(c+1) and a chunk's
+    // records can still be in the Infinity Cache when phase B reads them.
+    int64_t chunk_tiles = n_tiles;
+    if (const char *e = std::getenv("QEH_PART_CHUNK")) {
+        const int64_t cr = std::strtoll(e, nullptr, 10);
+        if (cr > 0) chunk_tiles = std::max<int64_t>(1, cr / kFastTile);
     }
-    pb.cursor = cur.as<unsigned long long>();
-    pb.overflow = (uint32_t *)(cur.as<char>() + 2 * kParts * 8);
-    pb.scale = (float)kParts / (float)(t.range ? t.range : 1);
+    const int64_t n_chunks = (n_tiles + chunk_tiles - 1) / chunk_tiles;
+    const int n_slots = n_chunks > 1 ? 2 : 1;
+    const int64_t chunk_rows = std::min<int64_t>(chunk_tiles, n_tiles) * kFastTile;
+    const uint64_t cap = (uint64_t)(chunk_rows / kParts) + (uint64_t)(chunk_rows / kParts) / 4 + 65536;
+    const size_t kb = key64 ? 8 : 4;
+    DevBuf kbuf, vbuf, cur;
+    if (kbuf.alloc(ctx, cap * kb * kParts * n_slots) != QEH_OK) return 0;
+    if (nacol && vbuf.alloc(ctx, cap * 8 * kParts * nacol * n_slots) != QEH_OK) return 0;
+    const size_t cur_bytes = 2 * kParts * 8 + 64;  // cursors + overflow word, per slot
+    if (cur.alloc(ctx, cur_bytes * n_slots) != QEH_OK) return 0;
+    PartBufs pbs[2]{};
     int lg = 0;
     while ((1ull << lg) < t.mask + 1) ++lg;
-    pb.shift = lg > 3 ? lg - 3 : 0;
-    if (hipMemsetAsync(cur.p, 0, 2 * kParts * 8 + 64, ctx->stream) != hipSuccess) return 0;
+    for (int sl = 0; sl < n_slots; ++sl) {
+        PartBufs &pb = pbs[sl];
+        pb.cap = cap;
+        pb.batch = n_chunks > 1 ? 2048 : kPartBatch;
+        for (int p = 0; p < kParts; ++p) {
+            pb.key[p] = (char *)kbuf.p + ((size_t)sl * kParts + p) * cap * kb;
+            for (int c = 0; c < nacol; ++c)
+                pb.val[c][p] = (int64_t *)vbuf.p + (((size_t)sl * nacol + c) * kParts + p) * cap;
+        }
+        pb.cursor = (unsigned long long *)(cur.as<char>() + sl * cur_bytes);
+        pb.overflow = (uint32_t *)(cur.as<char>() + sl * cur_bytes + 2 * kParts * 8);
+        pb.scale = (float)kParts / (float)(t.range ? t.range : 1);
+        pb.shift = lg > 3 ? lg - 3 : 0;
+    }
+    if (hipMemsetAsync(cur.p, 0, cur_bytes * n_slots, ctx->stream) != hipSuccess) return 0;
+    if (n_chunks > 1 && !ctx->aux_stream &&
+        hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) != hipSuccess)
+        return 0;
+    hipEvent_t evA[2] = {}, evB[2] = {};
+    if (n_chunks > 1)
+        for (int sl = 0; sl < 2; ++sl) {
+            hipEventCreateWithFlags(&evA[sl], hipEventDisableTiming);
+            hipEventCreateWithFlags(&evB[sl], hipEventDisableTiming);
+        }
     const bool nt = fast_nt_mode() == 1;
-    {
-        KernelTimer kt(ctx, "join_partition");
-        const int grid = grid_for(ctx, rows, kFastTile, 8);
+    const int gridB = ctx->props.multiProcessorCount * std::max(1, per_cu);
+    const size_t shmB = lds_bytes + 16;
+    for (int64_t c = 0; c < n_chunks; ++c) {
+        const int sl = (int)(c % n_slots);
+        const PartBufs &pb = pbs[sl];
+        const int64_t t0 = c * chunk_tiles, nt_c = std::min<int64_t>(chunk_tiles, n_tiles - t0);
+        FastIn inc = in;
+        const int64_t off = t0 * kFastTile;
+        inc.key += off;
+        for (int i = 0; i < nterms; ++i) inc.term[i] += off;
+        for (int i = 0; i < nacol; ++i) inc.acol[i] += off;
+        hipStream_t sB = n_chunks > 1 ? ctx->aux_stream : ctx->stream;
+        if (c >= 2) {  // slot reuse: B(c-2) must be done; overflow flags are sticky per slot
+            hipStreamWaitEvent(ctx->stream, evB[sl], 0);
+            hipMemsetAsync(pb.cursor, 0, 2 * kParts * 8, ctx->stream);
+        }
+        {
+            KernelTimer kt(ctx, "join_partition");
+            const int grid = grid_for(ctx, nt_c * kFastTile, kFastTile, 8);
 #define QEH_PA(NTV, NAV, K64, NTB) \
-    hipLaunchKernelGGL((k_join_partition<NTV, NAV, K64, NTB>), dim3(grid), dim3(kBlock), 0, ctx->stream, in, pp.terms, t, n_tiles, pb)
+    hipLaunchKernelGGL((k_join_partition<NTV, NAV, K64, NTB>), dim3(grid), dim3(kBlock), 0, ctx->stream, inc, pp.terms, t, nt_c, pb)
 #define QEH_PA_NA(NTV, K64, NTB)                         \
     if (nacol == 0) QEH_PA(NTV, 0, K64, NTB);            \
     else if (nacol == 1) QEH_PA(NTV, 1, K64, NTB);       \
@@ -1046,28 +1127,43 @@ static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, con
     if (nterms == 0) { QEH_PA_NA(0, K64, NTB) }          \
     else if (nterms == 1) { QEH_PA_NA(1, K64, NTB) }     \
     else { QEH_PA_NA(2, K64, NTB) }
-        if (key64) { if (nt) { QEH_PA_NT(true, true) } else { QEH_PA_NT(true, false) } }
-        else { if (nt) { QEH_PA_NT(false, true) } else { QEH_PA_NT(false, false) } }
+            if (key64) { if (nt) { QEH_PA_NT(true, true) } else { QEH_PA_NT(true, false) } }
+            else { if (nt) { QEH_PA_NT(false, true) } else { QEH_PA_NT(false, false) } }
 #undef QEH_PA_NT
 #undef QEH_PA_NA
 #undef QEH_PA
-    }
-    {
-        KernelTimer kt(ctx, "join_probe_parts");
-        const size_t shm = lds_bytes + 16;
-        const int grid = ctx->props.multiProcessorCount * std::max(1, per_cu);
+        }
+        if (n_chunks > 1) {
+            hipEventRecord(evA[sl], ctx->stream);
+            hipStreamWaitEvent(sB, evA[sl], 0);
+        }
+        {
 #define QEH_PB(NAV, K64) \
-    hipLaunchKernelGGL((k_join_probe_parts<NAV, K64>), dim3(grid), dim3(kBlock), shm, ctx->stream, pb, in, t, specs, G, states)
-        if (key64) { if (nacol == 0) QEH_PB(0, true); else if (nacol == 1) QEH_PB(1, true); else QEH_PB(2, true); }
-        else { if (nacol == 0) QEH_PB(0, false); else if (nacol == 1) QEH_PB(1, false); else QEH_PB(2, false); }
+    hipLaunchKernelGGL((k_join_probe_parts<NAV, K64>), dim3(gridB), dim3(kBlock), shmB, sB, pb, in, t, specs, G, states)
+            if (key64) { if (nacol == 0) QEH_PB(0, true); else if (nacol == 1) QEH_PB(1, true); else QEH_PB(2, true); }
+            else { if (nacol == 0) QEH_PB(0, false); else if (nacol == 1) QEH_PB(1, false); else QEH_PB(2, false); }
 #undef QEH_PB
+        }
+        if (n_chunks > 1) hipEventRecord(evB[sl], sB);
     }
+    if (n_chunks > 1) {
+        for (int sl = 0; sl < 2; ++sl) hipStreamWaitEvent(ctx->stream, evB[sl], 0);
+        for (int sl = 0; sl < 2; ++sl) {
+            hipEventDestroy(evA[sl]);
+            hipEventDestroy(evB[sl]);
+        }
+    }
+    QEH_HIP(hipGetLastError());
     launch_tail(ctx, cols, n, rows, pp, src, specs, G, states, err, lds_bytes);
     uint32_t of = 0;
-    if (read_small(ctx, &of, pb.overflow, 4) != QEH_OK) return 0;
+    for (int sl = 0; sl < n_slots; ++sl) {
+        uint32_t o = 0;
+        if (read_small(ctx, &o, pbs[sl].overflow, 4) != QEH_OK) return 0;
+        of |= o;
+    }
     if (of) {
         *overflowed = true;
-        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
                            ctx->stream, states, G, specs);
         return 0;
     }
@@ -1126,16 +1222,20 @@ constexpr int kRetryBigger = 100;  // internal: group table too small
 
 // Run the row-aggregation kernel and finalize into owned output columns.
 static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, const PredPlan &pp,
-                          const GidSource &src, const AggSpecs &specs, int64_t G, const KeyCols &out_keys_src,
+                          const GidSource &src, const AggSpecs &specs_in, int64_t G, const KeyCols &out_keys_src,
                           const int32_t *key_dtypes, const uint32_t *rep_row, bool drop_empty, const char *kname,
                           qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups) {
     DevBuf states, errw;
     const int64_t Gs = std::max<int64_t>(G, 1);
-    QEH_TRY(states.alloc(ctx, (size_t)specs.n_slots * Gs * 8));
+    AggSpecs specs = specs_in;
+    specs.shards = 1;  // state copies (shard_states): up to 64 while they stay small
+    while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
+    if (std::getenv("QEH_NO_SHARDS")) specs.shards = 1;
+    QEH_TRY(states.alloc(ctx, (size_t)specs.shards * specs.n_slots * Gs * 8));
     QEH_TRY(errw.alloc(ctx, 8));
     QEH_HIP(hipMemsetAsync(errw.p, 0, 8, ctx->stream));
-    hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
-                       states.as<uint64_t>(), Gs, specs);
+    hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock), 0,
+                       ctx->stream, states.as<uint64_t>(), Gs, specs);
     const size_t lds_bytes = (size_t)specs.n_slots * Gs * 8;
     const bool lds = lds_bytes <= kLdsStateBudget;
     if (n > 0 && G > 0) {
@@ -1174,6 +1274,9 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         else launch_agg_rows<GM_GROUP>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
     }
     QEH_HIP(hipGetLastError());
+    if (specs.shards > 1)
+        hipLaunchKernelGGL(k_states_reduce, dim3(grid_for(ctx, specs.n_slots * Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
+                           states.as<uint64_t>(), Gs, specs);
     if (gm == GM_LDSHASH) {  // table overflow: the caller regrows and reruns
         uint32_t of = 0;
         QEH_TRY(read_small(ctx, &of, src.gt.overflow, 4));

@@ -68,6 +68,7 @@ struct qeh_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t aux_stream = nullptr;  // second queue for overlapped pipeline stages (created on first use)
     qeh::DevicePool *pool = nullptr;
     hipDeviceProp_t props{};
     // small scratch (status words, counters, flags), zeroed per call

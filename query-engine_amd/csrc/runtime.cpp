@@ -231,6 +231,10 @@ int qeh_shutdown(qeh_ctx *ctx) {
     if (ctx->pinned) hipHostFree(ctx->pinned);
     delete ctx->pool;
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    if (ctx->aux_stream) {
+        hipStreamSynchronize(ctx->aux_stream);
+        hipStreamDestroy(ctx->aux_stream);
+    }
     delete ctx;
     return QEH_OK;
 }
