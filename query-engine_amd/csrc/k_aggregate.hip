@@ -1077,6 +1077,7 @@ static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, con
         PartBufs &pb = pbs[sl];
         pb.cap = cap;
         pb.batch = n_chunks > 1 ? 2048 : kPartBatch;
+        if (const char *e = std::getenv("QEH_PART_BATCH")) pb.batch = std::strtoull(e, nullptr, 10);
         for (int p = 0; p < kParts; ++p) {
             pb.key[p] = (char *)kbuf.p + ((size_t)sl * kParts + p) * cap * kb;
             for (int c = 0; c < nacol; ++c)
