@@ -158,6 +158,7 @@ constexpr int kFastR = 2 * kFastPairs;
 constexpr int kFastTile = kBlock * kFastR;  // 2048 rows per workgroup iteration
 
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
 struct FastIn {
     const int64_t *key;
@@ -200,9 +201,14 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
 template <int NTERMS, int NACOL, bool NT>
 struct FastTile {
     v2i64 key[kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
+    v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
     uint32_t sel;
     __device__ __forceinline__ void load(const FastIn &in, const PredTerms &terms, int64_t base) {
-        v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
+        issue(in, base);
+        eval(in, terms);
+    }
+    // issue every load of the tile (no use of the data: they stay in flight)
+    __device__ __forceinline__ void issue(const FastIn &in, int64_t base) {
 #pragma unroll
         for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
 #pragma unroll
@@ -213,6 +219,9 @@ struct FastTile {
         for (int c = 0; c < NACOL; ++c)
 #pragma unroll
             for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
+    }
+    // evaluate the term predicate into `sel`
+    __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
         sel = (1u << kFastR) - 1u;
 #pragma unroll
         for (int i = 0; i < NTERMS; ++i) {
@@ -292,192 +301,274 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
     }
 }
 
-// ---- XCD-partitioned probe (tables larger than one XCD's L2) -----------------------
-// Phase A streams the probe columns once, filters, and appends each selected
-// row's (key, aggregate inputs) to one of 8 partitions = 8 contiguous slices
-// of the table.  Phase B's workgroups read their XCD id and drain the
-// partition of the same index first (stealing the others' leftovers), so each
-// XCD's 4 MiB L2 only ever holds 1/8 of the table.  Placement only affects
-// speed: every item is processed exactly once whatever the XCD mapping.
-constexpr int kParts = 8;
-constexpr int kPartBatch = 16384;
-constexpr int kPartUnroll = 16;  // phase B items in flight per lane
+// ---- LDS-slice partitioned probe (direct u16 tables larger than L2) ----------------
+// A single fused pass pays one L2 miss (a 64-B Infinity-Cache request) per
+// probe once the table outgrows an XCD's 4 MiB L2; at the BASELINE shape
+// (1e7-key u16 table = 20 MB) that doubles the pass.  This path splits the
+// table into slices of 2^16 entries (128 KB, one CU's LDS) and runs:
+//   phase A (k_slice_partition): stream the probe columns once, filter, rank
+//     each selected row by slice in LDS, stage the tile sorted by slice, and
+//     append each slice's (16-bit key offset, aggregate input) items to the
+//     workgroup's own region for that slice in whole 32-item chunks (64 B of
+//     keys + 256 B of values per chunk: whole-sector HBM writes).  The < 32
+//     items left over per slice are carried in LDS into the next tile.
+//   phase B (k_slice_probe): a workgroup loads one slice into LDS and drains
+//     that slice's regions with LDS lookups and LDS aggregate states.
+// HBM bytes per selected row: 2 + 8*NACOL written and read back; lookups
+// cost LDS cycles only.
+constexpr int kSliceBits = 16;
+constexpr int kSliceKeys = 1 << kSliceBits;
+constexpr int kSliceMaxF = 160;                  // slices: key range <= 160 * 65536
+constexpr int kSliceBlock = 1024;                // one workgroup per CU in both phases
+constexpr int kSliceTile = kSliceBlock * kFastR;  // 8192 probe rows per phase-A iteration
+constexpr int kSliceChunk = 32;                  // items per flushed chunk
+constexpr int kSliceStateWords = 3584;           // phase-B LDS aggregate states (n_slots * G)
 
-struct PartBufs {
-    void *key[kParts];             // uint32 key offsets (DIRECT) or int64 keys (PACKED)
-    int64_t *val[2][kParts];
-    unsigned long long *cursor;    // [0..8): fill cursors (phase A), [8..16): batch cursors (phase B)
-    uint64_t cap;                  // items per partition
-    uint64_t batch;                // phase B items per grab
-    float scale;                   // DIRECT: partition = key offset * scale
-    int32_t shift;                 // PACKED: partition = slot >> shift
-    uint32_t *overflow;
+// Workgroup barrier ordering LDS only: the next tile's global loads stay in
+// flight across it (__syncthreads also drains vmcnt).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct SliceRegions {
+    uint16_t *key;        // [grid][F][cap] key - kmin - slice * 2^16
+    int64_t *val;         // [grid][F][cap] aggregate input (NACOL == 1)
+    uint32_t *count;      // [grid][F]
+    uint32_t *overflow;   // set when a region fills up (skewed probe keys)
+    uint64_t cap;         // items per region, multiple of kSliceChunk
+    int32_t F;            // slices
+    int32_t _pad;
 };
 
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & 7u;
-}
-
-template <int NTERMS, int NACOL, bool KEY64, bool NT>
-__global__ __launch_bounds__(kBlock) void k_join_partition(FastIn in, PredTerms terms, HashTable t, int64_t n_tiles,
-                                                           PartBufs pb) {
-    typedef typename std::conditional<KEY64, int64_t, uint32_t>::type KeyT;
-    __shared__ uint32_t cnt[kParts], lofs[kParts];
-    __shared__ uint32_t s_total;
-    __shared__ unsigned long long base[kParts];
-    __shared__ KeyT skey[kFastTile];
-    __shared__ int64_t sval[NACOL > 0 ? NACOL : 1][kFastTile];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        if (threadIdx.x < kParts) cnt[threadIdx.x] = 0;
-        __syncthreads();
-        const int64_t b0 = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
-        FastTile<NTERMS, NACOL, NT> ft;
-        ft.load(in, terms, b0);
-        uint32_t sel = ft.sel;
-        uint32_t part[kFastR], pos[kFastR];
+template <int NTERMS, int NACOL, bool NT>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
+                                                                 int64_t n_tiles, SliceRegions rg) {
+    constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
+    constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
+    __shared__ uint32_t cnt[MAXF], lofs[MAXF], cn[MAXF], pos[MAXF], mpre[MAXF];
+    __shared__ uint32_t s_chunks;
+    __shared__ uint16_t chunk_slice[TILE / CH + MAXF];
+    __shared__ uint16_t st_key[TILE];
+    __shared__ int64_t st_v[VC ? TILE : 1];
+    __shared__ uint16_t c_key[MAXF * CH];
+    __shared__ int64_t c_v[VC ? MAXF * CH : 1];
+    const int F = rg.F;
+    const uint64_t cap = rg.cap;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < MAXF; i += kSliceBlock) cnt[i] = 0, cn[i] = 0, pos[i] = 0;
+    __syncthreads();
+    const uint64_t region0 = (uint64_t)blockIdx.x * F;
+    bool ovf = false;
+    FastTile<NTERMS, NACOL, NT> ft;
+    int64_t tile = blockIdx.x;
+    if (tile < n_tiles) ft.issue(in, tile * TILE + (int64_t)wave * (64 * R) + 2 * lane);
+    for (; tile < n_tiles; tile += gridDim.x) {
+        ft.eval(in, terms);
+        uint32_t sel = ft.sel, off[R], rk[R];
 #pragma unroll
-        for (int r = 0; r < kFastR; ++r) {
-            part[r] = 0;
-            pos[r] = 0;
+        for (int r = 0; r < R; ++r) {
+            const uint64_t o = (uint64_t)ft.k(r) - (uint64_t)kmin;  // out of range -> huge, dropped
+            off[r] = (uint32_t)o;
+            rk[r] = 0;
+            if (((sel >> r) & 1) && o < range) rk[r] = atomicAdd(&cnt[(uint32_t)o >> kSliceBits], 1u);
+            else sel &= ~(1u << r);
+        }
+        int64_t vcur[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) vcur[r] = VC ? ft.a(0, r) : 0;
+        lds_barrier();  // counts complete
+        if (wave == 0) {
+            // three consecutive slices per lane: exclusive scans of the staged
+            // counts (tile offsets) and of the whole chunks each slice flushes
+            uint32_t n3[3], m3[3], ns = 0, ms = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int b = lane * 3 + q;
+                n3[q] = b < F ? cnt[b] : 0u;
+                m3[q] = b < F ? (cn[b] + n3[q]) / CH : 0u;
+                ns += n3[q];
+                ms += m3[q];
+            }
+            uint32_t ni = ns, mi = ms;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t a = __shfl_up(ni, d, 64), c = __shfl_up(mi, d, 64);
+                if (lane >= d) ni += a, mi += c;
+            }
+            uint32_t no = ni - ns, mo = mi - ms;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int b = lane * 3 + q;
+                if (b < MAXF) lofs[b] = no, mpre[b] = mo;
+                no += n3[q];
+                mo += m3[q];
+            }
+            if (lane == 63) s_chunks = mi;
+        }
+        lds_barrier();  // offsets ready
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
             if (!((sel >> r) & 1)) continue;
-            const int64_t k = ft.k(r);
-            if (k < t.kmin || k > t.kmax) {  // cannot match: drop here
-                sel &= ~(1u << r);
-                continue;
+            const uint32_t s = lofs[off[r] >> kSliceBits] + rk[r];
+            st_key[s] = (uint16_t)(off[r] & (kSliceKeys - 1));
+            if (VC) st_v[s] = vcur[r];
+        }
+        if (tid < F) {
+            const uint32_t m = (cn[tid] + cnt[tid]) / CH, m0 = mpre[tid];
+            for (uint32_t j = 0; j < m; ++j) chunk_slice[m0 + j] = (uint16_t)tid;
+        }
+        if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
+        lds_barrier();  // staged
+        {
+            // whole chunks: carried items first, then this tile's; one chunk per half-wave
+            const uint32_t M = s_chunks;
+            const uint32_t kx0 = tid & (CH - 1);
+            for (uint32_t c = tid / CH; c < M; c += kSliceBlock / CH) {
+                const uint32_t b = chunk_slice[c];
+                const uint32_t kx = (c - mpre[b]) * CH + kx0, cb = cn[b];
+                uint16_t kv;
+                int64_t vv = 0;
+                if (kx < cb) {
+                    kv = c_key[b * CH + kx];
+                    if (VC) vv = c_v[b * CH + kx];
+                } else {
+                    kv = st_key[lofs[b] + kx - cb];
+                    if (VC) vv = st_v[lofs[b] + kx - cb];
+                }
+                const uint64_t dst = (uint64_t)pos[b] + kx;
+                if (dst < cap) {
+                    const uint64_t o = (region0 + b) * cap + dst;
+                    rg.key[o] = kv;
+                    if (VC) __builtin_nontemporal_store(vv, rg.val + o);
+                } else {
+                    ovf = true;
+                }
             }
-            uint32_t p;
-            if (KEY64) {
-                p = (uint32_t)((hash64((uint64_t)k) & t.mask) >> pb.shift);
-            } else {
-                p = (uint32_t)((float)((uint64_t)k - (uint64_t)t.kmin) * pb.scale);
-                p = p > kParts - 1 ? kParts - 1 : p;
+        }
+        lds_barrier();  // flushed: carries may be replaced
+        for (int p = tid; p < F * CH; p += kSliceBlock) {
+            const int b = p / CH, kx = p % CH;
+            const uint32_t cb = cn[b], nb = cnt[b], T = cb + nb, L = T % CH;
+            int src = -1;
+            if (T < CH) {
+                if (kx >= (int)cb && kx < (int)T) src = (int)(lofs[b] + kx - cb);  // append
+            } else if (kx < (int)L) {
+                src = (int)(lofs[b] + nb - L + kx);  // the tile's last L items
             }
-            part[r] = p;
-            pos[r] = atomicAdd(&cnt[p], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int p = 0; p < kParts; ++p) {
-                lofs[p] = acc;
-                acc += cnt[p];
+            if (src >= 0) {
+                c_key[b * CH + kx] = st_key[src];
+                if (VC) c_v[b * CH + kx] = st_v[src];
             }
-            s_total = acc;
         }
-        if (threadIdx.x < kParts) {
-            const uint32_t c = cnt[threadIdx.x];
-            base[threadIdx.x] = c ? atomicAdd(&pb.cursor[threadIdx.x], (unsigned long long)c) : 0ull;
+        lds_barrier();  // carries updated
+        if (tid < F) {
+            const uint32_t T = cn[tid] + cnt[tid];
+            pos[tid] += (T / CH) * CH;
+            cn[tid] = T % CH;
+            cnt[tid] = 0;
         }
-        __syncthreads();
-        // stage the tile's rows in LDS grouped by partition ...
-#pragma unroll
-        for (int r = 0; r < kFastR; ++r) {
-            if (!((sel >> r) & 1)) continue;
-            const uint32_t s = lofs[part[r]] + pos[r];
-            const int64_t k = ft.k(r);
-            skey[s] = KEY64 ? (KeyT)k : (KeyT)((uint64_t)k - (uint64_t)t.kmin);
-#pragma unroll
-            for (int c = 0; c < NACOL; ++c) sval[c][s] = ft.ac[c][r >> 1][r & 1];
+        lds_barrier();
+    }
+    for (int p = tid; p < F * CH; p += kSliceBlock) {  // partial last chunks
+        const int b = p / CH, kx = p % CH;
+        if (kx >= (int)cn[b]) continue;
+        const uint64_t dst = (uint64_t)pos[b] + kx;
+        if (dst < cap) {
+            const uint64_t o = (region0 + b) * cap + dst;
+            rg.key[o] = c_key[b * CH + kx];
+            if (VC) rg.val[o] = c_v[b * CH + kx];
+        } else {
+            ovf = true;
         }
-        __syncthreads();
-        // ... and copy them out: consecutive lanes write consecutive slots, so
-        // every partition's rows leave as contiguous, coalesced runs
-        const uint32_t total = s_total;
-        for (uint32_t i = threadIdx.x; i < total; i += kBlock) {
-            uint32_t p = 0;
-#pragma unroll
-            for (int q = 1; q < kParts; ++q) p += lofs[q] <= i ? 1u : 0u;  // last partition starting at or before i
-            const uint64_t dst = base[p] + (i - lofs[p]);
-            if (dst >= pb.cap) {
-                *pb.overflow = 1u;
-                continue;
-            }
-            ((KeyT *)pb.key[p])[dst] = skey[i];
-#pragma unroll
-            for (int c = 0; c < NACOL; ++c) pb.val[c][p][dst] = sval[c][i];
-        }
-        __syncthreads();
+    }
+    if (ovf) *rg.overflow = 1u;
+    for (int b = tid; b < F; b += kSliceBlock) {
+        const uint64_t n = (uint64_t)pos[b] + cn[b];
+        rg.count[region0 + b] = (uint32_t)(n < cap ? n : cap);
     }
 }
 
-template <int NACOL, bool KEY64>
-__global__ __launch_bounds__(kBlock) void k_join_probe_parts(PartBufs pb, FastIn in, HashTable t, AggSpecs specs,
-                                                             int64_t G, uint64_t *__restrict__ gstates_all) {
+// Phase B.  Region slots are enumerated slice-major (slot = b * nreg + r);
+// workgroup w drains the contiguous slot range [w*T/grid, (w+1)*T/grid), so it
+// loads at most a few slices, and its waves take the range's regions in turn.
+template <int NACOL>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, HashTable t, FastIn in,
+                                                             AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
+    constexpr int VC = NACOL > 0 ? 1 : 0;
+    __shared__ __attribute__((aligned(16))) uint16_t tslice[kSliceKeys];
+    __shared__ uint64_t lst[kSliceStateWords];
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int W = kSliceBlock / 64;
     const int64_t words = (int64_t)specs.n_slots * G;
-    unsigned long long *grab = (unsigned long long *)&lds[words];
-    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = 0;
+    for (int64_t i = tid; i < words; i += kSliceBlock) lst[i] = 0;
     __syncthreads();
     for (int a = 0; a < specs.n; ++a) {
         const AggSpec sp = specs.a[a];
         if (sp.kind == AK_MIN || sp.kind == AK_MAX)
-            for (int64_t g = threadIdx.x; g < G; g += blockDim.x) lds[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
+            for (int64_t g = tid; g < G; g += kSliceBlock) lst[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
     }
-    __syncthreads();
-    const uint32_t x = xcc_id();
-    for (int k = 0; k < kParts; ++k) {
-        const uint32_t p = (x + k) & (kParts - 1);
-        unsigned long long filled = __hip_atomic_load(&pb.cursor[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t n_p = filled < pb.cap ? filled : pb.cap;
-        for (;;) {
-            if (threadIdx.x == 0) *grab = atomicAdd(&pb.cursor[kParts + p], (unsigned long long)pb.batch);
-            __syncthreads();
-            const uint64_t b = *grab;
-            __syncthreads();
-            if (b >= n_p) break;
-            const uint64_t e = b + pb.batch < n_p ? b + pb.batch : n_p;
-            constexpr int U = kPartUnroll;
-            for (uint64_t i0 = b + threadIdx.x; i0 < e; i0 += U * kBlock) {
-                int64_t kk[U];
-                int64_t vv[NACOL > 0 ? NACOL : 1][U];
-                uint32_t live = 0;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint64_t i = i0 + (uint64_t)u * kBlock;
-                    if (i < e) live |= 1u << u;
-                    const uint64_t ii = i < e ? i : b;
-                    kk[u] = KEY64 ? __builtin_nontemporal_load(&((const int64_t *)pb.key[p])[ii])
-                                  : (int64_t)((uint64_t)t.kmin +
-                                              __builtin_nontemporal_load(&((const uint32_t *)pb.key[p])[ii]));
-#pragma unroll
-                    for (int c = 0; c < NACOL; ++c) vv[c][u] = __builtin_nontemporal_load(&pb.val[c][p][ii]);
+    const int F = rg.F;
+    const int64_t T = (int64_t)F * nreg;
+    const int64_t s0 = (int64_t)blockIdx.x * T / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+    for (int64_t sb = s0; sb < s1;) {
+        const int b = (int)(sb / nreg);
+        const int64_t se = std::min<int64_t>(s1, (int64_t)(b + 1) * nreg);
+        __syncthreads();
+        {
+            const uint64_t k0 = (uint64_t)b << kSliceBits;
+            const uint64_t nk = t.range - k0 < (uint64_t)kSliceKeys ? t.range - k0 : (uint64_t)kSliceKeys;
+            for (int i = tid * 8; i < kSliceKeys; i += kSliceBlock * 8) {
+                v4u32 w = {0u, 0u, 0u, 0u};
+                if ((uint64_t)i + 8 <= nk) {
+                    w = *(const v4u32 *)(t.payload16 + k0 + i);
+                } else {
+                    for (int q = 0; q < 8; ++q)
+                        if ((uint64_t)(i + q) < nk) w[q >> 1] |= (uint32_t)t.payload16[k0 + i + q] << ((q & 1) * 16);
                 }
-                uint32_t gid[U];
-                uint32_t hit = 0;
+                *(v4u32 *)&tslice[i] = w;
+            }
+        }
+        __syncthreads();
+        for (int64_t s = sb + wave; s < se; s += W) {
+            const uint64_t reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
+            const uint32_t n_r = rg.count[reg];
+            const uint16_t *kp = rg.key + reg * rg.cap;
+            const int64_t *vp = VC ? rg.val + reg * rg.cap : nullptr;
+            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
+                uint32_t e[8];
+                int64_t v[8];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    gid[u] = 0;
-                    if (((live >> u) & 1) && probe_unique(t, kk[u], gid[u])) hit |= 1u << u;
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t i = i0 + j * 64 + lane;
+                    const uint32_t ii = i < n_r ? i : 0u;
+                    e[j] = __builtin_nontemporal_load(kp + ii);
+                    v[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
                 }
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (!((hit >> u) & 1)) continue;
-                    const uint32_t g = gid[u];
-                    atomicAdd((unsigned long long *)&lds[g], 1ull);
+                for (int j = 0; j < 8; ++j) e[j] = (i0 + j * 64 + lane < n_r) ? (uint32_t)tslice[e[j]] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (!e[j]) continue;
+                    const uint32_t g = e[j] - 1u;
+                    atomicAdd((unsigned long long *)&lst[g], 1ull);
                     for (int a = 0; a < specs.n; ++a) {
                         const AggSpec sp = specs.a[a];
                         if (sp.kind == AK_COUNT) continue;
-                        const int cs = in.agg_colslot[a];
-                        int64_t v = (NACOL > 1 && cs == 1) ? vv[NACOL > 1 ? 1 : 0][u] : vv[0][u];
-                        agg_apply<true>(sp.kind, &lds[(int64_t)sp.val_slot * G + g], agg_input(sp.kind, sp.in_type, v));
+                        agg_apply<true>(sp.kind, &lst[(int64_t)sp.val_slot * G + g], agg_input(sp.kind, sp.in_type, v[j]));
                     }
                 }
             }
         }
+        sb = se;
     }
     __syncthreads();
-    for (int64_t g = threadIdx.x; g < G; g += blockDim.x) {
-        uint64_t rows = lds[g];
+    for (int64_t g = tid; g < G; g += kSliceBlock) {
+        const uint64_t rows = lst[g];
         if (!rows) continue;
         atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
         for (int a = 0; a < specs.n; ++a) {
             const AggSpec sp = specs.a[a];
             if (sp.kind != AK_COUNT)
-                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lds[(int64_t)sp.val_slot * G + g]);
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * G + g]);
         }
     }
 }
@@ -1032,138 +1123,70 @@ static uint64_t table_bytes(const HashTable &t) {
     return (t.mask + 1) * 16;
 }
 
-// XCD-partitioned probe (phase A + phase B).  Returns 1 when it ran, 0 when
-// not eligible, and falls back (re-initialising the states) on partition
-// overflow (heavily skewed keys).
-static int try_partitioned_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp,
-                                const GidSource &src, const AggSpecs &specs, int64_t G, uint64_t *states,
-                                uint32_t *err, size_t lds_bytes, int per_cu, bool *overflowed) {
-    *overflowed = false;
-    if (std::getenv("QEH_NO_PART")) return 0;
+// LDS-slice partitioned probe (k_slice_partition + k_slice_probe) for unique
+// direct u16 tables past an XCD's L2.  Returns 1 when it ran; 0 when not
+// eligible, or when a region overflowed (probe keys skewed onto few slices),
+// in which case the states are re-initialised for the single pass.
+static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
+                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes) {
+    if (std::getenv("QEH_NO_SLICES")) return 0;
     FastIn in;
     int nterms, nacol;
     if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol)) return 0;
     const HashTable &t = src.jt;
-    const uint64_t min_bytes = std::getenv("QEH_PART_MIN_BYTES") ? std::strtoull(std::getenv("QEH_PART_MIN_BYTES"), nullptr, 10)
-                                                                 : UINT64_MAX;  // opt-in until it beats the single pass
-    if (table_bytes(t) < min_bytes) return 0;  // fits one XCD's L2 well enough: single pass
-    const int64_t n_tiles = n / kFastTile;
+    if (t.kind != TK_DIRECT || !t.payload16 || nacol > 1) return 0;
+    if ((int64_t)specs.n_slots * G > kSliceStateWords) return 0;
+    const uint64_t F = (t.range + kSliceKeys - 1) >> kSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return 0;
+    // below ~1.5 L2s the single pass's lookups mostly hit L2 and it wins
+    uint64_t min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
+    if (table_bytes(t) < min_bytes) return 0;
+    const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return 0;
-    const int64_t rows = n_tiles * kFastTile;
-    const bool key64 = t.kind == TK_PACKED;
-    // QEH_PART_CHUNK = fact rows per pipeline chunk (0: one chunk).  Chunks run
-    // phase A on the main stream and phase B on the auxiliary stream, two
-    // partition-buffer slots in flight, so B(c) overlaps A(c+1) and a chunk's
-    // records can still be in the Infinity Cache when phase B reads them.
-    int64_t chunk_tiles = n_tiles;
-    if (const char *e = std::getenv("QEH_PART_CHUNK")) {
-        const int64_t cr = std::strtoll(e, nullptr, 10);
-        if (cr > 0) chunk_tiles = std::max<int64_t>(1, cr / kFastTile);
-    }
-    const int64_t n_chunks = (n_tiles + chunk_tiles - 1) / chunk_tiles;
-    const int n_slots = n_chunks > 1 ? 2 : 1;
-    const int64_t chunk_rows = std::min<int64_t>(chunk_tiles, n_tiles) * kFastTile;
-    const uint64_t cap = (uint64_t)(chunk_rows / kParts) + (uint64_t)(chunk_rows / kParts) / 4 + 65536;
-    const size_t kb = key64 ? 8 : 4;
-    DevBuf kbuf, vbuf, cur;
-    if (kbuf.alloc(ctx, cap * kb * kParts * n_slots) != QEH_OK) return 0;
-    if (nacol && vbuf.alloc(ctx, cap * 8 * kParts * nacol * n_slots) != QEH_OK) return 0;
-    const size_t cur_bytes = 2 * kParts * 8 + 64;  // cursors + overflow word, per slot
-    if (cur.alloc(ctx, cur_bytes * n_slots) != QEH_OK) return 0;
-    PartBufs pbs[2]{};
-    int lg = 0;
-    while ((1ull << lg) < t.mask + 1) ++lg;
-    for (int sl = 0; sl < n_slots; ++sl) {
-        PartBufs &pb = pbs[sl];
-        pb.cap = cap;
-        pb.batch = n_chunks > 1 ? 2048 : kPartBatch;
-        if (const char *e = std::getenv("QEH_PART_BATCH")) pb.batch = std::strtoull(e, nullptr, 10);
-        for (int p = 0; p < kParts; ++p) {
-            pb.key[p] = (char *)kbuf.p + ((size_t)sl * kParts + p) * cap * kb;
-            for (int c = 0; c < nacol; ++c)
-                pb.val[c][p] = (int64_t *)vbuf.p + (((size_t)sl * nacol + c) * kParts + p) * cap;
-        }
-        pb.cursor = (unsigned long long *)(cur.as<char>() + sl * cur_bytes);
-        pb.overflow = (uint32_t *)(cur.as<char>() + sl * cur_bytes + 2 * kParts * 8);
-        pb.scale = (float)kParts / (float)(t.range ? t.range : 1);
-        pb.shift = lg > 3 ? lg - 3 : 0;
-    }
-    if (hipMemsetAsync(cur.p, 0, cur_bytes * n_slots, ctx->stream) != hipSuccess) return 0;
-    if (n_chunks > 1 && !ctx->aux_stream &&
-        hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking) != hipSuccess)
-        return 0;
-    hipEvent_t evA[2] = {}, evB[2] = {};
-    if (n_chunks > 1)
-        for (int sl = 0; sl < 2; ++sl) {
-            hipEventCreateWithFlags(&evA[sl], hipEventDisableTiming);
-            hipEventCreateWithFlags(&evB[sl], hipEventDisableTiming);
-        }
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    // capacity for every row selected with keys uniform over the slices, +25 %
+    const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
+    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
+    cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
+    const uint64_t nreg = (uint64_t)grid * F;
+    DevBuf kbuf, vbuf, cbuf;
+    if (kbuf.alloc(ctx, nreg * cap * 2 + 64) != QEH_OK) return 0;
+    if (nacol && vbuf.alloc(ctx, nreg * cap * 8 + 64) != QEH_OK) return 0;
+    if (cbuf.alloc(ctx, nreg * 4 + 64) != QEH_OK) return 0;
+    SliceRegions rg{};
+    rg.key = kbuf.as<uint16_t>();
+    rg.val = nacol ? vbuf.as<int64_t>() : nullptr;
+    rg.count = cbuf.as<uint32_t>();
+    rg.overflow = rg.count + nreg;
+    rg.cap = cap;
+    rg.F = (int32_t)F;
+    if (hipMemsetAsync(rg.overflow, 0, 4, ctx->stream) != hipSuccess) return 0;
     const bool nt = fast_nt_mode() == 1;
-    const int gridB = ctx->props.multiProcessorCount * std::max(1, per_cu);
-    const size_t shmB = lds_bytes + 16;
-    for (int64_t c = 0; c < n_chunks; ++c) {
-        const int sl = (int)(c % n_slots);
-        const PartBufs &pb = pbs[sl];
-        const int64_t t0 = c * chunk_tiles, nt_c = std::min<int64_t>(chunk_tiles, n_tiles - t0);
-        FastIn inc = in;
-        const int64_t off = t0 * kFastTile;
-        inc.key += off;
-        for (int i = 0; i < nterms; ++i) inc.term[i] += off;
-        for (int i = 0; i < nacol; ++i) inc.acol[i] += off;
-        hipStream_t sB = n_chunks > 1 ? ctx->aux_stream : ctx->stream;
-        if (c >= 2) {  // slot reuse: B(c-2) must be done; overflow flags are sticky per slot
-            hipStreamWaitEvent(ctx->stream, evB[sl], 0);
-            hipMemsetAsync(pb.cursor, 0, 2 * kParts * 8, ctx->stream);
-        }
-        {
-            KernelTimer kt(ctx, "join_partition");
-            const int grid = grid_for(ctx, nt_c * kFastTile, kFastTile, 8);
-#define QEH_PA(NTV, NAV, K64, NTB) \
-    hipLaunchKernelGGL((k_join_partition<NTV, NAV, K64, NTB>), dim3(grid), dim3(kBlock), 0, ctx->stream, inc, pp.terms, t, nt_c, pb)
-#define QEH_PA_NA(NTV, K64, NTB)                         \
-    if (nacol == 0) QEH_PA(NTV, 0, K64, NTB);            \
-    else if (nacol == 1) QEH_PA(NTV, 1, K64, NTB);       \
-    else QEH_PA(NTV, 2, K64, NTB);
-#define QEH_PA_NT(K64, NTB)                              \
-    if (nterms == 0) { QEH_PA_NA(0, K64, NTB) }          \
-    else if (nterms == 1) { QEH_PA_NA(1, K64, NTB) }     \
-    else { QEH_PA_NA(2, K64, NTB) }
-            if (key64) { if (nt) { QEH_PA_NT(true, true) } else { QEH_PA_NT(true, false) } }
-            else { if (nt) { QEH_PA_NT(false, true) } else { QEH_PA_NT(false, false) } }
-#undef QEH_PA_NT
-#undef QEH_PA_NA
-#undef QEH_PA
-        }
-        if (n_chunks > 1) {
-            hipEventRecord(evA[sl], ctx->stream);
-            hipStreamWaitEvent(sB, evA[sl], 0);
-        }
-        {
-#define QEH_PB(NAV, K64) \
-    hipLaunchKernelGGL((k_join_probe_parts<NAV, K64>), dim3(gridB), dim3(kBlock), shmB, sB, pb, in, t, specs, G, states)
-            if (key64) { if (nacol == 0) QEH_PB(0, true); else if (nacol == 1) QEH_PB(1, true); else QEH_PB(2, true); }
-            else { if (nacol == 0) QEH_PB(0, false); else if (nacol == 1) QEH_PB(1, false); else QEH_PB(2, false); }
-#undef QEH_PB
-        }
-        if (n_chunks > 1) hipEventRecord(evB[sl], sB);
-    }
-    if (n_chunks > 1) {
-        for (int sl = 0; sl < 2; ++sl) hipStreamWaitEvent(ctx->stream, evB[sl], 0);
-        for (int sl = 0; sl < 2; ++sl) {
-            hipEventDestroy(evA[sl]);
-            hipEventDestroy(evB[sl]);
-        }
-    }
-    QEH_HIP(hipGetLastError());
-    launch_tail(ctx, cols, n, rows, pp, src, specs, G, states, err, lds_bytes);
+#define QEH_SA(NTV, NAV, NTB)                                                                                  \
+    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
+                       pp.terms, t.kmin, t.range, n_tiles, rg)
+#define QEH_SA_NA(NTV, NTB)                    \
+    if (nacol == 0) QEH_SA(NTV, 0, NTB);       \
+    else QEH_SA(NTV, 1, NTB);
+#define QEH_SA_NT(NTB)                         \
+    if (nterms == 0) { QEH_SA_NA(0, NTB) }     \
+    else if (nterms == 1) { QEH_SA_NA(1, NTB) } \
+    else { QEH_SA_NA(2, NTB) }
+    if (nt) { QEH_SA_NT(true) } else { QEH_SA_NT(false) }
+#undef QEH_SA_NT
+#undef QEH_SA_NA
+#undef QEH_SA
+    const int gridB = ctx->props.multiProcessorCount;
+    if (nacol == 0)
+        hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G, states);
+    else
+        hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G, states);
+    if (hipGetLastError() != hipSuccess) return 0;
+    launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
     uint32_t of = 0;
-    for (int sl = 0; sl < n_slots; ++sl) {
-        uint32_t o = 0;
-        if (read_small(ctx, &o, pbs[sl].overflow, 4) != QEH_OK) return 0;
-        of |= o;
-    }
+    if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
     if (of) {
-        *overflowed = true;
         hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
                            ctx->stream, states, G, specs);
         return 0;
@@ -1247,11 +1270,10 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         KernelTimer kt(ctx, kname);
         if (gm == GM_ZERO) launch_agg_rows<GM_ZERO>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
         else if (gm == GM_JOIN) {
-            bool ovf = false;
-            if (lds && try_partitioned_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
-                                            lds_bytes, per_cu, &ovf) == 1) {
+            if (lds && try_slice_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
+                                      lds_bytes) == 1) {
             } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
-                                       lds_bytes, per_cu)))
+                                              lds_bytes, per_cu)))
                 launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
                                          states.as<uint64_t>(), errw.as<uint32_t>());
         }

@@ -141,30 +141,53 @@ def test_no_predicate_and_empty_inputs(ctx):
     assert len(gk[0][0]) == 0 and len(wk[0][0]) == 0
 
 
+V_AGGS = [(AF.Sum, 2), (AF.Count, 2), (AF.Avg, 2), (AF.Min, 2), (AF.Max, 2)]  # one aggregate column
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["direct", "packed"])
-def test_xcd_partitioned_probe(ctx, monkeypatch, table):
-    """Phase A (filter + partition by table slice) / phase B (XCD-affine probe)
-    forced on small tables; ragged tail handled by the generic kernel."""
-    monkeypatch.setenv("QEH_PART_MIN_BYTES", "0")
-    monkeypatch.setenv("QEH_FORCE_TABLE", table)
-    x, k, v, dk, dg = metric_data(1_000_003, 100_000, 1024)
+@pytest.mark.parametrize("n_fact,n_dim,groups,key0,pred,aggs", [
+    (1_000_003, 100_000, 1024, 0, PRED, V_AGGS),                  # 2 slices, ragged tail
+    (700_001, 300_001, 700, -12_345, PRED, AGGS),                 # 5 slices, last one partial, negative kmin
+    (500_000, 200_000, 1024, 7, None, AGGS),                      # no predicate
+    (400_000, 70_000, 300, 0, binop(col(0), BinaryOp.Greater, lit(20)) & binop(col(0), BinaryOp.Less, lit(80)),
+     [(AF.Count, 2)]),                                            # two terms; COUNT only: keys-only exchange
+])
+def test_slice_partitioned_probe(ctx, monkeypatch, n_fact, n_dim, groups, key0, pred, aggs):
+    """Phase A (filter + stage by 64 Ki-key table slice + chunked region
+    writes) / phase B (slice in LDS, LDS lookups and states), forced on small
+    tables; misses below and above the key range; ragged tail by the generic
+    kernel."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, groups)
+    k = k + key0
+    dk = dk + key0
+    k[::97] = key0 - 1 - k[::97]       # below kmin
+    k[5::101] = key0 + n_dim + k[5::101]  # above kmax
     probe = [(x, None), (k, None), (v, None)]
-    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Avg, 2), (AF.Min, 0), (AF.Max, 2), (AF.Sum, 0)]
-    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
-    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0, 2])
+    gk, ga, wk, wa = run_both(ctx, probe, 1, pred, (dk, None), [(dg, None)], aggs)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[j for j, (f, c) in enumerate(aggs) if f in (AF.Sum, AF.Avg)])
 
 
 @pytest.mark.gpu
-def test_xcd_partition_overflow_falls_back(ctx, monkeypatch):
-    """Every probe key in one table slice overflows its partition: the
-    operator must re-run on the single-pass kernel and stay exact."""
-    monkeypatch.setenv("QEH_PART_MIN_BYTES", "0")
+def test_slice_probe_metric_table_default_threshold(ctx):
+    """The BASELINE shape at 1/50 scale: 20M fact rows x 10M-key dim (20 MB u16
+    table), slice path chosen by default."""
+    x, k, v, dk, dg = metric_data(20_000_000, 10_000_000, 1024)
+    probe = [(x, None), (k, None), (v, None)]
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+def test_slice_overflow_falls_back(ctx, monkeypatch):
+    """Every probe key in one table slice overflows its regions: the operator
+    must re-run on the single-pass kernel and stay exact."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
     rng = np.random.default_rng(5)
-    n, nd = 600_000, 80_000
+    n, nd = 600_000, 400_000
     dk = rng.permutation(nd).astype(np.int64)
     dg = rng.integers(0, 100, nd)
-    k = rng.integers(0, nd // 16, n)  # all in partition 0
+    k = rng.integers(0, 60_000, n)  # all in slice 0
     x = np.full(n, 99, np.int64)
     v = rng.random(n)
     gk, ga, wk, wa = run_both(ctx, [(x, None), (k, None), (v, None)], 1, PRED, (dk, None), [(dg, None)], AGGS)
