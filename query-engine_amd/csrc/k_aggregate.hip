@@ -1163,6 +1163,8 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     rg.F = (int32_t)F;
     if (hipMemsetAsync(rg.overflow, 0, 4, ctx->stream) != hipSuccess) return 0;
     const bool nt = fast_nt_mode() == 1;
+    {
+    KernelTimer kta(ctx, "slice_partition");
 #define QEH_SA(NTV, NAV, NTB)                                                                                  \
     hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
                        pp.terms, t.kmin, t.range, n_tiles, rg)
@@ -1177,11 +1179,17 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
 #undef QEH_SA_NT
 #undef QEH_SA_NA
 #undef QEH_SA
-    const int gridB = ctx->props.multiProcessorCount;
-    if (nacol == 0)
-        hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G, states);
-    else
-        hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G, states);
+    }
+    {
+        KernelTimer ktb(ctx, "slice_probe");
+        const int gridB = ctx->props.multiProcessorCount;
+        if (nacol == 0)
+            hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G,
+                               states);
+        else
+            hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G,
+                               states);
+    }
     if (hipGetLastError() != hipSuccess) return 0;
     launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
     uint32_t of = 0;

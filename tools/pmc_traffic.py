@@ -6,7 +6,10 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per
 128-B fabric request of a wide streaming read, i.e. reads exactly half the
 bytes of a 16-B-per-lane coalesced stream -> doubled here; WRITE_SIZE is
 exact for 16-B streaming stores.  Units of both counters are KiB.
-Writes <dir>/traffic.json and prints a table."""
+Writes <dir>/traffic.json and prints a table.  With --emit FILE --rows N it
+also writes the bench-readable per-step HBM bytes of the metric query's probe
+pipeline (k_slice_partition + k_slice_probe, or the single-pass
+k_join_agg_fast, plus the ragged-tail k_agg_rows) to FILE."""
 import csv
 import glob
 import json
@@ -51,7 +54,37 @@ def main(d):
                       "hbm_bytes": 2 * f + w}
         print(f"{k[:80]:80s} fetch_raw={f / 1e9:8.3f} GB  fetch_x2={2 * f / 1e9:8.3f} GB  write={w / 1e9:8.3f} GB")
     json.dump({"kernels": summary, "stats": stats}, open(os.path.join(d, "traffic.json"), "w"), indent=1)
+    return summary, stats
+
+
+PIPELINE = ("k_slice_partition", "k_slice_probe", "k_join_agg_fast", "k_agg_rows<1")
+
+
+def emit(summary, stats, path, rows):
+    """Per-launch HBM bytes and average durations of the probe pipeline's kernels."""
+    comp, dur = {}, {}
+    for k, v in summary.items():
+        if any(p in k for p in PIPELINE):
+            comp[k] = v["hbm_bytes"]
+    for r in stats:
+        k = short(r["Name"])
+        if any(p in k for p in PIPELINE):
+            dur[k] = float(r.get("AverageNs", 0) or 0) / 1e6
+    out = {"rows": rows, "kernel": "join_filter_aggregate", "hbm_bytes_per_launch": sum(comp.values()),
+           "components_hbm_bytes": comp, "components_avg_ms": dur,
+           "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, mean per dispatch, summed over the "
+                   "pipeline's kernels (one dispatch each per query)"}
+    json.dump(out, open(path, "w"), indent=1)
+    print("emitted", path, json.dumps(out))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--emit")
+    ap.add_argument("--rows", type=int, default=1_000_000_000)
+    a = ap.parse_args()
+    summary, stats = main(a.dir)
+    if a.emit:
+        emit(summary, stats, a.emit, a.rows)

@@ -18,5 +18,5 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
     > "$OUT/fetch.log" 2>&1 || { echo "FETCH_SIZE pass failed"; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- "${BENCH[@]}" \
     > "$OUT/write.log" 2>&1 || { echo "WRITE_SIZE pass failed"; exit 1; }
-python3 "$ROOT/tools/pmc_traffic.py" "$OUT" > "$OUT/summary.txt" 2>&1 || { echo "parse failed"; cat "$OUT/summary.txt"; exit 1; }
+python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --emit "$OUT/traffic_latest.json" > "$OUT/summary.txt" 2>&1 || { echo "parse failed"; cat "$OUT/summary.txt"; exit 1; }
 cat "$OUT/summary.txt"
