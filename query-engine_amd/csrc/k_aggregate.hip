@@ -490,11 +490,12 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
 // workgroup w drains the contiguous slot range [w*T/grid, (w+1)*T/grid), so it
 // loads at most a few slices, and its waves take the range's regions in turn.
 template <int NACOL>
-__global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, HashTable t, FastIn in,
+__global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
                                                              AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
     constexpr int VC = NACOL > 0 ? 1 : 0;
     __shared__ __attribute__((aligned(16))) uint16_t tslice[kSliceKeys];
     __shared__ uint64_t lst[kSliceStateWords];
+    uint32_t *lcnt = (uint32_t *)lst;
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int W = kSliceBlock / 64;
@@ -508,12 +509,26 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     }
     const int F = rg.F;
     const int64_t T = (int64_t)F * nreg;
-    const int64_t s0 = (int64_t)blockIdx.x * T / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+    // splits == 0: one contiguous slot range per workgroup; else units of
+    // nreg/splits regions of one slice dealt round-robin
+    const int64_t units = splits ? (int64_t)F * splits : (int64_t)gridDim.x;
+    int cur_b = -1;
+    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    int64_t s0, s1;
+    if (splits) {
+        const int64_t ub = u / splits, sp = u % splits;
+        s0 = ub * nreg + sp * nreg / splits;
+        s1 = ub * nreg + (sp + 1) * nreg / splits;
+    } else {
+        s0 = u * T / gridDim.x;
+        s1 = (u + 1) * T / gridDim.x;
+    }
     for (int64_t sb = s0; sb < s1;) {
         const int b = (int)(sb / nreg);
         const int64_t se = std::min<int64_t>(s1, (int64_t)(b + 1) * nreg);
         __syncthreads();
-        {
+        if (b != cur_b) {
+            cur_b = b;
             const uint64_t k0 = (uint64_t)b << kSliceBits;
             const uint64_t nk = t.range - k0 < (uint64_t)kSliceKeys ? t.range - k0 : (uint64_t)kSliceKeys;
             for (int i = tid * 8; i < kSliceKeys; i += kSliceBlock * 8) {
@@ -545,24 +560,42 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) e[j] = (i0 + j * 64 + lane < n_r) ? (uint32_t)tslice[e[j]] : 0u;
+                // aggregate kinds are uniform: switch once per aggregate, then
+                // issue the 8 items' LDS atomics back to back
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    if (!e[j]) continue;
-                    const uint32_t g = e[j] - 1u;
-                    atomicAdd((unsigned long long *)&lst[g], 1ull);
-                    for (int a = 0; a < specs.n; ++a) {
-                        const AggSpec sp = specs.a[a];
-                        if (sp.kind == AK_COUNT) continue;
-                        agg_apply<true>(sp.kind, &lst[(int64_t)sp.val_slot * G + g], agg_input(sp.kind, sp.in_type, v[j]));
+                for (int j = 0; j < 8; ++j)  // row counts as u32 in slot 0's words (< 2^32 rows per workgroup)
+                    if (e[j]) atomicAdd(lcnt + (e[j] - 1u), 1u);
+                for (int a = 0; a < specs.n; ++a) {
+                    const AggSpec sp = specs.a[a];
+                    uint64_t *st = lst + (int64_t)sp.val_slot * G - 1;  // indexed by entry = gid + 1
+                    switch (sp.kind) {
+                        case AK_SUM_F:
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) atomicAdd((double *)&st[e[j]], as_f64(v[j]));
+                            break;
+                        case AK_SUM_I:
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) atomicAdd((unsigned long long *)&st[e[j]], (unsigned long long)v[j]);
+                            break;
+                        case AK_MIN:
+                        case AK_MAX:
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) agg_apply<true>(sp.kind, &st[e[j]], agg_input(sp.kind, sp.in_type, v[j]));
+                            break;
+                        default: break;  // COUNT: the row count slot
                     }
                 }
             }
         }
         sb = se;
     }
+    }
     __syncthreads();
     for (int64_t g = tid; g < G; g += kSliceBlock) {
-        const uint64_t rows = lst[g];
+        const uint64_t rows = lcnt[g];
         if (!rows) continue;
         atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
         for (int a = 0; a < specs.n; ++a) {
@@ -1183,12 +1216,14 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     {
         KernelTimer ktb(ctx, "slice_probe");
         const int gridB = ctx->props.multiProcessorCount;
+        int splits = 0;
+        if (const char *e = std::getenv("QEH_SLICE_SPLITS")) splits = std::atoi(e);
         if (nacol == 0)
-            hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G,
-                               states);
+            hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, t, in,
+                               specs, G, states);
         else
-            hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, in, specs, G,
-                               states);
+            hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, t, in,
+                               specs, G, states);
     }
     if (hipGetLastError() != hipSuccess) return 0;
     launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);

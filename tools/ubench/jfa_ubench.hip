@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_phaseb(const uint32_t *__restrict__ 
 template <bool NTS>
 __global__ __launch_bounds__(kBlock) void k_mixed(const int64_t *__restrict__ x, const int64_t *__restrict__ k,
                                                   const int64_t *__restrict__ v, int64_t n_tiles, int64_t *__restrict__ ov,
-                                                  uint16_t *__restrict__ ok) {
+                                                  uint16_t *__restrict__ ok, int64_t ring_items = 0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const int64_t base = tile * kTile + (int64_t)wave * (64 * kR) + 2 * lane;
@@ -196,7 +196,8 @@ __global__ __launch_bounds__(kBlock) void k_mixed(const int64_t *__restrict__ x,
 #pragma unroll
         for (int j = 0; j < kPairs; ++j) vv[j] = ld2(v + base + j * 128);
         // 4 output items per lane: v (32 B) + keys (8 B)
-        const int64_t ob = (tile * kTile) / 2 + (int64_t)wave * (64 * kR / 2) + 4 * lane;
+        int64_t ob = (tile * kTile) / 2 + (int64_t)wave * (64 * kR / 2) + 4 * lane;
+        if (ring_items) ob %= ring_items;  // writes wrap around a small ring
         v2i64 o0 = {vv[0][0] + xx[0][0], vv[1][0] + xx[1][0]}, o1 = {vv[2][0] + xx[2][0], vv[3][0] + xx[3][0]};
         if (NTS) {
             __builtin_nontemporal_store(o0, (v2i64 *)(ov + ob));
@@ -270,9 +271,18 @@ int main(int argc, char **argv) {
             report("mixed, nontemporal stores",
                    time_it([&] { hipLaunchKernelGGL((k_mixed<true>), dim3(grid), dim3(kBlock), 0, 0, x, k, v, n_tiles, ov, okk); }, reps));
         }
+        for (int64_t ring_mb : {16, 64, 128, 512}) {
+            const int64_t ring = ring_mb * (1 << 20) / 8;
+            char name[96];
+            std::snprintf(name, sizeof name, "mixed, writes into a %lld MB ring", (long long)ring_mb);
+            report(name, time_it([&] { hipLaunchKernelGGL((k_mixed<false>), dim3(cus * 8), dim3(kBlock), 0, 0, x, k, v, n_tiles, ov, okk, ring); }, reps));
+            std::snprintf(name, sizeof name, "mixed NT, writes into a %lld MB ring", (long long)ring_mb);
+            report(name, time_it([&] { hipLaunchKernelGGL((k_mixed<true>), dim3(cus * 8), dim3(kBlock), 0, 0, x, k, v, n_tiles, ov, okk, ring); }, reps));
+        }
         CK(hipFree(ov));
         CK(hipFree(okk));
     }
+    if (argc > 4) return 0;  // mixed-traffic section only
     for (int per_cu : {4, 8}) {
         const int grid = cus * per_cu;
         std::printf("-- fused, %d workgroups/CU\n", per_cu);
