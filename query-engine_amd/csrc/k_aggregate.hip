@@ -1656,11 +1656,13 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
 
     // build side: dense group ids of the build rows, then the join table with gid payloads
     GroupTable gt;
-    DevBuf gid_of_row;
-    QEH_TRY(assign_group_ids(ctx, build_group_keys, n_group_keys, build_key->length, &gt, &gid_of_row));
+    DevBuf slot_of_row;
+    QEH_TRY(group_slots_of_rows(ctx, build_group_keys, n_group_keys, build_key->length, &gt, &slot_of_row));
     BuiltTable bt;
-    QEH_TRY(build_join_table(ctx, *build_key, gid_of_row.as<uint32_t>(),
-                             (uint64_t)std::max<int64_t>(gt.groups - 1, 0), &bt));
+    RowPayload rp;  // payload = dense group id of the build row, read through its slot
+    rp.slot = slot_of_row.as<uint32_t>();
+    rp.dense = gt.dense.as<uint64_t>();
+    QEH_TRY(build_join_table(ctx, *build_key, rp, (uint64_t)std::max<int64_t>(gt.groups - 1, 0), &bt));
     GidSource src{};
     src.jt = bt.t;
     src.key_col = probe_key_idx;

@@ -24,15 +24,43 @@ struct MinMax {
     uint32_t bad;  // unsupported key type seen
 };
 
-__global__ void k_key_minmax(ColRef key, int64_t n, MinMax *out) {
+__global__ __launch_bounds__(kBlock) void k_key_minmax(ColRef key, int64_t n, MinMax *out) {
+    __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
+    __shared__ uint64_t scnt[kBlock / 64];
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     uint64_t cnt = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (!col_valid(key, i)) continue;
-        int64_t k = load_i64(key, i);
-        mn = k < mn ? k : mn;
-        mx = k > mx ? k : mx;
-        ++cnt;
+    if (key.validity == nullptr && key.dtype == QEH_DT_INT64 && ((uintptr_t)key.values & 15) == 0) {
+        // no nulls: 16-B loads, four in flight per thread, counted once
+        typedef long long v2 __attribute__((ext_vector_type(2)));
+        const v2 *kv = (const v2 *)key.values;
+        const int64_t pairs = n / 2, stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pairs; i += 4 * stride) {
+            v2 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = kv[i + u * stride < pairs ? i + u * stride : i];  // pad with pair i
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t a = q[u].x, b = q[u].y;
+                mn = a < mn ? a : mn;
+                mx = a > mx ? a : mx;
+                mn = b < mn ? b : mn;
+                mx = b > mx ? b : mx;
+            }
+        }
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t k = ((const int64_t *)key.values)[n - 1];
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+        cnt = (blockIdx.x == 0 && threadIdx.x == 0) ? (uint64_t)n : 0;
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            if (!col_valid(key, i)) continue;
+            int64_t k = load_i64(key, i);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+            ++cnt;
+        }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -42,7 +70,15 @@ __global__ void k_key_minmax(ColRef key, int64_t n, MinMax *out) {
         mx = b > mx ? b : mx;
         cnt += c;
     }
-    if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) smn[w] = mn, smx[w] = mx, scnt[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one set of atomics per workgroup
+        for (int i = 1; i < kBlock / 64; ++i) {
+            mn = smn[i] < mn ? smn[i] : mn;
+            mx = smx[i] > mx ? smx[i] : mx;
+            cnt += scnt[i];
+        }
         atomicMin((long long *)&out->mn, (long long)mn);
         atomicMax((long long *)&out->mx, (long long)mx);
         atomicAdd((unsigned long long *)&out->cnt, (unsigned long long)cnt);
@@ -57,21 +93,63 @@ __global__ void k_minmax_init(MinMax *m) {
 }
 
 // ---- inserts -------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t payload_of(const uint32_t *row_payload, int64_t row) {
-    return row_payload ? row_payload[row] : (uint32_t)row;
+__device__ __forceinline__ uint32_t payload_of(const RowPayload &rp, int64_t row) {
+    if (rp.ids) return rp.ids[row];
+    if (rp.slot) return (uint32_t)rp.dense[rp.slot[row]];
+    return (uint32_t)row;
 }
 
-__global__ void k_insert_direct(ColRef key, int64_t n, const uint32_t *row_payload, HashTable t, uint32_t *dup) {
+// DIRECT inserts: entry = payload + 1 at key - kmin, plain stores (any writer
+// of a duplicated key wins).  Duplicates are found afterwards by counting the
+// non-empty entries: fewer than valid build rows <=> some key repeats (the
+// table is then rebuilt hashed).  No returning atomics on the build path.
+__global__ void k_insert_direct(ColRef key, int64_t n, RowPayload rp, HashTable t) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
-        int64_t k = load_i64(key, i);
-        uint32_t e = payload_of(row_payload, i) + 1u;
-        uint32_t old = atomicCAS(&t.payload[(uint64_t)k - (uint64_t)t.kmin], 0u, e);
-        if (old != 0u) *dup = 1u;
+        t.payload[(uint64_t)load_i64(key, i) - (uint64_t)t.kmin] = payload_of(rp, i) + 1u;
     }
 }
 
-__global__ void k_insert_packed(ColRef key, int64_t n, const uint32_t *row_payload, HashTable t, uint32_t *dup) {
+__global__ void k_insert_direct16(ColRef key, int64_t n, RowPayload rp, HashTable t) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        t.payload16[(uint64_t)load_i64(key, i) - (uint64_t)t.kmin] = (uint16_t)(payload_of(rp, i) + 1u);
+    }
+}
+
+// Non-zero entries of a table of `n` words of `bytes` bytes (2 or 4), summed into *out.
+__global__ __launch_bounds__(kBlock) void k_count_nonzero(const void *__restrict__ table, uint64_t n, int bytes,
+                                                          unsigned long long *out) {
+    __shared__ uint64_t part[kBlock / 64];
+    uint64_t c = 0;
+    const uint64_t words = bytes == 2 ? n / 8 : n / 4;  // 16-B chunks
+    const uint4 *v = (const uint4 *)table;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 q = v[i];
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (bytes == 2) c += ((w[j] & 0xFFFFu) != 0u) + ((w[j] >> 16) != 0u);
+            else c += w[j] != 0u;
+        }
+    }
+    if (blockIdx.x == 0) {  // ragged tail
+        const uint64_t done = bytes == 2 ? words * 8 : words * 4;
+        for (uint64_t i = done + threadIdx.x; i < n; i += blockDim.x)
+            c += bytes == 2 ? ((const uint16_t *)table)[i] != 0 : ((const uint32_t *)table)[i] != 0u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int i = 0; i < kBlock / 64; ++i) t += part[i];
+        if (t) atomicAdd(out, (unsigned long long)t);
+    }
+}
+
+__global__ void k_insert_packed(ColRef key, int64_t n, RowPayload row_payload, HashTable t, uint32_t *dup) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
         int64_t k = load_i64(key, i);
@@ -89,7 +167,7 @@ __global__ void k_insert_packed(ColRef key, int64_t n, const uint32_t *row_paylo
     }
 }
 
-__global__ void k_insert_wide(ColRef key, int64_t n, const uint32_t *row_payload, HashTable t) {
+__global__ void k_insert_wide(ColRef key, int64_t n, RowPayload row_payload, HashTable t) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
         int64_t k = load_i64(key, i);
@@ -103,11 +181,6 @@ __global__ void k_insert_wide(ColRef key, int64_t n, const uint32_t *row_payload
             h = (h + 1) & t.mask;
         }
     }
-}
-
-__global__ void k_narrow_direct(const uint32_t *__restrict__ in, uint64_t n, uint16_t *__restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = (uint16_t)in[i];
 }
 
 // Duplicate detection for WIDE tables (separate launch: all slots are final).
@@ -132,7 +205,7 @@ static int bits_for(uint64_t v) {  // bits to represent values 0..v
     return b;
 }
 
-int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload, uint64_t payload_max,
+int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_payload, uint64_t payload_max,
                      BuiltTable *out, int force_kind) {
     QEH_TRY(check_column(key, "join key"));
     if (key.dtype != QEH_DT_INT64 && key.dtype != QEH_DT_INT32)
@@ -146,7 +219,7 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_pa
         KernelTimer kt(ctx, "join_build");
         hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
         if (n > 0)
-            hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, n, kBlock * 16, 4)), dim3(kBlock), 0, ctx->stream, kr, n,
+            hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, n, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kr, n,
                                mm.as<MinMax>());
     }
     QEH_HIP(hipGetLastError());
@@ -184,32 +257,38 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_pa
     if (kind == TK_DIRECT) {
         t.kind = TK_DIRECT;
         t.range = range;
-        QEH_TRY(out->payload.alloc(ctx, range * 4));
-        t.payload = out->payload.as<uint32_t>();
+        // entries fit 16 bits: half the table's cache footprint, built in place
+        const bool narrow = payload_max < 0xFFFFull && !std::getenv("QEH_NO_U16");
+        unsigned long long *nz = (unsigned long long *)flag.p;
         {
             KernelTimer kt(ctx, "join_build");
-            QEH_HIP(hipMemsetAsync(t.payload, 0, range * 4, ctx->stream));
-            hipLaunchKernelGGL(k_insert_direct, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t,
-                               flag.as<uint32_t>());
+            const int gc = grid_for(ctx, (int64_t)(range / 8 + 1), kBlock * 4, 1);  // one partial sum per CU
+            if (narrow) {
+                QEH_TRY(out->payload16.alloc(ctx, range * 2 + 16));
+                t.payload16 = out->payload16.as<uint16_t>();
+                QEH_HIP(hipMemsetAsync(t.payload16, 0, range * 2 + 16, ctx->stream));
+                hipLaunchKernelGGL(k_insert_direct16, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
+                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)t.payload16, range, 2,
+                                   nz);
+            } else {
+                QEH_TRY(out->payload.alloc(ctx, range * 4 + 16));
+                t.payload = out->payload.as<uint32_t>();
+                QEH_HIP(hipMemsetAsync(t.payload, 0, range * 4 + 16, ctx->stream));
+                hipLaunchKernelGGL(k_insert_direct, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
+                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)t.payload, range, 4,
+                                   nz);
+            }
         }
         QEH_HIP(hipGetLastError());
-        QEH_TRY(read_small(ctx, &dup, flag.p, 4));
-        if (!dup) {
+        unsigned long long filled = 0;
+        QEH_TRY(read_small(ctx, &filled, flag.p, 8));
+        if (filled == (unsigned long long)hm.cnt) {
             t.unique = 1;
-            if (payload_max < 0xFFFFull && !std::getenv("QEH_NO_U16")) {  // entries fit 16 bits: halve the table's cache footprint
-                QEH_TRY(out->payload16.alloc(ctx, range * 2));
-                {
-                    KernelTimer kt(ctx, "join_build");
-                    hipLaunchKernelGGL(k_narrow_direct, dim3(grid_for(ctx, (int64_t)range, kBlock * 8, 8)), dim3(kBlock), 0,
-                                       ctx->stream, t.payload, range, out->payload16.as<uint16_t>());
-                }
-                QEH_HIP(hipGetLastError());
-                t.payload16 = out->payload16.as<uint16_t>();
-                t.payload = nullptr;
-                out->payload.reset();
-            }
             return QEH_OK;
         }
+        t.payload16 = nullptr;
+        t.payload = nullptr;
+        out->payload16.reset();
         // duplicate build keys: a perfect-hash slot holds one row; rebuild hashed
         out->payload.reset();
         QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
@@ -256,12 +335,19 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_pa
 }
 
 // ---- group ids over key tuples ------------------------------------------------------
+// Insert every row's key tuple; slot_of_row[i] = its slot.  A row that probes
+// more than kGroupMaxProbe slots flags overflow and the host retries with an
+// 8x table; once flagged, the remaining rows stop early.
+constexpr uint64_t kGroupMaxProbe = 64;
+
 __global__ void k_group_insert(KeyCols keys, int64_t n, uint32_t *__restrict__ slots, uint64_t mask,
                                uint32_t *__restrict__ slot_of_row, uint32_t *overflow) {
+    int iter = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if ((++iter & 7) == 0 && __hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         uint64_t h = tuple_hash(keys, i) & mask;
         uint64_t probe = 0;
-        for (; probe <= mask; ++probe) {
+        for (; probe <= mask && probe < kGroupMaxProbe; ++probe) {
             // read first: few groups x many rows would otherwise serialise on
             // atomics to the same words; a stale EMPTY just falls into the CAS
             uint32_t old = __hip_atomic_load(&slots[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -269,7 +355,10 @@ __global__ void k_group_insert(KeyCols keys, int64_t n, uint32_t *__restrict__ s
             if (old == kEmpty32 || tuple_eq(keys, old, i)) break;
             h = (h + 1) & mask;
         }
-        if (probe > mask) *overflow = 1u;
+        if (probe > mask || probe >= kGroupMaxProbe) {
+            *overflow = 1u;
+            return;
+        }
         if (slot_of_row) slot_of_row[i] = (uint32_t)h;
     }
 }
@@ -291,8 +380,21 @@ __global__ void k_row_gid(const uint32_t *__restrict__ slot_of_row, int64_t n, c
         gid[i] = (uint32_t)dense[slot_of_row[i]];
 }
 
+// DIRECT group table (one non-null integer key of bounded range): slot =
+// key - kmin, slots[slot] = any row carrying the key (plain stores).
+__global__ void k_group_direct(ColRef key, int64_t n, int64_t kmin, uint32_t *__restrict__ slots,
+                               uint32_t *__restrict__ slot_of_row) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)((uint64_t)load_i64(key, i) - (uint64_t)kmin);
+        slots[s] = (uint32_t)i;
+        slot_of_row[i] = s;
+    }
+}
+
+static int group_table_finish(qeh_ctx *ctx, GroupTable *out);
+
 int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *out,
-                      uint32_t *slot_of_row) {
+                      uint32_t *slot_of_row, bool allow_direct) {
     if (n_keys < 1 || n_keys > kMaxGroupKeys)
         return fail(QEH_E_UNSUPPORTED, "1..4 group keys supported on the device");
     KeyCols &kc = out->keys;
@@ -304,8 +406,36 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
         if (keys[i].length != n_rows) return fail(QEH_E_INVALID, "group key length mismatch");
         kc.c[i] = make_colref(keys[i]);
     }
-    // capacity: 2x the row bound capped at 2^21 slots, grown 4x on overflow
-    uint64_t cap = std::max<uint64_t>(1024, next_pow2((uint64_t)std::min<int64_t>(n_rows, 1 << 20) * 2));
+    out->direct = false;
+    if (allow_direct && slot_of_row && n_keys == 1 && n_rows > 0 && kc.c[0].validity == nullptr &&
+        (kc.c[0].dtype == QEH_DT_INT64 || kc.c[0].dtype == QEH_DT_INT32) && !std::getenv("QEH_NO_DIRECT_GROUPS")) {
+        DevBuf mm;
+        QEH_TRY(mm.alloc(ctx, sizeof(MinMax) + 16));
+        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
+        hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, n_rows, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kc.c[0],
+                           n_rows, mm.as<MinMax>());
+        QEH_HIP(hipGetLastError());
+        MinMax hm{};
+        QEH_TRY(read_small(ctx, &hm, mm.p, sizeof(MinMax)));
+        const uint64_t range = (uint64_t)hm.mx - (uint64_t)hm.mn + 1ull;
+        if (range != 0 && range <= std::max<uint64_t>(4 * (uint64_t)n_rows, 65536) && range < (1ull << 31)) {
+            out->direct = true;
+            out->kmin = hm.mn;
+            out->cap = range;
+            QEH_TRY(out->slots.alloc(ctx, range * 4));
+            QEH_HIP(hipMemsetAsync(out->slots.p, 0xFF, range * 4, ctx->stream));
+            {
+                KernelTimer kt(ctx, "group_insert");
+                hipLaunchKernelGGL(k_group_direct, dim3(grid_for(ctx, n_rows, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                                   kc.c[0], n_rows, hm.mn, out->slots.as<uint32_t>(), slot_of_row);
+            }
+            QEH_HIP(hipGetLastError());
+            return group_table_finish(ctx, out);
+        }
+    }
+    // capacity: start at 16 Ki slots (L2-resident; the common few-groups case)
+    // bounded by 2x the rows, grown 8x whenever a probe sequence overflows
+    uint64_t cap = std::max<uint64_t>(1024, std::min<uint64_t>(16384, next_pow2((uint64_t)std::max<int64_t>(n_rows, 1) * 2)));
     DevBuf flag;
     QEH_TRY(flag.alloc(ctx, 8));
     for (;;) {
@@ -322,9 +452,15 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
         QEH_TRY(read_small(ctx, &ovf, flag.p, 4));
         if (!ovf) break;
         if (cap >= (1ull << 33)) return fail(QEH_E_OOM, "group table overflow");
-        cap <<= 2;
+        cap <<= 3;
     }
     out->cap = cap;
+    return group_table_finish(ctx, out);
+}
+
+// Dense ids 0..G-1 in slot order and a representative row per group.
+static int group_table_finish(qeh_ctx *ctx, GroupTable *out) {
+    const uint64_t cap = out->cap;
     DevBuf occ;
     QEH_TRY(occ.alloc(ctx, cap * 4));
     QEH_TRY(out->dense.alloc(ctx, cap * 8));
@@ -341,11 +477,16 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
     return QEH_OK;
 }
 
+int group_slots_of_rows(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
+                        DevBuf *slot_of_row) {
+    QEH_TRY(slot_of_row->alloc(ctx, (size_t)std::max<int64_t>(n_rows, 1) * 4));
+    return build_group_table(ctx, keys, n_keys, n_rows, table, slot_of_row->as<uint32_t>(), true);
+}
+
 int assign_group_ids(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
                      DevBuf *gid_of_row) {
     DevBuf slot_of_row;
-    QEH_TRY(slot_of_row.alloc(ctx, (size_t)std::max<int64_t>(n_rows, 1) * 4));
-    QEH_TRY(build_group_table(ctx, keys, n_keys, n_rows, table, slot_of_row.as<uint32_t>()));
+    QEH_TRY(group_slots_of_rows(ctx, keys, n_keys, n_rows, table, &slot_of_row));
     QEH_TRY(gid_of_row->alloc(ctx, (size_t)std::max<int64_t>(n_rows, 1) * 4));
     if (n_rows > 0)
         hipLaunchKernelGGL(k_row_gid, dim3(grid_for(ctx, n_rows, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,

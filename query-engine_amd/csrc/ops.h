@@ -24,8 +24,21 @@ struct BuiltTable {
     DevBuf slots, payload, state, payload16;
     int64_t n_inserted = 0;
 };
-int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload,
-                     uint64_t payload_max, BuiltTable *out, int force_kind = -1);
+// Payload of build row i: ids[i] if ids, else dense[slot[i]] if slot (group
+// ids straight from a group table), else i.
+struct RowPayload {
+    const uint32_t *ids = nullptr;
+    const uint32_t *slot = nullptr;
+    const uint64_t *dense = nullptr;
+};
+int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &payload, uint64_t payload_max,
+                     BuiltTable *out, int force_kind = -1);
+inline int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload, uint64_t payload_max,
+                            BuiltTable *out, int force_kind = -1) {
+    RowPayload rp;
+    rp.ids = row_payload;
+    return build_join_table(ctx, key, rp, payload_max, out, force_kind);
+}
 
 // Group table over key tuples: slots hold a representative row id; dense ids
 // 0..G-1 follow slot order.  rep_row[g] = a row carrying group g's key.
@@ -36,9 +49,14 @@ struct GroupTable {
     DevBuf rep_row;  // uint32[G]
     uint64_t cap = 0;
     int64_t groups = 0;
+    bool direct = false;  // slot = key - kmin (one integer key); not probe-able with group_find
+    int64_t kmin = 0;
 };
 int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *out,
-                      uint32_t *slot_of_row /* optional, device uint32[n_rows] */);
+                      uint32_t *slot_of_row /* optional, device uint32[n_rows] */, bool allow_direct = false);
+// build_group_table + per-row slots (uint32[n_rows]; dense id = table->dense[slot]).
+int group_slots_of_rows(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
+                        DevBuf *slot_of_row);
 // build_group_table + per-row dense ids (uint32[n_rows]).
 int assign_group_ids(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
                      DevBuf *gid_of_row);

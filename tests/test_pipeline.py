@@ -174,7 +174,15 @@ def test_slice_probe_metric_table_default_threshold(ctx):
     table), slice path chosen by default."""
     x, k, v, dk, dg = metric_data(20_000_000, 10_000_000, 1024)
     probe = [(x, None), (k, None), (v, None)]
-    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS)
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS)
+        # the metric shape must take the slice pipeline (not a silent slower fallback)
+        assert ctx.kernel_time("slice_partition")[1] == 1
+        assert ctx.kernel_time("slice_probe")[1] == 1
+    finally:
+        ctx.timing(False)
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
 
 
