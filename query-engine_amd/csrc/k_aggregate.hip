@@ -245,6 +245,42 @@ struct FastTile {
     }
 };
 
+// Apply one tile's rows (mask m, LDS state slot per row) to LDS states laid
+// out [value slot][stride] with row counts in slot 0.  Aggregate kinds are
+// uniform, so the switch sits outside the row loop and each aggregate's LDS
+// atomics for the tile's rows issue back to back.
+template <int NTERMS, int NACOL, bool NT>
+__device__ __forceinline__ void lds_apply_rows(uint64_t *lds, int64_t stride, const AggSpecs &specs, const FastIn &in,
+                                               const FastTile<NTERMS, NACOL, NT> &ft, uint32_t m, const int *slot) {
+#pragma unroll
+    for (int r = 0; r < kFastR; ++r)
+        if ((m >> r) & 1) atomicAdd((unsigned long long *)&lds[slot[r]], 1ull);
+    for (int a = 0; a < specs.n; ++a) {
+        const AggSpec sp = specs.a[a];
+        uint64_t *st = lds + (int64_t)sp.val_slot * stride;
+        const int cs = in.agg_colslot[a];
+        switch (sp.kind) {
+            case AK_SUM_F:
+#pragma unroll
+                for (int r = 0; r < kFastR; ++r)
+                    if ((m >> r) & 1) atomicAdd((double *)&st[slot[r]], as_f64(ft.a(cs, r)));
+                break;
+            case AK_SUM_I:
+#pragma unroll
+                for (int r = 0; r < kFastR; ++r)
+                    if ((m >> r) & 1) atomicAdd((unsigned long long *)&st[slot[r]], (unsigned long long)ft.a(cs, r));
+                break;
+            case AK_MIN:
+            case AK_MAX:
+#pragma unroll
+                for (int r = 0; r < kFastR; ++r)
+                    if ((m >> r) & 1) agg_apply<true>(sp.kind, &st[slot[r]], agg_input(sp.kind, sp.in_type, ft.a(cs, r)));
+                break;
+            default: break;  // COUNT of a no-null column = the row count
+        }
+    }
+}
+
 template <int NTERMS, int NACOL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, HashTable t,
                                                           int64_t G, int64_t n_tiles, uint64_t *__restrict__ gstates_all) {
@@ -268,25 +304,16 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
         ft.load(in, terms, base);
         const uint32_t sel = ft.sel;
         uint32_t gid[kFastR];
+        int slot[kFastR];
         uint32_t hit = 0;
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
             gid[r] = 0;
             if ((sel >> r) & 1)
                 if (probe_unique(t, ft.k(r), gid[r])) hit |= 1u << r;
+            slot[r] = (int)gid[r];
         }
-#pragma unroll
-        for (int r = 0; r < kFastR; ++r) {
-            if (!((hit >> r) & 1)) continue;
-            const uint32_t g = gid[r];
-            atomicAdd((unsigned long long *)&lds[g], 1ull);
-            for (int a = 0; a < specs.n; ++a) {
-                const AggSpec sp = specs.a[a];
-                if (sp.kind == AK_COUNT) continue;
-                const int64_t x = agg_input(sp.kind, sp.in_type, ft.a(in.agg_colslot[a], r));
-                agg_apply<true>(sp.kind, &lds[(int64_t)sp.val_slot * G + g], x);
-            }
-        }
+        lds_apply_rows(lds, G, specs, in, ft, hit, slot);
     }
     __syncthreads();
     for (int64_t g = threadIdx.x; g < G; g += blockDim.x) {
@@ -748,8 +775,8 @@ __device__ __forceinline__ uint32_t lds_hash(int64_t key) {
 // group slot found in a per-workgroup LDS hash of keys (linear probing, CAS
 // insert); keys that do not fit the LDS table (or INT64_MIN, the empty
 // marker) update the HBM table's states directly with global atomics.
-template <int NTERMS, int NACOL, bool NT>
-__global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, GTable gt,
+template <int NTERMS, int NACOL, bool NT, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void k_group_agg_fast(FastIn in, PredTerms terms, AggSpecs specs, GTable gt,
                                                            int lcap, int64_t G, int64_t n_tiles,
                                                            uint64_t *__restrict__ gstates_all) {
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
@@ -768,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms 
     const int64_t gcap = (int64_t)gt.mask + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const int64_t base = tile * kFastTile + (int64_t)wave * (64 * kFastR) + 2 * lane;
+        const int64_t base = tile * (BLOCK * kFastR) + (int64_t)wave * (64 * kFastR) + 2 * lane;
         FastTile<NTERMS, NACOL, NT> ft;
         ft.load(in, terms, base);
         const uint32_t sel = ft.sel;
@@ -798,19 +825,14 @@ __global__ __launch_bounds__(kBlock) void k_group_agg_fast(FastIn in, PredTerms 
                 h = (h + 1) & (lcap - 1);
             }
         }
+        uint32_t in_lds = 0;
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) in_lds |= (((sel >> r) & 1) && slot[r] >= 0) ? 1u << r : 0u;
+        lds_apply_rows(lst, lcap, specs, in, ft, in_lds, slot);
 #pragma unroll
         for (int r = 0; r < kFastR; ++r) {
             if (!((sel >> r) & 1)) continue;
-            if (slot[r] >= 0) {
-                const int h = slot[r];
-                atomicAdd((unsigned long long *)&lst[h], 1ull);
-                for (int a = 0; a < specs.n; ++a) {
-                    const AggSpec sp = specs.a[a];
-                    if (sp.kind == AK_COUNT) continue;
-                    agg_apply<true>(sp.kind, &lst[(int64_t)sp.val_slot * lcap + h],
-                                    agg_input(sp.kind, sp.in_type, ft.a(in.agg_colslot[a], r)));
-                }
-            } else {
+            if (slot[r] < 0) {
                 const int64_t key = ft.k(r);
                 const int64_t g = key == kEmptyKey ? gcap + 1 : gt_slot(gt, key);
                 if (g < 0) continue;  // overflow flagged; host regrows and reruns
@@ -1249,14 +1271,23 @@ static bool lds_group_fast(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     while (lcap > 256 && (size_t)(1 + specs.n_slots) * lcap * 8 > 64 * 1024) lcap >>= 1;
     const size_t shm = (size_t)(1 + specs.n_slots) * lcap * 8;
     if (shm > 64 * 1024) return false;
-    const int64_t n_tiles = n / kFastTile;
+    // big LDS tables leave room for few workgroups per CU: make them 1024 threads
+    // wide so a CU still holds 16-32 waves of loads in flight
+    const bool wide = shm > 40 * 1024;
+    const int block = wide ? 1024 : kBlock;
+    const int64_t tile_rows = (int64_t)block * kFastR;
+    const int64_t n_tiles = n / tile_rows;
     if (n_tiles > 0) {
-        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / shm));
-        const int grid = grid_for(ctx, n_tiles * kFastTile, kFastTile, per_cu);
+        const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(wide ? 2 : 8, (160 * 1024) / shm));
+        const int grid = grid_for(ctx, n_tiles * tile_rows, (int)tile_rows, per_cu);
         const bool nt = fast_nt_mode() == 1;
-#define QEH_GF(NTV, NAV, NTB)                                                                                       \
-    hipLaunchKernelGGL((k_group_agg_fast<NTV, NAV, NTB>), dim3(grid), dim3(kBlock), shm, ctx->stream, in, pp.terms, \
-                       specs, src.gt, lcap, G, n_tiles, states)
+#define QEH_GF(NTV, NAV, NTB)                                                                                            \
+    if (wide)                                                                                                            \
+        hipLaunchKernelGGL((k_group_agg_fast<NTV, NAV, NTB, 1024>), dim3(grid), dim3(1024), shm, ctx->stream, in,        \
+                           pp.terms, specs, src.gt, lcap, G, n_tiles, states);                                          \
+    else                                                                                                                 \
+        hipLaunchKernelGGL((k_group_agg_fast<NTV, NAV, NTB>), dim3(grid), dim3(kBlock), shm, ctx->stream, in, pp.terms, \
+                           specs, src.gt, lcap, G, n_tiles, states)
 #define QEH_GF_NA(NTV, NTB)                       \
     if (nacol == 0) QEH_GF(NTV, 0, NTB);          \
     else if (nacol == 1) QEH_GF(NTV, 1, NTB);     \
@@ -1270,7 +1301,7 @@ static bool lds_group_fast(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
 #undef QEH_GF_NA
 #undef QEH_GF
     }
-    const int64_t done = n_tiles * kFastTile;
+    const int64_t done = n_tiles * tile_rows;
     if (done < n) {
         ColSet tail = cols;
         for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);

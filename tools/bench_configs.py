@@ -80,7 +80,7 @@ def cfg2(ctx, scale):
     dt = time.perf_counter() - t0
     cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows, {dt:.2f} s"}
     kms = kt["aggregate_rows"] + kt["group_insert"]
-    line("cfg2 filter+group-by 1e8", n, wall, 32.0 * n, kms, "group_insert + k_agg_rows<GM_GROUP,PM_TERMS,LDS>", cpu)
+    line("cfg2 filter+group-by 1e8", n, wall, 32.0 * n, kms, "k_group_agg_fast (LDS key hash per workgroup)", cpu)
 
 
 def cfg3(ctx, scale):
@@ -106,7 +106,7 @@ def cfg3(ctx, scale):
     dt = time.perf_counter() - t0
     cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} probe x {nd} build, {dt:.2f} s"}
     kms = kt["join_probe"] + kt["join_gather"]
-    line("cfg3 inner join 1e9 x 1e7", n, wall, 32.0 * n, kms, "k_join_probe + k_gather", cpu,
+    line("cfg3 inner join 1e9 x 1e7", n, wall, 32.0 * n, kms, "k_join_mat (fused probe + materialise)", cpu,
          {"output_rows": rows, "build_ms": kt["join_build"]})
 
 
