@@ -75,18 +75,29 @@ def cpu_baseline(args):
                       f"(build included), {dt:.2f} s"}
 
 
+def torch_device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("QEH_BENCH_SHARE_GPU"):  # rehearsal only: several ranks on one GPU
+        local = local % max(torch_device_count(), 1)
     dist = world > 1
     import torch
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("QEH_BENCH_BACKEND", "nccl")  # "gloo": host-exchange rehearsal (several ranks per GPU)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     import qe_hip
     from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit
 
@@ -143,7 +154,8 @@ def main():
     ctx.timing(False)
 
     if dist:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        cdev = "cuda" if tdist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -153,7 +165,7 @@ def main():
     counted = int(counts.sum())
     groups = int(g)
     if dist:
-        t = torch.tensor([counted, groups], device="cuda", dtype=torch.int64)
+        t = torch.tensor([counted, groups], device=cdev, dtype=torch.int64)
         tdist.all_reduce(t)
         counted, groups = int(t[0].item()), int(t[1].item())
     total_rows = n * world
