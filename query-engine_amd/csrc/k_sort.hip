@@ -257,6 +257,7 @@ struct RadixState {
     int cur = 0;
     int64_t n = 0;
     bool enc_injective = false;  // k[cur] encodes the last-sorted column one-to-one (no null-flag pass)
+    int part_shift = -1;         // >= 0: k[cur] holds (first key << part_shift) | ..., the pair encoding
     bool key32 = false;          // k[] currently holds 32-bit keys (column range fits 32 bits)
 };
 
@@ -351,6 +352,131 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
     return QEH_OK;
 }
 
+// ---- two-key sorts (ROW_NUMBER's PARTITION BY k ORDER BY v, ORDER BY a, b) ----------------
+// One LSD sort over the pair encoding K = (enc(k) << bv) | (enc(v) >> shift)
+// instead of one sort per column.  When the two ranges need more than 64 bits,
+// v keeps only its top bv bits (total 48 or 64) and a fix-up pass sorts the
+// runs of equal K (rare: rows that share k and the top bits of v) by the
+// dropped low bits, ties by row index, so the order stays exact.
+constexpr int64_t kPairMaxRun = 64;
+
+__device__ __forceinline__ uint64_t enc_key(const ColRef &c, int64_t row, int64_t mn, int64_t mx, int asc) {
+    const int64_t x = ordered_key(c, row);
+    return asc ? (uint64_t)x - (uint64_t)mn : (uint64_t)mx - (uint64_t)x;
+}
+
+template <typename KeyT>
+__global__ void k_encode_pair(ColRef a, ColRef b, int64_t n, int64_t amn, int64_t amx, int aasc, int64_t bmn, int64_t bmx,
+                              int basc, int bv, int shift, KeyT *__restrict__ keys, uint32_t *__restrict__ perm) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t ka = enc_key(a, i, amn, amx, aasc), kb = enc_key(b, i, bmn, bmx, basc);
+        keys[i] = (KeyT)((bv >= 64 ? 0ull : ka << bv) | (kb >> shift));
+        perm[i] = (uint32_t)i;
+    }
+}
+
+__global__ void k_fix_pair_runs(const uint64_t *__restrict__ K, uint32_t *__restrict__ perm, int64_t n, ColRef b, int64_t bmn,
+                                int64_t bmx, int basc, int shift, uint32_t *overflow) {
+    const uint64_t mask = (1ull << shift) - 1ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = K[i];
+        if (K[i + 1] != k || (i > 0 && K[i - 1] == k)) continue;  // not the start of a run of equal K
+        int64_t j = i + 1;
+        while (j + 1 < n && K[j + 1] == k && j - i < kPairMaxRun) ++j;
+        if (j + 1 < n && K[j + 1] == k) {
+            *overflow = 1u;  // a long run: the caller falls back to the per-column sort
+            continue;
+        }
+        // stable LSD from the identity left the run in row order: insertion-sort it by the low bits
+        for (int64_t a = i + 1; a <= j; ++a) {
+            const uint32_t r = perm[a];
+            const uint64_t lo = enc_key(b, r, bmn, bmx, basc) & mask;
+            int64_t c = a - 1;
+            while (c >= i) {
+                const uint32_t rc = perm[c];
+                const uint64_t lc = enc_key(b, rc, bmn, bmx, basc) & mask;
+                if (lc < lo || (lc == lo && rc < r)) break;
+                perm[c + 1] = rc;
+                --c;
+            }
+            perm[c + 1] = r;
+        }
+    }
+}
+
+constexpr int kPairNotEligible = -1;
+
+static int sort_perm_pair(qeh_ctx *ctx, const qeh_column &ca, const qeh_column &cb, bool aasc, bool basc, int64_t n,
+                          RadixState &rs) {
+    if (std::getenv("QEH_NO_PAIR_SORT")) return kPairNotEligible;
+    if ((ca.validity && ca.null_count != 0) || (cb.validity && cb.null_count != 0)) return kPairNotEligible;
+    const ColRef a = make_colref(ca), b = make_colref(cb);
+    DevBuf st;
+    QEH_TRY(st.alloc(ctx, 2 * sizeof(KeyStats) + 16));
+    KeyStats ks[2];
+    {
+        KernelTimer kt(ctx, "sort_encode");
+        KeyStats *d = st.as<KeyStats>();
+        hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, d);
+        hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, d + 1);
+        const int g = grid_for(ctx, n, kBlock * 8, 1);
+        hipLaunchKernelGGL(k_key_stats, dim3(g), dim3(kBlock), 0, ctx->stream, a, nullptr, n, d);
+        hipLaunchKernelGGL(k_key_stats, dim3(g), dim3(kBlock), 0, ctx->stream, b, nullptr, n, d + 1);
+    }
+    QEH_HIP(hipGetLastError());
+    QEH_TRY(read_small(ctx, ks, st.p, sizeof ks));
+    const int ba = bit_length((uint64_t)ks[0].mx - (uint64_t)ks[0].mn);
+    const int bb = bit_length((uint64_t)ks[1].mx - (uint64_t)ks[1].mn);
+    int bv, shift, total;
+    if (ba + bb <= 64) {
+        bv = bb;
+        shift = 0;
+        total = ba + bb;
+    } else if (ba <= 40) {
+        total = ba <= 32 ? 48 : 64;  // keep >= 16 bits of b: equal-K runs stay rare
+        bv = total - ba;
+        shift = bb - bv;
+    } else {
+        return kPairNotEligible;
+    }
+    if (total == 0) total = 1;
+    rs.key32 = total <= 32;
+    {
+        KernelTimer kt(ctx, "sort_encode");
+        const int g = grid_for(ctx, n, kBlock * 8, 8);
+        const int o = 1 - rs.cur;
+        if (rs.key32)
+            hipLaunchKernelGGL(k_encode_pair<uint32_t>, dim3(g), dim3(kBlock), 0, ctx->stream, a, b, n, ks[0].mn, ks[0].mx,
+                               aasc ? 1 : 0, ks[1].mn, ks[1].mx, basc ? 1 : 0, bv, shift, rs.k[o].as<uint32_t>(),
+                               rs.v[o].as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_encode_pair<uint64_t>, dim3(g), dim3(kBlock), 0, ctx->stream, a, b, n, ks[0].mn, ks[0].mx,
+                               aasc ? 1 : 0, ks[1].mn, ks[1].mx, basc ? 1 : 0, bv, shift, rs.k[o].as<uint64_t>(),
+                               rs.v[o].as<uint32_t>());
+        rs.cur = o;
+    }
+    QEH_HIP(hipGetLastError());
+    QEH_TRY(radix_passes(ctx, rs, total));
+    if (shift > 0) {
+        DevBuf flag;
+        QEH_TRY(flag.alloc(ctx, 8));
+        QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
+        {
+            KernelTimer kt(ctx, "sort_encode");
+            hipLaunchKernelGGL(k_fix_pair_runs, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                               rs.k[rs.cur].as<uint64_t>(), rs.v[rs.cur].as<uint32_t>(), n, b, ks[1].mn, ks[1].mx,
+                               basc ? 1 : 0, shift, flag.as<uint32_t>());
+        }
+        QEH_HIP(hipGetLastError());
+        uint32_t of = 0;
+        QEH_TRY(read_small(ctx, &of, flag.p, 4));
+        if (of) return kPairNotEligible;
+    }
+    rs.enc_injective = false;
+    rs.part_shift = bv;
+    return QEH_OK;
+}
+
 // Stable lexicographic permutation by keys (last key sorted first).
 static int sort_perm(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending, int64_t n,
                      RadixState &rs) {
@@ -360,7 +486,15 @@ static int sort_perm(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int
         QEH_TRY(rs.v[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4));
     }
     rs.cur = 0;
+    rs.part_shift = -1;
     if (n == 0) return QEH_OK;
+    if (n_keys == 2) {
+        const int r = sort_perm_pair(ctx, keys[0], keys[1], ascending ? ascending[0] != 0 : true,
+                                     ascending ? ascending[1] != 0 : true, n, rs);
+        if (r != kPairNotEligible) return r;
+        rs.cur = 0;  // fall back: the per-column sort starts from the identity
+        rs.part_shift = -1;
+    }
     for (int j = n_keys - 1; j >= 0; --j)
         QEH_TRY(sort_by_column(ctx, rs, keys[j], ascending ? ascending[j] != 0 : true, j == n_keys - 1));
     return QEH_OK;
@@ -400,9 +534,9 @@ __global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, in
 // single partition key: compare the sorted encodings (coalesced) instead of
 // gathering the key column through the permutation
 template <typename KeyT>
-__global__ void k_part_flags_enc(const KeyT *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags) {
+__global__ void k_part_flags_enc(const KeyT *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags, int shift = 0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        flags[i] = i == 0 || enc[i] != enc[i - 1];
+        flags[i] = i == 0 || (enc[i] >> shift) != (enc[i - 1] >> shift);
 }
 
 // seg_excl[i] = number of partition starts before i; start_of[seg] = sorted index of its first row
@@ -555,12 +689,14 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     const int grid = grid_for(ctx, n, kBlock * 8, 8);
     {
         KernelTimer kt(ctx, "row_number");
-        if (n_part == 1 && rs.enc_injective && rs.key32)
+        const int sh = rs.part_shift >= 0 ? rs.part_shift : 0;
+        const bool enc_ok = n_part == 1 && (rs.enc_injective || (rs.part_shift >= 0 && n_order == 1));
+        if (enc_ok && rs.key32)
             hipLaunchKernelGGL(k_part_flags_enc<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                               rs.k[rs.cur].as<uint32_t>(), n, flags.as<uint32_t>());
-        else if (n_part == 1 && rs.enc_injective)
+                               rs.k[rs.cur].as<uint32_t>(), n, flags.as<uint32_t>(), sh);
+        else if (enc_ok)
             hipLaunchKernelGGL(k_part_flags_enc<uint64_t>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                               rs.k[rs.cur].as<uint64_t>(), n, flags.as<uint32_t>());
+                               rs.k[rs.cur].as<uint64_t>(), n, flags.as<uint32_t>(), sh);
         else
             hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
     }

@@ -125,6 +125,44 @@ def test_row_number(ctx, n, parts):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hi_vals,asc", [(4, True), (4, False), (1, True)])
+def test_row_number_pair_key_truncated(ctx, hi_vals, asc):
+    """PARTITION BY k ORDER BY v with a 62-bit v range: the pair sort keeps only
+    the top bits of v and fixes up runs of rows that share them (hi_vals=4:
+    runs of ~a dozen rows, sorted in place; hi_vals=1: one run per partition
+    longer than the fix-up cap, so the operator falls back to the per-column
+    sort).  Ties in v broken by input position."""
+    r = np.random.default_rng(hi_vals)
+    n = 400_000
+    k = r.integers(0, 2 ** 12, n).astype(np.int64)
+    hi = r.integers(0, hi_vals, n).astype(np.int64)
+    lo = r.integers(0, 2 ** 33, n).astype(np.int64)
+    v = (hi << 58) + lo - 2 ** 61
+    v[::1000] = v[::1000] // (2 ** 20) * (2 ** 20)  # a few exact duplicates of the low bits too
+    v[7] = 2 ** 61  # 62-bit span
+    v[11] = v[12]
+    k[11] = k[12]
+    rn = ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [asc]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k)], [ob.HostCol(v)], [asc])
+    assert np.array_equal(rn, want)
+
+
+@pytest.mark.gpu
+def test_sort_two_keys_pair_path(ctx):
+    r = np.random.default_rng(21)
+    n = 200_000
+    a = r.integers(-5, 5, n).astype(np.int32)
+    b = r.integers(-(2 ** 62), 2 ** 62, n).astype(np.int64)
+    b[::3] = b[1::3][: len(b[::3])]  # ties in b
+    for asc in ([True, True], [False, True], [True, False]):
+        perm, want = sort_both(ctx, [(a, None), (b, None)], asc)
+        assert np.array_equal(perm, want)
+    f = np.round(r.standard_normal(n), 1)
+    perm, want = sort_both(ctx, [(f, None), (a, None)], [False, True])
+    assert np.array_equal(perm, want)
+
+
+@pytest.mark.gpu
 def test_row_number_nulls_desc_two_order_keys(ctx):
     r = np.random.default_rng(12)
     n = 50_000
