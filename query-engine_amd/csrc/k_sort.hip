@@ -539,19 +539,101 @@ __global__ void k_part_flags_enc(const KeyT *__restrict__ enc, int64_t n, uint32
         flags[i] = i == 0 || (enc[i] >> shift) != (enc[i - 1] >> shift);
 }
 
-// seg_excl[i] = number of partition starts before i; start_of[seg] = sorted index of its first row
-__global__ void k_part_starts(const uint32_t *__restrict__ flags, const uint64_t *__restrict__ seg_excl, int64_t n,
-                              uint64_t *__restrict__ start_of) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        if (flags[i]) start_of[seg_excl[i]] = (uint64_t)i;
+// Row numbers without materialising partition ids: rn(i) = i - start(i) + 1,
+// start(i) = the last partition start <= i.  Chunks of kRnChunk sorted
+// positions: (1) each chunk's last start, (2) an exclusive prefix max over
+// chunks, (3) per chunk a block max-scan seeded with (2), then the scatter
+// rn[perm[i]] into input order.  No partition count is read back.
+constexpr int kRnPer = 16;
+constexpr int64_t kRnChunk = (int64_t)kBlock * kRnPer;
+
+__global__ __launch_bounds__(kBlock) void k_rn_chunk_last(const uint32_t *__restrict__ flags, int64_t n, int64_t nchunks,
+                                                          int64_t *__restrict__ last) {
+    __shared__ int64_t red[kBlock / 64];
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        int64_t m = -1;
+        const int64_t base = c * kRnChunk;
+        for (int j = 0; j < kRnPer; ++j) {
+            const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+            if (i < n && flags[i]) m = i > m ? i : m;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const int64_t o = __shfl_xor(m, d, 64);
+            m = o > m ? o : m;
+        }
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < kBlock / 64; ++w) m = red[w] > m ? red[w] : m;
+            last[c] = m;
+        }
+        __syncthreads();
+    }
 }
 
-__global__ void k_row_numbers(const uint32_t *__restrict__ flags, const uint64_t *__restrict__ seg_excl,
-                              const uint64_t *__restrict__ start_of, const uint32_t *__restrict__ perm, int64_t n,
-                              int64_t *__restrict__ rn) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t seg = seg_excl[i] + flags[i] - 1;  // inclusive count - 1
-        rn[perm[i]] = (int64_t)((uint64_t)i - start_of[seg] + 1);
+// in place: last[c] <- max(last[0..c-1]) (exclusive), one workgroup
+__global__ __launch_bounds__(1024) void k_rn_prefix_max(int64_t *__restrict__ last, int64_t nchunks) {
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (nchunks + 1023) / 1024, lo = (int64_t)t * per, hi = lo + per < nchunks ? lo + per : nchunks;
+    int64_t m = -1;
+    for (int64_t c = lo; c < hi; ++c) m = last[c] > m ? last[c] : m;
+    part[t] = m;
+    __syncthreads();
+    if (t == 0) {
+        int64_t run = -1;
+        for (int i = 0; i < 1024; ++i) {
+            const int64_t x = part[i];
+            part[i] = run;
+            run = x > run ? x : run;
+        }
+    }
+    __syncthreads();
+    int64_t run = part[t];
+    for (int64_t c = lo; c < hi; ++c) {
+        const int64_t x = last[c];
+        last[c] = run;
+        run = x > run ? x : run;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rn_write(const uint32_t *__restrict__ flags, const int64_t *__restrict__ carry,
+                                                     const uint32_t *__restrict__ perm, int64_t n, int64_t nchunks,
+                                                     int64_t *__restrict__ rn) {
+    __shared__ int64_t wmax[kBlock / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        // thread t owns kRnPer consecutive positions
+        const int64_t base = c * kRnChunk + (int64_t)t * kRnPer;
+        uint32_t f[kRnPer];
+        int64_t m = -1;
+#pragma unroll
+        for (int j = 0; j < kRnPer; ++j) {
+            const int64_t i = base + j;
+            f[j] = i < n ? flags[i] : 0u;
+            if (f[j]) m = i;
+        }
+        // exclusive max-scan of the threads' last starts, seeded with the chunks before
+        int64_t incl = m;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl = o > incl ? o : incl;
+        }
+        if (lane == 63) wmax[w] = incl;
+        __syncthreads();
+        int64_t start = carry[c];
+        for (int q = 0; q < w; ++q) start = wmax[q] > start ? wmax[q] : start;
+        const int64_t prev = __shfl_up(incl, 1, 64);
+        if (lane > 0) start = prev > start ? prev : start;
+#pragma unroll
+        for (int j = 0; j < kRnPer; ++j) {
+            const int64_t i = base + j;
+            if (f[j]) start = i;
+            if (i < n) rn[perm[i]] = i - start + 1;
+        }
+        __syncthreads();
     }
 }
 
@@ -676,9 +758,8 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out_rn));
     if (n == 0) return QEH_OK;
     const uint32_t *perm = rs.v[rs.cur].as<uint32_t>();
-    DevBuf flags, seg, starts;
+    DevBuf flags, seg;
     int s = flags.alloc(ctx, (size_t)n * 4);
-    if (s == QEH_OK) s = seg.alloc(ctx, (size_t)n * 8);
     if (s != QEH_OK) {
         qeh_column_release(ctx, out_rn);
         return s;
@@ -700,19 +781,20 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
         else
             hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, flags.as<uint32_t>());
     }
-    uint64_t nseg = 0;
-    s = exclusive_scan_u32(ctx, flags.as<uint32_t>(), seg.as<uint64_t>(), n, &nseg);
-    if (s == QEH_OK) s = starts.alloc(ctx, (size_t)std::max<uint64_t>(nseg, 1) * 8);
+    const int64_t nchunks = (n + kRnChunk - 1) / kRnChunk;
+    s = seg.alloc(ctx, (size_t)nchunks * 8);
     if (s != QEH_OK) {
         qeh_column_release(ctx, out_rn);
         return s;
     }
     {
         KernelTimer kt(ctx, "row_number");
-        hipLaunchKernelGGL(k_part_starts, dim3(grid), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<uint64_t>(), n,
-                           starts.as<uint64_t>());
-        hipLaunchKernelGGL(k_row_numbers, dim3(grid), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<uint64_t>(),
-                           starts.as<uint64_t>(), perm, n, (int64_t *)out_rn->values);
+        const int gc = (int)std::min<int64_t>(nchunks, (int64_t)ctx->props.multiProcessorCount * 8);
+        hipLaunchKernelGGL(k_rn_chunk_last, dim3(gc), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), n, nchunks,
+                           seg.as<int64_t>());
+        hipLaunchKernelGGL(k_rn_prefix_max, dim3(1), dim3(1024), 0, ctx->stream, seg.as<int64_t>(), nchunks);
+        hipLaunchKernelGGL(k_rn_write, dim3(gc), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<int64_t>(), perm, n,
+                           nchunks, (int64_t *)out_rn->values);
     }
     QEH_HIP(hipGetLastError());
     QEH_HIP(hipStreamSynchronize(ctx->stream));
