@@ -633,6 +633,132 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     }
 }
 
+// ---- LDS-slice materialising INNER join (BASELINE config 3) -----------------------------
+// Same phase A as the aggregate (k_slice_partition: items = 16-bit key offset +
+// the probe payload).  Phase B writes the joined rows: the build payload is
+// stored in the u16 table as (a - amin) + 1, so a slice in LDS answers both
+// "matches?" and "with which value?".  Rows leave in slice order (the join's
+// row order is not part of its contract); each wave reserves
+// its matches with one atomic per 512 items and writes them contiguously.
+// write the wave's matches of one 8-items-per-lane step at out[*base ...]
+// (j-major, lanes in order within j: contiguous stores), advancing *base
+__device__ __forceinline__ void emit_matches(const uint32_t *e, const int64_t *v, const bool *live, int64_t amin,
+                                             uint64_t *base, int64_t *__restrict__ out_v, int64_t *__restrict__ out_a) {
+    uint64_t b = *base;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const bool m = live[j] && e[j] != 0u;
+        const uint64_t mask = __ballot(m);
+        if (m) {
+            const uint64_t pos = b + mbcnt(mask);
+            out_v[pos] = v[j];
+            out_a[pos] = (int64_t)(e[j] - 1u) + amin;
+        }
+        b += popc64(mask);
+    }
+    *base = b;
+}
+
+__device__ __forceinline__ void load_slice(uint16_t *tslice, const HashTable &t, int b, int tid) {
+    const uint64_t k0 = (uint64_t)b << kSliceBits;
+    const uint64_t nk = t.range - k0 < (uint64_t)kSliceKeys ? t.range - k0 : (uint64_t)kSliceKeys;
+    for (int i = tid * 8; i < kSliceKeys; i += kSliceBlock * 8) {
+        v4u32 w = {0u, 0u, 0u, 0u};
+        if ((uint64_t)i + 8 <= nk) {
+            w = *(const v4u32 *)(t.payload16 + k0 + i);
+        } else {
+            for (int q = 0; q < 8; ++q)
+                if ((uint64_t)(i + q) < nk) w[q >> 1] |= (uint32_t)t.payload16[k0 + i + q] << ((q & 1) * 16);
+        }
+        *(v4u32 *)&tslice[i] = w;
+    }
+}
+
+// Phase B of the join in two passes, no atomics: EMIT = false counts each
+// region's matches (keys only) into counts[slot]; after an exclusive scan of
+// those (slot order), EMIT = true writes each region's matches from its base.
+template <bool EMIT>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_join_b(SliceRegions rg, int nreg, HashTable t, int64_t amin,
+                                                              uint32_t *__restrict__ counts, const uint64_t *__restrict__ bases,
+                                                              int64_t *__restrict__ out_v, int64_t *__restrict__ out_a) {
+    __shared__ __attribute__((aligned(16))) uint16_t tslice[kSliceKeys];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int W = kSliceBlock / 64;
+    const int F = rg.F;
+    const int64_t T = (int64_t)F * nreg;
+    const int64_t s0 = (int64_t)blockIdx.x * T / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+    for (int64_t sb = s0; sb < s1;) {
+        const int b = (int)(sb / nreg);
+        const int64_t se = std::min<int64_t>(s1, (int64_t)(b + 1) * nreg);
+        __syncthreads();
+        load_slice(tslice, t, b, tid);
+        __syncthreads();
+        for (int64_t s = sb + wave; s < se; s += W) {
+            const uint64_t reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
+            const uint32_t n_r = rg.count[reg];
+            const uint16_t *kp = rg.key + reg * rg.cap;
+            const int64_t *vp = rg.val + reg * rg.cap;
+            uint64_t base = EMIT ? bases[s] : 0;
+            uint32_t matches = 0;
+            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
+                uint32_t e[8];
+                int64_t v[8];
+                bool live[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t i = i0 + j * 64 + lane;
+                    live[j] = i < n_r;
+                    const uint32_t ii = live[j] ? i : 0u;
+                    e[j] = __builtin_nontemporal_load(kp + ii);
+                    v[j] = EMIT ? __builtin_nontemporal_load(vp + ii) : 0;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e[j] = live[j] ? (uint32_t)tslice[e[j]] : 0u;
+                if (EMIT) {
+                    emit_matches(e, v, live, amin, &base, out_v, out_a);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) matches += (uint32_t)popc64(__ballot(live[j] && e[j] != 0u));
+                }
+            }
+            if (!EMIT && lane == 0) counts[s] = matches;
+        }
+        sb = se;
+    }
+}
+
+// ragged tail (< one 8192-row tile): probe the u16 table directly and append
+// after the regions' rows (a few waves: one atomic each per 512 rows)
+__global__ __launch_bounds__(kBlock) void k_slice_join_tail(const int64_t *__restrict__ key, const int64_t *__restrict__ val,
+                                                            int64_t n, HashTable t, int64_t amin, int64_t *__restrict__ out_v,
+                                                            int64_t *__restrict__ out_a, unsigned long long *counter) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * 8 + (threadIdx.x & ~63) * 8; i0 < n;
+         i0 += (int64_t)gridDim.x * blockDim.x * 8) {
+        uint32_t e[8];
+        int64_t v[8];
+        bool live[8];
+        uint32_t total = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t i = i0 + j * 64 + lane;
+            live[j] = i < n;
+            e[j] = 0u;
+            v[j] = 0;
+            if (live[j]) {
+                const uint64_t o = (uint64_t)key[i] - (uint64_t)t.kmin;
+                if (o < t.range) e[j] = t.payload16[o];
+                v[j] = val[i];
+            }
+            total += (uint32_t)popc64(__ballot(live[j] && e[j] != 0u));
+        }
+        unsigned long long b = 0;
+        if (lane == 0 && total) b = atomicAdd(counter, (unsigned long long)total);
+        uint64_t base = __shfl(b, 0, 64);
+        emit_matches(e, v, live, amin, &base, out_v, out_a);
+    }
+}
+
 // ---- single-pass GROUP BY on one key: LDS hash table per workgroup ----------------------
 // Each workgroup aggregates its rows into an LDS open-addressing table keyed by
 // the key's 64-bit payload (ints sign-extended, floats as bits); rows whose key
@@ -1257,6 +1383,111 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         return 0;
     }
     return 1;
+}
+
+int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_column &probe_val,
+                           const qeh_column &build_key, const qeh_column &build_val, qeh_column *out_probe,
+                           qeh_column *out_build, int64_t *out_rows) {
+    if (std::getenv("QEH_NO_SLICES")) return kSliceJoinNotEligible;
+    const ColRef pk = make_colref(probe_key), pv = make_colref(probe_val);
+    if (probe_key.dtype != QEH_DT_INT64 || !fast_col_ok(pk) || !fast_col_ok(pv)) return kSliceJoinNotEligible;
+    if (build_val.dtype != QEH_DT_INT64 || (build_val.validity && build_val.null_count != 0)) return kSliceJoinNotEligible;
+    if (build_key.validity && build_key.null_count != 0) return kSliceJoinNotEligible;
+    const int64_t n = probe_key.length;
+    const int64_t n_tiles = n / kSliceTile;
+    if (n_tiles == 0 || build_key.length == 0) return kSliceJoinNotEligible;
+    // build payload as a frame-of-reference u16: (a - amin) + 1 in the direct table
+    int64_t amin, amax, avalid;
+    QEH_TRY(column_minmax(ctx, build_val, &amin, &amax, &avalid));
+    if ((uint64_t)amax - (uint64_t)amin >= 0xFFFEull) return kSliceJoinNotEligible;
+    BuiltTable bt;
+    RowPayload rp;
+    rp.values = (const int64_t *)build_val.values + build_val.offset;
+    rp.bias = amin;
+    QEH_TRY(build_join_table(ctx, build_key, rp, (uint64_t)amax - (uint64_t)amin, &bt));
+    const HashTable &t = bt.t;
+    if (!t.unique || t.kind != TK_DIRECT || !t.payload16) return kSliceJoinNotEligible;
+    const uint64_t F = (t.range + kSliceKeys - 1) >> kSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return kSliceJoinNotEligible;
+    uint64_t min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
+    if (table_bytes(t) < min_bytes) return kSliceJoinNotEligible;
+
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
+    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
+    cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
+    const uint64_t nreg = (uint64_t)grid * F;
+    DevBuf kbuf, vbuf, cbuf;
+    QEH_TRY(kbuf.alloc(ctx, nreg * cap * 2 + 64));
+    QEH_TRY(vbuf.alloc(ctx, nreg * cap * 8 + 64));
+    QEH_TRY(cbuf.alloc(ctx, nreg * 4 + 64));
+    SliceRegions rg{};
+    rg.key = kbuf.as<uint16_t>();
+    rg.val = vbuf.as<int64_t>();
+    rg.count = cbuf.as<uint32_t>();
+    rg.overflow = rg.count + nreg;                                         // 4 B
+    unsigned long long *counter = (unsigned long long *)(cbuf.as<char>() + ((nreg * 4 + 15) & ~15ull));  // 8 B
+    rg.cap = cap;
+    rg.F = (int32_t)F;
+    QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
+    QEH_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
+    QEH_TRY(alloc_column(ctx, probe_val.dtype, n, false, out_probe));
+    int st = alloc_column(ctx, QEH_DT_INT64, n, false, out_build);
+    if (st != QEH_OK) {
+        qeh_column_release(ctx, out_probe);
+        return st;
+    }
+    FastIn in{};
+    in.key = (const int64_t *)pk.values;
+    in.acol[0] = (const int64_t *)pv.values;
+    in.agg_colslot[0] = 0;
+    PredTerms none{};
+    const bool nt = fast_nt_mode() == 1;
+    int64_t *ov = (int64_t *)out_probe->values, *oa = (int64_t *)out_build->values;
+    const uint64_t T = nreg;  // region slots, slice-major
+    DevBuf counts, bases;
+    if (st == QEH_OK) st = counts.alloc(ctx, T * 4 + 16);
+    if (st == QEH_OK) st = bases.alloc(ctx, T * 8 + 16);
+    uint64_t region_rows = 0;
+    const int gridB = ctx->props.multiProcessorCount;
+    if (st == QEH_OK) {
+        KernelTimer kt(ctx, "join_probe");
+        if (nt)
+            hipLaunchKernelGGL((k_slice_partition<0, 1, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
+                               t.kmin, t.range, n_tiles, rg);
+        else
+            hipLaunchKernelGGL((k_slice_partition<0, 1, false>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
+                               t.kmin, t.range, n_tiles, rg);
+        hipLaunchKernelGGL((k_slice_join_b<false>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin,
+                           counts.as<uint32_t>(), nullptr, nullptr, nullptr);
+    }
+    if (st == QEH_OK) st = exclusive_scan_u32(ctx, counts.as<uint32_t>(), bases.as<uint64_t>(), (int64_t)T, &region_rows);
+    uint32_t of = 0;
+    if (st == QEH_OK) st = read_small(ctx, &of, rg.overflow, 4);
+    if (st == QEH_OK && of) st = kSliceJoinNotEligible;
+    if (st == QEH_OK) {
+        KernelTimer kt(ctx, "join_probe");
+        hipLaunchKernelGGL((k_slice_join_b<true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin, nullptr,
+                           bases.as<uint64_t>(), ov, oa);
+        const int64_t done = n_tiles * kSliceTile;
+        hipLaunchKernelGGL(k_fill_i64, dim3(1), dim3(1), 0, ctx->stream, (int64_t *)counter, (int64_t)1, (int64_t)region_rows);
+        if (done < n)
+            hipLaunchKernelGGL(k_slice_join_tail, dim3(grid_for(ctx, n - done, kBlock * 8, 2)), dim3(kBlock), 0, ctx->stream,
+                               in.key + done, in.acol[0] + done, n - done, t, amin, ov, oa, counter);
+        if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
+    }
+    uint64_t res[2] = {0, 0};
+    if (st == QEH_OK) st = read_small(ctx, &res[1], counter, 8);
+    if (st != QEH_OK) {
+        qeh_column_release(ctx, out_probe);
+        qeh_column_release(ctx, out_build);
+        return st;
+    }
+    out_probe->length = (int64_t)res[1];
+    out_build->length = (int64_t)res[1];
+    *out_rows = (int64_t)res[1];
+    return QEH_OK;
 }
 
 // Fast single-key GROUP BY (k_group_agg_fast) over the full tiles, generic

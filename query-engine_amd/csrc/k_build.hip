@@ -95,6 +95,7 @@ __global__ void k_minmax_init(MinMax *m) {
 // ---- inserts -------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t payload_of(const RowPayload &rp, int64_t row) {
     if (rp.ids) return rp.ids[row];
+    if (rp.values) return (uint32_t)((uint64_t)rp.values[row] - (uint64_t)rp.bias);
     if (rp.slot) return (uint32_t)rp.dense[rp.slot[row]];
     return (uint32_t)row;
 }
@@ -191,6 +192,23 @@ __global__ void k_wide_dups(ColRef key, int64_t n, HashTable t, uint32_t *dup) {
         int c = table_probe(t, k, [](uint32_t) {});
         if (c > 1) *dup = 1u;
     }
+}
+
+int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid) {
+    DevBuf mm;
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) + 16));
+    const ColRef c = make_colref(col);
+    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
+    if (col.length > 0)
+        hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, col.length, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, c,
+                           col.length, mm.as<MinMax>());
+    QEH_HIP(hipGetLastError());
+    MinMax hm{};
+    QEH_TRY(read_small(ctx, &hm, mm.p, sizeof(MinMax)));
+    *mn = hm.mn;
+    *mx = hm.mx;
+    *valid = (int64_t)hm.cnt;
+    return QEH_OK;
 }
 
 static uint64_t next_pow2(uint64_t x) {

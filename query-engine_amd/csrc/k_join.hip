@@ -449,6 +449,11 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
         if (probe_cols[i].length != probe_key->length) return fail(QEH_E_INVALID, "probe columns have different lengths");
     for (int i = 0; i < n_build_cols; ++i)
         if (build_cols[i].length != build_key->length) return fail(QEH_E_INVALID, "build columns have different lengths");
+    if (n_probe_cols == 1 && n_build_cols == 1) {  // BASELINE config 3 shape: LDS-slice pipeline
+        const int r = slice_join_materialise(ctx, *probe_key, probe_cols[0], *build_key, build_cols[0], out_probe, out_build,
+                                             out_rows);
+        if (r != kSliceJoinNotEligible) return r;
+    }
     BuiltTable bt;
     QEH_TRY(build_join_table(ctx, *build_key, nullptr, (uint64_t)std::max<int64_t>(build_key->length - 1, 0), &bt));
     {

@@ -30,7 +30,17 @@ struct RowPayload {
     const uint32_t *ids = nullptr;
     const uint32_t *slot = nullptr;
     const uint64_t *dense = nullptr;
+    const int64_t *values = nullptr;  // payload = values[i] - bias (frame of reference)
+    int64_t bias = 0;
 };
+// min / max / valid count of an integer column (one synchronous read).
+int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid);
+// LDS-slice materialising INNER join of one probe payload and one Int64 build
+// payload (k_aggregate.hip); kSliceJoinNotEligible when the shapes do not fit.
+constexpr int kSliceJoinNotEligible = -1;
+int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_column &probe_val,
+                           const qeh_column &build_key, const qeh_column &build_val, qeh_column *out_probe,
+                           qeh_column *out_build, int64_t *out_rows);
 int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &payload, uint64_t payload_max,
                      BuiltTable *out, int force_kind = -1);
 inline int build_join_table(qeh_ctx *ctx, const qeh_column &key, const uint32_t *row_payload, uint64_t payload_max,

@@ -61,6 +61,24 @@ def test_join_table_layouts(ctx, monkeypatch, table):
     assert sorted_rows(got) == sorted_rows(want)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_probe,n_build,key0,arange", [(1_000_003, 300_000, 0, 1000), (500_000, 200_001, -77_777, 60_000),
+                                                         (300_000, 100_000, 5, 70_000)])
+def test_join_slice_path(ctx, monkeypatch, n_probe, n_build, key0, arange):
+    """The LDS-slice materialising join (config 3 shape: one probe payload, one
+    Int64 build payload stored as a u16 frame of reference), forced on small
+    tables; misses below and above the key range; ragged tail; a payload range
+    past 16 bits falls back to the ordered fused join.  Multiset compare."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    r = np.random.default_rng(n_build)
+    bk = r.permutation(n_build).astype(np.int64) + key0
+    ba = r.integers(-(arange // 2), arange - arange // 2, n_build).astype(np.int64)
+    pk = r.integers(key0 - 1000, key0 + n_build + 1000, n_probe).astype(np.int64)
+    pv = r.random(n_probe)
+    got, want = join_both(ctx, (pk, None), [(pv, None)], (bk, None), [(ba, None)])
+    assert sorted_rows(got) == sorted_rows(want)
+
+
 def sort_both(ctx, keys, asc):
     perm = ctx.sort_indices([ctx.upload(*k) for k in keys], asc).to_numpy()[0]
     want = ob.sort_indices([ob.HostCol(*k) for k in keys], asc)
