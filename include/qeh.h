@@ -177,6 +177,12 @@ int qeh_generate(qeh_ctx *ctx, int kind, uint64_t seed, uint64_t col_id, int64_t
 int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
                const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows);
 
+/* Filter followed by LimitExec (executor.rs:299-341): the first `max_rows` rows that qualify
+ * (order-preserving; max_rows < 0: all) — the same rows as qeh_filter then a slice, but
+ * outputs are sized to max_rows and input tiles past the cap are not read. */
+int qeh_filter_limit(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                     const int32_t *out_idx, int n_out, int64_t max_rows, qeh_column *out, int64_t *out_rows);
+
 /* Projection expression: operators.rs:13-62 evaluate_expr over one input.
  * Column references are returned zero-copy (owned = 0). */
 int qeh_eval(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *expr,

@@ -126,12 +126,26 @@ typedef struct qeh_plan {
     int32_t root;
 } qeh_plan;
 
-/* `DataSource::scan()` result for one Scan / IndexScan source (borrowed). */
+/* `DataSource::scan()` result for one Scan / IndexScan source (borrowed).
+ * cache_key != 0: the caller promises that every source passed with this key
+ * holds identical data (e.g. a MemoryDataSource's table id + version, memory.rs
+ * scan() returns clones of the same Arc'd batches); the device copy made by the
+ * first query is kept on the context and reused without touching the batches
+ * until qeh_source_cache_evict.  0: import on every call (the reference's
+ * per-query Vec<RecordBatch>). */
 typedef struct qeh_source {
     struct ArrowSchema *schema;        /* struct schema of the batches          */
     struct ArrowArray *const *batches; /* struct arrays, one per RecordBatch    */
     int64_t n_batches;
+    uint64_t cache_key;
 } qeh_source;
+
+/* Drop the cached device copy of `cache_key` (0: every entry). */
+int qeh_source_cache_evict(qeh_ctx *ctx, uint64_t cache_key);
+/* Cache occupancy and counters since the context was created. */
+int qeh_source_cache_stats(qeh_ctx *ctx, int64_t *entries, int64_t *bytes, int64_t *hits, int64_t *misses);
+/* Device bytes the cache may hold before it drops its oldest entries (default 64 GiB). */
+int qeh_source_cache_budget(qeh_ctx *ctx, int64_t bytes);
 
 /* Execute `plan` on the device.  On success *out_n_batches is 0 (the
  * reference returns no batches; out_* untouched, release == NULL) or 1

@@ -14,6 +14,7 @@
 // GROUP BY, INNER equi-join, Sort and ROW_NUMBER follow the intended
 // semantics; Limit slices (executor.rs:299-341); SubqueryScan and IndexScan
 // behave as in the reference (executor.rs:72-88).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -124,6 +125,27 @@ int import_column(qeh_ctx *ctx, const qeh_source &src, int ci, int dt, Col *out)
     c.owned = 1;
     c.length = total;
     c.null_count = 0;
+    const size_t es0 = dtype_size(dt);
+    if (!any_nulls && dt != QEH_DT_BOOL && dt != QEH_DT_UTF8 && es0) {
+        // no nulls, fixed width: each batch's value buffer goes straight to its
+        // place in the device column (no host staging, no per-row loop)
+        void *p = nullptr;
+        QEH_TRY(ctx->pool->alloc(total ? (size_t)total * es0 : 8, &p));
+        int64_t pos = 0;
+        for (int64_t b = 0; b < src.n_batches; ++b) {
+            const ArrowArray *batch = src.batches[b];
+            const ArrowArray *ch = batch->children[ci];
+            const int64_t len = batch->length, off = batch->offset + ch->offset;
+            if (len)
+                QEH_HIP(hipMemcpyAsync((char *)p + (size_t)pos * es0, (const uint8_t *)ch->buffers[1] + (size_t)off * es0,
+                                       (size_t)len * es0, hipMemcpyHostToDevice, ctx->stream));
+            pos += len;
+        }
+        c.values = p;
+        QEH_HIP(hipStreamSynchronize(ctx->stream));  // the batches are borrowed for this call only
+        *out = own(ctx, c);
+        return QEH_OK;
+    }
     const size_t vbytes = (size_t)((total + 63) / 64) * 8 + 8;
     std::vector<uint8_t> valid;
     if (any_nulls) valid.assign(vbytes, 0);
@@ -181,7 +203,86 @@ int import_column(qeh_ctx *ctx, const qeh_source &src, int ci, int dt, Col *out)
     return QEH_OK;
 }
 
+int import_source_uncached(qeh_ctx *ctx, const qeh_source &src, Table *t);
+
+size_t table_device_bytes(const Table &t) {
+    size_t b = 0;
+    for (const Col &c : t.cols) {
+        const size_t es = dtype_size(c.c.dtype);
+        if (c.c.dtype == QEH_DT_UTF8) b += (size_t)c.c.values_bytes + (size_t)(c.c.length + 1) * 4;
+        else if (c.c.dtype == QEH_DT_BOOL) b += (size_t)(c.c.length + 7) / 8;
+        else b += (size_t)c.c.length * es;
+        if (c.c.validity) b += (size_t)(c.c.length + 7) / 8;
+    }
+    return b;
+}
+
+}  // namespace
+
+namespace qeh {
+struct SourceCache {
+    std::mutex mu;
+    struct Entry {
+        std::shared_ptr<void> table;  // Table (shared column owners)
+        size_t bytes = 0;
+        uint64_t stamp = 0;
+    };
+    std::map<uint64_t, Entry> entries;
+    uint64_t clock = 0;
+    size_t bytes = 0;
+    size_t budget = size_t(64) << 30;
+    int64_t hits = 0, misses = 0;
+    void evict_oldest_until(size_t limit) {
+        while (bytes > limit && !entries.empty()) {
+            auto victim = entries.begin();
+            for (auto it = entries.begin(); it != entries.end(); ++it)
+                if (it->second.stamp < victim->second.stamp) victim = it;
+            bytes -= victim->second.bytes;
+            entries.erase(victim);
+        }
+    }
+};
+}  // namespace qeh
+
+namespace {
+
+SourceCache &source_cache(qeh_ctx *ctx) {
+    if (!ctx->source_cache) ctx->source_cache = std::make_shared<SourceCache>();
+    return *ctx->source_cache;
+}
+
+// Scan input: the cached device copy for a non-zero cache_key, else an import.
 int import_source(qeh_ctx *ctx, const qeh_source &src, Table *t) {
+    if (src.cache_key == 0) return import_source_uncached(ctx, src, t);
+    SourceCache &sc = source_cache(ctx);
+    {
+        std::lock_guard<std::mutex> g(sc.mu);
+        auto it = sc.entries.find(src.cache_key);
+        if (it != sc.entries.end()) {
+            *t = *std::static_pointer_cast<Table>(it->second.table);
+            it->second.stamp = ++sc.clock;
+            ++sc.hits;
+            return QEH_OK;
+        }
+    }
+    QEH_TRY(import_source_uncached(ctx, src, t));
+    auto keep = std::make_shared<Table>(*t);
+    const size_t bytes = table_device_bytes(*t);
+    std::lock_guard<std::mutex> g(sc.mu);
+    ++sc.misses;
+    if (bytes <= sc.budget) {
+        sc.evict_oldest_until(sc.budget - bytes);
+        auto &e = sc.entries[src.cache_key];
+        sc.bytes -= e.bytes;  // 0 unless another thread inserted the same key meanwhile
+        e.table = keep;
+        e.bytes = bytes;
+        e.stamp = ++sc.clock;
+        sc.bytes += bytes;
+    }
+    return QEH_OK;
+}
+
+int import_source_uncached(qeh_ctx *ctx, const qeh_source &src, Table *t) {
     if (!src.schema) return fail(QEH_E_INVALID, "source without schema");
     t->fields.clear();
     t->cols.clear();
@@ -431,22 +532,81 @@ class Executor {
     }
 
     int filter_table(const Table &in, const qeh_expr &pred, Table *out) {
-        out->fields = in.fields;
-        out->cols.clear();
-        auto cols = raw(in);
-        std::vector<int32_t> idx(cols.size());
+        std::vector<int32_t> idx(in.cols.size());
         for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
-        std::vector<qeh_column> res(std::max<size_t>(cols.size(), 1));
+        return filter_columns(in, pred, idx, -1, out);
+    }
+
+    // Filter keeping only columns `idx` of `in` (in that order) and at most `cap` rows (< 0: all).
+    int filter_columns(const Table &in, const qeh_expr &pred, const std::vector<int32_t> &idx, int64_t cap, Table *out) {
+        out->fields.clear();
+        out->cols.clear();
+        for (int32_t i : idx) out->fields.push_back(in.fields[i]);
+        auto cols = raw(in);
+        std::vector<qeh_column> res(std::max<size_t>(idx.size(), 1));
         int64_t rows = 0;
         if (cols.empty()) return fail(QEH_E_UNSUPPORTED, "filter over a batch without columns");
-        QEH_TRY(qeh_filter(ctx_, cols.data(), (int)cols.size(), &pred, idx.data(), (int)idx.size(), res.data(), &rows));
-        for (size_t i = 0; i < cols.size(); ++i) out->cols.push_back(own(ctx_, res[i]));
+        QEH_TRY(qeh_filter_limit(ctx_, cols.data(), (int)cols.size(), &pred, idx.data(), (int)idx.size(), cap, res.data(),
+                                 &rows));
+        for (size_t i = 0; i < idx.size(); ++i) out->cols.push_back(own(ctx_, res[i]));
         out->rows = rows;
         out->batches = (in.batches > 0 && rows > 0) ? 1 : 0;  // empty batches are dropped (executor.rs:149-151)
         return QEH_OK;
     }
 
+    // Projection(Filter(X)) [under Limit]: the filter gathers only the columns the projection
+    // reads, and with `cap` >= 0 only the first `cap` qualifying rows (the Limit's skip + fetch).
+    // Expressions are re-indexed onto the gathered columns; the result equals the unfused
+    // Filter -> Projection -> Limit chain (the cap is only passed for pure column projections,
+    // so no expression error on a row past the limit can go unseen).
+    int filter_project(const qeh_plan_node &proj, int64_t cap, Table *out, int depth) {
+        const qeh_plan_node &fn = plan_->nodes[proj.input];
+        Table in;
+        QEH_TRY(run(fn.input, &in, depth + 2));
+        std::vector<int32_t> remap(in.cols.size(), -1), idx;
+        for (int i = 0; i < proj.n_exprs; ++i)
+            for (int k = 0; k < proj.exprs[i].n_nodes; ++k) {
+                const qeh_expr_node &x = proj.exprs[i].nodes[k];
+                if (x.kind != QEH_EX_COLUMN) continue;
+                if (x.index < 0 || x.index >= (int)in.cols.size())
+                    return fail(QEH_E_INVALID, "Column index " + std::to_string(x.index) + " out of bounds");
+                if (remap[x.index] < 0) {
+                    remap[x.index] = (int32_t)idx.size();
+                    idx.push_back(x.index);
+                }
+            }
+        std::sort(idx.begin(), idx.end());
+        for (size_t j = 0; j < idx.size(); ++j) remap[idx[j]] = (int32_t)j;
+        Table f;
+        QEH_TRY(filter_columns(in, fn.predicate, idx, cap, &f));
+        out->fields.clear();
+        out->cols.clear();
+        for (int i = 0; i < proj.n_exprs; ++i) {
+            std::vector<qeh_expr_node> nodes(proj.exprs[i].nodes, proj.exprs[i].nodes + proj.exprs[i].n_nodes);
+            for (auto &x : nodes)
+                if (x.kind == QEH_EX_COLUMN) x.index = remap[x.index];
+            qeh_expr e = proj.exprs[i];
+            e.nodes = nodes.data();
+            Col c;
+            QEH_TRY(eval(f, e, &c));
+            std::string name = (proj.field_names && i < proj.n_fields && proj.field_names[i])
+                                   ? proj.field_names[i]
+                                   : "col_" + std::to_string(i);
+            out->fields.push_back({name, c.c.dtype, true});
+            out->cols.push_back(c);
+        }
+        out->rows = f.rows;
+        out->batches = proj.n_exprs == 0 ? 0 : f.batches;  // executor.rs:109-111
+        return QEH_OK;
+    }
+
+    bool fusable_filter_projection(const qeh_plan_node &proj) const {
+        return proj.kind == QEH_PLAN_PROJECTION && plan_->nodes[proj.input].kind == QEH_PLAN_FILTER &&
+               !std::getenv("QEH_NO_FUSION");
+    }
+
     int projection(const qeh_plan_node &nd, Table *out, int depth) {
+        if (fusable_filter_projection(nd)) return filter_project(nd, -1, out, depth);
         Table in;
         QEH_TRY(run(nd.input, &in, depth + 1));
         out->fields.clear();
@@ -536,6 +696,12 @@ class Executor {
         out->rows = rows;
         out->batches = rows > 0 ? 1 : 0;  // executor.rs:374-376 keeps non-empty joins only
         return QEH_OK;
+    }
+
+    static bool all_column_exprs(const qeh_plan_node &proj) {
+        for (int i = 0; i < proj.n_exprs; ++i)
+            if (expr_as_column(&proj.exprs[i]) < 0) return false;
+        return true;
     }
 
     static bool all_columns(const qeh_expr *e, int n, int lo, int hi) {
@@ -732,7 +898,20 @@ class Executor {
 
     int limit(const qeh_plan_node &nd, Table *out, int depth) {
         Table in;
-        QEH_TRY(run(nd.input, &in, depth + 1));
+        const qeh_plan_node &child = plan_->nodes[nd.input];
+        const int64_t cap = nd.fetch >= 0 && !std::getenv("QEH_NO_FUSION")
+                                ? std::max<int64_t>(nd.skip, 0) + nd.fetch : -1;
+        if (cap >= 0 && child.kind == QEH_PLAN_FILTER) {  // Limit(Filter(X)): stop at skip + fetch rows
+            Table x;
+            QEH_TRY(run(child.input, &x, depth + 2));
+            std::vector<int32_t> idx(x.cols.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+            QEH_TRY(filter_columns(x, child.predicate, idx, cap, &in));
+        } else if (cap >= 0 && fusable_filter_projection(child) && all_column_exprs(child)) {
+            QEH_TRY(filter_project(child, cap, &in, depth + 1));
+        } else {
+            QEH_TRY(run(nd.input, &in, depth + 1));
+        }
         const int64_t start = std::min<int64_t>(std::max<int64_t>(nd.skip, 0), in.rows);
         int64_t end = in.rows;
         if (nd.fetch >= 0) end = std::min<int64_t>(end, start + nd.fetch);
@@ -807,5 +986,52 @@ extern "C" int qeh_execute_plan(qeh_ctx *ctx, const qeh_plan *plan, const qeh_so
     if (t.batches == 0) return QEH_OK;
     QEH_TRY(export_table(ctx, t, out_schema, out_batch));
     *out_n_batches = 1;
+    return QEH_OK;
+}
+
+extern "C" int qeh_source_cache_evict(qeh_ctx *ctx, uint64_t cache_key) {
+    if (!ctx) return qeh::fail(QEH_E_INVALID, "null context");
+    if (!ctx->source_cache) return QEH_OK;
+    qeh::DeviceGuard dg(ctx->device);
+    qeh::SourceCache &sc = *ctx->source_cache;
+    std::lock_guard<std::mutex> g(sc.mu);
+    if (cache_key == 0) {
+        sc.entries.clear();
+        sc.bytes = 0;
+        return QEH_OK;
+    }
+    auto it = sc.entries.find(cache_key);
+    if (it != sc.entries.end()) {
+        sc.bytes -= it->second.bytes;
+        sc.entries.erase(it);
+    }
+    return QEH_OK;
+}
+
+extern "C" int qeh_source_cache_stats(qeh_ctx *ctx, int64_t *entries, int64_t *bytes, int64_t *hits, int64_t *misses) {
+    if (!ctx) return qeh::fail(QEH_E_INVALID, "null context");
+    int64_t e = 0, b = 0, h = 0, m = 0;
+    if (ctx->source_cache) {
+        qeh::SourceCache &sc = *ctx->source_cache;
+        std::lock_guard<std::mutex> g(sc.mu);
+        e = (int64_t)sc.entries.size();
+        b = (int64_t)sc.bytes;
+        h = sc.hits;
+        m = sc.misses;
+    }
+    if (entries) *entries = e;
+    if (bytes) *bytes = b;
+    if (hits) *hits = h;
+    if (misses) *misses = m;
+    return QEH_OK;
+}
+
+extern "C" int qeh_source_cache_budget(qeh_ctx *ctx, int64_t bytes) {
+    if (!ctx || bytes < 0) return qeh::fail(QEH_E_INVALID, "qeh_source_cache_budget: bad argument");
+    qeh::DeviceGuard dg(ctx->device);
+    qeh::SourceCache &sc = source_cache(ctx);
+    std::lock_guard<std::mutex> g(sc.mu);
+    sc.budget = (size_t)bytes;
+    sc.evict_oldest_until(sc.budget);
     return QEH_OK;
 }

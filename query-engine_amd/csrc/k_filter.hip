@@ -47,7 +47,8 @@ template <int PM>
 __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64_t n_tiles, PredTerms terms,
                                                    DevProgram prog, OutSpecs outs, uint64_t *__restrict__ status,
                                                    unsigned long long *__restrict__ ticket, uint32_t *__restrict__ errp,
-                                                   uint64_t *__restrict__ total_out) {
+                                                   uint64_t *__restrict__ total_out, uint64_t cap, uint64_t exit_at,
+                                                   uint64_t *__restrict__ done) {
     __shared__ uint32_t wave_cnt[kFR][kBlock / 64];
     __shared__ uint32_t wave_off[kFR][kBlock / 64];
     __shared__ int64_t s_tile;
@@ -57,7 +58,16 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t err = 0;
     for (;;) {
-        if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1ull);
+        if (threadIdx.x == 0) {
+            int64_t t = (int64_t)atomicAdd(ticket, 1ull);
+            if (t < n_tiles && ld_agent(done)) {
+                // the first `cap` rows are already placed: publish a prefix >= cap so that a
+                // successor that started before `done` was raised still completes its look-back
+                st_agent(&status[t], kFlagIncl | cap);
+                t = n_tiles;
+            }
+            s_tile = t;
+        }
         __syncthreads();
         const int64_t tile = s_tile;
         if (tile >= n_tiles) break;
@@ -101,18 +111,21 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
             if (lane == 0) {
                 s_prefix = prefix;
                 if (tile == n_tiles - 1) *total_out = prefix + total;
+                if (prefix + total >= exit_at) st_agent(done, 1ull);
             }
         }
         // stage validity / boolean bits of this tile's output range in LDS
         for (int i = threadIdx.x; i < outs.n * (kFTile / 32 + 2); i += blockDim.x) (&vbits[0][0])[i] = 0;
         __syncthreads();
         const uint64_t prefix = s_prefix;
+        const uint32_t lim = prefix >= cap ? 0u : (uint32_t)std::min<uint64_t>(total, cap - prefix);  // rows kept
         const uint32_t shift = (uint32_t)(prefix & 31);  // bit offset of the tile's first row in its word
 #pragma unroll
         for (int r = 0; r < kFR; ++r) {
             if (!((sel >> r) & 1)) continue;
             const int64_t row = row0 + (int64_t)r * kBlock;
             const uint32_t local = wave_off[r][wave] + rank[r];
+            if (local >= lim) continue;
             const uint64_t pos = prefix + local;
             for (int c = 0; c < outs.n; ++c) {
                 const OutSpec &o = outs.o[c];
@@ -136,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
         __syncthreads();
         // validity (and boolean values) words: interior words are owned by this
         // tile; the first and last word may be shared with neighbours -> atomicOr
-        const uint32_t nwords = (shift + total + 31) / 32;
+        const uint32_t nwords = lim ? (shift + lim + 31) / 32 : 0;
         for (int c = 0; c < outs.n; ++c) {
             const OutSpec &o = outs.o[c];
             const bool bool_vals = o.dtype == QEH_DT_BOOL;
@@ -150,6 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
                 for (int r = 0; r < kFR; ++r) {
                     if (!((sel >> r) & 1)) continue;
                     const int64_t row = row0 + (int64_t)r * kBlock;
+                    if (wave_off[r][wave] + rank[r] >= lim) continue;
                     if (!o.src_valid || bit_at(o.src_valid, o.src_vbit0 + row)) {
                         const uint32_t b = wave_off[r][wave] + rank[r] + shift;
                         atomicOr(&vbits[kMaxCols][b >> 5], 1u << (b & 31));
@@ -208,7 +222,8 @@ __device__ __forceinline__ v2i64f ff_pair(const int64_t *p, int64_t row, int64_t
 template <int NTERMS, int NC>
 __global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t n_tiles, PredTerms terms,
                                                         uint64_t *__restrict__ status, unsigned long long *__restrict__ ticket,
-                                                        uint32_t *__restrict__ errp, uint64_t *__restrict__ total_out) {
+                                                        uint32_t *__restrict__ errp, uint64_t *__restrict__ total_out,
+                                                        uint64_t cap, uint64_t exit_at, uint64_t *__restrict__ done) {
     constexpr int W = kBlock / 64;
     __shared__ int64_t stage[kFTile];
     __shared__ uint32_t cnt[W][kFFPairs], offs[W][kFFPairs];
@@ -217,7 +232,16 @@ __global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t
     __shared__ uint32_t s_total;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (;;) {
-        if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1ull);
+        if (threadIdx.x == 0) {
+            int64_t t = (int64_t)atomicAdd(ticket, 1ull);
+            if (t < n_tiles && ld_agent(done)) {
+                // the first `cap` rows are already placed: publish a prefix >= cap so that a
+                // successor that started before `done` was raised still completes its look-back
+                st_agent(&status[t], kFlagIncl | cap);
+                t = n_tiles;
+            }
+            s_tile = t;
+        }
         __syncthreads();
         const int64_t tile = s_tile;
         if (tile >= n_tiles) break;
@@ -284,10 +308,12 @@ __global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t
             if (lane == 0) {
                 s_prefix = prefix;
                 if (tile == n_tiles - 1) *total_out = prefix + total;
+                if (prefix + total >= exit_at) st_agent(done, 1ull);
             }
         }
         __syncthreads();
         const uint64_t prefix = s_prefix;
+        const uint32_t lim = prefix >= cap ? 0u : (uint32_t)std::min<uint64_t>(total, cap - prefix);  // rows kept
         auto emit = [&](auto cc) {
             constexpr int c = decltype(cc)::value;
             if constexpr (c < NC) {
@@ -297,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t
                         if ((sel >> r) & 1) stage[offs[wave][r >> 1] + rank[r]] = cv[c][r >> 1][r & 1];
                     __syncthreads();
                     int64_t *dst = in.out[c] + prefix;
-                    for (uint32_t i = threadIdx.x; i < total; i += kBlock) __builtin_nontemporal_store(stage[i], &dst[i]);
+                    for (uint32_t i = threadIdx.x; i < lim; i += kBlock) __builtin_nontemporal_store(stage[i], &dst[i]);
                     __syncthreads();
                 }
             }
@@ -351,8 +377,8 @@ __global__ void k_iota_u32(uint32_t *out, int64_t n) {
         out[i] = (uint32_t)i;
 }
 
-extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
-                          const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows) {
+static int filter_impl(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                       const int32_t *out_idx, int n_out, int64_t max_rows, qeh_column *out, int64_t *out_rows) {
     if (!ctx || !out_rows || (n_out > 0 && (!out || !out_idx))) return fail(QEH_E_INVALID, "qeh_filter: bad argument");
     *out_rows = 0;
     DeviceGuard dg(ctx->device);
@@ -361,6 +387,11 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     const int64_t n = n_cols > 0 ? cols[0].length : 0;
     for (int i = 0; i < n_cols; ++i)
         if (cols[i].length != n) return fail(QEH_E_INVALID, "filter columns have different lengths");
+    // LIMIT pushed into the filter: rows past `cap` are neither written nor allocated, and tiles
+    // claimed after the first `cap` selected rows are placed are not read at all
+    const uint64_t cap = max_rows < 0 ? kValMask : std::min<uint64_t>((uint64_t)max_rows, kValMask);
+    const int64_t n_alloc = (int64_t)std::min<uint64_t>((uint64_t)n, cap);
+    uint64_t exit_at = kValMask;  // set below for predicates that cannot raise
     std::vector<int32_t> dts(n_cols);
     for (int i = 0; i < n_cols; ++i) dts[i] = cols[i].dtype;
     DevProgram prog;
@@ -368,6 +399,9 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     if (prog.result_type != QEH_DT_BOOL) return fail(QEH_E_TYPE, "Filter predicate must return boolean");
     PredTerms terms{};
     const bool fast = lower_to_terms(predicate, dts.data(), n_cols, &terms);
+    // comparisons of columns with literals cannot raise, so tiles past the cap may go unread;
+    // a general predicate (arithmetic may overflow) is evaluated on every row, as the reference does
+    if (fast) exit_at = cap;
     for (int j = 0; j < n_out; ++j)
         if (out_idx[j] < 0 || out_idx[j] >= n_cols) return fail(QEH_E_INVALID, "filter output column index out of range");
     // fixed-width outputs are compacted by the kernel; Utf8 outputs are
@@ -387,13 +421,13 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     for (size_t q = 0; q < fixed.size(); ++q) {
         const int j = fixed[q];
         const qeh_column &src = cols[out_idx[j]];
-        int s = alloc_column(ctx, src.dtype, n, src.validity != nullptr, &out[j]);
+        int s = alloc_column(ctx, src.dtype, n_alloc, src.validity != nullptr, &out[j]);
         if (s != QEH_OK) {
             cleanup();
             return s;
         }
         made[j] = 1;
-        const size_t words = ((size_t)(n + 63) / 64) * 8;
+        const size_t words = ((size_t)(n_alloc + 63) / 64) * 8;
         if (src.validity) QEH_HIP(hipMemsetAsync(out[j].validity, 0, words ? words : 8, ctx->stream));
         if (src.dtype == QEH_DT_BOOL) QEH_HIP(hipMemsetAsync(out[j].values, 0, words ? words : 8, ctx->stream));
         const ColRef cr = make_colref(src);
@@ -407,7 +441,7 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     }
     if (!utf8.empty()) {
         int s = iota.alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4);
-        if (s == QEH_OK) s = rowids.alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 4);
+        if (s == QEH_OK) s = rowids.alloc(ctx, (size_t)std::max<int64_t>(n_alloc, 1) * 4);
         if (s != QEH_OK) {
             cleanup();
             return s;
@@ -466,13 +500,14 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
         unsigned long long *ticket = (unsigned long long *)scr;
         uint32_t *err = (uint32_t *)((char *)scr + 8);
         uint64_t *tot = (uint64_t *)((char *)scr + 16);
+        uint64_t *done = (uint64_t *)((char *)scr + 24);
         uint64_t *status = (uint64_t *)((char *)scr + hdr);
         const int grid = grid_for(ctx, n, kFTile, 4);
         {
             KernelTimer kt(ctx, "filter");
             if (ff) {
 #define QEH_FF(NTV, NCV) \
-    hipLaunchKernelGGL((k_filter_fast<NTV, NCV>), dim3(grid), dim3(kBlock), 0, ctx->stream, ffi, n_tiles, terms, status, ticket, err, tot)
+    hipLaunchKernelGGL((k_filter_fast<NTV, NCV>), dim3(grid), dim3(kBlock), 0, ctx->stream, ffi, n_tiles, terms, status, ticket, err, tot, cap, exit_at, done)
 #define QEH_FF_NC(NTV)                                    \
     if (ff_nc == 1) QEH_FF(NTV, 1);                       \
     else if (ff_nc == 2) QEH_FF(NTV, 2);                  \
@@ -483,20 +518,20 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
 #undef QEH_FF
             } else if (fast)
                 hipLaunchKernelGGL(k_filter<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n, n_tiles, terms, prog, os,
-                                   status, ticket, err, tot);
+                                   status, ticket, err, tot, cap, exit_at, done);
             else
                 hipLaunchKernelGGL(k_filter<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, cs, n, n_tiles, terms, prog, os,
-                                   status, ticket, err, tot);
+                                   status, ticket, err, tot, cap, exit_at, done);
         }
         QEH_HIP(hipGetLastError());
-        uint64_t hdrv[3];
-        s = read_small(ctx, hdrv, scr, 24);
+        uint64_t hdrv[4];
+        s = read_small(ctx, hdrv, scr, 32);
         if (s == QEH_OK) s = kernel_error_status((uint32_t)hdrv[1], "filter");
         if (s != QEH_OK) {
             cleanup();
             return s;
         }
-        total = hdrv[2];
+        total = hdrv[3] ? cap : std::min<uint64_t>(hdrv[2], cap);  // done: at least `cap` rows qualified
     }
     for (int j : utf8) {
         int s = gather_column(ctx, cols[out_idx[j]], rowids.as<uint32_t>(), (int64_t)total, &out[j]);
@@ -513,6 +548,17 @@ extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, cons
     }
     *out_rows = (int64_t)total;
     return QEH_OK;
+}
+
+extern "C" int qeh_filter(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                          const int32_t *out_idx, int n_out, qeh_column *out, int64_t *out_rows) {
+    return filter_impl(ctx, cols, n_cols, predicate, out_idx, n_out, -1, out, out_rows);
+}
+
+extern "C" int qeh_filter_limit(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                                const int32_t *out_idx, int n_out, int64_t max_rows, qeh_column *out,
+                                int64_t *out_rows) {
+    return filter_impl(ctx, cols, n_cols, predicate, out_idx, n_out, max_rows, out, out_rows);
 }
 
 extern "C" int qeh_eval(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *expr, int64_t n_rows,

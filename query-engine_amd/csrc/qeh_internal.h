@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -64,6 +65,10 @@ struct TimingRecord {
 
 }  // namespace qeh
 
+namespace qeh {
+struct SourceCache;  // device-resident Scan inputs (executor.hip)
+}
+
 struct qeh_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -82,6 +87,8 @@ struct qeh_ctx {
     std::vector<qeh::TimingRecord> timing_pending;
     std::vector<hipEvent_t> event_free;
     std::map<std::string, std::pair<double, int64_t>> timing_done;
+    // Scan inputs kept on the device between queries (qeh_source.cache_key)
+    std::shared_ptr<qeh::SourceCache> source_cache;
 };
 
 namespace qeh {

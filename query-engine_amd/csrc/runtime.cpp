@@ -229,6 +229,7 @@ int qeh_shutdown(qeh_ctx *ctx) {
     for (auto e : ctx->event_free) hipEventDestroy(e);
     if (ctx->scratch) ctx->pool->free(ctx->scratch);
     if (ctx->pinned) hipHostFree(ctx->pinned);
+    ctx->source_cache.reset();  // its columns go back to the pool first
     delete ctx->pool;
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     if (ctx->aux_stream) {

@@ -72,6 +72,7 @@ SIGNATURES = {
     "qeh_kernel_time": (I, [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I64)]),
     "qeh_generate": (I, [P, I, U64, U64, I64, I64, I64, I64, P]),
     "qeh_filter": (I, [P, COLP, I, EXPRP, C.POINTER(C.c_int32), I, COLP, C.POINTER(I64)]),
+    "qeh_filter_limit": (I, [P, COLP, I, EXPRP, C.POINTER(C.c_int32), I, I64, COLP, C.POINTER(I64)]),
     "qeh_eval": (I, [P, COLP, I, EXPRP, I64, COLP]),
     "qeh_expr_type": (I, [C.POINTER(C.c_int32), I, EXPRP, C.POINTER(C.c_int32)]),
     "qeh_hash_aggregate": (I, [P, COLP, I, COLP, I, AGGP, I, I64, COLP, COLP, C.POINTER(I64)]),
@@ -89,6 +90,9 @@ SIGNATURES = {
     "qeh_validity_to_bytes": (I, [P, COLP, P]),
     "qeh_bytes_to_validity": (I, [P, P, I64, P]),
     "qeh_execute_plan": (I, [P, P, P, I, P, P, C.POINTER(I64)]),  # include/qeh_plan.h; typed in plan.py
+    "qeh_source_cache_evict": (I, [P, C.c_uint64]),
+    "qeh_source_cache_stats": (I, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+    "qeh_source_cache_budget": (I, [P, I64]),
 }
 
 _lib = None

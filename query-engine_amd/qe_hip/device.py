@@ -233,14 +233,20 @@ class Context:
 
     # ---- operators -------------------------------------------------------
     def filter(self, cols: Sequence[DeviceColumn], predicate: PhysicalExpr,
-               out_idx: Optional[Sequence[int]] = None) -> Tuple[List[DeviceColumn], int]:
+               out_idx: Optional[Sequence[int]] = None, max_rows: Optional[int] = None
+               ) -> Tuple[List[DeviceColumn], int]:
+        """qeh_filter; with `max_rows`, qeh_filter_limit (the first max_rows qualifying rows)."""
         out_idx = list(range(len(cols))) if out_idx is None else list(out_idx)
         e, keep = predicate.to_c()
         cin = self._cols(cols)
         oi = (C.c_int32 * max(len(out_idx), 1))(*out_idx)
         cout = (abi.QehColumn * max(len(out_idx), 1))()
         rows = C.c_int64()
-        abi.check(self.lib.qeh_filter(self.h, cin, len(cols), C.byref(e), oi, len(out_idx), cout, C.byref(rows)))
+        if max_rows is None:
+            abi.check(self.lib.qeh_filter(self.h, cin, len(cols), C.byref(e), oi, len(out_idx), cout, C.byref(rows)))
+        else:
+            abi.check(self.lib.qeh_filter_limit(self.h, cin, len(cols), C.byref(e), oi, len(out_idx), int(max_rows),
+                                                cout, C.byref(rows)))
         return [self._wrap(cout[i]) for i in range(len(out_idx))], rows.value
 
     def eval(self, cols: Sequence[DeviceColumn], expr: PhysicalExpr, n_rows: Optional[int] = None) -> DeviceColumn:

@@ -14,6 +14,7 @@ runs `qeh_execute_plan` on the device and imports the result as
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -80,7 +81,7 @@ class QehPlanC(C.Structure):
 
 class QehSourceC(C.Structure):
     _fields_ = [("schema", C.POINTER(ArrowSchemaC)), ("batches", C.POINTER(C.POINTER(ArrowArrayC))),
-                ("n_batches", C.c_int64)]
+                ("n_batches", C.c_int64), ("cache_key", C.c_uint64)]
 
 
 # ---- DataSource -------------------------------------------------------------------
@@ -93,13 +94,36 @@ class DataSource:
     def schema(self) -> pa.Schema:
         raise NotImplementedError
 
+    def cache_key(self) -> int:
+        """Non-zero: scan() returns the same batches for as long as this key is in use, so the
+        executor may keep their device copy between queries (qeh_source.cache_key). 0: import
+        on every execute, as the reference re-scans on every execute (executor.rs:71-76)."""
+        return 0
+
+
+_next_cache_key = itertools.count(1)
+
 
 class MemoryDataSource(DataSource):
-    """crates/query-storage/src/memory.rs:305-308: scan() clones the batches."""
+    """crates/query-storage/src/memory.rs:305-308: scan() clones the batches.
 
-    def __init__(self, schema: pa.Schema, batches: Sequence[pa.RecordBatch]):
+    `device_cache=True` keeps the imported columns resident on the device between queries; the
+    key changes whenever the batches do (`insert`), so a stale copy is never read."""
+
+    def __init__(self, schema: pa.Schema, batches: Sequence[pa.RecordBatch], device_cache: bool = False):
         self._schema = schema
         self._batches = list(batches)
+        self._device_cache = device_cache
+        self._key = next(_next_cache_key) if device_cache else 0
+
+    def insert(self, batch: pa.RecordBatch):
+        """memory.rs insert_batch: append, and retire the cached device copy's key."""
+        self._batches.append(batch)
+        if self._device_cache:
+            self._key = next(_next_cache_key)
+
+    def cache_key(self) -> int:
+        return self._key
 
     def scan(self):
         return list(self._batches)
@@ -317,7 +341,8 @@ class QueryExecutor:
                 b._export_to_c(C.addressof(a))
                 arrs.append(a)
             ptrs = (C.POINTER(ArrowArrayC) * max(len(arrs), 1))(*[C.pointer(a) for a in arrs])
-            srcs.append(QehSourceC(C.pointer(sch), C.cast(ptrs, C.POINTER(C.POINTER(ArrowArrayC))), len(arrs)))
+            srcs.append(QehSourceC(C.pointer(sch), C.cast(ptrs, C.POINTER(C.POINTER(ArrowArrayC))), len(arrs),
+                                   int(ds.cache_key())))
             exported.append((sch, arrs, ptrs))
         src_arr = (QehSourceC * max(len(srcs), 1))(*srcs)
         out_s, out_a, nb = ArrowSchemaC(), ArrowArrayC(), C.c_int64()
@@ -334,3 +359,22 @@ class QueryExecutor:
         if nb.value == 0:
             return []
         return [pa.RecordBatch._import_from_c(C.addressof(out_a), C.addressof(out_s))]
+
+    # ---- device-resident Scan cache (qeh_source_cache_*) ----
+    def cache_stats(self) -> dict:
+        lib = abi.load()
+        e, b, h, m = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        abi.check(lib.qeh_source_cache_stats(self.ctx.h, C.byref(e), C.byref(b), C.byref(h), C.byref(m)))
+        return {"entries": e.value, "bytes": b.value, "hits": h.value, "misses": m.value}
+
+    def cache_evict(self, source: Optional[DataSource] = None):
+        """Drop `source`'s device copy (all copies when None)."""
+        lib = abi.load()
+        key = 0 if source is None else int(source.cache_key())
+        if source is not None and key == 0:
+            return
+        abi.check(lib.qeh_source_cache_evict(self.ctx.h, C.c_uint64(key)))
+
+    def cache_budget(self, nbytes: int):
+        lib = abi.load()
+        abi.check(lib.qeh_source_cache_budget(self.ctx.h, C.c_int64(nbytes)))

@@ -11,7 +11,7 @@ import pyarrow as pa
 import pytest
 
 import oracle_bind as ob
-from helpers import assert_grouped_equal, rows_of, sorted_rows
+from helpers import assert_grouped_equal, assert_rows_equal, rows_of, sorted_rows
 from qe_hip import AggregateExpr, AggregateFunction as AF, BinaryOp, UnaryExpr, UnaryOp, abi, binop, col, lit
 from qe_hip import (Filter, HashAggregate, HashJoin, JoinType, Limit, MemoryDataSource, Projection, QueryExecutor,
                     Scan, Sort, SubqueryScan, Window, WindowExpr, WindowFunctionType)
@@ -203,3 +203,112 @@ def test_device_filter_matches_arrow_goldens(qx, name):
     out = qx.execute(Filter(Scan(source(t, 3)), PREDS[name]))
     want = [(z[f"{name}__{c}"], z[f"{name}__{c}__valid"]) for c in COLS]
     assert rows_of(as_cols(out)) == rows_of(want)
+
+
+@pytest.mark.gpu
+def test_device_scan_cache(ctx):
+    """§8 f1: a DataSource with a cache key keeps its device columns between queries; results stay
+    identical to the uncached import, insert() retires the stale copy, evict/budget drop entries."""
+    qx = QueryExecutor(ctx)
+    qx.cache_evict()
+    fact, dim = metric_tables(200_000, 10_000, 128)
+    plain = qx.execute(metric_plan(fact, dim, chunks=2))
+    fsrc = MemoryDataSource(fact.schema, fact.to_batches(max_chunksize=70_000), device_cache=True)
+    dsrc = MemoryDataSource(dim.schema, dim.to_batches(), device_cache=True)
+
+    def plan():
+        join = HashJoin(Scan(fsrc), Scan(dsrc), JoinType.Inner,
+                        binop(Column("f.k", 1), BinaryOp.Equal, Column("d.k", 3)))
+        filt = Filter(join, binop(Column("f.x", 0), BinaryOp.Greater, lit(49)))
+        return HashAggregate(filt, [Column("d.g", 4)],
+                             [AggregateExpr(AF.Sum, Column("f.v", 2)), AggregateExpr(AF.Count, Column("f.v", 2))])
+
+    s0 = qx.cache_stats()
+    first = qx.execute(plan())
+    s1 = qx.cache_stats()
+    assert s1["misses"] - s0["misses"] == 2 and s1["entries"] == 2
+    assert s1["bytes"] == 200_000 * 24 + 10_000 * 16
+    second = qx.execute(plan())
+    s2 = qx.cache_stats()
+    assert s2["hits"] - s1["hits"] == 2 and s2["misses"] == s1["misses"]
+    for a in (first, second):
+        assert_rows_equal(sorted_rows(as_cols(a)), sorted_rows(as_cols(plain)), float_cols=[1])
+
+    # insert(): new key, so the next query imports the grown table
+    extra = pa.table({"f.x": np.full(5, 99, np.int64), "f.k": np.asarray(dim.column(0))[:5],
+                      "f.v": np.ones(5)}).to_batches()[0]
+    fsrc.insert(extra)
+    grown = qx.execute(plan())
+    s3 = qx.cache_stats()
+    assert s3["misses"] - s2["misses"] == 1
+    want = qx.execute(HashAggregate(Filter(
+        HashJoin(Scan(source(pa.concat_tables([fact, pa.Table.from_batches([extra])]))), Scan(source(dim)),
+                 JoinType.Inner, binop(Column("f.k", 1), BinaryOp.Equal, Column("d.k", 3))),
+        binop(Column("f.x", 0), BinaryOp.Greater, lit(49))), [Column("d.g", 4)],
+        [AggregateExpr(AF.Sum, Column("f.v", 2)), AggregateExpr(AF.Count, Column("f.v", 2))]))
+    assert_rows_equal(sorted_rows(as_cols(grown)), sorted_rows(as_cols(want)), float_cols=[1])
+
+    qx.cache_evict(dsrc)
+    assert qx.cache_stats()["entries"] == 2  # old fact key + new fact key
+    qx.cache_budget(200_005 * 24)  # room for the newest fact copy only
+    assert qx.cache_stats()["entries"] == 1
+    qx.cache_evict()
+    assert qx.cache_stats()["entries"] == 0 and qx.cache_stats()["bytes"] == 0
+    qx.cache_budget(64 << 30)
+
+    # nullable + string + bool columns through a cached scan
+    t = pa.table({"t.s": pa.array(["a", None, "ccc", "dd"] * 50), "t.b": pa.array([True, False, None, True] * 50),
+                  "t.i": pa.array([1, None, 3, 4] * 50, pa.int64())})
+    ts = MemoryDataSource(t.schema, t.to_batches(max_chunksize=64), device_cache=True)
+    p = Filter(Scan(ts), binop(Column("t.i", 2), BinaryOp.Greater, lit(1)))
+    a, b = qx.execute(p), qx.execute(p)
+    ref = qx.execute(Filter(Scan(source(t)), binop(Column("t.i", 2), BinaryOp.Greater, lit(1))))
+    assert [x.to_pylist() for x in pa.Table.from_batches(a).columns] == \
+        [x.to_pylist() for x in pa.Table.from_batches(b).columns] == \
+        [x.to_pylist() for x in pa.Table.from_batches(ref).columns]
+    assert qx.cache_stats()["hits"] >= 1
+    qx.cache_evict()
+
+
+def _arrow_rows(batches):
+    if not batches:
+        return []
+    t = pa.Table.from_batches(batches)
+    return list(zip(*[c.to_pylist() for c in t.columns])), t.schema.names
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["limit_filter", "limit_proj_filter", "proj_filter_expr", "limit_proj_expr",
+                                   "limit_skip_past_end", "limit_zero"])
+def test_fused_filter_projection_limit(qx, monkeypatch, shape):
+    """§8 f1: Limit(Projection(Filter(Scan))) and its sub-shapes run as one capped filter over the
+    projected columns; results equal the unfused chain (QEH_NO_FUSION) and the oracle filter."""
+    r = np.random.default_rng(len(shape))
+    n = 400_003
+    t = pa.table({"t.x": pa.array(r.integers(0, 100, n), pa.int64()),
+                  "t.s": pa.array([f"s{i % 977}" if i % 13 else None for i in range(n)]),
+                  "t.v": pa.array(r.random(n), mask=r.random(n) < 0.1),
+                  "t.b": pa.array(r.random(n) < 0.5),
+                  "t.i": pa.array(r.integers(-(2 ** 20), 2 ** 20, n), pa.int64())})
+    pred = binop(Column("t.x", 0), BinaryOp.Greater, lit(90))
+    filt = Filter(Scan(source(t, 3)), pred)
+    cols_proj = Projection(filt, [Column("t.i", 4), Column("t.s", 1), Column("t.b", 3), Column("t.v", 2)],
+                           ["t.i", "t.s", "t.b", "t.v"])
+    expr_proj = Projection(filt, [binop(Column("t.i", 4), BinaryOp.Add, Column("t.x", 0)), Column("t.s", 1)],
+                           ["y", "t.s"])
+    plan = {"limit_filter": Limit(filt, 17, 5000),
+            "limit_proj_filter": Limit(cols_proj, 0, 1234),
+            "proj_filter_expr": expr_proj,
+            "limit_proj_expr": Limit(expr_proj, 3, 10),
+            "limit_skip_past_end": Limit(cols_proj, 10 ** 8, 5),
+            "limit_zero": Limit(filt, 0, 0)}[shape]
+    fused = _arrow_rows(qx.execute(plan))
+    monkeypatch.setenv("QEH_NO_FUSION", "1")
+    plain = _arrow_rows(qx.execute(plan))
+    assert fused == plain
+    if shape == "limit_proj_filter":
+        keep = np.nonzero(np.asarray(t.column(0)) > 90)[0][:1234]
+        rows, names = fused
+        assert names == ["t.i", "t.s", "t.b", "t.v"]
+        assert [x[0] for x in rows] == np.asarray(t.column(4))[keep].tolist()
+        assert [x[1] for x in rows] == [t.column(1)[int(i)].as_py() for i in keep]

@@ -185,3 +185,53 @@ def test_fast_filter_output_subset_and_aligned_offset(ctx):
     keep = x > 49
     assert rows == int(keep.sum())
     assert np.array_equal(out[0].to_numpy()[0], v[keep])
+
+
+def run_filter_limit(ctx, cols, pred, cap, offset=0):
+    """qeh_filter_limit == the oracle's full filter, then the first `cap` rows (LimitExec)."""
+    dev = [ctx.upload(v, m, offset=offset) for v, m in cols]
+    out, rows = ctx.filter(dev, pred, max_rows=cap)
+    want, wrows, _ = ob.filter([ob.HostCol(v, m) for v, m in cols], pred)
+    assert rows == min(wrows, cap)
+    for j, (g, w) in enumerate(zip([c.to_numpy() for c in out], want)):
+        wv, wm = w
+        same_col(g, (np.asarray(wv)[:cap], np.asarray(wm)[:cap]), f"col {j} cap {cap}")
+    return rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gt_int", "and_or", "bare_bool", "arith", "modulo"])
+@pytest.mark.parametrize("cap", [0, 1, 31, 33, 2048, 5000, 10 ** 9])
+def test_filter_limit_generic(ctx, name, cap):
+    """Generic kernel (nullable int/float/bool columns): rows past the cap are dropped inside the
+    filter; validity and bit-packed booleans stay exact at the cut."""
+    run_filter_limit(ctx, table(20_011, seed=cap % 97), PREDS[name], cap)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [0, 1, 7, 4096, 100_000, 10 ** 9])
+@pytest.mark.parametrize("n", [1, 2049, 3_000_001])
+def test_filter_limit_fast_early_exit(ctx, monkeypatch, cap, n):
+    """k_filter_fast with a cap: tiles claimed after `cap` rows are placed publish a >= cap prefix
+    and stop (no hang, no missing rows); the same rows with the generic kernel."""
+    r = np.random.default_rng(n + cap)
+    cols = [(r.integers(0, 100, n).astype(np.int64), None), (r.random(n), None)]
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    rows = run_filter_limit(ctx, cols, pred, cap)
+    monkeypatch.setenv("QEH_NO_FAST_FILTER", "1")
+    assert run_filter_limit(ctx, cols, pred, cap) == rows
+
+
+@pytest.mark.gpu
+def test_filter_limit_still_raises_past_the_cap(ctx):
+    """A predicate that can raise is evaluated on every row even under a cap (the reference
+    evaluates the whole batch before LimitExec slices it)."""
+    n = 100_000
+    big = np.zeros(n, np.int64)
+    big[-1] = 2 ** 62  # overflows only on the last row
+    dev = [ctx.upload(np.arange(n, dtype=np.int64)), ctx.upload(big)]
+    pred = binop(binop(col(1), BinaryOp.Multiply, lit(4)), BinaryOp.GreaterEqual, lit(0))
+    with pytest.raises(QehError) as e:
+        ctx.filter(dev, pred, max_rows=10)
+    assert e.value.status == abi.QEH_E_OVERFLOW
+
