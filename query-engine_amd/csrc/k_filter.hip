@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(ColSet cols, int64_t n, int64
     for (;;) {
         if (threadIdx.x == 0) {
             int64_t t = (int64_t)atomicAdd(ticket, 1ull);
-            if (t < n_tiles && ld_agent(done)) {
+            if (exit_at != kValMask && t < n_tiles && ld_agent(done)) {
                 // the first `cap` rows are already placed: publish a prefix >= cap so that a
                 // successor that started before `done` was raised still completes its look-back
                 st_agent(&status[t], kFlagIncl | cap);
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_fast(FastFilterIn in, int64_t
     for (;;) {
         if (threadIdx.x == 0) {
             int64_t t = (int64_t)atomicAdd(ticket, 1ull);
-            if (t < n_tiles && ld_agent(done)) {
+            if (exit_at != kValMask && t < n_tiles && ld_agent(done)) {
                 // the first `cap` rows are already placed: publish a prefix >= cap so that a
                 // successor that started before `done` was raised still completes its look-back
                 st_agent(&status[t], kFlagIncl | cap);
@@ -491,7 +491,7 @@ static int filter_impl(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const q
     uint64_t total = 0;
     if (n_tiles > 0) {
         void *scr = nullptr;
-        const size_t hdr = 64;
+        const size_t hdr = 256;  // ticket/err/total in one line, `done` in its own (away from the ticket atomics)
         int s = scratch_zeroed(ctx, hdr + (size_t)n_tiles * 8, &scr);
         if (s != QEH_OK) {
             cleanup();
@@ -500,7 +500,7 @@ static int filter_impl(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const q
         unsigned long long *ticket = (unsigned long long *)scr;
         uint32_t *err = (uint32_t *)((char *)scr + 8);
         uint64_t *tot = (uint64_t *)((char *)scr + 16);
-        uint64_t *done = (uint64_t *)((char *)scr + 24);
+        uint64_t *done = (uint64_t *)((char *)scr + 128);
         uint64_t *status = (uint64_t *)((char *)scr + hdr);
         const int grid = grid_for(ctx, n, kFTile, 4);
         {
@@ -524,14 +524,14 @@ static int filter_impl(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const q
                                    status, ticket, err, tot, cap, exit_at, done);
         }
         QEH_HIP(hipGetLastError());
-        uint64_t hdrv[4];
-        s = read_small(ctx, hdrv, scr, 32);
+        uint64_t hdrv[17];
+        s = read_small(ctx, hdrv, scr, 136);
         if (s == QEH_OK) s = kernel_error_status((uint32_t)hdrv[1], "filter");
         if (s != QEH_OK) {
             cleanup();
             return s;
         }
-        total = hdrv[3] ? cap : std::min<uint64_t>(hdrv[2], cap);  // done: at least `cap` rows qualified
+        total = hdrv[16] ? cap : std::min<uint64_t>(hdrv[2], cap);  // done: at least `cap` rows qualified
     }
     for (int j : utf8) {
         int s = gather_column(ctx, cols[out_idx[j]], rowids.as<uint32_t>(), (int64_t)total, &out[j]);

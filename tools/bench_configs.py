@@ -8,10 +8,12 @@
   cfg5  ROW_NUMBER() OVER (PARTITION BY k ORDER BY v), k in [0, 2^20)
         (16 B read + 8 B write per row)
   filter  the Filter operator alone: SELECT x, k, v WHERE x > 49 (24 B in + 12 B out avg per row)
+  limit   the same filter under LIMIT 1000 (capped filter, early exit)
+  plan    the metric query through QueryExecutor from host Arrow batches, cold vs device-cached Scan
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
-usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter] [--scale 1.0]
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan] [--scale 1.0]
 """
 import argparse
 import json
@@ -50,7 +52,7 @@ def timed(ctx, fn, reps, names):
 
 
 def line(cfg, rows, wall, alg_bytes, kernel_ms, kernel, cpu, extra=None):
-    gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+    gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms and alg_bytes else None
     d = {"config": cfg, "rows": rows, "rows_per_s": rows / wall, "ms_per_run": wall * 1e3,
          "dominant_kernel": kernel, "kernel_ms": kernel_ms, "alg_bytes": alg_bytes,
          "achieved_GBs": gbs, "frac_of_8TBs": gbs / PEAK if gbs else None, "cpu_baseline": cpu}
@@ -147,6 +149,60 @@ def cfg_filter(ctx, scale):
          {"selected": rows})
 
 
+def cfg_limit(ctx, scale):
+    """SELECT x, k, v FROM t WHERE x > 49 LIMIT 1000 over 5e8 rows: qeh_filter_limit stops claiming
+    tiles once 1000 rows are placed (the reference filters every row, then slices)."""
+    n = int(5e8 * scale)
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 1024)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+
+    def fn():
+        out, rows = ctx.filter([x, k, v], pred, max_rows=1000)
+        for c in out:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 20, ["filter"])
+    line("filter+limit 5e8 x3 cols LIMIT 1000", n, wall, None, kt["filter"], "k_filter_fast (capped)", None,
+         {"selected": rows, "note": "rows_per_s counts the table's rows; only the leading tiles are read"})
+
+
+def cfg_plan(ctx, scale):
+    """The metric query through QueryExecutor.execute from host Arrow batches (the reference's
+    MemoryDataSource path): cold = every execute imports the Scan batches over PCIe; cached = the
+    sources carry a cache key, so the device copy from the first execute is reused."""
+    import pyarrow as pa
+    from qe_hip import (AggregateExpr, Filter, HashAggregate, HashJoin, JoinType, MemoryDataSource,
+                        QueryExecutor, Scan)
+    from qe_hip.expr import Column
+    n, nd = int(1e8 * scale), int(1e7 * scale)
+    cols = {"f.x": (abi.GEN_UNIFORM_MOD, 1, 100), "f.k": (abi.GEN_UNIFORM_MOD, 2, nd), "f.v": (abi.GEN_UNIT_F64, 3, 0)}
+    fact = pa.table({name: ctx.generate(kind, SEED, cid, n, mod).to_numpy()[0] for name, (kind, cid, mod) in cols.items()})
+    dim = pa.table({"d.k": ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd).to_numpy()[0],
+                    "d.g": ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1024).to_numpy()[0]})
+    qx = QueryExecutor(ctx)
+    out = {}
+    for mode in ("cold", "cached"):
+        cache = mode == "cached"
+        fs = MemoryDataSource(fact.schema, fact.to_batches(max_chunksize=1 << 23), device_cache=cache)
+        ds = MemoryDataSource(dim.schema, dim.to_batches(), device_cache=cache)
+        join = HashJoin(Scan(fs), Scan(ds), JoinType.Inner, binop(Column("f.k", 1), BinaryOp.Equal, Column("d.k", 3)))
+        plan = HashAggregate(Filter(join, binop(Column("f.x", 0), BinaryOp.Greater, lit(49))), [Column("d.g", 4)],
+                             [AggregateExpr(AF.Sum, Column("f.v", 2)), AggregateExpr(AF.Count, Column("f.v", 2))])
+        qx.execute(plan)
+        reps = 3 if mode == "cold" else 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = qx.execute(plan)
+        wall = (time.perf_counter() - t0) / reps
+        out[mode] = wall
+        line(f"plan metric query 1e8 x 1e7 from host Arrow ({mode})", n, wall, None, None, None, None,
+             {"groups": res[0].num_rows, "host_bytes_per_execute": 24 * n + 16 * nd if mode == "cold" else 0,
+              "pcie_inclusive_GBs": (24 * n + 16 * nd) / wall / 1e9 if mode == "cold" else None})
+        qx.cache_evict()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="cfg2,cfg3,cfg5,filter")
@@ -158,7 +214,8 @@ def main():
     ctx = qe_hip.Context(0)
     ctx.set_stream(s.cuda_stream)
     for name in args.only.split(","):
-        {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter}[name](ctx, args.scale)
+        {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
+         "plan": cfg_plan}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
