@@ -222,6 +222,17 @@ int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, const qeh_col
                         const qeh_column *build_cols, int n_build_cols, qeh_column *out_probe,
                         qeh_column *out_build, int64_t *out_rows);
 
+/* LEFT / RIGHT / FULL equi-join on one Int32/Int64 key.  The reference sends
+ * these through the same Cartesian join_batches as INNER (executor.rs:383-435); the intended
+ * semantics extend the INNER contract: every matching (left, right) pair, plus each unmatched left
+ * row (LEFT, FULL) with NULL right columns, plus each unmatched right row (RIGHT, FULL) with NULL
+ * left columns; NULL keys never match.  join_type: qeh_join_type values (qeh_plan.h) 1 LEFT,
+ * 2 RIGHT, 3 FULL (0 = INNER, forwarded to qeh_hash_join_inner with the left side probing).
+ * Row order: preserved side's row order, FULL's unmatched right rows last (compare as multisets). */
+int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column *left_key, const qeh_column *left_cols,
+                        int n_left_cols, const qeh_column *right_key, const qeh_column *right_cols, int n_right_cols,
+                        qeh_column *out_left, qeh_column *out_right, int64_t *out_rows);
+
 /* Fused filter -> hash-join -> group-by (the BASELINE metric path):
  *   SELECT <build group keys>, AGG(probe cols)... FROM probe JOIN build
  *   ON probe.key = build.key WHERE <predicate over probe cols> GROUP BY <build keys>

@@ -156,6 +156,7 @@ static void arr_to_col(const arr *a, const int64_t *idx, int64_t m, qo_col *out)
     out->valid = calloc((size_t)(m > 0 ? m : 1), 1);
     for (int64_t k = 0; k < m; ++k) {
         int64_t r = idx ? idx[k] : k;
+        if (r < 0) continue; /* outer-join filler row: NULL */
         out->valid[k] = a->v[r];
         switch (out->dtype) {
             case QEH_DT_BOOL: ((uint8_t *)out->values)[k] = (uint8_t)(a->i[r] & 1); break;
@@ -684,6 +685,75 @@ int qo_hash_join_inner(const qo_col *probe_key, const qo_col *probe_cols, int n_
     *out_rows = cnt;
     free(pi);
     free(bi);
+    jmap_free(&m);
+    arr_free(&pk);
+    arr_free(&bk);
+    return s;
+}
+
+/* LEFT / RIGHT / FULL equi-join.  The reference routes these
+ * through the same Cartesian join_batches as INNER (executor.rs:383-435); the
+ * intended semantics extend the INNER contract: every matching (left, right)
+ * pair, plus each left row without a match (LEFT, FULL) with the right columns
+ * NULL, plus each right row without a match (RIGHT, FULL) with the left
+ * columns NULL.  NULL keys never match.  Row order: LEFT and FULL in left-row
+ * order (matches of one row in build order), the unmatched right rows of FULL
+ * after them in right-row order; RIGHT in right-row order. */
+static void pairs_push(int64_t **a, int64_t **b, int64_t *cnt, int64_t *cap, int64_t x, int64_t y) {
+    if (*cnt == *cap) {
+        *cap *= 2;
+        *a = realloc(*a, (size_t)*cap * sizeof(int64_t));
+        *b = realloc(*b, (size_t)*cap * sizeof(int64_t));
+    }
+    (*a)[*cnt] = x;
+    (*b)[(*cnt)++] = y;
+}
+
+int qo_hash_join_outer(int join_type, const qo_col *left_key, const qo_col *left_cols, int n_left,
+                       const qo_col *right_key, const qo_col *right_cols, int n_right, qo_col *out_left,
+                       qo_col *out_right, int64_t *out_rows) {
+    if (join_type < 1 || join_type > 3) return err(QEH_E_INVALID, "outer join type must be LEFT, RIGHT or FULL");
+    const int right_outer = join_type == 2;
+    /* RIGHT probes with the right side and builds on the left */
+    const qo_col *pkc = right_outer ? right_key : left_key, *bkc = right_outer ? left_key : right_key;
+    arr pk, bk;
+    int s = join_key_arr(pkc, &pk);
+    if (s != QEH_OK) return s;
+    s = join_key_arr(bkc, &bk);
+    if (s != QEH_OK) { arr_free(&pk); return s; }
+    jmap m;
+    jmap_build(&bk, &m);
+    int64_t cap = pk.n + bk.n + 1, cnt = 0;
+    int64_t *pi = malloc((size_t)cap * sizeof(int64_t)), *bi = malloc((size_t)cap * sizeof(int64_t));
+    uint8_t *hit = calloc((size_t)bk.n + 1, 1);
+    for (int64_t r = 0; r < pk.n; ++r) {
+        int any = 0;
+        if (pk.v[r])
+            for (int64_t b = jmap_first(&m, pk.i[r]); b >= 0; b = m.next[b]) {
+                pairs_push(&pi, &bi, &cnt, &cap, r, b);
+                hit[b] = 1;
+                any = 1;
+            }
+        if (!any) pairs_push(&pi, &bi, &cnt, &cap, r, -1);
+    }
+    if (join_type == 3)
+        for (int64_t b = 0; b < bk.n; ++b)
+            if (!hit[b]) pairs_push(&pi, &bi, &cnt, &cap, -1, b);
+    const int64_t *li = right_outer ? bi : pi, *ri = right_outer ? pi : bi;
+    for (int j = 0; j < n_left && s == QEH_OK; ++j) {
+        arr a;
+        s = col_to_arr(&left_cols[j], &a);
+        if (s == QEH_OK) { arr_to_col(&a, li, cnt, &out_left[j]); arr_free(&a); }
+    }
+    for (int j = 0; j < n_right && s == QEH_OK; ++j) {
+        arr a;
+        s = col_to_arr(&right_cols[j], &a);
+        if (s == QEH_OK) { arr_to_col(&a, ri, cnt, &out_right[j]); arr_free(&a); }
+    }
+    *out_rows = cnt;
+    free(pi);
+    free(bi);
+    free(hit);
     jmap_free(&m);
     arr_free(&pk);
     arr_free(&bk);

@@ -52,6 +52,10 @@ int qo_hash_aggregate(const qo_col *keys, int n_keys, const qo_col *inputs, int 
 int qo_hash_join_inner(const qo_col *probe_key, const qo_col *probe_cols, int n_probe,
                        const qo_col *build_key, const qo_col *build_cols, int n_build,
                        qo_col *out_probe, qo_col *out_build, int64_t *out_rows);
+/* LEFT (1) / RIGHT (2) / FULL (3) equi-join, values of qeh_join_type (qeh_plan.h). */
+int qo_hash_join_outer(int join_type, const qo_col *left_key, const qo_col *left_cols, int n_left,
+                       const qo_col *right_key, const qo_col *right_cols, int n_right, qo_col *out_left,
+                       qo_col *out_right, int64_t *out_rows);
 int qo_join_filter_aggregate(const qo_col *probe_cols, int n_probe, int probe_key_idx,
                              const qeh_expr_node *pred, int n_pred, const qo_col *build_key,
                              const qo_col *build_group_keys, int n_group_keys, const qeh_agg *aggs,

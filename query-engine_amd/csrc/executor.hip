@@ -683,13 +683,15 @@ class Executor {
             QEH_HIP(hipStreamSynchronize(ctx_->stream));
             rows = m;
         } else {
-            if (nd.join_type != QEH_JOIN_INNER)
-                return fail(QEH_E_UNSUPPORTED, "LEFT/RIGHT/FULL joins are not implemented on the device (SURVEY.md §8 f3)");
             int lk, rk;
             if (!equi_keys(nd.predicate, (int)l.cols.size(), &lk, &rk))
                 return fail(QEH_E_UNSUPPORTED, "only single-column equi-joins (l.k = r.k) run on the device");
-            QEH_TRY(qeh_hash_join_inner(ctx_, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(), (int)rc.size(),
-                                        lo.data(), ro.data(), &rows));
+            if (nd.join_type == QEH_JOIN_INNER)
+                QEH_TRY(qeh_hash_join_inner(ctx_, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(), (int)rc.size(),
+                                            lo.data(), ro.data(), &rows));
+            else  // LEFT / RIGHT / FULL
+                QEH_TRY(qeh_hash_join_outer(ctx_, nd.join_type, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(),
+                                            (int)rc.size(), lo.data(), ro.data(), &rows));
             for (auto &c : lo) out->cols.push_back(own(ctx_, c));
             for (auto &c : ro) out->cols.push_back(own(ctx_, c));
         }

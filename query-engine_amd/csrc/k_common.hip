@@ -172,8 +172,9 @@ __global__ void k_gather(ColRef src, const uint32_t *__restrict__ idx, int64_t m
         int64_t i = w * 64 + lane;
         bool live = i < m;
         uint32_t j = live ? idx[i] : 0;
-        bool valid = live && col_valid(src, j);
-        if (live) out[i] = ((const T *)src.values)[j];
+        const bool hit = live && j != kNullRow;  // kNullRow: outer-join filler -> NULL
+        bool valid = hit && col_valid(src, j);
+        if (live) out[i] = hit ? ((const T *)src.values)[j] : T(0);
         if (out_valid) {
             uint64_t b = __ballot(valid);
             if (lane == 0) out_valid[w] = b;
@@ -189,8 +190,9 @@ __global__ void k_gather_bool(ColRef src, const uint32_t *__restrict__ idx, int6
         int64_t i = w * 64 + lane;
         bool live = i < m;
         uint32_t j = live ? idx[i] : 0;
-        bool v = live && bit_at((const uint8_t *)src.values, src.vbit0 + j);
-        bool valid = live && col_valid(src, j);
+        const bool hit = live && j != kNullRow;
+        bool v = hit && bit_at((const uint8_t *)src.values, src.vbit0 + j);
+        bool valid = hit && col_valid(src, j);
         uint64_t bv = __ballot(v), bn = __ballot(valid);
         if (lane == 0) {
             out[w] = bv;
@@ -203,6 +205,10 @@ __global__ void k_gather_bool(ColRef src, const uint32_t *__restrict__ idx, int6
 __global__ void k_utf8_lengths(const int32_t *__restrict__ offs, int64_t off0, const uint32_t *__restrict__ idx, int64_t m,
                                uint32_t *__restrict__ len) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        if (idx[i] == kNullRow) {
+            len[i] = 0;
+            continue;
+        }
         const int64_t r = off0 + idx[i];
         len[i] = (uint32_t)(offs[r + 1] - offs[r]);
     }
@@ -220,13 +226,27 @@ __global__ void k_utf8_copy(const int32_t *__restrict__ offs, int64_t off0, cons
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
     for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < m; w += nw) {
+        if (idx[w] == kNullRow) continue;
         const int64_t r = off0 + idx[w];
         const int32_t s = offs[r], e = offs[r + 1], d = out_offs[w];
         for (int32_t b = lane; b < e - s; b += 64) out[d + b] = data[s + b];
     }
 }
 
-static int gather_utf8(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out) {
+// validity bits of gathered rows (kNullRow -> NULL)
+__global__ void k_gather_valid(ColRef src, const uint32_t *__restrict__ idx, int64_t m, uint64_t *__restrict__ out_valid) {
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int lane = threadIdx.x & 63;
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w * 64 < m; w += nwaves) {
+        const int64_t i = w * 64 + lane;
+        const uint32_t j = i < m ? idx[i] : kNullRow;
+        const uint64_t b = __ballot(j != kNullRow && col_valid(src, j));
+        if (lane == 0) out_valid[w] = b;
+    }
+}
+
+static int gather_utf8(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out,
+                       bool nullable_idx) {
     std::memset(out, 0, sizeof(*out));
     out->dtype = QEH_DT_UTF8;
     out->owned = 1;
@@ -255,20 +275,15 @@ static int gather_utf8(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx,
     if (m > 0)
         hipLaunchKernelGGL(k_utf8_copy, dim3(grid_for(ctx, m, kBlock / 64, 8)), dim3(kBlock), 0, ctx->stream, src.offsets,
                            src.offset, (const uint8_t *)src.values, idx, m, out->offsets, (uint8_t *)out->values);
-    if (src.validity) {
+    if (src.validity || nullable_idx) {
         void *v = nullptr;
         const size_t vb = std::max<size_t>(((size_t)(m + 63) / 64) * 8, 8);
         QEH_TRY(ctx->pool->alloc(vb, &v));
         out->validity = (uint8_t *)v;
         out->null_count = -1;
-        ColRef sr = make_colref(src);
-        sr.dtype = QEH_DT_BOOL;  // only validity is read (values pointer unused for bits)
-        sr.values = src.validity;
-        // reuse the boolean gather: values = validity bits, validity = none
-        ColRef vr = sr;
-        vr.validity = nullptr;
-        hipLaunchKernelGGL(k_gather_bool, dim3(grid_for(ctx, (m + 63) / 64, kBlock / 64, 8)), dim3(kBlock), 0, ctx->stream,
-                           vr, idx, m, (uint64_t *)out->validity, (uint64_t *)nullptr);
+        if (m > 0)
+            hipLaunchKernelGGL(k_gather_valid, dim3(grid_for(ctx, (m + 63) / 64, kBlock / 64, 8)), dim3(kBlock), 0,
+                               ctx->stream, make_colref(src), idx, m, (uint64_t *)out->validity);
     } else {
         out->null_count = 0;
     }
@@ -276,10 +291,11 @@ static int gather_utf8(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx,
     return QEH_OK;
 }
 
-int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out) {
+int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out,
+                  bool nullable_idx) {
     QEH_TRY(check_column(src, "gather"));
-    if (src.dtype == QEH_DT_UTF8) return gather_utf8(ctx, src, idx, m, out);
-    bool with_valid = src.validity != nullptr;
+    if (src.dtype == QEH_DT_UTF8) return gather_utf8(ctx, src, idx, m, out, nullable_idx);
+    bool with_valid = src.validity != nullptr || nullable_idx;
     QEH_TRY(alloc_column(ctx, src.dtype, m, with_valid, out));
     if (m == 0) return QEH_OK;
     ColRef s = make_colref(src);

@@ -30,12 +30,14 @@ namespace qeh {
 constexpr int kJR = 8;
 constexpr int kJTile = kBlock * kJR;
 
-template <bool UNIQUE>
+// OUTER: a probe row without a match (NULL key included) still emits one pair (row, kNullRow);
+// `matched` (FULL joins) gets a 1 at every build row that matched.
+template <bool UNIQUE, bool OUTER>
 __global__ __launch_bounds__(kBlock) void k_join_probe(ColRef key, int64_t n, int64_t n_tiles, HashTable t,
                                                        uint64_t *__restrict__ status, unsigned long long *__restrict__ ticket,
                                                        uint32_t *__restrict__ out_probe, uint32_t *__restrict__ out_build,
                                                        uint64_t cap, uint32_t *__restrict__ errp,
-                                                       uint64_t *__restrict__ total_out) {
+                                                       uint64_t *__restrict__ total_out, uint8_t *__restrict__ matched) {
     __shared__ uint32_t wave_cnt[kJR][kBlock / 64];
     __shared__ uint32_t wave_off[kJR][kBlock / 64];
     __shared__ int64_t s_tile;
@@ -64,6 +66,10 @@ __global__ __launch_bounds__(kBlock) void k_join_probe(ColRef key, int64_t n, in
                 });
                 cnt[r] = c;
                 first[r] = f;
+            }
+            if (OUTER && cnt[r] == 0 && row0 + (int64_t)r * kBlock < n) {
+                cnt[r] = 1;
+                first[r] = kNullRow;
             }
         }
         uint32_t excl[kJR];
@@ -106,17 +112,19 @@ __global__ __launch_bounds__(kBlock) void k_join_probe(ColRef key, int64_t n, in
             if (!cnt[r]) continue;
             const uint32_t prow = (uint32_t)(row0 + (int64_t)r * kBlock);
             uint64_t pos = prefix + wave_off[r][wave] + excl[r];
-            if (UNIQUE) {
+            if (UNIQUE || (OUTER && first[r] == kNullRow)) {
                 if (pos < cap) {
                     out_probe[pos] = prow;
                     out_build[pos] = first[r];
                 }
+                if (OUTER && matched && first[r] != kNullRow) matched[first[r]] = 1;
             } else {
                 table_probe(t, kv[r], [&](uint32_t p) {
                     if (pos < cap) {
                         out_probe[pos] = prow;
                         out_build[pos] = p;
                     }
+                    if (OUTER && matched) matched[p] = 1;
                     ++pos;
                 });
             }
@@ -126,10 +134,13 @@ __global__ __launch_bounds__(kBlock) void k_join_probe(ColRef key, int64_t n, in
 }
 
 // total matches (duplicate build keys: sizes the output before the probe pass)
+template <bool OUTER>
 __global__ void k_join_count(ColRef key, int64_t n, HashTable t, unsigned long long *total) {
     uint64_t c = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        if (col_valid(key, i)) c += (uint64_t)table_probe(t, load_i64(key, i), [](uint32_t) {});
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t m = col_valid(key, i) ? (uint64_t)table_probe(t, load_i64(key, i), [](uint32_t) {}) : 0;
+        c += (OUTER && m == 0) ? 1 : m;
+    }
     c = wave_sum_u64(c);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(total, (unsigned long long)c);
 }
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(kBlock) void k_join_mat(MatIn in, int64_t n_tiles, 
 }
 
 int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt, DevBuf *probe_idx,
-                 DevBuf *build_idx, int64_t *out_rows) {
+                 DevBuf *build_idx, int64_t *out_rows, bool outer, uint8_t *matched, int64_t reserve) {
     const int64_t n = probe_key.length;
     const ColRef kr = make_colref(probe_key);
     uint64_t cap = (uint64_t)n;
@@ -292,14 +303,20 @@ int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt
         QEH_TRY(scratch_zeroed(ctx, 64, &scr));
         {
             KernelTimer kt(ctx, "join_count");
-            hipLaunchKernelGGL(k_join_count, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, kr, n, bt.t,
-                               (unsigned long long *)scr);
+            if (outer)
+                hipLaunchKernelGGL(k_join_count<true>, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, kr,
+                                   n, bt.t, (unsigned long long *)scr);
+            else
+                hipLaunchKernelGGL(k_join_count<false>, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                                   kr, n, bt.t, (unsigned long long *)scr);
         }
         QEH_HIP(hipGetLastError());
         QEH_TRY(read_small(ctx, &cap, scr, 8));
     }
-    QEH_TRY(probe_idx->alloc(ctx, std::max<uint64_t>(cap, 1) * 4));
-    QEH_TRY(build_idx->alloc(ctx, std::max<uint64_t>(cap, 1) * 4));
+    if (cap + (uint64_t)reserve >= (uint64_t)kNullRow)
+        return fail(QEH_E_UNSUPPORTED, "join output beyond 2^32 - 1 rows");
+    QEH_TRY(probe_idx->alloc(ctx, std::max<uint64_t>(cap + reserve, 1) * 4));
+    QEH_TRY(build_idx->alloc(ctx, std::max<uint64_t>(cap + reserve, 1) * 4));
     const int64_t n_tiles = (n + kJTile - 1) / kJTile;
     uint64_t total = 0;
     if (n_tiles > 0) {
@@ -312,12 +329,17 @@ int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt
         const int grid = grid_for(ctx, n, kJTile, 4);
         {
             KernelTimer kt(ctx, "join_probe");
-            if (bt.t.unique)
-                hipLaunchKernelGGL(k_join_probe<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, n_tiles, bt.t, status,
-                                   ticket, probe_idx->as<uint32_t>(), build_idx->as<uint32_t>(), cap, err, tot);
-            else
-                hipLaunchKernelGGL(k_join_probe<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, n_tiles, bt.t, status,
-                                   ticket, probe_idx->as<uint32_t>(), build_idx->as<uint32_t>(), cap, err, tot);
+#define QEH_JP(U, O)                                                                                             \
+    hipLaunchKernelGGL((k_join_probe<U, O>), dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, n_tiles, bt.t, status, \
+                       ticket, probe_idx->as<uint32_t>(), build_idx->as<uint32_t>(), cap, err, tot, matched)
+            if (bt.t.unique) {
+                if (outer) QEH_JP(true, true);
+                else QEH_JP(true, false);
+            } else {
+                if (outer) QEH_JP(false, true);
+                else QEH_JP(false, false);
+            }
+#undef QEH_JP
         }
         QEH_HIP(hipGetLastError());
         uint64_t hdr[3];
@@ -328,6 +350,52 @@ int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt
     }
     *out_rows = (int64_t)total;
     return QEH_OK;
+}
+
+// ---- FULL join: build rows no probe row matched, appended in build-row order ------------
+constexpr int kUmRows = kBlock * 8;
+
+__global__ void k_unmatched_count(const uint8_t *__restrict__ matched, int64_t n, uint32_t *__restrict__ counts) {
+    const int64_t base = (int64_t)blockIdx.x * kUmRows;
+    uint32_t c = 0;
+    for (int r = threadIdx.x; r < kUmRows; r += kBlock) c += (base + r < n && !matched[base + r]) ? 1u : 0u;
+    c = (uint32_t)wave_sum_u64(c);
+    __shared__ uint32_t part[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// one block per kUmRows rows; rows leave in order (ballot ranks per 256-row step)
+__global__ void k_unmatched_emit(const uint8_t *__restrict__ matched, int64_t n, const uint64_t *__restrict__ base_of,
+                                 uint64_t out0, uint32_t *__restrict__ out_probe, uint32_t *__restrict__ out_build) {
+    __shared__ uint32_t wcnt[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kUmRows;
+    uint64_t pos = out0 + base_of[blockIdx.x];
+    for (int step = 0; step < kUmRows; step += kBlock) {
+        const int64_t row = base + step + threadIdx.x;
+        const bool um = row < n && !matched[row];
+        const uint64_t b = __ballot(um);
+        if (lane == 0) wcnt[wave] = (uint32_t)popc64(b);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            before += w < wave ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (um) {
+            const uint64_t o = pos + before + mbcnt(b);
+            out_probe[o] = kNullRow;
+            out_build[o] = (uint32_t)row;
+        }
+        pos += total;
+        __syncthreads();
+    }
 }
 
 static bool mat_col_ok(const qeh_column &c) {
@@ -463,7 +531,7 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
     }
     DevBuf pidx, bidx;
     int64_t m = 0;
-    QEH_TRY(join_indices(ctx, *probe_key, bt, &pidx, &bidx, &m));
+    QEH_TRY(join_indices(ctx, *probe_key, bt, &pidx, &bidx, &m, false, nullptr, 0));
     int made_p = 0, made_b = 0;
     int s = QEH_OK;
     for (int i = 0; i < n_probe_cols && s == QEH_OK; ++i) {
@@ -483,6 +551,88 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
     if (s != QEH_OK) {
         for (int i = 0; i < made_p; ++i) qeh_column_release(ctx, &out_probe[i]);
         for (int i = 0; i < made_b; ++i) qeh_column_release(ctx, &out_build[i]);
+        return s;
+    }
+    *out_rows = m;
+    return QEH_OK;
+}
+
+// LEFT / RIGHT / FULL equi-join (include/qeh.h).  The preserved side probes (LEFT,
+// FULL: left; RIGHT: right) a table built over the other side; unmatched probe rows emit
+// (row, kNullRow), and FULL appends the build rows no probe row matched as (kNullRow, row).  The
+// filler side's columns come out NULL through the null-aware gather.
+extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column *left_key, const qeh_column *left_cols,
+                                   int n_left_cols, const qeh_column *right_key, const qeh_column *right_cols,
+                                   int n_right_cols, qeh_column *out_left, qeh_column *out_right, int64_t *out_rows) {
+    if (!ctx || !left_key || !right_key || !out_rows || (n_left_cols > 0 && (!left_cols || !out_left)) ||
+        (n_right_cols > 0 && (!right_cols || !out_right)))
+        return fail(QEH_E_INVALID, "qeh_hash_join_outer: bad argument");
+    *out_rows = 0;
+    if (join_type == 0)
+        return qeh_hash_join_inner(ctx, left_key, left_cols, n_left_cols, right_key, right_cols, n_right_cols, out_left,
+                                   out_right, out_rows);
+    if (join_type < 1 || join_type > 3) return fail(QEH_E_INVALID, "outer join type must be LEFT (1), RIGHT (2) or FULL (3)");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*left_key, "left key"));
+    QEH_TRY(check_column(*right_key, "right key"));
+    for (const qeh_column *k : {left_key, right_key})
+        if (k->dtype != QEH_DT_INT64 && k->dtype != QEH_DT_INT32)
+            return fail(QEH_E_UNSUPPORTED, "hash join keys must be Int32/Int64 on the device");
+    for (int i = 0; i < n_left_cols; ++i)
+        if (left_cols[i].length != left_key->length) return fail(QEH_E_INVALID, "left columns have different lengths");
+    for (int i = 0; i < n_right_cols; ++i)
+        if (right_cols[i].length != right_key->length) return fail(QEH_E_INVALID, "right columns have different lengths");
+    const bool right_outer = join_type == 2, full = join_type == 3;
+    const qeh_column &pk = right_outer ? *right_key : *left_key;
+    const qeh_column &bk = right_outer ? *left_key : *right_key;
+    if (pk.length >= (int64_t)kNullRow || bk.length >= (int64_t)kNullRow)
+        return fail(QEH_E_UNSUPPORTED, "join inputs beyond 2^32 - 1 rows");
+    BuiltTable bt;
+    QEH_TRY(build_join_table(ctx, bk, nullptr, (uint64_t)std::max<int64_t>(bk.length - 1, 0), &bt));
+    DevBuf matched, pidx, bidx;
+    if (full) {
+        QEH_TRY(matched.alloc(ctx, (size_t)std::max<int64_t>(bk.length, 1)));
+        QEH_HIP(hipMemsetAsync(matched.p, 0, (size_t)std::max<int64_t>(bk.length, 1), ctx->stream));
+    }
+    int64_t m = 0;
+    QEH_TRY(join_indices(ctx, pk, bt, &pidx, &bidx, &m, true, full ? matched.as<uint8_t>() : nullptr,
+                         full ? bk.length : 0));
+    if (full && bk.length > 0) {
+        const int64_t nb = (bk.length + kUmRows - 1) / kUmRows;
+        DevBuf counts, bases;
+        QEH_TRY(counts.alloc(ctx, (size_t)nb * 4));
+        QEH_TRY(bases.alloc(ctx, (size_t)nb * 8));
+        hipLaunchKernelGGL(k_unmatched_count, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, matched.as<uint8_t>(),
+                           bk.length, counts.as<uint32_t>());
+        uint64_t extra = 0;
+        QEH_TRY(exclusive_scan_u32(ctx, counts.as<uint32_t>(), bases.as<uint64_t>(), nb, &extra));
+        hipLaunchKernelGGL(k_unmatched_emit, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, matched.as<uint8_t>(),
+                           bk.length, bases.as<uint64_t>(), (uint64_t)m, pidx.as<uint32_t>(), bidx.as<uint32_t>());
+        QEH_HIP(hipGetLastError());
+        m += (int64_t)extra;
+    }
+    // probe side: NULL only for FULL's appended rows; build side: NULL for unmatched probe rows
+    const uint32_t *lidx = right_outer ? bidx.as<uint32_t>() : pidx.as<uint32_t>();
+    const uint32_t *ridx = right_outer ? pidx.as<uint32_t>() : bidx.as<uint32_t>();
+    const bool lnull = right_outer || full, rnull = !right_outer || full;
+    int made_l = 0, made_r = 0, s = QEH_OK;
+    for (int i = 0; i < n_left_cols && s == QEH_OK; ++i) {
+        KernelTimer kt(ctx, "join_gather");
+        s = gather_column(ctx, left_cols[i], lidx, m, &out_left[i], lnull);
+        if (s == QEH_OK) ++made_l;
+    }
+    for (int i = 0; i < n_right_cols && s == QEH_OK; ++i) {
+        KernelTimer kt(ctx, "join_gather");
+        s = gather_column(ctx, right_cols[i], ridx, m, &out_right[i], rnull);
+        if (s == QEH_OK) ++made_r;
+    }
+    if (s == QEH_OK) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("outer join: ") + hipGetErrorString(e));
+    }
+    if (s != QEH_OK) {
+        for (int i = 0; i < made_l; ++i) qeh_column_release(ctx, &out_left[i]);
+        for (int i = 0; i < made_r; ++i) qeh_column_release(ctx, &out_right[i]);
         return s;
     }
     *out_rows = m;

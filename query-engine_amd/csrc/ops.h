@@ -71,8 +71,11 @@ int group_slots_of_rows(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_
 int assign_group_ids(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *table,
                      DevBuf *gid_of_row);
 
-// Gather rows `idx[0..m)` of a column into a new owned column.
-int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out);
+// Gather rows `idx[0..m)` of a column into a new owned column.  With `nullable_idx`, an index of
+// kNullRow yields NULL (outer-join filler rows) and the output always carries a validity bitmap.
+constexpr uint32_t kNullRow = 0xFFFFFFFFu;
+int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out,
+                  bool nullable_idx = false);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);

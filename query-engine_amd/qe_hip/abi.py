@@ -79,6 +79,7 @@ SIGNATURES = {
     "qeh_filter_aggregate": (I, [P, COLP, I, EXPRP, C.POINTER(C.c_int32), I, AGGP, I, I64, COLP, COLP,
                                  C.POINTER(I64)]),
     "qeh_hash_join_inner": (I, [P, COLP, COLP, I, COLP, COLP, I, COLP, COLP, C.POINTER(I64)]),
+    "qeh_hash_join_outer": (I, [P, I, COLP, COLP, I, COLP, COLP, I, COLP, COLP, C.POINTER(I64)]),
     "qeh_join_filter_aggregate": (I, [P, COLP, I, I, EXPRP, COLP, COLP, I, AGGP, I, COLP, COLP,
                                       C.POINTER(I64)]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),

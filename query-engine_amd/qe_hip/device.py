@@ -312,6 +312,18 @@ class Context:
         return ([self._wrap(op[i]) for i in range(len(probe_cols))],
                 [self._wrap(ob[i]) for i in range(len(build_cols))], rows.value)
 
+    def hash_join_outer(self, join_type: int, left_key: DeviceColumn, left_cols: Sequence[DeviceColumn],
+                        right_key: DeviceColumn, right_cols: Sequence[DeviceColumn]):
+        """qeh_hash_join_outer: join_type 1 LEFT, 2 RIGHT, 3 FULL (0 INNER)."""
+        cl, cr = self._cols(left_cols), self._cols(right_cols)
+        ol = (abi.QehColumn * max(len(left_cols), 1))()
+        orr = (abi.QehColumn * max(len(right_cols), 1))()
+        rows = C.c_int64()
+        abi.check(self.lib.qeh_hash_join_outer(self.h, int(join_type), C.byref(left_key.c), cl, len(left_cols),
+                                               C.byref(right_key.c), cr, len(right_cols), ol, orr, C.byref(rows)))
+        return ([self._wrap(ol[i]) for i in range(len(left_cols))],
+                [self._wrap(orr[i]) for i in range(len(right_cols))], rows.value)
+
     def join_filter_aggregate(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                               predicate: Optional[PhysicalExpr], build_key: DeviceColumn,
                               build_group_keys: Sequence[DeviceColumn], aggs: Sequence[Tuple[int, int]]):

@@ -143,6 +143,15 @@ def hash_join_inner(probe_key: HostCol, probe_cols, build_key: HostCol, build_co
     return ([_take(op[i]) for i in range(len(probe_cols))], [_take(ob[i]) for i in range(len(build_cols))], rows.value)
 
 
+def hash_join_outer(join_type: int, left_key: HostCol, left_cols, right_key: HostCol, right_cols):
+    ol = (QoCol * max(len(left_cols), 1))()
+    orr = (QoCol * max(len(right_cols), 1))()
+    rows = C.c_int64()
+    _check(lib().qo_hash_join_outer(int(join_type), C.byref(left_key.c), _arr(left_cols), len(left_cols),
+                                    C.byref(right_key.c), _arr(right_cols), len(right_cols), ol, orr, C.byref(rows)))
+    return ([_take(ol[i]) for i in range(len(left_cols))], [_take(orr[i]) for i in range(len(right_cols))], rows.value)
+
+
 def join_filter_aggregate(probe_cols, probe_key_idx, pred, build_key: HostCol, build_group_keys, aggs):
     ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
     ok = (QoCol * max(len(build_group_keys), 1))()

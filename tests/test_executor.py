@@ -312,3 +312,43 @@ def test_fused_filter_projection_limit(qx, monkeypatch, shape):
         assert names == ["t.i", "t.s", "t.b", "t.v"]
         assert [x[0] for x in rows] == np.asarray(t.column(4))[keep].tolist()
         assert [x[1] for x in rows] == [t.column(1)[int(i)].as_py() for i in keep]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["Left", "Right", "Full"])
+def test_outer_join_plans(qx, jt):
+    """HashJoin{join_type: Left/Right/Full} through QueryExecutor (Utf8 payload included): rows ==
+    the oracle's outer join; the NULL-filled side keeps its types; an empty side -> no batches
+    (executor.rs:350-352)."""
+    r = np.random.default_rng(3)
+    a = pa.table({"a.id": pa.array(r.integers(0, 400, 3000), pa.int64(), mask=r.random(3000) < 0.05),
+                  "a.s": pa.array([f"a{i}" for i in range(3000)])})
+    b = pa.table({"b.id": pa.array(r.permutation(600)[:500], pa.int64()),
+                  "b.x": pa.array(r.random(500)),
+                  "b.t": pa.array([f"b{i}" if i % 5 else None for i in range(500)])})
+    code = getattr(JoinType, jt)
+    plan = HashJoin(Scan(source(a, 2)), Scan(source(b)), code, binop(Column("a.id", 0), BinaryOp.Equal, Column("b.id", 2)))
+    out = qx.execute(plan)
+    assert out[0].schema.names == ["a.id", "a.s", "b.id", "b.x", "b.t"]
+    got = pa.Table.from_batches(out)
+    got_rows = sorted(zip(*[c.to_pylist() for c in got.columns]), key=lambda t: tuple((x is None, x) for x in t))
+    aid = ob.HostCol(*as_cols(a.to_batches())[0])
+    bc = as_cols(b.to_batches())
+    li, ri, n = ob.hash_join_outer({"Left": 1, "Right": 2, "Full": 3}[jt], aid,
+                                   [aid, ob.HostCol(np.arange(3000, dtype=np.int64))],
+                                   ob.HostCol(*bc[0]), [ob.HostCol(*bc[0]), ob.HostCol(*bc[1]),
+                                                        ob.HostCol(np.arange(500, dtype=np.int64))])
+    assert got.num_rows == n
+    s_of_a, t_of_b = a.column(1).to_pylist(), b.column(2).to_pylist()
+    want = []
+    for i in range(n):
+        ai = li[1][0][i] if li[1][1][i] else None
+        bi = ri[2][0][i] if ri[2][1][i] else None
+        want.append((int(li[0][0][i]) if li[0][1][i] else None, None if ai is None else s_of_a[ai],
+                     int(ri[0][0][i]) if ri[0][1][i] else None, float(ri[1][0][i]) if ri[1][1][i] else None,
+                     None if bi is None else t_of_b[bi]))
+    want.sort(key=lambda t: tuple((x is None, x) for x in t))
+    assert got_rows == want
+    empty = MemoryDataSource(b.schema, [])
+    assert qx.execute(HashJoin(Scan(source(a)), Scan(empty), code,
+                               binop(Column("a.id", 0), BinaryOp.Equal, Column("b.id", 2)))) == []

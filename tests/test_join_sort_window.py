@@ -308,3 +308,73 @@ def test_join_fused_with_array_offsets(ctx):
     wp, wb, wrows = ob.hash_join_inner(ob.HostCol(pk), [ob.HostCol(pv)], ob.HostCol(bk), [ob.HostCol(ba)])
     assert rows == wrows
     assert rows_of([c.to_numpy() for c in op + obd]) == rows_of(wp + wb)
+
+
+# ---- LEFT / RIGHT / FULL ---------------------------------------------
+JT = {"left": 1, "right": 2, "full": 3}
+
+
+def outer_both(ctx, jt, lk, lcols, rk, rcols):
+    dl = [ctx.upload(*c) for c in lcols]
+    dr = [ctx.upload(*c) for c in rcols]
+    ol, orr, rows = ctx.hash_join_outer(JT[jt], ctx.upload(*lk), dl, ctx.upload(*rk), dr)
+    got = [c.to_numpy() for c in ol] + [c.to_numpy() for c in orr]
+    wl, wr, wrows = ob.hash_join_outer(JT[jt], ob.HostCol(*lk), [ob.HostCol(*c) for c in lcols], ob.HostCol(*rk),
+                                       [ob.HostCol(*c) for c in rcols])
+    assert rows == wrows
+    return got, wl + wr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "right", "full"])
+def test_outer_join_arrow_goldens(ctx, jt):
+    """Device == Arrow's hash join on the committed fixtures (tests/golden/join_*.npz)."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(gold, "join.npz"), allow_pickle=False)
+    w = np.load(os.path.join(gold, f"join_{jt}.npz"), allow_pickle=False)
+
+    def c(zz, name):
+        return zz[name], zz[name + "__valid"]
+    lk, lv, rk, ra = c(z, "left_lk"), c(z, "left_lv"), c(z, "right_rk"), c(z, "right_ra")
+    dl = [ctx.upload(*lk), ctx.upload(*lv)]
+    dr = [ctx.upload(*rk), ctx.upload(*ra)]
+    ol, orr, rows = ctx.hash_join_outer(JT[jt], ctx.upload(*lk), dl, ctx.upload(*rk), dr)
+    got = [x.to_numpy() for x in ol + orr]
+    want = [c(w, "out_" + n) for n in ("lk", "lv", "rk", "ra")]
+    assert rows == len(want[0][0])
+    assert sorted_rows(got) == sorted_rows(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "right", "full"])
+@pytest.mark.parametrize("shape", ["unique", "dups_nulls_int32", "empty_left", "empty_right", "disjoint", "large"])
+def test_outer_join_vs_oracle(ctx, jt, shape):
+    r = np.random.default_rng(len(shape) * 7 + JT[jt])
+    if shape == "unique":
+        rk = (r.permutation(5000) * 2).astype(np.int64)
+        lk = r.integers(0, 10_000, 20_000).astype(np.int64)
+        lkv = rkv = None
+    elif shape == "dups_nulls_int32":
+        rk = r.integers(0, 300, 2000).astype(np.int32)
+        lk = r.integers(0, 400, 30_000).astype(np.int64)
+        lkv, rkv = r.random(len(lk)) > 0.05, r.random(len(rk)) > 0.1
+    elif shape == "empty_left":
+        lk, rk = np.zeros(0, np.int64), r.integers(0, 50, 100).astype(np.int64)
+        lkv = rkv = None
+    elif shape == "empty_right":
+        lk, rk = r.integers(0, 50, 100).astype(np.int64), np.zeros(0, np.int64)
+        lkv = rkv = None
+    elif shape == "disjoint":
+        lk, rk = np.arange(0, 1000, dtype=np.int64), np.arange(5000, 5500, dtype=np.int64)
+        lkv = rkv = None
+    else:
+        rk = r.permutation(400_000).astype(np.int64)[:300_000]
+        lk = r.integers(0, 500_000, 2_000_000).astype(np.int64)
+        lkv = rkv = None
+    if lkv is None:
+        lkv = np.ones(len(lk), bool) if shape == "dups_nulls_int32" else None
+    lcols = [(lk, lkv), (r.random(len(lk)), r.random(len(lk)) > 0.2), (r.random(len(lk)) > 0.5, None)]
+    rcols = [(rk, rkv), (r.integers(-9, 9, len(rk)).astype(np.int32), None)]
+    got, want = outer_both(ctx, jt, (lk, lkv), lcols, (rk, rkv), rcols)
+    assert sorted_rows(got) == sorted_rows(want)

@@ -97,6 +97,42 @@ def test_oracle_inner_join_matches_arrow():
     assert sorted_rows(p + b) == sorted_rows(want)
 
 
+@pytest.mark.parametrize("jt", ["left", "right", "full"])
+def test_oracle_outer_join_matches_arrow(jt):
+    """LEFT / RIGHT / FULL joins: the oracle's rows == Arrow's hash join (tests/golden/join_*.npz),
+    NULL-filled sides included, as multisets."""
+    z = load("join")
+    (lk, lkv), (lv, lvv) = cols_of(z, "left_", ["lk", "lv"])
+    (rk, rkv), (ra, rav) = cols_of(z, "right_", ["rk", "ra"])
+    code = {"left": 1, "right": 2, "full": 3}[jt]
+    lo, ro, rows = ob.hash_join_outer(code, ob.HostCol(lk, lkv), [ob.HostCol(lk, lkv), ob.HostCol(lv, lvv)],
+                                      ob.HostCol(rk, rkv), [ob.HostCol(rk, rkv), ob.HostCol(ra, rav)])
+    want = cols_of(load("join_" + jt), "out_", ["lk", "lv", "rk", "ra"])
+    assert rows == len(want[0][0])
+    assert sorted_rows(lo + ro) == sorted_rows(want)
+
+
+def test_oracle_outer_join_known_answer():
+    """Hand-derived: left keys [1, 2, 2, NULL, 5], right keys [2, 3, NULL, 2, 1]."""
+    lk = ob.HostCol(np.array([1, 2, 2, 0, 5], np.int64), np.array([1, 1, 1, 0, 1], bool))
+    rk = ob.HostCol(np.array([2, 3, 0, 2, 1], np.int64), np.array([1, 1, 0, 1, 1], bool))
+    li = ob.HostCol(np.arange(5, dtype=np.int64))
+    ri = ob.HostCol(np.arange(10, 15, dtype=np.int64))
+    pairs = {}
+    for code in (1, 2, 3):
+        lo, ro, n = ob.hash_join_outer(code, lk, [li], rk, [ri])
+        pairs[code] = sorted_rows(lo + ro)
+    inner = [(0, 14), (1, 10), (1, 13), (2, 10), (2, 13)]
+    assert pairs[1] == sorted_rows_of(inner + [(3, None), (4, None)])
+    assert pairs[2] == sorted_rows_of(inner + [(None, 11), (None, 12)])
+    assert pairs[3] == sorted_rows_of(inner + [(3, None), (4, None), (None, 11), (None, 12)])
+
+
+def sorted_rows_of(rows):
+    from helpers import _key
+    return sorted(rows, key=_key)
+
+
 def test_oracle_sort_matches_arrow():
     z = load("sort")
     inputs = golden_inputs(z)

@@ -11,7 +11,7 @@ which implements the same Arrow semantics for these kernels:
   compute::{sum,min,max}, count    -> pc.sum/min/max/count (non-overflowing data: pyarrow
                                       widens Int32 sums, arrow-rs wraps them)
 Intended-semantics operators are pinned the same way:
-  GROUP BY -> Table.group_by().aggregate();  INNER JOIN -> Table.join("inner");
+  GROUP BY -> Table.group_by().aggregate();  INNER / LEFT / RIGHT / FULL JOIN -> Table.join(...);
   Sort     -> pc.sort_indices(null_placement="at_start") (stable);
   ROW_NUMBER -> numpy lexsort (no Arrow kernel; documented as numpy-pinned).
 Config 1's known answer comes from the reference's own data/employees.csv
@@ -128,6 +128,17 @@ def main():
     put_table("out_", j, d)
     save("join", **d)
     manifest["fixtures"]["join"] = {"rows": j.num_rows}
+
+    # ---- LEFT / RIGHT / FULL outer joins on the same inputs (Arrow's hash join,
+    # NULL keys never match, both key columns kept)
+    for jt in ("left outer", "right outer", "full outer"):
+        j = left.join(right, keys="lk", right_keys="rk", join_type=jt, use_threads=False, coalesce_keys=False)
+        j = j.select(["lk", "lv", "rk", "ra"])
+        d = {}
+        put_table("out_", j, d)
+        name = "join_" + jt.split()[0]
+        save(name, **d)
+        manifest["fixtures"][name] = {"rows": j.num_rows, "inputs": "join.npz left_/right_"}
 
     # ---- stable multi-key sort, nulls first
     keys = [("k", "ascending"), ("v", "descending"), ("x", "ascending")]
