@@ -253,6 +253,24 @@ int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_
 int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending,
                      qeh_column *out_perm);
 
+/* qeh_sort_indices with arrow SortOptions.nulls_first per key (nulls_first NULL: all first),
+ * as Merge::sorted passes it (crates/query-distributed/src/operators.rs:97-104,163-172). */
+int qeh_sort_indices_nulls(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending,
+                           const int8_t *nulls_first, qeh_column *out_perm);
+
+/* arrow concat of one column's parts (same dtype), as concat_batches does per column
+ * (operators.rs:206-216, executor.rs:176-181). */
+int qeh_concat(qeh_ctx *ctx, const qeh_column *parts, int n_parts, qeh_column *out);
+
+/* Merge::execute with MergeStrategy::SortedMerge (operators.rs:143-193): concatenate the
+ * partitions' columns (`parts` = [n_parts][n_cols], partition-major) and sort the rows by
+ * columns key_idx[0..n_keys) (ascending / nulls_first per key); n_keys == 0 returns the
+ * concatenation, as the reference does when no sort column name resolves.  Outputs n_cols
+ * owned columns. */
+int qeh_merge_sorted(qeh_ctx *ctx, const qeh_column *parts, int n_parts, int n_cols, const int32_t *key_idx,
+                     const int8_t *ascending, const int8_t *nulls_first, int n_keys, qeh_column *out,
+                     int64_t *out_rows);
+
 /* Gather rows `indices` (UINT32 or INT64 device column) of `col`. */
 int qeh_take(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out);
 

@@ -836,14 +836,19 @@ typedef struct {
     const arr *k;
     int nk;
     const int8_t *asc;
+    const int8_t *nulls_first; /* NULL: all first */
 } sort_ctx;
 
-/* arrow SortOptions default nulls_first = true (distributed/operators.rs:97-104) */
+/* arrow SortOptions default nulls_first = true (distributed/operators.rs:97-104); Merge::sorted
+ * passes it per column (operators.rs:163-172) */
 static int row_cmp(const sort_ctx *c, int64_t a, int64_t b) {
     for (int j = 0; j < c->nk; ++j) {
         const arr *k = &c->k[j];
         int va = k->v[a], vb = k->v[b];
-        if (va != vb) return va ? 1 : -1; /* NULL first */
+        if (va != vb) {
+            const int nf = c->nulls_first ? c->nulls_first[j] != 0 : 1;
+            return (va ? 1 : -1) * (nf ? 1 : -1);
+        }
         if (!va) continue;
         int64_t x = key_bits(k, a), y = key_bits(k, b);
         int r = (x > y) - (x < y);
@@ -865,7 +870,14 @@ static void msort(const sort_ctx *c, int64_t *idx, int64_t *tmp, int64_t n) {
     memcpy(idx, tmp, (size_t)n * sizeof(int64_t));
 }
 
+static int sorted_perm_nulls(const qo_col *keys, int n_keys, const int8_t *asc, const int8_t *nulls_first, int64_t n,
+                             int64_t **perm_out, arr **ka_out);
 static int sorted_perm(const qo_col *keys, int n_keys, const int8_t *asc, int64_t n, int64_t **perm_out, arr **ka_out) {
+    return sorted_perm_nulls(keys, n_keys, asc, NULL, n, perm_out, ka_out);
+}
+
+static int sorted_perm_nulls(const qo_col *keys, int n_keys, const int8_t *asc, const int8_t *nulls_first, int64_t n,
+                             int64_t **perm_out, arr **ka_out) {
     arr *ka = calloc((size_t)n_keys + 1, sizeof(arr));
     int s = QEH_OK;
     for (int j = 0; j < n_keys && s == QEH_OK; ++j) s = col_to_arr(&keys[j], &ka[j]);
@@ -873,7 +885,7 @@ static int sorted_perm(const qo_col *keys, int n_keys, const int8_t *asc, int64_
     int64_t *tmp = malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
     for (int64_t r = 0; r < n; ++r) perm[r] = r;
     if (s == QEH_OK) {
-        sort_ctx c = {ka, n_keys, asc};
+        sort_ctx c = {ka, n_keys, asc, nulls_first};
         msort(&c, perm, tmp, n);
     }
     free(tmp);
@@ -886,6 +898,20 @@ int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int
     int64_t *perm;
     arr *ka;
     int s = sorted_perm(keys, n_keys, ascending, n_rows, &perm, &ka);
+    if (s == QEH_OK)
+        for (int64_t r = 0; r < n_rows; ++r) out_perm[r] = (uint32_t)perm[r];
+    for (int j = 0; j < n_keys; ++j) arr_free(&ka[j]);
+    free(ka);
+    free(perm);
+    return s;
+}
+
+/* Merge::sorted's lexsort (operators.rs:163-186) with per-key nulls_first, stable. */
+int qo_sort_indices_nulls(const qo_col *keys, int n_keys, const int8_t *ascending, const int8_t *nulls_first,
+                          int64_t n_rows, uint32_t *out_perm) {
+    int64_t *perm;
+    arr *ka;
+    int s = sorted_perm_nulls(keys, n_keys, ascending, nulls_first, n_rows, &perm, &ka);
     if (s == QEH_OK)
         for (int64_t r = 0; r < n_rows; ++r) out_perm[r] = (uint32_t)perm[r];
     for (int j = 0; j < n_keys; ++j) arr_free(&ka[j]);

@@ -62,6 +62,8 @@ int qo_join_filter_aggregate(const qo_col *probe_cols, int n_probe, int probe_ke
                              int n_aggs, qo_col *out_keys, qo_col *out_aggs, int64_t *out_groups);
 int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int64_t n_rows,
                     uint32_t *out_perm);
+int qo_sort_indices_nulls(const qo_col *keys, int n_keys, const int8_t *ascending, const int8_t *nulls_first,
+                          int64_t n_rows, uint32_t *out_perm);
 int qo_row_number(const qo_col *part, int n_part, const qo_col *order, int n_order,
                   const int8_t *ascending, int64_t n_rows, int64_t *out_rn);
 

@@ -94,15 +94,17 @@ __global__ void k_stats_init(KeyStats *s) {
 
 // encoded key of row perm[i] (or i) -> keys[i]; perm_out[i] = perm[i] (or i)
 // mode 0: value encoding (NULL -> 0, values biased by `bias`); mode 1: null flag only
+// `null_code`: the key of a NULL row (0 = NULLs first; above every value code = NULLs last)
 template <typename KeyT>
 __global__ void k_encode(ColRef c, const uint32_t *__restrict__ perm, int64_t n, int64_t mn, int64_t mx, int asc,
-                         uint64_t bias, int mode, KeyT *__restrict__ keys, uint32_t *__restrict__ perm_out) {
+                         uint64_t bias, int mode, uint64_t null_code, KeyT *__restrict__ keys,
+                         uint32_t *__restrict__ perm_out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = perm ? perm[i] : i;
-        uint64_t k = 0;
+        uint64_t k = null_code;
         if (col_valid(c, r)) {
             if (mode == 1) {
-                k = 1;
+                k = null_code ? 0 : 1;
             } else {
                 const int64_t x = ordered_key(c, r);
                 k = asc ? (uint64_t)x - (uint64_t)mn + bias : (uint64_t)mx - (uint64_t)x + bias;
@@ -325,7 +327,8 @@ static int bit_length(uint64_t x) {
 
 // Encode key column `c` through the current permutation (or identity) and
 // sort by it.  Returns the key range bits used.
-static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, bool asc, bool first) {
+static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, bool asc, bool first,
+                          bool nulls_last = false) {
     const ColRef c = make_colref(col);
     const int64_t n = rs.n;
     DevBuf st;
@@ -342,15 +345,19 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
     QEH_TRY(read_small(ctx, &ks, st.p, sizeof ks));
     const bool nullable = col.validity != nullptr && col.null_count != 0;
     int bits = 1;  // all NULL (or empty)
-    uint64_t bias = nullable ? 1 : 0;
+    // NULLs first: NULL -> 0, values -> 1 .. span+1; NULLs last: values -> 0 .. span, NULL -> span+1
+    uint64_t bias = (nullable && !nulls_last) ? 1 : 0;
+    uint64_t null_code = 0;
     bool null_pass = false;
     if (ks.mn <= ks.mx) {
-        const uint64_t span = (uint64_t)ks.mx - (uint64_t)ks.mn;  // values map to bias .. span+bias
+        const uint64_t span = (uint64_t)ks.mx - (uint64_t)ks.mn;
         if (nullable && span == UINT64_MAX) {  // 2^64 values + NULL: 65 bits -> separate null-flag pass
             bias = 0;
             null_pass = true;
         }
-        bits = bit_length(span + bias);
+        const uint64_t top = span + ((nullable && !null_pass) ? 1 : 0);
+        if (nullable && nulls_last && !null_pass) null_code = top;
+        bits = bit_length(top);
         if (bits == 0) bits = 1;
     }
     for (int pass = 0; pass < (null_pass ? 2 : 1); ++pass) {
@@ -361,12 +368,14 @@ static int sort_by_column(qeh_ctx *ctx, RadixState &rs, const qeh_column &col, b
         {
             KernelTimer kt(ctx, "sort_encode");
             const int g = grid_for(ctx, n, kBlock * 8, 8);
+            // the null-flag pass (pass 1) orders NULL vs value: code 1 for NULL when NULLs go last
+            const uint64_t nc = pass == 0 ? null_code : (nulls_last ? 1 : 0);
             if (rs.key32)
                 hipLaunchKernelGGL(k_encode<uint32_t>, dim3(g), dim3(kBlock), 0, ctx->stream, c, pm, n, ks.mn, ks.mx,
-                                   asc ? 1 : 0, bias, pass, rs.k[o].as<uint32_t>(), rs.v[o].as<uint32_t>());
+                                   asc ? 1 : 0, bias, pass, nc, rs.k[o].as<uint32_t>(), rs.v[o].as<uint32_t>());
             else
                 hipLaunchKernelGGL(k_encode<uint64_t>, dim3(g), dim3(kBlock), 0, ctx->stream, c, pm, n, ks.mn, ks.mx,
-                                   asc ? 1 : 0, bias, pass, rs.k[o].as<uint64_t>(), rs.v[o].as<uint32_t>());
+                                   asc ? 1 : 0, bias, pass, nc, rs.k[o].as<uint64_t>(), rs.v[o].as<uint32_t>());
         }
         QEH_HIP(hipGetLastError());
         rs.cur = o;
@@ -503,7 +512,7 @@ static int sort_perm_pair(qeh_ctx *ctx, const qeh_column &ca, const qeh_column &
 
 // Stable lexicographic permutation by keys (last key sorted first).
 static int sort_perm(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending, int64_t n,
-                     RadixState &rs) {
+                     RadixState &rs, const int8_t *nulls_first = nullptr) {
     rs.n = n;
     for (int b = 0; b < 2; ++b) {
         QEH_TRY(rs.k[b].alloc(ctx, (size_t)std::max<int64_t>(n, 1) * 8));
@@ -520,7 +529,8 @@ static int sort_perm(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int
         rs.part_shift = -1;
     }
     for (int j = n_keys - 1; j >= 0; --j)
-        QEH_TRY(sort_by_column(ctx, rs, keys[j], ascending ? ascending[j] != 0 : true, j == n_keys - 1));
+        QEH_TRY(sort_by_column(ctx, rs, keys[j], ascending ? ascending[j] != 0 : true, j == n_keys - 1,
+                               nulls_first ? nulls_first[j] == 0 : false));
     return QEH_OK;
 }
 
@@ -726,6 +736,20 @@ extern "C" int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys
     QEH_TRY(check_sort_keys(keys, n_keys, &n));
     RadixState rs;
     QEH_TRY(sort_perm(ctx, keys, n_keys, ascending, n, rs));
+    QEH_TRY(alloc_column(ctx, QEH_DT_UINT32, n, false, out_perm));
+    if (n > 0) QEH_HIP(hipMemcpyAsync(out_perm->values, rs.v[rs.cur].p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+extern "C" int qeh_sort_indices_nulls(qeh_ctx *ctx, const qeh_column *keys, int n_keys, const int8_t *ascending,
+                                      const int8_t *nulls_first, qeh_column *out_perm) {
+    if (!ctx || !keys || !out_perm) return fail(QEH_E_INVALID, "qeh_sort_indices_nulls: bad argument");
+    DeviceGuard dg(ctx->device);
+    int64_t n;
+    QEH_TRY(check_sort_keys(keys, n_keys, &n));
+    RadixState rs;
+    QEH_TRY(sort_perm(ctx, keys, n_keys, ascending, n, rs, nulls_first));
     QEH_TRY(alloc_column(ctx, QEH_DT_UINT32, n, false, out_perm));
     if (n > 0) QEH_HIP(hipMemcpyAsync(out_perm->values, rs.v[rs.cur].p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     QEH_HIP(hipStreamSynchronize(ctx->stream));

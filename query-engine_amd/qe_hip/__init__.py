@@ -11,3 +11,4 @@ from .expr import (AggregateExpr, AggregateFunction, BinaryExpr, BinaryOp, Colum
 from .plan import (DataSource, Filter, HashAggregate, HashJoin, IndexScan, JoinType, Limit,  # noqa: F401
                    MemoryDataSource, Projection, QueryExecutor, Scan, Sort, SubqueryScan, Window, WindowExpr,
                    WindowFunctionType)
+from .merge import Merge, MergeStrategy, SortColumn  # noqa: F401,E402

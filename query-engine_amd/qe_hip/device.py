@@ -351,6 +351,35 @@ class Context:
         abi.check(self.lib.qeh_sort_indices(self.h, ck, len(keys), asc, C.byref(out)))
         return self._wrap(out)
 
+    def sort_indices_nulls(self, keys: Sequence[DeviceColumn], ascending: Sequence[bool],
+                           nulls_first: Sequence[bool]) -> DeviceColumn:
+        ck = self._cols(keys)
+        asc = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in ascending])
+        nf = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in nulls_first])
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_sort_indices_nulls(self.h, ck, len(keys), asc, nf, C.byref(out)))
+        return self._wrap(out)
+
+    def concat(self, parts: Sequence[DeviceColumn]) -> DeviceColumn:
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_concat(self.h, self._cols(parts), len(parts), C.byref(out)))
+        return self._wrap(out)
+
+    def merge_sorted(self, parts: Sequence[Sequence[DeviceColumn]], key_idx: Sequence[int],
+                     ascending: Sequence[bool], nulls_first: Sequence[bool]) -> Tuple[List[DeviceColumn], int]:
+        """qeh_merge_sorted: parts = one column list per partition (same schema)."""
+        ncols = len(parts[0]) if parts else 0
+        flat = [c for p in parts for c in p]
+        cp = self._cols(flat)
+        ki = (C.c_int32 * max(len(key_idx), 1))(*key_idx)
+        asc = (C.c_int8 * max(len(key_idx), 1))(*[1 if a else 0 for a in ascending])
+        nf = (C.c_int8 * max(len(key_idx), 1))(*[1 if a else 0 for a in nulls_first])
+        out = (abi.QehColumn * max(ncols, 1))()
+        rows = C.c_int64()
+        abi.check(self.lib.qeh_merge_sorted(self.h, cp, len(parts), ncols, ki, asc, nf, len(key_idx), out,
+                                            C.byref(rows)))
+        return [self._wrap(out[i]) for i in range(ncols)], rows.value
+
     def take(self, col: DeviceColumn, indices: DeviceColumn) -> DeviceColumn:
         out = abi.QehColumn()
         abi.check(self.lib.qeh_take(self.h, C.byref(col.c), C.byref(indices.c), C.byref(out)))

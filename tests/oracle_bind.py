@@ -170,6 +170,15 @@ def join_filter_aggregate(probe_cols, probe_key_idx, pred, build_key: HostCol, b
             g.value)
 
 
+def sort_indices_nulls(keys: Sequence[HostCol], ascending: Sequence[bool], nulls_first: Sequence[bool]) -> np.ndarray:
+    n = len(keys[0].values) if keys else 0
+    out = np.empty(max(n, 1), np.uint32)
+    asc = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in ascending])
+    nf = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in nulls_first])
+    _check(lib().qo_sort_indices_nulls(_arr(keys), len(keys), asc, nf, C.c_int64(n), out.ctypes.data_as(C.c_void_p)))
+    return out[:n]
+
+
 def sort_indices(keys: Sequence[HostCol], ascending: Sequence[bool]) -> np.ndarray:
     n = len(keys[0].values) if keys else 0
     out = np.empty(max(n, 1), np.uint32)

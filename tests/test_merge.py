@@ -1,0 +1,108 @@
+"""Merge (crates/query-distributed/src/operators.rs:75-224) on the device: qeh_concat,
+qeh_sort_indices_nulls and qeh_merge_sorted vs the oracle, the Arrow golden
+(tests/golden/merge_sorted.npz) and the reference's own known answer
+(operators.rs:343-374: merging [3, 1] and [4, 2] sorted gives [1, 2, 3, 4])."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from qe_hip import Merge, MergeStrategy, SortColumn
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def host(c):
+    v, m = c.to_numpy()
+    return v, (np.ones(len(v), bool) if m is None else m)
+
+
+@pytest.mark.gpu
+def test_merge_sorted_reference_known_answer(ctx):
+    m = Merge.sorted(ctx, ["value"], [SortColumn("value", True, True)])
+    out = m.execute([[[ctx.upload(np.array([3, 1], np.int64))]], [[ctx.upload(np.array([4, 2], np.int64))]]])
+    assert len(out) == 1
+    assert out[0][0].to_numpy()[0].tolist() == [1, 2, 3, 4]
+
+
+@pytest.mark.gpu
+def test_merge_sorted_matches_arrow_golden(ctx):
+    z = np.load(os.path.join(GOLD, "merge_sorted.npz"), allow_pickle=False)
+    names = ["x", "i", "v", "f", "b", "k"]
+    cols = [(z["in_" + n], z["in_" + n + "__valid"]) for n in names]
+    bounds = np.concatenate([[0], np.cumsum(z["part_rows"])])
+    parts = [[[ctx.upload(v[a:b], m[a:b]) for v, m in cols]] for a, b in zip(bounds[:-1], bounds[1:])]
+    m = Merge.sorted(ctx, names, [SortColumn("k", False, False), SortColumn("x", True, True),
+                                  SortColumn("v", True, False), SortColumn("missing", True, True)])
+    out = m.execute(parts)
+    perm = z["perm"]
+    for j, (v, mk) in enumerate(cols):
+        gv, gm = host(out[0][j])
+        assert np.array_equal(gm, mk[perm]), names[j]
+        assert np.array_equal(gv[gm], v[perm][mk[perm]]), names[j]
+
+
+@pytest.mark.gpu
+def test_merge_strategies_concat_union_and_unresolved_names(ctx):
+    a = [ctx.upload(np.array([5, 6], np.int64))]
+    b = [ctx.upload(np.array([1], np.int64))]
+    for strat in (MergeStrategy.Concat(), MergeStrategy.UnionDistinct(["value"])):
+        out = Merge(ctx, ["value"], strat).execute([[a], [b, a]])
+        assert [c[0].to_numpy()[0].tolist() for c in out] == [[5, 6], [1], [5, 6]]
+    out = Merge.sorted(ctx, ["value"], [SortColumn("nope")]).execute([[a], [b]])
+    assert out[0][0].to_numpy()[0].tolist() == [5, 6, 1]  # no resolvable sort column: concatenation
+    assert Merge.sorted(ctx, ["value"], [SortColumn("value")]).execute([[], []]) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [[0, 5], [1, 1, 1], [31, 33, 64, 7], [1000, 0, 4097]])
+def test_concat_all_types_with_offsets(ctx, sizes):
+    r = np.random.default_rng(sum(sizes))
+    kinds = []
+    for n in sizes:
+        kinds.append([
+            (r.integers(-50, 50, n).astype(np.int64), r.random(n) > 0.2),
+            (r.random(n) > 0.5, r.random(n) > 0.3),
+            (r.random(n).astype(np.float32), None),
+            (np.array([f"s{int(x)}" * (int(x) % 4) for x in r.integers(0, 100, n)], dtype=object), r.random(n) > 0.1),
+        ])
+    for j in range(4):
+        parts = [ctx.upload(k[j][0], k[j][1], offset=(i * 3) % 5) if j != 3 else ctx.upload(k[j][0], k[j][1])
+                 for i, k in enumerate(kinds)]
+        got = ctx.concat(parts)
+        want_v = np.concatenate([k[j][0] for k in kinds]) if sum(sizes) else np.zeros(0)
+        want_m = np.concatenate([np.ones(len(k[j][0]), bool) if k[j][1] is None else k[j][1] for k in kinds])
+        gv, gm = host(got)
+        assert len(gv) == sum(sizes)
+        assert np.array_equal(gm, want_m)
+        if j == 3:
+            assert [x for x, ok in zip(gv, gm) if ok] == [x for x, ok in zip(want_v, want_m) if ok]
+        else:
+            assert np.array_equal(np.asarray(gv)[gm], np.asarray(want_v)[want_m])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["int64_nulls_last_desc", "mixed_three_keys", "full_range_nulls_last", "float_keys"])
+def test_sort_indices_nulls_vs_oracle(ctx, case):
+    r = np.random.default_rng(len(case))
+    n = 200_003
+    if case == "int64_nulls_last_desc":
+        keys = [(r.integers(-1000, 1000, n).astype(np.int64), r.random(n) > 0.1)]
+        asc, nf = [False], [False]
+    elif case == "mixed_three_keys":
+        keys = [(r.integers(0, 20, n).astype(np.int32), r.random(n) > 0.05),
+                (r.integers(0, 50, n).astype(np.int64), r.random(n) > 0.2),
+                (r.random(n), r.random(n) > 0.1)]
+        asc, nf = [True, False, True], [False, True, False]
+    elif case == "full_range_nulls_last":
+        keys = [(r.integers(-(2 ** 63), 2 ** 63 - 1, n, dtype=np.int64), r.random(n) > 0.3)]
+        keys[0][0][:2] = [-(2 ** 63), 2 ** 63 - 1]
+        keys[0][1][:2] = True
+        asc, nf = [True], [False]
+    else:
+        keys = [(np.round(r.standard_normal(n), 2), r.random(n) > 0.1), (r.integers(0, 9, n).astype(np.int64), None)]
+        asc, nf = [False, True], [False, True]
+    got = ctx.sort_indices_nulls([ctx.upload(v, m) for v, m in keys], asc, nf).to_numpy()[0]
+    want = ob.sort_indices_nulls([ob.HostCol(v, m) for v, m in keys], asc, nf)
+    assert np.array_equal(got, want)

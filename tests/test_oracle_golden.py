@@ -133,6 +133,19 @@ def sorted_rows_of(rows):
     return sorted(rows, key=_key)
 
 
+MERGE_KEYS = [("k", False, False), ("x", True, True), ("v", True, False)]  # (column, ascending, nulls_first)
+
+
+def test_oracle_merge_sorted_matches_arrow():
+    """Merge::sorted's ordering (distributed/operators.rs:143-193) with per-key nulls_first:
+    the oracle's stable lexsort == Arrow's sort_indices on tests/golden/merge_sorted.npz."""
+    z = load("merge_sorted")
+    cols = dict(zip([c for c, _, _ in MERGE_KEYS], cols_of(z, "in_", [c for c, _, _ in MERGE_KEYS])))
+    perm = ob.sort_indices_nulls([ob.HostCol(*cols[c]) for c, _, _ in MERGE_KEYS], [a for _, a, _ in MERGE_KEYS],
+                                 [nf for _, _, nf in MERGE_KEYS])
+    assert np.array_equal(perm, z["perm"])
+
+
 def test_oracle_sort_matches_arrow():
     z = load("sort")
     inputs = golden_inputs(z)

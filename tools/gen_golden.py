@@ -149,6 +149,19 @@ def main():
     save("sort", **d)
     manifest["fixtures"]["sort"] = {"keys": keys}
 
+    # ---- Merge::sorted (distributed/operators.rs:143-193): three partitions concatenated, then
+    # sorted with per-key descending / nulls_first (Arrow sort_indices is stable; the reference's
+    # lexsort_to_indices may order ties either way)
+    parts = [t.slice(0, 1000), t.slice(1000, 1500), t.slice(2500, N - 2500)]
+    cat = pa.concat_tables(parts)
+    mkeys = [("k", "descending", "at_end"), ("x", "ascending", "at_start"), ("v", "ascending", "at_end")]
+    midx = pc.sort_indices(cat, sort_keys=mkeys)
+    d = {"part_rows": np.array([p.num_rows for p in parts], np.int64)}
+    put_table("in_", cat, d)
+    d["perm"] = np.asarray(midx.to_numpy(), np.uint32)
+    save("merge_sorted", **d)
+    manifest["fixtures"]["merge_sorted"] = {"keys": mkeys, "parts": [p.num_rows for p in parts]}
+
     # ---- ROW_NUMBER() OVER (PARTITION BY k ORDER BY x) (numpy-pinned)
     kk, kv = col_arrays(t["k"].combine_chunks())
     xx, xv = col_arrays(t["x"].combine_chunks())
