@@ -228,7 +228,10 @@ int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, const qeh_col
  * row (LEFT, FULL) with NULL right columns, plus each unmatched right row (RIGHT, FULL) with NULL
  * left columns; NULL keys never match.  join_type: qeh_join_type values (qeh_plan.h) 1 LEFT,
  * 2 RIGHT, 3 FULL (0 = INNER, forwarded to qeh_hash_join_inner with the left side probing).
- * Row order: preserved side's row order, FULL's unmatched right rows last (compare as multisets). */
+ * Row order: preserved side's row order, FULL's unmatched right rows last (compare as multisets).
+ * LEFT / RIGHT over a unique Int-keyed build side whose payloads are non-null 8-byte columns
+ * return the preserved side's columns as views of the inputs (owned = 0, like arrow's column
+ * clones): keep the inputs alive while using them; every other output is owned. */
 int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column *left_key, const qeh_column *left_cols,
                         int n_left_cols, const qeh_column *right_key, const qeh_column *right_cols, int n_right_cols,
                         qeh_column *out_left, qeh_column *out_right, int64_t *out_rows);

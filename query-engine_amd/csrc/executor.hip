@@ -692,8 +692,10 @@ class Executor {
             else  // LEFT / RIGHT / FULL
                 QEH_TRY(qeh_hash_join_outer(ctx_, nd.join_type, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(),
                                             (int)rc.size(), lo.data(), ro.data(), &rows));
-            for (auto &c : lo) out->cols.push_back(own(ctx_, c));
-            for (auto &c : ro) out->cols.push_back(own(ctx_, c));
+            // a column returned as a view (owned = 0: an outer join's preserved side) keeps the
+            // input's owner alive
+            for (size_t i = 0; i < lo.size(); ++i) out->cols.push_back(lo[i].owned ? own(ctx_, lo[i]) : l.cols[i]);
+            for (size_t i = 0; i < ro.size(); ++i) out->cols.push_back(ro[i].owned ? own(ctx_, ro[i]) : r.cols[i]);
         }
         out->rows = rows;
         out->batches = rows > 0 ? 1 : 0;  // executor.rs:374-376 keeps non-empty joins only

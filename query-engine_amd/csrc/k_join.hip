@@ -352,6 +352,70 @@ int join_indices(qeh_ctx *ctx, const qeh_column &probe_key, const BuiltTable &bt
     return QEH_OK;
 }
 
+// ---- outer joins over a unique build key: one output row per probe row, in probe order ----
+// bidx[i] = build row matching probe row i, or kNullRow (no match / NULL key); FULL also flags
+// the matched build rows.  No compaction: the output position of probe row i is i.
+__global__ void k_outer_lookup(ColRef key, int64_t n, HashTable t, uint32_t *__restrict__ bidx,
+                               uint8_t *__restrict__ matched) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t p = kNullRow;
+        if (col_valid(key, i)) table_probe(t, load_i64(key, i), [&](uint32_t q) { p = q; });
+        bidx[i] = p;
+        if (matched && p != kNullRow) matched[p] = 1;
+    }
+}
+
+// Unique DIRECT build with <= 3 non-null 8-byte build columns, embedded by key offset
+// (k_embed_build): one presence-bit test (the bitmap stays L2-resident) and one record read per
+// probe row, outputs written in probe order with their validity words from one ballot per wave.
+struct OuterEmbedOut {
+    int64_t *bout[kMatMaxB];
+    uint64_t *bvalid[kMatMaxB];
+};
+
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_outer_embed(ColRef key, int64_t n, const int64_t *__restrict__ rec,
+                                                        const uint32_t *__restrict__ present, int64_t kmin, int64_t kmax,
+                                                        OuterEmbedOut out) {
+    constexpr int U = 4;  // 64-row groups per wave in flight
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t g0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * U; g0 * 64 < n; g0 += nw * U) {
+        uint64_t off[U];
+        bool hit[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+            const bool valid = i < n && col_valid(key, i);
+            const int64_t k = valid ? load_i64(key, i) : 0;
+            const bool in = valid && k >= kmin && k <= kmax;
+            off[u] = in ? (uint64_t)k - (uint64_t)kmin : 0;
+            hit[u] = in && ((present[off[u] >> 5] >> (off[u] & 31)) & 1u);
+        }
+        int64_t v[U][NB];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) v[u][b] = hit[u] ? rec[off[u] * NB + b] : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+            const uint64_t mask = __ballot(hit[u]);
+            if (i < n)
+#pragma unroll
+                for (int b = 0; b < NB; ++b) out.bout[b][i] = v[u][b];
+            if (lane == 0 && (g0 + u) * 64 < n)
+#pragma unroll
+                for (int b = 0; b < NB; ++b) out.bvalid[b][g0 + u] = mask;
+        }
+    }
+}
+
+__global__ void k_iota_then_null(uint32_t *__restrict__ out, int64_t n, int64_t m) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = i < n ? (uint32_t)i : kNullRow;
+}
+
 // ---- FULL join: build rows no probe row matched, appended in build-row order ------------
 constexpr int kUmRows = kBlock * 8;
 
@@ -595,8 +659,93 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         QEH_HIP(hipMemsetAsync(matched.p, 0, (size_t)std::max<int64_t>(bk.length, 1), ctx->stream));
     }
     int64_t m = 0;
-    QEH_TRY(join_indices(ctx, pk, bt, &pidx, &bidx, &m, true, full ? matched.as<uint8_t>() : nullptr,
-                         full ? bk.length : 0));
+    // unique build keys: every probe row yields exactly one row, at its own position
+    const bool in_place = bt.t.unique && !std::getenv("QEH_OUTER_COMPACT");
+    const qeh_column *bcols = right_outer ? left_cols : right_cols;
+    const qeh_column *pcols = right_outer ? right_cols : left_cols;
+    const int nbc = right_outer ? n_left_cols : n_right_cols, npc = right_outer ? n_right_cols : n_left_cols;
+    qeh_column *bout = right_outer ? out_left : out_right;
+    qeh_column *pout = right_outer ? out_right : out_left;
+    bool embed = in_place && !full && bt.t.kind == TK_DIRECT && nbc >= 1 && nbc <= kMatMaxB && bt.t.range <= (1ull << 31) &&
+                 !std::getenv("QEH_NO_FUSED_JOIN");
+    for (int i = 0; embed && i < nbc; ++i) embed = mat_col_ok(bcols[i]);
+    if (embed) {
+        // LEFT/RIGHT over a unique DIRECT build: build columns embedded by key offset, one fused
+        // probe writes them in probe order; the preserved side's columns are returned as views of
+        // the inputs (owned = 0, a RecordBatch column clone)
+        const uint64_t range = bt.t.range;
+        const int64_t n = pk.length, nbuild = bk.length;
+        DevBuf rec, present;
+        QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * nbc, 1) * 8));
+        QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
+        QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+        auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
+        if (nbuild > 0) {
+            KernelTimer kt(ctx, "join_build");
+            hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                               make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
+                               nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>());
+        }
+        int made = 0, s = QEH_OK;
+        OuterEmbedOut eo{};
+        for (int i = 0; i < nbc && s == QEH_OK; ++i) {
+            s = alloc_column(ctx, bcols[i].dtype, n, true, &bout[i]);
+            if (s == QEH_OK) {
+                ++made;
+                eo.bout[i] = (int64_t *)bout[i].values;
+                eo.bvalid[i] = (uint64_t *)bout[i].validity;
+            }
+        }
+        if (s == QEH_OK && n > 0) {
+            KernelTimer kt(ctx, "join_probe");
+            const int grid = grid_for(ctx, (n + 255) / 256, kBlock / 64, 8);
+            if (nbc == 1)
+                hipLaunchKernelGGL(k_outer_embed<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n,
+                                   rec.as<int64_t>(), present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
+            else if (nbc == 2)
+                hipLaunchKernelGGL(k_outer_embed<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n,
+                                   rec.as<int64_t>(), present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
+            else
+                hipLaunchKernelGGL(k_outer_embed<3>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n,
+                                   rec.as<int64_t>(), present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("outer join: ") + hipGetErrorString(e));
+        }
+        if (s == QEH_OK) {
+            hipError_t e = hipStreamSynchronize(ctx->stream);
+            if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("outer join: ") + hipGetErrorString(e));
+        }
+        if (s != QEH_OK) {
+            for (int i = 0; i < made; ++i) qeh_column_release(ctx, &bout[i]);
+            return s;
+        }
+        for (int i = 0; i < npc; ++i) {
+            pout[i] = pcols[i];
+            pout[i].owned = 0;
+        }
+        *out_rows = n;
+        return QEH_OK;
+    }
+    if (in_place) {
+        const int64_t n = pk.length;
+        QEH_TRY(bidx.alloc(ctx, (size_t)std::max<int64_t>(n + (full ? bk.length : 0), 1) * 4));
+        if (n > 0) {
+            KernelTimer kt(ctx, "join_probe");
+            hipLaunchKernelGGL(k_outer_lookup, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                               make_colref(pk), n, bt.t, bidx.as<uint32_t>(), full ? matched.as<uint8_t>() : nullptr);
+        }
+        QEH_HIP(hipGetLastError());
+        m = n;
+    } else {
+        QEH_TRY(join_indices(ctx, pk, bt, &pidx, &bidx, &m, true, full ? matched.as<uint8_t>() : nullptr,
+                             full ? bk.length : 0));
+    }
+    if (full && in_place) {  // probe side of FULL: rows 0..n-1 in place, the appended rows NULL
+        QEH_TRY(pidx.alloc(ctx, (size_t)std::max<int64_t>(m + bk.length, 1) * 4));
+        if (m + bk.length > 0)
+            hipLaunchKernelGGL(k_iota_then_null, dim3(grid_for(ctx, m + bk.length, kBlock * 4, 8)), dim3(kBlock), 0,
+                               ctx->stream, pidx.as<uint32_t>(), m, m + bk.length);
+    }
     if (full && bk.length > 0) {
         const int64_t nb = (bk.length + kUmRows - 1) / kUmRows;
         DevBuf counts, bases;
@@ -611,19 +760,26 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         QEH_HIP(hipGetLastError());
         m += (int64_t)extra;
     }
+    const bool probe_copy = in_place && !full;  // probe columns leave unchanged: one normalising copy each
     // probe side: NULL only for FULL's appended rows; build side: NULL for unmatched probe rows
     const uint32_t *lidx = right_outer ? bidx.as<uint32_t>() : pidx.as<uint32_t>();
     const uint32_t *ridx = right_outer ? pidx.as<uint32_t>() : bidx.as<uint32_t>();
     const bool lnull = right_outer || full, rnull = !right_outer || full;
     int made_l = 0, made_r = 0, s = QEH_OK;
-    for (int i = 0; i < n_left_cols && s == QEH_OK; ++i) {
+    auto out_col = [&](const qeh_column &src, const uint32_t *idx, bool nullable, bool probe_side, qeh_column *dst) {
         KernelTimer kt(ctx, "join_gather");
-        s = gather_column(ctx, left_cols[i], lidx, m, &out_left[i], lnull);
+        if (probe_side && probe_copy) {
+            const qeh_column *one = &src;
+            return concat_columns(ctx, &one, 1, dst);
+        }
+        return gather_column(ctx, src, idx, m, dst, nullable);
+    };
+    for (int i = 0; i < n_left_cols && s == QEH_OK; ++i) {
+        s = out_col(left_cols[i], lidx, lnull, !right_outer, &out_left[i]);
         if (s == QEH_OK) ++made_l;
     }
     for (int i = 0; i < n_right_cols && s == QEH_OK; ++i) {
-        KernelTimer kt(ctx, "join_gather");
-        s = gather_column(ctx, right_cols[i], ridx, m, &out_right[i], rnull);
+        s = out_col(right_cols[i], ridx, rnull, right_outer, &out_right[i]);
         if (s == QEH_OK) ++made_r;
     }
     if (s == QEH_OK) {

@@ -77,6 +77,10 @@ constexpr uint32_t kNullRow = 0xFFFFFFFFu;
 int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int64_t m, qeh_column *out,
                   bool nullable_idx = false);
 
+// Concatenate parts (same dtype) into one owned column with offset 0 (k_merge.hip); one part =
+// a normalising copy.
+int concat_columns(qeh_ctx *ctx, const qeh_column *const *parts, int n_parts, qeh_column *out);
+
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
 

@@ -321,8 +321,14 @@ class Context:
         rows = C.c_int64()
         abi.check(self.lib.qeh_hash_join_outer(self.h, int(join_type), C.byref(left_key.c), cl, len(left_cols),
                                                C.byref(right_key.c), cr, len(right_cols), ol, orr, C.byref(rows)))
-        return ([self._wrap(ol[i]) for i in range(len(left_cols))],
-                [self._wrap(orr[i]) for i in range(len(right_cols))], rows.value)
+
+        def wrap(c, src):
+            d = self._wrap(c)
+            if not c.owned:
+                d.parent = src  # a view of the input column: keep it alive
+            return d
+        return ([wrap(ol[i], left_cols[i]) for i in range(len(left_cols))],
+                [wrap(orr[i], right_cols[i]) for i in range(len(right_cols))], rows.value)
 
     def join_filter_aggregate(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                               predicate: Optional[PhysicalExpr], build_key: DeviceColumn,

@@ -352,3 +352,12 @@ def test_outer_join_plans(qx, jt):
     empty = MemoryDataSource(b.schema, [])
     assert qx.execute(HashJoin(Scan(source(a)), Scan(empty), code,
                                binop(Column("a.id", 0), BinaryOp.Equal, Column("b.id", 2)))) == []
+    # build side of non-null 8-byte columns only: LEFT / RIGHT return the preserved side as views
+    # of the scanned columns; the result must survive the inputs' release
+    b2 = b.select(["b.id", "b.x"])
+    plan2 = HashJoin(Scan(source(a, 2)), Scan(source(b2)), code,
+                     binop(Column("a.id", 0), BinaryOp.Equal, Column("b.id", 2)))
+    out2 = pa.Table.from_batches(qx.execute(plan2))
+    got2 = sorted(zip(*[c.to_pylist() for c in out2.columns]), key=lambda t: tuple((x is None, x) for x in t))
+    want2 = sorted([w[:4] for w in want], key=lambda t: tuple((x is None, x) for x in t))
+    assert got2 == want2

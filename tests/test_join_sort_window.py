@@ -378,3 +378,45 @@ def test_outer_join_vs_oracle(ctx, jt, shape):
     rcols = [(rk, rkv), (r.integers(-9, 9, len(rk)).astype(np.int32), None)]
     got, want = outer_both(ctx, jt, (lk, lkv), lcols, (rk, rkv), rcols)
     assert sorted_rows(got) == sorted_rows(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "right", "full"])
+def test_outer_join_unique_in_place_matches_compacting_path(ctx, monkeypatch, jt):
+    """Unique build keys take the in-place path (one row per probe row, probe order); the
+    compacting path (QEH_OUTER_COMPACT) and the oracle give the same rows, and LEFT keeps
+    probe order exactly."""
+    r = np.random.default_rng(11)
+    rk = (r.permutation(30_000) * 3).astype(np.int64)[:20_000]
+    lk = r.integers(0, 90_000, 70_001).astype(np.int64)
+    lkv = r.random(len(lk)) > 0.03
+    lcols = [(lk, lkv), (r.random(len(lk)), r.random(len(lk)) > 0.2)]
+    rcols = [(r.integers(-5, 5, len(rk)).astype(np.int64), r.random(len(rk)) > 0.1), (rk, None)]
+    got, want = outer_both(ctx, jt, (lk, lkv), lcols, (rk, None), rcols)
+    assert sorted_rows(got) == sorted_rows(want)
+    if jt == "left":
+        assert rows_of(got) == rows_of(want)
+    monkeypatch.setenv("QEH_OUTER_COMPACT", "1")
+    got2, _ = outer_both(ctx, jt, (lk, lkv), lcols, (rk, None), rcols)
+    assert sorted_rows(got2) == sorted_rows(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "right"])
+@pytest.mark.parametrize("nb", [1, 2, 3])
+def test_outer_join_embedded_build_path(ctx, jt, nb):
+    """LEFT/RIGHT over a unique DIRECT build with non-null 8-byte payloads: the fused embedded
+    probe (k_outer_embed) writes the build columns in probe order and returns the preserved
+    side as views; rows == oracle, in order."""
+    r = np.random.default_rng(nb * 5 + len(jt))
+    nbuild, nprobe = 50_000, 300_007
+    bk = (r.permutation(80_000)[:nbuild] - 1000).astype(np.int64)
+    pk = r.integers(-3000, 82_000, nprobe).astype(np.int64)
+    pkv = r.random(nprobe) > 0.02
+    bcols = [(bk, None), (r.random(nbuild), None), (r.integers(-9, 9, nbuild).astype(np.int64), None)][:nb]
+    pcols = [(pk, pkv), (r.random(nprobe) > 0.5, r.random(nprobe) > 0.1)]
+    if jt == "left":
+        got, want = outer_both(ctx, jt, (pk, pkv), pcols, (bk, None), bcols)
+    else:
+        got, want = outer_both(ctx, jt, (bk, None), bcols, (pk, pkv), pcols)
+    assert rows_of(got) == rows_of(want)

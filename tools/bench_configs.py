@@ -10,10 +10,12 @@
   filter  the Filter operator alone: SELECT x, k, v WHERE x > 49 (24 B in + 12 B out avg per row)
   limit   the same filter under LIMIT 1000 (capped filter, early exit)
   plan    the metric query through QueryExecutor from host Arrow batches, cold vs device-cached Scan
+  left / full   LEFT / FULL outer join 2e8 x 1e7, half the probe rows unmatched
+  merge   Merge::sorted of 8 partitions x 1.25e7 rows, ORDER BY k DESC NULLS LAST
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
-usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan] [--scale 1.0]
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge] [--scale 1.0]
 """
 import argparse
 import json
@@ -132,6 +134,70 @@ def cfg5(ctx, scale):
     line("cfg5 ROW_NUMBER 1e9", n, wall, 24.0 * n, kms, "k_rs_hist/k_rs_scatter (+encode, row numbers)", cpu, kt)
 
 
+def cfg_outer(ctx, scale, jt=1):
+    """LEFT (jt=1) / FULL (jt=3) join, 2e8 probe rows (keys uniform over twice the dim key range,
+    so half find no match) x 1e7 dim rows, materialising (f.v, d.a).  Algorithmic bytes: 16 B probe
+    read + 16 B output written per output row (+ the FULL tail)."""
+    n, nd = int(2e8 * scale), 10_000_000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 2 * nd)
+    fv = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1000)
+
+    def fn():
+        lo, ro, rows = ctx.hash_join_outer(jt, fk, [fk, fv], dk, [da])
+        for c in lo + ro:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 5, ["join_probe", "join_count", "join_gather", "join_build"])
+    m = 10_000_000
+    hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, m, 2 * nd)
+    hv = ob.generate(abi.GEN_UNIT_F64, SEED, 3, m)
+    hdk = ob.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    hda = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1000)
+    t0 = time.perf_counter()
+    ob.hash_join_outer(jt, ob.HostCol(hk), [ob.HostCol(hk), ob.HostCol(hv)], ob.HostCol(hdk), [ob.HostCol(hda)])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} probe x {nd} build, {dt:.2f} s"}
+    kms = kt["join_probe"] + kt["join_count"] + kt["join_gather"]
+    name = {1: "LEFT", 3: "FULL"}[jt]
+    # LEFT over the unique dim takes the embedded path: probe payloads leave as views, so only the
+    # key is read and the build column (+ validity) written; FULL gathers every output column
+    alg = 16.0 * n + n / 8 if jt == 1 else 16.0 * n + 24.0 * rows
+    line(f"{name} outer join 2e8 x 1e7 (50% unmatched)", n, wall, alg, kms,
+         "k_outer_lookup + copies / null-aware gathers", cpu, {"output_rows": rows, "kernel_split_ms": kt})
+
+
+def cfg_merge(ctx, scale):
+    """Merge::sorted of 8 partitions x 1.25e7 rows (k Int64 with 5 % NULLs, v Float64), ORDER BY k
+    DESC NULLS LAST.  Algorithmic bytes: read 16 B + write 16 B per row (+ validity)."""
+    parts = []
+    per = int(1.25e7 * scale)
+    for p in range(8):
+        k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED + p, 7, per, 2 ** 40)
+        kv, _ = k.to_numpy()
+        valid = np.random.default_rng(p).random(per) > 0.05
+        parts.append([ctx.upload(kv, valid), ctx.generate(abi.GEN_UNIT_F64, SEED + p, 8, per)])
+    n = 8 * per
+
+    def fn():
+        cols, rows = ctx.merge_sorted(parts, [0], [False], [False])
+        for c in cols:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 3, ["radix_pass", "sort_encode", "gather"])
+    hk = [p[0].to_numpy() for p in parts]
+    m = 4_000_000
+    hkk = np.concatenate([a for a, _ in hk])[:m]
+    hkv = np.concatenate([b for _, b in hk])[:m]
+    t0 = time.perf_counter()
+    ob.sort_indices_nulls([ob.HostCol(hkk, hkv)], [False], [False])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows sort, {dt:.2f} s"}
+    line("Merge::sorted 8 x 1.25e7 rows, ORDER BY k DESC NULLS LAST", n, wall, 32.0 * n, sum(kt.values()),
+         "k_rs_hist/k_rs_scatter + gathers", cpu, kt)
+
+
 def cfg_filter(ctx, scale):
     n = int(5e8 * scale)
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
@@ -215,7 +281,8 @@ def main():
     ctx.set_stream(s.cuda_stream)
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
-         "plan": cfg_plan}[name](ctx, args.scale)
+         "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
+         "merge": cfg_merge}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
