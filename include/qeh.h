@@ -310,6 +310,15 @@ int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int ascending, cons
  * fixed-width columns; `indices` UINT32 of the same length. */
 int qeh_scatter(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, qeh_column *out);
 
+/* Result encoding: PostgreSQL DataRow messages in text format, one per row,
+ * as crates/query-pgwire/src/result.rs:56-176 builds them through pgwire 0.28.0 (NULL -> length
+ * -1, booleans "t"/"f", integers in decimal, floats as Rust's Display: shortest round-trip
+ * digits without exponent, Utf8 bytes).  `out` is an owned Utf8 column whose string i is row
+ * i's complete message ('D', Int32 length, Int16 field count, fields), ready to be sent.
+ * Types: BOOL, INT32, INT64, UINT32 (as Int64), FLOAT32, FLOAT64, UTF8; <= 32 columns;
+ * QEH_E_UNSUPPORTED when the messages exceed 2 GiB (encode the batch in slices). */
+int qeh_encode_pg_datarows(qeh_ctx *ctx, const qeh_column *cols, int n_cols, qeh_column *out);
+
 /* Validity bitmap <-> one byte per row (1 = valid), for moving nullable
  * columns through byte-addressed collectives (RCCL all-to-all splits are
  * row counts, not bit offsets).  Buffers are device pointers. */

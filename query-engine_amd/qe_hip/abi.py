@@ -87,6 +87,7 @@ SIGNATURES = {
     "qeh_concat": (I, [P, COLP, I, COLP]),
     "qeh_merge_sorted": (I, [P, COLP, I, I, C.POINTER(C.c_int32), C.POINTER(C.c_int8), C.POINTER(C.c_int8), I, COLP,
                              C.POINTER(I64)]),
+    "qeh_encode_pg_datarows": (I, [P, COLP, I, COLP]),
     "qeh_take": (I, [P, COLP, COLP, COLP]),
     "qeh_row_number": (I, [P, COLP, I, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_hash_partition": (I, [P, COLP, I, C.POINTER(I64), COLP]),

@@ -66,6 +66,19 @@ class DeviceColumn:
         except Exception:
             pass
 
+    def to_bytes(self) -> List[bytes]:
+        """Utf8 column -> its strings as raw bytes (no decoding; e.g. encoded DataRow messages)."""
+        assert self.c.dtype == abi.DT_UTF8
+        n, off = self.c.length, self.c.offset
+        offs = np.empty(n + 1, np.int32)
+        self.ctx.d2h(offs, self.c.offsets + 4 * off, 4 * (n + 1))
+        nb = int(offs[-1]) if n else 0
+        data = np.empty(max(nb, 1), np.uint8)
+        if nb:
+            self.ctx.d2h(data, self.c.values, nb)
+        raw = data.tobytes()
+        return [raw[offs[i]:offs[i + 1]] for i in range(n)]
+
     def to_numpy(self) -> Tuple[np.ndarray, Optional[np.ndarray]]:
         """(values, validity-or-None) copied to the host."""
         n, off = self.c.length, self.c.offset
@@ -385,6 +398,12 @@ class Context:
         abi.check(self.lib.qeh_merge_sorted(self.h, cp, len(parts), ncols, ki, asc, nf, len(key_idx), out,
                                             C.byref(rows)))
         return [self._wrap(out[i]) for i in range(ncols)], rows.value
+
+    def encode_pg_datarows(self, cols: Sequence[DeviceColumn]) -> DeviceColumn:
+        """qeh_encode_pg_datarows: Utf8 column, string i = row i's DataRow message."""
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_encode_pg_datarows(self.h, self._cols(cols), len(cols), C.byref(out)))
+        return self._wrap(out)
 
     def take(self, col: DeviceColumn, indices: DeviceColumn) -> DeviceColumn:
         out = abi.QehColumn()

@@ -12,10 +12,11 @@
   plan    the metric query through QueryExecutor from host Arrow batches, cold vs device-cached Scan
   left / full   LEFT / FULL outer join 2e8 x 1e7, half the probe rows unmatched
   merge   Merge::sorted of 8 partitions x 1.25e7 rows, ORDER BY k DESC NULLS LAST
+  encode  pgwire DataRow text encoding of 1e7 result rows
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
-usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge] [--scale 1.0]
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge,encode] [--scale 1.0]
 """
 import argparse
 import json
@@ -198,6 +199,35 @@ def cfg_merge(ctx, scale):
          "k_rs_hist/k_rs_scatter + gathers", cpu, kt)
 
 
+def cfg_encode(ctx, scale):
+    """§8 f4: pgwire DataRow text encoding of a 1e7-row result (k Int64, sum Float64, count Int64),
+    the shape of the metric query's output rows at scale.  Bytes: 24 B read per row + the encoded
+    messages written."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pg_text
+    n = int(1e7 * scale)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 1 << 40)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    c = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 4, n, 1000000)
+
+    def fn():
+        out = ctx.encode_pg_datarows([k, v, c])
+        nb = out.c.values_bytes
+        out.release()
+        return nb
+    wall, kt, nbytes = timed(ctx, fn, 5, ["encode_len", "encode_write"])
+    m = 100_000
+    hk, hv, hc = (x.to_numpy()[0][:m] for x in (k, v, c))
+    t0 = time.perf_counter()
+    pg_text.encode_rows([("int64", hk.tolist()), ("float64", hv.tolist()), ("int64", hc.tolist())])
+    dt = time.perf_counter() - t0
+    cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+           "sample": f"{m} rows, oracle/pg_text.py (pure Python), {dt:.2f} s"}
+    line("pgwire DataRow text encoding 1e7 x (Int64, Float64, Int64)", n, wall, 24.0 * n + nbytes,
+         sum(kt.values()), "k_pg_row_len + k_pg_row_write (Schubfach shortest floats)", cpu,
+         {"encoded_bytes": nbytes, "kernel_split_ms": kt})
+
+
 def cfg_filter(ctx, scale):
     n = int(5e8 * scale)
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
@@ -282,7 +312,7 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
