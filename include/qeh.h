@@ -319,6 +319,23 @@ int qeh_scatter(qeh_ctx *ctx, const qeh_column *col, const qeh_column *indices, 
  * QEH_E_UNSUPPORTED when the messages exceed 2 GiB (encode the batch in slices). */
 int qeh_encode_pg_datarows(qeh_ctx *ctx, const qeh_column *cols, int n_cols, qeh_column *out);
 
+/* Arrow IPC stream of one batch (schema message, record batch message, end-of-stream), as
+ * SerializedBatch::from_batch writes it with arrow-rs's StreamWriter
+ * (crates/query-distributed/src/network.rs:56-72): fields nullable, named `names[i]`, body
+ * buffers 64-byte aligned.  Device columns are normalised to offset 0 on the device and copied
+ * into a host buffer the library allocates; free it with qeh_host_free. */
+int qeh_encode_arrow_ipc(qeh_ctx *ctx, const qeh_column *cols, const char *const *names, int n_cols,
+                         uint8_t **out_bytes, int64_t *out_size);
+void qeh_host_free(void *p);
+
+/* The first record batch of an Arrow IPC stream, as SerializedBatch::to_batch reads it
+ * (network.rs:75-90), uploaded into owned device columns out_cols[0 .. *out_n_cols); the field
+ * names come back NUL-separated in *out_names (free with qeh_host_free; may be NULL).  Int32 /
+ * Int64 / UInt32 / Float32 / Float64 / Utf8 / Bool fields; dictionaries, nesting and body
+ * compression -> QEH_E_UNSUPPORTED; malformed or truncated input -> QEH_E_INVALID. */
+int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t size, qeh_column *out_cols, int max_cols,
+                         int *out_n_cols, char **out_names, int64_t *out_rows);
+
 /* Validity bitmap <-> one byte per row (1 = valid), for moving nullable
  * columns through byte-addressed collectives (RCCL all-to-all splits are
  * row counts, not bit offsets).  Buffers are device pointers. */

@@ -88,6 +88,9 @@ SIGNATURES = {
     "qeh_merge_sorted": (I, [P, COLP, I, I, C.POINTER(C.c_int32), C.POINTER(C.c_int8), C.POINTER(C.c_int8), I, COLP,
                              C.POINTER(I64)]),
     "qeh_encode_pg_datarows": (I, [P, COLP, I, COLP]),
+    "qeh_encode_arrow_ipc": (I, [P, COLP, C.POINTER(C.c_char_p), I, C.POINTER(C.c_void_p), C.POINTER(I64)]),
+    "qeh_host_free": (None, [C.c_void_p]),
+    "qeh_decode_arrow_ipc": (I, [P, C.c_void_p, I64, COLP, I, C.POINTER(I), C.POINTER(C.c_void_p), C.POINTER(I64)]),
     "qeh_take": (I, [P, COLP, COLP, COLP]),
     "qeh_row_number": (I, [P, COLP, I, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_hash_partition": (I, [P, COLP, I, C.POINTER(I64), COLP]),

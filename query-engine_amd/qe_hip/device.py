@@ -405,6 +405,37 @@ class Context:
         abi.check(self.lib.qeh_encode_pg_datarows(self.h, self._cols(cols), len(cols), C.byref(out)))
         return self._wrap(out)
 
+    def encode_arrow_ipc(self, cols: Sequence[DeviceColumn], names: Sequence[str]) -> np.ndarray:
+        """qeh_encode_arrow_ipc: the batch as an Arrow IPC stream.  Returns a uint8 numpy view of
+        the library's pinned host buffer (no copy; freed when the array is collected).
+        `bytes(result)` or `pyarrow.py_buffer(result)` for consumers that need those."""
+        import weakref
+        nm = (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        p, size = C.c_void_p(), C.c_int64()
+        abi.check(self.lib.qeh_encode_arrow_ipc(self.h, self._cols(cols), nm, len(cols), C.byref(p), C.byref(size)))
+        holder = (C.c_uint8 * max(size.value, 1)).from_address(p.value)
+        weakref.finalize(holder, self.lib.qeh_host_free, C.c_void_p(p.value))
+        return np.frombuffer(holder, np.uint8, count=size.value)
+
+    def decode_arrow_ipc(self, data: bytes, max_cols: int = 256) -> Tuple[List[str], List[DeviceColumn], int]:
+        """qeh_decode_arrow_ipc: (names, device columns, rows) of the stream's first batch."""
+        out = (abi.QehColumn * max_cols)()
+        nc, rows, names = C.c_int(), C.c_int64(), C.c_void_p()
+        buf = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data, np.uint8)
+        ptr = C.c_void_p(buf.ctypes.data if len(buf) else None)
+        abi.check(self.lib.qeh_decode_arrow_ipc(self.h, ptr, len(buf), out, max_cols, C.byref(nc), C.byref(names),
+                                                C.byref(rows)))
+        parts: List[str] = []
+        try:
+            p = names.value
+            for _ in range(nc.value):  # NUL-separated, one per column
+                s = C.string_at(p)
+                parts.append(s.decode())
+                p += len(s) + 1
+        finally:
+            self.lib.qeh_host_free(names)
+        return parts, [self._wrap(out[i]) for i in range(nc.value)], rows.value
+
     def take(self, col: DeviceColumn, indices: DeviceColumn) -> DeviceColumn:
         out = abi.QehColumn()
         abi.check(self.lib.qeh_take(self.h, C.byref(col.c), C.byref(indices.c), C.byref(out)))

@@ -226,6 +226,24 @@ def cfg_encode(ctx, scale):
     line("pgwire DataRow text encoding 1e7 x (Int64, Float64, Int64)", n, wall, 24.0 * n + nbytes,
          sum(kt.values()), "k_pg_row_len + k_pg_row_write (Schubfach shortest floats)", cpu,
          {"encoded_bytes": nbytes, "kernel_split_ms": kt})
+    # Arrow IPC stream of the same batch (network.rs:56-72): device normalisation + copy to host
+    reps = 5
+    data = ctx.encode_arrow_ipc([k, v, c], ["k", "sum", "count"])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        data = ctx.encode_arrow_ipc([k, v, c], ["k", "sum", "count"])
+    wall = (time.perf_counter() - t0) / reps
+    names, cols, _ = ctx.decode_arrow_ipc(data)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        names, cols, _ = ctx.decode_arrow_ipc(data)
+        for x in cols:
+            x.release()
+    wall_d = (time.perf_counter() - t0) / reps
+    line("Arrow IPC stream encode 1e7 x (Int64, Float64, Int64), device -> host bytes", n, wall, None, None,
+         "device normalise + D2H copies", None,
+         {"stream_bytes": len(data), "host_GBs": len(data) / wall / 1e9, "decode_ms": wall_d * 1e3,
+          "decode_host_GBs": len(data) / wall_d / 1e9})
 
 
 def cfg_filter(ctx, scale):
