@@ -305,6 +305,20 @@ int qeh_hash_partition(qeh_ctx *ctx, const qeh_column *key, int n_parts, int64_t
 int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int ascending, const int64_t *splitters,
                         int n_splitters, int64_t *counts, qeh_column *out_perm);
 
+/* Partitioner::partition_by_hash over several key columns (distributed/partition.rs:151-212):
+ * a partition-major permutation, stable within a partition, with per-partition row counts.
+ * Int32 / Int64 / Utf8 keys; NULL cells are skipped when hashing, as compute_row_hash does
+ * (partition.rs:292-316).  The hash differs from the reference's SipHash: which partition a
+ * key lands in is not observable in query results; rows with equal keys always share one. */
+int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, int64_t *counts,
+                       qeh_column *out_perm);
+
+/* Partitioner::partition_by_range (partition.rs:259-341): row -> the first i with
+ * value < boundaries[i], else n_boundaries; NULL -> 0; a non-Int64 key puts every row in
+ * partition 0, as the reference does.  Same output as qeh_partition_hash. */
+int qeh_partition_range(qeh_ctx *ctx, const qeh_column *key, const int64_t *boundaries, int n_boundaries,
+                        int64_t *counts, qeh_column *out_perm);
+
 /* out[indices[i]] = col[i] (inverse of qeh_take for a permutation): returns
  * per-row results to their original positions after an exchange.  Non-null
  * fixed-width columns; `indices` UINT32 of the same length. */

@@ -698,6 +698,59 @@ __global__ void k_range_ids(ColRef key, int64_t n, const int64_t *__restrict__ s
     }
 }
 
+// PartitionStrategy::Hash over several key columns (partition.rs:151-212, compute_row_hash
+// :292-316): NULL cells contribute nothing to the row hash, as the reference skips them; Int32 /
+// Int64 values and Utf8 bytes are mixed into one 64-bit hash (the hash function is not
+// observable in results).
+struct HashKeys {
+    ColRef c[kMaxCols];
+    const int32_t *offs[kMaxCols];
+    const uint8_t *data[kMaxCols];
+    int32_t n;
+};
+
+__global__ void k_hash_ids_multi(HashKeys keys, int64_t n, uint32_t parts, uint64_t *__restrict__ ids,
+                                 uint32_t *__restrict__ idx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (int j = 0; j < keys.n; ++j) {
+            const ColRef &c = keys.c[j];
+            if (!col_valid(c, i)) continue;
+            uint64_t v;
+            if (c.dtype == QEH_DT_UTF8) {
+                v = 0xcbf29ce484222325ull;  // FNV-1a over the bytes
+                for (int32_t b = keys.offs[j][i]; b < keys.offs[j][i + 1]; ++b) v = (v ^ keys.data[j][b]) * 0x100000001b3ull;
+            } else {
+                v = (uint64_t)load_i64(c, i);
+            }
+            h = hash64(h ^ (hash64(v) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+        }
+        ids[i] = h % parts;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+// PartitionStrategy::Range (find_range_partition, partition.rs:320-341): the first boundary the
+// value is below, or len(boundaries); NULL -> 0; only Int64 keys are ranged (every other column
+// type lands in partition 0, as in the reference)
+__global__ void k_range_ids_first_below(ColRef key, int64_t n, const int64_t *__restrict__ b, int nb, int is_i64,
+                                        uint64_t *__restrict__ ids, uint32_t *__restrict__ idx) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t p = 0;
+        if (is_i64 && col_valid(key, i)) {
+            const int64_t v = ((const int64_t *)key.values)[i];
+            p = (uint32_t)nb;
+            for (int j = 0; j < nb; ++j)
+                if (v < b[j]) {
+                    p = (uint32_t)j;
+                    break;
+                }
+        }
+        ids[i] = p;
+        idx[i] = (uint32_t)i;
+    }
+}
+
 template <typename T>
 __global__ void k_scatter(const T *__restrict__ src, const uint32_t *__restrict__ idx, int64_t m, T *__restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
@@ -929,6 +982,58 @@ extern "C" int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int asce
         [&](uint64_t *ids, uint32_t *idx) {
             hipLaunchKernelGGL(k_range_ids, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, kc, n,
                                sp.as<int64_t>(), n_splitters, ascending ? 1 : 0, ids, idx);
+        },
+        "range_partition", counts, out_perm);
+}
+
+extern "C" int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, int64_t *counts,
+                                  qeh_column *out_perm) {
+    if (!ctx || !keys || n_keys < 1 || n_keys > kMaxCols || !counts || !out_perm || n_parts < 1 || n_parts > kRadix)
+        return fail(QEH_E_INVALID, "qeh_partition_hash: bad argument (1..12 keys, 1..256 partitions)");
+    DeviceGuard dg(ctx->device);
+    HashKeys hk{};
+    hk.n = n_keys;
+    const int64_t n = keys[0].length;
+    for (int j = 0; j < n_keys; ++j) {
+        QEH_TRY(check_column(keys[j], "partition key"));
+        if (keys[j].length != n) return fail(QEH_E_INVALID, "partition keys have different lengths");
+        if (keys[j].dtype != QEH_DT_INT64 && keys[j].dtype != QEH_DT_INT32 && keys[j].dtype != QEH_DT_UTF8)
+            return fail(QEH_E_UNSUPPORTED, "hash partition keys must be Int32 / Int64 / Utf8 (compute_row_hash)");
+        hk.c[j] = make_colref(keys[j]);
+        if (keys[j].dtype == QEH_DT_UTF8) {
+            hk.offs[j] = keys[j].offsets + keys[j].offset;
+            hk.data[j] = (const uint8_t *)keys[j].values;
+        }
+    }
+    return partition_perm(
+        ctx, n, n_parts,
+        [&](uint64_t *ids, uint32_t *idx) {
+            hipLaunchKernelGGL(k_hash_ids_multi, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
+                               (uint32_t)n_parts, ids, idx);
+        },
+        "hash_partition", counts, out_perm);
+}
+
+extern "C" int qeh_partition_range(qeh_ctx *ctx, const qeh_column *key, const int64_t *boundaries, int n_boundaries,
+                                   int64_t *counts, qeh_column *out_perm) {
+    if (!ctx || !key || !counts || !out_perm || n_boundaries < 0 || n_boundaries >= kRadix ||
+        (n_boundaries > 0 && !boundaries))
+        return fail(QEH_E_INVALID, "qeh_partition_range: bad argument (0..255 boundaries)");
+    DeviceGuard dg(ctx->device);
+    QEH_TRY(check_column(*key, "partition key"));
+    const int64_t n = key->length;
+    DevBuf bd;
+    QEH_TRY(bd.alloc(ctx, (size_t)std::max(n_boundaries, 1) * 8));
+    if (n_boundaries > 0)
+        QEH_HIP(hipMemcpyAsync(bd.p, boundaries, (size_t)n_boundaries * 8, hipMemcpyHostToDevice, ctx->stream));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    const ColRef kc = make_colref(*key);
+    const int is_i64 = key->dtype == QEH_DT_INT64;
+    return partition_perm(
+        ctx, n, n_boundaries + 1,
+        [&](uint64_t *ids, uint32_t *idx) {
+            hipLaunchKernelGGL(k_range_ids_first_below, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                               kc, n, bd.as<int64_t>(), n_boundaries, is_i64, ids, idx);
         },
         "range_partition", counts, out_perm);
 }

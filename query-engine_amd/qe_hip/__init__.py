@@ -12,3 +12,4 @@ from .plan import (DataSource, Filter, HashAggregate, HashJoin, IndexScan, JoinT
                    MemoryDataSource, Projection, QueryExecutor, Scan, Sort, SubqueryScan, Window, WindowExpr,
                    WindowFunctionType)
 from .merge import Merge, MergeStrategy, SortColumn  # noqa: F401,E402
+from .partition import DeviceBatch, Exchange, Partition, Partitioner, PartitionStrategy  # noqa: F401,E402

@@ -308,10 +308,12 @@ class Context:
     def copy_d2d(self, dst: int, src: int, nbytes: int) -> None:
         abi.check(self.lib.qeh_memcpy_d2d(self.h, dst, src, nbytes))
 
-    def wrap_device(self, dtype: int, ptr: int, n: int, validity: int = 0) -> DeviceColumn:
-        """View caller-owned device memory (e.g. a torch tensor) as a column."""
+    def wrap_device(self, dtype: int, ptr: int, n: int, validity: int = 0, offsets: int = 0,
+                    values_bytes: int = 0) -> DeviceColumn:
+        """View caller-owned device memory (e.g. a torch tensor) as a column (Utf8: `offsets` is
+        the int32[n + 1] offsets buffer and `ptr` the bytes)."""
         c = abi.QehColumn(dtype=dtype, owned=0, length=n, offset=0, null_count=0 if not validity else -1,
-                          values=ptr, validity=validity or None)
+                          values=ptr, validity=validity or None, offsets=offsets or None, values_bytes=values_bytes)
         return DeviceColumn(self, c, [])
 
     def hash_join_inner(self, probe_key: DeviceColumn, probe_cols: Sequence[DeviceColumn],
@@ -435,6 +437,20 @@ class Context:
         finally:
             self.lib.qeh_host_free(names)
         return parts, [self._wrap(out[i]) for i in range(nc.value)], rows.value
+
+    def slice(self, col: DeviceColumn, offset: int, length: int) -> DeviceColumn:
+        """Zero-copy view of rows [offset, offset + length) (RecordBatch::slice); keeps `col` alive."""
+        if offset < 0 or length < 0 or offset + length > len(col):
+            raise IndexError("slice outside the column")
+        c = abi.QehColumn()
+        C.pointer(c)[0] = col.c
+        c.owned = 0
+        c.offset = col.c.offset + offset
+        c.length = length
+        c.null_count = -1 if col.c.validity else 0
+        d = DeviceColumn(self, c)
+        d.parent = col
+        return d
 
     def take(self, col: DeviceColumn, indices: DeviceColumn) -> DeviceColumn:
         out = abi.QehColumn()

@@ -24,6 +24,7 @@ and host tensors under "gloo" (CPU rehearsal of the same code path).
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -38,10 +39,13 @@ TORCH_OF = {abi.DT_INT64: torch.int64, abi.DT_FLOAT64: torch.float64, abi.DT_INT
             abi.DT_FLOAT32: torch.float32, abi.DT_UINT32: torch.int32}
 
 
-def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=None
-             ) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=None,
+             byte_splits: Optional[dict] = None) -> Tuple[torch.Tensor, List[torch.Tensor]]:
     """All-to-all of partition-major payloads.  send_counts[r] rows of every
-    payload go to rank r.  Returns (recv_counts, received payloads)."""
+    payload go to rank r.  Returns (recv_counts, received payloads).
+    byte_splits: {payload index: per-rank element counts} for payloads whose
+    split is not the row split (the bytes of Utf8 columns); their receive
+    sizes are exchanged first."""
     world = dist.get_world_size(group)
     send_counts = send_counts.to(torch.int64)
     recv_counts = torch.empty_like(send_counts)
@@ -50,9 +54,15 @@ def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=
     outs = [int(x) for x in recv_counts.tolist()]
     assert len(ins) == world
     received = []
-    for p in payloads:
-        out = torch.empty((sum(outs),) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
-        dist.all_to_all_single(out, p.contiguous(), output_split_sizes=outs, input_split_sizes=ins, group=group)
+    for i, p in enumerate(payloads):
+        pin, pout = ins, outs
+        if byte_splits and i in byte_splits:
+            sc = torch.tensor(byte_splits[i], dtype=torch.int64, device=send_counts.device)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=group)
+            pin, pout = [int(x) for x in byte_splits[i]], [int(x) for x in rc.tolist()]
+        out = torch.empty((sum(pout),) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
+        dist.all_to_all_single(out, p.contiguous(), output_split_sizes=pout, input_split_sizes=pin, group=group)
         received.append(out)
     return recv_counts, received
 
@@ -71,10 +81,47 @@ class DistributedExecutor:
         self._keep: list = []  # tensors backing wrapped columns
 
     # ---- column <-> tensor ------------------------------------------------------
-    def _to_tensors(self, col: DeviceColumn) -> List[torch.Tensor]:
+    def _bits_to_bytes(self, col: DeviceColumn, bits_ptr: int) -> torch.Tensor:
+        """Bit-packed buffer (values of a Boolean column or any validity) -> one uint8 per row."""
         n = len(col)
-        if col.dtype == abi.DT_UTF8 or col.dtype == abi.DT_BOOL:
-            raise NotImplementedError("Utf8/Boolean columns are not exchanged between GPUs yet")
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        c = abi.QehColumn()
+        C.pointer(c)[0] = col.c
+        c.validity = bits_ptr
+        if n:
+            abi.check(self.ctx.lib.qeh_validity_to_bytes(self.ctx.h, c, out.data_ptr()))
+        return out
+
+    def _to_tensors(self, col: DeviceColumn) -> List[torch.Tensor]:
+        """Column -> payload tensors: values (Boolean: a byte per row; Utf8: int32 lengths, then
+        the bytes), then validity bytes when the column has a bitmap."""
+        n = len(col)
+        if col.dtype in (abi.DT_UTF8, abi.DT_BOOL):
+            if self.device == "cuda":
+                if col.dtype == abi.DT_BOOL:
+                    out = [self._bits_to_bytes(col, col.c.values)]
+                else:
+                    offs = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+                    self.ctx.copy_d2d(offs.data_ptr(), col.c.offsets + 4 * col.c.offset, 4 * (n + 1))
+                    self.ctx.sync()
+                    o0, o1 = (int(x) for x in offs[[0, n]].tolist())
+                    data = torch.empty(max(o1 - o0, 0), dtype=torch.uint8, device="cuda")
+                    if o1 > o0:
+                        self.ctx.copy_d2d(data.data_ptr(), col.c.values + o0, o1 - o0)
+                    out = [(offs[1:] - offs[:-1]).contiguous(), data]
+                if col.c.validity:
+                    out.append(self._bits_to_bytes(col, col.c.validity))
+                return out
+            v, m = col.to_numpy()
+            if col.dtype == abi.DT_BOOL:
+                out = [torch.from_numpy(np.asarray(v, np.uint8))]
+            else:
+                enc = [x.encode() for x in v]
+                out = [torch.tensor([len(b) for b in enc], dtype=torch.int32),
+                       torch.from_numpy(np.frombuffer(b"".join(enc), np.uint8).copy())]
+            if col.c.validity:
+                out.append(torch.from_numpy(m.astype(np.uint8)))
+            return out
         tdt = TORCH_OF[col.dtype]
         if self.device == "cuda":
             vals = torch.empty(n, dtype=tdt, device="cuda")
@@ -93,7 +140,9 @@ class DistributedExecutor:
             out.append(torch.from_numpy(m.astype(np.uint8)))
         return out
 
-    def _from_tensors(self, dtype: int, vals: torch.Tensor, valid: Optional[torch.Tensor]) -> DeviceColumn:
+    def _from_tensors(self, dtype: int, vals, valid: Optional[torch.Tensor]) -> DeviceColumn:
+        if dtype in (abi.DT_UTF8, abi.DT_BOOL):
+            return self._from_tensors_var(dtype, vals, valid)
         n = vals.shape[0]
         if self.device == "cuda":
             bitmap = 0
@@ -108,27 +157,67 @@ class DistributedExecutor:
         m = None if valid is None else valid.numpy().astype(bool)
         return self.ctx.upload(v, m)
 
+    def _bytes_to_bits(self, b: torch.Tensor) -> torch.Tensor:
+        n = b.shape[0]
+        bm = torch.zeros(((n + 63) // 64) * 8 + 8, dtype=torch.uint8, device="cuda")
+        if n:
+            abi.check(self.ctx.lib.qeh_bytes_to_validity(self.ctx.h, b.data_ptr(), n, bm.data_ptr()))
+        self._keep.append(bm)
+        return bm
+
+    def _from_tensors_var(self, dtype: int, vals, valid: Optional[torch.Tensor]) -> DeviceColumn:
+        if self.device == "cuda":
+            bitmap = self._bytes_to_bits(valid).data_ptr() if valid is not None else 0
+            if dtype == abi.DT_BOOL:
+                return self.ctx.wrap_device(dtype, self._bytes_to_bits(vals).data_ptr(), vals.shape[0], bitmap)
+            lens, data = vals
+            n = lens.shape[0]
+            offs = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+            if n:
+                offs[1:] = torch.cumsum(lens.to(torch.int64), 0).to(torch.int32)
+            if data.shape[0] == 0:
+                data = torch.zeros(8, dtype=torch.uint8, device="cuda")
+            self._keep.extend([offs, data])
+            return self.ctx.wrap_device(dtype, data.data_ptr(), n, bitmap, offsets=offs.data_ptr(),
+                                        values_bytes=int(offs[-1].item()) if n else 0)
+        m = None if valid is None else valid.numpy().astype(bool)
+        if dtype == abi.DT_BOOL:
+            return self.ctx.upload(vals.numpy().astype(bool), m)
+        lens, data = vals
+        raw = data.numpy().tobytes()
+        cum = np.concatenate([[0], np.cumsum(lens.numpy().astype(np.int64))])
+        strs = np.array([raw[cum[i]:cum[i + 1]].decode() for i in range(len(cum) - 1)], dtype=object)
+        return self.ctx.upload(strs, m)
+
     def _sync(self):
         if self.device == "cuda":
             self.ctx.sync()
 
     # ---- shuffle -----------------------------------------------------------------
     def _exchange_columns(self, cols: Sequence[DeviceColumn], counts) -> Tuple[List[DeviceColumn], List[int]]:
-        """All-to-all of partition-major columns: counts[r] leading rows go to rank r."""
-        payloads, shape = [], []
+        """All-to-all of partition-major columns: counts[r] leading rows go to rank r (Utf8
+        bytes travel with their own per-rank byte counts)."""
+        payloads, shape, byte_splits = [], [], {}
+        bounds = np.concatenate([[0], np.cumsum(np.asarray(counts, np.int64))])
         for t in cols:
             ts = self._to_tensors(t)
-            shape.append((t.dtype, len(ts) == 2))
+            nvals = 2 if t.dtype == abi.DT_UTF8 else 1
+            shape.append((t.dtype, len(ts) > nvals))
+            if t.dtype == abi.DT_UTF8:  # bytes per destination from the row lengths
+                lens = ts[0].to("cpu").numpy().astype(np.int64)
+                cum = np.concatenate([[0], np.cumsum(lens)])
+                byte_splits[len(payloads) + 1] = [int(cum[bounds[r + 1]] - cum[bounds[r]]) for r in range(self.world)]
             payloads.extend(ts)
         self._sync()
         recv_counts, recv = exchange(torch.tensor(np.asarray(counts), dtype=torch.int64, device=self.device), payloads,
-                                     self.group)
+                                     self.group, byte_splits)
         out, i = [], 0
         for dtype, nullable in shape:
-            vals = recv[i]
-            valid = recv[i + 1] if nullable else None
-            i += 2 if nullable else 1
-            out.append(self._from_tensors(dtype, vals, valid))
+            nvals = 2 if dtype == abi.DT_UTF8 else 1
+            vals = recv[i:i + nvals]
+            valid = recv[i + nvals] if nullable else None
+            i += nvals + (1 if nullable else 0)
+            out.append(self._from_tensors(dtype, vals[0] if nvals == 1 else vals, valid))
         return out, [int(x) for x in recv_counts.tolist()]
 
     def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
@@ -136,6 +225,28 @@ class DistributedExecutor:
         counts, perm = self.ctx.hash_partition(key, self.world)
         out, _ = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
         return out
+
+    def exchange(self, strategy, batch) -> "object":
+        """Exchange::execute across ranks (operators.rs:15-73, generalised to N GPUs): the
+        device partitioner (qe_hip.partition) splits this rank's batch into world_size
+        partitions — Hash / Range strategies must produce exactly world_size of them; Single
+        gathers everything on rank 0 — and partition p is sent to rank p in one all-to-all.
+        Returns the DeviceBatch this rank received (source-rank-major, stable)."""
+        from .partition import DeviceBatch, Partitioner, Single
+        if isinstance(strategy, Single):
+            n = batch.num_rows()
+            counts = np.zeros(self.world, np.int64)
+            counts[0] = n
+            cols = list(batch.columns)
+        else:
+            pt = Partitioner(self.ctx, strategy)
+            if pt.num_partitions() != self.world:
+                raise ValueError(f"exchange over {self.world} ranks needs {self.world} partitions, "
+                                 f"strategy gives {pt.num_partitions()}")
+            counts, perm = pt.batch_permutation(batch)
+            cols = [self.ctx.take(c, perm) for c in batch.columns]
+        recv, _ = self._exchange_columns(cols, counts)
+        return DeviceBatch(list(batch.names), recv)
 
     # ---- operators -----------------------------------------------------------------
     def hash_join_inner(self, probe_key_idx: int, probe_cols: Sequence[DeviceColumn], build_key_idx: int,

@@ -38,6 +38,97 @@ def mode_exchange(rank, world):
     assert got == want
 
 
+def mode_exchange_bytes(rank, world):
+    """Variable-size payloads (the bytes of Utf8 columns) ride the same all-to-all with their own
+    per-rank byte counts (exchange(..., byte_splits))."""
+    from qe_hip.distributed import exchange
+    r = np.random.default_rng(7 + rank)
+    n = 3000
+    dest = r.integers(0, world, n)
+    strs = [f"r{rank}-{i}-" + "x" * int(r.integers(0, 9)) for i in range(n)]
+    order = np.argsort(dest, kind="stable")
+    counts = np.bincount(dest, minlength=world)
+    enc = [strs[i].encode() for i in order]
+    lens = np.array([len(b) for b in enc], np.int32)
+    data = np.frombuffer(b"".join(enc), np.uint8).copy()
+    bounds = np.concatenate([[0], np.cumsum(counts)])
+    cum = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    splits = [int(cum[bounds[q + 1]] - cum[bounds[q]]) for q in range(world)]
+    rc, (rl, rd) = exchange(torch.tensor(counts), [torch.from_numpy(lens), torch.from_numpy(data)], byte_splits={1: splits})
+    raw = rd.numpy().tobytes()
+    c2 = np.concatenate([[0], np.cumsum(rl.numpy().astype(np.int64))])
+    got = sorted(raw[c2[i]:c2[i + 1]].decode() for i in range(len(rl)))
+    want = []
+    for q in range(world):
+        rq = np.random.default_rng(7 + q)
+        dq = rq.integers(0, world, n)
+        sq = [f"r{q}-{i}-" + "x" * int(rq.integers(0, 9)) for i in range(n)]
+        want += [sq[i] for i in range(n) if dq[i] == rank]
+    assert got == sorted(want)
+
+
+def mode_gpu_exchange(rank, world):
+    """DistributedExecutor.exchange: device Partitioner (Hash over Int64 + Utf8 keys, Range over
+    Int64, Single) + all-to-all of Int64 / Float64 / Utf8 / Boolean columns with NULLs."""
+    import qe_hip
+    from qe_hip.distributed import DistributedExecutor
+    from qe_hip.partition import DeviceBatch, Hash, Range, Single
+    ctx = qe_hip.Context(0)
+    dx = DistributedExecutor(ctx)
+
+    def rows(q):
+        r = np.random.default_rng(50 + q)
+        n = 4000 + 123 * q
+        k = r.integers(-50, 50, n).astype(np.int64)
+        km = r.random(n) > 0.05
+        s = np.array([f"s{int(x) % 7}" for x in r.integers(0, 100, n)], dtype=object)
+        sm = r.random(n) > 0.1
+        b = r.random(n) > 0.5
+        bm = r.random(n) > 0.2
+        v = r.random(n)
+        return k, km, s, sm, b, bm, v
+
+    def as_rows(cols):
+        out = []
+        vs = [c.to_numpy() for c in cols]
+        for i in range(len(cols[0])):
+            out.append(tuple(None if (m is not None and not m[i]) else (x[i].item() if hasattr(x[i], "item") else x[i])
+                             for x, m in vs))
+        return out
+
+    k, km, s, sm, b, bm, v = rows(rank)
+    batch = DeviceBatch(["k", "s", "b", "v"], [ctx.upload(k, km), ctx.upload(s, sm), ctx.upload(b, bm), ctx.upload(v)])
+    everything = []
+    for q in range(world):
+        kq, kmq, sq, smq, bq, bmq, vq = rows(q)
+        everything += [(None if not kmq[i] else int(kq[i]), None if not smq[i] else sq[i],
+                        None if not bmq[i] else bool(bq[i]), float(vq[i])) for i in range(len(kq))]
+    key = lambda t: tuple((x is None, x) for x in t)  # noqa: E731
+    for strat in (Hash(["k", "s"], world), Range("k", [int(x) for x in np.linspace(-40, 40, world - 1)]) if world > 1
+                  else Range("k", []), Single()):
+        got = dx.exchange(strat, batch)
+        mine = as_rows(got.columns)
+        allrecv = [None] * world
+        dist.all_gather_object(allrecv, mine)
+        union = sorted([t for part in allrecv for t in part], key=key)
+        assert union == sorted(everything, key=key), type(strat).__name__
+        if isinstance(strat, Hash):
+            owner = {}
+            for q, part in enumerate(allrecv):
+                for t in part:
+                    assert owner.setdefault((t[0], t[1]), q) == q  # equal keys share a rank
+        elif isinstance(strat, Range):
+            bnd = strat.boundaries
+            for t in mine:
+                if t[0] is None:
+                    assert rank == 0
+                else:
+                    assert rank == next((i for i, x in enumerate(bnd) if t[0] < x), len(bnd))
+        else:
+            assert (len(mine) == len(everything)) if rank == 0 else not mine
+    ctx.close()
+
+
 def mode_gpu(rank, world):
     import qe_hip
     import oracle_bind as ob
@@ -145,7 +236,8 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        {"exchange": mode_exchange, "gpu": mode_gpu}[mode](rank, world)
+        {"exchange": mode_exchange, "exchange_bytes": mode_exchange_bytes, "gpu": mode_gpu,
+         "gpu_exchange": mode_gpu_exchange}[mode](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -46,6 +46,19 @@ def test_exchange_gloo_cpu(world):
     launch("exchange", world)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_variable_size_payloads_gloo_cpu(world):
+    launch("exchange_bytes", world)
+
+
+@pytest.mark.gpu
+def test_device_exchange_two_ranks_on_one_gpu():
+    """§8 f2: DistributedExecutor.exchange with the device Partitioner (Hash / Range / Single) over
+    Int64, Float64, Utf8 and Boolean columns with NULLs; rows conserved, equal keys share a rank,
+    range ownership exact."""
+    launch("gpu_exchange", 2, timeout=600)
+
+
 def test_partial_final_decomposition():
     """The partial->final mapping of distributed/planner.rs:200-249: COUNT
     partials are summed, SUM/MIN/MAX partials re-aggregate with themselves."""

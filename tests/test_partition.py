@@ -1,0 +1,84 @@
+"""Partitioner / Exchange on the device: crates/query-distributed/src/
+partition.rs and operators.rs:15-73.  Known answers are the reference's own tests
+(partition.rs:381-455); range ownership is checked against a restatement of
+find_range_partition (partition.rs:320-341)."""
+import numpy as np
+import pytest
+
+from qe_hip import DeviceBatch, Exchange, Partitioner, PartitionStrategy
+from qe_hip.partition import PartitionError
+
+
+def batch(ctx, ids, names):
+    return DeviceBatch(["id", "name"], [ctx.upload(np.array(ids, np.int64)), ctx.upload(np.array(names, dtype=object))])
+
+
+def rows(b):
+    cols = [c.to_numpy() for c in b.columns]
+    return [tuple(None if (m is not None and not m[i]) else (v[i].item() if hasattr(v[i], "item") else v[i])
+                  for v, m in cols) for i in range(b.num_rows())]
+
+
+@pytest.mark.gpu
+def test_reference_partitioner_known_answers(ctx):
+    bs = [batch(ctx, [1, 2], ["a", "b"]), batch(ctx, [3, 4], ["c", "d"]), batch(ctx, [5, 6], ["e", "f"]),
+          batch(ctx, [7, 8], ["g", "h"])]
+    parts = Partitioner.round_robin(ctx, 2).partition(bs)  # test_round_robin_partition
+    assert len(parts) == 2 and [len(p.batches) for p in parts] == [2, 2]
+    assert [rows(b) for b in parts[0].batches] == [rows(bs[0]), rows(bs[2])]
+    parts = Partitioner.hash(ctx, ["id"], 3).partition([batch(ctx, [1, 2, 3, 4, 5], list("abcde"))])
+    assert len(parts) == 3 and sum(p.row_count() for p in parts) == 5  # test_hash_partition
+    parts = Partitioner(ctx, PartitionStrategy.Single()).partition(bs[:2])  # test_single_partition
+    assert len(parts) == 1 and len(parts[0].batches) == 2 and parts[0].row_count() == 4
+    assert Partitioner.round_robin(ctx, 4).num_partitions() == 4  # test_num_partitions
+    assert Partitioner.hash(ctx, [], 8).num_partitions() == 8
+    assert Partitioner(ctx, PartitionStrategy.Single()).num_partitions() == 1
+    assert Exchange.gather(ctx).num_partitions() == 1 and Exchange.hash(ctx, ["id"], 5).num_partitions() == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keys", [["k"], ["s"], ["k", "s"], ["k", "missing"]])
+def test_hash_partition_multi_key_conserves_and_colocates(ctx, keys):
+    r = np.random.default_rng(len(keys))
+    n = 50_000
+    k = r.integers(-30, 30, n).astype(np.int64)
+    km = r.random(n) > 0.05
+    s = np.array([f"v{int(x)}" for x in r.integers(0, 40, n)], dtype=object)
+    sm = r.random(n) > 0.1
+    b = DeviceBatch(["k", "s", "v"], [ctx.upload(k, km), ctx.upload(s, sm), ctx.upload(r.random(n))])
+    parts = Exchange.hash(ctx, keys, 7).execute([b, b])
+    got = [t for p in parts for bb in p.batches for t in rows(bb)]
+    assert sorted(got, key=str) == sorted(rows(b) * 2, key=str)
+    ki = [["k", "s", "v"].index(x) for x in keys if x in ("k", "s", "v")]
+    owner = {}
+    for p in parts:
+        for bb in p.batches:
+            assert bb.num_rows() > 0  # empty partition batches are not added
+            for t in rows(bb):
+                kt = tuple(t[i] for i in ki)
+                assert owner.setdefault(kt, p.index) == p.index
+
+
+@pytest.mark.gpu
+def test_range_partition_first_boundary_below_and_errors(ctx):
+    r = np.random.default_rng(2)
+    n = 20_000
+    k = r.integers(-100, 100, n).astype(np.int64)
+    km = r.random(n) > 0.1
+    bounds = [-50, 0, 0, 60]  # as given, not sorted-deduplicated: the first boundary above wins
+    b = DeviceBatch(["k"], [ctx.upload(k, km)])
+    parts = Partitioner(ctx, PartitionStrategy.Range("k", bounds)).partition([b])
+    assert len(parts) == 5
+    for p in parts:
+        for bb in p.batches:
+            for (x,) in rows(bb):
+                want = 0 if x is None else next((i for i, v in enumerate(bounds) if x < v), len(bounds))
+                assert p.index == want
+    # a non-Int64 key column lands in partition 0 (find_range_partition handles Int64 only)
+    f = DeviceBatch(["k"], [ctx.upload(r.random(100))])
+    parts = Partitioner(ctx, PartitionStrategy.Range("k", [0])).partition([f])
+    assert parts[0].row_count() == 100 and parts[1].row_count() == 0
+    with pytest.raises(PartitionError, match="Key column 'zz' not found"):
+        Partitioner(ctx, PartitionStrategy.Range("zz", [0])).partition([b])
+    with pytest.raises(PartitionError, match="No key columns found in batch"):
+        Partitioner.hash(ctx, ["zz"], 2).partition([b])

@@ -13,10 +13,11 @@
   left / full   LEFT / FULL outer join 2e8 x 1e7, half the probe rows unmatched
   merge   Merge::sorted of 8 partitions x 1.25e7 rows, ORDER BY k DESC NULLS LAST
   encode  pgwire DataRow text encoding of 1e7 result rows
+  partition  device side of a hash Exchange, 1e8 rows into 8 partitions
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
-usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge,encode] [--scale 1.0]
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge,encode,partition] [--scale 1.0]
 """
 import argparse
 import json
@@ -246,6 +247,29 @@ def cfg_encode(ctx, scale):
           "decode_host_GBs": len(data) / wall_d / 1e9})
 
 
+def cfg_partition(ctx, scale):
+    """§8 f2: the device side of a hash Exchange into 8 partitions (one per GPU of a node):
+    1e8 rows x (k Int64, v Float64) -> partition-major columns + counts.  Bytes: 16 B read +
+    16 B written per row (the permutation is an intermediate)."""
+    from qe_hip.partition import DeviceBatch, Hash, Partitioner
+    n = int(1e8 * scale)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, 1 << 40)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    pt = Partitioner(ctx, Hash(["k"], 8))
+    b = DeviceBatch(["k", "v"], [k, v])
+
+    def fn():
+        counts, perm = pt.batch_permutation(b)
+        moved = [ctx.take(c, perm) for c in b.columns]
+        for c in moved + [perm]:
+            c.release()
+        return counts
+    wall, kt, counts = timed(ctx, fn, 5, ["hash_partition", "radix_pass", "gather"])
+    line("hash Exchange 1e8 rows x (Int64, Float64) into 8 partitions (device side)", n, wall, 32.0 * n,
+         sum(kt.values()), "k_hash_ids_multi + 3-bit LSD pass + gathers", None,
+         {"kernel_split_ms": kt, "max_partition_share": float(max(counts)) / n})
+
+
 def cfg_filter(ctx, scale):
     n = int(5e8 * scale)
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
@@ -330,7 +354,7 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge, "encode": cfg_encode}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
