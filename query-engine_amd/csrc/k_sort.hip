@@ -314,6 +314,34 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
     return QEH_OK;
 }
 
+// One stable pass on the 8-bit digit at `shift` (u32 / u64 keys as KeyT).
+template <typename KeyT>
+static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
+    const int64_t n = rs.n;
+    if (n <= 1) return QEH_OK;
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)ctx->props.multiProcessorCount);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    DevBuf hist, offs;
+    QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
+    QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    KernelTimer kt(ctx, "radix_pass");
+    const int c = rs.cur;
+    hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
+                       hist.as<uint32_t>(), nblocks);
+    QEH_HIP(hipGetLastError());
+    QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+    hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
+                       rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
+                       rs.v[1 - c].as<uint32_t>());
+    QEH_HIP(hipGetLastError());
+    rs.cur = 1 - c;
+    return QEH_OK;
+}
+
+static int gc_of(qeh_ctx *ctx, int64_t nchunks) {
+    return (int)std::min<int64_t>(nchunks, (int64_t)ctx->props.multiProcessorCount * 8);
+}
+
 // Stable LSD passes over the low `bits` of the encoded keys in rs.
 static int radix_passes(qeh_ctx *ctx, RadixState &rs, int bits) {
     return rs.key32 ? radix_passes_t<uint32_t>(ctx, rs, bits) : radix_passes_t<uint64_t>(ctx, rs, bits);
@@ -632,9 +660,14 @@ __global__ __launch_bounds__(1024) void k_rn_prefix_max(int64_t *__restrict__ la
     }
 }
 
+// PAIRS: instead of scattering rn[perm[i]] (1e9 random 8-byte writes), write the pairs
+// (perm[i], rn) in sorted order; one stable radix pass on the destination's top bits then
+// groups them by output window and k_rn_scatter_windows writes one window at a time
+template <bool PAIRS>
 __global__ __launch_bounds__(kBlock) void k_rn_write(const uint32_t *__restrict__ flags, const int64_t *__restrict__ carry,
                                                      const uint32_t *__restrict__ perm, int64_t n, int64_t nchunks,
-                                                     int64_t *__restrict__ rn) {
+                                                     int64_t *__restrict__ rn, uint32_t *__restrict__ pair_dst,
+                                                     uint32_t *__restrict__ pair_rn) {
     __shared__ int64_t wmax[kBlock / 64];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -665,10 +698,25 @@ __global__ __launch_bounds__(kBlock) void k_rn_write(const uint32_t *__restrict_
         for (int j = 0; j < kRnPer; ++j) {
             const int64_t i = base + j;
             if (f[j]) start = i;
-            if (i < n) rn[perm[i]] = i - start + 1;
+            if (i < n) {
+                if (PAIRS) {
+                    pair_dst[i] = perm[i];
+                    pair_rn[i] = (uint32_t)(i - start + 1);
+                } else {
+                    rn[perm[i]] = i - start + 1;
+                }
+            }
         }
         __syncthreads();
     }
+}
+
+// pairs grouped by output window (destination >> shift): consecutive workgroups write inside
+// one window at a time, so the partial-line writes meet in L2 / the Infinity Cache instead of HBM
+__global__ void k_rn_scatter_windows(const uint32_t *__restrict__ dst, const uint32_t *__restrict__ val, int64_t n,
+                                     int64_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[dst[i]] = (int64_t)val[i];
 }
 
 // ---- hash partition ---------------------------------------------------------------------------
@@ -890,12 +938,39 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     }
     {
         KernelTimer kt(ctx, "row_number");
-        const int gc = (int)std::min<int64_t>(nchunks, (int64_t)ctx->props.multiProcessorCount * 8);
-        hipLaunchKernelGGL(k_rn_chunk_last, dim3(gc), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), n, nchunks,
+        hipLaunchKernelGGL(k_rn_chunk_last, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), n, nchunks,
                            seg.as<int64_t>());
         hipLaunchKernelGGL(k_rn_prefix_max, dim3(1), dim3(1024), 0, ctx->stream, seg.as<int64_t>(), nchunks);
-        hipLaunchKernelGGL(k_rn_write, dim3(gc), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(), seg.as<int64_t>(), perm, n,
-                           nchunks, (int64_t *)out_rn->values);
+    }
+    const int dbits = bit_length((uint64_t)(n - 1));
+    // Direct scatter by default: grouping the (destination, rn) pairs into 32 MB output windows
+    // first (one radix pass on the destination's top bits) measured slower at 1e9 rows (61 vs
+    // 40 ms: the windows' partial-line writes from all XCDs still reach HBM); kept behind
+    // QEH_RN_WINDOWED for experiments.
+    if (dbits <= 22 || !std::getenv("QEH_RN_WINDOWED")) {
+        KernelTimer kt(ctx, "row_number");
+        hipLaunchKernelGGL(k_rn_write<false>, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(),
+                           seg.as<int64_t>(), perm, n, nchunks, (int64_t *)out_rn->values, nullptr, nullptr);
+    } else {
+        // (destination, rn) pairs in sorted order into the spare radix buffers, one stable 8-bit
+        // pass on the destination's top bits (windows of 2^(dbits-8) rows), windowed scatter
+        const int o = 1 - rs.cur;
+        {
+            KernelTimer kt(ctx, "row_number");
+            hipLaunchKernelGGL(k_rn_write<true>, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream,
+                               flags.as<uint32_t>(), seg.as<int64_t>(), perm, n, nchunks, nullptr, rs.k[o].as<uint32_t>(),
+                               rs.v[o].as<uint32_t>());
+        }
+        rs.cur = o;
+        rs.key32 = true;
+        s = radix_pass_at<uint32_t>(ctx, rs, dbits - kRadixBits);
+        if (s != QEH_OK) {
+            qeh_column_release(ctx, out_rn);
+            return s;
+        }
+        KernelTimer kt(ctx, "row_number");
+        hipLaunchKernelGGL(k_rn_scatter_windows, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                           rs.k[rs.cur].as<uint32_t>(), rs.v[rs.cur].as<uint32_t>(), n, (int64_t *)out_rn->values);
     }
     QEH_HIP(hipGetLastError());
     QEH_HIP(hipStreamSynchronize(ctx->stream));

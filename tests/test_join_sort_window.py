@@ -420,3 +420,18 @@ def test_outer_join_embedded_build_path(ctx, jt, nb):
     else:
         got, want = outer_both(ctx, jt, (bk, None), bcols, (pk, pkv), pcols)
     assert rows_of(got) == rows_of(want)
+
+
+@pytest.mark.gpu
+def test_row_number_windowed_scatter_path(ctx, monkeypatch):
+    """n > 2^22: the direct scatter and the experimental windowed scatter (QEH_RN_WINDOWED:
+    (destination, rn) pairs grouped by output window by one radix pass) both match the oracle."""
+    r = np.random.default_rng(21)
+    n = 5_000_001
+    k = r.integers(0, 1 << 16, n).astype(np.int64)
+    v = r.integers(-(2 ** 40), 2 ** 40, n).astype(np.int64)
+    got = ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [True]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k)], [ob.HostCol(v)], [True])
+    assert np.array_equal(got, want)
+    monkeypatch.setenv("QEH_RN_WINDOWED", "1")
+    assert np.array_equal(ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [True]).to_numpy()[0], want)
