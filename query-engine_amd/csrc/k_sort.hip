@@ -494,7 +494,12 @@ static int sort_perm_pair(qeh_ctx *ctx, const qeh_column &ca, const qeh_column &
         shift = 0;
         total = ba + bb;
     } else if (ba <= 40) {
-        total = ba <= 32 ? 48 : 64;  // keep >= 16 bits of b: equal-K runs stay rare
+        // K keeps a's bits and the top bits of b; equal-K runs (fixed up exactly below) stay rare
+        // when K has ~10 bits more than the row count needs: total = roundup8(log2 n + 10), at
+        // least 16 bits of b, at most 64 (1e9 rows: 40 bits = 5 passes instead of 6)
+        total = std::min(64, (bit_length((uint64_t)n) + 10 + 7) / 8 * 8);
+        if (total < ba + 16) total = std::min(64, (ba + 16 + 7) / 8 * 8);
+        if (total < 40) total = 40;  // 64-bit keys (k_fix_pair_runs reads them as such)
         bv = total - ba;
         shift = bb - bv;
     } else {
