@@ -313,6 +313,12 @@ int qeh_range_partition(qeh_ctx *ctx, const qeh_column *key, int ascending, cons
 int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, int64_t *counts,
                        qeh_column *out_perm);
 
+/* qeh_partition_hash + the gathers in one go: `cols` leave in partition-major order (stable)
+ * as owned columns out_cols[0 .. n_cols), with per-partition counts.  Non-null Int64 / Float64
+ * columns are moved by a single tile-ranked pass; other columns through the permutation. */
+int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, const qeh_column *cols,
+                            int n_cols, int64_t *counts, qeh_column *out_cols);
+
 /* Partitioner::partition_by_range (partition.rs:259-341): row -> the first i with
  * value < boundaries[i], else n_boundaries; NULL -> 0; a non-Int64 key puts every row in
  * partition 0, as the reference does.  Same output as qeh_partition_hash. */

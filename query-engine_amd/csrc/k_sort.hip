@@ -277,6 +277,101 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     }
 }
 
+// Partition move (the device side of Exchange): one stable pass over u8 partition ids that
+// carries up to 4 non-null 8-byte payload columns to their partition-major positions, with the
+// same tile ranking and run-contiguous writes as k_rs_scatter — instead of a permutation
+// followed by one gather per column (a gather re-reads every source line once per partition).
+constexpr int kPmMaxCols = 4;
+constexpr int kPmIpt = 4;
+constexpr int kPmTile = kRsThreads * kPmIpt;  // 4096 rows: ids + 4 columns fit in LDS
+
+struct PmCols {
+    const uint64_t *src[kPmMaxCols];
+    uint64_t *dst[kPmMaxCols];
+    int32_t n;
+};
+
+template <int NC>
+__global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
+                                                             const uint64_t *__restrict__ offs, int nblocks, PmCols cols) {
+    constexpr int W = kRsThreads / 64;
+    constexpr int DW = kRadix / 64;
+    __shared__ uint64_t s_val[NC > 0 ? NC : 1][kPmTile];
+    __shared__ uint8_t s_id[kPmTile];
+    __shared__ uint32_t wcnt[W][kRadix];
+    __shared__ uint32_t loc[kRadix];
+    __shared__ uint32_t tot_s[kRadix];
+    __shared__ uint32_t wsum[DW];
+    __shared__ uint64_t run[kRadix];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    for (int64_t c0 = lo; c0 < hi; c0 += kPmTile) {
+        for (int i = t; i < W * kRadix; i += kRsThreads) (&wcnt[0][0])[i] = 0;
+        const int64_t base = c0 + (int64_t)wave * 64 * kPmIpt + lane;
+        uint32_t dg[kPmIpt];
+        uint64_t v[kPmIpt][NC > 0 ? NC : 1];
+#pragma unroll
+        for (int j = 0; j < kPmIpt; ++j) {
+            const int64_t i = base + j * 64;
+            const int64_t ii = i < hi ? i : hi - 1;
+            dg[j] = ids[ii];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[j][c] = __builtin_nontemporal_load(&cols.src[c][ii]);
+        }
+        __syncthreads();
+        uint32_t rk[kPmIpt];
+#pragma unroll
+        for (int j = 0; j < kPmIpt; ++j) {
+            const bool live = base + j * 64 < hi;
+            const uint64_t peers = digit_peers(dg[j], live);
+            const uint32_t before = wcnt[wave][dg[j]];
+            rk[j] = before + mbcnt(peers);
+            if (live && mbcnt(peers) == 0) wcnt[wave][dg[j]] = before + (uint32_t)popc64(peers);
+        }
+        __syncthreads();
+        uint32_t tot = 0, incl = 0;
+        if (t < kRadix) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = wcnt[w][t];
+                wcnt[w][t] = tot;
+                tot += c;
+            }
+            tot_s[t] = tot;
+            incl = wave_incl_scan(tot);
+            if (lane == 63) wsum[wave] = incl;
+        }
+        __syncthreads();
+        if (t < kRadix) {
+            uint32_t wbase = 0;
+#pragma unroll
+            for (int w = 0; w < DW; ++w) wbase += w < wave ? wsum[w] : 0;
+            loc[t] = wbase + incl - tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPmIpt; ++j) {
+            if (base + j * 64 < hi) {
+                const uint32_t p = loc[dg[j]] + wcnt[wave][dg[j]] + rk[j];
+                s_id[p] = (uint8_t)dg[j];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) s_val[c][p] = v[j][c];
+            }
+        }
+        __syncthreads();
+        const int cnt = (int)(hi - c0 < kPmTile ? hi - c0 : kPmTile);
+        for (int p = t; p < cnt; p += kRsThreads) {
+            const uint32_t d = s_id[p];
+            const uint64_t pos = run[d] + (uint64_t)(p - (int)loc[d]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) cols.dst[c][pos] = s_val[c][p];
+        }
+        __syncthreads();
+        if (t < kRadix) run[t] += tot_s[t];
+    }
+}
+
 // Sort state: encoded keys + permutation, double-buffered.
 struct RadixState {
     DevBuf k[2], v[2];
@@ -783,6 +878,25 @@ __global__ void k_hash_ids_multi(HashKeys keys, int64_t n, uint32_t parts, uint6
     }
 }
 
+__global__ void k_hash_ids8(HashKeys keys, int64_t n, uint32_t parts, uint8_t *__restrict__ ids) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (int j = 0; j < keys.n; ++j) {
+            const ColRef &c = keys.c[j];
+            if (!col_valid(c, i)) continue;
+            uint64_t v;
+            if (c.dtype == QEH_DT_UTF8) {
+                v = 0xcbf29ce484222325ull;
+                for (int32_t b = keys.offs[j][i]; b < keys.offs[j][i + 1]; ++b) v = (v ^ keys.data[j][b]) * 0x100000001b3ull;
+            } else {
+                v = (uint64_t)load_i64(c, i);
+            }
+            h = hash64(h ^ (hash64(v) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+        }
+        ids[i] = (uint8_t)(h % parts);
+    }
+}
+
 // PartitionStrategy::Range (find_range_partition, partition.rs:320-341): the first boundary the
 // value is below, or len(boundaries); NULL -> 0; only Int64 keys are ranged (every other column
 // type lands in partition 0, as in the reference)
@@ -1092,6 +1206,116 @@ extern "C" int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_ke
                                (uint32_t)n_parts, ids, idx);
         },
         "hash_partition", counts, out_perm);
+}
+
+static int make_hash_keys(const qeh_column *keys, int n_keys, HashKeys *hk, int64_t *n) {
+    hk->n = n_keys;
+    *n = keys[0].length;
+    for (int j = 0; j < n_keys; ++j) {
+        QEH_TRY(check_column(keys[j], "partition key"));
+        if (keys[j].length != *n) return fail(QEH_E_INVALID, "partition keys have different lengths");
+        if (keys[j].dtype != QEH_DT_INT64 && keys[j].dtype != QEH_DT_INT32 && keys[j].dtype != QEH_DT_UTF8)
+            return fail(QEH_E_UNSUPPORTED, "hash partition keys must be Int32 / Int64 / Utf8 (compute_row_hash)");
+        hk->c[j] = make_colref(keys[j]);
+        if (keys[j].dtype == QEH_DT_UTF8) {
+            hk->offs[j] = keys[j].offsets + keys[j].offset;
+            hk->data[j] = (const uint8_t *)keys[j].values;
+        }
+    }
+    return QEH_OK;
+}
+
+// Exchange's device side in one pass: partition ids, per-segment histograms, then the payload
+// columns moved to partition-major order (k_part_scatter).  Columns that are not non-null
+// 8-byte go through the permutation + gather path.
+extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts,
+                                       const qeh_column *cols, int n_cols, int64_t *counts, qeh_column *out_cols) {
+    if (!ctx || !keys || n_keys < 1 || n_keys > kMaxCols || !counts || n_parts < 1 || n_parts > kRadix || n_cols < 0 ||
+        (n_cols > 0 && (!cols || !out_cols)))
+        return fail(QEH_E_INVALID, "qeh_partition_hash_move: bad argument (1..12 keys, 1..256 partitions)");
+    DeviceGuard dg(ctx->device);
+    HashKeys hk{};
+    int64_t n;
+    QEH_TRY(make_hash_keys(keys, n_keys, &hk, &n));
+    for (int c = 0; c < n_cols; ++c) {
+        QEH_TRY(check_column(cols[c], "partition column"));
+        if (cols[c].length != n) return fail(QEH_E_INVALID, "partition columns and keys have different lengths");
+    }
+    auto movable = [](const qeh_column &c) {
+        return (c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_FLOAT64) && (!c.validity || c.null_count == 0);
+    };
+    std::vector<int> mv, other;
+    for (int c = 0; c < n_cols; ++c) (movable(cols[c]) ? mv : other).push_back(c);
+    std::fill(counts, counts + n_parts, 0);
+    std::vector<char> made(n_cols, 0);
+    auto cleanup = [&]() {
+        for (int c = 0; c < n_cols; ++c)
+            if (made[c]) qeh_column_release(ctx, &out_cols[c]);
+    };
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
+                                               (int64_t)ctx->props.multiProcessorCount);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    DevBuf ids, hist, offs;
+    QEH_TRY(ids.alloc(ctx, (size_t)std::max<int64_t>(n, 1)));
+    QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
+    QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    std::vector<uint32_t> h((size_t)kRadix * nblocks, 0);
+    if (n > 0) {
+        KernelTimer kt(ctx, "partition_move");
+        hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
+                           (uint32_t)n_parts, ids.as<uint8_t>());
+        hipLaunchKernelGGL(k_rs_hist<uint8_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, 0,
+                           hist.as<uint32_t>(), nblocks);
+        QEH_HIP(hipGetLastError());
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));
+        for (int p = 0; p < n_parts; ++p)
+            for (int b = 0; b < nblocks; ++b) counts[p] += h[(size_t)p * nblocks + b];
+    }
+    int s = QEH_OK;
+    for (int c : mv) {
+        if ((s = alloc_column(ctx, cols[c].dtype, n, false, &out_cols[c])) != QEH_OK) break;
+        made[c] = 1;
+    }
+    for (size_t g = 0; s == QEH_OK && g < mv.size() && n > 0; g += kPmMaxCols) {
+        PmCols pc{};
+        const int nc = (int)std::min<size_t>(kPmMaxCols, mv.size() - g);
+        pc.n = nc;
+        for (int q = 0; q < nc; ++q) {
+            const qeh_column &src = cols[mv[g + q]];
+            pc.src[q] = (const uint64_t *)src.values + src.offset;
+            pc.dst[q] = (uint64_t *)out_cols[mv[g + q]].values;
+        }
+        KernelTimer kt(ctx, "partition_move");
+#define QEH_PM(NCV)                                                                                                        \
+    hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, \
+                       offs.as<uint64_t>(), nblocks, pc)
+        if (nc == 1) QEH_PM(1);
+        else if (nc == 2) QEH_PM(2);
+        else if (nc == 3) QEH_PM(3);
+        else QEH_PM(4);
+#undef QEH_PM
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "partition move launch failed");
+    }
+    if (s == QEH_OK && !other.empty()) {  // permutation + gathers for the rest
+        int64_t c2[kRadix];
+        qeh_column perm{};
+        s = qeh_partition_hash(ctx, keys, n_keys, n_parts, c2, &perm);
+        for (size_t q = 0; s == QEH_OK && q < other.size(); ++q) {
+            s = gather_column(ctx, cols[other[q]], (const uint32_t *)perm.values, n, &out_cols[other[q]]);
+            if (s == QEH_OK) made[other[q]] = 1;
+        }
+        if (perm.owned) {
+            (void)hipStreamSynchronize(ctx->stream);
+            qeh_column_release(ctx, &perm);
+        }
+    }
+    if (s == QEH_OK) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("partition move: ") + hipGetErrorString(e));
+    }
+    if (s != QEH_OK) cleanup();
+    return s;
 }
 
 extern "C" int qeh_partition_range(qeh_ctx *ctx, const qeh_column *key, const int64_t *boundaries, int n_boundaries,

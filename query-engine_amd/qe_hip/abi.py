@@ -93,6 +93,7 @@ SIGNATURES = {
     "qeh_decode_arrow_ipc": (I, [P, C.c_void_p, I64, COLP, I, C.POINTER(I), C.POINTER(C.c_void_p), C.POINTER(I64)]),
     "qeh_partition_hash": (I, [P, COLP, I, I, C.POINTER(I64), COLP]),
     "qeh_partition_range": (I, [P, COLP, C.POINTER(I64), I, C.POINTER(I64), COLP]),
+    "qeh_partition_hash_move": (I, [P, COLP, I, I, COLP, I, C.POINTER(I64), COLP]),
     "qeh_take": (I, [P, COLP, COLP, COLP]),
     "qeh_row_number": (I, [P, COLP, I, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_hash_partition": (I, [P, COLP, I, C.POINTER(I64), COLP]),

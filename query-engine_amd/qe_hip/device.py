@@ -438,6 +438,14 @@ class Context:
             self.lib.qeh_host_free(names)
         return parts, [self._wrap(out[i]) for i in range(nc.value)], rows.value
 
+    def partition_hash_move(self, keys: Sequence[DeviceColumn], n_parts: int, cols: Sequence[DeviceColumn]):
+        """qeh_partition_hash_move: (counts, cols in partition-major order)."""
+        counts = (C.c_int64 * n_parts)()
+        out = (abi.QehColumn * max(len(cols), 1))()
+        abi.check(self.lib.qeh_partition_hash_move(self.h, self._cols(keys), len(keys), n_parts, self._cols(cols),
+                                                   len(cols), counts, out))
+        return np.array(counts[:], np.int64), [self._wrap(out[i]) for i in range(len(cols))]
+
     def slice(self, col: DeviceColumn, offset: int, length: int) -> DeviceColumn:
         """Zero-copy view of rows [offset, offset + length) (RecordBatch::slice); keeps `col` alive."""
         if offset < 0 or length < 0 or offset + length > len(col):

@@ -243,8 +243,7 @@ class DistributedExecutor:
             if pt.num_partitions() != self.world:
                 raise ValueError(f"exchange over {self.world} ranks needs {self.world} partitions, "
                                  f"strategy gives {pt.num_partitions()}")
-            counts, perm = pt.batch_permutation(batch)
-            cols = [self.ctx.take(c, perm) for c in batch.columns]
+            counts, cols = pt.batch_move(batch)
         recv, _ = self._exchange_columns(cols, counts)
         return DeviceBatch(list(batch.names), recv)
 

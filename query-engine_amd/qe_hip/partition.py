@@ -4,9 +4,10 @@ Mirrors crates/query-distributed/src/partition.rs (PartitionStrategy :21-46, Par
 Partitioner :93-357) and operators.rs:15-73 (Exchange).  A batch is a `DeviceBatch` (field names
 + device columns), since the reference resolves key columns by name in each batch's schema.
 
-* Hash: per batch, `qeh_partition_hash` over the named key columns (names that do not resolve are
-  skipped; none resolving is the reference's "No key columns found in batch" error), then one
-  gather per column and partition; empty partition batches are not added (partition.rs:190-193).
+* Hash: per batch, `qeh_partition_hash_move` over the named key columns (names that do not
+  resolve are skipped; none resolving is the reference's "No key columns found in batch" error):
+  partition ids, then the columns moved to partition-major order in one tile-ranked pass, sliced
+  per partition; empty partition batches are not added (partition.rs:190-193).
 * Range: `qeh_partition_range` (first boundary the Int64 value is below; NULL / other types -> 0).
   A missing key column is the reference's "Key column '<name>' not found" error.
 * RoundRobin: whole batches, batch i -> partition i % n (partition.rs:215-229).
@@ -146,6 +147,18 @@ class Partitioner:
             return np.array(counts[:], np.int64), self.ctx._wrap(out)
         raise TypeError("batch_permutation: row-level strategies only (Hash, Range)")
 
+    def batch_move(self, batch: DeviceBatch):
+        """(counts, the batch's columns in partition-major order): Hash moves the columns in one
+        device pass (qeh_partition_hash_move), Range through the permutation."""
+        s = self.strategy
+        if isinstance(s, Hash):
+            idx = [batch.names.index(n) for n in s.key_columns if n in batch.names]
+            if not idx:
+                raise PartitionError("No key columns found in batch")
+            return self.ctx.partition_hash_move([batch.columns[i] for i in idx], s.num_partitions, batch.columns)
+        counts, perm = self.batch_permutation(batch)
+        return counts, [self.ctx.take(c, perm) for c in batch.columns]
+
     def partition(self, batches: Sequence[DeviceBatch]) -> List[Partition]:
         s = self.strategy
         parts = [Partition(i) for i in range(self.num_partitions())]
@@ -158,9 +171,7 @@ class Partitioner:
                 parts[i % s.num_partitions].add_batch(b)
             return parts
         for b in batches:
-            counts, perm = self.batch_permutation(b)
-            # every column gathered once through the partition-major permutation, then sliced
-            moved = [self.ctx.take(c, perm) for c in b.columns]
+            counts, moved = self.batch_move(b)
             off = 0
             for p, cnt in enumerate(counts):
                 if cnt:

@@ -82,3 +82,30 @@ def test_range_partition_first_boundary_below_and_errors(ctx):
         Partitioner(ctx, PartitionStrategy.Range("zz", [0])).partition([b])
     with pytest.raises(PartitionError, match="No key columns found in batch"):
         Partitioner.hash(ctx, ["zz"], 2).partition([b])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", [(0, 3), (1, 1), (4095, 2), (4097, 8), (300_001, 256), (2_000_003, 8)])
+def test_partition_hash_move_matches_permutation(ctx, n, parts):
+    """qeh_partition_hash_move == qeh_partition_hash's permutation + gathers (same counts, same
+    stable partition-major order), with 1-5 movable columns and a nullable / Utf8 column that
+    take the gather path."""
+    r = np.random.default_rng(n + parts)
+    k = r.integers(-1000, 1000, n).astype(np.int64)
+    cols = [ctx.upload(k), ctx.upload(r.random(n)), ctx.upload(r.integers(0, 9, n).astype(np.int64)),
+            ctx.upload(r.random(n)), ctx.upload(r.random(n)),
+            ctx.upload(r.integers(0, 5, n).astype(np.int64), r.random(n) > 0.3),
+            ctx.upload(np.array([f"t{i % 11}" for i in range(n)], dtype=object))]
+    counts, moved = ctx.partition_hash_move([cols[0]], parts, cols)
+    import ctypes as C
+    from qe_hip import abi
+    c2 = (C.c_int64 * parts)()
+    perm = abi.QehColumn()
+    abi.check(ctx.lib.qeh_partition_hash(ctx.h, ctx._cols([cols[0]]), 1, parts, c2, C.byref(perm)))
+    perm = ctx._wrap(perm)
+    assert list(counts) == list(c2[:]) and counts.sum() == n
+    for c, m in zip(cols, moved):
+        want = ctx.take(c, perm).to_numpy()
+        got = m.to_numpy()
+        assert np.array_equal(got[0], want[0]) if got[1] is None else \
+            (np.array_equal(got[1], want[1]) and np.array_equal(got[0][got[1]], want[0][want[1]]))

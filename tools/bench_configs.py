@@ -259,14 +259,13 @@ def cfg_partition(ctx, scale):
     b = DeviceBatch(["k", "v"], [k, v])
 
     def fn():
-        counts, perm = pt.batch_permutation(b)
-        moved = [ctx.take(c, perm) for c in b.columns]
-        for c in moved + [perm]:
+        counts, moved = pt.batch_move(b)
+        for c in moved:
             c.release()
         return counts
-    wall, kt, counts = timed(ctx, fn, 5, ["hash_partition", "radix_pass", "gather"])
+    wall, kt, counts = timed(ctx, fn, 5, ["partition_move"])
     line("hash Exchange 1e8 rows x (Int64, Float64) into 8 partitions (device side)", n, wall, 32.0 * n,
-         sum(kt.values()), "k_hash_ids_multi + 3-bit LSD pass + gathers", None,
+         sum(kt.values()), "k_hash_ids8 + k_rs_hist + k_part_scatter (columns moved in one pass)", None,
          {"kernel_split_ms": kt, "max_partition_share": float(max(counts)) / n})
 
 
