@@ -6,8 +6,8 @@ Exchange (operators.rs:15-73) and partial/final aggregate and shuffle-join stage
 shapes (planner.rs:200-249) — and never executes workers.  Here the same
 stages run for real:
 
-  * shuffle(key, cols): device hash partition (qeh_hash_partition) -> device
-    gather into partition-major order -> ONE all_to_all per column over RCCL
+  * shuffle(key, cols): device hash partition + move into partition-major
+    order (qeh_partition_hash_move) -> ONE all_to_all per column over RCCL
     (counts first, so every rank knows its receive splits).
   * hash_join_inner: shuffle both sides by the join key, local device join.
   * group_by: local partial aggregate -> shuffle partial states by the first
@@ -222,8 +222,8 @@ class DistributedExecutor:
 
     def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
         """Route every row to rank hash(key) % world (partition.rs:151-212)."""
-        counts, perm = self.ctx.hash_partition(key, self.world)
-        out, _ = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
+        counts, moved = self.ctx.partition_hash_move([key], self.world, cols)  # one device pass
+        out, _ = self._exchange_columns(moved, counts)
         return out
 
     def exchange(self, strategy, batch) -> "object":
