@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--dim", type=int, default=10_000_000)
     ap.add_argument("--groups", type=int, default=1024)
     ap.add_argument("--threshold", type=int, default=49, help="WHERE f.x > threshold (49 = the BASELINE query)")
-    ap.add_argument("--cpu-sample", type=int, default=50_000_000, help="fact rows for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=100_000_000, help="fact rows for the CPU baseline (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch of the probe kernel (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -191,7 +191,7 @@ def main():
             traffic = None
 
     if rank == 0:
-        cpu = cpu_baseline(args)
+        cpu = cpu_baseline(args) if world == 1 else None  # the CPU baseline is an N=1 figure
         line = {
             "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
             "value": value,
