@@ -501,7 +501,8 @@ extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t 
     const int64_t rows = br.scalar<int64_t>(bm.header, 0, 0);
     const size_t nodes = br.table(bm.header, 1), bufs = br.table(bm.header, 2);
     if (br.field(bm.header, 3)) return fail(QEH_E_UNSUPPORTED, "ipc: compressed bodies are not supported");
-    if (!br.ok || rows < 0 || !nodes || !bufs || br.vec_len(nodes) != nf) return fail(QEH_E_INVALID, "ipc: malformed record batch");
+    if (!br.ok || rows < 0 || rows > ((int64_t)1 << 40) || !nodes || !bufs || br.vec_len(nodes) != nf)
+        return fail(QEH_E_INVALID, "ipc: malformed record batch");
     const uint32_t nb = br.vec_len(bufs);
     uint32_t bi = 0;
     auto buffer = [&](const uint8_t **p, int64_t *len) -> int {
@@ -549,12 +550,21 @@ extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t 
             c.offsets = (int32_t *)o;
             c.values = d;
             c.values_bytes = dl;
-            int32_t last;
+            // untrusted offsets: non-decreasing, inside the data buffer (device kernels index with them)
+            int32_t prev, last;
+            std::memcpy(&prev, op, 4);
+            bool mono = prev >= 0;
+            for (int64_t r = 1; mono && r <= rows; ++r) {
+                int32_t cur;
+                std::memcpy(&cur, op + r * 4, 4);
+                mono = cur >= prev;
+                prev = cur;
+            }
             std::memcpy(&last, op + rows * 4, 4);
-            if (last < 0 || last > dl) {
+            if (!mono || last < 0 || last > dl) {
                 ctx->pool->free(o);
                 ctx->pool->free(d);
-                s = fail(QEH_E_INVALID, "ipc: Utf8 offsets outside the data buffer");
+                s = fail(QEH_E_INVALID, "ipc: Utf8 offsets decreasing or outside the data buffer");
                 break;
             }
             QEH_HIP(hipMemcpyAsync(o, op, (size_t)(rows + 1) * 4, hipMemcpyHostToDevice, ctx->stream));

@@ -209,6 +209,18 @@ def test_arrow_ipc_decode_rejects_malformed(ctx):
     for bad in (data[:10], data[:len(data) // 2], b"\xff\xff\xff\xff" + b"\x10\x00\x00\x00" + b"\x00" * 16):
         with pytest.raises(QehError):
             ctx.decode_arrow_ipc(bad)
+    # a Utf8 column whose offsets decrease: rejected before anything reaches the device
+    st = pa.BufferOutputStream()
+    ts = pa.table({"s": pa.array(["ab", "cd", "ef"])})
+    with pa.ipc.new_stream(st, ts.schema) as w:
+        w.write_table(ts)
+    raw = bytearray(st.getvalue().to_pybytes())
+    import struct as _st
+    pat = _st.pack("<4i", 0, 2, 4, 6)
+    at = bytes(raw).index(pat)
+    raw[at:at + 16] = _st.pack("<4i", 0, 4, 2, 6)
+    with pytest.raises(QehError, match="offsets"):
+        ctx.decode_arrow_ipc(bytes(raw))
     only_schema = data[:data.index(b"\xff\xff\xff\xff", 8)]
     with pytest.raises(QehError, match="No batch found"):
         ctx.decode_arrow_ipc(only_schema + b"\xff\xff\xff\xff\x00\x00\x00\x00")
