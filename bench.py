@@ -224,7 +224,8 @@ def main():
                 "kernel": kernel_name,
                 "kernel_ms": avg_probe_ms,
                 "kernel_split_ms": kernel_split,
-                "operator_ms": probe_ms / max(probe_launches, 1),
+                # the operator's main-queue part (phase A runs on the second queue, under the build)
+                "operator_main_queue_ms": probe_ms / max(probe_launches, 1),
                 "alg_bytes_per_launch": alg_bytes,
             },
             "build_ms_per_step": build_ms / args.steps,

@@ -1304,12 +1304,124 @@ static uint64_t table_bytes(const HashTable &t) {
     return (t.mask + 1) * 16;
 }
 
+// Phase A does not need the join table — only its key range — so the fused join-aggregate
+// launches it on the context's second queue right after the build key's min/max, and the
+// build (group table, join table) runs on the main queue underneath it.  try_slice_join then
+// only waits for it before phase B.  When the finished table turns out not to fit the slice
+// path (duplicate keys, wide payloads), the prelaunched work is discarded.
+struct SlicePre {
+    bool launched = false;
+    int64_t kmin = 0;
+    uint64_t range = 0;
+    int grid = 0;
+    int64_t n_tiles = 0;
+    DevBuf kbuf, vbuf, cbuf;
+    SliceRegions rg{};
+    hipEvent_t done = nullptr;
+    ~SlicePre() {
+        if (done) {  // the buffers below must outlive the kernel
+            (void)hipEventSynchronize(done);
+            (void)hipEventDestroy(done);
+        }
+    }
+};
+
+// regions sized for every row selected with keys uniform over the slices, +25 %
+static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, int nacol, DevBuf *kbuf, DevBuf *vbuf,
+                          DevBuf *cbuf, SliceRegions *rg, hipStream_t stream) {
+    const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
+    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
+    cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
+    const uint64_t nreg = (uint64_t)grid * F;
+    if (kbuf->alloc(ctx, nreg * cap * 2 + 64) != QEH_OK) return false;
+    if (nacol && vbuf->alloc(ctx, nreg * cap * 8 + 64) != QEH_OK) return false;
+    if (cbuf->alloc(ctx, nreg * 4 + 64) != QEH_OK) return false;
+    *rg = SliceRegions{};
+    rg->key = kbuf->as<uint16_t>();
+    rg->val = nacol ? vbuf->as<int64_t>() : nullptr;
+    rg->count = cbuf->as<uint32_t>();
+    rg->overflow = rg->count + nreg;
+    rg->cap = cap;
+    rg->F = (int32_t)F;
+    return hipMemsetAsync(rg->overflow, 0, 4, stream) == hipSuccess;
+}
+
+static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol, int64_t kmin,
+                                   uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg, hipStream_t stream) {
+    const bool nt = fast_nt_mode() == 1;
+    KernelTimer kta(ctx, "slice_partition", stream);
+#define QEH_SA(NTV, NAV, NTB)                                                                                  \
+    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in, \
+                       pp.terms, kmin, range, n_tiles, rg)
+#define QEH_SA_NA(NTV, NTB)                    \
+    if (nacol == 0) QEH_SA(NTV, 0, NTB);       \
+    else QEH_SA(NTV, 1, NTB);
+#define QEH_SA_NT(NTB)                         \
+    if (nterms == 0) { QEH_SA_NA(0, NTB) }     \
+    else if (nterms == 1) { QEH_SA_NA(1, NTB) } \
+    else { QEH_SA_NA(2, NTB) }
+    if (nt) { QEH_SA_NT(true) } else { QEH_SA_NT(false) }
+#undef QEH_SA_NT
+#undef QEH_SA_NA
+#undef QEH_SA
+}
+
+// Launch phase A ahead of the build when the slice path is predictable from the build key's
+// range alone (and the group count is known to stay small).  Not launching is never an error.
+static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
+                           int key_col, const qeh_column &build_key, int64_t g_bound, SlicePre *pre) {
+    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP")) return QEH_OK;
+    if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
+    if (g_bound <= 0 || g_bound >= 0xFFFF || (int64_t)specs.n_slots * g_bound > kSliceStateWords) return QEH_OK;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 1) return QEH_OK;
+    const int64_t n_tiles = n / kSliceTile;
+    if (n_tiles == 0) return QEH_OK;
+    int64_t mn, mx, cnt;
+    QEH_TRY(column_minmax(ctx, build_key, &mn, &mx, &cnt));
+    if (cnt == 0) return QEH_OK;
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1ull;
+    // the DIRECT rule of build_join_table, and the slice path's own limits
+    if (range == 0 || range > 4 * (uint64_t)cnt + 1024 || range >= (1ull << 32)) return QEH_OK;
+    uint64_t min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
+    if (range * 2 < min_bytes) return QEH_OK;
+    const uint64_t F = (range + kSliceKeys - 1) >> kSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return QEH_OK;
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    hipStream_t side = aux_stream(ctx);
+    if (!side) return QEH_OK;
+    if (!slice_regions(ctx, n_tiles, grid, F, nacol, &pre->kbuf, &pre->vbuf, &pre->cbuf, &pre->rg, ctx->stream))
+        return QEH_OK;
+    hipEvent_t ready;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) return QEH_OK;
+    if (hipEventCreateWithFlags(&pre->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipEventDestroy(ready);
+        pre->done = nullptr;
+        return QEH_OK;
+    }
+    (void)hipEventRecord(ready, ctx->stream);  // inputs and the region buffers' reset are on the main queue
+    (void)hipStreamWaitEvent(side, ready, 0);
+    launch_slice_partition(ctx, in, pp, nterms, nacol, mn, range, n_tiles, grid, pre->rg, side);
+    (void)hipEventRecord(pre->done, side);
+    (void)hipEventDestroy(ready);
+    if (hipGetLastError() != hipSuccess) return fail(QEH_E_HIP, "slice prelaunch failed");
+    pre->launched = true;
+    pre->kmin = mn;
+    pre->range = range;
+    pre->grid = grid;
+    pre->n_tiles = n_tiles;
+    return QEH_OK;
+}
+
 // LDS-slice partitioned probe (k_slice_partition + k_slice_probe) for unique
 // direct u16 tables past an XCD's L2.  Returns 1 when it ran; 0 when not
 // eligible, or when a region overflowed (probe keys skewed onto few slices),
 // in which case the states are re-initialised for the single pass.
 static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
-                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes) {
+                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes,
+                          SlicePre *pre) {
     if (std::getenv("QEH_NO_SLICES")) return 0;
     FastIn in;
     int nterms, nacol;
@@ -1326,40 +1438,15 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return 0;
     const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
-    // capacity for every row selected with keys uniform over the slices, +25 %
-    const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
-    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
-    cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
-    const uint64_t nreg = (uint64_t)grid * F;
     DevBuf kbuf, vbuf, cbuf;
-    if (kbuf.alloc(ctx, nreg * cap * 2 + 64) != QEH_OK) return 0;
-    if (nacol && vbuf.alloc(ctx, nreg * cap * 8 + 64) != QEH_OK) return 0;
-    if (cbuf.alloc(ctx, nreg * 4 + 64) != QEH_OK) return 0;
     SliceRegions rg{};
-    rg.key = kbuf.as<uint16_t>();
-    rg.val = nacol ? vbuf.as<int64_t>() : nullptr;
-    rg.count = cbuf.as<uint32_t>();
-    rg.overflow = rg.count + nreg;
-    rg.cap = cap;
-    rg.F = (int32_t)F;
-    if (hipMemsetAsync(rg.overflow, 0, 4, ctx->stream) != hipSuccess) return 0;
-    const bool nt = fast_nt_mode() == 1;
-    {
-    KernelTimer kta(ctx, "slice_partition");
-#define QEH_SA(NTV, NAV, NTB)                                                                                  \
-    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
-                       pp.terms, t.kmin, t.range, n_tiles, rg)
-#define QEH_SA_NA(NTV, NTB)                    \
-    if (nacol == 0) QEH_SA(NTV, 0, NTB);       \
-    else QEH_SA(NTV, 1, NTB);
-#define QEH_SA_NT(NTB)                         \
-    if (nterms == 0) { QEH_SA_NA(0, NTB) }     \
-    else if (nterms == 1) { QEH_SA_NA(1, NTB) } \
-    else { QEH_SA_NA(2, NTB) }
-    if (nt) { QEH_SA_NT(true) } else { QEH_SA_NT(false) }
-#undef QEH_SA_NT
-#undef QEH_SA_NA
-#undef QEH_SA
+    if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->grid == grid &&
+        pre->n_tiles == n_tiles) {
+        rg = pre->rg;  // phase A already ran on the second queue, under the build
+        if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
+    } else {
+        if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
+        launch_slice_partition(ctx, in, pp, nterms, nacol, t.kmin, t.range, n_tiles, grid, rg, ctx->stream);
     }
     {
         KernelTimer ktb(ctx, "slice_probe");
@@ -1553,7 +1640,7 @@ constexpr int kRetryBigger = 100;  // internal: group table too small
 static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, const PredPlan &pp,
                           const GidSource &src, const AggSpecs &specs_in, int64_t G, const KeyCols &out_keys_src,
                           const int32_t *key_dtypes, const uint32_t *rep_row, bool drop_empty, const char *kname,
-                          qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups) {
+                          qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups, SlicePre *pre = nullptr) {
     DevBuf states, errw;
     const int64_t Gs = std::max<int64_t>(G, 1);
     AggSpecs specs = specs_in;
@@ -1576,7 +1663,7 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         if (gm == GM_ZERO) launch_agg_rows<GM_ZERO>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
         else if (gm == GM_JOIN) {
             if (lds && try_slice_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
-                                      lds_bytes) == 1) {
+                                      lds_bytes, pre) == 1) {
             } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
                                               lds_bytes, per_cu)))
                 launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
@@ -1916,6 +2003,17 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     if (probe_cols[probe_key_idx].dtype != QEH_DT_INT64 && probe_cols[probe_key_idx].dtype != QEH_DT_INT32)
         return fail(QEH_E_UNSUPPORTED, "hash join keys must be Int32/Int64 on the device");
 
+    // phase A of the slice path on the second queue, when its shape is known from the build key's
+    // range (and the group count is bounded by one integer group key's range)
+    SlicePre pre;
+    if (n_group_keys == 1 && (build_group_keys[0].dtype == QEH_DT_INT64 || build_group_keys[0].dtype == QEH_DT_INT32) &&
+        probe_key_idx < n_probe_cols) {
+        int64_t gmn, gmx, gcnt;
+        QEH_TRY(column_minmax(ctx, build_group_keys[0], &gmn, &gmx, &gcnt));
+        const uint64_t gr = gcnt ? (uint64_t)gmx - (uint64_t)gmn + 1ull : 0;
+        const int64_t g_bound = (gr == 0 || gr > (1ull << 20)) ? -1 : (int64_t)gr + 1;  // + the NULL group
+        QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, g_bound, &pre));
+    }
     // build side: dense group ids of the build rows, then the join table with gid payloads
     GroupTable gt;
     DevBuf slot_of_row;
@@ -1931,5 +2029,6 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     std::vector<int32_t> kd(n_group_keys);
     for (int i = 0; i < n_group_keys; ++i) kd[i] = build_group_keys[i].dtype;
     return aggregate_rows(ctx, GM_JOIN, cols, n, pp, src, specs, gt.groups, gt.keys, kd.data(),
-                          gt.rep_row.as<uint32_t>(), true, "join_filter_aggregate", out_keys, out_aggs, out_groups);
+                          gt.rep_row.as<uint32_t>(), true, "join_filter_aggregate", out_keys, out_aggs, out_groups,
+                          &pre);
 }

@@ -140,10 +140,14 @@ struct DevBuf {
 struct KernelTimer {
     qeh_ctx *ctx;
     const char *name;
+    hipStream_t stream;
     hipEvent_t a = nullptr, b = nullptr;
-    KernelTimer(qeh_ctx *c, const char *n);
+    KernelTimer(qeh_ctx *c, const char *n, hipStream_t s = nullptr);  // s: ctx->stream when null
     ~KernelTimer();
 };
+
+// The context's second queue (created on first use) for pipeline stages that overlap the main one.
+hipStream_t aux_stream(qeh_ctx *ctx);
 
 // Pinned staging for small D2H results.
 int read_small(qeh_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes);

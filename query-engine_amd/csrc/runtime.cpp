@@ -89,17 +89,22 @@ static hipEvent_t take_event(qeh_ctx *ctx) {
     return e;
 }
 
-KernelTimer::KernelTimer(qeh_ctx *c, const char *n) : ctx(c), name(n) {
+KernelTimer::KernelTimer(qeh_ctx *c, const char *n, hipStream_t s) : ctx(c), name(n), stream(s ? s : c->stream) {
     if (!ctx->timing) return;
     a = take_event(ctx);
     b = take_event(ctx);
-    hipEventRecord(a, ctx->stream);
+    hipEventRecord(a, stream);
 }
 
 KernelTimer::~KernelTimer() {
     if (!ctx->timing || !a) return;
-    hipEventRecord(b, ctx->stream);
+    hipEventRecord(b, stream);
     ctx->timing_pending.push_back({name, a, b});
+}
+
+hipStream_t aux_stream(qeh_ctx *ctx) {
+    if (!ctx->aux_stream) (void)hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking);
+    return ctx->aux_stream;
 }
 
 static void drain_timing(qeh_ctx *ctx) {
