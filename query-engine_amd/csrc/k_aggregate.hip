@@ -1369,18 +1369,25 @@ static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPla
 // Launch phase A ahead of the build when the slice path is predictable from the build key's
 // range alone (and the group count is known to stay small).  Not launching is never an error.
 static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
-                           int key_col, const qeh_column &build_key, int64_t g_bound, SlicePre *pre) {
+                           int key_col, const qeh_column &build_key, const qeh_column &group_key, SlicePre *pre) {
     if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP")) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
-    if (g_bound <= 0 || g_bound >= 0xFFFF || (int64_t)specs.n_slots * g_bound > kSliceStateWords) return QEH_OK;
+    if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
     FastIn in;
     int nterms, nacol;
     if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 1) return QEH_OK;
     const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return QEH_OK;
-    int64_t mn, mx, cnt;
-    QEH_TRY(column_minmax(ctx, build_key, &mn, &mx, &cnt));
+    // build key and group key ranges in one read; the group count is at most the group key's range
+    // (+ the NULL group)
+    const qeh_column both[2] = {build_key, group_key};
+    int64_t mns[2], mxs[2], cnts[2];
+    QEH_TRY(columns_minmax(ctx, both, 2, mns, mxs, cnts));
+    const int64_t mn = mns[0], mx = mxs[0], cnt = cnts[0];
     if (cnt == 0) return QEH_OK;
+    const uint64_t gr = cnts[1] ? (uint64_t)mxs[1] - (uint64_t)mns[1] + 1ull : 0;
+    const int64_t g_bound = (gr == 0 || gr > (1ull << 20)) ? -1 : (int64_t)gr + 1;
+    if (g_bound <= 0 || g_bound >= 0xFFFF || (int64_t)specs.n_slots * g_bound > kSliceStateWords) return QEH_OK;
     const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1ull;
     // the DIRECT rule of build_join_table, and the slice path's own limits
     if (range == 0 || range > 4 * (uint64_t)cnt + 1024 || range >= (1ull << 32)) return QEH_OK;
@@ -1438,11 +1445,15 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return 0;
     const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    bool tail_done = false;
     DevBuf kbuf, vbuf, cbuf;
     SliceRegions rg{};
     if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->grid == grid &&
         pre->n_tiles == n_tiles) {
         rg = pre->rg;  // phase A already ran on the second queue, under the build
+        // the ragged tail (rows past the last full tile) goes first: it overlaps phase A
+        launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+        tail_done = true;
         if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
     } else {
         if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
@@ -1461,7 +1472,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
                                specs, G, states);
     }
     if (hipGetLastError() != hipSuccess) return 0;
-    launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+    if (!tail_done) launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
     uint32_t of = 0;
     if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
     if (of) {
@@ -2006,14 +2017,7 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     // phase A of the slice path on the second queue, when its shape is known from the build key's
     // range (and the group count is bounded by one integer group key's range)
     SlicePre pre;
-    if (n_group_keys == 1 && (build_group_keys[0].dtype == QEH_DT_INT64 || build_group_keys[0].dtype == QEH_DT_INT32) &&
-        probe_key_idx < n_probe_cols) {
-        int64_t gmn, gmx, gcnt;
-        QEH_TRY(column_minmax(ctx, build_group_keys[0], &gmn, &gmx, &gcnt));
-        const uint64_t gr = gcnt ? (uint64_t)gmx - (uint64_t)gmn + 1ull : 0;
-        const int64_t g_bound = (gr == 0 || gr > (1ull << 20)) ? -1 : (int64_t)gr + 1;  // + the NULL group
-        QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, g_bound, &pre));
-    }
+    if (n_group_keys == 1) QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, build_group_keys[0], &pre));
     // build side: dense group ids of the build rows, then the join table with gid payloads
     GroupTable gt;
     DevBuf slot_of_row;

@@ -195,19 +195,29 @@ __global__ void k_wide_dups(ColRef key, int64_t n, HashTable t, uint32_t *dup) {
 }
 
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid) {
+    return columns_minmax(ctx, &col, 1, mn, mx, valid);
+}
+
+// several columns, one synchronous read for all of them
+int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int64_t *mx, int64_t *valid) {
+    if (n <= 0) return QEH_OK;
     DevBuf mm;
-    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) + 16));
-    const ColRef c = make_colref(col);
-    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
-    if (col.length > 0)
-        hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, col.length, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, c,
-                           col.length, mm.as<MinMax>());
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
+    for (int i = 0; i < n; ++i) {
+        const ColRef c = make_colref(cols[i]);
+        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>() + i);
+        if (cols[i].length > 0)
+            hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, cols[i].length, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream,
+                               c, cols[i].length, mm.as<MinMax>() + i);
+    }
     QEH_HIP(hipGetLastError());
-    MinMax hm{};
-    QEH_TRY(read_small(ctx, &hm, mm.p, sizeof(MinMax)));
-    *mn = hm.mn;
-    *mx = hm.mx;
-    *valid = (int64_t)hm.cnt;
+    std::vector<MinMax> hm((size_t)n);
+    QEH_TRY(read_small(ctx, hm.data(), mm.p, sizeof(MinMax) * (size_t)n));
+    for (int i = 0; i < n; ++i) {
+        mn[i] = hm[i].mn;
+        mx[i] = hm[i].mx;
+        valid[i] = (int64_t)hm[i].cnt;
+    }
     return QEH_OK;
 }
 

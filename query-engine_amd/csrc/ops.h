@@ -35,6 +35,8 @@ struct RowPayload {
 };
 // min / max / valid count of an integer column (one synchronous read).
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid);
+// min / max / valid count of several integer columns, one synchronous read.
+int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int64_t *mx, int64_t *valid);
 // LDS-slice materialising INNER join of one probe payload and one Int64 build
 // payload (k_aggregate.hip); kSliceJoinNotEligible when the shapes do not fit.
 constexpr int kSliceJoinNotEligible = -1;
