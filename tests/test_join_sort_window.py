@@ -63,12 +63,13 @@ def test_join_table_layouts(ctx, monkeypatch, table):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_probe,n_build,key0,arange", [(1_000_003, 300_000, 0, 1000), (500_000, 200_001, -77_777, 60_000),
-                                                         (300_000, 100_000, 5, 70_000)])
+                                                         (300_000, 100_000, 5, 70_000),
+                                                         (700_001, 250_000, 1 << 40, 1 << 50)])  # wide: fused join
 def test_join_slice_path(ctx, monkeypatch, n_probe, n_build, key0, arange):
     """The LDS-slice materialising join (config 3 shape: one probe payload, one
-    Int64 build payload stored as a u16 frame of reference), forced on small
-    tables; misses below and above the key range; ragged tail; a payload range
-    past 16 bits falls back to the ordered fused join.  Multiset compare."""
+    Int64 build payload), forced on small tables; misses below and above the key
+    range; ragged tail.  Payloads within 16 bits ride in the u16 table as a frame
+    of reference; wider ones fall back to the ordered fused join.  Multiset compare."""
     monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
     r = np.random.default_rng(n_build)
     bk = r.permutation(n_build).astype(np.int64) + key0

@@ -116,6 +116,26 @@ def cfg3(ctx, scale):
          {"output_rows": rows, "build_ms": kt["join_build"]})
 
 
+def cfg3_wide(ctx, scale):
+    """cfg3 with a full-range Int64 build payload: the u16 frame-of-reference of the slice path
+    does not apply, so the fused embedded-record join (k_join_mat) runs."""
+    n, nd = int(1e9 * scale), 10_000_000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    fv = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1 << 62)
+
+    def fn():
+        p, b, rows = ctx.hash_join_inner(fk, [fv], dk, [da])
+        for c in p + b:
+            c.release()
+        return rows
+    wall, kt, rows = timed(ctx, fn, 3, ["join_probe", "join_gather", "join_build", "join_mat"])
+    line("cfg3 inner join 1e9 x 1e7, full-range Int64 payload", n, wall, 32.0 * n, wall * 1e3,
+         "k_join_mat (embedded build records)", None, {"output_rows": rows, "kernel_split_ms": kt,
+                                                         "note": "kernel_ms = wall: the path has no single timer"})
+
+
 def cfg5(ctx, scale):
     n = int(1e9 * scale)
     k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 20)
@@ -353,7 +373,7 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition, "cfg3w": cfg3_wide}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
