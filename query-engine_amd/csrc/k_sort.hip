@@ -819,6 +819,30 @@ __global__ void k_rn_scatter_windows(const uint32_t *__restrict__ dst, const uin
         out[dst[i]] = (int64_t)val[i];
 }
 
+// start of every window in the window-grouped pairs (empty windows start where the next begins)
+__global__ void k_rn_window_starts(const uint32_t *__restrict__ dst, int64_t n, int shift, int64_t nwin,
+                                   int64_t *__restrict__ start) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w = i < n ? (int64_t)(dst[i] >> shift) : nwin;
+        const int64_t wp = i > 0 ? (int64_t)(dst[i - 1] >> shift) : -1;
+        for (int64_t q = wp + 1; q <= w; ++q) start[q] = i;  // windows (wp, w] begin at i
+    }
+}
+
+// XCD-local windows: workgroup b runs on XCD b % 8 (round-robin dispatch), and the workgroups of
+// one XCD walk that XCD's windows (w = xcd, xcd + 8, ...) together, so a window's output lines
+// (2 MB) are completed inside one L2 before they are written back
+__global__ void k_rn_scatter_xcd(const uint32_t *__restrict__ dst, const uint32_t *__restrict__ val,
+                                 const int64_t *__restrict__ start, int64_t nwin, int64_t *__restrict__ out) {
+    constexpr int kXcd = 8;
+    const int xcd = blockIdx.x % kXcd;
+    const int64_t per = gridDim.x / kXcd, me = blockIdx.x / kXcd;
+    for (int64_t w = xcd; w < nwin; w += kXcd) {
+        const int64_t a = start[w], b = start[w + 1];
+        for (int64_t i = a + me * blockDim.x + threadIdx.x; i < b; i += per * blockDim.x) out[dst[i]] = (int64_t)val[i];
+    }
+}
+
 // ---- hash partition ---------------------------------------------------------------------------
 __global__ void k_partition_ids(ColRef key, int64_t n, uint32_t parts, uint64_t *__restrict__ keys,
                                 uint32_t *__restrict__ idx) {
@@ -1062,10 +1086,11 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
         hipLaunchKernelGGL(k_rn_prefix_max, dim3(1), dim3(1024), 0, ctx->stream, seg.as<int64_t>(), nchunks);
     }
     const int dbits = bit_length((uint64_t)(n - 1));
-    // Direct scatter by default: grouping the (destination, rn) pairs into 32 MB output windows
-    // first (one radix pass on the destination's top bits) measured slower at 1e9 rows (61 vs
-    // 40 ms: the windows' partial-line writes from all XCDs still reach HBM); kept behind
-    // QEH_RN_WINDOWED for experiments.
+    // Direct scatter by default.  QEH_RN_WINDOWED (experiment, slower): group the (destination,
+    // rn) pairs into 2 MB output windows with two radix passes and scatter window by window with
+    // the workgroups of one XCD per window — 138 vs 104 ms for cfg 5 (the passes cost 23 ms and
+    // the windowed scatter did not beat the direct one; with one pass and 32 MB windows: 61 vs
+    // 40 ms for the row-number stage).
     if (dbits <= 22 || !std::getenv("QEH_RN_WINDOWED")) {
         KernelTimer kt(ctx, "row_number");
         hipLaunchKernelGGL(k_rn_write<false>, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags.as<uint32_t>(),
@@ -1082,14 +1107,23 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
         }
         rs.cur = o;
         rs.key32 = true;
-        s = radix_pass_at<uint32_t>(ctx, rs, dbits - kRadixBits);
+        // 2 MB output windows (2^18 rows): two stable passes on destination bits [dbits-12, dbits)
+        const int wshift = dbits - 12;
+        s = radix_pass_at<uint32_t>(ctx, rs, wshift);
+        if (s == QEH_OK) s = radix_pass_at<uint32_t>(ctx, rs, wshift + 8);
+        DevBuf starts;
+        const int64_t nwin = (int64_t)(((uint64_t)(n - 1) >> wshift) + 1);
+        if (s == QEH_OK) s = starts.alloc(ctx, (size_t)(nwin + 1) * 8);
         if (s != QEH_OK) {
             qeh_column_release(ctx, out_rn);
             return s;
         }
         KernelTimer kt(ctx, "row_number");
-        hipLaunchKernelGGL(k_rn_scatter_windows, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
-                           rs.k[rs.cur].as<uint32_t>(), rs.v[rs.cur].as<uint32_t>(), n, (int64_t *)out_rn->values);
+        hipLaunchKernelGGL(k_rn_window_starts, dim3(grid_for(ctx, n + 1, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream,
+                           rs.k[rs.cur].as<uint32_t>(), n, wshift, nwin, starts.as<int64_t>());
+        const int gx = (int)std::max<int64_t>(8, ctx->props.multiProcessorCount * 4 / 8 * 8);
+        hipLaunchKernelGGL(k_rn_scatter_xcd, dim3(gx), dim3(kBlock), 0, ctx->stream, rs.k[rs.cur].as<uint32_t>(),
+                           rs.v[rs.cur].as<uint32_t>(), starts.as<int64_t>(), nwin, (int64_t *)out_rn->values);
     }
     QEH_HIP(hipGetLastError());
     QEH_HIP(hipStreamSynchronize(ctx->stream));
