@@ -101,11 +101,15 @@ enum qeh_unop { QEH_UOP_NOT = 0, QEH_UOP_MINUS = 1 };
 typedef struct qeh_expr_node {
     int32_t kind;        /* enum qeh_expr_kind                              */
     int32_t op;          /* qeh_binop / qeh_unop                            */
-    int32_t index;       /* COLUMN: input column index                      */
+    int32_t index;       /* COLUMN: input column index; UTF8 LITERAL: byte length */
     int32_t lit_dtype;   /* LITERAL: enum qeh_dtype (NULL = ScalarValue::Null) */
     int32_t lit_is_null; /* LITERAL: typed None (e.g. Int64(None))         */
     int32_t _pad;
-    int64_t lit_i64;     /* BOOL/INT32/INT64 literal                        */
+    int64_t lit_i64;     /* BOOL/INT32/INT64 literal; UTF8 LITERAL: host address of
+                            its bytes (read during the call only).  Utf8 operands
+                            appear only in comparisons of two leaves (column /
+                            literal), evaluated by byte-wise lexicographic order,
+                            operators.rs:509-538 on StringArray             */
     double lit_f64;      /* FLOAT32/FLOAT64 literal                         */
 } qeh_expr_node;
 

@@ -382,6 +382,16 @@ static int filter_impl(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const q
     if (!ctx || !out_rows || (n_out > 0 && (!out || !out_idx))) return fail(QEH_E_INVALID, "qeh_filter: bad argument");
     *out_rows = 0;
     DeviceGuard dg(ctx->device);
+    for (int j = 0; j < n_out; ++j)
+        if (out_idx[j] < 0 || out_idx[j] >= n_cols) return fail(QEH_E_INVALID, "filter output column index out of range");
+    // Utf8 comparisons become BOOL columns appended after the inputs (k_utf8.hip)
+    Utf8Rewrite uw;
+    QEH_TRY(rewrite_utf8_compares(ctx, cols, n_cols, predicate, &uw));
+    if (uw.changed) {
+        cols = uw.cols.data();
+        n_cols = (int)uw.cols.size();
+        predicate = &uw.expr;
+    }
     ColSet cs;
     QEH_TRY(make_colset(cols, n_cols, &cs));
     const int64_t n = n_cols > 0 ? cols[0].length : 0;
@@ -568,7 +578,20 @@ extern "C" int qeh_eval(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const 
     DeviceGuard dg(ctx->device);
     for (int i = 0; i < n_cols; ++i)
         if (cols[i].length != n_rows) return fail(QEH_E_INVALID, "eval columns have different lengths");
+    Utf8Rewrite uw;  // Utf8 comparisons become BOOL columns appended after the inputs (k_utf8.hip)
+    QEH_TRY(rewrite_utf8_compares(ctx, cols, n_cols, expr, &uw));
+    const int n_in = n_cols;
+    if (uw.changed) {
+        cols = uw.cols.data();
+        n_cols = (int)uw.cols.size();
+        expr = &uw.expr;
+    }
     const int ci = expr_as_column(expr);
+    if (ci >= n_in) {  // the whole expression was one Utf8 comparison: hand its column over
+        *out = cols[ci];
+        uw.temps.erase(uw.temps.begin() + (ci - n_in));
+        return QEH_OK;
+    }
     if (ci >= 0) {  // zero-copy column reference (operators.rs:15-23)
         if (ci >= n_cols) return fail(QEH_E_INVALID, "Column index " + std::to_string(ci) + " out of bounds");
         *out = cols[ci];

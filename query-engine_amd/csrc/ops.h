@@ -1,6 +1,9 @@
 // Host-side helpers shared between operator translation units.
 #pragma once
 
+#include <memory>
+#include <vector>
+
 #include "expr.h"
 #include "grouptable.h"
 #include "hashtable.h"
@@ -82,6 +85,25 @@ int gather_column(qeh_ctx *ctx, const qeh_column &src, const uint32_t *idx, int6
 // Concatenate parts (same dtype) into one owned column with offset 0 (k_merge.hip); one part =
 // a normalising copy.
 int concat_columns(qeh_ctx *ctx, const qeh_column *const *parts, int n_parts, qeh_column *out);
+
+// Utf8 comparisons (k_utf8.hip): every comparison of two leaves with a Utf8 side is evaluated into
+// a temporary BOOL column appended to `cols`, and the expression rewritten to read it.  Owns the
+// temporaries; `changed` false means expr/cols are the inputs unchanged.
+struct Utf8Rewrite {
+    qeh_ctx *ctx = nullptr;
+    std::vector<qeh_column> cols;
+    std::vector<qeh_expr_node> nodes;
+    qeh_expr expr{};
+    std::vector<qeh_column> temps;
+    std::vector<std::unique_ptr<DevBuf>> bufs;
+    bool changed = false;
+    Utf8Rewrite() = default;
+    Utf8Rewrite(const Utf8Rewrite &) = delete;
+    Utf8Rewrite &operator=(const Utf8Rewrite &) = delete;
+    ~Utf8Rewrite();
+};
+int rewrite_utf8_compares(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *e, Utf8Rewrite *out);
+bool expr_has_utf8(const qeh_expr *e, const int32_t *dtypes, int n_cols);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);

@@ -204,7 +204,7 @@ class Context:
         n = len(strs)
         if valid is None:
             valid = np.array([x is not None for x in strs], bool)
-        enc = [(x or "").encode() if v else b"" for x, v in zip(strs, valid)]
+        enc = [(x if isinstance(x, bytes) else (x or "").encode()) if v else b"" for x, v in zip(strs, valid)]
         offs = np.zeros(n + 1, np.int32)
         offs[1:] = np.cumsum([len(b) for b in enc]) if n else []
         data = np.frombuffer(b"".join(enc), np.uint8) if offs[-1] else np.zeros(8, np.uint8)

@@ -72,7 +72,8 @@ class PhysicalExpr:
         nodes = self.postfix()
         arr = (abi.QehExprNode * len(nodes))(*nodes)
         e = abi.QehExpr(C.cast(arr, C.POINTER(abi.QehExprNode)), len(nodes))
-        return e, arr
+        # Utf8 literal bytes are referenced by address (index = length, lit_i64 = pointer)
+        return e, (arr, [n._utf8 for n in nodes if hasattr(n, "_utf8")])
 
     # operator sugar so tests read naturally
     def __and__(self, o): return BinaryExpr(self, BinaryOp.And, o)
@@ -100,7 +101,11 @@ class Literal(PhysicalExpr):
         elif v.dtype in (abi.DT_FLOAT32, abi.DT_FLOAT64):
             n.lit_f64 = float(v.value)
         elif v.dtype == abi.DT_UTF8:
-            raise NotImplementedError("Utf8 literals are not representable in qeh_expr")
+            b = v.value.encode() if isinstance(v.value, str) else bytes(v.value)
+            buf = C.create_string_buffer(b, max(len(b), 1))
+            n.index = len(b)
+            n.lit_i64 = C.addressof(buf)
+            n._utf8 = buf
         else:
             n.lit_i64 = int(v.value)
         out.append(n)
@@ -149,6 +154,8 @@ def lit(v) -> Literal:
         return Literal(ScalarValue.Int64(v))
     if isinstance(v, float):
         return Literal(ScalarValue.Float64(v))
+    if isinstance(v, (str, bytes)):  # string literals -> Utf8
+        return Literal(ScalarValue.Utf8(v))
     if isinstance(v, ScalarValue):
         return Literal(v)
     raise TypeError(v)
