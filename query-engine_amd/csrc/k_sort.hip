@@ -164,6 +164,43 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__
     if (threadIdx.x < kRadix) hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
+// Histogram of a pass whose digits the previous scatter wrote as a byte stream
+// (nd_out): 1 B per element instead of the 8-B key, 16 digits per 16-B load,
+// per-wave LDS counters (no cross-wave atomics on hot digits).
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist_u8(const uint8_t *__restrict__ dg, int64_t n, int64_t seg,
+                                                           uint32_t *__restrict__ hist, int nblocks) {
+    constexpr int W = kRsThreads / 64;
+    __shared__ uint32_t h[W][kRadix];
+    for (int i = threadIdx.x; i < W * kRadix; i += kRsThreads) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    // segments start at multiples of seg; the 16-B body is [a, b), head/tail bytewise
+    const int64_t a = (lo + 15) & ~(int64_t)15, b = hi & ~(int64_t)15;
+    if (a < b) {
+        for (int64_t i = a + 16 * (int64_t)threadIdx.x; i < b; i += 16 * (int64_t)kRsThreads) {
+            typedef unsigned int v4u32s __attribute__((ext_vector_type(4)));
+            const v4u32s w = __builtin_nontemporal_load((const v4u32s *)(dg + i));
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) atomicAdd(&h[wave][(ws[q] >> (8 * r)) & 0xff], 1u);
+        }
+        for (int64_t i = lo + threadIdx.x; i < a; i += kRsThreads) atomicAdd(&h[wave][dg[i]], 1u);
+        for (int64_t i = b + threadIdx.x; i < hi; i += kRsThreads) atomicAdd(&h[wave][dg[i]], 1u);
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += kRsThreads) atomicAdd(&h[wave][dg[i]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kRadix) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) c += h[w][threadIdx.x];
+        hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = c;
+    }
+}
+
 // Stable scatter, one 1024-thread workgroup per CU: rank each 8192-element
 // tile by digit (ballot peers + per-wave counters), reorder it in LDS, then
 // write every digit's run (≈ 32 elements = whole 128-byte lines) contiguously.
@@ -180,7 +217,8 @@ template <typename KeyT>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                            int nblocks, KeyT *__restrict__ keys_out,
-                                                           uint32_t *__restrict__ vals_out) {
+                                                           uint32_t *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
+                                                           int nshift) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
     __shared__ KeyT s_keys[kRsSTile];
@@ -266,6 +304,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
             const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
             keys_out[pos] = key;
             vals_out[pos] = s_vals[p];
+            if (nd_out) nd_out[pos] = (uint8_t)(key >> nshift);  // the next pass's digit (its histogram input)
         }
         lds_barrier();
         if (t < kRadix) run[t] += tot_s[t];
@@ -390,19 +429,28 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
     // one long-lived scatter workgroup per CU (see k_rs_scatter); hist uses the same segments
     const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)ctx->props.multiProcessorCount);
     const int64_t seg = (n + nblocks - 1) / nblocks;
-    DevBuf hist, offs;
+    DevBuf hist, offs, nd;
     QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
     QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    // every scatter but the last also writes the next pass's digit as one byte per element, so
+    // that pass's histogram reads 1 B instead of the key (sizeof(KeyT) B)
+    const bool multi = bits > kRadixBits && n >= (int64_t)kRsSTile;
+    if (multi) QEH_TRY(nd.alloc(ctx, (size_t)n));
     for (int shift = 0; shift < bits; shift += kRadixBits) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = rs.cur;
-        hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
-                           hist.as<uint32_t>(), nblocks);
+        if (multi && shift > 0)
+            hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, nd.as<uint8_t>(), n, seg,
+                               hist.as<uint32_t>(), nblocks);
+        else
+            hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg,
+                               shift, hist.as<uint32_t>(), nblocks);
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        const bool next = multi && shift + kRadixBits < bits;
         hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
                            rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
-                           rs.v[1 - c].as<uint32_t>());
+                           rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr, shift + kRadixBits);
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
@@ -427,7 +475,7 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
     hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
                        rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
-                       rs.v[1 - c].as<uint32_t>());
+                       rs.v[1 - c].as<uint32_t>(), nullptr, 0);
     QEH_HIP(hipGetLastError());
     rs.cur = 1 - c;
     return QEH_OK;
