@@ -363,14 +363,19 @@ struct SliceRegions {
     uint64_t cap;         // items per region, multiple of kSliceChunk
     int32_t F;            // slices
     int32_t _pad;
+    // exact layout (materialising join): region (workgroup r, slice b) starts at
+    // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
+    const uint64_t *rbase;
 };
+
 
 template <int NTERMS, int NACOL, bool NT>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
                                                                  int64_t n_tiles, SliceRegions rg) {
     constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
     constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
-    __shared__ uint32_t cnt[MAXF], lofs[MAXF], cn[MAXF], pos[MAXF], mpre[MAXF];
+    __shared__ uint32_t cnt[MAXF], lofs[MAXF], cn[MAXF], pos[MAXF], mpre[MAXF], hd[MAXF];
+    __shared__ uint64_t abase[MAXF];  // region start, aligned down to a whole chunk (exact layout)
     __shared__ uint32_t s_chunks;
     __shared__ uint16_t chunk_slice[TILE / CH + MAXF];
     __shared__ uint16_t st_key[TILE];
@@ -380,9 +385,20 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     const int F = rg.F;
     const uint64_t cap = rg.cap;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < MAXF; i += kSliceBlock) cnt[i] = 0, cn[i] = 0, pos[i] = 0;
-    __syncthreads();
     const uint64_t region0 = (uint64_t)blockIdx.x * F;
+    for (int i = tid; i < MAXF; i += kSliceBlock) {
+        cnt[i] = 0, pos[i] = 0, hd[i] = 0, abase[i] = 0;
+        if (i < F) {
+            // exact layout: regions start anywhere; chunks stay aligned to absolute multiples
+            // of CH items by starting each region h = start % CH placeholder items early (never
+            // written) -- whole 64-B key / 256-B value chunks, as with the capacity layout
+            const uint64_t st = rg.rbase ? rg.rbase[(uint64_t)i * gridDim.x + blockIdx.x] : (region0 + i) * cap;
+            hd[i] = (uint32_t)(st % CH);
+            abase[i] = st - hd[i];
+        }
+        cn[i] = hd[i];
+    }
+    __syncthreads();
     bool ovf = false;
     FastTile<NTERMS, NACOL, NT> ft;
     int64_t tile = blockIdx.x;
@@ -461,8 +477,10 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                     if (VC) vv = st_v[lofs[b] + kx - cb];
                 }
                 const uint64_t dst = (uint64_t)pos[b] + kx;
-                if (dst < cap) {
-                    const uint64_t o = (region0 + b) * cap + dst;
+                if (dst < hd[b]) {
+                    // placeholder ahead of the region's first item
+                } else if (dst < cap) {
+                    const uint64_t o = abase[b] + dst;
                     rg.key[o] = kv;
                     if (VC) __builtin_nontemporal_store(vv, rg.val + o);
                 } else {
@@ -498,8 +516,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         const int b = p / CH, kx = p % CH;
         if (kx >= (int)cn[b]) continue;
         const uint64_t dst = (uint64_t)pos[b] + kx;
+        if (dst < hd[b]) continue;
         if (dst < cap) {
-            const uint64_t o = (region0 + b) * cap + dst;
+            const uint64_t o = abase[b] + dst;
             rg.key[o] = c_key[b * CH + kx];
             if (VC) rg.val[o] = c_v[b * CH + kx];
         } else {
@@ -509,7 +528,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     if (ovf) *rg.overflow = 1u;
     for (int b = tid; b < F; b += kSliceBlock) {
         const uint64_t n = (uint64_t)pos[b] + cn[b];
-        rg.count[region0 + b] = (uint32_t)(n < cap ? n : cap);
+        rg.count[region0 + b] = (uint32_t)((n < cap ? n : cap) - hd[b]);
     }
 }
 
@@ -696,8 +715,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_join_b(SliceRegions rg, i
         for (int64_t s = sb + wave; s < se; s += W) {
             const uint64_t reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
             const uint32_t n_r = rg.count[reg];
-            const uint16_t *kp = rg.key + reg * rg.cap;
-            const int64_t *vp = rg.val + reg * rg.cap;
+            const uint64_t rb = rg.rbase ? rg.rbase[s] : reg * rg.cap;
+            const uint16_t *kp = rg.key + rb;
+            const int64_t *vp = rg.val + rb;
             uint64_t base = EMIT ? bases[s] : 0;
             uint32_t matches = 0;
             for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
@@ -725,6 +745,100 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_join_b(SliceRegions rg, i
         }
         sb = se;
     }
+}
+
+// Exact region sizes for phase A of the materialising join: the same tile ->
+// workgroup assignment as k_slice_partition, keys only (16-B loads), per-wave
+// LDS counters; counts[b * grid + wg] (slice-major slots).
+__global__ __launch_bounds__(kSliceBlock) void k_slice_count(const int64_t *__restrict__ key, int64_t kmin, uint64_t range,
+                                                             int64_t n_tiles, int F, uint32_t *__restrict__ counts) {
+    constexpr int W = kSliceBlock / 64;
+    __shared__ uint32_t cnt[W][kSliceMaxF];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    for (int i = tid; i < W * kSliceMaxF; i += kSliceBlock) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t base = tile * kSliceTile;
+        v2i64 kk[kSliceTile / (2 * kSliceBlock)];
+#pragma unroll
+        for (int q = 0; q < kSliceTile / (2 * kSliceBlock); ++q)
+            kk[q] = __builtin_nontemporal_load((const v2i64 *)(key + base + 2 * ((int64_t)q * kSliceBlock + tid)));
+#pragma unroll
+        for (int q = 0; q < kSliceTile / (2 * kSliceBlock); ++q)
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const uint64_t o = (uint64_t)kk[q][x] - (uint64_t)kmin;
+                if (o < range) atomicAdd(&cnt[wave][(uint32_t)(o >> kSliceBits)], 1u);
+            }
+    }
+    __syncthreads();
+    for (int b = tid; b < F; b += kSliceBlock) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) c += cnt[w][b];
+        counts[(uint64_t)b * gridDim.x + blockIdx.x] = c;
+    }
+}
+
+// Phase B of the exact-layout join: the probe payload already sits at its
+// output position (phase A wrote it into the output column), so each item only
+// needs the build payload written beside it: read the 16-bit key offset, look
+// it up in the LDS slice, store a.  Items without a match are counted (a
+// non-zero count sends the host to the compacting two-pass emit).
+__global__ __launch_bounds__(kSliceBlock) void k_slice_join_inplace(SliceRegions rg, int nreg, HashTable t, int64_t amin,
+                                                                    int64_t *__restrict__ out_a,
+                                                                    unsigned long long *__restrict__ misses) {
+    __shared__ __attribute__((aligned(16))) uint16_t tslice[kSliceKeys];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int W = kSliceBlock / 64;
+    const int F = rg.F;
+    const int64_t T = (int64_t)F * nreg;
+    const int64_t s0 = (int64_t)blockIdx.x * T / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+    uint32_t miss = 0;
+    for (int64_t sb = s0; sb < s1;) {
+        const int b = (int)(sb / nreg);
+        const int64_t se = std::min<int64_t>(s1, (int64_t)(b + 1) * nreg);
+        __syncthreads();
+        load_slice(tslice, t, b, tid);
+        __syncthreads();
+        for (int64_t s = sb + wave; s < se; s += W) {
+            const uint64_t reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
+            const uint32_t n_r = rg.count[reg];
+            const uint64_t rb = rg.rbase[s];
+            const uint16_t *kp = rg.key + rb;
+            int64_t *ap = out_a + rb;
+            // the next 1024 keys are loaded before this batch's lookups and stores
+            uint32_t e[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t i = j * 64 + lane;
+                e[j] = __builtin_nontemporal_load(kp + (i < n_r ? i : 0u));
+            }
+            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 16) {
+                uint32_t en[16];
+                const uint32_t i1 = i0 + 64 * 16;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t i = i1 + j * 64 + lane;
+                    en[j] = __builtin_nontemporal_load(kp + (i < n_r ? i : 0u));
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t i = i0 + j * 64 + lane;
+                    if (i < n_r) {
+                        const uint32_t x = tslice[e[j]];
+                        miss += x == 0u;
+                        __builtin_nontemporal_store((int64_t)(x - 1u) + amin, ap + i);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) e[j] = en[j];
+            }
+        }
+        sb = se;
+    }
+    const uint64_t m = wave_sum_u64(miss);
+    if (lane == 0 && m) atomicAdd(misses, (unsigned long long)m);
 }
 
 // ragged tail (< one 8192-row tile): probe the u16 table directly and append
@@ -1511,45 +1625,53 @@ int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_
     if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
     if (table_bytes(t) < min_bytes) return kSliceJoinNotEligible;
 
+    // Exact region layout: a key-only count pass sizes every (workgroup, slice) region, so
+    // phase A writes the probe payload straight into the output column (slice-major, no
+    // gaps) and phase B only adds the build payload beside it.  When some probe rows have
+    // no match, the two-pass emit compacts the regions into fresh columns instead.
     const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
-    const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
-    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
-    cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
     const uint64_t nreg = (uint64_t)grid * F;
-    DevBuf kbuf, vbuf, cbuf;
-    QEH_TRY(kbuf.alloc(ctx, nreg * cap * 2 + 64));
-    QEH_TRY(vbuf.alloc(ctx, nreg * cap * 8 + 64));
+    const uint64_t T = nreg;  // region slots, slice-major
+    DevBuf kbuf, cbuf, counts, bases;
     QEH_TRY(cbuf.alloc(ctx, nreg * 4 + 64));
+    QEH_TRY(counts.alloc(ctx, T * 4 + 16));
+    QEH_TRY(bases.alloc(ctx, T * 8 + 16));
+    FastIn in{};
+    in.key = (const int64_t *)pk.values;
+    in.acol[0] = (const int64_t *)pv.values;
+    in.agg_colslot[0] = 0;
+    uint64_t region_rows = 0;
+    {
+        KernelTimer kt(ctx, "join_probe");
+        hipLaunchKernelGGL(k_slice_count, dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in.key, t.kmin, t.range, n_tiles,
+                           (int)F, counts.as<uint32_t>());
+        QEH_HIP(hipGetLastError());
+    }
+    QEH_TRY(exclusive_scan_u32(ctx, counts.as<uint32_t>(), bases.as<uint64_t>(), (int64_t)T, &region_rows));
+    QEH_TRY(kbuf.alloc(ctx, region_rows * 2 + 64));
     SliceRegions rg{};
     rg.key = kbuf.as<uint16_t>();
-    rg.val = vbuf.as<int64_t>();
     rg.count = cbuf.as<uint32_t>();
-    rg.overflow = rg.count + nreg;                                         // 4 B
+    rg.overflow = rg.count + nreg;                                                                     // 4 B
     unsigned long long *counter = (unsigned long long *)(cbuf.as<char>() + ((nreg * 4 + 15) & ~15ull));  // 8 B
-    rg.cap = cap;
+    unsigned long long *misses = counter + 1;                                                          // 8 B
+    rg.cap = 1ull << 62;  // exact regions never overflow
     rg.F = (int32_t)F;
+    rg.rbase = bases.as<uint64_t>();
     QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
-    QEH_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
+    QEH_HIP(hipMemsetAsync(counter, 0, 16, ctx->stream));
     QEH_TRY(alloc_column(ctx, probe_val.dtype, n, false, out_probe));
     int st = alloc_column(ctx, QEH_DT_INT64, n, false, out_build);
     if (st != QEH_OK) {
         qeh_column_release(ctx, out_probe);
         return st;
     }
-    FastIn in{};
-    in.key = (const int64_t *)pk.values;
-    in.acol[0] = (const int64_t *)pv.values;
-    in.agg_colslot[0] = 0;
+    rg.val = (int64_t *)out_probe->values;
     PredTerms none{};
     const bool nt = fast_nt_mode() == 1;
-    int64_t *ov = (int64_t *)out_probe->values, *oa = (int64_t *)out_build->values;
-    const uint64_t T = nreg;  // region slots, slice-major
-    DevBuf counts, bases;
-    if (st == QEH_OK) st = counts.alloc(ctx, T * 4 + 16);
-    if (st == QEH_OK) st = bases.alloc(ctx, T * 8 + 16);
-    uint64_t region_rows = 0;
+    int64_t *oa = (int64_t *)out_build->values;
     const int gridB = ctx->props.multiProcessorCount;
-    if (st == QEH_OK) {
+    {
         KernelTimer kt(ctx, "join_probe");
         if (nt)
             hipLaunchKernelGGL((k_slice_partition<0, 1, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
@@ -1557,34 +1679,65 @@ int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_
         else
             hipLaunchKernelGGL((k_slice_partition<0, 1, false>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
                                t.kmin, t.range, n_tiles, rg);
-        hipLaunchKernelGGL((k_slice_join_b<false>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin,
-                           counts.as<uint32_t>(), nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_slice_join_inplace, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin, oa,
+                           misses);
+        if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
     }
-    if (st == QEH_OK) st = exclusive_scan_u32(ctx, counts.as<uint32_t>(), bases.as<uint64_t>(), (int64_t)T, &region_rows);
-    uint32_t of = 0;
-    if (st == QEH_OK) st = read_small(ctx, &of, rg.overflow, 4);
-    if (st == QEH_OK && of) st = kSliceJoinNotEligible;
+    uint64_t nmiss = 0;
+    if (st == QEH_OK) st = read_small(ctx, &nmiss, misses, 8);
+    qeh_column cv = *out_probe, ca = *out_build;  // the columns the tail appends to
+    if (st == QEH_OK && nmiss != 0) {
+        // some probe rows have no match: compact the regions (read from the first output
+        // column) into fresh columns with the two-pass emit
+        qeh_column cv2{}, ca2{};
+        DevBuf counts2, bases2;
+        st = alloc_column(ctx, probe_val.dtype, n, false, &cv2);
+        if (st == QEH_OK) st = alloc_column(ctx, QEH_DT_INT64, n, false, &ca2);
+        if (st == QEH_OK) st = counts2.alloc(ctx, T * 4 + 16);
+        if (st == QEH_OK) st = bases2.alloc(ctx, T * 8 + 16);
+        if (st == QEH_OK) {
+            KernelTimer kt(ctx, "join_probe");
+            hipLaunchKernelGGL((k_slice_join_b<false>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin,
+                               counts2.as<uint32_t>(), nullptr, nullptr, nullptr);
+        }
+        if (st == QEH_OK) st = exclusive_scan_u32(ctx, counts2.as<uint32_t>(), bases2.as<uint64_t>(), (int64_t)T, &region_rows);
+        if (st == QEH_OK) {
+            KernelTimer kt(ctx, "join_probe");
+            hipLaunchKernelGGL((k_slice_join_b<true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin,
+                               nullptr, bases2.as<uint64_t>(), (int64_t *)cv2.values, (int64_t *)ca2.values);
+            if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
+        }
+        if (st == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) st = fail(QEH_E_HIP, "slice join sync failed");
+        if (st == QEH_OK) {
+            qeh_column_release(ctx, out_probe);
+            qeh_column_release(ctx, out_build);
+            *out_probe = cv = cv2;
+            *out_build = ca = ca2;
+        } else {
+            if (cv2.values) qeh_column_release(ctx, &cv2);
+            if (ca2.values) qeh_column_release(ctx, &ca2);
+        }
+    }
     if (st == QEH_OK) {
         KernelTimer kt(ctx, "join_probe");
-        hipLaunchKernelGGL((k_slice_join_b<true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin, nullptr,
-                           bases.as<uint64_t>(), ov, oa);
         const int64_t done = n_tiles * kSliceTile;
         hipLaunchKernelGGL(k_fill_i64, dim3(1), dim3(1), 0, ctx->stream, (int64_t *)counter, (int64_t)1, (int64_t)region_rows);
         if (done < n)
             hipLaunchKernelGGL(k_slice_join_tail, dim3(grid_for(ctx, n - done, kBlock * 8, 2)), dim3(kBlock), 0, ctx->stream,
-                               in.key + done, in.acol[0] + done, n - done, t, amin, ov, oa, counter);
+                               in.key + done, in.acol[0] + done, n - done, t, amin, (int64_t *)cv.values,
+                               (int64_t *)ca.values, counter);
         if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
     }
-    uint64_t res[2] = {0, 0};
-    if (st == QEH_OK) st = read_small(ctx, &res[1], counter, 8);
+    uint64_t rows = 0;
+    if (st == QEH_OK) st = read_small(ctx, &rows, counter, 8);
     if (st != QEH_OK) {
         qeh_column_release(ctx, out_probe);
         qeh_column_release(ctx, out_build);
         return st;
     }
-    out_probe->length = (int64_t)res[1];
-    out_build->length = (int64_t)res[1];
-    *out_rows = (int64_t)res[1];
+    out_probe->length = (int64_t)rows;
+    out_build->length = (int64_t)rows;
+    *out_rows = (int64_t)rows;
     return QEH_OK;
 }
 

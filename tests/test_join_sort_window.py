@@ -80,6 +80,26 @@ def test_join_slice_path(ctx, monkeypatch, n_probe, n_build, key0, arange):
     assert sorted_rows(got) == sorted_rows(want)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_probe,n_build,n_miss", [(1_000_003, 300_000, 0), (819_200, 131_072, 0), (600_011, 200_000, 1),
+                                                    (400_000, 150_000, 777)])
+def test_join_slice_path_exact_regions(ctx, monkeypatch, n_probe, n_build, n_miss):
+    """Slice join with exact region sizes: when every probe row matches, the probe payload
+    stays where phase A wrote it (the output column) and phase B only adds the build payload;
+    any miss (one, or many) sends it through the compacting emit.  Ragged tails included."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    r = np.random.default_rng(n_probe)
+    bk = r.permutation(n_build).astype(np.int64) + 12_345
+    ba = r.integers(-30_000, 30_000, n_build).astype(np.int64)
+    pk = bk[r.integers(0, n_build, n_probe)]
+    if n_miss:
+        pk[r.choice(n_probe, n_miss, replace=False)] = -5  # below the key range
+    pv = r.random(n_probe)
+    got, want = join_both(ctx, (pk, None), [(pv, None)], (bk, None), [(ba, None)])
+    assert len(got[0][0]) == n_probe - n_miss
+    assert sorted_rows(got) == sorted_rows(want)
+
+
 def sort_both(ctx, keys, asc):
     perm = ctx.sort_indices([ctx.upload(*k) for k in keys], asc).to_numpy()[0]
     want = ob.sort_indices([ob.HostCol(*k) for k in keys], asc)

@@ -112,7 +112,7 @@ def cfg3(ctx, scale):
     dt = time.perf_counter() - t0
     cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} probe x {nd} build, {dt:.2f} s"}
     kms = kt["join_probe"] + kt["join_gather"]
-    line("cfg3 inner join 1e9 x 1e7", n, wall, 32.0 * n, kms, "k_slice_partition + k_slice_join_b (count, emit)", cpu,
+    line("cfg3 inner join 1e9 x 1e7", n, wall, 32.0 * n, kms, "k_slice_count + k_slice_partition + k_slice_join_inplace", cpu,
          {"output_rows": rows, "build_ms": kt["join_build"]})
 
 
