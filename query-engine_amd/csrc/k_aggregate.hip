@@ -1510,7 +1510,13 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     if (range * 2 < min_bytes) return QEH_OK;
     const uint64_t F = (range + kSliceKeys - 1) >> kSliceBits;
     if (F == 0 || F > (uint64_t)kSliceMaxF) return QEH_OK;
-    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    // optionally leave CUs to the build on the main queue (QEH_SLICE_RESERVE_CUS): with one
+    // phase-A workgroup on every CU the build's kernels wait for phase A to drain, but phase A
+    // loses more on fewer CUs than the build costs afterwards
+    int reserve = 0;
+    if (const char *e = std::getenv("QEH_SLICE_RESERVE_CUS")) reserve = std::atoi(e);
+    reserve = std::max(0, std::min(reserve, ctx->props.multiProcessorCount / 2));
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount - reserve, n_tiles);
     hipStream_t side = aux_stream(ctx);
     if (!side) return QEH_OK;
     if (!slice_regions(ctx, n_tiles, grid, F, nacol, &pre->kbuf, &pre->vbuf, &pre->cbuf, &pre->rg, ctx->stream))
@@ -1558,12 +1564,12 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     if (table_bytes(t) < min_bytes) return 0;
     const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return 0;
-    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
     bool tail_done = false;
     DevBuf kbuf, vbuf, cbuf;
     SliceRegions rg{};
-    if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->grid == grid &&
-        pre->n_tiles == n_tiles) {
+    if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->n_tiles == n_tiles) {
+        grid = pre->grid;  // phase A's workgroups = regions per slice
         rg = pre->rg;  // phase A already ran on the second queue, under the build
         // the ragged tail (rows past the last full tile) goes first: it overlaps phase A
         launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
@@ -2166,6 +2172,7 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     QEH_TRY(plan_aggs(aggs, n_aggs, probe_cols, n_probe_cols, idx.data(), &specs));
     if (probe_cols[probe_key_idx].dtype != QEH_DT_INT64 && probe_cols[probe_key_idx].dtype != QEH_DT_INT32)
         return fail(QEH_E_UNSUPPORTED, "hash join keys must be Int32/Int64 on the device");
+    MinMaxMemoScope memo(ctx);  // build key / group key ranges: read once for prelaunch, groups and join table
 
     // phase A of the slice path on the second queue, when its shape is known from the build key's
     // range (and the group count is bounded by one integer group key's range)

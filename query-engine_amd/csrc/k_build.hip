@@ -198,9 +198,31 @@ int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx,
     return columns_minmax(ctx, &col, 1, mn, mx, valid);
 }
 
-// several columns, one synchronous read for all of them
+static bool memo_get(qeh_ctx *ctx, const qeh_column &c, int64_t *mn, int64_t *mx, int64_t *cnt) {
+    if (!ctx->mm_memo_on) return false;
+    for (int i = 0; i < ctx->mm_memo_n; ++i) {
+        const auto &e = ctx->mm_memo[i];
+        if (e.values == c.values && e.validity == c.validity && e.offset == c.offset && e.length == c.length &&
+            e.dtype == c.dtype) {
+            *mn = e.mn, *mx = e.mx, *cnt = e.cnt;
+            return true;
+        }
+    }
+    return false;
+}
+
+static void memo_put(qeh_ctx *ctx, const qeh_column &c, int64_t mn, int64_t mx, int64_t cnt) {
+    const int cap = (int)(sizeof(ctx->mm_memo) / sizeof(ctx->mm_memo[0]));
+    if (!ctx->mm_memo_on || ctx->mm_memo_n >= cap) return;
+    ctx->mm_memo[ctx->mm_memo_n++] = {c.values, c.validity, c.offset, c.length, c.dtype, mn, mx, cnt};
+}
+
+// several columns, one synchronous read for all of them (none when every range is memoised)
 int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int64_t *mx, int64_t *valid) {
     if (n <= 0) return QEH_OK;
+    bool all = true;
+    for (int i = 0; i < n && all; ++i) all = memo_get(ctx, cols[i], &mn[i], &mx[i], &valid[i]);
+    if (all) return QEH_OK;
     DevBuf mm;
     QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
     for (int i = 0; i < n; ++i) {
@@ -217,6 +239,7 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
         mn[i] = hm[i].mn;
         mx[i] = hm[i].mx;
         valid[i] = (int64_t)hm[i].cnt;
+        memo_put(ctx, cols[i], mn[i], mx[i], valid[i]);
     }
     return QEH_OK;
 }
@@ -240,18 +263,12 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
         return fail(QEH_E_UNSUPPORTED, "hash join keys must be Int32/Int64 on the device");
     const int64_t n = key.length;
     ColRef kr = make_colref(key);
-    DevBuf mm;
-    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) + 16));
     MinMax hm{};
     {
-        KernelTimer kt(ctx, "join_build");
-        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
-        if (n > 0)
-            hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, n, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kr, n,
-                               mm.as<MinMax>());
+        int64_t mn, mx, cnt;
+        QEH_TRY(columns_minmax(ctx, &key, 1, &mn, &mx, &cnt));
+        hm.mn = mn, hm.mx = mx, hm.cnt = (uint64_t)cnt;
     }
-    QEH_HIP(hipGetLastError());
-    QEH_TRY(read_small(ctx, &hm, mm.p, sizeof(MinMax)));
 
     HashTable &t = out->t;
     t = HashTable{};
@@ -419,6 +436,26 @@ __global__ void k_group_direct(ColRef key, int64_t n, int64_t kmin, uint32_t *__
     }
 }
 
+// Small key ranges: the slots live in LDS per workgroup and each workgroup publishes only the
+// slots it filled.  Plain global stores from every row to a few hundred lines serialise on those
+// lines (90 us for 1e7 rows into 1024 slots; a winner per slot is all the table needs).
+constexpr uint32_t kGroupDirectLds = 16384;  // slots (64 KB of LDS)
+
+__global__ __launch_bounds__(kBlock) void k_group_direct_lds(ColRef key, int64_t n, int64_t kmin, uint32_t range,
+                                                             uint32_t *__restrict__ slots, uint32_t *__restrict__ slot_of_row) {
+    extern __shared__ uint32_t ls[];
+    for (uint32_t i = threadIdx.x; i < range; i += blockDim.x) ls[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)((uint64_t)load_i64(key, i) - (uint64_t)kmin);
+        ls[s] = (uint32_t)i;
+        slot_of_row[i] = s;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < range; i += blockDim.x)
+        if (ls[i] != 0xFFFFFFFFu) slots[i] = ls[i];
+}
+
 static int group_table_finish(qeh_ctx *ctx, GroupTable *out);
 
 int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t n_rows, GroupTable *out,
@@ -437,14 +474,12 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
     out->direct = false;
     if (allow_direct && slot_of_row && n_keys == 1 && n_rows > 0 && kc.c[0].validity == nullptr &&
         (kc.c[0].dtype == QEH_DT_INT64 || kc.c[0].dtype == QEH_DT_INT32) && !std::getenv("QEH_NO_DIRECT_GROUPS")) {
-        DevBuf mm;
-        QEH_TRY(mm.alloc(ctx, sizeof(MinMax) + 16));
-        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>());
-        hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, n_rows, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kc.c[0],
-                           n_rows, mm.as<MinMax>());
-        QEH_HIP(hipGetLastError());
         MinMax hm{};
-        QEH_TRY(read_small(ctx, &hm, mm.p, sizeof(MinMax)));
+        {
+            int64_t mn, mx, cnt;
+            QEH_TRY(columns_minmax(ctx, &keys[0], 1, &mn, &mx, &cnt));
+            hm.mn = mn, hm.mx = mx, hm.cnt = (uint64_t)cnt;
+        }
         const uint64_t range = (uint64_t)hm.mx - (uint64_t)hm.mn + 1ull;
         if (range != 0 && range <= std::max<uint64_t>(4 * (uint64_t)n_rows, 65536) && range < (1ull << 31)) {
             out->direct = true;
@@ -454,8 +489,13 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
             QEH_HIP(hipMemsetAsync(out->slots.p, 0xFF, range * 4, ctx->stream));
             {
                 KernelTimer kt(ctx, "group_insert");
-                hipLaunchKernelGGL(k_group_direct, dim3(grid_for(ctx, n_rows, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
-                                   kc.c[0], n_rows, hm.mn, out->slots.as<uint32_t>(), slot_of_row);
+                if (range <= kGroupDirectLds && !std::getenv("QEH_NO_GROUP_LDS"))
+                    hipLaunchKernelGGL(k_group_direct_lds, dim3(grid_for(ctx, n_rows, kBlock * 16, 1)), dim3(kBlock),
+                                       range * 4, ctx->stream, kc.c[0], n_rows, hm.mn, (uint32_t)range,
+                                       out->slots.as<uint32_t>(), slot_of_row);
+                else
+                    hipLaunchKernelGGL(k_group_direct, dim3(grid_for(ctx, n_rows, kBlock * 4, 8)), dim3(kBlock), 0,
+                                       ctx->stream, kc.c[0], n_rows, hm.mn, out->slots.as<uint32_t>(), slot_of_row);
             }
             QEH_HIP(hipGetLastError());
             return group_table_finish(ctx, out);

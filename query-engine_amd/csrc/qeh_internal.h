@@ -89,6 +89,17 @@ struct qeh_ctx {
     std::map<std::string, std::pair<double, int64_t>> timing_done;
     // Scan inputs kept on the device between queries (qeh_source.cache_key)
     std::shared_ptr<qeh::SourceCache> source_cache;
+    // integer-column min/max already read during the current operator call (its input
+    // columns are immutable for the call); on only inside a qeh::MinMaxMemoScope
+    struct MinMaxMemoEntry {
+        const void *values, *validity;
+        int64_t offset, length;
+        int32_t dtype;
+        int64_t mn, mx, cnt;
+    };
+    bool mm_memo_on = false;
+    int mm_memo_n = 0;
+    MinMaxMemoEntry mm_memo[4];
 };
 
 namespace qeh {
@@ -105,6 +116,14 @@ struct DeviceGuard {
         (void)hipGetDevice(&cur);
         if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
     }
+};
+
+// Enables ctx->mm_memo for one operator call, so the build side reads each key column's
+// range once (the prelaunch, the group table and the join table all need it).
+struct MinMaxMemoScope {
+    qeh_ctx *c;
+    explicit MinMaxMemoScope(qeh_ctx *ctx) : c(ctx) { c->mm_memo_on = true, c->mm_memo_n = 0; }
+    ~MinMaxMemoScope() { c->mm_memo_on = false, c->mm_memo_n = 0; }
 };
 
 // RAII device buffer from the pool.
