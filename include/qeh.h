@@ -289,6 +289,20 @@ int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_part,
                    const qeh_column *order_keys, int n_order, const int8_t *ascending,
                    qeh_column *out_rn);
 
+/* The other `WindowFunctionType`s (physical_plan.rs:160-170; semantics of
+ * docs/WINDOW_FUNCTIONS.md:67-205, the reference executor passes Window through,
+ * executor.rs:76-80) over the ROW_NUMBER order (PARTITION BY keys, then ORDER BY keys, ties by
+ * input position).  func = enum qeh_window_func (qeh_plan.h):
+ *   ROW_NUMBER / RANK / DENSE_RANK / NTILE(param >= 1) -> Int64, no NULLs;
+ *   LAG / LEAD(arg, param >= 0 rows) / FIRST_VALUE / LAST_VALUE(arg) -> arg's type
+ *   (Int32/Int64/Float32/Float64), NULL where arg is NULL or the offset leaves the partition
+ *   (then *dflt, the value's bit pattern, when dflt != NULL).  LAST_VALUE spans the whole
+ *   partition (WindowExpr carries no frame).  Peers compare keys by value bits (NULLs equal).
+ * With no keys (OVER ()), `arg` must be given and supplies the row count. */
+int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_keys, int n_part,
+               const qeh_column *order_keys, int n_order, const int8_t *ascending,
+               const qeh_column *arg, int64_t param, const int64_t *dflt, qeh_column *out);
+
 /* Hash partitioning for multi-GPU exchange (model: Partitioner::partition_by_hash,
  * crates/query-distributed/src/partition.rs:151-212; the hash function is not
  * observable in results, §8 row a15).  Writes `counts[n_parts]` and a

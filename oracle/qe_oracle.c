@@ -21,6 +21,7 @@
  *   INNER JOIN (executor.rs:363-381, `on` ignored)    -> qo_hash_join_inner
  *   Sort (identity, executor.rs:290-297)              -> qo_sort_indices
  *   ROW_NUMBER (docs/WINDOW_FUNCTIONS.md:44-65)       -> qo_row_number
+ *   RANK ... LAST_VALUE (docs/WINDOW_FUNCTIONS.md:67-205) -> qo_window
  * arrow-rs library semantics restated: cmp kernels are null-propagating and
  * compare floats by IEEE totalOrder; and/or are the non-Kleene variants (NULL
  * if either side is NULL); integer add/sub/mul/div are checked (error on
@@ -903,6 +904,83 @@ int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int
     for (int j = 0; j < n_keys; ++j) arr_free(&ka[j]);
     free(ka);
     free(perm);
+    return s;
+}
+
+/* Window functions of `WindowFunctionType` (physical_plan.rs:160-170) over the ROW_NUMBER order
+ * (partition keys ascending, then the ORDER BY keys, ties by input position).  Semantics from
+ * docs/WINDOW_FUNCTIONS.md (the reference executor passes Window through, executor.rs:76-80):
+ *   RANK (:67-89) = 1 + rows of the partition ordered strictly before the row's peers;
+ *   DENSE_RANK (:91-113) = 1 + distinct ORDER BY tuples before it; NTILE(n) (:115-137) = SQL
+ *   buckets (the first size % n buckets hold one row more); LAG/LEAD(col, n) (:139-175) = col
+ *   n rows before/after inside the partition, else dflt (NULL when dflt is NULL);
+ *   FIRST_VALUE / LAST_VALUE (:177-205) = col at the partition's first / last row (the
+ *   WindowExpr carries no frame; the doc's LAST_VALUE example spans the whole partition).
+ * out_bits holds Int64 results, or the argument's raw element bits (4-byte types zero-extended);
+ * out_valid one byte per row. */
+int qo_window(int func, const qo_col *part, int n_part, const qo_col *order, int n_order, const int8_t *ascending,
+              const qo_col *arg, int64_t param, const int64_t *dflt, int64_t n_rows, int64_t *out_bits,
+              uint8_t *out_valid) {
+    int nk = n_part + n_order;
+    qo_col *all = calloc((size_t)nk + 1, sizeof(qo_col));
+    int8_t *asc = calloc((size_t)nk + 1, 1);
+    for (int j = 0; j < n_part; ++j) { all[j] = part[j]; asc[j] = 1; }
+    for (int j = 0; j < n_order; ++j) { all[n_part + j] = order[j]; asc[n_part + j] = ascending ? ascending[j] : 1; }
+    int64_t *perm;
+    arr *ka;
+    int s = sorted_perm(all, nk, asc, n_rows, &perm, &ka);
+    const int value_fn = func >= 4;
+    int esz = 8;
+    if (s == QEH_OK && value_fn) {
+        if (!arg) s = err(QEH_E_INVALID, "oracle: window value function needs an argument");
+        else if (arg->dtype == QEH_DT_INT32 || arg->dtype == QEH_DT_FLOAT32) esz = 4;
+        else if (arg->dtype != QEH_DT_INT64 && arg->dtype != QEH_DT_FLOAT64)
+            s = err(QEH_E_UNSUPPORTED, "oracle: window argument type %s", dt_name(arg->dtype));
+    }
+    if (s == QEH_OK && func == 3 && param < 1) s = err(QEH_E_INVALID, "oracle: NTILE needs n >= 1");
+    if (s == QEH_OK && (func == 4 || func == 5) && param < 0) s = err(QEH_E_INVALID, "oracle: negative offset");
+    for (int64_t a = 0; s == QEH_OK && a < n_rows;) {
+        int64_t b = a + 1;  /* partition [a, b) in sorted order */
+        while (b < n_rows && tuple_eq(ka, perm[b - 1], ka, perm[b], n_part)) ++b;
+        int64_t peer = a, dense = 0;
+        for (int64_t i = a; i < b; ++i) {
+            if (i == a || !tuple_eq(ka, perm[i - 1], ka, perm[i], nk)) { peer = i; ++dense; }
+            const int64_t r0 = i - a, size = b - a, row = perm[i];
+            int64_t v = 0, src = -1;
+            uint8_t ok = 1;
+            switch (func) {
+                case 0: v = r0 + 1; break;
+                case 1: v = peer - a + 1; break;
+                case 2: v = dense; break;
+                case 3: {
+                    const int64_t q = size / param, r = size % param;
+                    v = r0 < r * (q + 1) ? r0 / (q + 1) + 1 : r + (r0 - r * (q + 1)) / q + 1;
+                    break;
+                }
+                case 4: src = i - param >= a ? perm[i - param] : -2; break;
+                case 5: src = i + param < b ? perm[i + param] : -2; break;
+                case 6: src = perm[a]; break;
+                case 7: src = perm[b - 1]; break;
+                default: s = err(QEH_E_UNSUPPORTED, "oracle: window function %d", func);
+            }
+            if (src == -2) {
+                ok = dflt != NULL;
+                v = dflt ? *dflt : 0;
+            } else if (src >= 0) {
+                ok = arg->valid ? arg->valid[src] != 0 : 1;
+                v = esz == 8 ? ((const int64_t *)arg->values)[src] : (int64_t)((const uint32_t *)arg->values)[src];
+                if (!ok) v = 0;
+            }
+            out_bits[row] = v;
+            out_valid[row] = ok;
+        }
+        a = b;
+    }
+    for (int j = 0; j < nk; ++j) arr_free(&ka[j]);
+    free(ka);
+    free(perm);
+    free(all);
+    free(asc);
     return s;
 }
 

@@ -66,6 +66,9 @@ int qo_sort_indices_nulls(const qo_col *keys, int n_keys, const int8_t *ascendin
                           int64_t n_rows, uint32_t *out_perm);
 int qo_row_number(const qo_col *part, int n_part, const qo_col *order, int n_order,
                   const int8_t *ascending, int64_t n_rows, int64_t *out_rn);
+int qo_window(int func, const qo_col *part, int n_part, const qo_col *order, int n_order, const int8_t *ascending,
+              const qo_col *arg, int64_t param, const int64_t *dflt, int64_t n_rows, int64_t *out_bits,
+              uint8_t *out_valid);
 
 #ifdef __cplusplus
 }

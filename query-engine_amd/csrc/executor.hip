@@ -930,14 +930,100 @@ class Executor {
         return QEH_OK;
     }
 
+    // integer literal argument of a window function (NTILE(n), LAG/LEAD offsets)
+    static bool lit_int(const qeh_expr &e, int64_t *v) {
+        if (e.n_nodes != 1 || e.nodes[0].kind != QEH_EX_LITERAL || e.nodes[0].lit_is_null) return false;
+        const int dt = e.nodes[0].lit_dtype;
+        if (dt != QEH_DT_INT32 && dt != QEH_DT_INT64) return false;
+        *v = e.nodes[0].lit_i64;
+        return true;
+    }
+
+    // RANK / DENSE_RANK / NTILE(n) / LAG / LEAD(col[, n[, default]]) / FIRST_VALUE / LAST_VALUE(col)
+    // (WindowFunctionType, physical_plan.rs:160-170) through qeh_window
+    int window_fn(const qeh_plan_node &nd, const qeh_window_expr &we, const Table &in, Table *out) {
+        std::vector<Col> pk, okc;
+        for (int i = 0; i < we.n_partition; ++i) {
+            Col c;
+            QEH_TRY(eval(in, we.partition_by[i], &c));
+            pk.push_back(c);
+        }
+        for (int i = 0; i < we.n_order; ++i) {
+            Col c;
+            QEH_TRY(eval(in, we.order_by[i], &c));
+            okc.push_back(c);
+        }
+        std::vector<qeh_column> pc, oc;
+        for (auto &c : pk) pc.push_back(c.c);
+        for (auto &c : okc) oc.push_back(c.c);
+        std::vector<int8_t> asc(std::max(we.n_order, 1), 1);
+        const bool value_fn = we.func >= QEH_WIN_LAG;
+        int64_t param = 0, dflt = 0;
+        bool has_dflt = false;
+        Col argc;
+        bool have_arg = false;
+        if (we.func == QEH_WIN_NTILE) {
+            if (we.n_args < 1 || !lit_int(we.args[0], &param))
+                return fail(QEH_E_UNSUPPORTED, "NTILE needs an integer literal bucket count");
+        } else if (value_fn) {
+            if (we.n_args < 1) return fail(QEH_E_INVALID, "window value function without an argument");
+            QEH_TRY(eval(in, we.args[0], &argc));
+            have_arg = true;
+            if (we.func == QEH_WIN_LAG || we.func == QEH_WIN_LEAD) {
+                param = 1;  // LAG(col) = LAG(col, 1)
+                if (we.n_args >= 2 && !lit_int(we.args[1], &param))
+                    return fail(QEH_E_UNSUPPORTED, "LAG/LEAD offset must be an integer literal");
+                if (we.n_args >= 3) {
+                    const qeh_expr &d = we.args[2];
+                    if (d.n_nodes != 1 || d.nodes[0].kind != QEH_EX_LITERAL)
+                        return fail(QEH_E_UNSUPPORTED, "LAG/LEAD default must be a literal");
+                    const qeh_expr_node &ln = d.nodes[0];
+                    if (!ln.lit_is_null && ln.lit_dtype != QEH_DT_NULL) {
+                        has_dflt = true;
+                        const int adt = argc.c.dtype;
+                        const bool lit_f = ln.lit_dtype == QEH_DT_FLOAT32 || ln.lit_dtype == QEH_DT_FLOAT64;
+                        if (adt == QEH_DT_FLOAT64) {
+                            const double x = lit_f ? ln.lit_f64 : (double)ln.lit_i64;
+                            std::memcpy(&dflt, &x, 8);
+                        } else if (adt == QEH_DT_FLOAT32) {
+                            const float x = (float)(lit_f ? ln.lit_f64 : (double)ln.lit_i64);
+                            uint32_t b;
+                            std::memcpy(&b, &x, 4);
+                            dflt = (int64_t)b;
+                        } else if (lit_f) {
+                            return fail(QEH_E_UNSUPPORTED, "LAG/LEAD float default for an integer column");
+                        } else {
+                            dflt = adt == QEH_DT_INT32 ? (int64_t)(uint32_t)(int32_t)ln.lit_i64 : ln.lit_i64;
+                        }
+                    }
+                }
+            }
+        } else if (pc.empty() && oc.empty() && !in.cols.empty()) {
+            argc = in.cols[0];  // OVER (): any input column carries the row count
+            have_arg = true;
+        }
+        qeh_column res{};
+        QEH_TRY(qeh_window(ctx_, we.func, pc.data(), (int)pc.size(), oc.data(), (int)oc.size(), asc.data(),
+                           have_arg ? &argc.c : nullptr, param, has_dflt ? &dflt : nullptr, &res));
+        static const char *names[] = {"row_number", "rank", "dense_rank", "ntile", "lag", "lead", "first_value", "last_value"};
+        const size_t idx = out->cols.size();
+        std::string name = (nd.field_names && (int)idx < nd.n_fields && nd.field_names[idx]) ? nd.field_names[idx]
+                                                                                            : names[we.func];
+        out->fields.push_back({name, res.dtype, true});
+        out->cols.push_back(own(ctx_, res));
+        return QEH_OK;
+    }
+
     int window(const qeh_plan_node &nd, Table *out, int depth) {
         Table in;
         QEH_TRY(run(nd.input, &in, depth + 1));
         *out = in;
         for (int w = 0; w < nd.n_window; ++w) {
             const qeh_window_expr &we = nd.window[w];
-            if (we.func != QEH_WIN_ROW_NUMBER)
-                return fail(QEH_E_UNSUPPORTED, "only ROW_NUMBER() runs on the device");
+            if (we.func != QEH_WIN_ROW_NUMBER) {
+                QEH_TRY(window_fn(nd, we, in, out));
+                continue;
+            }
             std::vector<Col> pk, okc;
             for (int i = 0; i < we.n_partition; ++i) {
                 Col c;

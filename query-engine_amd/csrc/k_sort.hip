@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/qeh_plan.h"
 #include "device_common.h"
 #include "ops.h"
 
@@ -1174,6 +1175,253 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
                            rs.v[rs.cur].as<uint32_t>(), starts.as<int64_t>(), nwin, (int64_t *)out_rn->values);
     }
     QEH_HIP(hipGetLastError());
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+// ---- RANK / DENSE_RANK / NTILE / LAG / LEAD / FIRST_VALUE / LAST_VALUE -------------------
+// Same sorted order as ROW_NUMBER.  In sorted positions: ps[i] = start of i's partition and
+// qs[i] = start of its peer group (last flagged position <= i: the chunked max-scan of the row
+// numbers), peer-group counts by an exclusive scan (DENSE_RANK), partition ends stored at their
+// start (NTILE / LEAD / LAST_VALUE); one kernel then writes every row's result into input order.
+
+// L[i] = last j <= i with flags[j] (k_rn_write's scan, writing the start instead of i - start + 1)
+__global__ __launch_bounds__(kBlock) void k_seg_start(const uint32_t *__restrict__ flags, const int64_t *__restrict__ carry,
+                                                      int64_t n, int64_t nchunks, int64_t *__restrict__ L) {
+    __shared__ int64_t wmax[kBlock / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const int64_t base = c * kRnChunk + (int64_t)t * kRnPer;
+        uint32_t f[kRnPer];
+        int64_t m = -1;
+#pragma unroll
+        for (int j = 0; j < kRnPer; ++j) {
+            const int64_t i = base + j;
+            f[j] = i < n ? flags[i] : 0u;
+            if (f[j]) m = i;
+        }
+        int64_t incl = m;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl = o > incl ? o : incl;
+        }
+        if (lane == 63) wmax[w] = incl;
+        __syncthreads();
+        int64_t start = carry[c];
+        for (int q = 0; q < w; ++q) start = wmax[q] > start ? wmax[q] : start;
+        const int64_t prev = __shfl_up(incl, 1, 64);
+        if (lane > 0) start = prev > start ? prev : start;
+#pragma unroll
+        for (int j = 0; j < kRnPer; ++j) {
+            const int64_t i = base + j;
+            if (f[j]) start = i;
+            if (i < n) L[i] = start;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_or_flags(uint32_t *__restrict__ a, const uint32_t *__restrict__ b, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] |= b[i];
+}
+
+// pend[ps[i]] = end of i's partition, written by its last row
+__global__ void k_part_end(const uint32_t *__restrict__ fp, const int64_t *__restrict__ ps, int64_t n,
+                           int64_t *__restrict__ pend) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (i == n - 1 || fp[i + 1]) pend[ps[i]] = i + 1;
+}
+
+__global__ void k_win_iota(uint32_t *__restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = (uint32_t)i;
+}
+
+struct WinArgs {
+    const uint32_t *perm;
+    const int64_t *ps, *qs, *pend;
+    const uint64_t *excl;  // exclusive scan of the peer flags
+    const uint32_t *fq;    // peer flags
+    ColRef arg;
+    int64_t param;
+    int64_t dflt;
+    int has_dflt;
+    int esz;               // argument element bytes (value functions)
+};
+
+template <int FUNC>
+__global__ void k_window_out(WinArgs a, int64_t n, void *__restrict__ out, uint8_t *__restrict__ valid8) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = a.ps[i], row = a.perm[i];
+        int64_t v = 0, src = -1;
+        uint8_t ok = 1;
+        if (FUNC == QEH_WIN_ROW_NUMBER) {
+            v = i - s + 1;
+        } else if (FUNC == QEH_WIN_RANK) {
+            v = a.qs[i] - s + 1;
+        } else if (FUNC == QEH_WIN_DENSE_RANK) {
+            v = (int64_t)(a.excl[i] + a.fq[i] - a.excl[s]);
+        } else if (FUNC == QEH_WIN_NTILE) {
+            const int64_t size = a.pend[s] - s, r0 = i - s, q = size / a.param, r = size % a.param;
+            v = r0 < r * (q + 1) ? r0 / (q + 1) + 1 : r + (r0 - r * (q + 1)) / q + 1;
+        } else if (FUNC == QEH_WIN_LAG) {
+            src = i - a.param >= s ? (int64_t)a.perm[i - a.param] : -2;
+        } else if (FUNC == QEH_WIN_LEAD) {
+            src = i + a.param < a.pend[s] ? (int64_t)a.perm[i + a.param] : -2;
+        } else if (FUNC == QEH_WIN_FIRST_VALUE) {
+            src = a.perm[s];
+        } else {  // LAST_VALUE: the partition's last row (whole-partition frame)
+            src = a.perm[a.pend[s] - 1];
+        }
+        if (FUNC >= QEH_WIN_LAG) {
+            if (src == -2) {
+                ok = (uint8_t)a.has_dflt;
+                v = a.dflt;
+            } else {
+                ok = col_valid(a.arg, src) ? 1 : 0;
+                v = a.esz == 8 ? ((const int64_t *)a.arg.values)[src] : (int64_t)((const uint32_t *)a.arg.values)[src];
+            }
+            valid8[row] = ok;
+            if (a.esz == 8) ((int64_t *)out)[row] = ok ? v : 0;
+            else ((uint32_t *)out)[row] = ok ? (uint32_t)v : 0u;
+        } else {
+            ((int64_t *)out)[row] = v;
+        }
+    }
+}
+
+extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_keys, int n_part, const qeh_column *order_keys,
+                          int n_order, const int8_t *ascending, const qeh_column *arg, int64_t param, const int64_t *dflt,
+                          qeh_column *out) {
+    if (!ctx || !out || n_part < 0 || n_order < 0) return fail(QEH_E_INVALID, "qeh_window: bad argument");
+    if (func < QEH_WIN_ROW_NUMBER || func > QEH_WIN_LAST_VALUE) return fail(QEH_E_INVALID, "qeh_window: unknown function");
+    if (n_part > kMaxGroupKeys || n_order > kMaxGroupKeys)
+        return fail(QEH_E_UNSUPPORTED, "at most 4 PARTITION BY and 4 ORDER BY keys on the device");
+    const bool value_fn = func >= QEH_WIN_LAG;
+    if (func == QEH_WIN_NTILE && param < 1) return fail(QEH_E_INVALID, "NTILE needs a bucket count >= 1");
+    if ((func == QEH_WIN_LAG || func == QEH_WIN_LEAD) && param < 0) return fail(QEH_E_INVALID, "LAG/LEAD offset must be >= 0");
+    int esz = 8;
+    if (value_fn) {
+        if (!arg) return fail(QEH_E_INVALID, "window value function needs an argument column");
+        QEH_TRY(check_column(*arg, "window argument"));
+        if (arg->dtype == QEH_DT_INT32 || arg->dtype == QEH_DT_FLOAT32) esz = 4;
+        else if (arg->dtype != QEH_DT_INT64 && arg->dtype != QEH_DT_FLOAT64)
+            return fail(QEH_E_UNSUPPORTED, "window value functions take Int32/Int64/Float32/Float64 on the device");
+    }
+    DeviceGuard dg(ctx->device);
+    std::vector<qeh_column> all;
+    std::vector<int8_t> asc;
+    for (int j = 0; j < n_part; ++j) all.push_back(part_keys[j]), asc.push_back(1);
+    for (int j = 0; j < n_order; ++j) all.push_back(order_keys[j]), asc.push_back(ascending ? ascending[j] : 1);
+    int64_t n = arg ? arg->length : 0;  // OVER (): the argument column gives the row count
+    if (!all.empty()) {
+        QEH_TRY(check_sort_keys(all.data(), (int)all.size(), &n));
+        if (value_fn && arg->length != n) return fail(QEH_E_INVALID, "window argument length mismatch");
+    } else if (!arg) {
+        return fail(QEH_E_INVALID, "qeh_window: OVER () needs a column for the row count");
+    }
+    if (func == QEH_WIN_ROW_NUMBER && !all.empty())  // the dedicated path (pair-key sort, no peer state)
+        return qeh_row_number(ctx, part_keys, n_part, order_keys, n_order, ascending, out);
+    const int odt = value_fn ? arg->dtype : QEH_DT_INT64;
+    QEH_TRY(alloc_column(ctx, odt, n, value_fn, out));
+    if (n == 0) return QEH_OK;
+    auto bail = [&](int s) {
+        qeh_column_release(ctx, out);
+        return s;
+    };
+    RadixState rs;
+    DevBuf iota;
+    const uint32_t *perm;
+    if (!all.empty()) {
+        int s = sort_perm(ctx, all.data(), (int)all.size(), asc.data(), n, rs);
+        if (s != QEH_OK) return bail(s);
+        perm = rs.v[rs.cur].as<uint32_t>();
+    } else {
+        if (iota.alloc(ctx, (size_t)n * 4) != QEH_OK) return bail(QEH_E_OOM);
+        hipLaunchKernelGGL(k_win_iota, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, iota.as<uint32_t>(), n);
+        perm = iota.as<uint32_t>();
+    }
+    const int grid = grid_for(ctx, n, kBlock * 8, 8);
+    const int64_t nchunks = (n + kRnChunk - 1) / kRnChunk;
+    DevBuf fp, fq, ps, qs, pend, excl, carry, valid8;
+    if (fp.alloc(ctx, (size_t)n * 4) != QEH_OK || ps.alloc(ctx, (size_t)n * 8) != QEH_OK ||
+        carry.alloc(ctx, (size_t)nchunks * 8) != QEH_OK)
+        return bail(QEH_E_OOM);
+    KernelTimer kt(ctx, "window");
+    KeyCols pk{};
+    pk.n = n_part;
+    for (int j = 0; j < n_part; ++j) pk.c[j] = make_colref(part_keys[j]);
+    hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, fp.as<uint32_t>());
+    auto seg_start = [&](const uint32_t *flags, int64_t *L) {
+        hipLaunchKernelGGL(k_rn_chunk_last, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags, n, nchunks,
+                           carry.as<int64_t>());
+        hipLaunchKernelGGL(k_rn_prefix_max, dim3(1), dim3(1024), 0, ctx->stream, carry.as<int64_t>(), nchunks);
+        hipLaunchKernelGGL(k_seg_start, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags, carry.as<int64_t>(), n,
+                           nchunks, L);
+    };
+    seg_start(fp.as<uint32_t>(), ps.as<int64_t>());
+    WinArgs a{};
+    a.perm = perm;
+    a.ps = ps.as<int64_t>();
+    a.param = param;
+    a.esz = esz;
+    if (func == QEH_WIN_RANK || func == QEH_WIN_DENSE_RANK) {
+        // peer flags: partition start or any ORDER BY key changes
+        if (fq.alloc(ctx, (size_t)n * 4) != QEH_OK) return bail(QEH_E_OOM);
+        KeyCols ok{};
+        ok.n = n_order;
+        for (int j = 0; j < n_order; ++j) ok.c[j] = make_colref(order_keys[j]);
+        if (n_order > 0) {
+            hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, ok, perm, n, fq.as<uint32_t>());
+            hipLaunchKernelGGL(k_or_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, fq.as<uint32_t>(), fp.as<uint32_t>(), n);
+        } else {
+            QEH_HIP(hipMemcpyAsync(fq.p, fp.p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        a.fq = fq.as<uint32_t>();
+        if (func == QEH_WIN_RANK) {
+            if (qs.alloc(ctx, (size_t)n * 8) != QEH_OK) return bail(QEH_E_OOM);
+            seg_start(fq.as<uint32_t>(), qs.as<int64_t>());
+            a.qs = qs.as<int64_t>();
+        } else {
+            if (excl.alloc(ctx, (size_t)n * 8) != QEH_OK) return bail(QEH_E_OOM);
+            int s = exclusive_scan_u32(ctx, fq.as<uint32_t>(), excl.as<uint64_t>(), n, nullptr);
+            if (s != QEH_OK) return bail(s);
+            a.excl = excl.as<uint64_t>();
+        }
+    }
+    if (func == QEH_WIN_NTILE || func == QEH_WIN_LEAD || func == QEH_WIN_LAST_VALUE) {
+        if (pend.alloc(ctx, (size_t)n * 8) != QEH_OK) return bail(QEH_E_OOM);
+        hipLaunchKernelGGL(k_part_end, dim3(grid), dim3(kBlock), 0, ctx->stream, fp.as<uint32_t>(), ps.as<int64_t>(), n,
+                           pend.as<int64_t>());
+        a.pend = pend.as<int64_t>();
+    }
+    if (value_fn) {
+        if (valid8.alloc(ctx, (size_t)n) != QEH_OK) return bail(QEH_E_OOM);
+        a.arg = make_colref(*arg);
+        a.has_dflt = dflt != nullptr;
+        if (dflt) a.dflt = esz == 8 ? *dflt : (int64_t)(uint32_t)*dflt;
+    }
+#define QEH_WIN(F)                                                                                                        \
+    hipLaunchKernelGGL(k_window_out<F>, dim3(grid), dim3(kBlock), 0, ctx->stream, a, n, out->values, valid8.as<uint8_t>())
+    switch (func) {
+        case QEH_WIN_ROW_NUMBER: QEH_WIN(QEH_WIN_ROW_NUMBER); break;  // OVER (): input order
+        case QEH_WIN_RANK: QEH_WIN(QEH_WIN_RANK); break;
+        case QEH_WIN_DENSE_RANK: QEH_WIN(QEH_WIN_DENSE_RANK); break;
+        case QEH_WIN_NTILE: QEH_WIN(QEH_WIN_NTILE); break;
+        case QEH_WIN_LAG: QEH_WIN(QEH_WIN_LAG); break;
+        case QEH_WIN_LEAD: QEH_WIN(QEH_WIN_LEAD); break;
+        case QEH_WIN_FIRST_VALUE: QEH_WIN(QEH_WIN_FIRST_VALUE); break;
+        default: QEH_WIN(QEH_WIN_LAST_VALUE); break;
+    }
+#undef QEH_WIN
+    QEH_HIP(hipGetLastError());
+    if (value_fn) {
+        int s = qeh_bytes_to_validity(ctx, valid8.as<uint8_t>(), n, out->validity);
+        if (s != QEH_OK) return bail(s);
+        out->null_count = -1;
+    }
     QEH_HIP(hipStreamSynchronize(ctx->stream));
     return QEH_OK;
 }

@@ -473,6 +473,31 @@ class Context:
         abi.check(self.lib.qeh_row_number(self.h, cp, len(part), co, len(order), asc, C.byref(out)))
         return self._wrap(out)
 
+    def window(self, func: int, part: Sequence[DeviceColumn], order: Sequence[DeviceColumn],
+               ascending: Sequence[bool], arg: Optional[DeviceColumn] = None, param: int = 0,
+               default=None) -> DeviceColumn:
+        """``WindowFunctionType`` ``func`` (qe_hip.plan.WindowFunctionType) OVER (PARTITION BY
+        part ORDER BY order): RANK / DENSE_RANK / NTILE(param) -> Int64; LAG / LEAD(arg, param)
+        / FIRST_VALUE / LAST_VALUE(arg) -> arg's type, NULL outside the partition unless
+        ``default`` is given (qeh_window)."""
+        cp, co = self._cols(part), self._cols(order)
+        asc = (C.c_int8 * max(len(order), 1))(*[1 if a else 0 for a in ascending])
+        d = None
+        if default is not None:
+            dt = {abi.DT_INT32: np.int32, abi.DT_INT64: np.int64, abi.DT_FLOAT32: np.float32,
+                  abi.DT_FLOAT64: np.float64}[arg.c.dtype]
+            bits = np.zeros(1, np.int64)
+            if np.dtype(dt).itemsize == 8:
+                bits.view(dt)[0] = default
+            else:
+                bits[0] = int(np.array([default], dt).view(np.uint32)[0])
+            d = C.byref(C.c_int64(int(bits[0])))
+        out = abi.QehColumn()
+        abi.check(self.lib.qeh_window(self.h, int(func), cp, len(part), co, len(order), asc,
+                                      C.byref(arg.c) if arg is not None else None, int(param), d,
+                                      C.byref(out)))
+        return self._wrap(out)
+
     def hash_partition(self, key: DeviceColumn, n_parts: int):
         counts = (C.c_int64 * n_parts)()
         out = abi.QehColumn()

@@ -187,6 +187,34 @@ def sort_indices(keys: Sequence[HostCol], ascending: Sequence[bool]) -> np.ndarr
     return out[:n]
 
 
+def window(func: int, part: Sequence[HostCol], order: Sequence[HostCol], ascending: Sequence[bool],
+           arg: Optional[HostCol] = None, param: int = 0, default=None, n: Optional[int] = None):
+    """qo_window: (values, valid).  Ranking functions -> int64 values, all valid; value functions
+    -> values in the argument's dtype, valid = bool array."""
+    if n is None:
+        n = len((list(part) + list(order) + ([arg] if arg is not None else []))[0].values)
+    bits = np.zeros(max(n, 1), np.int64)
+    valid = np.zeros(max(n, 1), np.uint8)
+    asc = (C.c_int8 * max(len(order), 1))(*[1 if a else 0 for a in ascending])
+    d = None
+    if default is not None:
+        dv = np.zeros(1, np.int64)
+        if arg.values.dtype.itemsize == 8:
+            dv.view(arg.values.dtype)[0] = default
+        else:
+            dv.view(np.uint32)[0] = np.array([default], arg.values.dtype).view(np.uint32)[0]
+        d = dv.ctypes.data_as(C.c_void_p)
+    argp = C.byref(arg.c) if arg is not None else None
+    _check(lib().qo_window(func, _arr(part), len(part), _arr(order), len(order), asc, argp, C.c_int64(param), d,
+                           C.c_int64(n), bits.ctypes.data_as(C.c_void_p), valid.ctypes.data_as(C.c_void_p)))
+    bits, valid = bits[:n], valid[:n].astype(bool)
+    if func < 4 or arg is None:
+        return bits, valid
+    dt = arg.values.dtype
+    vals = bits.view(dt) if dt.itemsize == 8 else bits.astype(np.uint32).view(dt)
+    return vals, valid
+
+
 def row_number(part: Sequence[HostCol], order: Sequence[HostCol], ascending: Sequence[bool]) -> np.ndarray:
     n = len((part or order)[0].values)
     out = np.empty(max(n, 1), np.int64)

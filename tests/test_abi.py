@@ -23,7 +23,7 @@ def test_header_declares_the_operator_surface():
     names = declared_functions()
     for required in ["qeh_init", "qeh_filter", "qeh_eval", "qeh_hash_aggregate", "qeh_filter_aggregate",
                      "qeh_hash_join_inner", "qeh_join_filter_aggregate", "qeh_sort_indices", "qeh_take",
-                     "qeh_row_number", "qeh_hash_partition", "qeh_last_error", "qeh_execute_plan"]:
+                     "qeh_row_number", "qeh_window", "qeh_hash_partition", "qeh_last_error", "qeh_execute_plan"]:
         assert required in names
 
 
