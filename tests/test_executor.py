@@ -361,3 +361,33 @@ def test_outer_join_plans(qx, jt):
     got2 = sorted(zip(*[c.to_pylist() for c in out2.columns]), key=lambda t: tuple((x is None, x) for x in t))
     want2 = sorted([w[:4] for w in want], key=lambda t: tuple((x is None, x) for x in t))
     assert got2 == want2
+
+
+@pytest.mark.gpu
+def test_window_functions_through_the_plan(qx):
+    """Window node with RANK / DENSE_RANK / NTILE(4) / LAG(w, 2, 0.5) / LAST_VALUE(v)
+    (WindowFunctionType, physical_plan.rs:160-179) vs the oracle."""
+    from qe_hip.plan import WindowFunctionType as W
+    r = np.random.default_rng(11)
+    n = 40_000
+    k = pa.array(r.integers(0, 30, n), pa.int64(), mask=r.random(n) < 0.05)
+    v = pa.array(r.integers(-10, 10, n), pa.int64())
+    w = pa.array(r.random(n), mask=r.random(n) < 0.1)
+    t = pa.table({"t.k": k, "t.v": v, "t.w": w})
+    part, order = [Column("t.k", 0)], [Column("t.v", 1)]
+    exprs = [WindowExpr(W.Rank, [], part, order), WindowExpr(W.DenseRank, [], part, order),
+             WindowExpr(W.Ntile, [lit(4)], part, order), WindowExpr(W.Lag, [Column("t.w", 2), lit(2), lit(0.5)], part, order),
+             WindowExpr(W.LastValue, [Column("t.v", 1)], part, order)]
+    names = ["t.k", "t.v", "t.w", "rk", "drk", "q", "lag", "lv"]
+    out = qx.execute(Window(Scan(source(t, 3)), exprs, names))
+    assert out[0].schema.names == names
+    cols = as_cols([t.to_batches()[0]])
+    hk, hv, hw = ob.HostCol(*cols[0]), ob.HostCol(*cols[1]), ob.HostCol(*cols[2])
+    assert np.array_equal(out[0].column(3).to_numpy(), ob.window(W.Rank, [hk], [hv], [True])[0])
+    assert np.array_equal(out[0].column(4).to_numpy(), ob.window(W.DenseRank, [hk], [hv], [True])[0])
+    assert np.array_equal(out[0].column(5).to_numpy(), ob.window(W.Ntile, [hk], [hv], [True], param=4)[0])
+    lag_v, lag_ok = ob.window(W.Lag, [hk], [hv], [True], arg=hw, param=2, default=0.5)
+    got = out[0].column(6)
+    assert np.array_equal(got.is_valid().to_numpy(zero_copy_only=False), lag_ok)
+    assert np.array_equal(got.to_numpy(zero_copy_only=False)[lag_ok], lag_v[lag_ok])
+    assert np.array_equal(out[0].column(7).to_numpy(zero_copy_only=False), ob.window(W.LastValue, [hk], [hv], [True], arg=hv)[0])
