@@ -724,21 +724,32 @@ static int check_sort_keys(const qeh_column *keys, int n_keys, int64_t *n) {
 
 // ---- ROW_NUMBER ----------------------------------------------------------------------------
 // flags[i] = 1 when sorted row i starts a new partition (partition columns differ from row i-1)
+// One gather per row: each lane loads its row's keys through the permutation and takes the
+// previous row's from the lane below (lane 0 loads its predecessor itself), halving the random
+// reads of comparing perm[i-1] with perm[i] directly.  Whole workgroups step together, so every
+// lane of a wave reaches the shuffles.
 __global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, int64_t n, uint32_t *__restrict__ flags) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        uint32_t f = 1;
-        if (i > 0) {
-            const int64_t a = perm[i - 1], b = perm[i];
-            f = 0;
-            for (int c = 0; c < part.n; ++c) {
-                const bool va = col_valid(part.c[c], a), vb = col_valid(part.c[c], b);
-                if (va != vb || (va && load_i64(part.c[c], a) != load_i64(part.c[c], b))) {
-                    f = 1;
-                    break;
-                }
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        const bool act = i < n;
+        const int64_t b = act ? (int64_t)perm[i] : 0;
+        const bool own_prev = act && lane == 0 && i > 0;
+        const int64_t a = own_prev ? (int64_t)perm[i - 1] : 0;
+        uint32_t f = 0;
+        for (int c = 0; c < part.n; ++c) {
+            const int vb = act && col_valid(part.c[c], b) ? 1 : 0;
+            const int64_t xb = vb ? load_i64(part.c[c], b) : 0;
+            int va = __shfl_up(vb, 1, 64);
+            int64_t xa = __shfl_up(xb, 1, 64);
+            if (own_prev) {
+                va = col_valid(part.c[c], a) ? 1 : 0;
+                xa = va ? load_i64(part.c[c], a) : 0;
             }
+            if (va != vb || (va && xa != xb)) f = 1;
         }
-        flags[i] = f;
+        if (act) flags[i] = i == 0 ? 1u : f;
     }
 }
 
@@ -1353,7 +1364,18 @@ extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_key
     KeyCols pk{};
     pk.n = n_part;
     for (int j = 0; j < n_part; ++j) pk.c[j] = make_colref(part_keys[j]);
-    hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, fp.as<uint32_t>());
+    // partition flags from the sorted encodings when they determine the partition key (as in
+    // qeh_row_number), else by comparing the key columns through the permutation
+    const int sh = rs.part_shift >= 0 ? rs.part_shift : 0;
+    const bool enc_ok = !all.empty() && n_part == 1 && (rs.enc_injective || (rs.part_shift >= 0 && n_order == 1));
+    if (enc_ok && rs.key32)
+        hipLaunchKernelGGL(k_part_flags_enc<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, rs.k[rs.cur].as<uint32_t>(), n,
+                           fp.as<uint32_t>(), sh);
+    else if (enc_ok)
+        hipLaunchKernelGGL(k_part_flags_enc<uint64_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, rs.k[rs.cur].as<uint64_t>(), n,
+                           fp.as<uint32_t>(), sh);
+    else
+        hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, pk, perm, n, fp.as<uint32_t>());
     auto seg_start = [&](const uint32_t *flags, int64_t *L) {
         hipLaunchKernelGGL(k_rn_chunk_last, dim3(gc_of(ctx, nchunks)), dim3(kBlock), 0, ctx->stream, flags, n, nchunks,
                            carry.as<int64_t>());

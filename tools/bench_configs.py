@@ -17,7 +17,7 @@
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
-usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,filter,limit,plan,left,full,merge,encode,partition] [--scale 1.0]
+usage: python tools/bench_configs.py [--only cfg2,cfg3,cfg5,window,filter,limit,plan,left,full,merge,encode,partition] [--scale 1.0]
 """
 import argparse
 import json
@@ -154,6 +154,27 @@ def cfg5(ctx, scale):
     cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows, {dt:.2f} s"}
     kms = sum(kt.values())
     line("cfg5 ROW_NUMBER 1e9", n, wall, 24.0 * n, kms, "k_rs_hist/k_rs_scatter (+encode, row numbers)", cpu, kt)
+
+
+def cfg_window(ctx, scale):
+    """RANK() and LAG(v, 1) OVER (PARTITION BY k ORDER BY v) on the cfg-5 data (1e9 rows)."""
+    from qe_hip.plan import WindowFunctionType as W
+    n = int(1e9 * scale)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 20)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    m = 2_000_000
+    hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 7, m, 2 ** 20)
+    hv = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 8, m, 2 ** 62, lo=-(2 ** 61))
+    for name, func, arg, alg in [("RANK", W.Rank, None, 24.0), ("LAG(v,1)", W.Lag, v, 24.0)]:
+        def fn():
+            ctx.window(func, [k], [v], [True], arg=arg, param=1).release()
+        wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "window"])
+        t0 = time.perf_counter()
+        ob.window(func, [ob.HostCol(hk)], [ob.HostCol(hv)], [True], arg=ob.HostCol(hv) if arg is not None else None,
+                  param=1)
+        dt = time.perf_counter() - t0
+        cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows, {dt:.2f} s"}
+        line(f"window {name} 1e9", n, wall, alg * n, sum(kt.values()), "radix sort + k_seg_start/k_window_out", cpu, kt)
 
 
 def cfg_outer(ctx, scale, jt=1):
@@ -373,7 +394,7 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition, "cfg3w": cfg3_wide}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
