@@ -301,6 +301,25 @@ class DistributedExecutor:
         back, _ = self._exchange_columns([rn], recv_counts)  # reverse: return what each source sent
         return self.ctx.scatter(back[0], perm)
 
+    def window(self, func: int, part_keys: Sequence[DeviceColumn], order_keys: Sequence[DeviceColumn],
+               ascending: Sequence[bool], arg: Optional[DeviceColumn] = None, param: int = 0,
+               default=None) -> DeviceColumn:
+        """Any ``WindowFunctionType`` OVER (PARTITION BY .. ORDER BY ..) over rank-sharded rows,
+        placed like ``row_number``: hash shuffle by the first partition key (with the order keys
+        and the argument), ``qeh_window`` on the owning rank, reverse all-to-all, then a gather
+        through the inverse permutation (the results of LAG/LEAD/… carry NULLs)."""
+        if not part_keys:
+            raise ValueError("distributed window functions need a PARTITION BY key")
+        counts, perm = self.ctx.hash_partition(part_keys[0], self.world)
+        cols = list(part_keys) + list(order_keys) + ([arg] if arg is not None else [])
+        recv, recv_counts = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
+        npk, nok = len(part_keys), len(order_keys)
+        res = self.ctx.window(func, recv[:npk], recv[npk:npk + nok], list(ascending),
+                              arg=recv[npk + nok] if arg is not None else None, param=param, default=default)
+        back, _ = self._exchange_columns([res], recv_counts)
+        inv = self.ctx.scatter(self.ctx.upload(np.arange(len(part_keys[0]), dtype=np.uint32)), perm)
+        return self.ctx.take(back[0], inv)
+
     def sort(self, cols: Sequence[DeviceColumn], key_idx: Sequence[int], ascending: Sequence[bool],
              samples_per_rank: int = 4096) -> List[DeviceColumn]:
         """ORDER BY over rank-sharded rows: range-partition on the first sort key

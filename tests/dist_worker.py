@@ -210,6 +210,23 @@ def mode_gpu(rank, world):
         V = np.concatenate([win(r)[2] for r in range(world)])
         want = ob.row_number([ob.HostCol(K, M)], [ob.HostCol(V)], [False])
         assert np.array_equal(res[0][0], want)
+    # --- distributed RANK and LAG(w, 2, default) (same placement as ROW_NUMBER)
+    from qe_hip.plan import WindowFunctionType as WF
+    ww_ = np.random.default_rng(170 + rank).normal(size=len(wk_))
+    wwm_ = np.random.default_rng(171 + rank).random(len(wk_)) > 0.1
+    rk = dx.window(WF.Rank, [ctx.upload(wk_, wm_)], [ctx.upload(wv_)], [False])
+    lg = dx.window(WF.Lag, [ctx.upload(wk_, wm_)], [ctx.upload(wv_)], [True], arg=ctx.upload(ww_, wwm_), param=2,
+                   default=0.25)
+    res = dx.gather_to_root([rk, lg])
+    if rank == 0:
+        WW = np.concatenate([np.random.default_rng(170 + r).normal(size=len(win(r)[0])) for r in range(world)])
+        WM = np.concatenate([np.random.default_rng(171 + r).random(len(win(r)[0])) > 0.1 for r in range(world)])
+        want_rk, _ = ob.window(WF.Rank, [ob.HostCol(K, M)], [ob.HostCol(V)], [False])
+        assert np.array_equal(res[0][0], want_rk)
+        want_lv, want_ok = ob.window(WF.Lag, [ob.HostCol(K, M)], [ob.HostCol(V)], [True], arg=ob.HostCol(WW, WM),
+                                     param=2, default=0.25)
+        assert np.array_equal(res[1][1], want_ok)
+        assert np.array_equal(res[1][0][want_ok], want_lv[want_ok])
     # --- distributed ORDER BY (sampled range partition, stable local sort)
     def srt(r):
         g = np.random.default_rng(90 + r)
