@@ -527,8 +527,64 @@ int build_group_table(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int64_t 
 }
 
 // Dense ids 0..G-1 in slot order and a representative row per group.
+// Small tables: occupancy, exclusive scan, dense ids, representative rows and the group count in
+// one workgroup.  Under the prelaunched phase A the separate single-workgroup scan kernel
+// (k_scan_top) was held for the whole of phase A, and the build behind it with it.
+constexpr int kSmallFinishPer = 16;
+constexpr uint64_t kSmallFinish = (uint64_t)kBlock * kSmallFinishPer;
+
+__global__ __launch_bounds__(kBlock) void k_group_finish_small(const uint32_t *__restrict__ slots, uint64_t cap,
+                                                               uint64_t *__restrict__ dense, uint32_t *__restrict__ rep_row,
+                                                               uint64_t *__restrict__ total) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t s[kSmallFinishPer], cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kSmallFinishPer; ++j) {
+        const uint64_t i = (uint64_t)t * kSmallFinishPer + j;
+        s[j] = i < cap ? slots[i] : kEmpty32;
+        cnt += s[j] != kEmpty32;
+    }
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+    uint32_t ex = base + incl - cnt;
+#pragma unroll
+    for (int j = 0; j < kSmallFinishPer; ++j) {
+        const uint64_t i = (uint64_t)t * kSmallFinishPer + j;
+        if (i >= cap) break;
+        dense[i] = ex;
+        if (s[j] != kEmpty32) rep_row[ex++] = s[j];
+    }
+    if (t == kBlock - 1) {
+        uint32_t g = 0;
+        for (int q = 0; q < kBlock / 64; ++q) g += wsum[q];
+        *total = g;
+    }
+}
+
 static int group_table_finish(qeh_ctx *ctx, GroupTable *out) {
     const uint64_t cap = out->cap;
+    if (cap <= kSmallFinish && !std::getenv("QEH_NO_SMALL_FINISH")) {
+        QEH_TRY(out->dense.alloc(ctx, cap * 8));
+        QEH_TRY(out->rep_row.alloc(ctx, std::max<uint64_t>(cap, 1) * 4));
+        DevBuf tot;
+        QEH_TRY(tot.alloc(ctx, 16));
+        hipLaunchKernelGGL(k_group_finish_small, dim3(1), dim3(kBlock), 0, ctx->stream, out->slots.as<uint32_t>(), cap,
+                           out->dense.as<uint64_t>(), out->rep_row.as<uint32_t>(), tot.as<uint64_t>());
+        QEH_HIP(hipGetLastError());
+        uint64_t G = 0;
+        QEH_TRY(read_small(ctx, &G, tot.p, 8));
+        out->groups = (int64_t)G;
+        return QEH_OK;
+    }
     DevBuf occ;
     QEH_TRY(occ.alloc(ctx, cap * 4));
     QEH_TRY(out->dense.alloc(ctx, cap * 8));
