@@ -362,7 +362,7 @@ struct SliceRegions {
     uint32_t *overflow;   // set when a region fills up (skewed probe keys)
     uint64_t cap;         // items per region, multiple of kSliceChunk
     int32_t F;            // slices
-    int32_t _pad;
+    int32_t pair_flush;   // phase A: flush two items per lane (4-B key, 16-B value stores)
     // exact layout (materialising join): region (workgroup r, slice b) starts at
     // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
     const uint64_t *rbase;
@@ -460,7 +460,50 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         }
         if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
         lds_barrier();  // staged
-        {
+        if (rg.pair_flush) {
+            // whole chunks, two consecutive items per lane (one chunk per quarter-wave): the items
+            // of a chunk sit at absolute multiples of CH, so even positions are 4-B / 16-B aligned
+            const uint32_t M = s_chunks;
+            const uint32_t kx0 = (tid & (CH / 2 - 1)) * 2;
+            for (uint32_t c = tid / (CH / 2); c < M; c += kSliceBlock / (CH / 2)) {
+                const uint32_t b = chunk_slice[c];
+                const uint32_t kx = (c - mpre[b]) * CH + kx0, cb = cn[b];
+                uint16_t kv[2];
+                int64_t vv[2] = {0, 0};
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const uint32_t x = kx + q;
+                    if (x < cb) {
+                        kv[q] = c_key[b * CH + x];
+                        if (VC) vv[q] = c_v[b * CH + x];
+                    } else {
+                        kv[q] = st_key[lofs[b] + x - cb];
+                        if (VC) vv[q] = st_v[lofs[b] + x - cb];
+                    }
+                }
+                const uint64_t dst = (uint64_t)pos[b] + kx;
+                const uint64_t o = abase[b] + dst;
+                if (dst >= hd[b] && dst + 1 < cap) {
+                    *(uint32_t *)(rg.key + o) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
+                    if (VC) {
+                        v2i64 w;
+                        w[0] = vv[0], w[1] = vv[1];
+                        __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        if (dst + q < hd[b]) continue;  // placeholder ahead of the region's first item
+                        if (dst + q < cap) {
+                            rg.key[o + q] = kv[q];
+                            if (VC) __builtin_nontemporal_store(vv[q], rg.val + o + q);
+                        } else {
+                            ovf = true;
+                        }
+                    }
+                }
+            }
+        } else {
             // whole chunks: carried items first, then this tile's; one chunk per half-wave
             const uint32_t M = s_chunks;
             const uint32_t kx0 = tid & (CH - 1);
@@ -1461,8 +1504,10 @@ static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, i
 }
 
 static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol, int64_t kmin,
-                                   uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg, hipStream_t stream) {
+                                   uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg_in, hipStream_t stream) {
     const bool nt = fast_nt_mode() == 1;
+    SliceRegions rg = rg_in;
+    rg.pair_flush = std::getenv("QEH_SLICE_SINGLE_FLUSH") ? 0 : 1;
     KernelTimer kta(ctx, "slice_partition", stream);
 #define QEH_SA(NTV, NAV, NTB)                                                                                  \
     hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in, \
