@@ -374,7 +374,11 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                                                                  int64_t n_tiles, SliceRegions rg) {
     constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
     constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
-    __shared__ uint32_t cnt[MAXF], lofs[MAXF], cn[MAXF], pos[MAXF], mpre[MAXF], hd[MAXF];
+    // per-slice tile counts, carried item counts and region write positions are double-buffered:
+    // tile t reads one copy while the next tile's copy is written, so no barrier ends the tile
+    __shared__ uint32_t cntb[2][MAXF], cnb[2][MAXF], posb[2][MAXF], lofs[MAXF], mpre[MAXF], hd[MAXF];
+    uint32_t *cnt = cntb[0], *cn = cnb[0], *pos = posb[0];
+    uint32_t *cnt_n = cntb[1], *cn_n = cnb[1], *pos_n = posb[1];
     __shared__ uint64_t abase[MAXF];  // region start, aligned down to a whole chunk (exact layout)
     __shared__ uint32_t s_chunks;
     __shared__ uint16_t chunk_slice[TILE / CH + MAXF];
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t region0 = (uint64_t)blockIdx.x * F;
     for (int i = tid; i < MAXF; i += kSliceBlock) {
-        cnt[i] = 0, pos[i] = 0, hd[i] = 0, abase[i] = 0;
+        cnt[i] = 0, cnt_n[i] = 0, pos[i] = 0, hd[i] = 0, abase[i] = 0;
         if (i < F) {
             // exact layout: regions start anywhere; chunks stay aligned to absolute multiples
             // of CH items by starting each region h = start % CH placeholder items early (never
@@ -455,8 +459,12 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             if (VC) st_v[s] = vcur[r];
         }
         if (tid < F) {
-            const uint32_t m = (cn[tid] + cnt[tid]) / CH, m0 = mpre[tid];
+            const uint32_t T = cn[tid] + cnt[tid], m = T / CH, m0 = mpre[tid];
             for (uint32_t j = 0; j < m; ++j) chunk_slice[m0 + j] = (uint16_t)tid;
+            // next tile's state (its copies were last read before this tile's first barrier)
+            pos_n[tid] = pos[tid] + m * CH;
+            cn_n[tid] = T % CH;
+            cnt_n[tid] = 0;
         }
         if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
         lds_barrier();  // staged
@@ -547,13 +555,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             }
         }
         lds_barrier();  // carries updated
-        if (tid < F) {
-            const uint32_t T = cn[tid] + cnt[tid];
-            pos[tid] += (T / CH) * CH;
-            cn[tid] = T % CH;
-            cnt[tid] = 0;
-        }
-        lds_barrier();
+        uint32_t *t0 = cnt, *t1 = cn, *t2 = pos;
+        cnt = cnt_n, cn = cn_n, pos = pos_n;
+        cnt_n = t0, cn_n = t1, pos_n = t2;
     }
     for (int p = tid; p < F * CH; p += kSliceBlock) {  // partial last chunks
         const int b = p / CH, kx = p % CH;
