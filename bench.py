@@ -45,34 +45,86 @@ def parse():
     ap.add_argument("--dim", type=int, default=10_000_000)
     ap.add_argument("--groups", type=int, default=1024)
     ap.add_argument("--threshold", type=int, default=49, help="WHERE f.x > threshold (49 = the BASELINE query)")
-    ap.add_argument("--cpu-sample", type=int, default=100_000_000, help="fact rows for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=100_000_000,
+                    help="fact rows for the 1-thread CPU baseline (0 = skip the CPU baseline)")
+    ap.add_argument("--cpu-sample-mt", type=int, default=400_000_000, help="fact rows for the all-cores CPU baseline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch of the probe kernel (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads() -> int:
+    """Threads for the all-cores leg: this process's CPU share (the GPU box sets
+    OMP_NUM_THREADS to it; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
+
+
 def cpu_baseline(args):
-    """Oracle (C restatement of the reference executor semantics) on a bounded
-    sample: the full dim table and the first `cpu-sample` fact rows, 1 thread."""
+    """The metric query on the host CPU, same run, same box, two variants:
+      * 1 thread: the oracle's line-by-line restatement of the reference executor
+        (qo_join_filter_aggregate; executor.rs is single-threaded, rayon unused) over the full
+        dim table and the first `cpu-sample` fact rows;
+      * all cores: qo_join_filter_aggregate_mt (OpenMP) over `cpu-sample-mt` fact rows.
+    Both from oracle/_native/liboracle.so built with -march=native on this host when gcc is
+    available (else the portable x86-64-v2 build).  `value` is the all-cores figure."""
     if args.cpu_sample <= 0:
         return None
+    import subprocess
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    native = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL).returncode == 0
     import oracle_bind as ob
+    native = native and ob.use_native()
     from qe_hip import AggregateFunction as AF, BinaryOp, abi, binop, col, lit
-    n = args.cpu_sample
-    x = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
-    k = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, args.dim)
-    v = ob.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    pred = binop(col(0), BinaryOp.Greater, lit(args.threshold))
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
     dk = ob.generate(abi.GEN_PERMUTATION, SEED, 0, args.dim, args.dim)
     dg = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 5, args.dim, args.groups)
-    pred = binop(col(0), BinaryOp.Greater, lit(49))
+
+    def fact(n):
+        return [ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)),
+                ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, args.dim)),
+                ob.HostCol(ob.generate(abi.GEN_UNIT_F64, SEED, 3, n))]
+
+    build = "-O3 -march=native (built on this host)" if native else "-O3 -march=x86-64-v2 (portable build)"
+    threads = host_threads()
+    out = {"unit": "rows/s", "kind": "port", "cpu_model": cpu_model(), "host_cpus_nproc": os.cpu_count()}
+    n1 = args.cpu_sample
+    f = fact(n1)
     t0 = time.perf_counter()
-    ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, pred, ob.HostCol(dk),
-                             [ob.HostCol(dg)], [(AF.Sum, 2), (AF.Count, 2)])
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate, 1 thread, {n} fact rows x {args.dim} dim rows "
-                      f"(build included), {dt:.2f} s"}
+    ob.join_filter_aggregate(f, 1, pred, ob.HostCol(dk), [ob.HostCol(dg)], aggs)
+    dt1 = time.perf_counter() - t0
+    del f
+    single = {"value": n1 / dt1, "cores": 1,
+              "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate (line-by-line restatement of executor.rs, "
+                        f"1 thread), {n1} fact rows x {args.dim} dim rows, build included, {dt1:.2f} s, {build}"}
+    nm = args.cpu_sample_mt
+    f = fact(nm)
+    ob.join_filter_aggregate_mt(f, 1, pred, ob.HostCol(dk), [ob.HostCol(dg)], aggs, threads)  # page in
+    t0 = time.perf_counter()
+    ob.join_filter_aggregate_mt(f, 1, pred, ob.HostCol(dk), [ob.HostCol(dg)], aggs, threads)
+    dtm = time.perf_counter() - t0
+    del f
+    out.update({"value": nm / dtm, "cores": threads,
+                "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate_mt (OpenMP, {threads} threads = this "
+                          f"process's CPU share of {os.cpu_count()} host CPUs), {nm} fact rows x {args.dim} dim rows, "
+                          f"build included, {dtm:.2f} s, {build}",
+                "single_thread": single})
+    return out
 
 
 def torch_device_count():

@@ -36,6 +36,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 static __thread char g_err[512];
 
@@ -67,6 +70,7 @@ static uint64_t splitmix64(uint64_t z) {
 void qo_generate(int kind, uint64_t seed, uint64_t col_id, int64_t row0, int64_t n, int64_t modulus,
                  int64_t lo, void *out) {
     const uint64_t base = seed ^ (col_id << 56);
+#pragma omp parallel for schedule(static, 1 << 16) if (n > (1 << 22))
     for (int64_t i = 0; i < n; ++i) {
         uint64_t row = (uint64_t)(row0 + i);
         if (kind == QEH_GEN_UNIFORM_MOD)
@@ -828,6 +832,351 @@ int qo_join_filter_aggregate(const qo_col *probe_cols, int n_probe, int probe_ke
     for (int j = 0; j < n_probe; ++j) arr_free(&ia[j]);
     for (int j = 0; j < n_group_keys; ++j) arr_free(&gk[j]);
     free(ia);
+    free(gk);
+    return s;
+}
+
+/* ---- literal Cartesian joins and joins on an arbitrary `on` ------------------------- */
+static int gather_side(const qo_col *cols, int n, const int64_t *idx, int64_t m, qo_col *out) {
+    int s = QEH_OK;
+    for (int j = 0; j < n && s == QEH_OK; ++j) {
+        arr a;
+        s = col_to_arr(&cols[j], &a);
+        if (s == QEH_OK) { arr_to_col(&a, idx, m, &out[j]); arr_free(&a); }
+    }
+    return s;
+}
+
+/* join_batches (executor.rs:500-540), the reference's INNER / LEFT / RIGHT / FULL join
+ * (executor.rs:363-435, `on` unused): left row li is repeated right_rows times
+ * (left row-major), right rows cycle; schema = left fields ++ right fields.  An empty side
+ * yields no batch at all (executor.rs:350-352): *out_rows = -1 then. */
+int qo_join_batches(const qo_col *left, int nl, const qo_col *right, int nr, qo_col *out, int64_t *out_rows) {
+    const int64_t L = nl > 0 ? left[0].length : 0, R = nr > 0 ? right[0].length : 0;
+    if (L == 0 || R == 0) { *out_rows = -1; return QEH_OK; }
+    const int64_t m = L * R;
+    int64_t *li = malloc((size_t)m * sizeof(int64_t)), *ri = malloc((size_t)m * sizeof(int64_t));
+    for (int64_t l = 0, k = 0; l < L; ++l)      /* executor.rs:509-513 */
+        for (int64_t r = 0; r < R; ++r, ++k) li[k] = l;
+    for (int64_t l = 0, k = 0; l < L; ++l)      /* executor.rs:522-526 */
+        for (int64_t r = 0; r < R; ++r, ++k) ri[k] = r;
+    int s = gather_side(left, nl, li, m, out);
+    if (s == QEH_OK) s = gather_side(right, nr, ri, m, out + nl);
+    free(li);
+    free(ri);
+    *out_rows = m;
+    return s;
+}
+
+/* execute_cross_join (executor.rs:437-498): the left index cycles fastest (for each right
+ * row, every left row: executor.rs:455-459, 470-474), i.e. right row-major. */
+int qo_cross_join(const qo_col *left, int nl, const qo_col *right, int nr, qo_col *out, int64_t *out_rows) {
+    const int64_t L = nl > 0 ? left[0].length : 0, R = nr > 0 ? right[0].length : 0;
+    if (L == 0 || R == 0) { *out_rows = -1; return QEH_OK; }
+    const int64_t m = L * R;
+    int64_t *li = malloc((size_t)m * sizeof(int64_t)), *ri = malloc((size_t)m * sizeof(int64_t));
+    for (int64_t r = 0, k = 0; r < R; ++r)
+        for (int64_t l = 0; l < L; ++l, ++k) { li[k] = l; ri[k] = r; }
+    int s = gather_side(left, nl, li, m, out);
+    if (s == QEH_OK) s = gather_side(right, nr, ri, m, out + nl);
+    free(li);
+    free(ri);
+    *out_rows = m;
+    return s;
+}
+
+/* Join on an arbitrary boolean `on` over the concatenated schema (planner.rs:148-157 resolves
+ * its column indices there) — the intended semantics of SURVEY.md §8.0 generalised from the
+ * equi-join: the pairs of join_batches' Cartesian product (left row-major) on which `on` is
+ * TRUE (NULL = not a match); LEFT / FULL add each left row without a match (right side NULL)
+ * at its place in left-row order, FULL then the unmatched right rows in right-row order;
+ * RIGHT is the mirror image (right-row order).  `on` is evaluated literally, column at a
+ * time, over blocks of the Cartesian product (O(L*R): small inputs only). */
+int qo_join_on(int join_type, const qo_col *left, int nl, const qo_col *right, int nr, const qeh_expr_node *on,
+               int n_on, qo_col *out_left, qo_col *out_right, int64_t *out_rows) {
+    if (join_type < 0 || join_type > 3) return err(QEH_E_INVALID, "join type must be INNER, LEFT, RIGHT or FULL");
+    const int64_t L = nl > 0 ? left[0].length : 0, R = nr > 0 ? right[0].length : 0;
+    int s = QEH_OK;
+    arr *la = calloc((size_t)nl + 1, sizeof(arr)), *ra = calloc((size_t)nr + 1, sizeof(arr));
+    for (int j = 0; j < nl && s == QEH_OK; ++j) s = col_to_arr(&left[j], &la[j]);
+    for (int j = 0; j < nr && s == QEH_OK; ++j) s = col_to_arr(&right[j], &ra[j]);
+    /* match[l * R + r] for the TRUE pairs, evaluated over blocks of left rows */
+    uint8_t *match = calloc((size_t)(L * R > 0 ? L * R : 1), 1);
+    const int64_t blk = R > 0 ? (((int64_t)1 << 20) / R > 0 ? ((int64_t)1 << 20) / R : 1) : 1;
+    qo_col *tmp = calloc((size_t)(nl + nr) + 1, sizeof(qo_col));
+    int64_t *li = malloc((size_t)(blk * R > 0 ? blk * R : 1) * sizeof(int64_t));
+    int64_t *ri = malloc((size_t)(blk * R > 0 ? blk * R : 1) * sizeof(int64_t));
+    for (int64_t l0 = 0; l0 < L && R > 0 && s == QEH_OK; l0 += blk) {
+        const int64_t l1 = l0 + blk < L ? l0 + blk : L, m = (l1 - l0) * R;
+        for (int64_t l = l0, k = 0; l < l1; ++l)
+            for (int64_t r = 0; r < R; ++r, ++k) { li[k] = l; ri[k] = r; }
+        for (int j = 0; j < nl; ++j) arr_to_col(&la[j], li, m, &tmp[j]);
+        for (int j = 0; j < nr; ++j) arr_to_col(&ra[j], ri, m, &tmp[nl + j]);
+        arr p;
+        s = eval_arr(tmp, nl + nr, m, on, n_on, &p);
+        for (int j = 0; j < nl + nr; ++j) qo_col_free(&tmp[j]);
+        if (s != QEH_OK) break;
+        if (p.t != QEH_DT_BOOL) { arr_free(&p); s = err(QEH_E_TYPE, "join condition must return boolean"); break; }
+        for (int64_t k = 0; k < m; ++k) match[l0 * R + k] = p.v[k] && p.i[k];
+        arr_free(&p);
+    }
+    free(tmp);
+    free(li);
+    free(ri);
+    if (s == QEH_OK) {
+        int64_t cap = L + R + 16, cnt = 0;
+        int64_t *pl = malloc((size_t)cap * sizeof(int64_t)), *pr = malloc((size_t)cap * sizeof(int64_t));
+        if (join_type == 2) { /* RIGHT: right-row order */
+            for (int64_t r = 0; r < R; ++r) {
+                int any = 0;
+                for (int64_t l = 0; l < L; ++l)
+                    if (match[l * R + r]) { pairs_push(&pl, &pr, &cnt, &cap, l, r); any = 1; }
+                if (!any) pairs_push(&pl, &pr, &cnt, &cap, -1, r);
+            }
+        } else {
+            uint8_t *hit = calloc((size_t)R + 1, 1);
+            for (int64_t l = 0; l < L; ++l) {
+                int any = 0;
+                for (int64_t r = 0; r < R; ++r)
+                    if (match[l * R + r]) { pairs_push(&pl, &pr, &cnt, &cap, l, r); hit[r] = 1; any = 1; }
+                if (!any && join_type != 0) pairs_push(&pl, &pr, &cnt, &cap, l, -1);
+            }
+            if (join_type == 3)
+                for (int64_t r = 0; r < R; ++r)
+                    if (!hit[r]) pairs_push(&pl, &pr, &cnt, &cap, -1, r);
+            free(hit);
+        }
+        for (int j = 0; j < nl; ++j) arr_to_col(&la[j], pl, cnt, &out_left[j]);
+        for (int j = 0; j < nr; ++j) arr_to_col(&ra[j], pr, cnt, &out_right[j]);
+        *out_rows = cnt;
+        free(pl);
+        free(pr);
+    }
+    free(match);
+    for (int j = 0; j < nl; ++j) arr_free(&la[j]);
+    for (int j = 0; j < nr; ++j) arr_free(&ra[j]);
+    free(la);
+    free(ra);
+    return s;
+}
+
+/* ---- all-cores CPU baseline of the metric query ----------------------------------------
+ * Same semantics as qo_join_filter_aggregate (HashAggregate(Filter(HashJoin)) with the
+ * filter over probe columns and group keys from the build side), restructured for T host
+ * threads (OpenMP): the build side is grouped and inserted into shared open-addressing
+ * tables with CAS (group ids then renumbered in build-row order of first appearance), the
+ * probe side is split into chunks of rows, each chunk's predicate evaluated over column
+ * slices, and every thread aggregates into its own state table; the states are merged in
+ * thread order.  Float sums therefore add in a different order (within the 1e-6 bound).
+ * The reference executor itself is single-threaded (rayon unused, Cargo.toml:18): this is a
+ * baseline for the host's cores, not a restatement of its execution order. */
+static void agg_merge(astate *d, const astate *s, int is_f) {
+    if (!s->cnt) return;
+    if (!d->cnt) { *d = *s; return; }
+    d->isum += s->isum;
+    d->fsum += s->fsum;
+    d->f32sum += s->f32sum;
+    if (is_f) {
+        if (tkey(s->fmin) < tkey(d->fmin)) d->fmin = s->fmin;
+        if (tkey(s->fmax) > tkey(d->fmax)) d->fmax = s->fmax;
+    } else {
+        if (s->imin < d->imin) d->imin = s->imin;
+        if (s->imax > d->imax) d->imax = s->imax;
+    }
+    d->cnt += s->cnt;
+}
+
+static int cmp_i64(const void *x, const void *y) {
+    const int64_t p = *(const int64_t *)x, q = *(const int64_t *)y;
+    return p < q ? -1 : p > q;
+}
+
+static qo_col col_slice(const qo_col *c, int64_t r0, int64_t n) {
+    qo_col o = *c;
+    o.length = n;
+    o.values = (char *)c->values + (size_t)r0 * esize(c->dtype);
+    if (c->valid) o.valid = c->valid + r0;
+    return o;
+}
+
+int qo_join_filter_aggregate_mt(const qo_col *probe_cols, int n_probe, int probe_key_idx, const qeh_expr_node *pred,
+                                int n_pred, const qo_col *build_key, const qo_col *build_group_keys, int n_group_keys,
+                                const qeh_agg *aggs, int n_aggs, int threads, qo_col *out_keys, qo_col *out_aggs,
+                                int64_t *out_groups) {
+    *out_groups = 0;
+    if (n_aggs == 0) return QEH_OK;
+    if (threads < 1) threads = 1;
+    const int64_t n = n_probe > 0 ? probe_cols[0].length : 0, nb = build_key->length;
+    int s = QEH_OK;
+    arr bk;
+    arr *gk = calloc((size_t)n_group_keys + 1, sizeof(arr));
+    s = join_key_arr(build_key, &bk);
+    for (int j = 0; j < n_group_keys && s == QEH_OK; ++j) s = col_to_arr(&build_group_keys[j], &gk[j]);
+    if (probe_cols[probe_key_idx].dtype != QEH_DT_INT64 && probe_cols[probe_key_idx].dtype != QEH_DT_INT32)
+        s = err(QEH_E_UNSUPPORTED, "oracle: join keys must be Int32/Int64");
+    for (int a = 0; a < n_aggs && s == QEH_OK; ++a) {
+        if (aggs[a].column < 0 || aggs[a].column >= n_probe) s = err(QEH_E_INVALID, "aggregate input index out of range");
+        else if (aggs[a].func != QEH_AGG_COUNT && !is_num(probe_cols[aggs[a].column].dtype))
+            s = err(QEH_E_TYPE, "Unsupported type for aggregate");
+    }
+    if (s != QEH_OK) {
+        arr_free(&bk);
+        for (int j = 0; j < n_group_keys; ++j) arr_free(&gk[j]);
+        free(gk);
+        return s;
+    }
+    /* build: group slots (CAS on representative row + 1), then dense ids in build-row order */
+    uint64_t gcap = 1024, jcap = 1024;
+    while (gcap < (uint64_t)nb * 2) gcap <<= 1;
+    while (jcap < (uint64_t)nb * 2) jcap <<= 1;
+    int64_t *gslot = calloc(gcap, sizeof(int64_t));     /* 0 = empty, else rep row + 1 */
+    int64_t *gid = malloc((size_t)(nb > 0 ? nb : 1) * sizeof(int64_t));
+    int64_t *jhead = malloc(jcap * sizeof(int64_t));   /* -1 = empty */
+    int64_t *jkey = malloc(jcap * sizeof(int64_t));
+    int64_t *jnext = malloc((size_t)(nb > 0 ? nb : 1) * sizeof(int64_t));
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (uint64_t i = 0; i < jcap; ++i) jhead[i] = -1;
+#pragma omp parallel for num_threads(threads) schedule(static, 65536)
+    for (int64_t r = 0; r < nb; ++r) {
+        uint64_t h = tuple_hash(gk, n_group_keys, r) & (gcap - 1);
+        for (;;) {
+            int64_t cur = __atomic_load_n(&gslot[h], __ATOMIC_ACQUIRE);
+            if (cur == 0) {
+                int64_t want = 0;
+                if (__atomic_compare_exchange_n(&gslot[h], &want, r + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                    gid[r] = (int64_t)h;
+                    break;
+                }
+                cur = want;
+            }
+            if (tuple_eq(gk, cur - 1, gk, r, n_group_keys)) { gid[r] = (int64_t)h; break; }
+            h = (h + 1) & (gcap - 1);
+        }
+        /* join table: key slot by CAS on the head (key written before publication) */
+        jnext[r] = -1;
+        if (!bk.v[r]) continue;
+        const int64_t k = bk.i[r];
+        uint64_t q = mix((uint64_t)k) & (jcap - 1);
+        for (;;) {
+            int64_t hd = __atomic_load_n(&jhead[q], __ATOMIC_ACQUIRE);
+            if (hd == -1) { /* claim the empty slot (-2 = key being written), then publish */
+                int64_t want = -1;
+                if (__atomic_compare_exchange_n(&jhead[q], &want, -2, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                    jkey[q] = k;
+                    __atomic_store_n(&jhead[q], r, __ATOMIC_RELEASE);
+                    break;
+                }
+                hd = want;
+            }
+            while (hd == -2) hd = __atomic_load_n(&jhead[q], __ATOMIC_ACQUIRE); /* slot being published */
+            if (jkey[q] == k) { /* push onto the chain */
+                int64_t old = __atomic_load_n(&jhead[q], __ATOMIC_ACQUIRE);
+                do { jnext[r] = old; } while (!__atomic_compare_exchange_n(&jhead[q], &old, r, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE));
+                break;
+            }
+            q = (q + 1) & (jcap - 1);
+        }
+    }
+    /* dense group ids: slots ordered by their representative row (first appearance) */
+    int64_t G0 = 0;
+    for (uint64_t i = 0; i < gcap; ++i) if (gslot[i]) ++G0;
+    int64_t *slot_rep = malloc((size_t)(G0 > 0 ? G0 : 1) * sizeof(int64_t));
+    int64_t *dense = malloc(gcap * sizeof(int64_t));
+    for (uint64_t i = 0, g = 0; i < gcap; ++i) if (gslot[i]) slot_rep[g++] = gslot[i] - 1;
+    qsort(slot_rep, (size_t)G0, sizeof(int64_t), cmp_i64);
+    for (int64_t g = 0; g < G0; ++g) {
+        const int64_t r = slot_rep[g];
+        dense[gid[r]] = g;
+    }
+#pragma omp parallel for num_threads(threads) schedule(static, 65536)
+    for (int64_t r = 0; r < nb; ++r) gid[r] = dense[gid[r]];
+    /* probe: chunks of rows, thread-private states */
+    const int64_t chunk = 1 << 16;
+    const int64_t nchunks = (n + chunk - 1) / chunk;
+    astate *st = calloc((size_t)threads * (size_t)(G0 > 0 ? G0 : 1) * (size_t)n_aggs, sizeof(astate));
+    int64_t *rows = calloc((size_t)threads * (size_t)(G0 > 0 ? G0 : 1), sizeof(int64_t));
+    int fail_s = QEH_OK;
+#pragma omp parallel num_threads(threads)
+    {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        astate *my = st + (size_t)t * (size_t)(G0 > 0 ? G0 : 1) * (size_t)n_aggs;
+        int64_t *myrows = rows + (size_t)t * (size_t)(G0 > 0 ? G0 : 1);
+        qo_col *sl = calloc((size_t)n_probe + 1, sizeof(qo_col));
+        arr *ia = calloc((size_t)n_probe + 1, sizeof(arr));
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t c = 0; c < nchunks; ++c) {
+            const int64_t r0 = c * chunk, m = r0 + chunk < n ? chunk : n - r0;
+            for (int j = 0; j < n_probe; ++j) sl[j] = col_slice(&probe_cols[j], r0, m);
+            arr pm;
+            int ls = QEH_OK, have = pred && n_pred > 0;
+            if (have) {
+                ls = eval_arr(sl, n_probe, m, pred, n_pred, &pm);
+                if (ls == QEH_OK && pm.t != QEH_DT_BOOL) { arr_free(&pm); ls = QEH_E_TYPE; }
+            }
+            if (ls != QEH_OK) { fail_s = ls; continue; }
+            for (int j = 0; j < n_probe; ++j) col_to_arr(&sl[j], &ia[j]);
+            const arr *pk = &ia[probe_key_idx];
+            for (int64_t r = 0; r < m; ++r) {
+                if (!pk->v[r]) continue;
+                if (have && !(pm.v[r] && pm.i[r])) continue;
+                const int64_t k = pk->i[r];
+                uint64_t q = mix((uint64_t)k) & (jcap - 1);
+                int64_t b = -1;
+                while (jhead[q] >= 0) {
+                    if (jkey[q] == k) { b = jhead[q]; break; }
+                    q = (q + 1) & (jcap - 1);
+                }
+                for (; b >= 0; b = jnext[b]) {
+                    const int64_t g = gid[b];
+                    myrows[g]++;
+                    for (int a = 0; a < n_aggs; ++a) agg_update(&my[g * n_aggs + a], &ia[aggs[a].column], r);
+                }
+            }
+            for (int j = 0; j < n_probe; ++j) arr_free(&ia[j]);
+            if (have) arr_free(&pm);
+        }
+        free(sl);
+        free(ia);
+    }
+    if (fail_s != QEH_OK) {
+        s = fail_s == QEH_E_TYPE ? err(QEH_E_TYPE, "Filter predicate must return boolean") : fail_s;
+    } else {
+        /* merge in thread order; groups without a joined row do not exist in the result */
+        astate *fin = calloc((size_t)(G0 > 0 ? G0 : 1) * (size_t)n_aggs, sizeof(astate));
+        int64_t *rep = malloc((size_t)(G0 > 0 ? G0 : 1) * sizeof(int64_t));
+        int64_t G = 0;
+        arr *ia = calloc((size_t)n_probe + 1, sizeof(arr));
+        for (int j = 0; j < n_probe; ++j) ia[j].t = probe_cols[j].dtype;
+        for (int64_t g = 0; g < G0; ++g) {
+            int64_t cnt = 0;
+            for (int t = 0; t < threads; ++t) cnt += rows[(size_t)t * (size_t)G0 + g];
+            if (!cnt) continue;
+            for (int a = 0; a < n_aggs; ++a)
+                for (int t = 0; t < threads; ++t)
+                    agg_merge(&fin[G * n_aggs + a], &st[((size_t)t * (size_t)G0 + g) * n_aggs + a],
+                              is_float(probe_cols[aggs[a].column].dtype));
+            rep[G++] = slot_rep[g];
+        }
+        emit_groups(gk, n_group_keys, ia, aggs, n_aggs, G, rep, fin, out_keys, out_aggs);
+        *out_groups = G;
+        free(ia);
+        free(fin);
+        free(rep);
+    }
+    free(st);
+    free(rows);
+    free(slot_rep);
+    free(dense);
+    free(gslot);
+    free(gid);
+    free(jhead);
+    free(jkey);
+    free(jnext);
+    arr_free(&bk);
+    for (int j = 0; j < n_group_keys; ++j) arr_free(&gk[j]);
     free(gk);
     return s;
 }

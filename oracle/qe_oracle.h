@@ -60,6 +60,21 @@ int qo_join_filter_aggregate(const qo_col *probe_cols, int n_probe, int probe_ke
                              const qeh_expr_node *pred, int n_pred, const qo_col *build_key,
                              const qo_col *build_group_keys, int n_group_keys, const qeh_agg *aggs,
                              int n_aggs, qo_col *out_keys, qo_col *out_aggs, int64_t *out_groups);
+/* literal Cartesian joins: join_batches (executor.rs:500-540, left row-major; the reference's
+ * INNER/LEFT/RIGHT/FULL) and execute_cross_join (executor.rs:437-498, right row-major).
+ * out = left columns then right columns; *out_rows = -1 when a side is empty (no batch). */
+int qo_join_batches(const qo_col *left, int nl, const qo_col *right, int nr, qo_col *out, int64_t *out_rows);
+int qo_cross_join(const qo_col *left, int nl, const qo_col *right, int nr, qo_col *out, int64_t *out_rows);
+/* join on an arbitrary boolean `on` over left ++ right columns; join_type 0 INNER, 1 LEFT,
+ * 2 RIGHT, 3 FULL (the intended semantics) */
+int qo_join_on(int join_type, const qo_col *left, int nl, const qo_col *right, int nr, const qeh_expr_node *on,
+               int n_on, qo_col *out_left, qo_col *out_right, int64_t *out_rows);
+/* all-cores CPU baseline of qo_join_filter_aggregate (OpenMP, `threads` threads) */
+int qo_join_filter_aggregate_mt(const qo_col *probe_cols, int n_probe, int probe_key_idx,
+                                const qeh_expr_node *pred, int n_pred, const qo_col *build_key,
+                                const qo_col *build_group_keys, int n_group_keys, const qeh_agg *aggs,
+                                int n_aggs, int threads, qo_col *out_keys, qo_col *out_aggs,
+                                int64_t *out_groups);
 int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int64_t n_rows,
                     uint32_t *out_perm);
 int qo_sort_indices_nulls(const qo_col *keys, int n_keys, const int8_t *ascending, const int8_t *nulls_first,

@@ -477,7 +477,7 @@ extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t 
     const size_t fields = sr.table(schema_msg.header, 1);
     const uint32_t nf = fields ? sr.vec_len(fields) : 0;
     if (!sr.ok) return fail(QEH_E_INVALID, "ipc: malformed schema");
-    if ((int)nf > max_cols) return fail(QEH_E_INVALID, "ipc: more columns than out_cols holds");
+    if (max_cols < 0 || nf > (uint32_t)max_cols) return fail(QEH_E_INVALID, "ipc: more columns than out_cols holds");
     std::vector<int> dts(nf);
     std::string names;
     for (uint32_t i = 0; i < nf; ++i) {
@@ -509,7 +509,7 @@ extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t 
         if (bi >= nb) return fail(QEH_E_INVALID, "ipc: too few buffers");
         const size_t at = bufs + 4 + 16 * (size_t)bi++;
         const int64_t off = br.rd<int64_t>(at), l = br.rd<int64_t>(at + 8);
-        if (!br.ok || off < 0 || l < 0 || off + l > bm.body_len) return fail(QEH_E_INVALID, "ipc: buffer outside the body");
+        if (!br.ok || off < 0 || l < 0 || off > (int64_t)bm.body_len || l > (int64_t)bm.body_len - off) return fail(QEH_E_INVALID, "ipc: buffer outside the body");
         *p = bm.body + off;
         *len = l;
         return QEH_OK;

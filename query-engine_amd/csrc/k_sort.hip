@@ -754,11 +754,14 @@ __global__ void k_part_flags(KeyCols part, const uint32_t *__restrict__ perm, in
 }
 
 // single partition key: compare the sorted encodings (coalesced) instead of
-// gathering the key column through the permutation
+// gathering the key column through the permutation.  shift >= the key width means the
+// partition key occupies no bits (one distinct value): only row 0 starts a partition (a shift
+// by the full width would be undefined and the hardware masks it to 0).
 template <typename KeyT>
 __global__ void k_part_flags_enc(const KeyT *__restrict__ enc, int64_t n, uint32_t *__restrict__ flags, int shift = 0) {
+    const bool one_part = shift >= (int)(8 * sizeof(KeyT));
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        flags[i] = i == 0 || (enc[i] >> shift) != (enc[i - 1] >> shift);
+        flags[i] = i == 0 || (!one_part && (enc[i] >> shift) != (enc[i - 1] >> shift));
 }
 
 // Row numbers without materialising partition ids: rn(i) = i - start(i) + 1,
@@ -1278,9 +1281,9 @@ __global__ void k_window_out(WinArgs a, int64_t n, void *__restrict__ out, uint8
             const int64_t size = a.pend[s] - s, r0 = i - s, q = size / a.param, r = size % a.param;
             v = r0 < r * (q + 1) ? r0 / (q + 1) + 1 : r + (r0 - r * (q + 1)) / q + 1;
         } else if (FUNC == QEH_WIN_LAG) {
-            src = i - a.param >= s ? (int64_t)a.perm[i - a.param] : -2;
+            src = a.param <= i - s ? (int64_t)a.perm[i - a.param] : -2;
         } else if (FUNC == QEH_WIN_LEAD) {
-            src = i + a.param < a.pend[s] ? (int64_t)a.perm[i + a.param] : -2;
+            src = a.param < a.pend[s] - i ? (int64_t)a.perm[i + a.param] : -2;  // no i + param overflow
         } else if (FUNC == QEH_WIN_FIRST_VALUE) {
             src = a.perm[s];
         } else {  // LAST_VALUE: the partition's last row (whole-partition frame)
@@ -1398,8 +1401,8 @@ extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_key
         if (n_order > 0) {
             hipLaunchKernelGGL(k_part_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, ok, perm, n, fq.as<uint32_t>());
             hipLaunchKernelGGL(k_or_flags, dim3(grid), dim3(kBlock), 0, ctx->stream, fq.as<uint32_t>(), fp.as<uint32_t>(), n);
-        } else {
-            QEH_HIP(hipMemcpyAsync(fq.p, fp.p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        } else if (hipMemcpyAsync(fq.p, fp.p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) {
+            return bail(fail(QEH_E_HIP, "qeh_window: device copy failed"));
         }
         a.fq = fq.as<uint32_t>();
         if (func == QEH_WIN_RANK) {
@@ -1438,13 +1441,13 @@ extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_key
         default: QEH_WIN(QEH_WIN_LAST_VALUE); break;
     }
 #undef QEH_WIN
-    QEH_HIP(hipGetLastError());
+    if (hipGetLastError() != hipSuccess) return bail(fail(QEH_E_HIP, "qeh_window: kernel launch failed"));
     if (value_fn) {
         int s = qeh_bytes_to_validity(ctx, valid8.as<uint8_t>(), n, out->validity);
         if (s != QEH_OK) return bail(s);
         out->null_count = -1;
     }
-    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return bail(fail(QEH_E_HIP, "qeh_window: stream synchronize failed"));
     return QEH_OK;
 }
 

@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "query-engine_amd"))
 from qe_hip import abi  # noqa: E402  (enum values + expression node struct)
 
 ORACLE_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+NATIVE_PATH = os.path.join(ROOT, "oracle", "_native", "liboracle.so")  # -march=native build (bench.py)
 
 NP_OF = {abi.DT_INT32: np.int32, abi.DT_INT64: np.int64, abi.DT_FLOAT32: np.float32,
          abi.DT_FLOAT64: np.float64, abi.DT_UINT32: np.uint32, abi.DT_BOOL: np.uint8}
@@ -37,6 +38,16 @@ class OracleError(RuntimeError):
 
 
 _lib = None
+
+
+def use_native() -> bool:
+    """Load the -march=native build (bench.py's CPU baseline) instead of the portable one.
+    Must be called before the first oracle call; returns False when it is not built."""
+    global ORACLE_PATH
+    if _lib is None and os.path.exists(NATIVE_PATH):
+        ORACLE_PATH = NATIVE_PATH
+        return True
+    return ORACLE_PATH == NATIVE_PATH
 
 
 def lib():
@@ -168,6 +179,57 @@ def join_filter_aggregate(probe_cols, probe_key_idx, pred, build_key: HostCol, b
                                           ca, len(aggs), ok, oa, C.byref(g)))
     return ([_take(ok[i]) for i in range(len(build_group_keys))], [_take(oa[i]) for i in range(len(aggs))],
             g.value)
+
+
+def join_filter_aggregate_mt(probe_cols, probe_key_idx, pred, build_key: HostCol, build_group_keys, aggs,
+                             threads: int):
+    """qo_join_filter_aggregate_mt: the all-cores (OpenMP) CPU baseline of the metric query."""
+    ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+    ok = (QoCol * max(len(build_group_keys), 1))()
+    oa = (QoCol * max(len(aggs), 1))()
+    g = C.c_int64()
+    if pred is not None:
+        nodes = pred.postfix()
+        na = (abi.QehExprNode * len(nodes))(*nodes)
+        nn = len(nodes)
+    else:
+        na, nn = None, 0
+    _check(lib().qo_join_filter_aggregate_mt(_arr(probe_cols), len(probe_cols), probe_key_idx, na, nn,
+                                             C.byref(build_key.c), _arr(build_group_keys), len(build_group_keys),
+                                             ca, len(aggs), int(threads), ok, oa, C.byref(g)))
+    return ([_take(ok[i]) for i in range(len(build_group_keys))], [_take(oa[i]) for i in range(len(aggs))],
+            g.value)
+
+
+def _cartesian(fn, left, right):
+    out = (QoCol * max(len(left) + len(right), 1))()
+    rows = C.c_int64()
+    _check(fn(_arr(left), len(left), _arr(right), len(right), out, C.byref(rows)))
+    if rows.value < 0:
+        return None, -1  # an empty side: no batch (executor.rs:350-352)
+    return [_take(out[i]) for i in range(len(left) + len(right))], rows.value
+
+
+def join_batches(left: Sequence[HostCol], right: Sequence[HostCol]):
+    """qo_join_batches — literal join_batches (executor.rs:500-540): (columns, rows), left row-major."""
+    return _cartesian(lib().qo_join_batches, left, right)
+
+
+def cross_join(left: Sequence[HostCol], right: Sequence[HostCol]):
+    """qo_cross_join — literal execute_cross_join (executor.rs:437-498): right row-major."""
+    return _cartesian(lib().qo_cross_join, left, right)
+
+
+def join_on(join_type: int, left: Sequence[HostCol], right: Sequence[HostCol], on):
+    """qo_join_on: join on an arbitrary boolean expression over left ++ right columns."""
+    nodes = on.postfix()
+    na = (abi.QehExprNode * len(nodes))(*nodes)
+    ol = (QoCol * max(len(left), 1))()
+    orr = (QoCol * max(len(right), 1))()
+    rows = C.c_int64()
+    _check(lib().qo_join_on(int(join_type), _arr(left), len(left), _arr(right), len(right), na, len(nodes), ol, orr,
+                            C.byref(rows)))
+    return [_take(ol[i]) for i in range(len(left))], [_take(orr[i]) for i in range(len(right))], rows.value
 
 
 def sort_indices_nulls(keys: Sequence[HostCol], ascending: Sequence[bool], nulls_first: Sequence[bool]) -> np.ndarray:

@@ -221,6 +221,13 @@ def test_arrow_ipc_decode_rejects_malformed(ctx):
     raw[at:at + 16] = _st.pack("<4i", 0, 4, 2, 6)
     with pytest.raises(QehError, match="offsets"):
         ctx.decode_arrow_ipc(bytes(raw))
+    # a buffer whose offset + length overflows int64 (2^62 + 2^62): rejected, never dereferenced
+    bufs = _st.pack("<4q", 0, 0, 0, 24)  # validity (0, 0), values (0, 24) of the Int64 column
+    raw = bytearray(data)
+    at = bytes(raw).index(bufs)
+    raw[at:at + 32] = _st.pack("<4q", 0, 0, 2 ** 62, 2 ** 62)
+    with pytest.raises(QehError, match="outside the body"):
+        ctx.decode_arrow_ipc(bytes(raw))
     only_schema = data[:data.index(b"\xff\xff\xff\xff", 8)]
     with pytest.raises(QehError, match="No batch found"):
         ctx.decode_arrow_ipc(only_schema + b"\xff\xff\xff\xff\x00\x00\x00\x00")

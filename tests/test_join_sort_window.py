@@ -202,6 +202,29 @@ def test_sort_two_keys_pair_path(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt,lo,hi", [(np.int32, -(2 ** 31), 2 ** 31 - 1), (np.int64, -(2 ** 63), 2 ** 63 - 1),
+                                      (np.int64, 0, 2 ** 32 - 1)])
+def test_row_number_single_partition_full_width_order_key(ctx, dt, lo, hi):
+    """One distinct PARTITION BY value and an ORDER BY key whose span needs exactly 32 or 64
+    bits: the pair encoding gives the partition key zero bits (part_shift = key width), and
+    every row must still count as one partition (ROW_NUMBER 1..n, RANK by order value)."""
+    from qe_hip.plan import WindowFunctionType as WF
+    r = np.random.default_rng(31)
+    n = 20_000
+    k = np.full(n, 7, np.int64)
+    v = r.integers(lo, hi, n, dtype=np.int64, endpoint=True).astype(dt)
+    v[0], v[1] = lo, hi
+    v[5] = v[6]  # a tie
+    rn = ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [True]).to_numpy()[0]
+    want = ob.row_number([ob.HostCol(k)], [ob.HostCol(v)], [True])
+    assert np.array_equal(rn, want)
+    assert sorted(rn.tolist()) == list(range(1, n + 1))
+    rk = ctx.window(WF.Rank, [ctx.upload(k)], [ctx.upload(v)], [False]).to_numpy()[0]
+    want_rk, _ = ob.window(WF.Rank, [ob.HostCol(k)], [ob.HostCol(v)], [False])
+    assert np.array_equal(rk, want_rk)
+
+
+@pytest.mark.gpu
 def test_row_number_nulls_desc_two_order_keys(ctx):
     r = np.random.default_rng(12)
     n = 50_000
