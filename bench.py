@@ -10,14 +10,23 @@ dim : k = a permutation of [0,1e7), g Int64 in [0,1024)        
 One step = one execution of the query over device-resident synthetic columns
 (data generated in HBM by the counter-based generator before timing): build
 the dim hash table, probe + filter + aggregate every fact row, finalize the
-groups, and for N>1 the partial->final aggregate exchange over RCCL.
+groups, and for N>1 the RCCL exchanges.
 
-Multi-GPU (torchrun, one rank per GPU): every rank holds its own 1e9-row fact
-shard (weak scaling, BASELINE config 4) and the replicated dim (broadcast
-join: each rank generates it, no data-path collective); the partial
-per-group states are all-gathered over RCCL and merged on the device by a
-second HashAggregate (the reference's partial/final aggregate stage shape,
+Default workload (the metric, strong scaling): 1e9 fact rows in total, split
+across the N GPUs (torchrun, one rank per GPU); the dim is sharded too and
+all-gathered over RCCL inside the step (broadcast join), the partial per-group
+states are shuffled by group key over RCCL all-to-all and merged on the owning
+rank (the reference's partial/final aggregate stage shape,
 crates/query-distributed/src/planner.rs:200-249).
+
+--workload cfg4 (BASELINE config 4, weak scaling): 1e9 fact rows per GPU; both
+sides hash-partitioned by the join key and exchanged over RCCL all-to-all
+(shuffle join, partition.rs:151-212), local fused join + partial aggregate,
+partial/final by group key.  Runs through a world-1 RCCL group at N = 1.
+
+After the timed steps the result is checked at the full size: Σ COUNT over the
+groups equals the device filter's count of x > 49, Σ SUM(v) equals the
+device's filtered Σ v (1e-6), and every group is present.
 """
 from __future__ import annotations
 
@@ -41,7 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000_000, help="fact rows per GPU")
+    ap.add_argument("--workload", choices=["metric", "cfg4"], default="metric",
+                    help="metric: the BASELINE query, 1e9 fact rows in total (strong scaling); cfg4: BASELINE "
+                         "config 4, hash-partitioned join + aggregate, --rows fact rows per GPU (weak scaling)")
+    ap.add_argument("--rows", type=int, default=1_000_000_000,
+                    help="fact rows (metric: in total; cfg4: per GPU)")
     ap.add_argument("--dim", type=int, default=10_000_000)
     ap.add_argument("--groups", type=int, default=1024)
     ap.add_argument("--threshold", type=int, default=49, help="WHERE f.x > threshold (49 = the BASELINE query)")
@@ -132,6 +145,22 @@ def torch_device_count():
     return torch.cuda.device_count()
 
 
+def shard(total: int, world: int, rank: int):
+    """[start, start + count) of `total` rows owned by `rank` (contiguous, balanced)."""
+    base, rem = divmod(total, world)
+    count = base + (1 if rank < rem else 0)
+    return rank * base + min(rank, rem), count
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,11 +168,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("QEH_BENCH_SHARE_GPU"):  # rehearsal only: several ranks on one GPU
         local = local % max(torch_device_count(), 1)
-    dist = world > 1
+    cfg4 = args.workload == "cfg4"
+    # config 4 always runs the distributed plan (a world-1 RCCL group at N = 1); the metric
+    # query at N = 1 is the local operator, at N > 1 the broadcast join over RCCL
+    dist = world > 1 or cfg4
     import torch
     if dist:
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         backend = os.environ.get("QEH_BENCH_BACKEND", "nccl")  # "gloo": host-exchange rehearsal (several ranks per GPU)
         if backend == "nccl":
@@ -159,13 +195,21 @@ def main():
     ctx = qe_hip.Context(local)
     ctx.set_stream(stream.cuda_stream)
 
-    n, nd = args.rows, args.dim
-    row0 = rank * n
+    nd = args.dim
+    if cfg4:  # weak scaling: `rows` fact rows on every GPU
+        row0, n = rank * args.rows, args.rows
+        total_rows = args.rows * world
+    else:     # strong scaling: `rows` fact rows in total, split across the GPUs
+        row0, n = shard(args.rows, world, rank)
+        total_rows = args.rows
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100, row0=row0)
     k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd, row0=row0)
     v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n, row0=row0)
-    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
-    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, args.groups)
+    # the dimension: whole on one GPU; sharded across ranks for N > 1 / config 4 (each rank
+    # holds rows [d0, d0 + dn) of the same table) and moved by RCCL inside the step
+    d0, dn = shard(nd, world, rank) if dist else (0, nd)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, dn, nd, row0=d0)
+    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, dn, args.groups, row0=d0)
     ctx.sync()
     pred = binop(col(0, "f.x"), BinaryOp.Greater, lit(args.threshold))
     aggs = [(AF.Sum, 2), (AF.Count, 2)]
@@ -176,11 +220,13 @@ def main():
         dx = DistributedExecutor(ctx)
 
     def step():
+        if cfg4:  # hash-partitioned join: both sides shuffled by f.k / d.k over RCCL all-to-all
+            return dx.join_filter_aggregate_shuffle([x, k, v], 1, pred, dk, [dg], aggs)
         if not dist:
             return ctx.join_filter_aggregate([x, k, v], 1, pred, dk, [dg], aggs)
-        # broadcast join (dim replicated), partial states shuffled by group key
-        # over RCCL all-to-all, final aggregate on the owning rank
-        return dx.join_filter_aggregate_broadcast([x, k, v], 1, pred, dk, [dg], aggs)
+        # broadcast join: the dim shards all-gathered over RCCL, partial states shuffled by
+        # group key over RCCL all-to-all, final aggregate on the owning rank
+        return dx.join_filter_aggregate_broadcast([x, k, v], 1, pred, dk, [dg], aggs, build_sharded=True)
 
     for _ in range(args.warmup):
         step()
@@ -199,10 +245,8 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    probe_ms, probe_launches = ctx.kernel_time("join_filter_aggregate")
-    part_ms, part_launches = ctx.kernel_time("slice_partition")
-    sprobe_ms, _ = ctx.kernel_time("slice_probe")
-    build_ms, _ = ctx.kernel_time("join_build")
+    names = ["join_filter_aggregate", "slice_partition", "slice_probe", "join_build", "filter", "partition_move"]
+    kt = {nm: ctx.kernel_time(nm) for nm in names}
     ctx.timing(False)
 
     if dist:
@@ -211,19 +255,40 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # sanity on the result: every selected row landed in exactly one group
+    # result checks at the full size (size-independent properties): every selected fact row
+    # landed in exactly one group (Σ COUNT = rows with x > threshold, counted independently on
+    # the device by the filter operator), and Σ SUM(v) over the groups = the filtered Σ v
     gk, ga, g = res
     counts, _ = ga[1].to_numpy()
-    counted = int(counts.sum())
-    groups = int(g)
+    sums, _ = ga[0].to_numpy()
+    counted, groups, vsum = int(counts.sum()), int(g), float(sums.sum())
+    fx, want_rows = ctx.filter([x, v], pred, out_idx=[1])
+    _, want_sum_cols, _ = ctx.hash_aggregate([], fx, [(AF.Sum, 0)])
+    want_sum = float(want_sum_cols[0].to_numpy()[0][0]) if want_rows else 0.0
     if dist:
-        t = torch.tensor([counted, groups], device=cdev, dtype=torch.int64)
+        t = torch.tensor([counted, groups, want_rows], device=cdev, dtype=torch.int64)
         tdist.all_reduce(t)
-        counted, groups = int(t[0].item()), int(t[1].item())
-    total_rows = n * world
+        counted, groups, want_rows = (int(q) for q in t.tolist())
+        t = torch.tensor([vsum, want_sum], device=cdev, dtype=torch.float64)
+        tdist.all_reduce(t)
+        vsum, want_sum = (float(q) for q in t.tolist())
+    assert counted == want_rows, f"Σ COUNT over groups {counted} != rows passing the filter {want_rows}"
+    assert abs(vsum - want_sum) <= 1e-6 * max(abs(want_sum), 1e-300), f"Σ SUM(v) {vsum} != filtered Σ v {want_sum}"
+    assert groups == args.groups, f"{groups} groups, expected {args.groups}"
+
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_rows * args.steps / elapsed
-    if part_launches:  # LDS-slice partitioned pipeline: the two kernels' own event times
+    part_ms, part_launches = kt["slice_partition"]
+    sprobe_ms, _ = kt["slice_probe"]
+    probe_ms, probe_launches = kt["join_filter_aggregate"]
+    if cfg4:  # the local device pipeline of the hash-partitioned plan: filter, partition, fused join
+        local_ms = (kt["filter"][0] + kt["partition_move"][0] + probe_ms + kt["join_build"][0]) / args.steps
+        avg_probe_ms = local_ms
+        kernel_name = ("config-4 local pipeline per step: filter + partition_move + join_build + "
+                       "join_filter_aggregate (HIP events)")
+        kernel_split = {nm: kt[nm][0] / args.steps for nm in ("filter", "partition_move", "join_build",
+                                                                 "join_filter_aggregate")}
+    elif part_launches:  # LDS-slice partitioned pipeline: the two kernels' own event times
         avg_probe_ms = (part_ms + sprobe_ms) / part_launches
         kernel_name = "k_slice_partition + k_slice_probe (HIP events 'slice_partition' + 'slice_probe')"
         kernel_split = {"partition_ms": part_ms / part_launches, "probe_ms": sprobe_ms / part_launches}
@@ -231,10 +296,10 @@ def main():
         avg_probe_ms = probe_ms / max(probe_launches, 1)
         kernel_name = "k_join_agg_fast (HIP events 'join_filter_aggregate')"
         kernel_split = None
-    alg_bytes = 24.0 * n  # x, k, v read once per fact row
+    alg_bytes = 24.0 * n  # x, k, v read once per fact row of this GPU
     achieved = alg_bytes / (avg_probe_ms * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(args.traffic_json) and not dist:
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("rows") == n and tj.get("kernel") == "join_filter_aggregate":
@@ -243,7 +308,18 @@ def main():
             traffic = None
 
     if rank == 0:
-        cpu = cpu_baseline(args) if world == 1 else None  # the CPU baseline is an N=1 figure
+        cpu = cpu_baseline(args) if world == 1 and not cfg4 else None  # the CPU baseline is an N=1 figure
+        if cfg4:
+            workload = ("BASELINE config 4: hash-partitioned join + aggregate (filter f.x > 49, both sides "
+                        "hash-partitioned by the join key over RCCL all-to-all, local fused join + partial "
+                        "aggregate, partial states shuffled by d.g, final aggregate)")
+            par = f"fact {n} rows per GPU x{world} (weak scaling), dim sharded x{world}, shuffle join over RCCL"
+        else:
+            workload = ("filter->hash-join->group-by (BASELINE metric query): SELECT d.g, SUM(f.v), COUNT(f.v) "
+                        "FROM fact f JOIN dim d ON f.k = d.k WHERE f.x > 49 GROUP BY d.g")
+            par = (f"fact {args.rows} rows split x{world} (strong scaling)"
+                   + (f", dim sharded x{world} and all-gathered over RCCL inside the step (broadcast join), partial "
+                      "states shuffled by RCCL all-to-all, final aggregate per owner rank" if dist else ""))
         line = {
             "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
             "value": value,
@@ -253,18 +329,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if cfg4 else "strong",
             "vs_baseline": None,
             "dtype": "int64/f64",
             "data": "synthetic (counter-based splitmix64, generated in HBM; BASELINE.md §2)",
             "config": {
-                "workload": "filter->hash-join->group-by (BASELINE metric query): SELECT d.g, SUM(f.v), COUNT(f.v) "
-                            "FROM fact f JOIN dim d ON f.k = d.k WHERE f.x > 49 GROUP BY d.g",
+                "workload": workload,
+                "fact_rows_total": total_rows,
                 "fact_rows_per_gpu": n,
                 "dim_rows": nd,
                 "groups": args.groups,
-                "parallelism": f"fact sharded x{world}, dim replicated (broadcast join)"
-                               + (", partial states shuffled by RCCL all-to-all, final aggregate per owner rank" if dist else ""),
+                "parallelism": par,
             },
             "roofline": {
                 "bound": "hbm",
@@ -280,9 +355,11 @@ def main():
                 "operator_main_queue_ms": probe_ms / max(probe_launches, 1),
                 "alg_bytes_per_launch": alg_bytes,
             },
-            "build_ms_per_step": build_ms / args.steps,
+            "build_ms_per_step": kt["join_build"][0] / args.steps,
             "result_groups": groups,
             "result_rows_counted": counted,
+            "result_check": "Σ COUNT == device filter count, Σ SUM(v) == device filtered Σ v (1e-6), groups == "
+                            f"{args.groups}: passed",
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -41,30 +41,104 @@ TORCH_OF = {abi.DT_INT64: torch.int64, abi.DT_FLOAT64: torch.float64, abi.DT_INT
 
 def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=None,
              byte_splits: Optional[dict] = None) -> Tuple[torch.Tensor, List[torch.Tensor]]:
-    """All-to-all of partition-major payloads.  send_counts[r] rows of every
-    payload go to rank r.  Returns (recv_counts, received payloads).
-    byte_splits: {payload index: per-rank element counts} for payloads whose
-    split is not the row split (the bytes of Utf8 columns); their receive
-    sizes are exchanged first."""
+    """All-to-all of partition-major payloads (host-level helper used by the CPU tests).
+    send_counts[r] rows of every payload go to rank r.  Returns (recv_counts, received).
+    byte_splits: {payload index: per-rank element counts} for payloads whose split is not the
+    row split (the bytes of Utf8 columns).  All sizes travel in ONE all_gather of a metadata
+    vector; the payloads then move with one all_to_all_single each."""
     world = dist.get_world_size(group)
-    send_counts = send_counts.to(torch.int64)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    ins = [int(x) for x in send_counts.tolist()]
-    outs = [int(x) for x in recv_counts.tolist()]
-    assert len(ins) == world
+    rank = dist.get_rank(group)
+    byte_splits = byte_splits or {}
+    keys = sorted(byte_splits)
+    meta = np.concatenate([np.asarray(send_counts.cpu().numpy() if isinstance(send_counts, torch.Tensor) else send_counts,
+                                      np.int64)] + [np.asarray(byte_splits[i], np.int64) for i in keys])
+    dev = payloads[0].device if payloads else torch.device("cpu")
+    M = _allgather_meta(meta, world, dev, group)
+    recv_counts = torch.tensor(M[:, rank], dtype=torch.int64)
     received = []
     for i, p in enumerate(payloads):
-        pin, pout = ins, outs
-        if byte_splits and i in byte_splits:
-            sc = torch.tensor(byte_splits[i], dtype=torch.int64, device=send_counts.device)
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc, group=group)
-            pin, pout = [int(x) for x in byte_splits[i]], [int(x) for x in rc.tolist()]
-        out = torch.empty((sum(pout),) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
-        dist.all_to_all_single(out, p.contiguous(), output_split_sizes=pout, input_split_sizes=pin, group=group)
-        received.append(out)
+        if i in byte_splits:
+            j = keys.index(i)
+            pin = [int(x) for x in byte_splits[i]]
+            pout = [int(x) for x in M[:, world * (j + 1) + rank]]
+        else:
+            pin = [int(x) for x in M[rank, :world]]
+            pout = [int(x) for x in M[:, rank]]
+        received.append(_all_to_all(p, pin, pout, group))
     return recv_counts, received
+
+
+def _allgather_meta(meta: np.ndarray, world: int, device, group=None) -> np.ndarray:
+    """all_gather of one int64 vector per rank -> [world, len] on the host (one host sync)."""
+    return _allgather_meta_t(torch.from_numpy(np.ascontiguousarray(meta, np.int64)).to(device), world, group)
+
+
+def _allgather_meta_t(t: torch.Tensor, world: int, group=None) -> np.ndarray:
+    out = torch.empty(world * t.numel(), dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(out, t.to(torch.int64).contiguous(), group=group)
+    return out.cpu().numpy().reshape(world, -1)
+
+
+# Largest message per peer in one RCCL round of an exchange.  RCCL 2.26 (the torch wheel's)
+# loses the second half of a world-1 all_to_all self-send once it passes ~1 GB
+# (tools/debug/a2a_big.py: 0.8 GB intact, 1.6 GB half wrong); large exchanges therefore never
+# self-send through RCCL and move in rounds of at most this many bytes per peer.
+A2A_CHUNK_BYTES = 256 << 20
+
+
+def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], group=None) -> torch.Tensor:
+    """Variable all-to-all of one partition-major payload: pin[r] leading rows go to rank r,
+    pout[r] rows arrive from rank r.  The local partition never goes through the collective
+    (one device copy, or the input itself at world size 1); under "nccl" the remote partitions
+    move as grouped send/recv (dist.all_to_all over views, ncclGroupStart/End) in rounds of at
+    most A2A_CHUNK_BYTES per peer; "gloo" (host tensors, rehearsal) uses all_to_all_single."""
+    world = len(pin)
+    me = dist.get_rank(group)
+    if world == 1:
+        return p if p.is_contiguous() else p.contiguous()
+    p = p.contiguous()
+    shape = tuple(p.shape[1:])
+    out = torch.empty((sum(pout),) + shape, dtype=p.dtype, device=p.device)
+    if p.device.type != "cuda":
+        dist.all_to_all_single(out, p, output_split_sizes=list(pout), input_split_sizes=list(pin), group=group)
+        return out
+    ioff = np.concatenate([[0], np.cumsum(pin)]).astype(np.int64)
+    ooff = np.concatenate([[0], np.cumsum(pout)]).astype(np.int64)
+    if pin[me]:
+        out[ooff[me]:ooff[me] + pout[me]].copy_(p[ioff[me]:ioff[me] + pin[me]])
+    row_bytes = max(p.element_size() * int(np.prod(shape, dtype=np.int64)), 1)
+    cap = max(A2A_CHUNK_BYTES // row_bytes, 1)
+    rounds = max([(max(pin[r], pout[r]) + cap - 1) // cap for r in range(world) if r != me] + [0])
+    empty = p.new_empty((0,) + shape)
+    for t in range(rounds):
+        ins, outs = [], []
+        for r in range(world):
+            if r == me:
+                ins.append(empty)
+                outs.append(out.new_empty((0,) + shape))
+                continue
+            a = min(t * cap, pin[r])
+            b = min((t + 1) * cap, pin[r])
+            c = min(t * cap, pout[r])
+            d = min((t + 1) * cap, pout[r])
+            ins.append(p[ioff[r] + a:ioff[r] + b])
+            outs.append(out[ooff[r] + c:ooff[r] + d])
+        dist.all_to_all(outs, ins, group=group)
+    return out
+
+
+class _DeviceView:
+    """__cuda_array_interface__ over a library-owned device buffer: torch.as_tensor wraps it
+    without a copy and keeps this object (and the column it references) alive."""
+
+    def __init__(self, ptr: int, n: int, typestr: str, owner):
+        self.owner = owner
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+TYPESTR = {abi.DT_INT64: "<i8", abi.DT_FLOAT64: "<f8", abi.DT_INT32: "<i4", abi.DT_FLOAT32: "<f4",
+           abi.DT_UINT32: "<u4"}
 
 
 # partial -> final aggregate decomposition (distributed/planner.rs:200-249 stage shape)
@@ -78,7 +152,6 @@ class DistributedExecutor:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-        self._keep: list = []  # tensors backing wrapped columns
 
     # ---- column <-> tensor ------------------------------------------------------
     def _bits_to_bytes(self, col: DeviceColumn, bits_ptr: int) -> torch.Tensor:
@@ -124,10 +197,12 @@ class DistributedExecutor:
             return out
         tdt = TORCH_OF[col.dtype]
         if self.device == "cuda":
-            vals = torch.empty(n, dtype=tdt, device="cuda")
-            if n:
-                item = vals.element_size()
-                self.ctx.copy_d2d(vals.data_ptr(), col.c.values + col.c.offset * item, n * item)
+            item = torch.empty(0, dtype=tdt).element_size()
+            if n:  # a zero-copy view of the column's values (the view keeps the column alive)
+                vals = torch.as_tensor(_DeviceView(col.c.values + col.c.offset * item, n, TYPESTR[col.dtype], col),
+                                       device="cuda")
+            else:
+                vals = torch.empty(0, dtype=tdt, device="cuda")
             out = [vals]
             if col.c.validity:
                 vb = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -145,14 +220,19 @@ class DistributedExecutor:
             return self._from_tensors_var(dtype, vals, valid)
         n = vals.shape[0]
         if self.device == "cuda":
+            keep = [vals]
             bitmap = 0
             if valid is not None:
                 bm = torch.zeros(((n + 63) // 64) * 8 + 8, dtype=torch.uint8, device="cuda")
-                abi.check(self.ctx.lib.qeh_bytes_to_validity(self.ctx.h, valid.data_ptr(), n, bm.data_ptr()))
-                self._keep.append(bm)
+                if n:
+                    abi.check(self.ctx.lib.qeh_bytes_to_validity(self.ctx.h, valid.data_ptr(), n, bm.data_ptr()))
+                keep.append(bm)
                 bitmap = bm.data_ptr()
-            self._keep.append(vals)
-            return self.ctx.wrap_device(dtype, vals.data_ptr(), n, bitmap)
+            if n == 0:  # a non-null pointer for empty columns
+                keep[0] = torch.empty(1, dtype=vals.dtype, device="cuda")
+            d = self.ctx.wrap_device(dtype, keep[0].data_ptr(), n, bitmap)
+            d.parent = keep  # the torch buffers live as long as the column
+            return d
         v = vals.numpy().astype(NP_OF[dtype], copy=False)
         m = None if valid is None else valid.numpy().astype(bool)
         return self.ctx.upload(v, m)
@@ -162,14 +242,20 @@ class DistributedExecutor:
         bm = torch.zeros(((n + 63) // 64) * 8 + 8, dtype=torch.uint8, device="cuda")
         if n:
             abi.check(self.ctx.lib.qeh_bytes_to_validity(self.ctx.h, b.data_ptr(), n, bm.data_ptr()))
-        self._keep.append(bm)
         return bm
 
     def _from_tensors_var(self, dtype: int, vals, valid: Optional[torch.Tensor]) -> DeviceColumn:
         if self.device == "cuda":
-            bitmap = self._bytes_to_bits(valid).data_ptr() if valid is not None else 0
+            keep = []
+            bitmap = 0
+            if valid is not None:
+                keep.append(self._bytes_to_bits(valid))
+                bitmap = keep[-1].data_ptr()
             if dtype == abi.DT_BOOL:
-                return self.ctx.wrap_device(dtype, self._bytes_to_bits(vals).data_ptr(), vals.shape[0], bitmap)
+                keep.append(self._bytes_to_bits(vals))
+                d = self.ctx.wrap_device(dtype, keep[-1].data_ptr(), vals.shape[0], bitmap)
+                d.parent = keep
+                return d
             lens, data = vals
             n = lens.shape[0]
             offs = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
@@ -177,9 +263,11 @@ class DistributedExecutor:
                 offs[1:] = torch.cumsum(lens.to(torch.int64), 0).to(torch.int32)
             if data.shape[0] == 0:
                 data = torch.zeros(8, dtype=torch.uint8, device="cuda")
-            self._keep.extend([offs, data])
-            return self.ctx.wrap_device(dtype, data.data_ptr(), n, bitmap, offsets=offs.data_ptr(),
-                                        values_bytes=int(offs[-1].item()) if n else 0)
+            keep.extend([offs, data])
+            d = self.ctx.wrap_device(dtype, data.data_ptr(), n, bitmap, offsets=offs.data_ptr(),
+                                     values_bytes=int(data.shape[0]) if n else 0)
+            d.parent = keep
+            return d
         m = None if valid is None else valid.numpy().astype(bool)
         if dtype == abi.DT_BOOL:
             return self.ctx.upload(vals.numpy().astype(bool), m)
@@ -195,30 +283,52 @@ class DistributedExecutor:
 
     # ---- shuffle -----------------------------------------------------------------
     def _exchange_columns(self, cols: Sequence[DeviceColumn], counts) -> Tuple[List[DeviceColumn], List[int]]:
-        """All-to-all of partition-major columns: counts[r] leading rows go to rank r (Utf8
-        bytes travel with their own per-rank byte counts)."""
-        payloads, shape, byte_splits = [], [], {}
-        bounds = np.concatenate([[0], np.cumsum(np.asarray(counts, np.int64))])
-        for t in cols:
-            ts = self._to_tensors(t)
-            nvals = 2 if t.dtype == abi.DT_UTF8 else 1
-            shape.append((t.dtype, len(ts) > nvals))
-            if t.dtype == abi.DT_UTF8:  # bytes per destination from the row lengths
-                lens = ts[0].to("cpu").numpy().astype(np.int64)
-                cum = np.concatenate([[0], np.cumsum(lens)])
-                byte_splits[len(payloads) + 1] = [int(cum[bounds[r + 1]] - cum[bounds[r]]) for r in range(self.world)]
-            payloads.extend(ts)
+        """All-to-all of partition-major columns: counts[r] leading rows go to rank r.
+        One all_gather carries every rank's row counts, per-column has-validity flags and the
+        per-destination byte counts of Utf8 columns; nullability is then agreed across ranks
+        (a column is sent with validity bytes when ANY rank's shard has a bitmap, all-valid bytes
+        from the shards without one) so every rank issues the same sequence of collectives.
+        Then one all_to_all_single per payload, with no further host round trip."""
+        w, me = self.world, self.rank
+        counts = np.asarray(counts, np.int64)
+        bounds = np.concatenate([[0], np.cumsum(counts)])
+        tens = [self._to_tensors(t) for t in cols]
+        flags = np.array([1 if t.c.validity else 0 for t in cols], np.int64)
+        utf8 = [j for j, t in enumerate(cols) if t.dtype == abi.DT_UTF8]
+        byte_counts = []
+        for j in utf8:  # bytes per destination from the row lengths (device cumsum, gathered below)
+            lens = tens[j][0].to(torch.int64)
+            cum = torch.zeros(len(lens) + 1, dtype=torch.int64, device=lens.device)
+            if len(lens):
+                cum[1:] = torch.cumsum(lens, 0)
+            b = torch.as_tensor(bounds, dtype=torch.int64, device=lens.device)
+            byte_counts.append(cum[b[1:]] - cum[b[:-1]])
         self._sync()
-        recv_counts, recv = exchange(torch.tensor(np.asarray(counts), dtype=torch.int64, device=self.device), payloads,
-                                     self.group, byte_splits)
-        out, i = [], 0
-        for dtype, nullable in shape:
-            nvals = 2 if dtype == abi.DT_UTF8 else 1
-            vals = recv[i:i + nvals]
-            valid = recv[i + nvals] if nullable else None
-            i += nvals + (1 if nullable else 0)
-            out.append(self._from_tensors(dtype, vals[0] if nvals == 1 else vals, valid))
-        return out, [int(x) for x in recv_counts.tolist()]
+        meta = [torch.as_tensor(counts, device=self.device), torch.as_tensor(flags, device=self.device)] + \
+               [bc.to(self.device) for bc in byte_counts]
+        meta_t = torch.cat(meta) if meta else torch.zeros(0, dtype=torch.int64, device=self.device)
+        M = _allgather_meta_t(meta_t, w, self.group)
+        sin, sout = [int(x) for x in M[me, :w]], [int(x) for x in M[:, me]]
+        nullable = M[:, w:w + len(cols)].max(axis=0) > 0 if len(cols) else np.zeros(0, bool)
+        out = []
+        for j, t in enumerate(cols):
+            ts = tens[j]
+            nvals = 2 if t.dtype == abi.DT_UTF8 else 1
+            vals = []
+            for q in range(nvals):
+                if t.dtype == abi.DT_UTF8 and q == 1:
+                    u = utf8.index(j)
+                    off = w + len(cols) + w * u
+                    vals.append(_all_to_all(ts[1], [int(x) for x in M[me, off:off + w]],
+                                            [int(x) for x in M[:, off + me]], self.group))
+                else:
+                    vals.append(_all_to_all(ts[q], sin, sout, self.group))
+            valid = None
+            if nullable[j]:
+                vb = ts[nvals] if len(ts) > nvals else torch.ones(len(t), dtype=torch.uint8, device=self.device)
+                valid = _all_to_all(vb, sin, sout, self.group)
+            out.append(self._from_tensors(t.dtype, vals[0] if nvals == 1 else vals, valid))
+        return out, sout
 
     def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
         """Route every row to rank hash(key) % world (partition.rs:151-212)."""
@@ -269,20 +379,113 @@ class DistributedExecutor:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
         pk, pa_, g = self.ctx.hash_aggregate(keys, inputs, aggs)
-        if g == 0 and not pk:
-            pk = [self.ctx.empty(k.dtype, 0) for k in keys]
-            pa_ = [self.ctx.empty(abi.DT_INT64, 0) for _ in aggs]
+        if g == 0:
+            pk, pa_ = self._empty_partials(keys, inputs, aggs)
         return self._final(pk, pa_, aggs)
 
+    def _empty_partials(self, keys, inputs, aggs):
+        """Zero-row partial states with the types every other rank's partials have (SUM of a
+        float -> Float64, of an integer -> Int64; COUNT -> Int64; MIN / MAX keep the input type),
+        so all ranks exchange identically typed columns."""
+        def out_dt(f, c):
+            t = inputs[c].dtype
+            if f == AF.Count:
+                return abi.DT_INT64
+            if f == AF.Sum:
+                return abi.DT_FLOAT64 if t in (abi.DT_FLOAT64, abi.DT_FLOAT32) else abi.DT_INT64
+            return t
+        return ([self.ctx.empty(k.dtype, 0) for k in keys], [self.ctx.empty(out_dt(f, c), 0) for f, c in aggs])
+
+    def allgather_columns(self, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
+        """Every rank's shard of `cols`, concatenated in rank order, on every rank: the
+        broadcast side of a broadcast join.  Fixed-width columns move with one padded
+        all_gather each (ring, bandwidth-optimal on xGMI); validity travels as bytes when any
+        shard has a bitmap.  Utf8 / Boolean shards go through the all-to-all exchange."""
+        n = len(cols[0]) if cols else 0
+        flags = [1 if c.c.validity else 0 for c in cols]
+        M = _allgather_meta_t(torch.tensor([n] + flags, dtype=torch.int64, device=self.device), self.world,
+                              self.group)
+        rows = [int(x) for x in M[:, 0]]
+        if any(c.dtype in (abi.DT_UTF8, abi.DT_BOOL) for c in cols):
+            rep = [self.ctx.concat([c] * self.world) if self.world > 1 else c for c in cols]
+            out, _ = self._exchange_columns(rep, [n] * self.world)
+            return out
+        nullable = M[:, 1:].max(axis=0) > 0 if cols else []
+        mx = max(rows) if rows else 0
+        out = []
+        for j, c in enumerate(cols):
+            ts = self._to_tensors(c)
+            vals = self._gather_padded(ts[0], n, mx, rows)
+            valid = None
+            if nullable[j]:
+                vb = ts[1] if len(ts) > 1 else torch.ones(n, dtype=torch.uint8, device=self.device)
+                valid = self._gather_padded(vb, n, mx, rows)
+            out.append(self._from_tensors(c.dtype, vals, valid))
+        return out
+
+    def _gather_padded(self, t: torch.Tensor, n: int, mx: int, rows: Sequence[int]) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if n < mx:
+            pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
+            pad[:n] = t
+            t = pad
+        buf = torch.empty(self.world * mx, dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group)
+        if all(r == mx for r in rows):
+            return buf
+        return torch.cat([buf[q * mx:q * mx + rows[q]] for q in range(self.world)])
+
     def join_filter_aggregate_broadcast(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
-                                        aggs):
-        """Broadcast join: `build_*` replicated on every rank, `probe_cols` = this
-        rank's shard.  Fused local pipeline, then partial/final merge."""
+                                        aggs, build_sharded: bool = False):
+        """Broadcast join (the BASELINE metric path): `probe_cols` = this rank's fact shard.
+        With build_sharded, `build_*` are this rank's shard of the dimension and are all-gathered
+        first (over RCCL under "nccl"); otherwise they are replicated already.  Then the fused
+        local pipeline, and the partial per-group states are shuffled by group key and merged on
+        the owning rank (partial/final aggregate, distributed/planner.rs:200-249)."""
         for f, _ in aggs:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        if build_sharded:
+            full = self.allgather_columns([build_key] + list(build_group_keys))
+            build_key, build_group_keys = full[0], full[1:]
         pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
                                                     build_group_keys, aggs)
+        if g == 0:
+            pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
+        return self._final(pk, pa_, aggs)
+
+    def join_filter_aggregate_shuffle(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
+                                      aggs):
+        """Hash-partitioned join + aggregate (BASELINE config 4; the reference's shuffle-join and
+        partial/final aggregate stage shapes, distributed/planner.rs:200-249, with hash
+        partitioning by key, partition.rs:151-212).  Both inputs are this rank's shards:
+          1. the probe side is filtered locally, keeping only the join key and the aggregate
+             inputs (the predicate reads probe columns only);
+          2. both sides are hash-partitioned by the join key on the device and exchanged with
+             one all-to-all per column, so every key's probe and build rows meet on one rank;
+          3. the local fused join + aggregate runs on what arrived, and the partial per-group
+             states are shuffled by group key and merged on the owning rank."""
+        for f, _ in aggs:
+            if f not in FINAL_OF:
+                raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        need = sorted({probe_key_idx} | {c for _, c in aggs})
+        remap = {c: i for i, c in enumerate(need)}
+        if predicate is not None:
+            cols, _ = self.ctx.filter(probe_cols, predicate, out_idx=need)
+        else:
+            cols = [probe_cols[i] for i in need]
+        pk_col = cols[remap[probe_key_idx]]
+        pcounts, pmoved = self.ctx.partition_hash_move([pk_col], self.world, cols)
+        bcols = [build_key] + list(build_group_keys)
+        bcounts, bmoved = self.ctx.partition_hash_move([build_key], self.world, bcols)
+        precv, _ = self._exchange_columns(pmoved, pcounts)
+        brecv, _ = self._exchange_columns(bmoved, bcounts)
+        local_aggs = [(f, remap[c]) for f, c in aggs]
+        pk, pa_, g = self.ctx.join_filter_aggregate(precv, remap[probe_key_idx], None, brecv[0], brecv[1:],
+                                                    local_aggs)
+        if g == 0:
+            pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
         return self._final(pk, pa_, aggs)
 
     def row_number(self, part_keys: Sequence[DeviceColumn], order_keys: Sequence[DeviceColumn],

@@ -248,13 +248,139 @@ def mode_gpu(rank, world):
     ctx.close()
 
 
+def metric_shards(rank, world, n=120_000, nd=30_000, groups=97):
+    """This rank's fact shard (x, k with NULLs and misses, v) and dim shard (k with one
+    duplicate, g) of one table split by rows; plus the whole tables for the oracle."""
+    def fact(q):
+        g = np.random.default_rng(300 + q)
+        x = g.integers(0, 100, n).astype(np.int64)
+        k = g.integers(0, nd + 1000, n).astype(np.int64)
+        km = g.random(n) > 0.02
+        v = g.random(n)
+        return x, k, km, v
+    dk_all = np.random.default_rng(5).permutation(nd).astype(np.int64)
+    dk_all[11] = dk_all[12]
+    dg_all = np.random.default_rng(6).integers(0, groups, nd).astype(np.int64)
+    b = np.linspace(0, nd, world + 1).astype(int)
+    whole = [np.concatenate(c) for c in zip(*[fact(q) for q in range(world)])]
+    return fact(rank), (dk_all[b[rank]:b[rank + 1]], dg_all[b[rank]:b[rank + 1]]), whole, (dk_all, dg_all)
+
+
+def check_metric_plans(rank, world, dx, ctx):
+    """Config 4's hash-partitioned join + aggregate and the sharded broadcast join, both vs the
+    oracle's intended-semantics join + filter + aggregate over the whole tables."""
+    import oracle_bind as ob
+    from helpers import assert_grouped_equal
+    from qe_hip import AggregateFunction as AF, BinaryOp, binop, col, lit
+    (x, k, km, v), (dk, dg), (X, K, KM, V), (DK, DG) = metric_shards(rank, world)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Max, 2)]
+    fact = [ctx.upload(x), ctx.upload(k, km), ctx.upload(v)]
+    want = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(K, KM), ob.HostCol(V)], 1, pred, ob.HostCol(DK),
+                                    [ob.HostCol(DG)], aggs)
+    for name, fn in (("shuffle", dx.join_filter_aggregate_shuffle),
+                     ("broadcast", lambda *a: dx.join_filter_aggregate_broadcast(*a, build_sharded=True))):
+        keys, aggs_out, ng = fn(fact, 1, pred, ctx.upload(dk), [ctx.upload(dg)], aggs)
+        res = dx.gather_to_root(keys + aggs_out)
+        if rank == 0:
+            assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=[0, 2]), name
+
+
+def mode_gpu_cfg4(rank, world):
+    """BASELINE config 4 as named (hash-partitioned join + aggregate) and the sharded broadcast
+    join, two ranks on one GPU over gloo; plus an exchange where only one rank's shard has a
+    validity bitmap (nullability must be agreed, or the collectives pair up wrongly)."""
+    import qe_hip
+    from qe_hip.distributed import DistributedExecutor
+    ctx = qe_hip.Context(0)
+    dx = DistributedExecutor(ctx)
+    check_metric_plans(rank, world, dx, ctx)
+    r = np.random.default_rng(40 + rank)
+    n = 5000 + 17 * rank
+    a = r.integers(0, 50, n).astype(np.int64)
+    am = (r.random(n) > 0.2) if rank == 0 else None  # rank 0's shard has NULLs, the others none
+    b = r.random(n)
+    keys = dx.shuffle(ctx.upload(a, am), [ctx.upload(a, am), ctx.upload(b)])
+    got = dx.gather_to_root(keys)
+    full = dx.allgather_columns([ctx.upload(a, am), ctx.upload(b)])
+    if rank == 0:
+        rows = []
+        for q in range(world):
+            rq = np.random.default_rng(40 + q)
+            nq = 5000 + 17 * q
+            aq = rq.integers(0, 50, nq).astype(np.int64)
+            mq = (rq.random(nq) > 0.2) if q == 0 else np.ones(nq, bool)
+            bq = rq.random(nq)
+            rows += [(int(aq[i]) if mq[i] else None, float(bq[i])) for i in range(nq)]
+        from helpers import rows_of, _key
+        assert sorted(rows_of(got), key=_key) == sorted(rows, key=_key)
+        fv = [c.to_numpy() for c in full]
+        assert rows_of([(fv[0][0], fv[0][1]), (fv[1][0], fv[1][1])]) == rows  # rank order, NULLs kept
+    ctx.close()
+
+
+def mode_nccl1(rank, world):
+    """The RCCL path itself: world_size 1 over the "nccl" backend (device tensors through
+    all_gather / all_to_all on the GPU): exchange, shuffle join, partial/final GROUP BY, the
+    sharded broadcast join and config 4's shuffle join, each vs the oracle."""
+    import torch
+    import qe_hip
+    import oracle_bind as ob
+    from helpers import assert_grouped_equal, sorted_rows
+    from qe_hip import AggregateFunction as AF
+    from qe_hip.distributed import DistributedExecutor
+    from qe_hip.partition import DeviceBatch, Hash
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    ctx = qe_hip.Context(0)
+    ctx.set_stream(s.cuda_stream)
+    dx = DistributedExecutor(ctx)
+    assert dx.device == "cuda"
+    r = np.random.default_rng(3)
+    n = 50_000
+    k = r.integers(-100, 100, n).astype(np.int64)
+    km = r.random(n) > 0.1
+    st = np.array([f"s{i % 13}" for i in range(n)], dtype=object)
+    b = r.random(n) > 0.5
+    v = r.random(n)
+    got = dx.exchange(Hash(["k"], 1), DeviceBatch(["k", "s", "b", "v"], [ctx.upload(k, km), ctx.upload(st),
+                                                                         ctx.upload(b), ctx.upload(v)]))
+    want = [(k, km), (st, None), (b, None), (v, None)]
+    assert sorted_rows([c.to_numpy() for c in got.columns]) == sorted_rows(want)
+    fk = r.integers(0, 3000, 40_000).astype(np.int64)
+    fv = r.random(40_000)
+    dk = np.arange(0, 3000, 2, dtype=np.int64)
+    da = dk * 7
+    op, obd, rows = dx.hash_join_inner(0, [ctx.upload(fk), ctx.upload(fv)], 0, [ctx.upload(dk), ctx.upload(da)])
+    wp, wb, wrows = ob.hash_join_inner(ob.HostCol(fk), [ob.HostCol(fk), ob.HostCol(fv)], ob.HostCol(dk),
+                                       [ob.HostCol(dk), ob.HostCol(da)])
+    assert rows == wrows
+    assert sorted_rows([c.to_numpy() for c in op + obd]) == sorted_rows(wp + wb)
+    gkey = r.integers(0, 300, 30_000).astype(np.int64)
+    gv = r.integers(-1000, 1000, 30_000).astype(np.int64)
+    aggs = [(AF.Sum, 0), (AF.Count, 0), (AF.Min, 0), (AF.Max, 0)]
+    keys, aggs_out, ng = dx.group_by([ctx.upload(gkey)], [ctx.upload(gv)], aggs)
+    wk, wa, wg, _ = ob.hash_aggregate([ob.HostCol(gkey)], [ob.HostCol(gv)], aggs)
+    assert ng == wg
+    assert_grouped_equal([c.to_numpy() for c in keys], [c.to_numpy() for c in aggs_out], wk, wa)
+    check_metric_plans(rank, world, dx, ctx)
+    torch.cuda.synchronize()
+    ctx.set_stream(0)
+    ctx.close()
+
+
 def main():
     mode = sys.argv[1]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if mode == "nccl1":
+        import torch
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         {"exchange": mode_exchange, "exchange_bytes": mode_exchange_bytes, "gpu": mode_gpu,
-         "gpu_exchange": mode_gpu_exchange}[mode](rank, world)
+         "gpu_exchange": mode_gpu_exchange, "gpu_cfg4": mode_gpu_cfg4, "nccl1": mode_nccl1}[mode](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

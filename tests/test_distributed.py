@@ -87,6 +87,20 @@ def test_two_ranks_on_one_gpu():
 
 
 @pytest.mark.gpu
+def test_rccl_world_size_one():
+    """The "nccl" backend (RCCL) with world_size 1 on the GPU: exchange, shuffle join,
+    partial/final GROUP BY, the sharded broadcast join and config 4's shuffle join vs the oracle."""
+    launch("nccl1", 1, timeout=300)
+
+
+@pytest.mark.gpu
+def test_config4_shuffle_join_two_ranks_on_one_gpu():
+    """BASELINE config 4 (hash-partitioned join + aggregate) and the sharded broadcast join over two
+    ranks (gloo, one GPU) vs the oracle; an exchange where only one shard carries NULLs."""
+    launch("gpu_cfg4", 2, timeout=300)
+
+
+@pytest.mark.gpu
 def test_device_tensor_round_trip(ctx):
     """The RCCL path's column <-> cuda-tensor conversion (device copies and
     validity bytes), exercised in one process without a collective."""
