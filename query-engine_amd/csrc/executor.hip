@@ -462,13 +462,62 @@ int export_table(qeh_ctx *ctx, const Table &t, ArrowSchema *os, ArrowArray *oa) 
     return QEH_OK;
 }
 
-// ---- cross join index generation -------------------------------------------------------
-__global__ void k_cross_indices(int64_t nl, int64_t nr, uint32_t *li, uint32_t *ri) {
+// ---- Cartesian index generation -------------------------------------------------------
+// left row-major = join_batches (executor.rs:500-540, the reference's INNER/LEFT/RIGHT/FULL);
+// right row-major = execute_cross_join (executor.rs:437-498: the left index cycles fastest)
+__global__ void k_cross_indices(int64_t nl, int64_t nr, uint32_t *li, uint32_t *ri, int right_major) {
     const int64_t m = nl * nr;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-        li[i] = (uint32_t)(i / nr);  // left row-major (executor.rs:437-498)
-        ri[i] = (uint32_t)(i % nr);
+        li[i] = right_major ? (uint32_t)(i % nl) : (uint32_t)(i / nr);
+        ri[i] = right_major ? (uint32_t)(i / nl) : (uint32_t)(i % nr);
     }
+}
+
+// ---- joins on a general `on` ------------------------------------------------------------
+// Several equi conjuncts: one Int64 key per side; exact bit-packing of (key - min) when the
+// spans fit 63 bits, else a 64-bit hash of the tuple (the full `on` is then re-checked).
+struct PackSpec {
+    uint64_t mn[kMaxGroupKeys];
+    int32_t shift[kMaxGroupKeys];
+    int32_t n;
+    int32_t hash;
+};
+
+__global__ void k_pack_keys(KeyCols keys, PackSpec ps, int64_t n, int64_t *__restrict__ out, uint64_t *__restrict__ vwords) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x - lane); base < n; base += stride) {
+        const int64_t i = base + lane;
+        bool ok = i < n;
+        uint64_t v = ps.hash ? 0x9E3779B97F4A7C15ull : 0ull;
+        for (int c = 0; c < ps.n; ++c) {
+            if (!ok) break;
+            if (!col_valid(keys.c[c], i)) {
+                ok = false;  // a NULL component: the tuple never matches (NULL = x is not TRUE)
+                break;
+            }
+            const uint64_t x = (uint64_t)load_i64(keys.c[c], i) - ps.mn[c];
+            v = ps.hash ? hash64(v ^ (hash64(x) + 0x9E3779B97F4A7C15ull + (v << 6) + (v >> 2))) : (v | (x << ps.shift[c]));
+        }
+        if (i < n) out[i] = ok ? (int64_t)v : 0;
+        const uint64_t m = __ballot(ok);
+        if (lane == 0) vwords[base >> 6] = m;
+    }
+}
+
+__global__ void k_iota_u32(uint32_t *out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)i;
+}
+
+__global__ void k_fill_u32(uint32_t *out, int64_t n, uint32_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) out[i] = v;
+}
+
+// flags[idx[i]] = 1 (plain stores: idempotent)
+__global__ void k_mark_rows(const uint32_t *__restrict__ idx, int64_t m, int32_t *__restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        flags[idx[i]] = 1;
 }
 
 // ---- the executor ------------------------------------------------------------------------
@@ -671,7 +720,8 @@ class Executor {
             QEH_TRY(ri.alloc(ctx_, (size_t)std::max<int64_t>(m, 1) * 4));
             if (m > 0)
                 hipLaunchKernelGGL(k_cross_indices, dim3(grid_for(ctx_, m, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream,
-                                   l.rows, r.rows, li.as<uint32_t>(), ri.as<uint32_t>());
+                                   l.rows, r.rows, li.as<uint32_t>(), ri.as<uint32_t>(),
+                                   nd.join_type == QEH_JOIN_CROSS ? 1 : 0);
             for (size_t i = 0; i < lc.size(); ++i) {
                 QEH_TRY(gather_column(ctx_, lc[i], li.as<uint32_t>(), m, &lo[i]));
                 out->cols.push_back(own(ctx_, lo[i]));
@@ -684,8 +734,8 @@ class Executor {
             rows = m;
         } else {
             int lk, rk;
-            if (!equi_keys(nd.predicate, (int)l.cols.size(), &lk, &rk))
-                return fail(QEH_E_UNSUPPORTED, "only single-column equi-joins (l.k = r.k) run on the device");
+            if (!equi_keys(nd.predicate, (int)l.cols.size(), &lk, &rk) || !int_key(lc[lk]) || !int_key(rc[rk]))
+                return join_general(nd, l, r, out);
             if (nd.join_type == QEH_JOIN_INNER)
                 QEH_TRY(qeh_hash_join_inner(ctx_, &lc[lk], lc.data(), (int)lc.size(), &rc[rk], rc.data(), (int)rc.size(),
                                             lo.data(), ro.data(), &rows));
@@ -699,6 +749,290 @@ class Executor {
         }
         out->rows = rows;
         out->batches = rows > 0 ? 1 : 0;  // executor.rs:374-376 keeps non-empty joins only
+        return QEH_OK;
+    }
+
+    static bool int_key(const qeh_column &c) { return c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_INT32; }
+
+    // Postfix ranges [b, e) of the AND-ed conjuncts of `e` (nested ANDs flattened).  A malformed
+    // expression yields itself as the only conjunct (its evaluation reports the error).
+    static void split_conjuncts(const qeh_expr &e, std::vector<std::pair<int, int>> *out) {
+        const int n = e.n_nodes;
+        std::vector<int> start(std::max(n, 1), 0);
+        bool ok = n > 0;
+        for (int i = 0; i < n && ok; ++i) {
+            const qeh_expr_node &x = e.nodes[i];
+            if (x.kind == QEH_EX_BINARY) {
+                ok = i >= 2 && start[i - 1] >= 1;
+                if (ok) start[i] = start[start[i - 1] - 1];
+            } else if (x.kind == QEH_EX_UNARY) {
+                ok = i >= 1;
+                if (ok) start[i] = start[i - 1];
+            } else {
+                start[i] = i;
+            }
+        }
+        if (!ok || start[n - 1] != 0) {
+            out->push_back({0, n});
+            return;
+        }
+        std::vector<int> stack{n - 1};
+        std::vector<std::pair<int, int>> found;
+        while (!stack.empty()) {
+            const int root = stack.back();
+            stack.pop_back();
+            const qeh_expr_node &x = e.nodes[root];
+            if (x.kind == QEH_EX_BINARY && x.op == QEH_OP_AND) {
+                const int right = root - 1, left = start[right] - 1;
+                stack.push_back(right);  // left conjunct first
+                stack.push_back(left);
+            } else {
+                found.push_back({start[root], root + 1});
+            }
+        }
+        *out = found;
+    }
+
+    // One conjunct `Column(a) = Column(b)` with one side in each input and integer keys.
+    static bool equi_conjunct(const qeh_expr_node *x, int len, int nl, const std::vector<qeh_column> &lc,
+                              const std::vector<qeh_column> &rc, int *lk, int *rk) {
+        if (len != 3 || x[0].kind != QEH_EX_COLUMN || x[1].kind != QEH_EX_COLUMN || x[2].kind != QEH_EX_BINARY ||
+            x[2].op != QEH_OP_EQ)
+            return false;
+        int a = x[0].index, b = x[1].index;
+        if (a >= nl && b < nl) std::swap(a, b);
+        if (!(a >= 0 && a < nl && b >= nl && b - nl < (int)rc.size())) return false;
+        if (!int_key(lc[a]) || !int_key(rc[b - nl])) return false;
+        *lk = a;
+        *rk = b - nl;
+        return true;
+    }
+
+    // Pack several key columns of each side into one Int64 key column per side (k_pack_keys).
+    int pack_keys(const std::vector<qeh_column> &lc, const std::vector<int> &lk, const std::vector<qeh_column> &rc,
+                  const std::vector<int> &rk, Col *lkey, Col *rkey, bool *hashed) {
+        const int nk = (int)lk.size();
+        PackSpec ps{};
+        ps.n = nk;
+        int bits = 0;
+        for (int j = 0; j < nk; ++j) {
+            const qeh_column pair[2] = {lc[lk[j]], rc[rk[j]]};
+            int64_t mn[2], mx[2], cnt[2];
+            QEH_TRY(columns_minmax(ctx_, pair, 2, mn, mx, cnt));
+            int64_t lo = INT64_MAX, hi = INT64_MIN;
+            for (int q = 0; q < 2; ++q)
+                if (cnt[q]) lo = std::min(lo, mn[q]), hi = std::max(hi, mx[q]);
+            if (lo > hi) lo = hi = 0;
+            ps.mn[j] = (uint64_t)lo;
+            const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+            int w = 0;
+            while (w < 64 && (span >> w)) ++w;
+            ps.shift[j] = bits;
+            bits += w;
+        }
+        ps.hash = bits > 63 ? 1 : 0;
+        *hashed = ps.hash != 0;
+        for (int side = 0; side < 2; ++side) {
+            const auto &cols = side == 0 ? lc : rc;
+            const auto &ks = side == 0 ? lk : rk;
+            KeyCols kc{};
+            kc.n = nk;
+            int64_t n = 0;
+            for (int j = 0; j < nk; ++j) kc.c[j] = make_colref(cols[ks[j]]), n = cols[ks[j]].length;
+            qeh_column c{};
+            QEH_TRY(alloc_column(ctx_, QEH_DT_INT64, n, true, &c));
+            Col held = own(ctx_, c);
+            if (n > 0)
+                hipLaunchKernelGGL(k_pack_keys, dim3(grid_for(ctx_, n, kBlock, 8)), dim3(kBlock), 0, ctx_->stream, kc, ps, n,
+                                   (int64_t *)c.values, (uint64_t *)c.validity);
+            QEH_HIP(hipGetLastError());
+            *(side == 0 ? lkey : rkey) = held;
+        }
+        return QEH_OK;
+    }
+
+    int iota_column(int64_t n, Col *out) {
+        qeh_column c{};
+        QEH_TRY(alloc_column(ctx_, QEH_DT_UINT32, n, false, &c));
+        *out = own(ctx_, c);
+        if (n > 0)
+            hipLaunchKernelGGL(k_iota_u32, dim3(grid_for(ctx_, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream,
+                               (uint32_t *)c.values, n);
+        QEH_HIP(hipGetLastError());
+        return QEH_OK;
+    }
+
+    // Rows of a side that no surviving pair references: their indices (UInt32 column).
+    int unmatched_rows(const Col &pairs_idx, int64_t m, int64_t n, Col *out, int64_t *count) {
+        qeh_column fl{};
+        QEH_TRY(alloc_column(ctx_, QEH_DT_INT32, n, false, &fl));
+        Col flags = own(ctx_, fl);
+        QEH_HIP(hipMemsetAsync(fl.values, 0, (size_t)std::max<int64_t>(n, 1) * 4, ctx_->stream));
+        if (m > 0)
+            hipLaunchKernelGGL(k_mark_rows, dim3(grid_for(ctx_, m, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream,
+                               (const uint32_t *)pairs_idx.c.values + pairs_idx.c.offset, m, (int32_t *)fl.values);
+        QEH_HIP(hipGetLastError());
+        Col ids;
+        QEH_TRY(iota_column(n, &ids));
+        Table t;
+        t.fields = {{"flag", QEH_DT_INT32, false}, {"row", QEH_DT_UINT32, false}};
+        t.cols = {flags, ids};
+        t.rows = n;
+        t.batches = 1;
+        const qeh_expr_node nodes[3] = {
+            {QEH_EX_COLUMN, 0, 0}, {QEH_EX_LITERAL, 0, 0}, {QEH_EX_BINARY, QEH_OP_EQ, 0}};
+        std::vector<qeh_expr_node> nv(nodes, nodes + 3);
+        nv[1].lit_dtype = QEH_DT_INT64;
+        nv[1].lit_i64 = 0;
+        qeh_expr pred{nv.data(), 3};
+        Table f;
+        QEH_TRY(filter_columns(t, pred, {1}, -1, &f));
+        *out = f.cols[0];
+        *count = f.rows;
+        return QEH_OK;
+    }
+
+    // Join whose `on` is not a single integer equi-key: AND-ed equi conjuncts become the hash key
+    // (packed when there are several), everything else is checked by evaluating the whole `on`
+    // over the candidate pairs; with no equi conjunct the candidates are the Cartesian product
+    // (left row-major, as join_batches builds it).  LEFT / RIGHT / FULL add the rows no
+    // surviving pair references, the other side NULL.  Output row order: the matching pairs,
+    // then unmatched left rows, then unmatched right rows (the join contract is a multiset).
+    int join_general(const qeh_plan_node &nd, const Table &l, const Table &r, Table *out) {
+        const int nl = (int)l.cols.size(), nr = (int)r.cols.size();
+        auto lc = raw(l), rc = raw(r);
+        std::vector<std::pair<int, int>> conj;
+        split_conjuncts(nd.predicate, &conj);
+        std::vector<int> lks, rks;
+        bool need_check = false;
+        for (auto &bc : conj) {
+            int a, b;
+            if ((int)lks.size() < kMaxGroupKeys &&
+                equi_conjunct(nd.predicate.nodes + bc.first, bc.second - bc.first, nl, lc, rc, &a, &b)) {
+                lks.push_back(a);
+                rks.push_back(b);
+            } else {
+                need_check = true;
+            }
+        }
+        if (l.rows >= (int64_t)0xFFFFFFFF || r.rows >= (int64_t)0xFFFFFFFF)
+            return fail(QEH_E_UNSUPPORTED, "join input beyond 2^32 rows");
+        Col pl, pr;  // candidate pairs: UInt32 row indices into l and r
+        int64_t m = 0;
+        if (lks.empty()) {
+            m = l.rows * r.rows;
+            if (m >= (int64_t)0xFFFFFFFF)
+                return fail(QEH_E_UNSUPPORTED, "join without an equi-key conjunct: Cartesian product beyond 2^32 rows");
+            qeh_column a{}, b{};
+            QEH_TRY(alloc_column(ctx_, QEH_DT_UINT32, m, false, &a));
+            pl = own(ctx_, a);
+            QEH_TRY(alloc_column(ctx_, QEH_DT_UINT32, m, false, &b));
+            pr = own(ctx_, b);
+            if (m > 0)
+                hipLaunchKernelGGL(k_cross_indices, dim3(grid_for(ctx_, m, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream,
+                                   l.rows, r.rows, (uint32_t *)a.values, (uint32_t *)b.values, 0);
+            QEH_HIP(hipGetLastError());
+            need_check = true;
+        } else {
+            Col lkey, rkey;
+            if (lks.size() == 1) {
+                lkey.c = lc[lks[0]];
+                rkey.c = rc[rks[0]];
+            } else {
+                bool hashed = false;
+                QEH_TRY(pack_keys(lc, lks, rc, rks, &lkey, &rkey, &hashed));
+                need_check = need_check || hashed;
+            }
+            Col lid, rid;
+            QEH_TRY(iota_column(l.rows, &lid));
+            QEH_TRY(iota_column(r.rows, &rid));
+            qeh_column po{}, bo{};
+            QEH_TRY(qeh_hash_join_inner(ctx_, &lkey.c, &lid.c, 1, &rkey.c, &rid.c, 1, &po, &bo, &m));
+            pl = po.owned ? own(ctx_, po) : lid;
+            pr = bo.owned ? own(ctx_, bo) : rid;
+            if (!po.owned) pl.c = po;
+            if (!bo.owned) pr.c = bo;
+        }
+        if (need_check && m > 0) {
+            // gather the columns `on` reads for every candidate pair, evaluate it, keep the pairs
+            const uint64_t used = (nl + nr) <= 64 ? expr_columns(&nd.predicate) : ~0ull;
+            Table t;
+            std::vector<int32_t> pos(nl + nr, -1);
+            for (int i = 0; i < nl + nr; ++i) {
+                if (i < 64 && !((used >> i) & 1)) continue;
+                const bool left = i < nl;
+                qeh_column g{};
+                QEH_TRY(gather_column(ctx_, left ? lc[i] : rc[i - nl], (const uint32_t *)(left ? pl : pr).c.values +
+                                      (left ? pl : pr).c.offset, m, &g));
+                pos[i] = (int32_t)t.cols.size();
+                t.cols.push_back(own(ctx_, g));
+                t.fields.push_back({"", g.dtype, true});
+            }
+            const int32_t ipl = (int32_t)t.cols.size();
+            t.cols.push_back(pl);
+            t.cols.push_back(pr);
+            t.fields.push_back({"l", QEH_DT_UINT32, false});
+            t.fields.push_back({"r", QEH_DT_UINT32, false});
+            t.rows = m;
+            t.batches = 1;
+            std::vector<qeh_expr_node> nodes(nd.predicate.nodes, nd.predicate.nodes + nd.predicate.n_nodes);
+            for (auto &x : nodes)
+                if (x.kind == QEH_EX_COLUMN) {
+                    if (x.index < 0 || x.index >= nl + nr)
+                        return fail(QEH_E_INVALID, "Column index " + std::to_string(x.index) + " out of bounds");
+                    x.index = pos[x.index];
+                }
+            qeh_expr on{nodes.data(), (int32_t)nodes.size()};
+            Table f;
+            QEH_TRY(filter_columns(t, on, {ipl, ipl + 1}, -1, &f));
+            pl = f.cols[0];
+            pr = f.cols[1];
+            m = f.rows;
+        }
+        // outer joins: the rows no surviving pair references, other side NULL (kNullRow)
+        const bool keep_left = nd.join_type == QEH_JOIN_LEFT || nd.join_type == QEH_JOIN_FULL;
+        const bool keep_right = nd.join_type == QEH_JOIN_RIGHT || nd.join_type == QEH_JOIN_FULL;
+        Col ul, ur;
+        int64_t nul = 0, nur = 0;
+        if (keep_left) QEH_TRY(unmatched_rows(pl, m, l.rows, &ul, &nul));
+        if (keep_right) QEH_TRY(unmatched_rows(pr, m, r.rows, &ur, &nur));
+        const int64_t total = m + nul + nur;
+        DevBuf li, ri;
+        QEH_TRY(li.alloc(ctx_, (size_t)std::max<int64_t>(total, 1) * 4));
+        QEH_TRY(ri.alloc(ctx_, (size_t)std::max<int64_t>(total, 1) * 4));
+        auto copy_idx = [&](uint32_t *dst, const Col &src, int64_t n) -> int {
+            if (n > 0)
+                QEH_HIP(hipMemcpyAsync(dst, (const uint32_t *)src.c.values + src.c.offset, (size_t)n * 4,
+                                       hipMemcpyDeviceToDevice, ctx_->stream));
+            return QEH_OK;
+        };
+        auto fill_null = [&](uint32_t *dst, int64_t n) -> int {
+            if (n > 0)
+                hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(ctx_, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx_->stream, dst, n,
+                                   kNullRow);
+            QEH_HIP(hipGetLastError());
+            return QEH_OK;
+        };
+        QEH_TRY(copy_idx(li.as<uint32_t>(), pl, m));
+        QEH_TRY(copy_idx(ri.as<uint32_t>(), pr, m));
+        QEH_TRY(copy_idx(li.as<uint32_t>() + m, ul, nul));
+        QEH_TRY(fill_null(ri.as<uint32_t>() + m, nul));
+        QEH_TRY(fill_null(li.as<uint32_t>() + m + nul, nur));
+        QEH_TRY(copy_idx(ri.as<uint32_t>() + m + nul, ur, nur));
+        const bool outer = nd.join_type != QEH_JOIN_INNER;
+        for (int i = 0; i < nl; ++i) {
+            qeh_column g{};
+            QEH_TRY(gather_column(ctx_, lc[i], li.as<uint32_t>(), total, &g, outer));
+            out->cols.push_back(own(ctx_, g));
+        }
+        for (int i = 0; i < nr; ++i) {
+            qeh_column g{};
+            QEH_TRY(gather_column(ctx_, rc[i], ri.as<uint32_t>(), total, &g, outer));
+            out->cols.push_back(own(ctx_, g));
+        }
+        QEH_HIP(hipStreamSynchronize(ctx_->stream));
+        out->rows = total;
+        out->batches = total > 0 ? 1 : 0;
         return QEH_OK;
     }
 
