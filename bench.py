@@ -288,10 +288,12 @@ def main():
                        "join_filter_aggregate (HIP events)")
         kernel_split = {nm: kt[nm][0] / args.steps for nm in ("filter", "partition_move", "join_build",
                                                                  "join_filter_aggregate")}
-    elif part_launches:  # LDS-slice partitioned pipeline: the two kernels' own event times
-        avg_probe_ms = (part_ms + sprobe_ms) / part_launches
+    elif part_launches:  # LDS-slice partitioned pipeline: the two kernels' own event times per query
+        q = max(part_launches // max(args.steps, 1), 1) if part_launches >= args.steps else 1
+        per = part_launches / q  # queries timed (launches per query > 1 for the chunked pipeline)
+        avg_probe_ms = (part_ms + sprobe_ms) / per
         kernel_name = "k_slice_partition + k_slice_probe (HIP events 'slice_partition' + 'slice_probe')"
-        kernel_split = {"partition_ms": part_ms / part_launches, "probe_ms": sprobe_ms / part_launches}
+        kernel_split = {"partition_ms": part_ms / per, "probe_ms": sprobe_ms / per, "launches_per_query": q}
     else:
         avg_probe_ms = probe_ms / max(probe_launches, 1)
         kernel_name = "k_join_agg_fast (HIP events 'join_filter_aggregate')"

@@ -363,6 +363,7 @@ struct SliceRegions {
     uint64_t cap;         // items per region, multiple of kSliceChunk
     int32_t F;            // slices
     int32_t pair_flush;   // phase A: flush two items per lane (4-B key, 16-B value stores)
+    int32_t cached_store; // phase A: plain value stores (stay in the Infinity Cache) instead of nt
     // exact layout (materialising join): region (workgroup r, slice b) starts at
     // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
     const uint64_t *rbase;
@@ -496,7 +497,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                     if (VC) {
                         v2i64 w;
                         w[0] = vv[0], w[1] = vv[1];
-                        __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                        if (rg.cached_store) *(v2i64 *)(rg.val + o) = w;
+                        else __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
                     }
                 } else {
 #pragma unroll
@@ -1512,6 +1514,7 @@ static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPla
     const bool nt = fast_nt_mode() == 1;
     SliceRegions rg = rg_in;
     rg.pair_flush = std::getenv("QEH_SLICE_SINGLE_FLUSH") ? 0 : 1;
+    if (std::getenv("QEH_SLICE_CACHED_STORE")) rg.cached_store = 1;
     KernelTimer kta(ctx, "slice_partition", stream);
 #define QEH_SA(NTV, NAV, NTB)                                                                                  \
     hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in, \
@@ -1529,11 +1532,17 @@ static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPla
 #undef QEH_SA
 }
 
+// Tiles per chunk of the chunked slice pipeline (QEH_SLICE_CHUNK_TILES; 0 = one pass).
+static int64_t slice_chunk_tiles() {
+    const char *e = std::getenv("QEH_SLICE_CHUNK_TILES");
+    return e ? std::strtoll(e, nullptr, 10) : 0;
+}
+
 // Launch phase A ahead of the build when the slice path is predictable from the build key's
 // range alone (and the group count is known to stay small).  Not launching is never an error.
 static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
                            int key_col, const qeh_column &build_key, const qeh_column &group_key, SlicePre *pre) {
-    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP")) return QEH_OK;
+    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
     if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
     FastIn in;
@@ -1591,6 +1600,18 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     return QEH_OK;
 }
 
+static void launch_slice_probe(qeh_ctx *ctx, const SliceRegions &rg, int nreg, const HashTable &t, const FastIn &in,
+                               const AggSpecs &specs, int64_t G, uint64_t *states, int nacol) {
+    KernelTimer ktb(ctx, "slice_probe");
+    const int gridB = ctx->props.multiProcessorCount;
+    if (nacol == 0)
+        hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, in, specs, G,
+                           states);
+    else
+        hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, in, specs, G,
+                           states);
+}
+
 // LDS-slice partitioned probe (k_slice_partition + k_slice_probe) for unique
 // direct u16 tables past an XCD's L2.  Returns 1 when it ran; 0 when not
 // eligible, or when a region overflowed (probe keys skewed onto few slices),
@@ -1625,6 +1646,37 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         tail_done = true;
         if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
     } else {
+        const int64_t chunk = slice_chunk_tiles();
+        if (chunk > 0 && chunk < n_tiles) {
+            // chunked pipeline: phase A and phase B alternate over chunks of `chunk` tiles; each
+            // chunk's exchange (plain stores) is read back by its phase B from the Infinity Cache
+            const int gridc = (int)std::min<int64_t>(ctx->props.multiProcessorCount, chunk);
+            if (!slice_regions(ctx, chunk, gridc, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
+            rg.cached_store = 1;
+            for (int64_t t0 = 0; t0 < n_tiles; t0 += chunk) {
+                const int64_t nt = std::min<int64_t>(chunk, n_tiles - t0);
+                FastIn ic = in;
+                const int64_t r0 = t0 * kSliceTile;
+                ic.key += r0;
+                for (int q = 0; q < 2; ++q) {
+                    if (ic.term[q]) ic.term[q] += r0;
+                    if (ic.acol[q]) ic.acol[q] += r0;
+                }
+                const int g = (int)std::min<int64_t>(gridc, nt);
+                launch_slice_partition(ctx, ic, pp, nterms, nacol, t.kmin, t.range, nt, g, rg, ctx->stream);
+                launch_slice_probe(ctx, rg, g, t, ic, specs, G, states, nacol);
+            }
+            if (hipGetLastError() != hipSuccess) return 0;
+            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+            uint32_t of = 0;
+            if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
+            if (of) {
+                hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * G, kBlock * 4, 8)),
+                                   dim3(kBlock), 0, ctx->stream, states, G, specs);
+                return 0;
+            }
+            return 1;
+        }
         if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
         launch_slice_partition(ctx, in, pp, nterms, nacol, t.kmin, t.range, n_tiles, grid, rg, ctx->stream);
     }
