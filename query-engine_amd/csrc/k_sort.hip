@@ -1108,6 +1108,10 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     }
     int64_t n;
     QEH_TRY(check_sort_keys(all.data(), (int)all.size(), &n));
+    if (n_part == 1 && n_order == 1) {  // one bounded partition key: partition instead of sorting
+        const int s = window_msd(ctx, QEH_WIN_ROW_NUMBER, part_keys[0], order_keys[0], asc[1] != 0, 0, out_rn);
+        if (s != kWindowMsdNotEligible) return s;
+    }
     RadixState rs;
     QEH_TRY(sort_perm(ctx, all.data(), (int)all.size(), asc.data(), n, rs));
     QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out_rn));
@@ -1338,6 +1342,10 @@ extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_key
     }
     if (func == QEH_WIN_ROW_NUMBER && !all.empty())  // the dedicated path (pair-key sort, no peer state)
         return qeh_row_number(ctx, part_keys, n_part, order_keys, n_order, ascending, out);
+    if (n_part == 1 && n_order == 1 && (func == QEH_WIN_RANK || func == QEH_WIN_DENSE_RANK || func == QEH_WIN_NTILE)) {
+        const int s = window_msd(ctx, func, part_keys[0], order_keys[0], asc[1] != 0, param, out);
+        if (s != kWindowMsdNotEligible) return s;
+    }
     const int odt = value_fn ? arg->dtype : QEH_DT_INT64;
     QEH_TRY(alloc_column(ctx, odt, n, value_fn, out));
     if (n == 0) return QEH_OK;

@@ -105,6 +105,13 @@ struct Utf8Rewrite {
 int rewrite_utf8_compares(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *e, Utf8Rewrite *out);
 bool expr_has_utf8(const qeh_expr *e, const int32_t *dtypes, int n_cols);
 
+// Window functions over one bounded integer PARTITION BY key and one ORDER BY key by partitioning
+// (k_window.hip): ROW_NUMBER / RANK / DENSE_RANK / NTILE into a fresh Int64 column.
+// kWindowMsdNotEligible (nothing allocated) when the shapes do not fit.
+constexpr int kWindowMsdNotEligible = -1;
+int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
+               qeh_column *out);
+
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
 

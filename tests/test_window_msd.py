@@ -1,0 +1,98 @@
+"""The partitioning window path (k_window.hip: ROW_NUMBER / RANK / DENSE_RANK / NTILE over one
+bounded integer PARTITION BY key and one ORDER BY key) against the oracle (qo_row_number /
+qo_window, which follow docs/WINDOW_FUNCTIONS.md:44-140).  QEH_WINDOW_MSD=1 forces the path below
+its default size threshold so small cases exercise every kernel; a group larger than the
+wave sort's 2048 rows must fall back to the LSD path and stay correct."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from qe_hip.plan import WindowFunctionType as W
+
+
+def _msd_ran(ctx):
+    ms, n = ctx.kernel_time("window_sort")
+    return n > 0
+
+
+def _run(ctx, func, k, v, asc, param=0):
+    ctx.timing(True)
+    ctx.timing_reset()
+    if func == W.RowNumber:
+        got = ctx.row_number([ctx.upload(k)], [ctx.upload(v)], [asc]).to_numpy()[0]
+        want = ob.row_number([ob.HostCol(k)], [ob.HostCol(v)], [asc])
+    else:
+        got = ctx.window(func, [ctx.upload(k)], [ctx.upload(v)], [asc], param=param).to_numpy()[0]
+        want, _ = ob.window(func, [ob.HostCol(k)], [ob.HostCol(v)], [asc], param=param)
+    ran = _msd_ran(ctx)
+    ctx.timing(False)
+    return got, want, ran
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.DenseRank, 0), (W.Ntile, 3)])
+@pytest.mark.parametrize("n,parts", [(1, 1), (1000, 7), (70_000, 1 << 20), (300_001, 1000), (2_000_000, 4096)])
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_window_matches_oracle(ctx, monkeypatch, func, param, n, parts, asc):
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(n + parts)
+    k = r.integers(0, parts, n).astype(np.int64) + 1000  # offset range (k - kmin)
+    v = r.integers(-40, 40, n).astype(np.int64)  # many ties: RANK / DENSE_RANK peers, input-order tiebreak
+    got, want, ran = _run(ctx, func, k, v, asc, param)
+    assert ran
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vdt", [np.int32, np.float64, np.float32])
+def test_msd_window_order_key_types(ctx, monkeypatch, vdt):
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(3)
+    n = 200_000
+    k = r.integers(-500, 500, n).astype(np.int32)
+    if vdt == np.int32:
+        v = r.integers(-(2 ** 31), 2 ** 31, n, dtype=np.int64).astype(np.int32)
+        v[:2] = [-(2 ** 31), 2 ** 31 - 1]
+    else:
+        v = np.round(r.standard_normal(n), 2).astype(vdt)
+        v[:4] = [-0.0, 0.0, np.inf, -np.inf]
+    for func in (W.RowNumber, W.Rank):
+        got, want, ran = _run(ctx, func, k, v, False)
+        assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_msd_window_full_range_order_key(ctx, monkeypatch):
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(4)
+    n = 100_000
+    k = r.integers(0, 30, n).astype(np.int64)
+    v = r.integers(-(2 ** 63), 2 ** 63 - 1, n, dtype=np.int64)
+    v[:3] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, np.iinfo(np.int64).max]
+    for asc in (True, False):
+        got, want, ran = _run(ctx, W.RowNumber, k, v, asc)
+        assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_msd_window_big_group_falls_back(ctx, monkeypatch):
+    """A PARTITION BY group above 2048 rows: the wave sort declines, the LSD path answers."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(5)
+    n = 50_000
+    k = r.integers(0, 100, n).astype(np.int64)
+    k[:5000] = 42
+    v = r.integers(-9, 9, n).astype(np.int64)
+    got, want, _ = _run(ctx, W.Rank, k, v, True)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_msd_window_default_threshold_full_shape(ctx):
+    """Without forcing: 2^21 rows, k in [0, 2^20) (the config-5 shape scaled down) take the path."""
+    n = 1 << 21
+    from qe_hip import abi
+    kk = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 7, n, 2 ** 20)
+    vv = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    got, want, ran = _run(ctx, W.RowNumber, kk, vv, True)
+    assert ran and np.array_equal(got, want)
