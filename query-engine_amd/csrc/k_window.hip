@@ -35,22 +35,24 @@ constexpr int kWmBlock = 1024;                // partition passes: one workgroup
 constexpr int kWmTile = 8192;                 // rows per partition-pass tile (8 per thread)
 constexpr int kWmDig = 1024;                  // digits per partition pass
 constexpr int kWmSortBlock = 256;             // group sort: 4 waves
-constexpr int kWmMaxR = 32;                   // rows per lane in the group sort -> groups <= 2048
 constexpr int kWmWinBits = 15;                // output window = 2^15 rows (128 KB of u32 in LDS)
 
-// exclusive scan of one value per thread over a 1024-thread block; *total gets the sum
-__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t *wsum, uint32_t *total) {
+// Workgroup barrier ordering LDS only: the next tile's global loads stay in flight across it
+// (__syncthreads would also drain vmcnt and serialise the prefetch).
+__device__ __forceinline__ void wm_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// exclusive scan of one value per thread over a 1024-thread block
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t *wsum) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_scan(v);
     if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
+    wm_barrier();
     if (wave == 0) {
         const uint32_t w = lane < kWmBlock / 64 ? wsum[lane] : 0u;
         const uint32_t wi = wave_incl_scan(w);
         if (lane < kWmBlock / 64) wsum[lane] = wi - w;
-        if (lane == kWmBlock / 64 - 1 && total) *total = wi;
     }
-    __syncthreads();
+    wm_barrier();
     return inc - v + wsum[wave];
 }
 
@@ -85,6 +87,16 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
 }
 
+// Tile skeleton shared by the partition passes: rank the tile's rows by digit with LDS atomics,
+// scan the digit counts, stage the rows sorted by digit, write each digit's run at its running
+// position.  Rows of tile t + 1 are loaded (into registers) before tile t is staged.
+#define WM_TILE_RANK(NJ)                                                   \
+    _Pragma("unroll") for (int j = 0; j < NJ; ++j) rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u; \
+    wm_barrier();                                                          \
+    const uint32_t c_ = cnt[tid];                                          \
+    lofs[tid] = block_excl_scan1024(c_, wsum);                             \
+    wm_barrier();
+
 // ---- pass 1: partition (order key, row id, low key bits) by the high digit -------------------
 __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
                                                        const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
@@ -100,25 +112,34 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, i
     __syncthreads();
     const uint32_t lmask = (1u << sh.lb) - 1u;
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
+    int64_t kv[8], ovv[8];
+    auto load = [&](int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t i = t0 + j * kWmBlock + tid;
+            const int64_t ii = i < r1 ? i : r0;
+            kv[j] = load_i64(key, ii);
+            ovv[j] = load_i64(ord, ii);
+        }
+    };
+    if (r0 < r1) load(r0);
     for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
         uint32_t d[8], rk[8], kl[8];
         uint64_t ok[8];
         bool live[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int64_t i = t0 + j * kWmBlock + tid;
-            live[j] = i < r1;
-            const int64_t ii = live[j] ? i : r0;
-            const uint64_t kk = (uint64_t)load_i64(key, ii) - (uint64_t)sh.kmin;
+            live[j] = t0 + j * kWmBlock + tid < r1;
+            const uint64_t kk = (uint64_t)kv[j] - (uint64_t)sh.kmin;
             d[j] = (uint32_t)(kk >> sh.lb);
             kl[j] = (uint32_t)kk & lmask;
-            ok[j] = wm_order_key(ord, ii, asc);
-            rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u;
+            const int64_t o = (ord.dtype == QEH_DT_FLOAT32 || ord.dtype == QEH_DT_FLOAT64) ? f64_order_key(as_f64(ovv[j]))
+                                                                                          : ovv[j];
+            const uint64_t u = (uint64_t)o ^ 0x8000000000000000ull;
+            ok[j] = asc ? u : ~u;
         }
-        __syncthreads();
-        const uint32_t c = cnt[tid];
-        lofs[tid] = block_excl_scan1024(c, wsum, nullptr);
-        __syncthreads();
+        if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
+        WM_TILE_RANK(8)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if (!live[j]) continue;
@@ -128,7 +149,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, i
             st_kl[s] = (uint16_t)kl[j];
             st_d[s] = (uint16_t)d[j];
         }
-        __syncthreads();
+        wm_barrier();
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
@@ -137,10 +158,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, i
             o_id[p] = st_id[s];
             o_kl[p] = st_kl[s];
         }
-        __syncthreads();
-        lpos[tid] += c;
+        wm_barrier();
+        lpos[tid] += c_;
         cnt[tid] = 0;
-        __syncthreads();
+        wm_barrier();
     }
 }
 
@@ -162,37 +183,50 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass2(WmShape sh, const uint64_
         __syncthreads();
         for (uint64_t i = s0 + tid; i < s1; i += kWmBlock) atomicAdd(&cnt[i_kl[i]], 1u);
         __syncthreads();
-        const uint32_t c = cnt[tid];
-        const uint32_t ex = block_excl_scan1024(c, wsum, nullptr);
-        const int64_t part = (int64_t)b * L + tid;
-        if (tid < L && part < sh.nparts) pstart[part] = s0 + ex;
-        lpos[tid] = s0 + ex;
-        cnt[tid] = 0;
+        {
+            const uint32_t c = cnt[tid];
+            const uint32_t ex = block_excl_scan1024(c, wsum);
+            const int64_t part = (int64_t)b * L + tid;
+            if (tid < L && part < sh.nparts) pstart[part] = s0 + ex;
+            lpos[tid] = s0 + ex;
+            cnt[tid] = 0;
+        }
         __syncthreads();
+        uint64_t kx[8];
+        uint32_t ix[8], lx[8];
+        auto load = [&](uint64_t t0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
+                const uint64_t ii = i < s1 ? i : s0;
+                kx[j] = i_key[ii];
+                ix[j] = i_id[ii];
+                lx[j] = i_kl[ii];
+            }
+        };
+        if (s0 < s1) load(s0);
         for (uint64_t t0 = s0; t0 < s1; t0 += kWmTile) {
-            uint32_t d[8], rk[8];
+            uint32_t d[8], rk[8], ids[8];
+            uint64_t keys[8];
             bool live[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                live[j] = i < s1;
-                d[j] = live[j] ? i_kl[i] : 0u;
-                rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u;
+                live[j] = t0 + (uint64_t)(j * kWmBlock + tid) < s1;
+                d[j] = lx[j];
+                keys[j] = kx[j];
+                ids[j] = ix[j];
             }
-            __syncthreads();
-            const uint32_t cc = cnt[tid];
-            lofs[tid] = block_excl_scan1024(cc, wsum, nullptr);
-            __syncthreads();
+            if (t0 + kWmTile < s1) load(t0 + kWmTile);
+            WM_TILE_RANK(8)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (!live[j]) continue;
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
                 const uint32_t s = lofs[d[j]] + rk[j];
-                st_key[s] = i_key[i];
-                st_id[s] = i_id[i];
+                st_key[s] = keys[j];
+                st_id[s] = ids[j];
                 st_d[s] = (uint16_t)d[j];
             }
-            __syncthreads();
+            wm_barrier();
             const int m = (int)std::min<uint64_t>(kWmTile, s1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
@@ -200,44 +234,41 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass2(WmShape sh, const uint64_
                 o_key[p] = st_key[s];
                 o_id[p] = st_id[s];
             }
-            __syncthreads();
-            lpos[tid] += cc;
+            wm_barrier();
+            lpos[tid] += c_;
             cnt[tid] = 0;
-            __syncthreads();
+            wm_barrier();
         }
+        __syncthreads();
     }
 }
 
 // ---- group sort: one wave per PARTITION BY group --------------------------------------------
-__device__ __forceinline__ bool kv_less(uint64_t ak, uint32_t ai, uint64_t bk, uint32_t bi) {
-    return ak < bk || (ak == bk && ai < bi);
-}
-
+// A group of m <= 64 R rows is sorted by a 32-bit composite key: the top 21 significant bits of
+// (order key - the group's minimum) above the row's 11-bit position in the group.  The network
+// (bitonic, lane-major: element e = lane * R + r, so distances below R are register swaps,
+// unrolled by template recursion) therefore moves one dword per element.  Runs of equal 21-bit
+// prefixes -- truncation collisions and true ties -- are then re-sorted exactly by (order key,
+// row id) from the group's copy in LDS; a run above 64 rows (heavy ties) makes the operator
+// fall back to the LSD path.
 struct WmFunc {
     int32_t func;      // QEH_WIN_ROW_NUMBER / RANK / DENSE_RANK / NTILE
     int64_t param;     // NTILE buckets
     int32_t win_shift; // pass-5a digit = row id >> win_shift
+    int32_t skip_sort; // QEH_WM_SKIP_SORT (experiments: load/emit cost without the network)
 };
 
-// Elements in lane-major order: element e = lane * R + r.  Sorted ascending by (key, id).
-// The network is unrolled by template recursion (stage KK, distance J), so every register
-// index is a compile-time constant: no dynamic indexing, no scratch.
 template <int R, int KK, int J>
-__device__ __forceinline__ void bitonic_stage(uint64_t (&k)[R], uint32_t (&id)[R], int lane) {
+__device__ __forceinline__ void bitonic_stage32(uint32_t (&k)[R], int lane) {
     if constexpr (J < R) {  // partner in this lane's registers
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            constexpr int dummy = 0;
-            (void)dummy;
             const int r2 = r ^ J;
             if (r2 > r) {
-                const int e = lane * R + r;
-                const bool asc = (e & KK) == 0;
-                const bool sw = asc ? kv_less(k[r2], id[r2], k[r], id[r]) : kv_less(k[r], id[r], k[r2], id[r2]);
-                const uint64_t a = k[r], b = k[r2];
-                const uint32_t ia = id[r], ib = id[r2];
-                k[r] = sw ? b : a, k[r2] = sw ? a : b;
-                id[r] = sw ? ib : ia, id[r2] = sw ? ia : ib;
+                const bool asc = ((lane * R + r) & KK) == 0;
+                const uint32_t lo = min(k[r], k[r2]), hi = max(k[r], k[r2]);
+                k[r] = asc ? lo : hi;
+                k[r2] = asc ? hi : lo;
             }
         }
     } else {  // partner lane = lane ^ (J / R), same register
@@ -245,127 +276,175 @@ __device__ __forceinline__ void bitonic_stage(uint64_t (&k)[R], uint32_t (&id)[R
         const bool lower = (lane & LJ) == 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int e = lane * R + r;
-            const bool asc = (e & KK) == 0;
-            const uint64_t ok = __shfl_xor(k[r], LJ, 64);
-            const uint32_t oi = __shfl_xor(id[r], LJ, 64);
-            // the lower element keeps the min when ascending, the upper the max
-            const bool take = (lower == asc) ? kv_less(ok, oi, k[r], id[r]) : kv_less(k[r], id[r], ok, oi);
-            k[r] = take ? ok : k[r];
-            id[r] = take ? oi : id[r];
+            const bool asc = ((lane * R + r) & KK) == 0;
+            const uint32_t o = __shfl_xor(k[r], LJ, 64);
+            k[r] = (lower == asc) ? min(k[r], o) : max(k[r], o);
         }
     }
 }
 
 template <int R, int KK, int J>
-__device__ __forceinline__ void bitonic_merge(uint64_t (&k)[R], uint32_t (&id)[R], int lane) {
+__device__ __forceinline__ void bitonic_merge32(uint32_t (&k)[R], int lane) {
     if constexpr (J > 0) {
-        bitonic_stage<R, KK, J>(k, id, lane);
-        bitonic_merge<R, KK, J / 2>(k, id, lane);
+        bitonic_stage32<R, KK, J>(k, lane);
+        bitonic_merge32<R, KK, J / 2>(k, lane);
     }
 }
 
 template <int R, int KK>
-__device__ __forceinline__ void bitonic_sort(uint64_t (&k)[R], uint32_t (&id)[R], int lane) {
+__device__ __forceinline__ void bitonic_sort32(uint32_t (&k)[R], int lane) {
     if constexpr (KK <= 64 * R) {
-        bitonic_merge<R, KK, KK / 2>(k, id, lane);
-        bitonic_sort<R, KK * 2>(k, id, lane);
+        bitonic_merge32<R, KK, KK / 2>(k, lane);
+        bitonic_sort32<R, KK * 2>(k, lane);
     }
 }
 
-template <int R>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&k)[R], uint32_t (&id)[R], int lane) {
-    bitonic_sort<R, 2>(k, id, lane);
+__device__ __forceinline__ int wm_pad(int e) { return e + (e >> 5); }  // one pad dword per 32
+
+// Lanes of one wave exchange data through LDS: the compiler must not move an LDS access across
+// this point (it sees only per-lane dependences), and the wave's LDS operations complete.
+__device__ __forceinline__ void wm_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ bool wm_less(uint64_t a, uint32_t ia, uint64_t b, uint32_t ib) {
+    return a < b || (a == b && ia < ib);
 }
 
-template <int R>
+// per-wave LDS area for a group of up to P rows: order keys, row ids, composite keys (padded)
+template <int P>
+struct WmWaveLds {
+    uint64_t ov[P];
+    uint32_t id[P];
+    uint32_t k[P + P / 32];
+};
+
+template <int R, int P>
 __device__ void wm_group(const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid, int64_t s, int m,
-                         const WmFunc &f, uint64_t *__restrict__ pairs, uint32_t *__restrict__ whist, int lane) {
-    uint64_t k[R];
-    uint32_t id[R];
+                         const WmFunc &f, uint64_t *__restrict__ pairs, uint32_t *__restrict__ whist, WmWaveLds<P> &L,
+                         uint32_t *__restrict__ too_big, int lane) {
+    // coalesced loads (register-major e = r * 64 + lane) into LDS; the group's min / max
+    wm_wave_sync();  // the previous group's LDS reads are done
+    uint64_t mn = ~0ull, mx = 0ull;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int e = lane * R + r;
-        k[r] = e < m ? gkey[s + e] : ~0ull;
-        id[r] = e < m ? gid[s + e] : 0xFFFFFFFFu;
-    }
-    wave_bitonic<R>(k, id, lane);
-    uint32_t res[R];
-    if (f.func == QEH_WIN_ROW_NUMBER) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) res[r] = (uint32_t)(lane * R + r + 1);
-    } else if (f.func == QEH_WIN_NTILE) {
-        const int64_t q = m / f.param, rm = m % f.param;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t r0 = lane * R + r;
-            res[r] = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
-        }
-    } else {
-        // peer flags (a new ORDER BY value starts a peer group); the previous element of
-        // register 0 is the previous lane's last register
-        const uint64_t prev_last = __shfl_up(k[R - 1], 1, 64);
-        uint32_t flag[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint64_t pk = r > 0 ? k[r - 1] : prev_last;
-            flag[r] = (lane == 0 && r == 0) || pk != k[r] ? 1u : 0u;
-        }
-        if (f.func == QEH_WIN_RANK) {
-            // rank = 1 + position of the last peer-group start at or before e (max-scan)
-            uint32_t run = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (flag[r]) run = (uint32_t)(lane * R + r);
-                res[r] = run;
-            }
-            uint32_t carry = run;  // lane's last start (0 if none: lane 0 always has one)
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t t = __shfl_up(carry, d, 64);
-                if (lane >= d) carry = t > carry ? t : carry;
-            }
-            uint32_t before = __shfl_up(carry, 1, 64);
-            if (lane == 0) before = 0;
-            bool seen = false;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                seen = seen || flag[r];
-                res[r] = (seen ? res[r] : before) + 1u;
-            }
-        } else {  // DENSE_RANK: inclusive count of peer-group starts
-            uint32_t tot = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) tot += flag[r];
-            const uint32_t incl = wave_incl_scan(tot);
-            uint32_t acc = incl - tot;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                acc += flag[r];
-                res[r] = acc;
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = lane * R + r;
+        const int e = r * 64 + lane;
         if (e < m) {
-            pairs[s + e] = ((uint64_t)id[r] << 32) | res[r];
-            atomicAdd(&whist[id[r] >> f.win_shift], 1u);
+            const uint64_t o = gkey[s + e];
+            L.ov[e] = o;
+            L.id[e] = gid[s + e];
+            mn = o < mn ? o : mn;
+            mx = o > mx ? o : mx;
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    const uint64_t span = mx - mn;
+    const int sb = span ? 64 - __clzll((long long)span) : 0;
+    const int shift = sb > 21 ? sb - 21 : 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        L.k[wm_pad(e)] = e < m ? ((uint32_t)((L.ov[e] - mn) >> shift) << 11) | (uint32_t)e : 0xFFFFFFFFu;
+    }
+    wm_wave_sync();
+    if (!f.skip_sort) {
+        uint32_t k[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) k[r] = L.k[wm_pad(lane * R + r)];
+        bitonic_sort32<R, 2>(k, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) L.k[wm_pad(lane * R + r)] = k[r];
+        wm_wave_sync();
+    }
+    // exact order inside runs of equal prefixes (insertion sort by (order key, row id))
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e >= m) continue;
+        const uint32_t ke = L.k[wm_pad(e)] >> 11;
+        const bool start = e == 0 || (L.k[wm_pad(e - 1)] >> 11) != ke;
+        if (!start || e + 1 >= m || (L.k[wm_pad(e + 1)] >> 11) != ke) continue;
+        int len = 2;
+        while (e + len < m && (L.k[wm_pad(e + len)] >> 11) == ke) ++len;
+        if (len > 64) {
+            *too_big = 1u;
+            continue;
+        }
+        for (int a = 1; a < len; ++a) {
+            const uint32_t x = L.k[wm_pad(e + a)];
+            const uint64_t xo = L.ov[x & 2047];
+            const uint32_t xi = L.id[x & 2047];
+            int b = a - 1;
+            while (b >= 0) {
+                const uint32_t y = L.k[wm_pad(e + b)];
+                if (!wm_less(xo, xi, L.ov[y & 2047], L.id[y & 2047])) break;
+                L.k[wm_pad(e + b + 1)] = y;
+                --b;
+            }
+            L.k[wm_pad(e + b + 1)] = x;
+        }
+    }
+    wm_wave_sync();
+    // results in sorted order, register-major (coalesced emission)
+    uint32_t carry_rank = 0, carry_dense = 0;
+    uint64_t prev_ov = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        const bool live = e < m;
+        const uint32_t x = live ? L.k[wm_pad(e)] : 0u;
+        const uint32_t pos = x & 2047;
+        const uint64_t ov = live ? L.ov[pos] : 0ull;
+        const uint32_t rid = live ? L.id[pos] : 0u;
+        uint32_t res;
+        if (f.func == QEH_WIN_ROW_NUMBER) {
+            res = (uint32_t)e + 1u;
+        } else if (f.func == QEH_WIN_NTILE) {
+            const int64_t q = m / f.param, rm = m % f.param, r0 = e;
+            res = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
+        } else {
+            uint64_t pv = __shfl_up(ov, 1, 64);
+            if (lane == 0) pv = prev_ov;
+            const uint32_t flag = (e == 0 || pv != ov) ? 1u : 0u;
+            if (f.func == QEH_WIN_RANK) {
+                uint32_t v = flag ? (uint32_t)e : 0u;  // last peer-group start at or before e
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = __shfl_up(v, d, 64);
+                    if (lane >= d) v = t > v ? t : v;
+                }
+                v = v > carry_rank ? v : carry_rank;
+                res = v + 1u;
+                carry_rank = __shfl(v, 63, 64);
+            } else {  // DENSE_RANK
+                const uint32_t v = wave_incl_scan(flag) + carry_dense;
+                res = v;
+                carry_dense = __shfl(v, 63, 64);
+            }
+            prev_ov = __shfl(ov, 63, 64);
+        }
+        if (live) {
+            pairs[s + e] = ((uint64_t)rid << 32) | res;
+            atomicAdd(&whist[rid >> f.win_shift], 1u);
         }
     }
 }
 
 // Workgroup w owns groups [g0, g1) (contiguous rows [pstart[g0], pstart[g1])); its waves take
 // the groups in turn.  Window histograms are added to counts[digit * grid + w] for pass 5a.
-// BIG = false: groups of <= 1024 rows (register width <= 16); BIG = true: 1025..2048 rows, in a
-// kernel of its own so the wide network's registers do not limit the common case.
+// BIG = false: groups of <= 1024 rows; BIG = true: 1025..2048 rows, a kernel of its own so its
+// larger LDS area does not limit the common case.
 template <bool BIG>
 __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                           const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid,
                                                           uint64_t *__restrict__ pairs, uint32_t *__restrict__ counts,
                                                           uint32_t *__restrict__ too_big) {
+    constexpr int P = BIG ? 2048 : 1024;
     __shared__ uint32_t whist[kWmDig];
+    __shared__ WmWaveLds<P> wl[kWmSortBlock / 64];
     for (int i = threadIdx.x; i < kWmDig; i += kWmSortBlock) whist[i] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -376,19 +455,19 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, 
         if (m <= 0) continue;
         if (BIG) {
             if (m <= 1024) continue;
-            if (m > 64 * kWmMaxR) {
+            if (m > 2048) {
                 if (lane == 0) *too_big = 1u;
                 continue;
             }
-            wm_group<32>(gkey, gid, s, (int)m, f, pairs, whist, lane);
+            wm_group<32, P>(gkey, gid, s, (int)m, f, pairs, whist, wl[wave], too_big, lane);
         } else {
             const int mi = (int)m;
             if (mi > 1024) continue;
-            if (mi <= 64) wm_group<1>(gkey, gid, s, mi, f, pairs, whist, lane);
-            else if (mi <= 128) wm_group<2>(gkey, gid, s, mi, f, pairs, whist, lane);
-            else if (mi <= 256) wm_group<4>(gkey, gid, s, mi, f, pairs, whist, lane);
-            else if (mi <= 512) wm_group<8>(gkey, gid, s, mi, f, pairs, whist, lane);
-            else wm_group<16>(gkey, gid, s, mi, f, pairs, whist, lane);
+            if (mi <= 64) wm_group<1, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
+            else if (mi <= 128) wm_group<2, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
+            else if (mi <= 256) wm_group<4, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
+            else if (mi <= 512) wm_group<8, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
+            else wm_group<16, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
         }
     }
     __syncthreads();
@@ -396,92 +475,58 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, 
         if (whist[i]) atomicAdd(&counts[(int64_t)i * gridDim.x + blockIdx.x], whist[i]);
 }
 
-// ---- pass 5a: pairs partitioned by row id into windows (global, ranges = k_wm_sort's) --------
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass5a(WmShape sh, int nsort, int win_shift,
-                                                        const uint64_t *__restrict__ pstart,
-                                                        const uint64_t *__restrict__ base, const uint64_t *__restrict__ in,
-                                                        uint64_t *__restrict__ out) {
+// ---- pass 5a / 5b: pairs partitioned by row id ------------------------------------------------
+// 5a (global): digit = row id >> win_shift, over the row ranges of k_wm_sort's workgroups, at
+// positions from the scanned window histograms.  5b (segmented): window w holds exactly the row
+// ids [w << win_shift, (w + 1) << win_shift), so its region and every output window's place are
+// known without a histogram; digit = (row id >> kWmWinBits) within the window.
+template <bool SEG>
+__global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, int win_shift, int64_t nwin,
+                                                       const uint64_t *__restrict__ pstart,
+                                                       const uint64_t *__restrict__ base, const uint64_t *__restrict__ in,
+                                                       uint64_t *__restrict__ out) {
     __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
     __shared__ uint64_t lpos[kWmDig];
     __shared__ uint64_t st[kWmTile];
     __shared__ uint16_t st_d[kWmTile];
     const int tid = threadIdx.x;
-    for (int w = blockIdx.x; w < nsort; w += gridDim.x) {
-        const int64_t g0 = (int64_t)w * sh.nparts / nsort, g1 = (int64_t)(w + 1) * sh.nparts / nsort;
-        const uint64_t r0 = pstart[g0], r1 = pstart[g1];
-        cnt[tid] = 0;
-        lpos[tid] = base[(int64_t)tid * nsort + w];
-        __syncthreads();
-        for (uint64_t t0 = r0; t0 < r1; t0 += kWmTile) {
-            uint32_t d[8], rk[8];
-            uint64_t v[8];
-            bool live[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                live[j] = i < r1;
-                v[j] = live[j] ? in[i] : 0ull;
-                d[j] = (uint32_t)((v[j] >> 32) >> win_shift);
-                rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u;
-            }
-            __syncthreads();
-            const uint32_t c = cnt[tid];
-            lofs[tid] = block_excl_scan1024(c, wsum, nullptr);
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (!live[j]) continue;
-                const uint32_t s = lofs[d[j]] + rk[j];
-                st[s] = v[j];
-                st_d[s] = (uint16_t)d[j];
-            }
-            __syncthreads();
-            const int m = (int)std::min<uint64_t>(kWmTile, r1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                out[lpos[dd] + (uint64_t)(s - (int)lofs[dd])] = st[s];
-            }
-            __syncthreads();
-            lpos[tid] += c;
-            cnt[tid] = 0;
-            __syncthreads();
+    const uint32_t dmask = SEG ? (1u << (win_shift - kWmWinBits)) - 1u : 0xFFFFFFFFu;
+    const int dshift = SEG ? kWmWinBits : win_shift;
+    const int64_t units = SEG ? nwin : nsort;
+    for (int64_t w = blockIdx.x; w < units; w += gridDim.x) {
+        uint64_t r0, r1;
+        if (SEG) {
+            r0 = (uint64_t)w << win_shift;
+            r1 = std::min<uint64_t>((uint64_t)sh.n, (uint64_t)(w + 1) << win_shift);
+            lpos[tid] = r0 + ((uint64_t)tid << kWmWinBits);
+        } else {
+            r0 = pstart[w * sh.nparts / nsort];
+            r1 = pstart[(w + 1) * sh.nparts / nsort];
+            lpos[tid] = base[(int64_t)tid * nsort + w];
         }
-        __syncthreads();
-    }
-}
-
-// ---- pass 5b: inside each window, pairs partitioned by output sub-window ----------------------
-// Window w holds exactly the row ids [w << win_shift, (w + 1) << win_shift): its region and
-// every sub-window's place are known without a histogram.
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass5b(int64_t n, int win_shift, int64_t nwin,
-                                                        const uint64_t *__restrict__ in, uint64_t *__restrict__ out) {
-    __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
-    __shared__ uint64_t lpos[kWmDig];
-    __shared__ uint64_t st[kWmTile];
-    __shared__ uint16_t st_d[kWmTile];
-    const int tid = threadIdx.x;
-    const uint32_t dmask = (1u << (win_shift - kWmWinBits)) - 1u;
-    for (int64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
-        const uint64_t r0 = (uint64_t)w << win_shift, r1 = std::min<uint64_t>((uint64_t)n, (uint64_t)(w + 1) << win_shift);
         cnt[tid] = 0;
-        lpos[tid] = r0 + ((uint64_t)tid << kWmWinBits);
         __syncthreads();
+        uint64_t px[8];
+        auto load = [&](uint64_t t0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
+                px[j] = in[i < r1 ? i : r0];
+            }
+        };
+        if (r0 < r1) load(r0);
         for (uint64_t t0 = r0; t0 < r1; t0 += kWmTile) {
             uint32_t d[8], rk[8];
             uint64_t v[8];
             bool live[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                live[j] = i < r1;
-                v[j] = live[j] ? in[i] : 0ull;
-                d[j] = (uint32_t)((v[j] >> 32) >> kWmWinBits) & dmask;
-                rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u;
+                live[j] = t0 + (uint64_t)(j * kWmBlock + tid) < r1;
+                v[j] = px[j];
+                d[j] = (uint32_t)((v[j] >> 32) >> dshift) & dmask;
             }
-            __syncthreads();
-            const uint32_t c = cnt[tid];
-            lofs[tid] = block_excl_scan1024(c, wsum, nullptr);
-            __syncthreads();
+            if (t0 + kWmTile < r1) load(t0 + kWmTile);
+            WM_TILE_RANK(8)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (!live[j]) continue;
@@ -489,35 +534,47 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass5b(int64_t n, int win_shift
                 st[s] = v[j];
                 st_d[s] = (uint16_t)d[j];
             }
-            __syncthreads();
+            wm_barrier();
             const int m = (int)std::min<uint64_t>(kWmTile, r1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
                 out[lpos[dd] + (uint64_t)(s - (int)lofs[dd])] = st[s];
             }
-            __syncthreads();
-            lpos[tid] += c;
+            wm_barrier();
+            lpos[tid] += c_;
             cnt[tid] = 0;
-            __syncthreads();
+            wm_barrier();
         }
         __syncthreads();
     }
 }
 
 // ---- placement: one output window at a time through LDS, rows written in order ---------------
+// The next window's pairs are loaded while this window is written out.
 __global__ __launch_bounds__(kWmBlock) void k_wm_place(int64_t n, const uint64_t *__restrict__ pairs,
                                                        int64_t *__restrict__ out) {
-    __shared__ uint32_t buf[1 << kWmWinBits];
-    const int64_t nw = (n + (1 << kWmWinBits) - 1) >> kWmWinBits;
-    for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const int64_t r0 = w << kWmWinBits, r1 = std::min<int64_t>(n, r0 + (1 << kWmWinBits));
-        for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) {
-            const uint64_t p = pairs[i];
-            buf[(uint32_t)(p >> 32) - (uint32_t)r0] = (uint32_t)p;
+    constexpr int W = 1 << kWmWinBits, PER = W / kWmBlock;
+    __shared__ uint32_t buf[W];
+    const int64_t nw = (n + W - 1) >> kWmWinBits;
+    uint64_t px[PER];
+    auto load = [&](int64_t w) {
+        const int64_t r0 = w << kWmWinBits, r1 = std::min<int64_t>(n, r0 + W);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int64_t i = r0 + j * kWmBlock + threadIdx.x;
+            px[j] = i < r1 ? pairs[i] : ~0ull;
         }
-        __syncthreads();
+    };
+    if ((int64_t)blockIdx.x < nw) load(blockIdx.x);
+    for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
+        const int64_t r0 = w << kWmWinBits, r1 = std::min<int64_t>(n, r0 + W);
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (px[j] != ~0ull) buf[(uint32_t)(px[j] >> 32) - (uint32_t)r0] = (uint32_t)px[j];
+        if (w + gridDim.x < nw) load(w + gridDim.x);
+        wm_barrier();
         for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) out[i] = (int64_t)buf[i - r0];
-        __syncthreads();
+        wm_barrier();
     }
 }
 
@@ -605,6 +662,7 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     wf.func = func;
     wf.param = param;
     wf.win_shift = win_shift;
+    wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
     {
         KernelTimer kt(ctx, "window_sort");
         hipLaunchKernelGGL(k_wm_sort<false>, dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
@@ -626,12 +684,13 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         const uint64_t *placed = pa.as<uint64_t>();
         if (nwin > 1) {
             QEH_TRY(exclusive_scan_u32(ctx, cnt5.as<uint32_t>(), base5.as<uint64_t>(), nc5, nullptr));
-            hipLaunchKernelGGL(k_wm_pass5a, dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh, nsort, win_shift,
-                               pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(), pb.as<uint64_t>());
+            hipLaunchKernelGGL(k_wm_pass5<false>, dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh, nsort,
+                               win_shift, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(), pb.as<uint64_t>());
             placed = pb.as<uint64_t>();
             if (d2 > 0) {
-                hipLaunchKernelGGL(k_wm_pass5b, dim3((unsigned)std::min<int64_t>(cus, nwin)), dim3(kWmBlock), 0, ctx->stream, n,
-                                   win_shift, nwin, pb.as<uint64_t>(), pa.as<uint64_t>());
+                hipLaunchKernelGGL(k_wm_pass5<true>, dim3((unsigned)std::min<int64_t>(cus, nwin)), dim3(kWmBlock), 0,
+                                   ctx->stream, sh, nsort, win_shift, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(),
+                                   pb.as<uint64_t>(), pa.as<uint64_t>());
                 placed = pa.as<uint64_t>();
             }
         }
