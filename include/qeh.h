@@ -168,7 +168,10 @@ int qeh_kernel_time(qeh_ctx *ctx, const char *name, double *total_ms, int64_t *l
  *   UNIT_F64    : (double)(u >> 11) * 2^-53            in [0,1)
  *   PERMUTATION : (row * 0x9E3779B1 + col_id) % modulus  (bijection when
  *                 gcd(0x9E3779B1, modulus) == 1)                            */
-enum qeh_gen_kind { QEH_GEN_UNIFORM_MOD = 0, QEH_GEN_UNIT_F64 = 1, QEH_GEN_PERMUTATION = 2 };
+/* QEH_GEN_SPARSE_KEY: a 64-bit key H(x) = splitmix64(x ^ seed-derived salt), a bijection of x,
+ * with x = the row (modulus == 0: distinct dimension keys) or x = uniform(row) % modulus
+ * (modulus > 0: fact keys drawn from the same key set). */
+enum qeh_gen_kind { QEH_GEN_UNIFORM_MOD = 0, QEH_GEN_UNIT_F64 = 1, QEH_GEN_PERMUTATION = 2, QEH_GEN_SPARSE_KEY = 3 };
 int qeh_generate(qeh_ctx *ctx, int kind, uint64_t seed, uint64_t col_id, int64_t row0,
                  int64_t n, int64_t modulus, int64_t lo, void *out_values);
 

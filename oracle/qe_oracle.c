@@ -77,6 +77,9 @@ void qo_generate(int kind, uint64_t seed, uint64_t col_id, int64_t row0, int64_t
             ((int64_t *)out)[i] = (int64_t)(splitmix64(base + row) % (uint64_t)modulus) + lo;
         else if (kind == QEH_GEN_UNIT_F64)
             ((double *)out)[i] = (double)(splitmix64(base + row) >> 11) * 0x1.0p-53;
+        else if (kind == QEH_GEN_SPARSE_KEY)
+            ((int64_t *)out)[i] = (int64_t)splitmix64((modulus > 0 ? splitmix64(base + row) % (uint64_t)modulus : row) ^
+                                                      (seed * 0xD6E8FEB86659FD93ull));
         else
             ((int64_t *)out)[i] = (int64_t)((row * 0x9E3779B1ull + col_id) % (uint64_t)modulus) + lo;
     }

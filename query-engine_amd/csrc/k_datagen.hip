@@ -23,6 +23,9 @@ __global__ void k_generate(uint64_t seed, uint64_t col_id, int64_t row0, int64_t
             ((int64_t *)out)[i] = (int64_t)(splitmix64(base + row) % (uint64_t)modulus) + lo;
         } else if (KIND == QEH_GEN_UNIT_F64) {
             ((double *)out)[i] = (double)(splitmix64(base + row) >> 11) * 0x1.0p-53;
+        } else if (KIND == QEH_GEN_SPARSE_KEY) {
+            const uint64_t x = modulus > 0 ? splitmix64(base + row) % (uint64_t)modulus : row;
+            ((int64_t *)out)[i] = (int64_t)splitmix64(x ^ (seed * 0xD6E8FEB86659FD93ull));
         } else {
             ((int64_t *)out)[i] = (int64_t)((row * 0x9E3779B1ull + col_id) % (uint64_t)modulus) + lo;
         }
@@ -39,6 +42,8 @@ extern "C" int qeh_generate(qeh_ctx *ctx, int kind, uint64_t seed, uint64_t col_
     if (n <= 0) return QEH_OK;
     if ((kind == QEH_GEN_UNIFORM_MOD || kind == QEH_GEN_PERMUTATION) && modulus <= 0)
         return fail(QEH_E_INVALID, "qeh_generate: modulus must be positive");
+    if (kind == QEH_GEN_SPARSE_KEY && modulus < 0)
+        return fail(QEH_E_INVALID, "qeh_generate: modulus must be positive");
     DeviceGuard dg(ctx->device);
     const int grid = grid_for(ctx, n, kBlock * 8, 8);
     KernelTimer kt(ctx, "generate");
@@ -50,6 +55,10 @@ extern "C" int qeh_generate(qeh_ctx *ctx, int kind, uint64_t seed, uint64_t col_
         case QEH_GEN_UNIT_F64:
             hipLaunchKernelGGL(k_generate<QEH_GEN_UNIT_F64>, dim3(grid), dim3(kBlock), 0, ctx->stream, seed, col_id, row0, n,
                                modulus, lo, out_values);
+            break;
+        case QEH_GEN_SPARSE_KEY:
+            hipLaunchKernelGGL(k_generate<QEH_GEN_SPARSE_KEY>, dim3(grid), dim3(kBlock), 0, ctx->stream, seed, col_id, row0,
+                               n, modulus, lo, out_values);
             break;
         case QEH_GEN_PERMUTATION:
             hipLaunchKernelGGL(k_generate<QEH_GEN_PERMUTATION>, dim3(grid), dim3(kBlock), 0, ctx->stream, seed, col_id, row0,

@@ -25,7 +25,7 @@ EX_COLUMN, EX_LITERAL, EX_BINARY, EX_UNARY = 1, 2, 3, 4
  OP_AND, OP_OR) = range(13)
 UOP_NOT, UOP_MINUS = 0, 1
 AGG_COUNT, AGG_SUM, AGG_AVG, AGG_MIN, AGG_MAX = range(5)
-GEN_UNIFORM_MOD, GEN_UNIT_F64, GEN_PERMUTATION = 0, 1, 2
+GEN_UNIFORM_MOD, GEN_UNIT_F64, GEN_PERMUTATION, GEN_SPARSE_KEY = 0, 1, 2, 3
 
 
 class QehColumn(C.Structure):

@@ -200,3 +200,32 @@ def test_slice_overflow_falls_back(ctx, monkeypatch):
     v = rng.random(n)
     gk, ga, wk, wa = run_both(ctx, [(x, None), (k, None), (v, None)], 1, PRED, (dk, None), [(dg, None)], AGGS)
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["sparse", "g17", "agg2"])
+def test_metric_widened_shapes_1e7(ctx, shape):
+    """The metric query beyond the dense-key best case at 1e7 fact rows (tools/bench_configs.py
+    `shapes` measures them at 1e9): sparse 64-bit dim keys (GEN_SPARSE_KEY), 2^17 groups, and two
+    aggregate columns.  Device == oracle; the device generator == the oracle's for the new kind."""
+    n, nd = 10_000_000, 1_000_000
+    x = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    v = ob.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    groups = 1 << 17 if shape == "g17" else 1024
+    dg = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, groups)
+    if shape == "sparse":
+        k = ob.generate(abi.GEN_SPARSE_KEY, SEED, 2, n, nd)
+        dk = ob.generate(abi.GEN_SPARSE_KEY, SEED, 0, nd, 0)
+        dev = ctx.generate(abi.GEN_SPARSE_KEY, SEED, 2, 100_000, nd).to_numpy()[0]
+        assert np.array_equal(dev, k[:100_000])
+        assert len(np.unique(dk)) == nd and np.isin(k[:1000], dk).all()
+    else:
+        k = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+        dk = ob.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    probe = [(x, None), (k, None), (v, None)]
+    aggs = AGGS
+    if shape == "agg2":
+        probe.append((ob.generate(abi.GEN_UNIT_F64, SEED, 9, n), None))
+        aggs = [(AF.Sum, 2), (AF.Sum, 3), (AF.Count, 2)]
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=float_idx(aggs, probe))

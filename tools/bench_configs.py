@@ -136,6 +136,48 @@ def cfg3_wide(ctx, scale):
                                                          "note": "kernel_ms = wall: the path has no single timer"})
 
 
+def cfg_metric_shapes(ctx, scale, only=("sparse", "g17", "agg2")):
+    """The metric query beyond the dense-key best case (1e9 fact rows x 1e7 dim rows):
+      sparse  dim keys are sparse 64-bit values (H(i), GEN_SPARSE_KEY), fact keys drawn from them
+      g17     2^17 groups (d.g uniform in [0, 2^17))
+      agg2    two aggregate columns: SUM(f.v), SUM(f.w), COUNT(f.v)
+    Algorithmic bytes: 24 B per fact row (x, k, v; +8 B for w) + 16 B per dim row."""
+    n, nd = int(1e9 * scale), 10_000_000
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    names = ["join_filter_aggregate", "slice_partition", "slice_probe", "join_build", "aggregate_rows"]
+    for shape in only:
+        if shape == "sparse":
+            k = ctx.generate(abi.GEN_SPARSE_KEY, SEED, 2, n, nd)
+            dk = ctx.generate(abi.GEN_SPARSE_KEY, SEED, 0, nd, 0)
+            dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1024)
+            cols, aggs, alg = [x, k, v], [(AF.Sum, 2), (AF.Count, 2)], 24.0
+        elif shape == "g17":
+            k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+            dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+            dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1 << 17)
+            cols, aggs, alg = [x, k, v], [(AF.Sum, 2), (AF.Count, 2)], 24.0
+        else:
+            k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+            dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+            dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1024)
+            w = ctx.generate(abi.GEN_UNIT_F64, SEED, 9, n)
+            cols, aggs, alg = [x, k, v, w], [(AF.Sum, 2), (AF.Sum, 3), (AF.Count, 2)], 32.0
+
+        def fn():
+            gk, ga, g = ctx.join_filter_aggregate(cols, 1, pred, dk, [dg], aggs)
+            for c in gk + ga:
+                c.release()
+            return g
+        wall, kt, g = timed(ctx, fn, 5, names)
+        kms = kt["slice_partition"] + kt["slice_probe"] if kt["slice_partition"] else kt["join_filter_aggregate"]
+        line(f"metric shape {shape} 1e9 x 1e7", n, wall, alg * n + 16.0 * nd, kms,
+             "k_slice_partition + k_slice_probe" if kt["slice_partition"] else "single pass (join_filter_aggregate)",
+             None, {"groups": g, "kernel_split_ms": kt})
+        del k, dk, dg
+
+
 def cfg5(ctx, scale):
     n = int(1e9 * scale)
     k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 20)
@@ -394,7 +436,7 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge, "encode": cfg_encode, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
