@@ -252,11 +252,27 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass2(WmShape sh, const uint64_
 // row id) from the group's copy in LDS; a run above 64 rows (heavy ties) makes the operator
 // fall back to the LSD path.
 struct WmFunc {
-    int32_t func;      // QEH_WIN_ROW_NUMBER / RANK / DENSE_RANK / NTILE
-    int64_t param;     // NTILE buckets
+    int32_t func;      // QEH_WIN_* (ROW_NUMBER .. LAST_VALUE)
+    int64_t param;     // NTILE buckets / LAG, LEAD offset
     int32_t win_shift; // pass-5a digit = row id >> win_shift
     int32_t skip_sort; // QEH_WM_SKIP_SORT (experiments: load/emit cost without the network)
+    // value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column itself): the
+    // value is decoded from the group's order keys
+    int32_t odt;       // order key dtype
+    int32_t asc;
+    int32_t has_dflt;
+    int64_t dflt;      // default bits in the output width
 };
+
+// order key (wm_order_key encoding) -> the column's value bits in its own width
+__device__ __forceinline__ uint64_t wm_decode(uint64_t ok, int asc, int odt) {
+    const uint64_t u = asc ? ok : ~ok;
+    const int64_t o = (int64_t)(u ^ 0x8000000000000000ull);
+    if (odt == QEH_DT_FLOAT64) return (uint64_t)f64_bits(f64_from_order_key(o));
+    if (odt == QEH_DT_FLOAT32) return (uint64_t)__builtin_bit_cast(uint32_t, (float)f64_from_order_key(o));
+    if (odt == QEH_DT_INT32) return (uint64_t)(uint32_t)(int32_t)o;
+    return (uint64_t)o;
+}
 
 template <int R, int KK, int J>
 __device__ __forceinline__ void bitonic_stage32(uint32_t (&k)[R], int lane) {
@@ -317,10 +333,10 @@ struct WmWaveLds {
     uint32_t k[P + P / 32];
 };
 
-template <int R, int P>
+template <int R, int P, bool VF>
 __device__ void wm_group(const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid, int64_t s, int m,
-                         const WmFunc &f, uint64_t *__restrict__ pairs, uint32_t *__restrict__ whist, WmWaveLds<P> &L,
-                         uint32_t *__restrict__ too_big, int lane) {
+                         const WmFunc &f, uint64_t *__restrict__ pairs, uint64_t *__restrict__ vals,
+                         uint32_t *__restrict__ whist, WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
     // coalesced loads (register-major e = r * 64 + lane) into LDS; the group's min / max
     wm_wave_sync();  // the previous group's LDS reads are done
     uint64_t mn = ~0ull, mx = 0ull;
@@ -400,7 +416,21 @@ __device__ void wm_group(const uint64_t *__restrict__ gkey, const uint32_t *__re
         const uint64_t ov = live ? L.ov[pos] : 0ull;
         const uint32_t rid = live ? L.id[pos] : 0u;
         uint32_t res;
-        if (f.func == QEH_WIN_ROW_NUMBER) {
+        if (VF) {  // value functions: (valid flag, value of the source row)
+            int64_t es = e;
+            bool ok = true;
+            if (f.func == QEH_WIN_LAG) ok = f.param <= e, es = e - f.param;
+            else if (f.func == QEH_WIN_LEAD) ok = f.param < (int64_t)m - e, es = e + f.param;
+            else if (f.func == QEH_WIN_FIRST_VALUE) es = 0;
+            else es = m - 1;
+            uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
+            res = f.has_dflt ? 1u : 0u;
+            if (live && ok) {
+                bits = wm_decode(L.ov[L.k[wm_pad((int)es)] & 2047], f.asc, f.odt);
+                res = 1u;
+            }
+            if (live) vals[s + e] = bits;
+        } else if (f.func == QEH_WIN_ROW_NUMBER) {
             res = (uint32_t)e + 1u;
         } else if (f.func == QEH_WIN_NTILE) {
             const int64_t q = m / f.param, rm = m % f.param, r0 = e;
@@ -437,11 +467,11 @@ __device__ void wm_group(const uint64_t *__restrict__ gkey, const uint32_t *__re
 // the groups in turn.  Window histograms are added to counts[digit * grid + w] for pass 5a.
 // BIG = false: groups of <= 1024 rows; BIG = true: 1025..2048 rows, a kernel of its own so its
 // larger LDS area does not limit the common case.
-template <bool BIG>
+template <bool BIG, bool VF>
 __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                           const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid,
-                                                          uint64_t *__restrict__ pairs, uint32_t *__restrict__ counts,
-                                                          uint32_t *__restrict__ too_big) {
+                                                          uint64_t *__restrict__ pairs, uint64_t *__restrict__ vals,
+                                                          uint32_t *__restrict__ counts, uint32_t *__restrict__ too_big) {
     constexpr int P = BIG ? 2048 : 1024;
     __shared__ uint32_t whist[kWmDig];
     __shared__ WmWaveLds<P> wl[kWmSortBlock / 64];
@@ -459,15 +489,15 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, 
                 if (lane == 0) *too_big = 1u;
                 continue;
             }
-            wm_group<32, P>(gkey, gid, s, (int)m, f, pairs, whist, wl[wave], too_big, lane);
+            wm_group<32, P, VF>(gkey, gid, s, (int)m, f, pairs, vals, whist, wl[wave], too_big, lane);
         } else {
             const int mi = (int)m;
             if (mi > 1024) continue;
-            if (mi <= 64) wm_group<1, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
-            else if (mi <= 128) wm_group<2, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
-            else if (mi <= 256) wm_group<4, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
-            else if (mi <= 512) wm_group<8, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
-            else wm_group<16, P>(gkey, gid, s, mi, f, pairs, whist, wl[wave], too_big, lane);
+            if (mi <= 64) wm_group<1, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
+            else if (mi <= 128) wm_group<2, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
+            else if (mi <= 256) wm_group<4, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
+            else if (mi <= 512) wm_group<8, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
+            else wm_group<16, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
         }
     }
     __syncthreads();
@@ -479,26 +509,30 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, 
 // 5a (global): digit = row id >> win_shift, over the row ranges of k_wm_sort's workgroups, at
 // positions from the scanned window histograms.  5b (segmented): window w holds exactly the row
 // ids [w << win_shift, (w + 1) << win_shift), so its region and every output window's place are
-// known without a histogram; digit = (row id >> kWmWinBits) within the window.
-template <bool SEG>
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, int win_shift, int64_t nwin,
+// known without a histogram; digit = (row id >> wbits) within the window.  V: a value array
+// travels with the pairs (value functions; 4096-row tiles to fit the staging in LDS).
+template <bool SEG, bool V>
+__global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, int win_shift, int wbits, int64_t nwin,
                                                        const uint64_t *__restrict__ pstart,
                                                        const uint64_t *__restrict__ base, const uint64_t *__restrict__ in,
-                                                       uint64_t *__restrict__ out) {
+                                                       const uint64_t *__restrict__ inv, uint64_t *__restrict__ out,
+                                                       uint64_t *__restrict__ outv) {
+    constexpr int NJ = V ? 4 : 8, TILE = NJ * kWmBlock;
     __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
     __shared__ uint64_t lpos[kWmDig];
-    __shared__ uint64_t st[kWmTile];
-    __shared__ uint16_t st_d[kWmTile];
+    __shared__ uint64_t st[TILE];
+    __shared__ uint64_t stv[V ? TILE : 1];
+    __shared__ uint16_t st_d[TILE];
     const int tid = threadIdx.x;
-    const uint32_t dmask = SEG ? (1u << (win_shift - kWmWinBits)) - 1u : 0xFFFFFFFFu;
-    const int dshift = SEG ? kWmWinBits : win_shift;
+    const uint32_t dmask = SEG ? (1u << (win_shift - wbits)) - 1u : 0xFFFFFFFFu;
+    const int dshift = SEG ? wbits : win_shift;
     const int64_t units = SEG ? nwin : nsort;
     for (int64_t w = blockIdx.x; w < units; w += gridDim.x) {
         uint64_t r0, r1;
         if (SEG) {
             r0 = (uint64_t)w << win_shift;
             r1 = std::min<uint64_t>((uint64_t)sh.n, (uint64_t)(w + 1) << win_shift);
-            lpos[tid] = r0 + ((uint64_t)tid << kWmWinBits);
+            lpos[tid] = r0 + ((uint64_t)tid << wbits);
         } else {
             r0 = pstart[w * sh.nparts / nsort];
             r1 = pstart[(w + 1) * sh.nparts / nsort];
@@ -506,39 +540,45 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, in
         }
         cnt[tid] = 0;
         __syncthreads();
-        uint64_t px[8];
+        uint64_t px[NJ], pv[NJ];
         auto load = [&](uint64_t t0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                px[j] = in[i < r1 ? i : r0];
+                const uint64_t ii = i < r1 ? i : r0;
+                px[j] = in[ii];
+                if (V) pv[j] = inv[ii];
             }
         };
         if (r0 < r1) load(r0);
-        for (uint64_t t0 = r0; t0 < r1; t0 += kWmTile) {
-            uint32_t d[8], rk[8];
-            uint64_t v[8];
-            bool live[8];
+        for (uint64_t t0 = r0; t0 < r1; t0 += TILE) {
+            uint32_t d[NJ], rk[NJ];
+            uint64_t v[NJ], vv[NJ];
+            bool live[NJ];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 live[j] = t0 + (uint64_t)(j * kWmBlock + tid) < r1;
                 v[j] = px[j];
+                vv[j] = V ? pv[j] : 0ull;
                 d[j] = (uint32_t)((v[j] >> 32) >> dshift) & dmask;
             }
-            if (t0 + kWmTile < r1) load(t0 + kWmTile);
-            WM_TILE_RANK(8)
+            if (t0 + TILE < r1) load(t0 + TILE);
+            WM_TILE_RANK(NJ)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 if (!live[j]) continue;
                 const uint32_t s = lofs[d[j]] + rk[j];
                 st[s] = v[j];
+                if (V) stv[s] = vv[j];
                 st_d[s] = (uint16_t)d[j];
             }
             wm_barrier();
-            const int m = (int)std::min<uint64_t>(kWmTile, r1 - t0);
+            const int m = (int)std::min<uint64_t>(TILE, r1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
-                out[lpos[dd] + (uint64_t)(s - (int)lofs[dd])] = st[s];
+                const uint64_t p = lpos[dd] + (uint64_t)(s - (int)lofs[dd]);
+                out[p] = st[s];
+                if (V) outv[p] = stv[s];
             }
             wm_barrier();
             lpos[tid] += c_;
@@ -550,30 +590,55 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, in
 }
 
 // ---- placement: one output window at a time through LDS, rows written in order ---------------
-// The next window's pairs are loaded while this window is written out.
-__global__ __launch_bounds__(kWmBlock) void k_wm_place(int64_t n, const uint64_t *__restrict__ pairs,
-                                                       int64_t *__restrict__ out) {
-    constexpr int W = 1 << kWmWinBits, PER = W / kWmBlock;
-    __shared__ uint32_t buf[W];
-    const int64_t nw = (n + W - 1) >> kWmWinBits;
-    uint64_t px[PER];
+// The next window's pairs are loaded while this window is written out.  Rank functions: the low
+// 32 bits of a pair are the Int64 result.  Value functions (V): the low bit of a pair is the
+// validity, the value comes from `vals`; ESZ-byte values plus one validity byte per row.
+template <bool V, int ESZ>
+__global__ __launch_bounds__(kWmBlock) void k_wm_place(int64_t n, int wbits, const uint64_t *__restrict__ pairs,
+                                                       const uint64_t *__restrict__ vals, void *__restrict__ out,
+                                                       uint8_t *__restrict__ valid8) {
+    constexpr int WMAX = V ? (1 << 14) : (1 << 15), PER = WMAX / kWmBlock;
+    __shared__ uint32_t buf[V ? 1 : WMAX];
+    __shared__ uint64_t bufv[V ? WMAX : 1];
+    __shared__ uint8_t bufok[V ? WMAX : 1];
+    const int64_t W = (int64_t)1 << wbits;
+    const int64_t nw = (n + W - 1) >> wbits;
+    uint64_t px[PER], pv[PER];
     auto load = [&](int64_t w) {
-        const int64_t r0 = w << kWmWinBits, r1 = std::min<int64_t>(n, r0 + W);
+        const int64_t r0 = w << wbits, r1 = std::min<int64_t>(n, r0 + W);
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int64_t i = r0 + j * kWmBlock + threadIdx.x;
             px[j] = i < r1 ? pairs[i] : ~0ull;
+            if (V) pv[j] = i < r1 ? vals[i] : 0ull;
         }
     };
     if ((int64_t)blockIdx.x < nw) load(blockIdx.x);
     for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const int64_t r0 = w << kWmWinBits, r1 = std::min<int64_t>(n, r0 + W);
+        const int64_t r0 = w << wbits, r1 = std::min<int64_t>(n, r0 + W);
 #pragma unroll
-        for (int j = 0; j < PER; ++j)
-            if (px[j] != ~0ull) buf[(uint32_t)(px[j] >> 32) - (uint32_t)r0] = (uint32_t)px[j];
+        for (int j = 0; j < PER; ++j) {
+            if (px[j] == ~0ull) continue;
+            const uint32_t at = (uint32_t)(px[j] >> 32) - (uint32_t)r0;
+            if (V) {
+                bufv[at] = pv[j];
+                bufok[at] = (uint8_t)(px[j] & 1u);
+            } else {
+                buf[at] = (uint32_t)px[j];
+            }
+        }
         if (w + gridDim.x < nw) load(w + gridDim.x);
         wm_barrier();
-        for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) out[i] = (int64_t)buf[i - r0];
+        for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) {
+            if (!V) {
+                ((int64_t *)out)[i] = (int64_t)buf[i - r0];
+            } else {
+                const uint8_t ok = bufok[i - r0];
+                if (ESZ == 8) ((uint64_t *)out)[i] = ok ? bufv[i - r0] : 0ull;
+                else ((uint32_t *)out)[i] = ok ? (uint32_t)bufv[i - r0] : 0u;
+                valid8[i] = ok;
+            }
+        }
         wm_barrier();
     }
 }
@@ -586,9 +651,13 @@ static bool msd_forced() { return std::getenv("QEH_WINDOW_MSD") != nullptr; }
 
 // Returns kWindowMsdNotEligible (nothing allocated into *out) when the shapes do not fit.
 int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
-               qeh_column *out) {
+               const qeh_column *arg, const int64_t *dflt, qeh_column *out) {
     if (std::getenv("QEH_NO_WINDOW_MSD")) return kWindowMsdNotEligible;
-    if (func != QEH_WIN_ROW_NUMBER && func != QEH_WIN_RANK && func != QEH_WIN_DENSE_RANK && func != QEH_WIN_NTILE)
+    if (func < QEH_WIN_ROW_NUMBER || func > QEH_WIN_LAST_VALUE) return kWindowMsdNotEligible;
+    const bool value_fn = func >= QEH_WIN_LAG;
+    // value functions of the ORDER BY column itself (the value is decoded from its order key)
+    if (value_fn && (!arg || arg->values != order.values || arg->offset != order.offset || arg->dtype != order.dtype ||
+                     arg->length != order.length))
         return kWindowMsdNotEligible;
     const int64_t n = part.length;
     if (n != order.length || n <= 0 || n >= ((int64_t)1 << 32) - 1) return kWindowMsdNotEligible;
@@ -614,15 +683,19 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     const int cus = ctx->props.multiProcessorCount;
     const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (n + kWmTile - 1) / kWmTile));
     sh.span = ((n + g1 - 1) / g1 + kWmTile - 1) / kWmTile * kWmTile;
-    // output windows: nwb bits of row id above the 2^15-row placement window
+    // output windows of 2^wbits rows (the placement's LDS image); pass 5a digits = row id bits
+    // above the window, in at most two levels of 10 bits
+    const int wbits = value_fn ? 14 : kWmWinBits;
     int nbits = 0;
     while (nbits < 63 && ((uint64_t)(n - 1) >> nbits)) ++nbits;
-    const int above = std::max(0, nbits - kWmWinBits);
+    const int above = std::max(0, nbits - wbits);
     const int d2 = std::max(0, above - 10);                 // pass-5b digit bits
-    const int win_shift = kWmWinBits + d2;                  // pass-5a digit = id >> win_shift
+    if (d2 > 10) return kWindowMsdNotEligible;
+    const int win_shift = wbits + d2;                       // pass-5a digit = id >> win_shift
     const int64_t nwin = ((n - 1) >> win_shift) + 1;
+    const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
 
-    DevBuf cnt1, base1, key1, id1, kl1, key2, id2, pst, cnt5, base5, pa, pb, flag;
+    DevBuf cnt1, base1, key1, id1, kl1, key2, id2, pst, cnt5, base5, pa, pb, va, vb, valid8, flag;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
     const int64_t nc5 = (int64_t)kWmDig * nsort;
@@ -656,6 +729,8 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     id1.reset();
     kl1.reset();
     if (pa.alloc(ctx, n * 8) || pb.alloc(ctx, n * 8)) return fail(QEH_E_OOM, "window: out of device memory");
+    if (value_fn && (va.alloc(ctx, n * 8) || vb.alloc(ctx, n * 8) || valid8.alloc(ctx, n)))
+        return fail(QEH_E_OOM, "window: out of device memory");
     QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
     QEH_HIP(hipMemsetAsync(cnt5.p, 0, (size_t)nc5 * 4, ctx->stream));
     WmFunc wf{};
@@ -663,44 +738,84 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     wf.param = param;
     wf.win_shift = win_shift;
     wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
+    wf.odt = order.dtype;
+    wf.asc = asc ? 1 : 0;
+    wf.has_dflt = dflt != nullptr;
+    if (dflt) wf.dflt = esz == 8 ? *dflt : (int64_t)(uint32_t)*dflt;
     {
         KernelTimer kt(ctx, "window_sort");
-        hipLaunchKernelGGL(k_wm_sort<false>, dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
-                           key2.as<uint64_t>(), id2.as<uint32_t>(), pa.as<uint64_t>(), cnt5.as<uint32_t>(),
-                           flag.as<uint32_t>());
-        hipLaunchKernelGGL(k_wm_sort<true>, dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
-                           key2.as<uint64_t>(), id2.as<uint32_t>(), pa.as<uint64_t>(), cnt5.as<uint32_t>(),
-                           flag.as<uint32_t>());
+#define QEH_WM_SORT(BIG, VF)                                                                                         \
+    hipLaunchKernelGGL((k_wm_sort<BIG, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(), \
+                       key2.as<uint64_t>(), id2.as<uint32_t>(), pa.as<uint64_t>(), va.as<uint64_t>(), cnt5.as<uint32_t>(), \
+                       flag.as<uint32_t>())
+        if (value_fn) {
+            QEH_WM_SORT(false, true);
+            QEH_WM_SORT(true, true);
+        } else {
+            QEH_WM_SORT(false, false);
+            QEH_WM_SORT(true, false);
+        }
+#undef QEH_WM_SORT
     }
     QEH_HIP(hipGetLastError());
     uint32_t too_big = 0;
     QEH_TRY(read_small(ctx, &too_big, flag.p, 4));
-    if (too_big) return kWindowMsdNotEligible;  // a group above 2048 rows: the LSD path handles skew
+    if (too_big) return kWindowMsdNotEligible;  // a group above 2048 rows / a long tie run: the LSD path
     key2.reset();
     id2.reset();
-    QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out));
+    QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
     {
         KernelTimer kt(ctx, "window_place");
-        const uint64_t *placed = pa.as<uint64_t>();
+        const uint64_t *placed = pa.as<uint64_t>(), *placed_v = va.as<uint64_t>();
         if (nwin > 1) {
             QEH_TRY(exclusive_scan_u32(ctx, cnt5.as<uint32_t>(), base5.as<uint64_t>(), nc5, nullptr));
-            hipLaunchKernelGGL(k_wm_pass5<false>, dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh, nsort,
-                               win_shift, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(), pb.as<uint64_t>());
+            if (value_fn)
+                hipLaunchKernelGGL((k_wm_pass5<false, true>), dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh,
+                                   nsort, win_shift, wbits, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(),
+                                   va.as<uint64_t>(), pb.as<uint64_t>(), vb.as<uint64_t>());
+            else
+                hipLaunchKernelGGL((k_wm_pass5<false, false>), dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh,
+                                   nsort, win_shift, wbits, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(),
+                                   nullptr, pb.as<uint64_t>(), nullptr);
             placed = pb.as<uint64_t>();
+            placed_v = vb.as<uint64_t>();
             if (d2 > 0) {
-                hipLaunchKernelGGL(k_wm_pass5<true>, dim3((unsigned)std::min<int64_t>(cus, nwin)), dim3(kWmBlock), 0,
-                                   ctx->stream, sh, nsort, win_shift, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(),
-                                   pb.as<uint64_t>(), pa.as<uint64_t>());
+                const dim3 g5((unsigned)std::min<int64_t>(cus, nwin));
+                if (value_fn)
+                    hipLaunchKernelGGL((k_wm_pass5<true, true>), g5, dim3(kWmBlock), 0, ctx->stream, sh, nsort, win_shift, wbits,
+                                       nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pb.as<uint64_t>(), vb.as<uint64_t>(),
+                                       pa.as<uint64_t>(), va.as<uint64_t>());
+                else
+                    hipLaunchKernelGGL((k_wm_pass5<true, false>), g5, dim3(kWmBlock), 0, ctx->stream, sh, nsort, win_shift, wbits,
+                                       nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pb.as<uint64_t>(), nullptr,
+                                       pa.as<uint64_t>(), nullptr);
                 placed = pa.as<uint64_t>();
+                placed_v = va.as<uint64_t>();
             }
         }
-        const int64_t nw = (n + (1 << kWmWinBits) - 1) >> kWmWinBits;
-        hipLaunchKernelGGL(k_wm_place, dim3((unsigned)std::min<int64_t>((int64_t)cus * 2, nw)), dim3(kWmBlock), 0, ctx->stream,
-                           n, placed, (int64_t *)out->values);
+        const int64_t nw = (n + ((int64_t)1 << wbits) - 1) >> wbits;
+        const dim3 gp((unsigned)std::min<int64_t>((int64_t)cus * 2, nw));
+        if (!value_fn)
+            hipLaunchKernelGGL((k_wm_place<false, 8>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, nullptr, out->values,
+                               nullptr);
+        else if (esz == 8)
+            hipLaunchKernelGGL((k_wm_place<true, 8>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, placed_v, out->values,
+                               valid8.as<uint8_t>());
+        else
+            hipLaunchKernelGGL((k_wm_place<true, 4>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, placed_v, out->values,
+                               valid8.as<uint8_t>());
     }
     if (hipGetLastError() != hipSuccess) {
         qeh_column_release(ctx, out);
         return fail(QEH_E_HIP, "window: kernel launch failed");
+    }
+    if (value_fn) {
+        const int st = qeh_bytes_to_validity(ctx, valid8.as<uint8_t>(), n, out->validity);
+        if (st != QEH_OK) {
+            qeh_column_release(ctx, out);
+            return st;
+        }
+        out->null_count = -1;
     }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
         qeh_column_release(ctx, out);

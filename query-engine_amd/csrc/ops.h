@@ -109,8 +109,9 @@ bool expr_has_utf8(const qeh_expr *e, const int32_t *dtypes, int n_cols);
 // (k_window.hip): ROW_NUMBER / RANK / DENSE_RANK / NTILE into a fresh Int64 column.
 // kWindowMsdNotEligible (nothing allocated) when the shapes do not fit.
 constexpr int kWindowMsdNotEligible = -1;
+// LAG / LEAD / FIRST_VALUE / LAST_VALUE when `arg` is the ORDER BY column itself.
 int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
-               qeh_column *out);
+               const qeh_column *arg, const int64_t *dflt, qeh_column *out);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);

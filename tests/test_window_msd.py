@@ -96,3 +96,34 @@ def test_msd_window_default_threshold_full_shape(ctx):
     vv = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 8, n, 2 ** 62, lo=-(2 ** 61))
     got, want, ran = _run(ctx, W.RowNumber, kk, vv, True)
     assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param,default", [(W.Lag, 1, None), (W.Lag, 3, 7), (W.Lead, 1, None), (W.Lead, 2, -5),
+                                                (W.FirstValue, 0, None), (W.LastValue, 0, None)])
+@pytest.mark.parametrize("vdt", [np.int64, np.int32, np.float64, np.float32])
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_value_functions_of_the_order_column(ctx, monkeypatch, func, param, default, vdt, asc):
+    """LAG / LEAD / FIRST_VALUE / LAST_VALUE whose argument is the ORDER BY column (the config-5
+    window bench's LAG(v, 1)): values decoded from the group's order keys, NULL (or the default)
+    outside the partition."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(11)
+    n = 300_000
+    k = r.integers(0, 700, n).astype(np.int64)
+    if vdt in (np.int64, np.int32):
+        v = r.integers(-50, 50, n).astype(vdt)
+    else:
+        v = np.round(r.standard_normal(n), 2).astype(vdt)
+    d = None if default is None else vdt(default)
+    ctx.timing(True)
+    ctx.timing_reset()
+    dv = ctx.upload(v)
+    got_v, got_m = ctx.window(func, [ctx.upload(k)], [dv], [asc], arg=dv, param=param, default=d).to_numpy()
+    ran = _msd_ran(ctx)
+    ctx.timing(False)
+    want_v, want_m = ob.window(func, [ob.HostCol(k)], [ob.HostCol(v)], [asc], arg=ob.HostCol(v), param=param,
+                               default=d)
+    assert ran
+    assert np.array_equal(got_m, want_m)
+    assert np.array_equal(got_v[want_m].view(np.uint8), want_v[want_m].view(np.uint8))
