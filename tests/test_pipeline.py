@@ -229,3 +229,32 @@ def test_metric_widened_shapes_1e7(ctx, shape):
         aggs = [(AF.Sum, 2), (AF.Sum, 3), (AF.Count, 2)]
     gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=float_idx(aggs, probe))
+
+
+@pytest.mark.gpu
+def test_metric_full_size_properties(ctx):
+    """The BASELINE metric query at its full size (1e9 fact rows x 1e7 dim rows, generated in HBM):
+    size-independent properties, each against an independent device computation -- every row with
+    x > 49 is counted in exactly one group (Σ COUNT == the filter's row count), Σ SUM(v) over the
+    groups == the filtered Σ v (1e-6), all 1024 groups present, and every group's COUNT agrees with
+    a second execution (determinism of the integer results)."""
+    n, nd, groups = 1_000_000_000, 10_000_000, 1024
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, groups)
+    gk, ga, g = ctx.join_filter_aggregate([x, k, v], 1, PRED, dk, [dg], AGGS)
+    assert g == groups
+    keys = gk[0].to_numpy()[0]
+    sums, counts = ga[0].to_numpy()[0], ga[1].to_numpy()[0]
+    assert sorted(keys.tolist()) == list(range(groups))
+    fv, rows = ctx.filter([x, v], PRED, out_idx=[1])
+    _, tot, _ = ctx.hash_aggregate([], fv, [(AF.Sum, 0), (AF.Count, 0)])
+    assert int(counts.sum()) == rows == int(tot[1].to_numpy()[0][0])
+    want = float(tot[0].to_numpy()[0][0])
+    assert abs(float(sums.sum()) - want) <= 1e-6 * want
+    del fv
+    gk2, ga2, _ = ctx.join_filter_aggregate([x, k, v], 1, PRED, dk, [dg], AGGS)
+    order1, order2 = np.argsort(keys), np.argsort(gk2[0].to_numpy()[0])
+    assert np.array_equal(counts[order1], ga2[1].to_numpy()[0][order2])
