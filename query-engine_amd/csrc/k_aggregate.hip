@@ -363,7 +363,6 @@ struct SliceRegions {
     uint64_t cap;         // items per region, multiple of kSliceChunk
     int32_t F;            // slices
     int32_t pair_flush;   // phase A: flush two items per lane (4-B key, 16-B value stores)
-    int32_t cached_store; // phase A: plain value stores (stay in the Infinity Cache) instead of nt
     // exact layout (materialising join): region (workgroup r, slice b) starts at
     // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
     const uint64_t *rbase;
@@ -497,8 +496,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                     if (VC) {
                         v2i64 w;
                         w[0] = vv[0], w[1] = vv[1];
-                        if (rg.cached_store) *(v2i64 *)(rg.val + o) = w;
-                        else __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                        __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
                     }
                 } else {
 #pragma unroll
@@ -1514,7 +1512,6 @@ static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPla
     const bool nt = fast_nt_mode() == 1;
     SliceRegions rg = rg_in;
     rg.pair_flush = std::getenv("QEH_SLICE_SINGLE_FLUSH") ? 0 : 1;
-    if (std::getenv("QEH_SLICE_CACHED_STORE")) rg.cached_store = 1;
     KernelTimer kta(ctx, "slice_partition", stream);
 #define QEH_SA(NTV, NAV, NTB)                                                                                  \
     hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in, \
@@ -1641,8 +1638,24 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->n_tiles == n_tiles) {
         grid = pre->grid;  // phase A's workgroups = regions per slice
         rg = pre->rg;  // phase A already ran on the second queue, under the build
-        // the ragged tail (rows past the last full tile) goes first: it overlaps phase A
-        launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+        // The ragged tail (rows past the last full tile, one workgroup) runs on the second queue
+        // right after phase A, once the build it reads is done: launched beside phase A it sat on
+        // one CU for the whole of phase A (profiles/r02: 4.9 ms resident) and slowed that CU's
+        // phase-A workgroup, the one the static tile split waits for.  QEH_TAIL_BESIDE=1: old order.
+        if (std::getenv("QEH_TAIL_BESIDE")) {
+            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+        } else if (n > n_tiles * kSliceTile) {
+            hipStream_t side = aux_stream(ctx), main = ctx->stream;
+            hipEvent_t built;
+            if (hipEventCreateWithFlags(&built, hipEventDisableTiming) != hipSuccess) return 0;
+            (void)hipEventRecord(built, main);
+            (void)hipStreamWaitEvent(side, built, 0);
+            (void)hipEventDestroy(built);
+            ctx->stream = side;
+            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+            ctx->stream = main;
+            (void)hipEventRecord(pre->done, side);
+        }
         tail_done = true;
         if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
     } else {
@@ -1652,7 +1665,6 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
             // chunk's exchange (plain stores) is read back by its phase B from the Infinity Cache
             const int gridc = (int)std::min<int64_t>(ctx->props.multiProcessorCount, chunk);
             if (!slice_regions(ctx, chunk, gridc, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
-            rg.cached_store = 1;
             for (int64_t t0 = 0; t0 < n_tiles; t0 += chunk) {
                 const int64_t nt = std::min<int64_t>(chunk, n_tiles - t0);
                 FastIn ic = in;
