@@ -6,7 +6,8 @@
 //           (a "perfect hash": one 4-B read per probe, table <= 16 B/build row)
 //   PACKED  range < 2^(64-pbits): one uint64 per slot, entry = (key-kmin+1)<<pbits | payload,
 //           linear probing, load <= 0.6 -> one 8-B read per probe (same line almost always)
-//   WIDE    otherwise: int64 keys[] + uint32 payload[] + uint32 state[]
+//   WIDE    otherwise: 16-B slots {int64 key, uint64 payload+1 (0 = empty)}, linear probing,
+//           load <= 0.6 -> one 16-B read per probe step (key and payload in one sector)
 // Payload = build row id (materialising join) or dense group id (fused
 // join->aggregate).  Tables are rebuilt per query (they live for one
 // HashJoin execution, like the reference's per-query Vec<RecordBatch>).
@@ -27,11 +28,17 @@ struct HashTable {
     int64_t kmin;        // DIRECT/PACKED key base
     int64_t kmax;
     uint64_t range;      // DIRECT: entries
-    uint64_t *slots;     // PACKED entries / WIDE keys
-    uint32_t *payload;   // DIRECT entries / WIDE payloads
-    uint32_t *state;     // WIDE occupancy
+    uint64_t *slots;     // PACKED entries / WIDE slot pairs (key, payload+1)
+    uint32_t *payload;   // DIRECT entries
     uint16_t *payload16; // DIRECT with payloads < 65535: 2-B entries (half the cache footprint)
 };
+
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+
+// one WIDE slot (key, payload+1) as a single 16-B load
+__device__ __forceinline__ v2u64 wide_slot(const HashTable &t, uint64_t h) {
+    return ((const v2u64 *)t.slots)[h];
+}
 
 // Probe `key`; calls f(payload) for every match (first match only when
 // unique).  Returns number of matches.
@@ -63,9 +70,10 @@ __device__ __forceinline__ int table_probe(const HashTable &t, int64_t key, F &&
         return found;
     }
     for (uint64_t i = 0; i <= t.mask; ++i) {
-        if (t.state[h] == 0) break;
-        if ((int64_t)t.slots[h] == key) {
-            f(t.payload[h]);
+        const v2u64 e = wide_slot(t, h);
+        if (e[1] == 0) break;
+        if ((int64_t)e[0] == key) {
+            f((uint32_t)(e[1] - 1ull));
             ++found;
             if (t.unique) break;
         }

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_rows(ColSet cols, int64_t n, Pre
     }
 }
 
-// ---- fast fused probe: no-null 8-byte columns, unique DIRECT/PACKED table ------------
+// ---- fast fused probe: no-null 8-byte columns, unique join table (any layout) ----------
 // Each lane owns 8 rows as four 16-byte pairs (every load instruction of a
 // wave reads 1 KiB contiguous); all column loads of a tile are issued before
 // the predicate is evaluated, all table probes before any LDS update, so a
@@ -183,6 +183,18 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
         return e != 0;
     }
     uint64_t h = hash64((uint64_t)key) & t.mask;
+    if (t.kind == TK_WIDE) {
+        for (uint64_t i = 0; i <= t.mask; ++i) {
+            const v2u64 e = wide_slot(t, h);
+            if (e[1] == 0) return false;
+            if ((int64_t)e[0] == key) {
+                gid = (uint32_t)(e[1] - 1ull);
+                return true;
+            }
+            h = (h + 1) & t.mask;
+        }
+        return false;
+    }
     const uint64_t want = (uint64_t)key - (uint64_t)t.kmin + 1ull;
     for (uint64_t i = 0; i <= t.mask; ++i) {
         uint64_t e = t.slots[h];
@@ -1414,7 +1426,7 @@ static bool fast_cols_eligible(const ColSet &cols, const PredPlan &pp, int key_c
 
 static bool fast_eligible(const ColSet &cols, const PredPlan &pp, const GidSource &src, const AggSpecs &specs,
                           FastIn *inp, int *nterms_out, int *nacol_out) {
-    if (!src.jt.unique || (src.jt.kind != TK_DIRECT && src.jt.kind != TK_PACKED)) return false;
+    if (!src.jt.unique) return false;
     if (cols.c[src.key_col].dtype != QEH_DT_INT64) return false;
     return fast_cols_eligible(cols, pp, src.key_col, specs, inp, nterms_out, nacol_out);
 }

@@ -168,15 +168,17 @@ __global__ void k_insert_packed(ColRef key, int64_t n, RowPayload row_payload, H
     }
 }
 
+// WIDE: claim a slot by CAS on its payload word (0 = empty), then store the key.  Probes run
+// only after the build kernel has finished, so a claimed slot's key is always visible to them.
 __global__ void k_insert_wide(ColRef key, int64_t n, RowPayload row_payload, HashTable t) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
         int64_t k = load_i64(key, i);
+        const unsigned long long e = (unsigned long long)payload_of(row_payload, i) + 1ull;
         uint64_t h = hash64((uint64_t)k) & t.mask;
         for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-            if (atomicCAS(&t.state[h], 0u, 1u) == 0u) {
-                t.slots[h] = (uint64_t)k;
-                t.payload[h] = payload_of(row_payload, i);
+            if (atomicCAS((unsigned long long *)&t.slots[2 * h + 1], 0ull, e) == 0ull) {
+                t.slots[2 * h] = (uint64_t)k;
                 break;
             }
             h = (h + 1) & t.mask;
@@ -360,15 +362,11 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
         return QEH_OK;
     }
     t.kind = TK_WIDE;
-    QEH_TRY(out->slots.alloc(ctx, cap * 8));
-    QEH_TRY(out->payload.alloc(ctx, cap * 4));
-    QEH_TRY(out->state.alloc(ctx, cap * 4));
+    QEH_TRY(out->slots.alloc(ctx, cap * 16));
     t.slots = out->slots.as<uint64_t>();
-    t.payload = out->payload.as<uint32_t>();
-    t.state = out->state.as<uint32_t>();
     {
         KernelTimer kt(ctx, "join_build");
-        QEH_HIP(hipMemsetAsync(t.state, 0, cap * 4, ctx->stream));
+        QEH_HIP(hipMemsetAsync(t.slots, 0, cap * 16, ctx->stream));
         hipLaunchKernelGGL(k_insert_wide, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
         t.unique = 0;
         hipLaunchKernelGGL(k_wide_dups, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, t, flag.as<uint32_t>());

@@ -24,7 +24,7 @@ int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t 
 // (row_payload == nullptr) or row_payload[row].
 struct BuiltTable {
     HashTable t{};
-    DevBuf slots, payload, state, payload16;
+    DevBuf slots, payload, payload16;
     int64_t n_inserted = 0;
 };
 // Payload of build row i: ids[i] if ids, else dense[slot[i]] if slot (group
