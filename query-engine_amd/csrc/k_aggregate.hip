@@ -362,6 +362,10 @@ constexpr int kSliceBlock = 1024;                // one workgroup per CU in both
 constexpr int kSliceTile = kSliceBlock * kFastR;  // 8192 probe rows per phase-A iteration
 constexpr int kSliceChunk = 32;                  // items per flushed chunk
 constexpr int kSliceStateWords = 3584;           // phase-B LDS aggregate states (n_slots * G)
+// Group-range slices (G too large for LDS states): phase A looks the group id up and partitions
+// by gid >> kGidSliceBits; phase B aggregates one range of 2^kGidSliceBits groups in LDS.
+constexpr int kGidSliceBits = 12;
+constexpr int kGidStateWords = 16384;            // n_slots * 2^kGidSliceBits <= this (128 KB)
 
 // Workgroup barrier ordering LDS only: the next tile's global loads stay in
 // flight across it (__syncthreads also drains vmcnt).
@@ -381,10 +385,14 @@ struct SliceRegions {
 };
 
 
-template <int NTERMS, int NACOL, bool NT>
+// MODE 0: slices of the join key's offset (k - kmin) >> kSliceBits, items = 16-bit key offsets.
+// MODE 1: the group id is looked up here (any unique table layout) and rows are partitioned by
+// gid >> kGidSliceBits, items = gid & (2^kGidSliceBits - 1); `range` = number of groups.
+template <int NTERMS, int NACOL, bool NT, int MODE = 0>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
-                                                                 int64_t n_tiles, SliceRegions rg) {
+                                                                 int64_t n_tiles, SliceRegions rg, HashTable t) {
     constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
+    constexpr int SB = MODE ? kGidSliceBits : kSliceBits;
     constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
     // per-slice tile counts, carried item counts and region write positions are double-buffered:
     // tile t reads one copy while the next tile's copy is written, so no barrier ends the tile
@@ -422,13 +430,27 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     for (; tile < n_tiles; tile += gridDim.x) {
         ft.eval(in, terms);
         uint32_t sel = ft.sel, off[R], rk[R];
+        if constexpr (MODE == 1) {
+            // all probes first (independent loads in flight), then the LDS ranks
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint64_t o = (uint64_t)ft.k(r) - (uint64_t)kmin;  // out of range -> huge, dropped
-            off[r] = (uint32_t)o;
-            rk[r] = 0;
-            if (((sel >> r) & 1) && o < range) rk[r] = atomicAdd(&cnt[(uint32_t)o >> kSliceBits], 1u);
-            else sel &= ~(1u << r);
+            for (int r = 0; r < R; ++r) {
+                off[r] = 0;
+                if (((sel >> r) & 1) && !probe_unique(t, ft.k(r), off[r])) sel &= ~(1u << r);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                rk[r] = 0;
+                if ((sel >> r) & 1) rk[r] = atomicAdd(&cnt[off[r] >> SB], 1u);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint64_t o = (uint64_t)ft.k(r) - (uint64_t)kmin;  // out of range -> huge, dropped
+                off[r] = (uint32_t)o;
+                rk[r] = 0;
+                if (((sel >> r) & 1) && o < range) rk[r] = atomicAdd(&cnt[(uint32_t)o >> kSliceBits], 1u);
+                else sel &= ~(1u << r);
+            }
         }
         int64_t vcur[R];
 #pragma unroll
@@ -466,8 +488,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!((sel >> r) & 1)) continue;
-            const uint32_t s = lofs[off[r] >> kSliceBits] + rk[r];
-            st_key[s] = (uint16_t)(off[r] & (kSliceKeys - 1));
+            const uint32_t s = lofs[off[r] >> SB] + rk[r];
+            st_key[s] = (uint16_t)(off[r] & ((1u << SB) - 1u));
             if (VC) st_v[s] = vcur[r];
         }
         if (tid < F) {
@@ -594,24 +616,52 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
 // Phase B.  Region slots are enumerated slice-major (slot = b * nreg + r);
 // workgroup w drains the contiguous slot range [w*T/grid, (w+1)*T/grid), so it
 // loads at most a few slices, and its waves take the range's regions in turn.
-template <int NACOL>
-__global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
-                                                             AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
-    constexpr int VC = NACOL > 0 ? 1 : 0;
-    __shared__ __attribute__((aligned(16))) uint16_t tslice[kSliceKeys];
-    __shared__ uint64_t lst[kSliceStateWords];
-    uint32_t *lcnt = (uint32_t *)lst;
-    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int W = kSliceBlock / 64;
-    const int64_t words = (int64_t)specs.n_slots * G;
-    for (int64_t i = tid; i < words; i += kSliceBlock) lst[i] = 0;
+// Merge LDS states laid out [slot][stride] (row counts as u32 in slot 0's words) into the global
+// states for groups g0 + [0, ng).
+__device__ __forceinline__ void slice_states_flush(const uint64_t *lst, int64_t stride, int64_t g0, int64_t ng,
+                                                   const AggSpecs &specs, int64_t G, uint64_t *__restrict__ gstates) {
+    const uint32_t *lcnt = (const uint32_t *)lst;
+    for (int64_t i = threadIdx.x; i < ng; i += blockDim.x) {
+        const uint64_t rows = lcnt[i];
+        if (!rows) continue;
+        const int64_t g = g0 + i;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * stride + i]);
+        }
+    }
+}
+
+__device__ __forceinline__ void slice_states_init(uint64_t *lst, int64_t stride, const AggSpecs &specs) {
+    const int64_t words = (int64_t)specs.n_slots * stride;
+    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) lst[i] = 0;
     __syncthreads();
     for (int a = 0; a < specs.n; ++a) {
         const AggSpec sp = specs.a[a];
         if (sp.kind == AK_MIN || sp.kind == AK_MAX)
-            for (int64_t g = tid; g < G; g += kSliceBlock) lst[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
+            for (int64_t g = threadIdx.x; g < stride; g += blockDim.x)
+                lst[(int64_t)sp.val_slot * stride + g] = (uint64_t)agg_init_value(sp.kind);
     }
+}
+
+// IDENT = false: items are key offsets looked up in an LDS slice of the u16 table; states for all
+// G groups stay in LDS.  IDENT = true (group-range slices): items are group ids within the slice's
+// range of 2^kGidSliceBits groups, whose states live in LDS while the workgroup drains that slice
+// and are merged into the global states when it moves on.
+template <int NACOL, bool IDENT = false>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
+                                                             AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
+    constexpr int VC = NACOL > 0 ? 1 : 0;
+    __shared__ __attribute__((aligned(16))) uint16_t tslice[IDENT ? 8 : kSliceKeys];
+    __shared__ uint64_t lst[IDENT ? kGidStateWords : kSliceStateWords];
+    uint32_t *lcnt = (uint32_t *)lst;
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int W = kSliceBlock / 64;
+    const int64_t stride = IDENT ? (1 << kGidSliceBits) : G;  // LDS state words per slot
+    slice_states_init(lst, stride, specs);
     const int F = rg.F;
     const int64_t T = (int64_t)F * nreg;
     // splits == 0: one contiguous slot range per workgroup; else units of
@@ -632,7 +682,16 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
         const int b = (int)(sb / nreg);
         const int64_t se = std::min<int64_t>(s1, (int64_t)(b + 1) * nreg);
         __syncthreads();
-        if (b != cur_b) {
+        if (IDENT && b != cur_b) {
+            if (cur_b >= 0) {
+                const int64_t g0 = (int64_t)cur_b << kGidSliceBits;
+                slice_states_flush(lst, stride, g0, std::min<int64_t>(stride, G - g0), specs, G, gstates);
+                __syncthreads();
+                slice_states_init(lst, stride, specs);
+            }
+            cur_b = b;
+        }
+        if (!IDENT && b != cur_b) {
             cur_b = b;
             const uint64_t k0 = (uint64_t)b << kSliceBits;
             const uint64_t nk = t.range - k0 < (uint64_t)kSliceKeys ? t.range - k0 : (uint64_t)kSliceKeys;
@@ -664,7 +723,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                     v[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
                 }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) e[j] = (i0 + j * 64 + lane < n_r) ? (uint32_t)tslice[e[j]] : 0u;
+                for (int j = 0; j < 8; ++j)
+                    e[j] = (i0 + j * 64 + lane < n_r) ? (IDENT ? e[j] + 1u : (uint32_t)tslice[e[j]]) : 0u;
                 // aggregate kinds are uniform: switch once per aggregate, then
                 // issue the 8 items' LDS atomics back to back
 #pragma unroll
@@ -672,7 +732,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                     if (e[j]) atomicAdd(lcnt + (e[j] - 1u), 1u);
                 for (int a = 0; a < specs.n; ++a) {
                     const AggSpec sp = specs.a[a];
-                    uint64_t *st = lst + (int64_t)sp.val_slot * G - 1;  // indexed by entry = gid + 1
+                    uint64_t *st = lst + (int64_t)sp.val_slot * stride - 1;  // indexed by entry = gid + 1
                     switch (sp.kind) {
                         case AK_SUM_F:
 #pragma unroll
@@ -699,15 +759,13 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     }
     }
     __syncthreads();
-    for (int64_t g = tid; g < G; g += kSliceBlock) {
-        const uint64_t rows = lcnt[g];
-        if (!rows) continue;
-        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
-        for (int a = 0; a < specs.n; ++a) {
-            const AggSpec sp = specs.a[a];
-            if (sp.kind != AK_COUNT)
-                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lst[(int64_t)sp.val_slot * G + g]);
+    if (IDENT) {
+        if (cur_b >= 0) {
+            const int64_t g0 = (int64_t)cur_b << kGidSliceBits;
+            slice_states_flush(lst, stride, g0, std::min<int64_t>(stride, G - g0), specs, G, gstates);
         }
+    } else {
+        slice_states_flush(lst, stride, 0, G, specs, G, gstates);
     }
 }
 
@@ -1519,18 +1577,25 @@ static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, i
     return hipMemsetAsync(rg->overflow, 0, 4, stream) == hipSuccess;
 }
 
+// gid_table != nullptr: MODE 1 (group-range slices, `range` = groups)
 static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol, int64_t kmin,
-                                   uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg_in, hipStream_t stream) {
+                                   uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg_in, hipStream_t stream,
+                                   const HashTable *gid_table = nullptr) {
     const bool nt = fast_nt_mode() == 1;
     SliceRegions rg = rg_in;
     rg.pair_flush = std::getenv("QEH_SLICE_SINGLE_FLUSH") ? 0 : 1;
     KernelTimer kta(ctx, "slice_partition", stream);
-#define QEH_SA(NTV, NAV, NTB)                                                                                  \
-    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in, \
-                       pp.terms, kmin, range, n_tiles, rg)
+    const HashTable t = gid_table ? *gid_table : HashTable{};
+#define QEH_SA(NTV, NAV, NTB)                                                                                        \
+    if (gid_table)                                                                                                   \
+        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 1>), dim3(grid), dim3(kSliceBlock), 0, stream, in,     \
+                           pp.terms, kmin, range, n_tiles, rg, t);                                                   \
+    else                                                                                                             \
+        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in,        \
+                           pp.terms, kmin, range, n_tiles, rg, t)
 #define QEH_SA_NA(NTV, NTB)                    \
-    if (nacol == 0) QEH_SA(NTV, 0, NTB);       \
-    else QEH_SA(NTV, 1, NTB);
+    if (nacol == 0) { QEH_SA(NTV, 0, NTB); }   \
+    else { QEH_SA(NTV, 1, NTB); }
 #define QEH_SA_NT(NTB)                         \
     if (nterms == 0) { QEH_SA_NA(0, NTB) }     \
     else if (nterms == 1) { QEH_SA_NA(1, NTB) } \
@@ -1728,6 +1793,55 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     return 1;
 }
 
+// Group-range slices for joins whose group states do not fit LDS (G > kSliceStateWords /
+// n_slots): phase A (MODE 1) looks each selected row's group id up in the join table and
+// partitions the rows by gid >> kGidSliceBits; phase B (IDENT) aggregates each range of
+// 2^kGidSliceBits groups in LDS.  Replaces one scattered global atomic per row and aggregate
+// (the generic kernel) by 10 bytes of exchange per selected row.  Returns 1 when it ran; 0 when
+// not eligible or a region overflowed (skewed groups), with the states re-initialised.
+static int try_gid_slices(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
+                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err) {
+    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_GID_SLICES")) return 0;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol) || nacol > 1) return 0;
+    if (((int64_t)specs.n_slots << kGidSliceBits) > kGidStateWords) return 0;
+    const uint64_t F = ((uint64_t)G + (1u << kGidSliceBits) - 1) >> kGidSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return 0;
+    const int64_t n_tiles = n / kSliceTile;
+    if (n_tiles == 0) return 0;
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    DevBuf kbuf, vbuf, cbuf;
+    SliceRegions rg{};
+    if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
+    launch_slice_partition(ctx, in, pp, nterms, nacol, 0, (uint64_t)G, n_tiles, grid, rg, ctx->stream, &src.jt);
+    {
+        KernelTimer ktb(ctx, "slice_probe");
+        const int gridB = ctx->props.multiProcessorCount;
+        if (nacol == 0)
+            hipLaunchKernelGGL((k_slice_probe<0, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, 0, src.jt,
+                               in, specs, G, states);
+        else
+            hipLaunchKernelGGL((k_slice_probe<1, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, 0, src.jt,
+                               in, specs, G, states);
+    }
+    const int64_t done = n_tiles * kSliceTile;
+    if (done < n) {  // ragged tail: generic kernel, global states
+        ColSet tail = cols;
+        for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);
+        launch_agg_rows<GM_JOIN>(ctx, pp.mode, false, 1, 0, tail, n - done, pp, src, specs, G, states, err);
+    }
+    if (hipGetLastError() != hipSuccess) return 0;
+    uint32_t of = 0;
+    if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
+    if (of) {
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
+                           ctx->stream, states, G, specs);
+        return 0;
+    }
+    return 1;
+}
+
 int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_column &probe_val,
                            const qeh_column &build_key, const qeh_column &build_val, qeh_column *out_probe,
                            qeh_column *out_build, int64_t *out_rows) {
@@ -1806,10 +1920,10 @@ int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_
         KernelTimer kt(ctx, "join_probe");
         if (nt)
             hipLaunchKernelGGL((k_slice_partition<0, 1, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
-                               t.kmin, t.range, n_tiles, rg);
+                               t.kmin, t.range, n_tiles, rg, HashTable{});
         else
             hipLaunchKernelGGL((k_slice_partition<0, 1, false>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
-                               t.kmin, t.range, n_tiles, rg);
+                               t.kmin, t.range, n_tiles, rg, HashTable{});
         hipLaunchKernelGGL(k_slice_join_inplace, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin, oa,
                            misses);
         if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
@@ -1959,6 +2073,8 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         else if (gm == GM_JOIN) {
             if (lds && try_slice_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
                                       lds_bytes, pre) == 1) {
+            } else if (!lds && try_gid_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(),
+                                              errw.as<uint32_t>()) == 1) {
             } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
                                               lds_bytes, per_cu)))
                 launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,

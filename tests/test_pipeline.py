@@ -232,6 +232,31 @@ def test_metric_widened_shapes_1e7(ctx, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("groups,skew", [(40_000, False), (1 << 17, False), (300_001, False), (1 << 17, True)])
+def test_group_range_slices(ctx, groups, skew):
+    """More groups than LDS states hold: phase A looks the group id up and partitions the rows by
+    group range, phase B aggregates each range of 4096 groups in LDS (k_slice_partition MODE 1 +
+    k_slice_probe IDENT).  Integer SUM, MIN, MAX and COUNT bit-exact;
+    a group range holding most rows overflows its regions and the generic kernel answers.
+    (The float SUM case is test_metric_widened_shapes_1e7[g17].)"""
+    n, nd = 3_000_000, 400_000
+    x, k, v, dk, dg = metric_data(n, nd, groups)
+    if skew:
+        dg = dg.copy()
+        dg[: nd * 9 // 10] %= 64  # 90 % of the dim keys -> the first group range
+    vi = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 1 << 21, lo=-(1 << 20))
+    probe = [(x, None), (k, None), (vi, None)]  # one aggregate column: the path's limit
+    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Min, 2), (AF.Max, 2)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+    ran = ctx.kernel_time("slice_partition")[1] > 0
+    ctx.timing(False)
+    assert ran
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[])
+
+
+@pytest.mark.gpu
 def test_metric_full_size_properties(ctx):
     """The BASELINE metric query at its full size (1e9 fact rows x 1e7 dim rows, generated in HBM):
     size-independent properties, each against an independent device computation -- every row with
