@@ -171,7 +171,8 @@ def main():
     cfg4 = args.workload == "cfg4"
     # config 4 always runs the distributed plan (a world-1 RCCL group at N = 1); the metric
     # query at N = 1 is the local operator, at N > 1 the broadcast join over RCCL
-    dist = world > 1 or cfg4
+    # QEH_BENCH_FORCE_DIST=1: the N > 1 plan at N = 1 (measures its fixed per-step overhead)
+    dist = world > 1 or cfg4 or bool(os.environ.get("QEH_BENCH_FORCE_DIST"))
     import torch
     if dist:
         import torch.distributed as tdist

@@ -154,6 +154,7 @@ class Context:
 
     def set_stream(self, stream_handle: int) -> None:
         abi.check(self.lib.qeh_set_stream(self.h, stream_handle))
+        self.stream_handle = stream_handle
 
     # ---- timing ----------------------------------------------------------
     def timing(self, on: bool) -> None:

@@ -152,6 +152,7 @@ class DistributedExecutor:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        self.last_final = None  # how the last broadcast join merged its partial states
 
     # ---- column <-> tensor ------------------------------------------------------
     def _bits_to_bytes(self, col: DeviceColumn, bits_ptr: int) -> torch.Tensor:
@@ -278,8 +279,18 @@ class DistributedExecutor:
         return self.ctx.upload(strs, m)
 
     def _sync(self):
+        """Order the library's queue before torch / RCCL work: a host wait, unless the context
+        runs on torch's current stream (set_stream), where stream order already does it."""
         if self.device == "cuda":
+            if getattr(self.ctx, "stream_handle", None) == torch.cuda.current_stream().cuda_stream:
+                return
             self.ctx.sync()
+
+    def _sync_torch(self):
+        """Order torch / RCCL work before the library's queue reads its results: a wait on
+        torch's current stream, unless the context runs on it."""
+        if self.device == "cuda" and getattr(self.ctx, "stream_handle", None) != torch.cuda.current_stream().cuda_stream:
+            torch.cuda.current_stream().synchronize()
 
     # ---- shuffle -----------------------------------------------------------------
     def _exchange_columns(self, cols: Sequence[DeviceColumn], counts) -> Tuple[List[DeviceColumn], List[int]]:
@@ -328,6 +339,7 @@ class DistributedExecutor:
                 vb = ts[nvals] if len(ts) > nvals else torch.ones(len(t), dtype=torch.uint8, device=self.device)
                 valid = _all_to_all(vb, sin, sout, self.group)
             out.append(self._from_tensors(t.dtype, vals[0] if nvals == 1 else vals, valid))
+        self._sync_torch()
         return out, sout
 
     def shuffle(self, key: DeviceColumn, cols: Sequence[DeviceColumn]) -> List[DeviceColumn]:
@@ -421,6 +433,7 @@ class DistributedExecutor:
                 vb = ts[1] if len(ts) > 1 else torch.ones(n, dtype=torch.uint8, device=self.device)
                 valid = self._gather_padded(vb, n, mx, rows)
             out.append(self._from_tensors(c.dtype, vals, valid))
+        self._sync_torch()
         return out
 
     def _gather_padded(self, t: torch.Tensor, n: int, mx: int, rows: Sequence[int]) -> torch.Tensor:
@@ -453,7 +466,80 @@ class DistributedExecutor:
                                                     build_group_keys, aggs)
         if g == 0:
             pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
+        dense = self._final_dense(build_group_keys, probe_cols, pk, pa_, aggs)
+        self.last_final = "dense" if dense is not None else "shuffle"
+        if dense is not None:
+            return dense
         return self._final(pk, pa_, aggs)
+
+    DENSE_MAX_KEYS = 1 << 20
+
+    def _final_dense(self, build_group_keys, probe_cols, pk, pa_, aggs):
+        """Final aggregate of a broadcast join by all-reduce instead of a shuffle, when the single
+        group key is a non-null integer column of the (replicated) dimension whose range spans at
+        most DENSE_MAX_KEYS values: every rank scatters its partial states into dense arrays
+        indexed by key - min, one all_reduce per reduction op (SUM for float SUMs, COUNTs and a
+        presence flag; SUM / MIN / MAX over int64 for integer aggregates) merges them, and each
+        rank keeps the groups with (key - min) % world == rank.  Same result as _final (partial
+        states merged per group, each group on one rank) with one or two collectives and one host
+        read (the key range) instead of a partition kernel, a metadata all_gather, an all-to-all
+        per column and a hash aggregate.  None when not applicable (the caller shuffles)."""
+        if len(build_group_keys) != 1 or len(pk) != 1:
+            return None
+        gcol = build_group_keys[0]
+        if gcol.dtype not in (abi.DT_INT64, abi.DT_INT32) or gcol.c.validity:
+            return None  # (no NULL group key: the key comes from this column through an INNER join)
+        kinds = []
+        for (f, c), col in zip(aggs, pa_):
+            # partial states can be NULL only where an input value can (all-NULL group)
+            if f not in FINAL_OF or (f != AF.Count and probe_cols[c].c.validity):
+                return None
+            if f in (AF.Min, AF.Max) and col.dtype not in (abi.DT_INT64, abi.DT_INT32):
+                return None  # float MIN / MAX keep the shuffle (total-order semantics)
+            kinds.append(f)
+        self._sync()
+        gk = self._to_tensors(gcol)[0]
+        if gk.shape[0] == 0:
+            return None
+        lo, hi = (int(q) for q in torch.stack([gk.min().to(torch.int64), gk.max().to(torch.int64)]).tolist())
+        R = hi - lo + 1
+        if R > self.DENSE_MAX_KEYS:
+            return None
+        dev = gk.device
+        idx = self._to_tensors(pk[0])[0].to(torch.int64) - lo
+        vals = [self._to_tensors(c)[0] for c in pa_]
+        # f64 lanes: presence, float SUMs, COUNTs (exact below 2^53); i64 lanes: integer SUM / MIN / MAX
+        fl = [None] + [j for j, f in enumerate(kinds) if f == AF.Count or (f == AF.Sum and vals[j].is_floating_point())]
+        il = {op: [j for j, f in enumerate(kinds) if f == op and j not in fl] for op in (AF.Sum, AF.Min, AF.Max)}
+        fbuf = torch.zeros((len(fl), R), dtype=torch.float64, device=dev)
+        fbuf[0].index_fill_(0, idx, 1.0)
+        for q, j in enumerate(fl[1:], 1):
+            fbuf[q].index_copy_(0, idx, vals[j].to(torch.float64))
+        dist.all_reduce(fbuf, op=dist.ReduceOp.SUM, group=self.group)
+        ibufs = {}
+        for op, js in il.items():
+            if not js:
+                continue
+            init = {AF.Sum: 0, AF.Min: np.iinfo(np.int64).max, AF.Max: np.iinfo(np.int64).min}[op]
+            b = torch.full((len(js), R), init, dtype=torch.int64, device=dev)
+            for q, j in enumerate(js):
+                b[q].index_copy_(0, idx, vals[j].to(torch.int64))
+            rop = {AF.Sum: dist.ReduceOp.SUM, AF.Min: dist.ReduceOp.MIN, AF.Max: dist.ReduceOp.MAX}[op]
+            dist.all_reduce(b, op=rop, group=self.group)
+            ibufs[op] = (js, b)
+        keys = torch.arange(R, device=dev)
+        own = (fbuf[0] > 0) & (keys % self.world == self.rank)
+        sel = torch.nonzero(own).flatten()
+        out_keys = [self._from_tensors(pk[0].dtype, (sel + lo).to(TORCH_OF[pk[0].dtype]).contiguous(), None)]
+        out_aggs = [None] * len(kinds)
+        for q, j in enumerate(fl[1:], 1):
+            out_aggs[j] = fbuf[q][sel]
+        for js, b in ibufs.values():
+            for q, j in enumerate(js):
+                out_aggs[j] = b[q][sel]
+        cols = [self._from_tensors(c.dtype, v.to(TORCH_OF[c.dtype]).contiguous(), None) for c, v in zip(pa_, out_aggs)]
+        self._sync_torch()
+        return out_keys, cols, int(sel.shape[0])
 
     def join_filter_aggregate_shuffle(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
                                       aggs):

@@ -274,16 +274,21 @@ def check_metric_plans(rank, world, dx, ctx):
     from qe_hip import AggregateFunction as AF, BinaryOp, binop, col, lit
     (x, k, km, v), (dk, dg), (X, K, KM, V), (DK, DG) = metric_shards(rank, world)
     pred = binop(col(0), BinaryOp.Greater, lit(49))
-    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Max, 2)]
     fact = [ctx.upload(x), ctx.upload(k, km), ctx.upload(v)]
-    want = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(K, KM), ob.HostCol(V)], 1, pred, ob.HostCol(DK),
-                                    [ob.HostCol(DG)], aggs)
-    for name, fn in (("shuffle", dx.join_filter_aggregate_shuffle),
-                     ("broadcast", lambda *a: dx.join_filter_aggregate_broadcast(*a, build_sharded=True))):
-        keys, aggs_out, ng = fn(fact, 1, pred, ctx.upload(dk), [ctx.upload(dg)], aggs)
-        res = dx.gather_to_root(keys + aggs_out)
-        if rank == 0:
-            assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=[0, 2]), name
+    # float MAX: the broadcast join merges partial states by shuffle; SUM / COUNT and integer
+    # MIN / MAX / SUM: by dense all-reduce (DistributedExecutor._final_dense)
+    for aggs, floats, final in (([(AF.Sum, 2), (AF.Count, 2), (AF.Max, 2)], [0, 2], "shuffle"),
+                                ([(AF.Sum, 2), (AF.Count, 2), (AF.Min, 0), (AF.Max, 0), (AF.Sum, 0)], [0], "dense")):
+        want = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(K, KM), ob.HostCol(V)], 1, pred, ob.HostCol(DK),
+                                        [ob.HostCol(DG)], aggs)
+        for name, fn in (("shuffle", dx.join_filter_aggregate_shuffle),
+                         ("broadcast", lambda *a: dx.join_filter_aggregate_broadcast(*a, build_sharded=True))):
+            keys, aggs_out, ng = fn(fact, 1, pred, ctx.upload(dk), [ctx.upload(dg)], aggs)
+            if name == "broadcast":
+                assert dx.last_final == final, (dx.last_final, final)
+            res = dx.gather_to_root(keys + aggs_out)
+            if rank == 0:
+                assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=floats), name
 
 
 def mode_gpu_cfg4(rank, world):
