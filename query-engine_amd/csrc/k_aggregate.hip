@@ -2427,7 +2427,10 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     RowPayload rp;  // payload = dense group id of the build row, read through its slot
     rp.slot = slot_of_row.as<uint32_t>();
     rp.dense = gt.dense.as<uint64_t>();
-    QEH_TRY(build_join_table(ctx, *build_key, rp, (uint64_t)std::max<int64_t>(gt.groups - 1, 0), &bt));
+    ctx->build_beside_rows = pre.launched ? n : 0;
+    const int brc = build_join_table(ctx, *build_key, rp, (uint64_t)std::max<int64_t>(gt.groups - 1, 0), &bt);
+    ctx->build_beside_rows = 0;
+    QEH_TRY(brc);
     GidSource src{};
     src.jt = bt.t;
     src.key_col = probe_key_idx;

@@ -118,6 +118,23 @@ __global__ void k_insert_direct16(ColRef key, int64_t n, RowPayload rp, HashTabl
     }
 }
 
+// The same insert with the table split into 8 key ranges, range q written only by workgroups
+// b with b % 8 == q -- consecutive workgroup ids go to different XCDs, so each XCD's scattered
+// 2-B stores stay in its own L2 slice of the table (20 MB table / 8 < 4 MB L2) and leave as
+// whole lines, instead of every XCD dirtying partial lines all over the table.  Every
+// workgroup reads all keys (8 reads of an 80 MB key column, mostly Infinity-Cache hits).
+__global__ void k_insert_direct16_xcd(ColRef key, int64_t n, RowPayload rp, HashTable t) {
+    const uint32_t part = blockIdx.x & 7u;
+    const int64_t nb = gridDim.x >> 3;
+    const uint64_t span = (t.range + 7) >> 3;
+    for (int64_t i = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x; i < n; i += nb * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        const uint64_t o = (uint64_t)load_i64(key, i) - (uint64_t)t.kmin;
+        if (o / span != part) continue;
+        t.payload16[o] = (uint16_t)(payload_of(rp, i) + 1u);
+    }
+}
+
 // Non-zero entries of a table of `n` words of `bytes` bytes (2 or 4), summed into *out.
 __global__ __launch_bounds__(kBlock) void k_count_nonzero(const void *__restrict__ table, uint64_t n, int bytes,
                                                           unsigned long long *out) {
@@ -314,7 +331,17 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
                 QEH_TRY(out->payload16.alloc(ctx, range * 2 + 16));
                 t.payload16 = out->payload16.as<uint16_t>();
                 QEH_HIP(hipMemsetAsync(t.payload16, 0, range * 2 + 16, ctx->stream));
-                hipLaunchKernelGGL(k_insert_direct16, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
+                // XCD-split insert for tables past one L2 when the build runs under a long phase A:
+                // alone it is slower (every workgroup reads all keys: 0.75 vs 0.52 ms for 1e7
+                // rows), beside 1e9 probe rows it disturbs phase A less (6.65-6.76 vs 6.85 ms per
+                // metric step, same box).  QEH_INSERT_XCD=0/1 overrides.
+                bool xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n;
+                if (const char *e = std::getenv("QEH_INSERT_XCD")) xcd = std::atoi(e) != 0;
+                if (xcd)
+                    hipLaunchKernelGGL(k_insert_direct16_xcd, dim3(grid_for(ctx, n, kBlock * 4, 8) * 8), dim3(kBlock), 0,
+                                       ctx->stream, kr, n, row_payload, t);
+                else
+                    hipLaunchKernelGGL(k_insert_direct16, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
                 hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)t.payload16, range, 2,
                                    nz);
             } else {

@@ -100,6 +100,9 @@ struct qeh_ctx {
     bool mm_memo_on = false;
     int mm_memo_n = 0;
     MinMaxMemoEntry mm_memo[4];
+    // set by the fused join-aggregate while its build runs beside a prelaunched phase A: probe
+    // rows streaming meanwhile (build_join_table picks the XCD-split insert when it is long)
+    int64_t build_beside_rows = 0;
 };
 
 namespace qeh {
