@@ -1495,7 +1495,11 @@ static void launch_tail(qeh_ctx *ctx, const ColSet &cols, int64_t n, int64_t don
     if (done >= n) return;
     ColSet tail = cols;
     for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);
-    launch_agg_rows<GM_JOIN>(ctx, pp.mode, true, 1, lds_bytes, tail, n - done, pp, src, specs, G, states, err);
+    // a few workgroups (each merges its LDS partials into the global states): one took 70 us
+    // for the 6464 rows past the last full tile of a 1.25e8-row shard
+    const int grid = (int)std::min<int64_t>(16, (n - done + kAggTile - 1) / kAggTile);
+    launch_agg_rows<GM_JOIN>(ctx, pp.mode, true, std::max(grid, 1), lds_bytes, tail, n - done, pp, src, specs, G, states,
+                             err);
 }
 
 static bool try_fast_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
@@ -1710,6 +1714,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     if (n_tiles == 0) return 0;
     int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
     bool tail_done = false;
+    hipEvent_t tail_ev = nullptr;
     DevBuf kbuf, vbuf, cbuf;
     SliceRegions rg{};
     if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->n_tiles == n_tiles) {
@@ -1719,19 +1724,26 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         // right after phase A, once the build it reads is done: launched beside phase A it sat on
         // one CU for the whole of phase A (profiles/r02: 4.9 ms resident) and slowed that CU's
         // phase-A workgroup, the one the static tile split waits for.  QEH_TAIL_BESIDE=1: old order.
+        // Phase B waits for phase A only; the tail runs on the second queue beside phase B (both
+        // merge into the global states with atomics) and the main queue waits for it after phase B.
         if (std::getenv("QEH_TAIL_BESIDE")) {
             launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
         } else if (n > n_tiles * kSliceTile) {
             hipStream_t side = aux_stream(ctx), main = ctx->stream;
             hipEvent_t built;
             if (hipEventCreateWithFlags(&built, hipEventDisableTiming) != hipSuccess) return 0;
+            if (hipEventCreateWithFlags(&tail_ev, hipEventDisableTiming) != hipSuccess) {
+                (void)hipEventDestroy(built);
+                tail_ev = nullptr;
+                return 0;
+            }
             (void)hipEventRecord(built, main);
             (void)hipStreamWaitEvent(side, built, 0);
             (void)hipEventDestroy(built);
             ctx->stream = side;
             launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
             ctx->stream = main;
-            (void)hipEventRecord(pre->done, side);
+            (void)hipEventRecord(tail_ev, side);
         }
         tail_done = true;
         if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
@@ -1780,6 +1792,10 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         else
             hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, t, in,
                                specs, G, states);
+    }
+    if (tail_ev) {  // the tail beside phase B: the states are complete once it is done too
+        (void)hipStreamWaitEvent(ctx->stream, tail_ev, 0);
+        (void)hipEventDestroy(tail_ev);
     }
     if (hipGetLastError() != hipSuccess) return 0;
     if (!tail_done) launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
