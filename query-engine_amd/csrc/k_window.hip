@@ -64,6 +64,34 @@ __device__ __forceinline__ uint64_t wm_order_key(const ColRef &c, int64_t row, i
     return asc ? u : ~u;
 }
 
+// Typed element loads: the window kernels are instantiated per key / order-key element width, so the
+// loads of a tile are plain vector loads with no dtype switch between them (a switch per element
+// made the compiler wait for every load before issuing the next).  Values are converted after
+// loading, in registers.
+template <int ES>
+__device__ __forceinline__ uint64_t wm_ld(const void *p, int64_t i) {
+    if constexpr (ES == 4) return (uint64_t)((const uint32_t *)p)[i];
+    else return ((const uint64_t *)p)[i];
+}
+// non-temporal: streamed columns should not evict the result runs an inverse pass re-reads from L2
+template <int ES>
+__device__ __forceinline__ uint64_t wm_ld_nt(const void *p, int64_t i) {
+    if constexpr (ES == 4) return (uint64_t)__builtin_nontemporal_load((const uint32_t *)p + i);
+    else return __builtin_nontemporal_load((const uint64_t *)p + i);
+}
+__device__ __forceinline__ int64_t wm_key_val(uint64_t raw, int dtype) {
+    return dtype == QEH_DT_INT32 ? (int64_t)(int32_t)(uint32_t)raw : (int64_t)raw;
+}
+__device__ __forceinline__ uint64_t wm_order_bits(uint64_t raw, int dtype, int asc) {
+    int64_t o;
+    if (dtype == QEH_DT_INT32) o = (int64_t)(int32_t)(uint32_t)raw;
+    else if (dtype == QEH_DT_FLOAT32) o = f64_order_key((double)__builtin_bit_cast(float, (uint32_t)raw));
+    else if (dtype == QEH_DT_FLOAT64) o = f64_order_key(as_f64((int64_t)raw));
+    else o = (int64_t)raw;
+    const uint64_t u = (uint64_t)o ^ 0x8000000000000000ull;
+    return asc ? u : ~u;
+}
+
 struct WmShape {
     int64_t n;
     int64_t kmin;
@@ -74,13 +102,14 @@ struct WmShape {
 };
 
 // ---- pass 1: histogram of the high key digit per workgroup row range -------------------------
+template <int KES>
 __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, uint32_t *__restrict__ counts) {
     __shared__ uint32_t h[kWmDig];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
     for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) {
-        const uint64_t kk = (uint64_t)load_i64(key, i) - (uint64_t)sh.kmin;
+        const uint64_t kk = (uint64_t)wm_key_val(wm_ld<KES>(key.values, i), key.dtype) - (uint64_t)sh.kmin;
         atomicAdd(&h[kk >> sh.lb], 1u);
     }
     __syncthreads();
@@ -98,6 +127,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     wm_barrier();
 
 // ---- pass 1: partition (order key, row id, low key bits) by the high digit -------------------
+template <int KES, int OES>
 __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
                                                        const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
                                                        uint32_t *__restrict__ o_id, uint16_t *__restrict__ o_kl) {
@@ -112,14 +142,14 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, i
     __syncthreads();
     const uint32_t lmask = (1u << sh.lb) - 1u;
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-    int64_t kv[8], ovv[8];
+    uint64_t kv[8], ovv[8];
     auto load = [&](int64_t t0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int64_t i = t0 + j * kWmBlock + tid;
             const int64_t ii = i < r1 ? i : r0;
-            kv[j] = load_i64(key, ii);
-            ovv[j] = load_i64(ord, ii);
+            kv[j] = wm_ld<KES>(key.values, ii);
+            ovv[j] = wm_ld<OES>(ord.values, ii);
         }
     };
     if (r0 < r1) load(r0);
@@ -130,13 +160,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, i
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             live[j] = t0 + j * kWmBlock + tid < r1;
-            const uint64_t kk = (uint64_t)kv[j] - (uint64_t)sh.kmin;
+            const uint64_t kk = (uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin;
             d[j] = (uint32_t)(kk >> sh.lb);
             kl[j] = (uint32_t)kk & lmask;
-            const int64_t o = (ord.dtype == QEH_DT_FLOAT32 || ord.dtype == QEH_DT_FLOAT64) ? f64_order_key(as_f64(ovv[j]))
-                                                                                          : ovv[j];
-            const uint64_t u = (uint64_t)o ^ 0x8000000000000000ull;
-            ok[j] = asc ? u : ~u;
+            ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
         WM_TILE_RANK(8)
@@ -643,8 +670,543 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_place(int64_t n, int wbits, con
     }
 }
 
+// ---- id-free pipeline (rank functions): stable passes replayed in reverse -------------------
+// ROW_NUMBER / RANK / DENSE_RANK / NTILE carry no row ids.  Both partition passes rank a tile's
+// rows STABLY (rows of one digit keep their input order), so every PARTITION BY group ends up in
+// input order and ties sort by position in the group.  The sort writes each row's result (<= 2048,
+// u16) back at the row's own position in the group; two inverse passes then replay the partition
+// passes (same tiles, same deterministic ranks) and gather the results run by run, so the output
+// is written in input order with coalesced stores.  Bytes per row: 8 (histogram) + 16 + 10 (pass
+// 1) + 12 + 8 (pass 2) + 8 + 2 (sort) + 6 (inverse 2) + 10 + 8 (inverse 1) against 14 + 12 of ids
+// and pairs moved through three more passes on the id path.
+
+// Tile rows are wave-contiguous (row = wave * 64 * NJ + j * 64 + lane), so input order is
+// (wave, j, lane).  A wave ranks its rows per digit by ballot matching (lanes of one digit ranked
+// by lane, rounds in order) into per-wave LDS counters; a prefix over the waves gives every row its
+// slot in the digit-sorted tile.  Deterministic: an inverse pass replays it exactly.
+struct WmRankLds {
+    uint16_t wc[kWmBlock / 64][kWmDig];  // per-wave digit counts, then per-wave offsets
+    uint32_t lofs[kWmDig];               // digit start in the tile
+    uint32_t wsum[16];
+};
+
+// Returns the tile's count of digit threadIdx.x.
+template <int NJ>
+__device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], const bool (&live)[NJ], int dbits,
+                                                   uint32_t (&slot)[NJ], WmRankLds &R) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t *wz = (uint32_t *)R.wc[wave];
+    for (int i = lane; i < kWmDig / 2; i += 64) wz[i] = 0u;
+    wm_wave_sync();
+    uint32_t r[NJ];
+    const uint64_t below_mask = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        uint64_t m = __ballot(live[j]);
+        for (int b = 0; b < dbits; ++b) {
+            const bool bit = (d[j] >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint64_t below = m & below_mask;
+        uint32_t old = 0;
+        if (live[j] && below == 0) {
+            old = R.wc[wave][d[j]];
+            R.wc[wave][d[j]] = (uint16_t)(old + (uint32_t)__popcll(m));
+        }
+        const int leader = live[j] ? __ffsll((long long)m) - 1 : lane;
+        r[j] = (uint32_t)__shfl((int)old, leader, 64) + (uint32_t)__popcll(below);
+        wm_wave_sync();
+    }
+    wm_barrier();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWmBlock / 64; ++w) {
+        const uint32_t c = R.wc[w][tid];
+        R.wc[w][tid] = (uint16_t)tot;
+        tot += c;
+    }
+    const uint32_t lo = block_excl_scan1024(tot, R.wsum);
+    R.lofs[tid] = lo;
+    wm_barrier();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) slot[j] = live[j] ? R.lofs[d[j]] + R.wc[wave][d[j]] + r[j] : 0u;
+    return tot;
+}
+
+__host__ __device__ __forceinline__ int wm_digit_bits(int64_t ndig) {
+    int b = 0;
+    while (b < 11 && ((int64_t)1 << b) < ndig) ++b;
+    return b;
+}
+
+// pass 1: stable 2^dbits-way partition of (order key, low key bits) by the high key digit
+template <int KES, int OES>
+__global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
+                                                        const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
+                                                        uint16_t *__restrict__ o_kl) {
+    __shared__ WmRankLds R;
+    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint64_t st_key[kWmTile];
+    __shared__ uint16_t st_kl[kWmTile], st_d[kWmTile];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NJ = kWmTile / kWmBlock;
+    lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const int dbits = wm_digit_bits(sh.nb);
+    const uint32_t lmask = (1u << sh.lb) - 1u;
+    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
+    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
+    uint64_t kv[NJ], ovv[NJ];
+    auto load = [&](int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int64_t i = t0 + woff + j * 64;
+            const int64_t ii = i < r1 ? i : r0;
+            kv[j] = wm_ld<KES>(key.values, ii);
+            ovv[j] = wm_ld<OES>(ord.values, ii);
+        }
+    };
+    if (r0 < r1) load(r0);
+    for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
+        uint32_t d[NJ], kl[NJ], slot[NJ];
+        uint64_t ok[NJ];
+        bool live[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            live[j] = t0 + woff + j * 64 < r1;
+            const uint64_t kk = (uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin;
+            d[j] = (uint32_t)(kk >> sh.lb);
+            kl[j] = (uint32_t)kk & lmask;
+            ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
+        }
+        if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
+        const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            if (!live[j]) continue;
+            st_key[slot[j]] = ok[j];
+            st_kl[slot[j]] = (uint16_t)kl[j];
+            st_d[slot[j]] = (uint16_t)d[j];
+        }
+        wm_barrier();
+        const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+        for (int s = tid; s < m; s += kWmBlock) {
+            const uint32_t dd = st_d[s];
+            const uint64_t p = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+            o_key[p] = st_key[s];
+            o_kl[p] = st_kl[s];
+        }
+        wm_barrier();
+        lpos[tid] += tcnt;
+    }
+}
+
+// pass 2: inside each bucket, stable partition by the low digit; group starts -> pstart
+__global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
+                                                        const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
+                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart) {
+    __shared__ WmRankLds R;
+    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint64_t st_key[kWmTile];
+    __shared__ uint16_t st_d[kWmTile];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NJ = kWmTile / kWmBlock;
+    const int64_t L = (int64_t)1 << sh.lb;
+    const int dbits = sh.lb;
+    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
+    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
+        const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
+        R.lofs[tid] = 0;
+        __syncthreads();
+        for (int64_t i = s0 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
+        __syncthreads();
+        {
+            const uint32_t ex = block_excl_scan1024(R.lofs[tid], R.wsum);
+            const int64_t part = (int64_t)b * L + tid;
+            if (tid < L && part < sh.nparts) pstart[part] = (uint64_t)(s0 + ex);
+            lpos[tid] = (uint64_t)(s0 + ex);
+        }
+        __syncthreads();
+        uint64_t kx[NJ];
+        uint32_t lx[NJ];
+        auto load = [&](int64_t t0) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int64_t i = t0 + woff + j * 64;
+                const int64_t ii = i < s1 ? i : s0;
+                kx[j] = i_key[ii];
+                lx[j] = i_kl[ii];
+            }
+        };
+        if (s0 < s1) load(s0);
+        for (int64_t t0 = s0; t0 < s1; t0 += kWmTile) {
+            uint32_t d[NJ], slot[NJ];
+            uint64_t keys[NJ];
+            bool live[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                live[j] = t0 + woff + j * 64 < s1;
+                d[j] = lx[j];
+                keys[j] = kx[j];
+            }
+            if (t0 + kWmTile < s1) load(t0 + kWmTile);
+            const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                if (!live[j]) continue;
+                st_key[slot[j]] = keys[j];
+                st_d[slot[j]] = (uint16_t)d[j];
+            }
+            wm_barrier();
+            const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
+            for (int s = tid; s < m; s += kWmBlock) {
+                const uint32_t dd = st_d[s];
+                o_key[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])] = st_key[s];
+            }
+            wm_barrier();
+            lpos[tid] += tcnt;
+        }
+        __syncthreads();
+    }
+}
+
+// group sort without row ids: ties by position in the group (= input order, the passes being
+// stable); each row's result is written at its own position in the group
+// `pre` holds the group's order keys register-major (element r * 64 + lane in pre[r]), loaded by
+// the caller ahead of time.
+template <int R, int P, int RP>
+__device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
+                          WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
+    static_assert(R <= RP, "prefetch too short");
+    wm_wave_sync();  // the previous group's LDS reads are done
+    uint64_t mn = ~0ull, mx = 0ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < m) {
+            const uint64_t o = pre[r];
+            L.ov[e] = o;
+            mn = o < mn ? o : mn;
+            mx = o > mx ? o : mx;
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    const uint64_t span = mx - mn;
+    const int sb = span ? 64 - __clzll((long long)span) : 0;
+    const int shift = sb > 21 ? sb - 21 : 0;
+    wm_wave_sync();  // every lane's order keys are in LDS
+    uint32_t k[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane * R + r;  // lane-major: the network's layout
+        k[r] = e < m ? ((uint32_t)((L.ov[e] - mn) >> shift) << 11) | (uint32_t)e : 0xFFFFFFFFu;
+    }
+    if (!f.skip_sort) bitonic_sort32<R, 2>(k, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) L.k[wm_pad(lane * R + r)] = k[r];
+    wm_wave_sync();
+    // exact order inside runs of equal prefixes (insertion sort by (order key, position))
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e >= m) continue;
+        const uint32_t ke = L.k[wm_pad(e)] >> 11;
+        const bool start = e == 0 || (L.k[wm_pad(e - 1)] >> 11) != ke;
+        if (!start || e + 1 >= m || (L.k[wm_pad(e + 1)] >> 11) != ke) continue;
+        int len = 2;
+        while (e + len < m && (L.k[wm_pad(e + len)] >> 11) == ke) ++len;
+        if (len > 64) {
+            *too_big = 1u;
+            continue;
+        }
+        for (int a = 1; a < len; ++a) {
+            const uint32_t x = L.k[wm_pad(e + a)];
+            const uint64_t xo = L.ov[x & 2047];
+            int b = a - 1;
+            while (b >= 0) {
+                const uint32_t y = L.k[wm_pad(e + b)];
+                if (!wm_less(xo, x & 2047, L.ov[y & 2047], y & 2047)) break;
+                L.k[wm_pad(e + b + 1)] = y;
+                --b;
+            }
+            L.k[wm_pad(e + b + 1)] = x;
+        }
+    }
+    wm_wave_sync();
+    uint32_t carry_rank = 0, carry_dense = 0;
+    uint64_t prev_ov = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        const bool live = e < m;
+        const uint32_t x = live ? L.k[wm_pad(e)] : 0u;
+        const uint32_t pos = x & 2047;
+        const uint64_t ov = live ? L.ov[pos] : 0ull;
+        uint32_t res;
+        if (f.func == QEH_WIN_ROW_NUMBER) {
+            res = (uint32_t)e + 1u;
+        } else if (f.func == QEH_WIN_NTILE) {
+            const int64_t q = m / f.param, rm = m % f.param, r0 = e;
+            res = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
+        } else {
+            uint64_t pv = __shfl_up(ov, 1, 64);
+            if (lane == 0) pv = prev_ov;
+            const uint32_t flag = (e == 0 || pv != ov) ? 1u : 0u;
+            if (f.func == QEH_WIN_RANK) {
+                uint32_t v = flag ? (uint32_t)e : 0u;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = __shfl_up(v, d, 64);
+                    if (lane >= d) v = t > v ? t : v;
+                }
+                v = v > carry_rank ? v : carry_rank;
+                res = v + 1u;
+                carry_rank = __shfl(v, 63, 64);
+            } else {  // DENSE_RANK
+                const uint32_t v = wave_incl_scan(flag) + carry_dense;
+                res = v;
+                carry_dense = __shfl(v, 63, 64);
+            }
+            prev_ov = __shfl(ov, 63, 64);
+        }
+        if (live) L.id[pos] = res;
+    }
+    wm_wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < m) res_out[s + e] = (uint16_t)L.id[e];
+    }
+}
+
+// One wave per group.  BIG: the rare groups of 1025..2048 rows, a kernel of its own (larger LDS
+// area).  (Loading the next group's keys while sorting this one needed 256 VGPRs and ran slower.)
+template <bool BIG>
+__global__ __launch_bounds__(kWmSortBlock) void k_wm2_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
+                                                           const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
+                                                           uint32_t *__restrict__ too_big) {
+    constexpr int P = BIG ? 2048 : 1024;
+    __shared__ WmWaveLds<P> wl[kWmSortBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t g0 = (int64_t)blockIdx.x * sh.nparts / gridDim.x, g1 = (int64_t)(blockIdx.x + 1) * sh.nparts / gridDim.x;
+    for (int64_t g = g0 + wave; g < g1; g += kWmSortBlock / 64) {
+        const int64_t s = (int64_t)pstart[g];
+        const int64_t m = (int64_t)pstart[g + 1] - s;
+        if (m <= 0) continue;
+        if (BIG) {
+            if (m <= 1024) continue;
+            if (m > 2048) {
+                if (lane == 0) *too_big = 1u;
+                continue;
+            }
+        } else if (m > 1024) {
+            continue;
+        }
+        constexpr int RP = BIG ? 32 : 16;
+        uint64_t pre[RP];
+#pragma unroll
+        for (int r = 0; r < RP; ++r) {
+            const int e = r * 64 + lane;
+            pre[r] = e < m ? gkey[s + e] : 0ull;
+        }
+        const int mi = (int)m;
+        if (BIG) wm2_group<RP, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 64) wm2_group<1, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 128) wm2_group<2, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 256) wm2_group<4, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 512) wm2_group<8, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else wm2_group<RP, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+    }
+}
+
+// inverse of pass 2: replay each bucket's tiles, gather the results run by run (group order ->
+// pass-1 order)
+__global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_t *__restrict__ bstart,
+                                                       const uint64_t *__restrict__ pstart, const uint16_t *__restrict__ i_kl,
+                                                       const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1) {
+    __shared__ WmRankLds R;
+    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NJ = kWmTile / kWmBlock;
+    const int64_t L = (int64_t)1 << sh.lb;
+    const int dbits = sh.lb;
+    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
+    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
+        const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
+        {
+            const int64_t part = (int64_t)b * L + tid;
+            lpos[tid] = (tid < L && part < sh.nparts) ? pstart[part] : 0ull;
+        }
+        __syncthreads();
+        uint32_t lx[NJ];
+        auto load = [&](int64_t t0) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int64_t i = t0 + woff + j * 64;
+                lx[j] = __builtin_nontemporal_load(i_kl + (i < s1 ? i : s0));
+            }
+        };
+        if (s0 < s1) load(s0);
+        for (int64_t t0 = s0; t0 < s1; t0 += kWmTile) {
+            uint32_t d[NJ], slot[NJ];
+            bool live[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                live[j] = t0 + woff + j * 64 < s1;
+                d[j] = lx[j];
+            }
+            if (t0 + kWmTile < s1) load(t0 + kWmTile);
+            const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
+            wm_barrier();
+            const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
+            for (int s = tid; s < m; s += kWmBlock) {
+                const uint32_t dd = st_d[s];
+                st_r[s] = res2[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])];
+            }
+            wm_barrier();
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (live[j]) __builtin_nontemporal_store(st_r[slot[j]], res1 + t0 + woff + j * 64);
+            lpos[tid] += tcnt;
+            wm_barrier();
+        }
+        __syncthreads();
+    }
+}
+
+// inverse of pass 1: replay each workgroup's tiles, gather the results run by run and write them in
+// input order as Int64
+template <int KES>
+__global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, const uint64_t *__restrict__ base,
+                                                       const uint16_t *__restrict__ res1, int64_t *__restrict__ out) {
+    __shared__ WmRankLds R;
+    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NJ = kWmTile / kWmBlock;
+    lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const int dbits = wm_digit_bits(sh.nb);
+    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
+    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
+    uint64_t kv[NJ];
+    auto load = [&](int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int64_t i = t0 + woff + j * 64;
+            kv[j] = wm_ld_nt<KES>(key.values, i < r1 ? i : r0);
+        }
+    };
+    if (r0 < r1) load(r0);
+    for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
+        uint32_t d[NJ], slot[NJ];
+        bool live[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            live[j] = t0 + woff + j * 64 < r1;
+            d[j] = (uint32_t)(((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) >> sh.lb);
+        }
+        if (t0 + kWmTile < r1) load(t0 + kWmTile);
+        const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
+        wm_barrier();
+        const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+        for (int s = tid; s < m; s += kWmBlock) {
+            const uint32_t dd = st_d[s];
+            st_r[s] = res1[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])];
+        }
+        wm_barrier();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            if (live[j]) __builtin_nontemporal_store((int64_t)st_r[slot[j]], out + t0 + woff + j * 64);
+        lpos[tid] += tcnt;
+        wm_barrier();
+    }
+}
+
 __global__ void k_wm_set2(uint64_t *a, uint64_t *b, uint64_t v) {
     if (threadIdx.x == 0) *a = v, *b = v;
+}
+
+// The id-free pipeline for the rank functions (shapes checked by window_msd).
+static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
+                       WmShape sh, qeh_column *out) {
+    const int64_t n = sh.n;
+    const int cus = ctx->props.multiProcessorCount;
+    const int g1 = (int)((n + sh.span - 1) / sh.span);
+    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag;
+    const int64_t nc1 = (int64_t)kWmDig * g1;
+    if (cnt1.alloc(ctx, nc1 * 4) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
+        key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
+        flag.alloc(ctx, 8))
+        return fail(QEH_E_OOM, "window: out of device memory");
+    const ColRef kc = make_colref(part), oc = make_colref(order);
+    const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
+    const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
+    int gbx = 2;  // bucket workgroups per CU (pass 2 / its inverse)
+    if (const char *e = std::getenv("QEH_WM_GBX")) gbx = std::max(1, std::atoi(e));
+    const int gb = std::min(cus * gbx, sh.nb);
+    {
+        KernelTimer kt(ctx, "window_partition");
+        hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
+        QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
+        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? k_wm2_pass1<4, 4> : k_wm2_pass1<4, 8>) : (oes == 4 ? k_wm2_pass1<8, 4> : k_wm2_pass1<8, 8>),
+                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh,
+                           base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
+        // bucket starts = the scanned bases of workgroup 0 per digit, then n
+        QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
+                           pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
+        hipLaunchKernelGGL(k_wm2_pass2, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), key1.as<uint64_t>(),
+                           kl1.as<uint16_t>(), key2.as<uint64_t>(), pst.as<uint64_t>());
+    }
+    QEH_HIP(hipGetLastError());
+    key1.reset();
+    if (res2.alloc(ctx, n * 2)) return fail(QEH_E_OOM, "window: out of device memory");
+    QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
+    WmFunc wf{};
+    wf.func = func;
+    wf.param = param;
+    wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
+    const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
+    {
+        KernelTimer kt(ctx, "window_sort");
+        hipLaunchKernelGGL((k_wm2_sort<false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
+                           key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>());
+        hipLaunchKernelGGL((k_wm2_sort<true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
+                           key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>());
+    }
+    QEH_HIP(hipGetLastError());
+    uint32_t too_big = 0;
+    QEH_TRY(read_small(ctx, &too_big, flag.p, 4));
+    if (too_big) return kWindowMsdNotEligible;  // a group above 2048 rows / a long tie run: the LSD path
+    key2.reset();
+    if (res1.alloc(ctx, n * 2)) return fail(QEH_E_OOM, "window: out of device memory");
+    QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out));
+    {
+        KernelTimer kt(ctx, "window_place");
+        hipLaunchKernelGGL(k_wm2_inv2, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
+                           kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>());
+        hipLaunchKernelGGL(kes == 4 ? k_wm2_inv1<4> : k_wm2_inv1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, base1.as<uint64_t>(),
+                           res1.as<uint16_t>(), (int64_t *)out->values);
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        qeh_column_release(ctx, out);
+        return fail(QEH_E_HIP, "window: kernel failed");
+    }
+    return QEH_OK;
 }
 
 static bool msd_forced() { return std::getenv("QEH_WINDOW_MSD") != nullptr; }
@@ -681,7 +1243,11 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     sh.nb = (int32_t)(((range - 1) >> sh.lb) + 1);
     sh.nparts = (int64_t)range;
     const int cus = ctx->props.multiProcessorCount;
-    const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (n + kWmTile - 1) / kWmTile));
+    // pass-1 workgroups (row spans): two per CU by default, so the replaying inverse pass (80 KB of
+    // LDS) runs two per CU and one's barrier phases overlap the other's memory phases
+    int g1x = 2;
+    if (const char *e = std::getenv("QEH_WM_G1X")) g1x = std::max(1, std::atoi(e));
+    const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * g1x, (n + kWmTile - 1) / kWmTile));
     sh.span = ((n + g1 - 1) / g1 + kWmTile - 1) / kWmTile * kWmTile;
     // output windows of 2^wbits rows (the placement's LDS image); pass 5a digits = row id bits
     // above the window, in at most two levels of 10 bits
@@ -695,6 +1261,7 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     const int64_t nwin = ((n - 1) >> win_shift) + 1;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
 
+    if (!value_fn && !std::getenv("QEH_WM_IDS")) return window_noid(ctx, func, part, order, asc, param, sh, out);
     DevBuf cnt1, base1, key1, id1, kl1, key2, id2, pst, cnt5, base5, pa, pb, va, vb, valid8, flag;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
@@ -704,11 +1271,14 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         cnt5.alloc(ctx, nc5 * 4) || base5.alloc(ctx, (nc5 + 1) * 8) || flag.alloc(ctx, 8))
         return fail(QEH_E_OOM, "window: out of device memory");
     const ColRef kc = make_colref(part), oc = make_colref(order);
+    const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
+    const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
     {
         KernelTimer kt(ctx, "window_partition");
-        hipLaunchKernelGGL(k_wm_hist1, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
+        hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
         QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
-        hipLaunchKernelGGL(k_wm_pass1, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, base1.as<uint64_t>(),
+        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? k_wm_pass1<4, 4> : k_wm_pass1<4, 8>) : (oes == 4 ? k_wm_pass1<8, 4> : k_wm_pass1<8, 8>),
+                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, base1.as<uint64_t>(),
                            key1.as<uint64_t>(), id1.as<uint32_t>(), kl1.as<uint16_t>());
     }
     QEH_HIP(hipGetLastError());
