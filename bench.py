@@ -282,13 +282,17 @@ def main():
     part_ms, part_launches = kt["slice_partition"]
     sprobe_ms, _ = kt["slice_probe"]
     probe_ms, probe_launches = kt["join_filter_aggregate"]
-    if cfg4:  # the local device pipeline of the hash-partitioned plan: filter, partition, fused join
-        local_ms = (kt["filter"][0] + kt["partition_move"][0] + probe_ms + kt["join_build"][0]) / args.steps
+    if cfg4:  # the local device pipeline of the hash-partitioned plan: (filter +) exchange pass, fused join
+        # the local join runs the LDS-slice pipeline when its table shape allows (then its two kernels'
+        # events), else the single fused pass; at world size 1 the exchange is the identity (no pass)
+        join_ms = part_ms + sprobe_ms if part_launches else probe_ms
+        local_ms = (kt["filter"][0] + kt["partition_move"][0] + join_ms) / args.steps
         avg_probe_ms = local_ms
-        kernel_name = ("config-4 local pipeline per step: filter + partition_move + join_build + "
-                       "join_filter_aggregate (HIP events)")
-        kernel_split = {nm: kt[nm][0] / args.steps for nm in ("filter", "partition_move", "join_build",
-                                                                 "join_filter_aggregate")}
+        kernel_name = ("config-4 local pipeline per step: fused filter + hash exchange passes (partition_move; "
+                       "filter if not fused) + the local fused join-aggregate (slice_partition + slice_probe, or "
+                       "join_filter_aggregate) (HIP events)")
+        kernel_split = {"filter": kt["filter"][0] / args.steps, "partition_move": kt["partition_move"][0] / args.steps,
+                        "join": join_ms / args.steps, "join_kernels": "slice" if part_launches else "single pass"}
     elif part_launches:  # LDS-slice partitioned pipeline: the two kernels' own event times per query
         q = max(part_launches // max(args.steps, 1), 1) if part_launches >= args.steps else 1
         per = part_launches / q  # queries timed (launches per query > 1 for the chunked pipeline)

@@ -340,6 +340,17 @@ int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_p
 int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, const qeh_column *cols,
                             int n_cols, int64_t *counts, qeh_column *out_cols);
 
+/* FilterExec followed by the hash Exchange of a shuffle stage (executor.rs:131-155, then
+ * partition.rs:151-212 / operators.rs:15-73; config 4's probe side), fused: rows of `cols` whose
+ * `predicate` is TRUE are hash-partitioned by cols[key_idx] (same partition function as
+ * qeh_partition_hash), and columns move_idx[0 .. n_move) leave partition-major (stable) in
+ * out_cols, with per-partition counts.  The predicate must be an AND / OR list of column-literal
+ * comparisons; the key Int32 / Int64; moved columns non-null Int64 / Float64 (1..4) -- otherwise
+ * QEH_E_UNSUPPORTED and the caller runs qeh_filter + qeh_partition_hash_move. */
+int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                                   int key_idx, int n_parts, const int32_t *move_idx, int n_move, int64_t *counts,
+                                   qeh_column *out_cols);
+
 /* Partitioner::partition_by_range (partition.rs:259-341): row -> the first i with
  * value < boundaries[i], else n_boundaries; NULL -> 0; a non-Int64 key puts every row in
  * partition 0, as the reference does.  Same output as qeh_partition_hash. */

@@ -77,16 +77,60 @@ __device__ __forceinline__ void put_slot(ExprRegs<R> &X, int s, const int64_t (&
 // Load rows row0 + r*stride (r < R) of column c; rows >= n are invalid.
 // With stride = 64 and row0 = base + lane every load instruction of a wave
 // reads one contiguous 64-element run (fully coalesced).
+// The dtype switch sits outside the row loop: each arm issues its R loads back to back (a switch
+// per row made the compiler wait for every load before the next).
+template <int R, typename T>
+__device__ __forceinline__ void load_rows_t(const void *p, int64_t row0, int64_t stride, int64_t n, T (&raw)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t row = row0 + r * stride;
+        raw[r] = row < n ? ((const T *)p)[row] : T(0);
+    }
+}
+
 template <int R>
 __device__ __forceinline__ void load_rows(const ColRef &c, int64_t row0, int64_t stride, int64_t n,
                                           int64_t (&out)[R], uint32_t &valid) {
+    switch (c.dtype) {
+        case 3:    // INT64
+        case 5: {  // FLOAT64 bits
+            load_rows_t<R, int64_t>(c.values, row0, stride, n, out);
+            break;
+        }
+        case 2: {  // INT32
+            int32_t t[R];
+            load_rows_t<R, int32_t>(c.values, row0, stride, n, t);
+#pragma unroll
+            for (int r = 0; r < R; ++r) out[r] = (int64_t)t[r];
+            break;
+        }
+        case 7: {  // UINT32
+            uint32_t t[R];
+            load_rows_t<R, uint32_t>(c.values, row0, stride, n, t);
+#pragma unroll
+            for (int r = 0; r < R; ++r) out[r] = (int64_t)t[r];
+            break;
+        }
+        case 4: {  // FLOAT32, widened exactly
+            float t[R];
+            load_rows_t<R, float>(c.values, row0, stride, n, t);
+#pragma unroll
+            for (int r = 0; r < R; ++r) out[r] = __builtin_bit_cast(int64_t, (double)t[r]);
+            break;
+        }
+        default: {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int64_t row = row0 + r * stride;
+                out[r] = row < n ? load_i64(c, row) : 0;
+            }
+        }
+    }
     valid = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int64_t row = row0 + r * stride;
-        bool live = row < n;
-        out[r] = live ? load_i64(c, row) : 0;
-        if (live && col_valid(c, row)) valid |= 1u << r;
+        const int64_t row = row0 + r * stride;
+        if (row < n && col_valid(c, row)) valid |= 1u << r;
     }
 }
 

@@ -26,6 +26,7 @@
 
 #include "../../include/qeh_plan.h"
 #include "device_common.h"
+#include "expr_device.h"
 #include "ops.h"
 
 namespace qeh {
@@ -331,9 +332,12 @@ struct PmCols {
     int32_t n;
 };
 
+// Rows whose id is >= `drop` (the filtered-out rows of a fused filter + exchange) are ranked last
+// and not written.
 template <int NC>
 __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
-                                                             const uint64_t *__restrict__ offs, int nblocks, PmCols cols) {
+                                                             const uint64_t *__restrict__ offs, int nblocks, PmCols cols,
+                                                             uint32_t drop) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;
     __shared__ uint64_t s_val[NC > 0 ? NC : 1][kPmTile];
@@ -403,6 +407,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
         const int cnt = (int)(hi - c0 < kPmTile ? hi - c0 : kPmTile);
         for (int p = t; p < cnt; p += kRsThreads) {
             const uint32_t d = s_id[p];
+            if (d >= drop) continue;
             const uint64_t pos = run[d] + (uint64_t)(p - (int)loc[d]);
 #pragma unroll
             for (int c = 0; c < NC; ++c) cols.dst[c][pos] = s_val[c][p];
@@ -981,6 +986,29 @@ __global__ void k_hash_ids8(HashKeys keys, int64_t n, uint32_t parts, uint8_t *_
             h = hash64(h ^ (hash64(v) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
         }
         ids[i] = (uint8_t)(h % parts);
+    }
+}
+
+// The filter of a shuffle fused into the Exchange's id pass (config 4's probe side): rows whose
+// predicate (an AND / OR list of column-literal comparisons) is TRUE get hash(key) % parts,
+// the others `parts` (dropped by k_part_scatter).  One key column, Int32 / Int64.
+__global__ __launch_bounds__(kBlock) void k_hash_ids8_pred(ColRef key, ColSet cols, PredTerms terms, int64_t n,
+                                                           uint32_t parts, uint8_t *__restrict__ ids) {
+    constexpr int R = 4;
+    for (int64_t t0 = (int64_t)blockIdx.x * kBlock * R; t0 < n; t0 += (int64_t)gridDim.x * kBlock * R) {
+        const int64_t row0 = t0 + threadIdx.x;
+        const uint32_t m = eval_terms<R>(terms, cols, row0, kBlock, n);
+        int64_t kv[R];
+        uint32_t kvalid;
+        load_rows<R>(key, row0, kBlock, n, kv, kvalid);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t i = row0 + (int64_t)r * kBlock;
+            if (i >= n) continue;
+            uint64_t h = 0x9E3779B97F4A7C15ull;  // k_hash_ids8's hash of one key column (NULL skipped)
+            if ((kvalid >> r) & 1u) h = hash64(h ^ (hash64((uint64_t)kv[r]) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+            ids[i] = ((m >> r) & 1u) ? (uint8_t)(h % parts) : (uint8_t)parts;
+        }
     }
 }
 
@@ -1652,7 +1680,7 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         KernelTimer kt(ctx, "partition_move");
 #define QEH_PM(NCV)                                                                                                        \
     hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, \
-                       offs.as<uint64_t>(), nblocks, pc)
+                       offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix)
         if (nc == 1) QEH_PM(1);
         else if (nc == 2) QEH_PM(2);
         else if (nc == 3) QEH_PM(3);
@@ -1678,6 +1706,94 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("partition move: ") + hipGetErrorString(e));
     }
     if (s != QEH_OK) cleanup();
+    return s;
+}
+
+// Filter + Exchange device side in two passes over the probe columns: partition ids of the
+// qualifying rows (k_hash_ids8_pred), per-segment histograms, then the moved columns written
+// partition-major with the rejected rows left out (k_part_scatter with a drop id).
+extern "C" int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *cols, int n_cols, const qeh_expr *predicate,
+                                              int key_idx, int n_parts, const int32_t *move_idx, int n_move,
+                                              int64_t *counts, qeh_column *out_cols) {
+    if (!ctx || !cols || n_cols < 1 || n_cols > kMaxCols || !predicate || key_idx < 0 || key_idx >= n_cols || !counts ||
+        n_parts < 1 || n_parts >= kRadix || n_move < 1 || n_move > kPmMaxCols || !move_idx || !out_cols)
+        return fail(QEH_E_INVALID, "qeh_filter_partition_hash_move: bad argument (1..255 partitions, 1..4 moved columns)");
+    DeviceGuard dg(ctx->device);
+    const int64_t n = cols[0].length;
+    for (int c = 0; c < n_cols; ++c) {
+        QEH_TRY(check_column(cols[c], "filter-partition column"));
+        if (cols[c].length != n) return fail(QEH_E_INVALID, "filter-partition columns have different lengths");
+    }
+    const qeh_column &kc = cols[key_idx];
+    if (kc.dtype != QEH_DT_INT64 && kc.dtype != QEH_DT_INT32)
+        return fail(QEH_E_UNSUPPORTED, "qeh_filter_partition_hash_move: the key must be Int32 / Int64");
+    for (int q = 0; q < n_move; ++q) {
+        if (move_idx[q] < 0 || move_idx[q] >= n_cols) return fail(QEH_E_INVALID, "moved column index out of range");
+        const qeh_column &c = cols[move_idx[q]];
+        if ((c.dtype != QEH_DT_INT64 && c.dtype != QEH_DT_FLOAT64) || (c.validity && c.null_count != 0))
+            return fail(QEH_E_UNSUPPORTED, "qeh_filter_partition_hash_move: moved columns must be non-null Int64 / Float64");
+    }
+    std::vector<int32_t> dts(n_cols);
+    for (int i = 0; i < n_cols; ++i) dts[i] = cols[i].dtype;
+    DevProgram prog;
+    QEH_TRY(compile_expr(predicate, dts.data(), n_cols, &prog));
+    if (prog.result_type != QEH_DT_BOOL) return fail(QEH_E_TYPE, "Filter predicate must return boolean");
+    PredTerms terms{};
+    if (!lower_to_terms(predicate, dts.data(), n_cols, &terms))
+        return fail(QEH_E_UNSUPPORTED, "qeh_filter_partition_hash_move: predicate is not a list of column-literal comparisons");
+    ColSet cs;
+    QEH_TRY(make_colset(cols, n_cols, &cs));
+    std::fill(counts, counts + n_parts, 0);
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
+                                               (int64_t)ctx->props.multiProcessorCount);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    DevBuf ids, hist, offs;
+    QEH_TRY(ids.alloc(ctx, (size_t)std::max<int64_t>(n, 1)));
+    QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
+    QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    std::vector<uint32_t> h((size_t)kRadix * nblocks, 0);
+    int64_t kept = 0;
+    if (n > 0) {
+        KernelTimer kt(ctx, "partition_move");
+        hipLaunchKernelGGL(k_hash_ids8_pred, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                           make_colref(kc), cs, terms, n, (uint32_t)n_parts, ids.as<uint8_t>());
+        hipLaunchKernelGGL(k_rs_hist<uint8_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, 0,
+                           hist.as<uint32_t>(), nblocks);
+        QEH_HIP(hipGetLastError());
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));
+        for (int p = 0; p < n_parts; ++p)
+            for (int b = 0; b < nblocks; ++b) counts[p] += h[(size_t)p * nblocks + b];
+        for (int p = 0; p < n_parts; ++p) kept += counts[p];
+    }
+    int made = 0, s = QEH_OK;
+    for (; made < n_move; ++made)
+        if ((s = alloc_column(ctx, cols[move_idx[made]].dtype, kept, false, &out_cols[made])) != QEH_OK) break;
+    if (s == QEH_OK && kept > 0) {
+        PmCols pc{};
+        pc.n = n_move;
+        for (int q = 0; q < n_move; ++q) {
+            const qeh_column &src = cols[move_idx[q]];
+            pc.src[q] = (const uint64_t *)src.values + src.offset;
+            pc.dst[q] = (uint64_t *)out_cols[q].values;
+        }
+        KernelTimer kt(ctx, "partition_move");
+#define QEH_FPM(NCV)                                                                                                       \
+    hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, \
+                       offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts)
+        if (n_move == 1) QEH_FPM(1);
+        else if (n_move == 2) QEH_FPM(2);
+        else if (n_move == 3) QEH_FPM(3);
+        else QEH_FPM(4);
+#undef QEH_FPM
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "filter-partition move launch failed");
+    }
+    if (s == QEH_OK) {
+        const hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) s = fail(QEH_E_HIP, std::string("filter-partition move: ") + hipGetErrorString(e));
+    }
+    if (s != QEH_OK)
+        for (int q = 0; q < made; ++q) qeh_column_release(ctx, &out_cols[q]);
     return s;
 }
 

@@ -447,6 +447,18 @@ class Context:
                                                    len(cols), counts, out))
         return np.array(counts[:], np.int64), [self._wrap(out[i]) for i in range(len(cols))]
 
+    def filter_partition_hash_move(self, cols: Sequence[DeviceColumn], predicate: PhysicalExpr, key_idx: int,
+                                   n_parts: int, move_idx: Sequence[int]):
+        """qeh_filter_partition_hash_move: (counts, cols[move_idx] of the qualifying rows in
+        partition-major order).  Raises QehError(QEH_E_UNSUPPORTED) for shapes it does not take."""
+        e, keep = predicate.to_c()
+        counts = (C.c_int64 * n_parts)()
+        mi = (C.c_int32 * len(move_idx))(*move_idx)
+        out = (abi.QehColumn * len(move_idx))()
+        abi.check(self.lib.qeh_filter_partition_hash_move(self.h, self._cols(cols), len(cols), C.byref(e), key_idx,
+                                                          n_parts, mi, len(move_idx), counts, out))
+        return np.array(counts[:], np.int64), [self._wrap(out[i]) for i in range(len(move_idx))]
+
     def slice(self, col: DeviceColumn, offset: int, length: int) -> DeviceColumn:
         """Zero-copy view of rows [offset, offset + length) (RecordBatch::slice); keeps `col` alive."""
         if offset < 0 or length < 0 or offset + length > len(col):

@@ -555,14 +555,32 @@ class DistributedExecutor:
         for f, _ in aggs:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        if self.world == 1:
+            # one partition: both hash exchanges are the identity, so the plan is the local fused
+            # operator on this rank's rows (its partial states still go through the final stage)
+            pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
+                                                        build_group_keys, aggs)
+            if g == 0:
+                pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
+            return self._final(pk, pa_, aggs)
         need = sorted({probe_key_idx} | {c for _, c in aggs})
         remap = {c: i for i, c in enumerate(need)}
-        if predicate is not None:
-            cols, _ = self.ctx.filter(probe_cols, predicate, out_idx=need)
-        else:
-            cols = [probe_cols[i] for i in need]
-        pk_col = cols[remap[probe_key_idx]]
-        pcounts, pmoved = self.ctx.partition_hash_move([pk_col], self.world, cols)
+        pcounts = None
+        if predicate is not None and len(need) <= 4:
+            # filter fused into the exchange's partition pass (one read of the probe columns)
+            try:
+                pcounts, pmoved = self.ctx.filter_partition_hash_move(probe_cols, predicate, probe_key_idx,
+                                                                      self.world, need)
+            except abi.QehError as e:
+                if e.status != abi.QEH_E_UNSUPPORTED:
+                    raise
+        if pcounts is None:
+            if predicate is not None:
+                cols, _ = self.ctx.filter(probe_cols, predicate, out_idx=need)
+            else:
+                cols = [probe_cols[i] for i in need]
+            pk_col = cols[remap[probe_key_idx]]
+            pcounts, pmoved = self.ctx.partition_hash_move([pk_col], self.world, cols)
         bcols = [build_key] + list(build_group_keys)
         bcounts, bmoved = self.ctx.partition_hash_move([build_key], self.world, bcols)
         precv, _ = self._exchange_columns(pmoved, pcounts)

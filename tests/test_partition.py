@@ -109,3 +109,42 @@ def test_partition_hash_move_matches_permutation(ctx, n, parts):
         got = m.to_numpy()
         assert np.array_equal(got[0], want[0]) if got[1] is None else \
             (np.array_equal(got[1], want[1]) and np.array_equal(got[0][got[1]], want[0][want[1]]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", [(0, 2), (1, 1), (4097, 2), (300_001, 7), (2_000_003, 8)])
+@pytest.mark.parametrize("int32_key", [False, True])
+def test_filter_partition_hash_move_matches_filter_then_partition(ctx, n, parts, int32_key):
+    """qeh_filter_partition_hash_move == qeh_filter followed by qeh_partition_hash_move (same
+    per-partition counts, same stable partition-major rows): the shuffle's filter fused into the
+    exchange's id pass (config 4's probe side)."""
+    from qe_hip import BinaryOp, binop, col, lit
+    r = np.random.default_rng(n * 3 + parts)
+    x = r.integers(0, 100, n).astype(np.int64)
+    k = r.integers(-5000, 5000, n).astype(np.int32 if int32_key else np.int64)
+    v = r.random(n)
+    w = r.integers(-9, 9, n).astype(np.int64)
+    cols = [ctx.upload(x), ctx.upload(k), ctx.upload(v), ctx.upload(w)]
+    pred = binop(binop(col(0, "x"), BinaryOp.Greater, lit(49)), BinaryOp.And,
+                 binop(col(3, "w"), BinaryOp.NotEqual, lit(0)))
+    move = [1, 2, 3] if not int32_key else [2, 3]
+    counts, moved = ctx.filter_partition_hash_move(cols, pred, 1, parts, move)
+    kept, _ = ctx.filter(cols, pred, out_idx=[1] + move)
+    want_counts, want = ctx.partition_hash_move([kept[0]], parts, kept[1:])
+    assert list(counts) == list(want_counts)
+    assert counts.sum() == int(((x > 49) & (w != 0)).sum())
+    for got, exp in zip(moved, want):
+        assert np.array_equal(got.to_numpy()[0], exp.to_numpy()[0])
+
+
+@pytest.mark.gpu
+def test_filter_partition_hash_move_declines_general_predicates(ctx):
+    """A predicate that is not a list of column-literal comparisons: QEH_E_UNSUPPORTED (the
+    distributed plan then filters and partitions separately)."""
+    from qe_hip import BinaryOp, abi, binop, col, lit
+    n = 1000
+    cols = [ctx.upload(np.arange(n, dtype=np.int64)), ctx.upload(np.ones(n))]
+    pred = binop(binop(col(0, "a"), BinaryOp.Add, lit(1)), BinaryOp.Greater, lit(5))
+    with pytest.raises(abi.QehError) as ei:
+        ctx.filter_partition_hash_move(cols, pred, 0, 2, [1])
+    assert ei.value.status == abi.QEH_E_UNSUPPORTED
