@@ -257,6 +257,16 @@ int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_
                               int n_group_keys, const qeh_agg *aggs, int n_aggs,
                               qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups);
 
+/* Phase A of qeh_join_filter_aggregate ahead of its build side (a distributed broadcast join:
+ * the build shards are still arriving over RCCL).  build_key_range / group_key_range = [min, max,
+ * non-null count] of the full build key / the single build group key.  The next
+ * qeh_join_filter_aggregate with the same probe columns, key and predicate adopts the launched
+ * work when its build columns have exactly these ranges, and discards it otherwise -- results
+ * never depend on the hint.  Not launching (shape outside the LDS-slice path) is not an error. */
+int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                        int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
+                                        int n_aggs, const int64_t *build_key_range, const int64_t *group_key_range);
+
 /* Stable lexicographic sort -> permutation (UINT32 row ids) of the input.
  * Intended semantics of `Sort` (physical_plan.rs:40-44; executor.rs:290-297
  * is the identity): per-key ascending flag, NULLs first, floats totalOrder. */

@@ -1561,6 +1561,55 @@ struct SlicePre {
     }
 };
 
+// Build-side ranges phase A is planned from: build key min / max / non-null count and the
+// group key's (one integer group key).
+struct BuildRanges {
+    int64_t mn[2], mx[2], cnt[2];
+    bool operator==(const BuildRanges &o) const {
+        return std::memcmp(mn, o.mn, sizeof mn) == 0 && std::memcmp(mx, o.mx, sizeof mx) == 0 &&
+               std::memcmp(cnt, o.cnt, sizeof cnt) == 0;
+    }
+};
+
+// Phase A launched by qeh_join_filter_aggregate_prelaunch, waiting on the context for the call it
+// belongs to: the same probe columns, key and predicate (compared by identity / by value).
+struct PendingSlice {
+    SlicePre pre;
+    std::vector<const void *> vals;
+    std::vector<int64_t> offs, lens;
+    int key_idx = -1;
+    std::vector<uint8_t> pred;  // the predicate's serialised form (empty = none)
+    BuildRanges br{};
+    static std::vector<uint8_t> serialise(const qeh_expr *e);
+    bool matches(const qeh_column *cols, int n_cols, int key, const qeh_expr *predicate) const {
+        if (n_cols != (int)vals.size() || key != key_idx) return false;
+        for (int i = 0; i < n_cols; ++i)
+            if (cols[i].values != vals[i] || cols[i].offset != offs[i] || cols[i].length != lens[i]) return false;
+        return serialise(predicate) == pred;
+    }
+    void take(SlicePre *dst) {
+        dst->launched = pre.launched;
+        dst->kmin = pre.kmin;
+        dst->range = pre.range;
+        dst->grid = pre.grid;
+        dst->n_tiles = pre.n_tiles;
+        std::swap(dst->kbuf.p, pre.kbuf.p), std::swap(dst->kbuf.n, pre.kbuf.n), std::swap(dst->kbuf.ctx, pre.kbuf.ctx);
+        std::swap(dst->vbuf.p, pre.vbuf.p), std::swap(dst->vbuf.n, pre.vbuf.n), std::swap(dst->vbuf.ctx, pre.vbuf.ctx);
+        std::swap(dst->cbuf.p, pre.cbuf.p), std::swap(dst->cbuf.n, pre.cbuf.n), std::swap(dst->cbuf.ctx, pre.cbuf.ctx);
+        dst->rg = pre.rg;
+        std::swap(dst->done, pre.done);
+        pre.launched = false;
+    }
+};
+
+std::vector<uint8_t> PendingSlice::serialise(const qeh_expr *e) {
+    std::vector<uint8_t> b;
+    if (!e || !e->nodes || e->n_nodes <= 0) return b;
+    b.resize((size_t)e->n_nodes * sizeof(qeh_expr_node));
+    std::memcpy(b.data(), e->nodes, b.size());
+    return b;
+}
+
 // regions sized for every row selected with keys uniform over the slices, +25 %
 static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, int nacol, DevBuf *kbuf, DevBuf *vbuf,
                           DevBuf *cbuf, SliceRegions *rg, hipStream_t stream) {
@@ -1616,6 +1665,9 @@ static int64_t slice_chunk_tiles() {
     return e ? std::strtoll(e, nullptr, 10) : 0;
 }
 
+static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
+                                  int key_col, const BuildRanges &br, SlicePre *pre);
+
 // Launch phase A ahead of the build when the slice path is predictable from the build key's
 // range alone (and the group count is known to stay small).  Not launching is never an error.
 static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
@@ -1623,16 +1675,25 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
     if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
+    if (n / kSliceTile == 0) return QEH_OK;
+    // build key and group key ranges in one read; the group count is at most the group key's range
+    // (+ the NULL group)
+    const qeh_column both[2] = {build_key, group_key};
+    BuildRanges br;
+    QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
+    return slice_prelaunch_ranges(ctx, cols, n, pp, specs, key_col, br, pre);
+}
+
+static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
+                                  int key_col, const BuildRanges &br, SlicePre *pre) {
+    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
+    if (cols.c[key_col].dtype != QEH_DT_INT64) return QEH_OK;
     FastIn in;
     int nterms, nacol;
     if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 1) return QEH_OK;
     const int64_t n_tiles = n / kSliceTile;
     if (n_tiles == 0) return QEH_OK;
-    // build key and group key ranges in one read; the group count is at most the group key's range
-    // (+ the NULL group)
-    const qeh_column both[2] = {build_key, group_key};
-    int64_t mns[2], mxs[2], cnts[2];
-    QEH_TRY(columns_minmax(ctx, both, 2, mns, mxs, cnts));
+    const int64_t *mns = br.mn, *mxs = br.mx, *cnts = br.cnt;
     const int64_t mn = mns[0], mx = mxs[0], cnt = cnts[0];
     if (cnt == 0) return QEH_OK;
     const uint64_t gr = cnts[1] ? (uint64_t)mxs[1] - (uint64_t)mns[1] + 1ull : 0;
@@ -2399,6 +2460,55 @@ extern "C" int qeh_filter_aggregate(qeh_ctx *ctx, const qeh_column *cols, int n_
                                    input_batches, out_keys, out_aggs, out_groups);
 }
 
+// Phase A of the fused join-aggregate ahead of its build side: the caller knows the build key's
+// and group key's [min, max, non-null count] (e.g. from a small collective over the shards) while
+// the build columns are still in flight (an RCCL all-gather), so phase A streams the probe side
+// meanwhile.  The next qeh_join_filter_aggregate adopts it when its probe columns, key and
+// predicate are the same and the build columns it gets have exactly these ranges; otherwise the
+// work is discarded.  Not launching (shape not eligible) is not an error.
+extern "C" int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                                   int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
+                                                   int n_aggs, const int64_t *build_key_range,
+                                                   const int64_t *group_key_range) {
+    if (!ctx || !probe_cols || n_probe_cols < 1 || !build_key_range || !group_key_range || (n_aggs > 0 && !aggs))
+        return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_prelaunch: bad argument");
+    if (probe_key_idx < 0 || probe_key_idx >= n_probe_cols) return fail(QEH_E_INVALID, "probe key index out of range");
+    DeviceGuard dg(ctx->device);
+    ctx->pending_slice.reset();
+    if (n_aggs == 0) return QEH_OK;
+    const int64_t n = probe_cols[0].length;
+    for (int i = 0; i < n_probe_cols; ++i)
+        if (probe_cols[i].length != n) return fail(QEH_E_INVALID, "probe columns have different lengths");
+    ColSet cols;
+    QEH_TRY(make_colset(probe_cols, n_probe_cols, &cols));
+    std::vector<int32_t> dts(n_probe_cols);
+    std::vector<int> idx(n_probe_cols);
+    for (int i = 0; i < n_probe_cols; ++i) {
+        dts[i] = probe_cols[i].dtype;
+        idx[i] = i;
+    }
+    PredPlan pp;
+    QEH_TRY(plan_predicate(predicate, dts.data(), n_probe_cols, &pp));
+    AggSpecs specs;
+    QEH_TRY(plan_aggs(aggs, n_aggs, probe_cols, n_probe_cols, idx.data(), &specs));
+    auto p = std::make_shared<PendingSlice>();
+    for (int q = 0; q < 2; ++q) {
+        const int64_t *r = q ? group_key_range : build_key_range;
+        p->br.mn[q] = r[0], p->br.mx[q] = r[1], p->br.cnt[q] = r[2];
+    }
+    QEH_TRY(slice_prelaunch_ranges(ctx, cols, n, pp, specs, probe_key_idx, p->br, &p->pre));
+    if (!p->pre.launched) return QEH_OK;
+    for (int i = 0; i < n_probe_cols; ++i) {
+        p->vals.push_back(probe_cols[i].values);
+        p->offs.push_back(probe_cols[i].offset);
+        p->lens.push_back(probe_cols[i].length);
+    }
+    p->key_idx = probe_key_idx;
+    p->pred = PendingSlice::serialise(predicate);
+    ctx->pending_slice = p;
+    return QEH_OK;
+}
+
 extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
                                          int probe_key_idx, const qeh_expr *predicate, const qeh_column *build_key,
                                          const qeh_column *build_group_keys, int n_group_keys, const qeh_agg *aggs,
@@ -2434,7 +2544,22 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     // phase A of the slice path on the second queue, when its shape is known from the build key's
     // range (and the group count is bounded by one integer group key's range)
     SlicePre pre;
-    if (n_group_keys == 1) QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, build_group_keys[0], &pre));
+    std::shared_ptr<PendingSlice> pend = std::static_pointer_cast<PendingSlice>(ctx->pending_slice);
+    ctx->pending_slice.reset();
+    if (pend && n_group_keys == 1 && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate)) {
+        // adopt the phase A launched by qeh_join_filter_aggregate_prelaunch if the build columns that
+        // arrived have exactly the ranges it was planned from
+        const qeh_column both[2] = {*build_key, build_group_keys[0]};
+        BuildRanges br;
+        if (build_key->dtype == QEH_DT_INT64 &&
+            (build_group_keys[0].dtype == QEH_DT_INT64 || build_group_keys[0].dtype == QEH_DT_INT32)) {
+            QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
+            if (br == pend->br) pend->take(&pre);
+        }
+    }
+    pend.reset();  // not adopted: waits for its phase A, frees its regions
+    if (!pre.launched && n_group_keys == 1)
+        QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, build_group_keys[0], &pre));
     // build side: dense group ids of the build rows, then the join table with gid payloads
     GroupTable gt;
     DevBuf slot_of_row;

@@ -103,6 +103,10 @@ struct qeh_ctx {
     // set by the fused join-aggregate while its build runs beside a prelaunched phase A: probe
     // rows streaming meanwhile (build_join_table picks the XCD-split insert when it is long)
     int64_t build_beside_rows = 0;
+    // phase A launched ahead by qeh_join_filter_aggregate_prelaunch (build-side ranges given by the
+    // caller while the build columns are still in flight); adopted or discarded by the next
+    // qeh_join_filter_aggregate (a qeh::PendingSlice)
+    std::shared_ptr<void> pending_slice;
 };
 
 namespace qeh {

@@ -234,6 +234,7 @@ int qeh_shutdown(qeh_ctx *ctx) {
     for (auto e : ctx->event_free) hipEventDestroy(e);
     if (ctx->scratch) ctx->pool->free(ctx->scratch);
     if (ctx->pinned) hipHostFree(ctx->pinned);
+    ctx->pending_slice.reset();  // waits for a prelaunched phase A; its buffers go back to the pool
     ctx->source_cache.reset();  // its columns go back to the pool first
     delete ctx->pool;
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);

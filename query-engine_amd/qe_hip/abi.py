@@ -82,6 +82,7 @@ SIGNATURES = {
     "qeh_hash_join_outer": (I, [P, I, COLP, COLP, I, COLP, COLP, I, COLP, COLP, C.POINTER(I64)]),
     "qeh_join_filter_aggregate": (I, [P, COLP, I, I, EXPRP, COLP, COLP, I, AGGP, I, COLP, COLP,
                                       C.POINTER(I64)]),
+    "qeh_join_filter_aggregate_prelaunch": (I, [P, COLP, I, I, EXPRP, AGGP, I, C.POINTER(I64), C.POINTER(I64)]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_sort_indices_nulls": (I, [P, COLP, I, C.POINTER(C.c_int8), C.POINTER(C.c_int8), COLP]),
     "qeh_concat": (I, [P, COLP, I, COLP]),

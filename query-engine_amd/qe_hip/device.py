@@ -366,6 +366,22 @@ class Context:
         return ([self._wrap(ok[i]) for i in range(len(build_group_keys))],
                 [self._wrap(oa[i]) for i in range(len(aggs))], g.value)
 
+    def join_filter_aggregate_prelaunch(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                                        predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],
+                                        build_key_range: Sequence[int], group_key_range: Sequence[int]) -> None:
+        """qeh_join_filter_aggregate_prelaunch: start phase A from the build side's [min, max, count]
+        ranges; the next join_filter_aggregate on the same probe columns adopts or discards it."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        br = (C.c_int64 * 3)(*[int(q) for q in build_key_range])
+        gr = (C.c_int64 * 3)(*[int(q) for q in group_key_range])
+        abi.check(self.lib.qeh_join_filter_aggregate_prelaunch(self.h, cp, len(probe_cols), probe_key_idx,
+                                                               C.byref(e) if e is not None else None, ca, len(aggs),
+                                                               br, gr))
+
     def sort_indices(self, keys: Sequence[DeviceColumn], ascending: Sequence[bool]) -> DeviceColumn:
         ck = self._cols(keys)
         asc = (C.c_int8 * max(len(keys), 1))(*[1 if a else 0 for a in ascending])

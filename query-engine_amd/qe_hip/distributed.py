@@ -460,7 +460,10 @@ class DistributedExecutor:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
         if build_sharded:
-            full = self.allgather_columns([build_key] + list(build_group_keys))
+            full = self._allgather_beside_phase_a(probe_cols, probe_key_idx, predicate, build_key,
+                                                  build_group_keys, aggs)
+            if full is None:
+                full = self.allgather_columns([build_key] + list(build_group_keys))
             build_key, build_group_keys = full[0], full[1:]
         pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
                                                     build_group_keys, aggs)
@@ -471,6 +474,53 @@ class DistributedExecutor:
         if dense is not None:
             return dense
         return self._final(pk, pa_, aggs)
+
+    def _allgather_beside_phase_a(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs):
+        """The dimension all-gather overlapped with phase A of the fused operator: one small
+        all_gather of every shard's [rows, key min / max, group key min / max] gives the full build
+        side's ranges, the padded column all-gathers are issued asynchronously, phase A is launched
+        from the ranges (qeh_join_filter_aggregate_prelaunch) while they run, and only then does the
+        queue wait for them.  None when the shape does not allow it (the caller all-gathers first)."""
+        cols = [build_key] + list(build_group_keys)
+        if (self.world == 1 or self.device != "cuda" or len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
+                or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32) or any(c.c.validity for c in cols)):
+            return None
+        n = len(build_key)
+        ts = [self._to_tensors(c)[0] for c in cols]
+        big, small = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+        if n:
+            kk, gg = torch.aminmax(ts[0]), torch.aminmax(ts[1].to(torch.int64))
+            st = torch.stack([torch.tensor(n, dtype=torch.int64, device=ts[0].device), kk.min, kk.max, gg.min, gg.max])
+        else:
+            st = torch.tensor([0, big, small, big, small], dtype=torch.int64, device=self.device)
+        self._sync()
+        M = _allgather_meta_t(st, self.world, self.group)
+        rows = [int(x) for x in M[:, 0]]
+        total, mx = sum(rows), max(rows)
+        if total == 0:
+            return None
+        live = M[M[:, 0] > 0]
+        krange = [int(live[:, 1].min()), int(live[:, 2].max()), total]
+        grange = [int(live[:, 3].min()), int(live[:, 4].max()), total]
+        bufs, works = [], []
+        for t in ts:
+            if n < mx:
+                pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
+                pad[:n] = t
+                t = pad
+            buf = torch.empty(self.world * mx, dtype=t.dtype, device=t.device)
+            works.append(dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group, async_op=True))
+            bufs.append(buf)
+        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, krange, grange)
+        for w in works:
+            w.wait()
+        out = []
+        for c, buf in zip(cols, bufs):
+            if any(r != mx for r in rows):
+                buf = torch.cat([buf[q * mx:q * mx + rows[q]] for q in range(self.world)])
+            out.append(self._from_tensors(c.dtype, buf, None))
+        self._sync_torch()
+        return out
 
     DENSE_MAX_KEYS = 1 << 20
 

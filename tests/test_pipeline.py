@@ -283,3 +283,38 @@ def test_metric_full_size_properties(ctx):
     gk2, ga2, _ = ctx.join_filter_aggregate([x, k, v], 1, PRED, dk, [dg], AGGS)
     order1, order2 = np.argsort(keys), np.argsort(gk2[0].to_numpy()[0])
     assert np.array_equal(counts[order1], ga2[1].to_numpy()[0][order2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hint", ["exact", "wrong_key_range", "wrong_group_range", "other_probe"])
+def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
+    """qeh_join_filter_aggregate_prelaunch (phase A launched from caller-given build ranges while
+    the build shards are in flight): the next fused call adopts it only when its probe columns and
+    the build columns' actual [min, max, count] match; otherwise it is discarded and the call
+    runs its own phase A.  The result equals the oracle's either way."""
+    n_fact, n_dim = 4_000_000, 4_000_000
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 1024)
+    probe = [ctx.upload(x), ctx.upload(k), ctx.upload(v)]
+    bkey, bg = ctx.upload(dk), ctx.upload(dg)
+    kr = [int(dk.min()), int(dk.max()), n_dim]
+    gr = [int(dg.min()), int(dg.max()), n_dim]
+    pre_probe = probe
+    if hint == "wrong_key_range":
+        kr = [kr[0], kr[1] + 70_000, n_dim]
+    elif hint == "wrong_group_range":
+        gr = [gr[0], gr[1] - 1, n_dim]
+    elif hint == "other_probe":
+        pre_probe = [ctx.upload(x), ctx.upload(k), ctx.upload(v)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        ctx.join_filter_aggregate_prelaunch(pre_probe, 1, PRED, AGGS, kr, gr)
+        gk, ga, g = ctx.join_filter_aggregate(probe, 1, PRED, bkey, [bg], AGGS)
+        launches = ctx.kernel_time("slice_partition")[1]
+    finally:
+        ctx.timing(False)
+    assert launches == (1 if hint == "exact" else 2)
+    wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(dk),
+                                          [ob.HostCol(dg)], AGGS)
+    assert g == wg
+    assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
