@@ -650,7 +650,8 @@ __device__ __forceinline__ void slice_states_init(uint64_t *lst, int64_t stride,
 // G groups stay in LDS.  IDENT = true (group-range slices): items are group ids within the slice's
 // range of 2^kGidSliceBits groups, whose states live in LDS while the workgroup drains that slice
 // and are merged into the global states when it moves on.
-template <int NACOL, bool IDENT = false>
+// PF: the next 512 items of a region are loaded while this chunk is looked up and aggregated.
+template <int NACOL, bool IDENT = false, bool PF = false>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
                                                              AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
     constexpr int VC = NACOL > 0 ? 1 : 0;
@@ -712,16 +713,25 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             const uint32_t n_r = rg.count[reg];
             const uint16_t *kp = rg.key + reg * rg.cap;
             const int64_t *vp = VC ? rg.val + reg * rg.cap : nullptr;
-            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
-                uint32_t e[8];
-                int64_t v[8];
+            uint32_t en[8];
+            int64_t vn[8];
+            auto ld = [&](uint32_t i0) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const uint32_t i = i0 + j * 64 + lane;
                     const uint32_t ii = i < n_r ? i : 0u;
-                    e[j] = __builtin_nontemporal_load(kp + ii);
-                    v[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
+                    en[j] = __builtin_nontemporal_load(kp + ii);
+                    vn[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
                 }
+            };
+            if (PF && n_r) ld(0);
+            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
+                uint32_t e[8];
+                int64_t v[8];
+                if (!PF) ld(i0);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e[j] = en[j], v[j] = vn[j];
+                if (PF && i0 + 64 * 8 < n_r) ld(i0 + 64 * 8);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     e[j] = (i0 + j * 64 + lane < n_r) ? (IDENT ? e[j] + 1u : (uint32_t)tslice[e[j]]) : 0u;
@@ -1739,16 +1749,30 @@ static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, c
     return QEH_OK;
 }
 
+static bool slice_probe_prefetch() {
+    static const int v = [] {
+        const char *e = std::getenv("QEH_SLICE_B_PREFETCH");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v != 0;
+}
+
 static void launch_slice_probe(qeh_ctx *ctx, const SliceRegions &rg, int nreg, const HashTable &t, const FastIn &in,
                                const AggSpecs &specs, int64_t G, uint64_t *states, int nacol) {
     KernelTimer ktb(ctx, "slice_probe");
     const int gridB = ctx->props.multiProcessorCount;
-    if (nacol == 0)
-        hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, in, specs, G,
-                           states);
-    else
-        hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, in, specs, G,
-                           states);
+    const bool pf = slice_probe_prefetch();
+#define QEH_SB(NAV, PFV)                                                                                           \
+    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, \
+                       in, specs, G, states)
+    if (nacol == 0) {
+        if (pf) QEH_SB(0, true);
+        else QEH_SB(0, false);
+    } else {
+        if (pf) QEH_SB(1, true);
+        else QEH_SB(1, false);
+    }
+#undef QEH_SB
 }
 
 // LDS-slice partitioned probe (k_slice_partition + k_slice_probe) for unique
@@ -1847,12 +1871,18 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         const int gridB = ctx->props.multiProcessorCount;
         int splits = 0;
         if (const char *e = std::getenv("QEH_SLICE_SPLITS")) splits = std::atoi(e);
-        if (nacol == 0)
-            hipLaunchKernelGGL((k_slice_probe<0>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, t, in,
-                               specs, G, states);
-        else
-            hipLaunchKernelGGL((k_slice_probe<1>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, t, in,
-                               specs, G, states);
+        const bool pf = slice_probe_prefetch();
+#define QEH_SB(NAV, PFV)                                                                                              \
+    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, \
+                       t, in, specs, G, states)
+        if (nacol == 0) {
+            if (pf) QEH_SB(0, true);
+            else QEH_SB(0, false);
+        } else {
+            if (pf) QEH_SB(1, true);
+            else QEH_SB(1, false);
+        }
+#undef QEH_SB
     }
     if (tail_ev) {  // the tail beside phase B: the states are complete once it is done too
         (void)hipStreamWaitEvent(ctx->stream, tail_ev, 0);
