@@ -690,10 +690,12 @@ struct WmRankLds {
     uint32_t wsum[16];
 };
 
-// Returns the tile's count of digit threadIdx.x.
-template <int NJ>
+// Returns the tile's count of digit threadIdx.x.  DB >= 0: the digit width as a compile-time
+// constant (the ballot loop unrolls); DB < 0: `dbits` at run time.
+template <int NJ, int DB = -1>
 __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], const bool (&live)[NJ], int dbits,
                                                    uint32_t (&slot)[NJ], WmRankLds &R) {
+    if constexpr (DB >= 0) dbits = DB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *wz = (uint32_t *)R.wc[wave];
     for (int i = lane; i < kWmDig / 2; i += 64) wz[i] = 0u;
@@ -703,7 +705,8 @@ __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], cons
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         uint64_t m = __ballot(live[j]);
-        for (int b = 0; b < dbits; ++b) {
+#pragma unroll
+        for (int b = 0; b < (DB >= 0 ? DB : dbits); ++b) {
             const bool bit = (d[j] >> b) & 1u;
             const uint64_t bb = __ballot(bit);
             m &= bit ? bb : ~bb;
@@ -741,7 +744,7 @@ __host__ __device__ __forceinline__ int wm_digit_bits(int64_t ndig) {
 }
 
 // pass 1: stable 2^dbits-way partition of (order key, low key bits) by the high key digit
-template <int KES, int OES>
+template <int KES, int OES, int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
                                                         const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
                                                         uint16_t *__restrict__ o_kl) {
@@ -781,7 +784,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
             ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
-        const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             if (!live[j]) continue;
@@ -803,6 +806,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
 }
 
 // pass 2: inside each bucket, stable partition by the low digit; group starts -> pstart
+template <int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
                                                         uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart) {
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
                 keys[j] = kx[j];
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
-            const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+            const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 if (!live[j]) continue;
@@ -1027,6 +1031,7 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm2_sort(WmShape sh, WmFunc f,
 
 // inverse of pass 2: replay each bucket's tiles, gather the results run by run (group order ->
 // pass-1 order)
+template <int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                        const uint64_t *__restrict__ pstart, const uint16_t *__restrict__ i_kl,
                                                        const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1) {
@@ -1063,7 +1068,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
                 d[j] = lx[j];
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
-            const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+            const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
@@ -1086,7 +1091,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
 
 // inverse of pass 1: replay each workgroup's tiles, gather the results run by run and write them in
 // input order as Int64
-template <int KES>
+template <int KES, int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, const uint64_t *__restrict__ base,
                                                        const uint16_t *__restrict__ res1, int64_t *__restrict__ out) {
     __shared__ WmRankLds R;
@@ -1117,7 +1122,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
             d[j] = (uint32_t)(((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) >> sh.lb);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);
-        const uint32_t tcnt = wm_stable_rank<NJ>(d, live, dbits, slot, R);
+        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
             if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
@@ -1162,14 +1167,18 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         KernelTimer kt(ctx, "window_partition");
         hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
         QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
-        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? k_wm2_pass1<4, 4> : k_wm2_pass1<4, 8>) : (oes == 4 ? k_wm2_pass1<8, 4> : k_wm2_pass1<8, 8>),
+        const bool d1 = wm_digit_bits(sh.nb) == 10;
+        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? (d1 ? k_wm2_pass1<4, 4, 10> : k_wm2_pass1<4, 4, -1>)
+                                                : (d1 ? k_wm2_pass1<4, 8, 10> : k_wm2_pass1<4, 8, -1>))
+                                    : (oes == 4 ? (d1 ? k_wm2_pass1<8, 4, 10> : k_wm2_pass1<8, 4, -1>)
+                                                : (d1 ? k_wm2_pass1<8, 8, 10> : k_wm2_pass1<8, 8, -1>)),
                            dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh,
                            base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
         // bucket starts = the scanned bases of workgroup 0 per digit, then n
         QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
-        hipLaunchKernelGGL(k_wm2_pass2, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), key1.as<uint64_t>(),
+        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), key1.as<uint64_t>(),
                            kl1.as<uint16_t>(), key2.as<uint64_t>(), pst.as<uint64_t>());
     }
     QEH_HIP(hipGetLastError());
@@ -1197,9 +1206,11 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out));
     {
         KernelTimer kt(ctx, "window_place");
-        hipLaunchKernelGGL(k_wm2_inv2, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
+        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_inv2<10> : k_wm2_inv2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
                            kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>());
-        hipLaunchKernelGGL(kes == 4 ? k_wm2_inv1<4> : k_wm2_inv1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, base1.as<uint64_t>(),
+        const bool d1i = wm_digit_bits(sh.nb) == 10;
+        hipLaunchKernelGGL(kes == 4 ? (d1i ? k_wm2_inv1<4, 10> : k_wm2_inv1<4, -1>) : (d1i ? k_wm2_inv1<8, 10> : k_wm2_inv1<8, -1>),
+                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, base1.as<uint64_t>(),
                            res1.as<uint16_t>(), (int64_t *)out->values);
     }
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
