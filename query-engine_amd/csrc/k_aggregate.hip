@@ -1779,9 +1779,11 @@ static void launch_slice_probe(qeh_ctx *ctx, const SliceRegions &rg, int nreg, c
 // direct u16 tables past an XCD's L2.  Returns 1 when it ran; 0 when not
 // eligible, or when a region overflowed (probe keys skewed onto few slices),
 // in which case the states are re-initialised for the single pass.
+// ovf_copy != nullptr: the overflow flag is copied there (stream-ordered) and 2 returned instead of
+// reading it here; the caller reads it with its other results and re-runs on overflow.
 static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
                           const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes,
-                          SlicePre *pre) {
+                          SlicePre *pre, uint32_t *ovf_copy = nullptr) {
     if (std::getenv("QEH_NO_SLICES")) return 0;
     FastIn in;
     int nterms, nacol;
@@ -1890,6 +1892,10 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     }
     if (hipGetLastError() != hipSuccess) return 0;
     if (!tail_done) launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+    if (ovf_copy) {
+        if (hipMemcpyAsync(ovf_copy, rg.overflow, 4, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) return -1;
+        return 2;
+    }
     uint32_t of = 0;
     if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
     if (of) {
@@ -2164,28 +2170,36 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
     if (std::getenv("QEH_NO_SHARDS")) specs.shards = 1;
     QEH_TRY(states.alloc(ctx, (size_t)specs.shards * specs.n_slots * Gs * 8));
-    QEH_TRY(errw.alloc(ctx, 8));
-    QEH_HIP(hipMemsetAsync(errw.p, 0, 8, ctx->stream));
+    // status words, read back in one go: [0] kernel error bits, [1] slice-region overflow, [2..3] groups
+    QEH_TRY(errw.alloc(ctx, 16));
+    QEH_HIP(hipMemsetAsync(errw.p, 0, 16, ctx->stream));
+    bool ovf_pending = false;
     hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock), 0,
                        ctx->stream, states.as<uint64_t>(), Gs, specs);
     const size_t lds_bytes = (size_t)specs.n_slots * Gs * 8;
     const bool lds = lds_bytes <= kLdsStateBudget;
+    // fused join-aggregate when the LDS-slice pipeline does not run (or overflowed)
+    auto join_fallback = [&](int grid, int per_cu) {
+        if (!lds && try_gid_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>()) == 1) {
+        } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
+                                          lds_bytes, per_cu)))
+            launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
+                                     states.as<uint64_t>(), errw.as<uint32_t>());
+    };
+    int per_cu = lds ? (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds_bytes, 1))) : 8;
+    per_cu = std::min(per_cu, 8);
+    const int grid = grid_for(ctx, n, kAggTile, per_cu);
     if (n > 0 && G > 0) {
-        // LDS partials: ~3-6 workgroups per CU; fewer per CU when the state is large
-        int per_cu = lds ? (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds_bytes, 1))) : 8;
-        per_cu = std::min(per_cu, 8);
-        int grid = grid_for(ctx, n, kAggTile, per_cu);
+        // LDS partials: ~3-6 workgroups per CU; fewer per CU when the state is large (per_cu above)
         KernelTimer kt(ctx, kname);
         if (gm == GM_ZERO) launch_agg_rows<GM_ZERO>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
         else if (gm == GM_JOIN) {
-            if (lds && try_slice_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
-                                      lds_bytes, pre) == 1) {
-            } else if (!lds && try_gid_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(),
-                                              errw.as<uint32_t>()) == 1) {
-            } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
-                                              lds_bytes, per_cu)))
-                launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,
-                                         states.as<uint64_t>(), errw.as<uint32_t>());
+            const int sj = lds ? try_slice_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
+                                                lds_bytes, pre, errw.as<uint32_t>() + 1)
+                               : 0;
+            if (sj < 0) return fail(QEH_E_HIP, "slice join: overflow flag copy failed");
+            ovf_pending = sj == 2;
+            if (sj == 0) join_fallback(grid, per_cu);
         }
         else if (gm == GM_LDSHASH && lds_group_fast(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(),
                                                       errw.as<uint32_t>())) {
@@ -2207,34 +2221,52 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         else launch_agg_rows<GM_GROUP>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
     }
     QEH_HIP(hipGetLastError());
-    if (specs.shards > 1)
-        hipLaunchKernelGGL(k_states_reduce, dim3(grid_for(ctx, specs.n_slots * Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
-                           states.as<uint64_t>(), Gs, specs);
+    auto reduce_shards = [&]() {
+        if (specs.shards > 1)
+            hipLaunchKernelGGL(k_states_reduce, dim3(grid_for(ctx, specs.n_slots * Gs, kBlock, 8)), dim3(kBlock), 0,
+                               ctx->stream, states.as<uint64_t>(), Gs, specs);
+    };
+    reduce_shards();
     if (gm == GM_LDSHASH) {  // table overflow: the caller regrows and reruns
         uint32_t of = 0;
         QEH_TRY(read_small(ctx, &of, src.gt.overflow, 4));
         if (of) return kRetryBigger;
     }
 
-    // compact non-empty groups
+    // compact non-empty groups; the group count lands in the status words
     DevBuf flags, pos;
     uint64_t out_n = (uint64_t)G;
     const uint64_t *posp = nullptr;
     if (drop_empty && G > 0) {
         QEH_TRY(flags.alloc(ctx, Gs * 4));
         QEH_TRY(pos.alloc(ctx, Gs * 8));
+        posp = pos.as<uint64_t>();
+    }
+    auto compact = [&]() -> int {
+        if (!posp) return QEH_OK;
         hipLaunchKernelGGL(k_group_nonempty, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
                            states.as<uint64_t>(), Gs, flags.as<uint32_t>());
-        QEH_TRY(exclusive_scan_u32(ctx, flags.as<uint32_t>(), pos.as<uint64_t>(), G, &out_n));
-        posp = pos.as<uint64_t>();
-    } else {
-        uint32_t e = 0;
-        QEH_TRY(read_small(ctx, &e, errw.p, 4));
-        QEH_TRY(kernel_error_status(e, "aggregate"));
+        return exclusive_scan_u32_dev(ctx, flags.as<uint32_t>(), pos.as<uint64_t>(), G, (uint64_t *)(errw.as<uint32_t>() + 2));
+    };
+    QEH_TRY(compact());
+    uint32_t stw[4];
+    QEH_TRY(read_small(ctx, stw, errw.p, 16));  // one host round trip: error bits, overflow, group count
+    if (ovf_pending && stw[1]) {
+        // a slice region overflowed (probe keys skewed onto few slices): the single fused pass instead
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock),
+                           0, ctx->stream, states.as<uint64_t>(), Gs, specs);
+        QEH_HIP(hipMemsetAsync(errw.p, 0, 16, ctx->stream));
+        {
+            KernelTimer kt(ctx, kname);
+            join_fallback(grid, per_cu);
+        }
+        QEH_HIP(hipGetLastError());
+        reduce_shards();
+        QEH_TRY(compact());
+        QEH_TRY(read_small(ctx, stw, errw.p, 16));
     }
-    uint32_t e = 0;
-    QEH_TRY(read_small(ctx, &e, errw.p, 4));
-    QEH_TRY(kernel_error_status(e, "aggregate"));
+    QEH_TRY(kernel_error_status(stw[0], "aggregate"));
+    if (posp) out_n = (uint64_t)stw[2] | ((uint64_t)stw[3] << 32);
 
     OutCols oc{};
     const int nk = out_keys_src.n;

@@ -24,7 +24,21 @@ struct MinMax {
     uint32_t bad;  // unsupported key type seen
 };
 
-__global__ __launch_bounds__(kBlock) void k_key_minmax(ColRef key, int64_t n, MinMax *out) {
+__device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, MinMax *out);
+
+__global__ __launch_bounds__(kBlock) void k_key_minmax(ColRef key, int64_t n, MinMax *out) { key_minmax_body(key, n, out); }
+
+// Several columns in one launch (blockIdx.y = column); k_minmax_init_n initialises their slots.
+constexpr int kMinMaxCols = 4;
+struct MinMaxJob {
+    ColRef c[kMinMaxCols];
+    int64_t n[kMinMaxCols];
+};
+__global__ __launch_bounds__(kBlock) void k_key_minmax_n(MinMaxJob j, MinMax *out) {
+    key_minmax_body(j.c[blockIdx.y], j.n[blockIdx.y], out + blockIdx.y);
+}
+
+__device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, MinMax *out) {
     __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
     __shared__ uint64_t scnt[kBlock / 64];
     int64_t mn = INT64_MAX, mx = INT64_MIN;
@@ -90,6 +104,16 @@ __global__ void k_minmax_init(MinMax *m) {
     m->mx = INT64_MIN;
     m->cnt = 0;
     m->bad = 0;
+}
+
+__global__ void k_minmax_init_n(MinMax *m, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        m[i].mn = INT64_MAX;
+        m[i].mx = INT64_MIN;
+        m[i].cnt = 0;
+        m[i].bad = 0;
+    }
 }
 
 // ---- inserts -------------------------------------------------------------------------
@@ -244,12 +268,20 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
     if (all) return QEH_OK;
     DevBuf mm;
     QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
-    for (int i = 0; i < n; ++i) {
-        const ColRef c = make_colref(cols[i]);
-        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, ctx->stream, mm.as<MinMax>() + i);
-        if (cols[i].length > 0)
-            hipLaunchKernelGGL(k_key_minmax, dim3(grid_for(ctx, cols[i].length, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream,
-                               c, cols[i].length, mm.as<MinMax>() + i);
+    // one init and one reduction launch per group of up to four columns (blockIdx.y = column)
+    hipLaunchKernelGGL(k_minmax_init_n, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, mm.as<MinMax>(), n);
+    for (int i0 = 0; i0 < n; i0 += kMinMaxCols) {
+        MinMaxJob j{};
+        int64_t longest = 0;
+        const int nc = std::min(kMinMaxCols, n - i0);
+        for (int q = 0; q < nc; ++q) {
+            j.c[q] = make_colref(cols[i0 + q]);
+            j.n[q] = cols[i0 + q].length;
+            longest = std::max<int64_t>(longest, cols[i0 + q].length);
+        }
+        if (longest > 0)
+            hipLaunchKernelGGL(k_key_minmax_n, dim3(grid_for(ctx, longest, kBlock * 8, 1), nc), dim3(kBlock), 0, ctx->stream, j,
+                               mm.as<MinMax>() + i0);
     }
     QEH_HIP(hipGetLastError());
     std::vector<MinMax> hm((size_t)n);

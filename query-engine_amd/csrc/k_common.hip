@@ -140,6 +140,21 @@ __global__ void k_scan_apply(const uint32_t *__restrict__ in, int64_t n, const u
     }
 }
 
+// As exclusive_scan_u32, the total written to device memory (no host read); n > 0.
+int exclusive_scan_u32_dev(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total_dev) {
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    DevBuf part;
+    QEH_TRY(part.alloc(ctx, (size_t)nb * 8));
+    {
+        KernelTimer kt(ctx, "scan");
+        hipLaunchKernelGGL(k_scan_partials, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, in, n, part.as<uint64_t>());
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, ctx->stream, part.as<uint64_t>(), nb, total_dev);
+        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, in, n, part.as<uint64_t>(), out);
+    }
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
 int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total) {
     if (n <= 0) {
         if (total) *total = 0;

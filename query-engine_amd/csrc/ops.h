@@ -18,6 +18,7 @@ int make_colset(const qeh_column *cols, int n, ColSet *out);
 
 // Device-wide exclusive scan of uint32 counts into uint64 offsets; returns
 // the total through *total (synchronous read).  `out` may alias nothing.
+int exclusive_scan_u32_dev(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total_dev);
 int exclusive_scan_u32(qeh_ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, uint64_t *total);
 
 // Join hash table built over `key` with payload either row ids
