@@ -1251,6 +1251,10 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     sh.n = n;
     sh.kmin = kmin;
     sh.lb = bits > 10 ? bits - 10 : 0;
+    if (const char *e = std::getenv("QEH_WM_LB")) {  // experiments: digit split between the passes
+        const int lb = std::atoi(e);
+        if (lb >= sh.lb && lb <= 10 && lb <= bits) sh.lb = lb;
+    }
     sh.nb = (int32_t)(((range - 1) >> sh.lb) + 1);
     sh.nparts = (int64_t)range;
     const int cus = ctx->props.multiProcessorCount;
