@@ -283,6 +283,7 @@ struct WmFunc {
     int64_t param;     // NTILE buckets / LAG, LEAD offset
     int32_t win_shift; // pass-5a digit = row id >> win_shift
     int32_t skip_sort; // QEH_WM_SKIP_SORT (experiments: load/emit cost without the network)
+    int32_t no_count;  // QEH_WM_NO_COUNT (experiments: the bitonic network for every group)
     // value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column itself): the
     // value is decoded from the group's order keys
     int32_t odt;       // order key dtype
@@ -875,12 +876,112 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     }
 }
 
+template <int R, int P, bool CSX = false>
+__device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
+                                               WmWaveLds<P> &L, int lane);
+
+constexpr int kWmCsCap = 16;  // counting sort: most rows one bucket may hold
+
+// Counting sort of one group (m <= P = 1024 rows, order keys register-major in pre): 2048 buckets
+// of the top 11 bits of (key - mn), packed 16-bit counters in L.id (free until the tail writes
+// results); rows are placed by bucket start + arrival, with their keys in L.ov at that slot, then
+// each row ranks itself exactly among its bucket's rows by (order key, position) -- the bucket
+// reads of all the lane's rows are interleaved, so a wave waits for LDS about as many times as its
+// fullest bucket holds rows.  L.k[wm_pad(i)] = position | slot << 11 of the i-th row in order
+// (the CSX tail's layout).  Returns false, with only L.id written, when a bucket holds more than
+// kWmCsCap rows.
+template <int R, int P, int RP>
+__device__ __forceinline__ bool wm2_count_sort(const uint64_t (&pre)[RP], int m, uint64_t mn, int sb, WmWaveLds<P> &L,
+                                               int lane) {
+    static_assert(P == 1024, "counting sort: groups of <= 1024 rows");
+    constexpr int NB = 11, C = (1 << NB) / 64;  // buckets; 16-bit counters per lane in the scan
+    const int shift = sb > NB ? sb - NB : 0;
+    uint32_t *cnt = L.id;  // 2048 u16 counters packed in P u32 words
+#pragma unroll
+    for (int q = 0; q < C / 2; ++q) cnt[q * 64 + lane] = 0u;
+    wm_wave_sync();
+    uint32_t ba[R];  // bucket | arrival << 16, then start | end << 16, then the row's sorted index
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        ba[r] = 0u;
+        if (e < m) {
+            const uint32_t bk = (uint32_t)((pre[r] - mn) >> shift), sh16 = (bk & 1u) * 16u;
+            const uint32_t old = atomicAdd(&cnt[bk >> 1], 1u << sh16);
+            ba[r] = bk | (((old >> sh16) & 0xFFFFu) << 16);
+        }
+    }
+    wm_wave_sync();
+    {
+        uint32_t w[C / 2], tot = 0, big = 0;
+#pragma unroll
+        for (int q = 0; q < C / 2; ++q) {
+            w[q] = cnt[lane * (C / 2) + q];
+            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+            tot += lo + hi;
+            big |= (lo > (uint32_t)kWmCsCap || hi > (uint32_t)kWmCsCap) ? 1u : 0u;
+        }
+        if (__ballot(big)) return false;
+        uint32_t run = wave_incl_scan(tot) - tot;
+#pragma unroll
+        for (int q = 0; q < C / 2; ++q) {  // this lane's own counters: no other lane reads them yet
+            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+            cnt[lane * (C / 2) + q] = run | ((run + lo) << 16);
+            run += lo + hi;
+        }
+    }
+    wm_wave_sync();
+    uint32_t maxc = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < m) {
+            const uint32_t bk = ba[r] & 0xFFFFu;
+            const uint32_t st = (cnt[bk >> 1] >> ((bk & 1u) * 16u)) & 0xFFFFu;
+            const uint32_t b1 = bk + 1;
+            const uint32_t en = b1 < (1u << NB) ? (cnt[b1 >> 1] >> ((b1 & 1u) * 16u)) & 0xFFFFu : (uint32_t)m;
+            const uint32_t slot = st + (ba[r] >> 16);
+            L.k[wm_pad(slot)] = (uint32_t)e;
+            L.ov[slot] = pre[r];
+            ba[r] = st | (en << 11) | (slot << 22);
+            maxc = max(maxc, en - st);
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) maxc = max(maxc, (uint32_t)__shfl_xor((int)maxc, d, 64));
+    wm_wave_sync();
+    uint32_t rank[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rank[r] = 0u;
+    if (maxc > 1) {
+        for (uint32_t j = 0; j < maxc; ++j) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t st = ba[r] & 0x7FFu, en = (ba[r] >> 11) & 0x7FFu;
+                if (st + j < en) {
+                    const uint32_t q = L.k[wm_pad(st + j)];
+                    rank[r] += wm_less(L.ov[st + j], q, pre[r], (uint32_t)(r * 64 + lane)) ? 1u : 0u;
+                }
+            }
+        }
+    }
+    wm_wave_sync();  // every bucket read is done: L.k takes the sorted order
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < m) L.k[wm_pad((ba[r] & 0x7FFu) + rank[r])] = (uint32_t)e | ((ba[r] >> 22) << 11);
+    }
+    return true;
+}
+
 // group sort without row ids: ties by position in the group (= input order, the passes being
 // stable); each row's result is written at its own position in the group
 // `pre` holds the group's order keys register-major (element r * 64 + lane in pre[r]), loaded by
 // the caller ahead of time.
-template <int R, int P, int RP>
-__device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
+// CS: the counting sort only -- returns false (no result written) when a bucket overflows, and
+// the caller queues the group for the network kernel; else the bitonic network (always true).
+template <int R, int P, int RP, bool CS>
+__device__ bool wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                           WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
     static_assert(R <= RP, "prefetch too short");
     wm_wave_sync();  // the previous group's LDS reads are done
@@ -890,7 +991,7 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
         const int e = r * 64 + lane;
         if (e < m) {
             const uint64_t o = pre[r];
-            L.ov[e] = o;
+            if (!CS) L.ov[e] = o;  // (the counting sort stores keys by bucket slot)
             mn = o < mn ? o : mn;
             mx = o > mx ? o : mx;
         }
@@ -903,8 +1004,18 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
     }
     const uint64_t span = mx - mn;
     const int sb = span ? 64 - __clzll((long long)span) : 0;
-    const int shift = sb > 21 ? sb - 21 : 0;
     wm_wave_sync();  // every lane's order keys are in LDS
+    // Counting sort first: bucket = the top log2(P) bits of (key - min), exact rank inside the
+    // bucket by (order key, position) -- a few LDS operations per row instead of the bitonic
+    // network's log2(64R)(log2(64R)+1)/2 compare-exchange stages.  Buckets hold under one row on
+    // average for spread keys; when one holds more than kWmCsCap rows (clustered keys, many
+    // ties) the group takes the network below.
+    if constexpr (CS) {
+        if (!wm2_count_sort<R, P, RP>(pre, m, mn, sb, L, lane)) return false;
+        wm2_group_tail<R, P, true>(s, m, f, res_out, L, lane);
+        return true;
+    }
+    const int shift = sb > 21 ? sb - 21 : 0;
     uint32_t k[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -942,6 +1053,16 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
             L.k[wm_pad(e + b + 1)] = x;
         }
     }
+    wm2_group_tail<R, P>(s, m, f, res_out, L, lane);
+    return true;
+}
+
+// With the group's order (position in the low 11 bits of L.k[wm_pad(i)], i = sorted index): the
+// function's value per row, written at the row's own position in the group.
+// CSX: the counting sort's layout, the key of the i-th row in order at L.ov[L.k[wm_pad(i)] >> 11].
+template <int R, int P, bool CSX>
+__device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
+                                               WmWaveLds<P> &L, int lane) {
     wm_wave_sync();
     uint32_t carry_rank = 0, carry_dense = 0;
     uint64_t prev_ov = 0;
@@ -951,7 +1072,7 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
         const bool live = e < m;
         const uint32_t x = live ? L.k[wm_pad(e)] : 0u;
         const uint32_t pos = x & 2047;
-        const uint64_t ov = live ? L.ov[pos] : 0ull;
+        const uint64_t ov = live ? L.ov[CSX ? (x >> 11) : pos] : 0ull;
         uint32_t res;
         if (f.func == QEH_WIN_ROW_NUMBER) {
             res = (uint32_t)e + 1u;
@@ -990,16 +1111,29 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
 }
 
 // One wave per group.  BIG: the rare groups of 1025..2048 rows, a kernel of its own (larger LDS
-// area).  (Loading the next group's keys while sorting this one needed 256 VGPRs and ran slower.)
-template <bool BIG>
-__global__ __launch_bounds__(kWmSortBlock) void k_wm2_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
+// area).  CS: groups of <= 1024 rows by counting sort; a group whose keys cluster (a bucket above
+// kWmCsCap rows) is appended to fb (fb[0] = count, fb[1..] = group numbers) and the network kernel
+// (CS = false, LIST = true) sorts the queued groups -- two kernels, so neither carries the other's
+// registers.  (Loading the next group's keys while sorting this one needed 256 VGPRs and ran slower.)
+template <bool BIG, bool CS, bool LIST>
+__global__ __launch_bounds__(kWmSortBlock, 2) void k_wm2_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                            const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
-                                                           uint32_t *__restrict__ too_big) {
+                                                           uint32_t *__restrict__ too_big, uint32_t *__restrict__ fb) {
+    static_assert(!(CS && (BIG || LIST)), "counting sort: groups of <= 1024 rows, range mode");
     constexpr int P = BIG ? 2048 : 1024;
-    __shared__ WmWaveLds<P> wl[kWmSortBlock / 64];
+    constexpr int W = kWmSortBlock / 64;
+    __shared__ WmWaveLds<P> wl[W];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t g0 = (int64_t)blockIdx.x * sh.nparts / gridDim.x, g1 = (int64_t)(blockIdx.x + 1) * sh.nparts / gridDim.x;
-    for (int64_t g = g0 + wave; g < g1; g += kWmSortBlock / 64) {
+    int64_t i0, i1, di;
+    if (LIST) {
+        i0 = (int64_t)blockIdx.x * W + wave, i1 = (int64_t)fb[0], di = (int64_t)gridDim.x * W;
+    } else {
+        i0 = (int64_t)blockIdx.x * sh.nparts / gridDim.x + wave;
+        i1 = (int64_t)(blockIdx.x + 1) * sh.nparts / gridDim.x;
+        di = W;
+    }
+    for (int64_t i = i0; i < i1; i += di) {
+        const int64_t g = LIST ? (int64_t)fb[1 + i] : i;
         const int64_t s = (int64_t)pstart[g];
         const int64_t m = (int64_t)pstart[g + 1] - s;
         if (m <= 0) continue;
@@ -1020,12 +1154,14 @@ __global__ __launch_bounds__(kWmSortBlock) void k_wm2_sort(WmShape sh, WmFunc f,
             pre[r] = e < m ? gkey[s + e] : 0ull;
         }
         const int mi = (int)m;
-        if (BIG) wm2_group<RP, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 64) wm2_group<1, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 128) wm2_group<2, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 256) wm2_group<4, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 512) wm2_group<8, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else wm2_group<RP, P>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        bool done;
+        if (BIG) done = wm2_group<RP, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 64) done = wm2_group<1, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 128) done = wm2_group<2, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 256) done = wm2_group<4, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 512) done = wm2_group<8, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else done = wm2_group<RP, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        if (CS && !done && lane == 0) fb[1 + atomicAdd(&fb[0], 1u)] = (uint32_t)g;
     }
 }
 
@@ -1178,24 +1314,37 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
-        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), key1.as<uint64_t>(),
-                           kl1.as<uint16_t>(), key2.as<uint64_t>(), pst.as<uint64_t>());
+        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+                           bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
+                           pst.as<uint64_t>());
     }
     QEH_HIP(hipGetLastError());
     key1.reset();
-    if (res2.alloc(ctx, n * 2)) return fail(QEH_E_OOM, "window: out of device memory");
+    DevBuf fbl;  // groups the counting sort queues for the network: count, then group numbers
+    if (res2.alloc(ctx, n * 2) || fbl.alloc(ctx, (sh.nparts + 1) * 4)) return fail(QEH_E_OOM, "window: out of device memory");
     QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
+    QEH_HIP(hipMemsetAsync(fbl.p, 0, 4, ctx->stream));
     WmFunc wf{};
     wf.func = func;
     wf.param = param;
     wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
+    wf.no_count = std::getenv("QEH_WM_NO_COUNT") ? 1 : 0;
     const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
     {
         KernelTimer kt(ctx, "window_sort");
-        hipLaunchKernelGGL((k_wm2_sort<false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
-                           key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>());
-        hipLaunchKernelGGL((k_wm2_sort<true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(),
-                           key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>());
+        if (wf.no_count || wf.skip_sort) {
+            hipLaunchKernelGGL((k_wm2_sort<false, false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
+        } else {
+            hipLaunchKernelGGL((k_wm2_sort<false, true, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
+                               fbl.as<uint32_t>());
+            hipLaunchKernelGGL((k_wm2_sort<false, false, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
+                               fbl.as<uint32_t>());
+        }
+        hipLaunchKernelGGL((k_wm2_sort<true, false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                           pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
     }
     QEH_HIP(hipGetLastError());
     uint32_t too_big = 0;
@@ -1206,8 +1355,9 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out));
     {
         KernelTimer kt(ctx, "window_place");
-        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_inv2<10> : k_wm2_inv2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
-                           kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>());
+        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_inv2<10> : k_wm2_inv2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+                           bst.as<uint64_t>(), pst.as<uint64_t>(), kl1.as<uint16_t>(), res2.as<uint16_t>(),
+                           res1.as<uint16_t>());
         const bool d1i = wm_digit_bits(sh.nb) == 10;
         hipLaunchKernelGGL(kes == 4 ? (d1i ? k_wm2_inv1<4, 10> : k_wm2_inv1<4, -1>) : (d1i ? k_wm2_inv1<8, 10> : k_wm2_inv1<8, -1>),
                            dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, base1.as<uint64_t>(),

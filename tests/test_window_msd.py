@@ -127,3 +127,30 @@ def test_msd_value_functions_of_the_order_column(ctx, monkeypatch, func, param, 
     assert ran
     assert np.array_equal(got_m, want_m)
     assert np.array_equal(got_v[want_m].view(np.uint8), want_v[want_m].view(np.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.DenseRank, 0), (W.Ntile, 4)])
+@pytest.mark.parametrize("vdt", [np.int64, np.float64])
+@pytest.mark.parametrize("parts", [300, 700])
+def test_msd_window_counting_sort_groups(ctx, monkeypatch, func, param, vdt, parts):
+    """Spread order keys (the group counting sort's case: buckets of the top key bits, exact rank
+    inside a bucket) with some duplicated values inside groups, so buckets hold equal keys ranked
+    by input position; group sizes up to ~1900 rows take both the 1024- and 2048-row kernels."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(21)
+    n = 400_000
+    k = r.integers(0, parts, n).astype(np.int64)
+    if vdt == np.int64:
+        v = r.integers(-(2 ** 62), 2 ** 62, n, dtype=np.int64)
+    else:
+        v = r.standard_normal(n) * 1e6
+    dup = r.random(n) < 0.1
+    src = r.integers(0, n, n)
+    same = k[src] == k  # copy a value from another row of the same group where one was drawn
+    v[dup & same] = v[src[dup & same]]
+    # a few near-equal keys in one bucket
+    v[:64] = v[0] + np.arange(64, dtype=v.dtype) * (1 if vdt == np.int64 else 1e-9)
+    k[:64] = k[0]
+    got, want, ran = _run(ctx, func, k, v.astype(vdt), True, param)
+    assert ran and np.array_equal(got, want)
