@@ -876,112 +876,18 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     }
 }
 
-template <int R, int P, bool CSX = false>
+template <int R, int P>
 __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                                                WmWaveLds<P> &L, int lane);
 
-constexpr int kWmCsCap = 16;  // counting sort: most rows one bucket may hold
-
-// Counting sort of one group (m <= P = 1024 rows, order keys register-major in pre): 2048 buckets
-// of the top 11 bits of (key - mn), packed 16-bit counters in L.id (free until the tail writes
-// results); rows are placed by bucket start + arrival, with their keys in L.ov at that slot, then
-// each row ranks itself exactly among its bucket's rows by (order key, position) -- the bucket
-// reads of all the lane's rows are interleaved, so a wave waits for LDS about as many times as its
-// fullest bucket holds rows.  L.k[wm_pad(i)] = position | slot << 11 of the i-th row in order
-// (the CSX tail's layout).  Returns false, with only L.id written, when a bucket holds more than
-// kWmCsCap rows.
-template <int R, int P, int RP>
-__device__ __forceinline__ bool wm2_count_sort(const uint64_t (&pre)[RP], int m, uint64_t mn, int sb, WmWaveLds<P> &L,
-                                               int lane) {
-    static_assert(P == 1024, "counting sort: groups of <= 1024 rows");
-    constexpr int NB = 11, C = (1 << NB) / 64;  // buckets; 16-bit counters per lane in the scan
-    const int shift = sb > NB ? sb - NB : 0;
-    uint32_t *cnt = L.id;  // 2048 u16 counters packed in P u32 words
-#pragma unroll
-    for (int q = 0; q < C / 2; ++q) cnt[q * 64 + lane] = 0u;
-    wm_wave_sync();
-    uint32_t ba[R];  // bucket | arrival << 16, then start | end << 16, then the row's sorted index
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        ba[r] = 0u;
-        if (e < m) {
-            const uint32_t bk = (uint32_t)((pre[r] - mn) >> shift), sh16 = (bk & 1u) * 16u;
-            const uint32_t old = atomicAdd(&cnt[bk >> 1], 1u << sh16);
-            ba[r] = bk | (((old >> sh16) & 0xFFFFu) << 16);
-        }
-    }
-    wm_wave_sync();
-    {
-        uint32_t w[C / 2], tot = 0, big = 0;
-#pragma unroll
-        for (int q = 0; q < C / 2; ++q) {
-            w[q] = cnt[lane * (C / 2) + q];
-            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
-            tot += lo + hi;
-            big |= (lo > (uint32_t)kWmCsCap || hi > (uint32_t)kWmCsCap) ? 1u : 0u;
-        }
-        if (__ballot(big)) return false;
-        uint32_t run = wave_incl_scan(tot) - tot;
-#pragma unroll
-        for (int q = 0; q < C / 2; ++q) {  // this lane's own counters: no other lane reads them yet
-            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
-            cnt[lane * (C / 2) + q] = run | ((run + lo) << 16);
-            run += lo + hi;
-        }
-    }
-    wm_wave_sync();
-    uint32_t maxc = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        if (e < m) {
-            const uint32_t bk = ba[r] & 0xFFFFu;
-            const uint32_t st = (cnt[bk >> 1] >> ((bk & 1u) * 16u)) & 0xFFFFu;
-            const uint32_t b1 = bk + 1;
-            const uint32_t en = b1 < (1u << NB) ? (cnt[b1 >> 1] >> ((b1 & 1u) * 16u)) & 0xFFFFu : (uint32_t)m;
-            const uint32_t slot = st + (ba[r] >> 16);
-            L.k[wm_pad(slot)] = (uint32_t)e;
-            L.ov[slot] = pre[r];
-            ba[r] = st | (en << 11) | (slot << 22);
-            maxc = max(maxc, en - st);
-        }
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) maxc = max(maxc, (uint32_t)__shfl_xor((int)maxc, d, 64));
-    wm_wave_sync();
-    uint32_t rank[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) rank[r] = 0u;
-    if (maxc > 1) {
-        for (uint32_t j = 0; j < maxc; ++j) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t st = ba[r] & 0x7FFu, en = (ba[r] >> 11) & 0x7FFu;
-                if (st + j < en) {
-                    const uint32_t q = L.k[wm_pad(st + j)];
-                    rank[r] += wm_less(L.ov[st + j], q, pre[r], (uint32_t)(r * 64 + lane)) ? 1u : 0u;
-                }
-            }
-        }
-    }
-    wm_wave_sync();  // every bucket read is done: L.k takes the sorted order
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        if (e < m) L.k[wm_pad((ba[r] & 0x7FFu) + rank[r])] = (uint32_t)e | ((ba[r] >> 22) << 11);
-    }
-    return true;
-}
+constexpr int kWmCsCap = 16;  // counting sort (k_wm2_csort_wg): most rows one bucket may hold
 
 // group sort without row ids: ties by position in the group (= input order, the passes being
 // stable); each row's result is written at its own position in the group
 // `pre` holds the group's order keys register-major (element r * 64 + lane in pre[r]), loaded by
 // the caller ahead of time.
-// CS: the counting sort only -- returns false (no result written) when a bucket overflows, and
-// the caller queues the group for the network kernel; else the bitonic network (always true).
-template <int R, int P, int RP, bool CS>
-__device__ bool wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
+template <int R, int P, int RP>
+__device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                           WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
     static_assert(R <= RP, "prefetch too short");
     wm_wave_sync();  // the previous group's LDS reads are done
@@ -991,7 +897,7 @@ __device__ bool wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
         const int e = r * 64 + lane;
         if (e < m) {
             const uint64_t o = pre[r];
-            if (!CS) L.ov[e] = o;  // (the counting sort stores keys by bucket slot)
+            L.ov[e] = o;
             mn = o < mn ? o : mn;
             mx = o > mx ? o : mx;
         }
@@ -1005,16 +911,6 @@ __device__ bool wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
     const uint64_t span = mx - mn;
     const int sb = span ? 64 - __clzll((long long)span) : 0;
     wm_wave_sync();  // every lane's order keys are in LDS
-    // Counting sort first: bucket = the top log2(P) bits of (key - min), exact rank inside the
-    // bucket by (order key, position) -- a few LDS operations per row instead of the bitonic
-    // network's log2(64R)(log2(64R)+1)/2 compare-exchange stages.  Buckets hold under one row on
-    // average for spread keys; when one holds more than kWmCsCap rows (clustered keys, many
-    // ties) the group takes the network below.
-    if constexpr (CS) {
-        if (!wm2_count_sort<R, P, RP>(pre, m, mn, sb, L, lane)) return false;
-        wm2_group_tail<R, P, true>(s, m, f, res_out, L, lane);
-        return true;
-    }
     const int shift = sb > 21 ? sb - 21 : 0;
     uint32_t k[R];
 #pragma unroll
@@ -1054,13 +950,11 @@ __device__ bool wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
         }
     }
     wm2_group_tail<R, P>(s, m, f, res_out, L, lane);
-    return true;
 }
 
 // With the group's order (position in the low 11 bits of L.k[wm_pad(i)], i = sorted index): the
 // function's value per row, written at the row's own position in the group.
-// CSX: the counting sort's layout, the key of the i-th row in order at L.ov[L.k[wm_pad(i)] >> 11].
-template <int R, int P, bool CSX>
+template <int R, int P>
 __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                                                WmWaveLds<P> &L, int lane) {
     wm_wave_sync();
@@ -1072,7 +966,7 @@ __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f
         const bool live = e < m;
         const uint32_t x = live ? L.k[wm_pad(e)] : 0u;
         const uint32_t pos = x & 2047;
-        const uint64_t ov = live ? L.ov[CSX ? (x >> 11) : pos] : 0ull;
+        const uint64_t ov = live ? L.ov[pos] : 0ull;
         uint32_t res;
         if (f.func == QEH_WIN_ROW_NUMBER) {
             res = (uint32_t)e + 1u;
@@ -1110,16 +1004,14 @@ __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f
     }
 }
 
-// One wave per group.  BIG: the rare groups of 1025..2048 rows, a kernel of its own (larger LDS
-// area).  CS: groups of <= 1024 rows by counting sort; a group whose keys cluster (a bucket above
-// kWmCsCap rows) is appended to fb (fb[0] = count, fb[1..] = group numbers) and the network kernel
-// (CS = false, LIST = true) sorts the queued groups -- two kernels, so neither carries the other's
-// registers.  (Loading the next group's keys while sorting this one needed 256 VGPRs and ran slower.)
-template <bool BIG, bool CS, bool LIST>
+// One wave per group, bitonic network.  BIG: the groups of 1025..2048 rows, a kernel of its own
+// (larger LDS area).  LIST: the groups the counting sort (k_wm2_csort_wg) queued in fb (fb[0] =
+// count, fb[1..] = group numbers); else every group of the size class.  (Loading the next group's
+// keys while sorting this one needed 256 VGPRs and ran slower.)
+template <bool BIG, bool LIST>
 __global__ __launch_bounds__(kWmSortBlock, 2) void k_wm2_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
-                                                           const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
-                                                           uint32_t *__restrict__ too_big, uint32_t *__restrict__ fb) {
-    static_assert(!(CS && (BIG || LIST)), "counting sort: groups of <= 1024 rows, range mode");
+                                                              const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
+                                                              uint32_t *__restrict__ too_big, const uint32_t *__restrict__ fb) {
     constexpr int P = BIG ? 2048 : 1024;
     constexpr int W = kWmSortBlock / 64;
     __shared__ WmWaveLds<P> wl[W];
@@ -1154,14 +1046,228 @@ __global__ __launch_bounds__(kWmSortBlock, 2) void k_wm2_sort(WmShape sh, WmFunc
             pre[r] = e < m ? gkey[s + e] : 0ull;
         }
         const int mi = (int)m;
-        bool done;
-        if (BIG) done = wm2_group<RP, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 64) done = wm2_group<1, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 128) done = wm2_group<2, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 256) done = wm2_group<4, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 512) done = wm2_group<8, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else done = wm2_group<RP, P, RP, CS>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        if (CS && !done && lane == 0) fb[1 + atomicAdd(&fb[0], 1u)] = (uint32_t)g;
+        if (BIG) wm2_group<RP, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 64) wm2_group<1, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 128) wm2_group<2, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 256) wm2_group<4, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 512) wm2_group<8, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else wm2_group<RP, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+    }
+}
+
+// Counting sort of a group, a whole workgroup per group (E rows per thread: groups of (LO, 256 E]
+// rows): buckets of the top log2(2P) bits of (order key - min), 16-bit counters packed in LDS,
+// rows placed by bucket start + arrival with their keys at that slot, then each row ranks itself
+// exactly among its bucket's rows by (order key, position) -- a few LDS operations per row instead
+// of a bitonic network's log2(P)(log2(P)+1)/2 compare-exchange stages.  Buckets hold under one row
+// on average for spread keys; a group with a bucket above kWmCsCap rows (clustered keys, many
+// ties) is queued in fb for the network kernel.  The workgroup's group bounds sit in LDS and the
+// next group's keys are loaded while this one is ranked (the barriers order LDS only, so the loads
+// stay in flight).
+constexpr int kWmCsMaxG = 512;  // groups per workgroup range (the grid is sized for it)
+
+template <int E>
+struct WmGroupLds {
+    static constexpr int P = 256 * E;
+    uint64_t ov[P];           // keys by bucket slot
+    uint32_t k[P + P / 32];   // slot -> position; then sorted index -> position | slot << 12 (padded)
+    uint32_t cnt[P];          // 2P packed 16-bit bucket counters, then starts; then results by position
+    uint64_t bnd[kWmCsMaxG + 1];
+    uint64_t mm[8];           // per-wave min / max
+    uint32_t ws[4], wf[4], wc[4], wt[4];
+};
+
+template <int E>
+__global__ __launch_bounds__(256) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
+                                                      const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
+                                                      uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big) {
+    constexpr int P = 256 * E, NB = E == 4 ? 11 : 12, LO = E == 4 ? 0 : 1024;  // groups of (LO, P] rows
+    static_assert((1 << NB) == 2 * P, "two buckets per row of capacity");
+    __shared__ WmGroupLds<E> L;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t g0 = (int64_t)blockIdx.x * sh.nparts / gridDim.x, g1 = (int64_t)(blockIdx.x + 1) * sh.nparts / gridDim.x;
+    for (int64_t i = t; i <= g1 - g0; i += 256) L.bnd[i] = pstart[g0 + i];
+    __syncthreads();
+    uint64_t keyN[E];
+    auto issue = [&](int64_t gi) {
+        const int64_t s = (int64_t)L.bnd[gi - g0];
+        const int m = (int)((int64_t)L.bnd[gi - g0 + 1] - s);
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            keyN[r] = (m > LO && m <= P && e < m) ? __builtin_nontemporal_load(gkey + s + e) : 0ull;
+        }
+    };
+    if (g0 < g1) issue(g0);
+    for (int64_t g = g0; g < g1; ++g) {
+        const int64_t s = (int64_t)L.bnd[g - g0];
+        const int m = (int)((int64_t)L.bnd[g - g0 + 1] - s);
+        uint64_t key[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r) key[r] = keyN[r];
+        if (g + 1 < g1) issue(g + 1);
+        if (m > P && E == 8 && t == 0) *too_big = 1u;  // above 2048 rows: the caller takes the LSD path
+        if (m <= LO || m > P) continue;  // (uniform) empty, or the other kernel's size class
+        uint64_t mn = ~0ull, mx = 0ull;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            if (e < m) mn = min(mn, key[r]), mx = max(mx, key[r]);
+            L.cnt[e] = 0u;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        if (lane == 0) L.mm[wave] = mn, L.mm[4 + wave] = mx;
+        wm_barrier();
+        mn = min(min(L.mm[0], L.mm[1]), min(L.mm[2], L.mm[3]));
+        mx = max(max(L.mm[4], L.mm[5]), max(L.mm[6], L.mm[7]));
+        const uint64_t span = mx - mn;
+        const int sb = span ? 64 - __clzll((long long)span) : 0;
+        const int shift = sb > NB ? sb - NB : 0;
+        uint32_t se[E], sl[E];  // bucket, then start | end << 16; arrival, then slot
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            se[r] = sl[r] = 0u;
+            if (e < m) {
+                const uint32_t bk = (uint32_t)((key[r] - mn) >> shift), sh16 = (bk & 1u) * 16u;
+                const uint32_t old = atomicAdd(&L.cnt[bk >> 1], 1u << sh16);
+                se[r] = bk;
+                sl[r] = (old >> sh16) & 0xFFFFu;
+            }
+        }
+        wm_barrier();
+        {  // exclusive scan of the 2P counters: thread t owns words E t .. E t + E - 1
+            uint32_t w[E], tot = 0, big = 0;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                w[q] = L.cnt[E * t + q];
+                const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+                tot += lo + hi;
+                big |= (lo > (uint32_t)kWmCsCap || hi > (uint32_t)kWmCsCap) ? 1u : 0u;
+            }
+            const uint32_t incl = wave_incl_scan(tot);
+            const bool wbig = __ballot(big) != 0;
+            if (lane == 63) L.ws[wave] = incl, L.wf[wave] = wbig ? 1u : 0u;
+            wm_barrier();
+            if (L.wf[0] | L.wf[1] | L.wf[2] | L.wf[3]) {  // (uniform) clustered keys: the network sorts it
+                if (t == 0) fb[1 + atomicAdd(&fb[0], 1u)] = (uint32_t)g;
+                wm_barrier();  // every thread has read the flags before the next group writes them
+                continue;
+            }
+            uint32_t run = incl - tot;
+#pragma unroll
+            for (int v = 0; v < 3; ++v) run += v < wave ? L.ws[v] : 0u;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+                L.cnt[E * t + q] = run | ((run + lo) << 16);
+                run += lo + hi;
+            }
+        }
+        wm_barrier();
+        uint32_t maxc = 0;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            if (e < m) {
+                const uint32_t bk = se[r];
+                const uint32_t st = (L.cnt[bk >> 1] >> ((bk & 1u) * 16u)) & 0xFFFFu;
+                const uint32_t b1 = bk + 1;
+                const uint32_t en = b1 < (1u << NB) ? (L.cnt[b1 >> 1] >> ((b1 & 1u) * 16u)) & 0xFFFFu : (uint32_t)m;
+                const uint32_t slot = st + sl[r];
+                L.k[wm_pad(slot)] = (uint32_t)e;
+                L.ov[slot] = key[r];
+                se[r] = st | (en << 16);
+                sl[r] = slot;
+                maxc = max(maxc, en - st);
+            }
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) maxc = max(maxc, (uint32_t)__shfl_xor((int)maxc, d, 64));
+        if (lane == 0) L.wc[wave] = maxc;
+        wm_barrier();
+        maxc = max(max(L.wc[0], L.wc[1]), max(L.wc[2], L.wc[3]));
+        uint32_t rank[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r) rank[r] = 0u;
+        for (uint32_t j = 0; maxc > 1 && j < maxc; ++j) {
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                const uint32_t st = se[r] & 0xFFFFu, en = se[r] >> 16;
+                if (st + j < en) {
+                    const uint32_t q = L.k[wm_pad(st + j)];
+                    rank[r] += wm_less(L.ov[st + j], q, key[r], (uint32_t)(r * 256 + t)) ? 1u : 0u;
+                }
+            }
+        }
+        wm_barrier();  // every bucket read is done: L.k takes the sorted order
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            if (e < m) L.k[wm_pad((se[r] & 0xFFFFu) + rank[r])] = (uint32_t)e | (sl[r] << 12);
+        }
+        wm_barrier();
+        // the function: wave w takes sorted indices [64 E w, 64 E (w + 1)) in E steps of 64
+        uint32_t rv[E], pos[E];
+        uint32_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int i = wave * 64 * E + r * 64 + lane;
+            const bool live = i < m;
+            const uint32_t x = live ? L.k[wm_pad(i)] : 0u;
+            pos[r] = x & 4095u;
+            rv[r] = 0u;
+            if (f.func == QEH_WIN_ROW_NUMBER) {
+                rv[r] = (uint32_t)i + 1u;
+            } else if (f.func == QEH_WIN_NTILE) {
+                const int64_t q = m / f.param, rm = m % f.param, r0 = i;
+                rv[r] = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
+            } else {
+                const uint64_t ov = live ? L.ov[x >> 12] : 0ull;
+                const uint64_t pv = (live && i > 0) ? L.ov[L.k[wm_pad(i - 1)] >> 12] : 0ull;
+                const uint32_t flag = (live && (i == 0 || pv != ov)) ? 1u : 0u;
+                if (f.func == QEH_WIN_RANK) {  // index of the last peer-group start at or before i
+                    uint32_t v = flag ? (uint32_t)i : 0u;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t u = __shfl_up(v, d, 64);
+                        if (lane >= d) v = u > v ? u : v;
+                    }
+                    v = v > carry ? v : carry;
+                    rv[r] = v;
+                    carry = __shfl(v, 63, 64);
+                } else {  // DENSE_RANK: peer-group starts so far
+                    const uint32_t v = wave_incl_scan(flag) + carry;
+                    rv[r] = v;
+                    carry = __shfl(v, 63, 64);
+                }
+            }
+        }
+        if (f.func == QEH_WIN_RANK || f.func == QEH_WIN_DENSE_RANK) {  // (uniform) carries across waves
+            if (lane == 0) L.wt[wave] = carry;
+            wm_barrier();
+            uint32_t c = 0;
+#pragma unroll
+            for (int v = 0; v < 3; ++v)
+                if (v < wave) c = f.func == QEH_WIN_RANK ? max(c, L.wt[v]) : c + L.wt[v];
+#pragma unroll
+            for (int r = 0; r < E; ++r) rv[r] = f.func == QEH_WIN_RANK ? max(rv[r], c) + 1u : rv[r] + c;
+        }
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if (wave * 64 * E + r * 64 + lane < m) L.cnt[pos[r]] = rv[r];
+        wm_barrier();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int e = r * 256 + t;
+            if (e < m) res[s + e] = (uint16_t)L.cnt[e];
+        }
+        wm_barrier();  // the group's LDS reads are done before the next group's writes
     }
 }
 
@@ -1333,18 +1439,28 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     {
         KernelTimer kt(ctx, "window_sort");
         if (wf.no_count || wf.skip_sort) {
-            hipLaunchKernelGGL((k_wm2_sort<false, false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_sort<false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
+            hipLaunchKernelGGL((k_wm2_sort<true, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
         } else {
-            hipLaunchKernelGGL((k_wm2_sort<false, true, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+            // counting sort, a workgroup per group, ranges of <= kWmCsMaxG groups per workgroup; then
+            // the network for the queued (clustered) groups of both size classes
+            const int64_t ncs = std::max<int64_t>(std::min<int64_t>((int64_t)cus * 16, sh.nparts),
+                                                  (sh.nparts + kWmCsMaxG - 1) / kWmCsMaxG);
+            hipLaunchKernelGGL(k_wm2_csort_wg<4>, dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                               flag.as<uint32_t>());
+            hipLaunchKernelGGL(k_wm2_csort_wg<8>, dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                               flag.as<uint32_t>());
+            hipLaunchKernelGGL((k_wm2_sort<false, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
                                fbl.as<uint32_t>());
-            hipLaunchKernelGGL((k_wm2_sort<false, false, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_sort<true, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
                                fbl.as<uint32_t>());
         }
-        hipLaunchKernelGGL((k_wm2_sort<true, false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
-                           pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
     }
     QEH_HIP(hipGetLastError());
     uint32_t too_big = 0;

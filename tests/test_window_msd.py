@@ -154,3 +154,21 @@ def test_msd_window_counting_sort_groups(ctx, monkeypatch, func, param, vdt, par
     k[:64] = k[0]
     got, want, ran = _run(ctx, func, k, v.astype(vdt), True, param)
     assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.DenseRank, 0), (W.Ntile, 5)])
+def test_msd_window_clustered_big_groups(ctx, monkeypatch, func, param):
+    """Groups of 1025..2048 rows with many ties: the counting sort queues them and the 2048-row
+    network kernel sorts the queue; one small clustered group and spread groups alongside."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(23)
+    n = 300_000
+    k = r.integers(0, 200, n).astype(np.int64)
+    v = r.integers(-(2 ** 40), 2 ** 40, n).astype(np.int64)
+    clustered = k < 100
+    v[clustered] = r.integers(-30, 30, int(clustered.sum()))
+    k[:700] = 500  # a small group, clustered too
+    v[:700] = r.integers(0, 3, 700)
+    got, want, ran = _run(ctx, func, k, v, True, param)
+    assert ran and np.array_equal(got, want)

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Window path check on the GPU box: partitioning-window parity tests, then cfg5 with the group
-# counting sort and with the bitonic network only (QEH_WM_NO_COUNT=1), then RANK / LAG.
+# Window path check on the GPU box: partitioning-window parity tests, then cfg5 with the
+# workgroup-per-group counting sort and with the network only (QEH_WM_NO_COUNT=1), then RANK / LAG.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_window_msd.py tests/test_join_sort_window.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/wtest.log 2>&1 || { tail -30 gpurun_out/wtest.log; exit 1; }
