@@ -92,6 +92,8 @@ __device__ __forceinline__ uint64_t wm_order_bits(uint64_t raw, int dtype, int a
     return asc ? u : ~u;
 }
 
+typedef unsigned int v4u32w __attribute__((ext_vector_type(4)));
+
 struct WmShape {
     int64_t n;
     int64_t kmin;
@@ -824,7 +826,19 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
         R.lofs[tid] = 0;
         __syncthreads();
-        for (int64_t i = s0 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
+        {  // the bucket's low-digit counts: 8 digits per 16-B load, aligned body, scalar edges
+            const int64_t a0 = std::min<int64_t>(s1, (s0 + 7) & ~(int64_t)7), a1 = std::max<int64_t>(a0, s1 & ~(int64_t)7);
+            for (int64_t i = s0 + tid; i < a0; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
+            for (int64_t i = a1 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
+            for (int64_t i = a0 + (int64_t)tid * 8; i < a1; i += (int64_t)kWmBlock * 8) {
+                const v4u32w w = __builtin_nontemporal_load((const v4u32w *)(i_kl + i));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    atomicAdd(&R.lofs[w[q] & 0xFFFFu], 1u);
+                    atomicAdd(&R.lofs[w[q] >> 16], 1u);
+                }
+            }
+        }
         __syncthreads();
         {
             const uint32_t ex = block_excl_scan1024(R.lofs[tid], R.wsum);
