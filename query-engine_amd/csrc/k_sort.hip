@@ -350,6 +350,23 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    // the next tile's ids and columns are loaded into registers while this tile is ranked, staged
+    // and written (the barriers below order LDS only, so those loads stay in flight)
+    uint32_t dgn[kPmIpt];
+    uint64_t vn[kPmIpt][NC > 0 ? NC : 1];
+    auto load = [&](int64_t c0) {
+        const int64_t base = c0 + (int64_t)wave * 64 * kPmIpt + lane;
+#pragma unroll
+        for (int j = 0; j < kPmIpt; ++j) {
+            const int64_t i = base + j * 64;
+            const int64_t ii = i < hi ? i : hi - 1;
+            dgn[j] = ids[ii];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) vn[j][c] = __builtin_nontemporal_load(&cols.src[c][ii]);
+        }
+    };
+    if (lo < hi) load(lo);
+    __syncthreads();  // run[]
     for (int64_t c0 = lo; c0 < hi; c0 += kPmTile) {
         for (int i = t; i < W * kRadix; i += kRsThreads) (&wcnt[0][0])[i] = 0;
         const int64_t base = c0 + (int64_t)wave * 64 * kPmIpt + lane;
@@ -357,13 +374,12 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
         uint64_t v[kPmIpt][NC > 0 ? NC : 1];
 #pragma unroll
         for (int j = 0; j < kPmIpt; ++j) {
-            const int64_t i = base + j * 64;
-            const int64_t ii = i < hi ? i : hi - 1;
-            dg[j] = ids[ii];
+            dg[j] = dgn[j];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) v[j][c] = __builtin_nontemporal_load(&cols.src[c][ii]);
+            for (int c = 0; c < NC; ++c) v[j][c] = vn[j][c];
         }
-        __syncthreads();
+        if (c0 + kPmTile < hi) load(c0 + kPmTile);
+        lds_barrier();
         uint32_t rk[kPmIpt];
 #pragma unroll
         for (int j = 0; j < kPmIpt; ++j) {
@@ -373,7 +389,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
             rk[j] = before + mbcnt(peers);
             if (live && mbcnt(peers) == 0) wcnt[wave][dg[j]] = before + (uint32_t)popc64(peers);
         }
-        __syncthreads();
+        lds_barrier();
         uint32_t tot = 0, incl = 0;
         if (t < kRadix) {
 #pragma unroll
@@ -386,14 +402,14 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
             incl = wave_incl_scan(tot);
             if (lane == 63) wsum[wave] = incl;
         }
-        __syncthreads();
+        lds_barrier();
         if (t < kRadix) {
             uint32_t wbase = 0;
 #pragma unroll
             for (int w = 0; w < DW; ++w) wbase += w < wave ? wsum[w] : 0;
             loc[t] = wbase + incl - tot;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int j = 0; j < kPmIpt; ++j) {
             if (base + j * 64 < hi) {
@@ -403,7 +419,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
                 for (int c = 0; c < NC; ++c) s_val[c][p] = v[j][c];
             }
         }
-        __syncthreads();
+        lds_barrier();
         const int cnt = (int)(hi - c0 < kPmTile ? hi - c0 : kPmTile);
         for (int p = t; p < cnt; p += kRsThreads) {
             const uint32_t d = s_id[p];
@@ -412,7 +428,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
 #pragma unroll
             for (int c = 0; c < NC; ++c) cols.dst[c][pos] = s_val[c][p];
         }
-        __syncthreads();
+        lds_barrier();
         if (t < kRadix) run[t] += tot_s[t];
     }
 }
@@ -986,6 +1002,38 @@ __global__ void k_hash_ids8(HashKeys keys, int64_t n, uint32_t parts, uint8_t *_
             h = hash64(h ^ (hash64(v) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
         }
         ids[i] = (uint8_t)(h % parts);
+    }
+}
+
+// k_hash_ids8 for one non-null Int64 key column: eight rows per thread (four 16-B loads, one 8-B
+// store of ids), the same hash.
+__global__ __launch_bounds__(kBlock) void k_hash_ids8_i64(const int64_t *__restrict__ key, int64_t n, uint32_t parts,
+                                                          uint8_t *__restrict__ ids) {
+    typedef long long v2i64h __attribute__((ext_vector_type(2)));
+    for (int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 8; i0 < n; i0 += (int64_t)gridDim.x * kBlock * 8) {
+        uint64_t v[8];
+        if (i0 + 8 <= n && (((uintptr_t)(key + i0)) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const v2i64h w = __builtin_nontemporal_load((const v2i64h *)(key + i0) + q);
+                v[2 * q] = (uint64_t)w[0], v[2 * q + 1] = (uint64_t)w[1];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = i0 + q < n ? (uint64_t)key[i0 + q] : 0ull;
+        }
+        uint64_t out = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            h = hash64(h ^ (hash64(v[q]) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+            out |= (uint64_t)(uint8_t)(h % parts) << (8 * q);
+        }
+        if (i0 + 8 <= n) {
+            *(uint64_t *)(ids + i0) = out;
+        } else {
+            for (int q = 0; q < 8 && i0 + q < n; ++q) ids[i0 + q] = (uint8_t)(out >> (8 * q));
+        }
     }
 }
 
@@ -1653,8 +1701,12 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
     std::vector<uint32_t> h((size_t)kRadix * nblocks, 0);
     if (n > 0) {
         KernelTimer kt(ctx, "partition_move");
-        hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
-                           (uint32_t)n_parts, ids.as<uint8_t>());
+        if (n_keys == 1 && keys[0].dtype == QEH_DT_INT64 && (!keys[0].validity || keys[0].null_count == 0))
+            hipLaunchKernelGGL(k_hash_ids8_i64, dim3(grid_for(ctx, (n + 7) / 8, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
+                               (const int64_t *)keys[0].values + keys[0].offset, n, (uint32_t)n_parts, ids.as<uint8_t>());
+        else
+            hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
+                               (uint32_t)n_parts, ids.as<uint8_t>());
         hipLaunchKernelGGL(k_rs_hist<uint8_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, 0,
                            hist.as<uint32_t>(), nblocks);
         QEH_HIP(hipGetLastError());

@@ -110,10 +110,33 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-    for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) {
-        const uint64_t kk = (uint64_t)wm_key_val(wm_ld<KES>(key.values, i), key.dtype) - (uint64_t)sh.kmin;
+    // 16-B loads (KES = 8: two keys, KES = 4: four) over the 16-B-aligned body, scalar edges
+    constexpr int PER = 16 / KES, U = 4;  // keys per load, loads in flight per thread
+    const char *kp = (const char *)key.values;
+    int64_t a0 = r0;
+    while (a0 < r1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
+    const int64_t body = (r1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
+    auto one = [&](uint64_t raw) {
+        const uint64_t kk = (uint64_t)wm_key_val(raw, key.dtype) - (uint64_t)sh.kmin;
         atomicAdd(&h[kk >> sh.lb], 1u);
+    };
+    for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
+        v4u32w w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load((const v4u32w *)(kp + (i + (int64_t)u * kWmBlock * PER) * KES));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (KES == 8) {
+                one((uint64_t)w[u][0] | ((uint64_t)w[u][1] << 32));
+                one((uint64_t)w[u][2] | ((uint64_t)w[u][3] << 32));
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) one((uint64_t)w[u][q]);
+            }
+        }
     }
+    for (int64_t i = r0 + threadIdx.x; i < a0; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+    for (int64_t i = a0 + body + threadIdx.x; i < r1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
     __syncthreads();
     counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
 }
