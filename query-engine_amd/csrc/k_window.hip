@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "../../include/qeh_plan.h"
 #include "device_common.h"
@@ -315,7 +316,23 @@ struct WmFunc {
     int32_t asc;
     int32_t has_dflt;
     int64_t dflt;      // default bits in the output width
+    uint64_t *vout;    // id-free path, value functions: each row's value bits at its pass-2 position
 };
+
+// Value functions at sorted index i of a group of m rows: the source row's sorted index (false when
+// the offset leaves the partition; LAST_VALUE spans the whole partition, as the reference's frame).
+__device__ __forceinline__ bool wm_value_src(const WmFunc &f, int i, int m, int &js) {
+    if (f.func == QEH_WIN_LAG) {
+        js = (int)(i - f.param);
+        return f.param <= i;
+    }
+    if (f.func == QEH_WIN_LEAD) {
+        js = (int)(i + f.param);
+        return f.param < (int64_t)m - i;
+    }
+    js = f.func == QEH_WIN_FIRST_VALUE ? 0 : m - 1;
+    return true;
+}
 
 // order key (wm_order_key encoding) -> the column's value bits in its own width
 __device__ __forceinline__ uint64_t wm_decode(uint64_t ok, int asc, int odt) {
@@ -913,7 +930,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     }
 }
 
-template <int R, int P>
+template <int R, int P, bool VF>
 __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                                                WmWaveLds<P> &L, int lane);
 
@@ -923,7 +940,7 @@ constexpr int kWmCsCap = 16;  // counting sort (k_wm2_csort_wg): most rows one b
 // stable); each row's result is written at its own position in the group
 // `pre` holds the group's order keys register-major (element r * 64 + lane in pre[r]), loaded by
 // the caller ahead of time.
-template <int R, int P, int RP>
+template <int R, int P, int RP, bool VF>
 __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                           WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
     static_assert(R <= RP, "prefetch too short");
@@ -986,12 +1003,13 @@ __device__ void wm2_group(const uint64_t (&pre)[RP], int64_t s, int m, const WmF
             L.k[wm_pad(e + b + 1)] = x;
         }
     }
-    wm2_group_tail<R, P>(s, m, f, res_out, L, lane);
+    wm2_group_tail<R, P, VF>(s, m, f, res_out, L, lane);
 }
 
 // With the group's order (position in the low 11 bits of L.k[wm_pad(i)], i = sorted index): the
 // function's value per row, written at the row's own position in the group.
-template <int R, int P>
+// VF: value functions (valid flag in res_out, value bits in f.vout); else rank functions.
+template <int R, int P, bool VF>
 __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f, uint16_t *__restrict__ res_out,
                                                WmWaveLds<P> &L, int lane) {
     wm_wave_sync();
@@ -1005,7 +1023,17 @@ __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f
         const uint32_t pos = x & 2047;
         const uint64_t ov = live ? L.ov[pos] : 0ull;
         uint32_t res;
-        if (f.func == QEH_WIN_ROW_NUMBER) {
+        if (VF) {  // (valid flag, value bits of the source row at pos)
+            int js;
+            const bool ok = wm_value_src(f, e, m, js);
+            uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
+            res = f.has_dflt ? 1u : 0u;
+            if (live && ok) {
+                bits = wm_decode(L.ov[L.k[wm_pad(js)] & 2047], f.asc, f.odt);
+                res = 1u;
+            }
+            if (live) f.vout[s + pos] = bits;
+        } else if (f.func == QEH_WIN_ROW_NUMBER) {
             res = (uint32_t)e + 1u;
         } else if (f.func == QEH_WIN_NTILE) {
             const int64_t q = m / f.param, rm = m % f.param, r0 = e;
@@ -1045,7 +1073,7 @@ __device__ __forceinline__ void wm2_group_tail(int64_t s, int m, const WmFunc &f
 // (larger LDS area).  LIST: the groups the counting sort (k_wm2_csort_wg) queued in fb (fb[0] =
 // count, fb[1..] = group numbers); else every group of the size class.  (Loading the next group's
 // keys while sorting this one needed 256 VGPRs and ran slower.)
-template <bool BIG, bool LIST>
+template <bool BIG, bool LIST, bool VF>
 __global__ __launch_bounds__(kWmSortBlock, 2) void k_wm2_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                               const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
                                                               uint32_t *__restrict__ too_big, const uint32_t *__restrict__ fb) {
@@ -1083,12 +1111,12 @@ __global__ __launch_bounds__(kWmSortBlock, 2) void k_wm2_sort(WmShape sh, WmFunc
             pre[r] = e < m ? gkey[s + e] : 0ull;
         }
         const int mi = (int)m;
-        if (BIG) wm2_group<RP, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 64) wm2_group<1, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 128) wm2_group<2, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 256) wm2_group<4, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else if (mi <= 512) wm2_group<8, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
-        else wm2_group<RP, P, RP>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        if (BIG) wm2_group<RP, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 64) wm2_group<1, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 128) wm2_group<2, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 256) wm2_group<4, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else if (mi <= 512) wm2_group<8, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
+        else wm2_group<RP, P, RP, VF>(pre, s, mi, f, res, wl[wave], too_big, lane);
     }
 }
 
@@ -1114,7 +1142,7 @@ struct WmGroupLds {
     uint32_t ws[4], wf[4], wc[4], wt[4];
 };
 
-template <int E>
+template <int E, bool VF>
 __global__ __launch_bounds__(256) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                       const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
                                                       uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big) {
@@ -1259,7 +1287,17 @@ __global__ __launch_bounds__(256) void k_wm2_csort_wg(WmShape sh, WmFunc f, cons
             const uint32_t x = live ? L.k[wm_pad(i)] : 0u;
             pos[r] = x & 4095u;
             rv[r] = 0u;
-            if (f.func == QEH_WIN_ROW_NUMBER) {
+            if (VF) {  // (valid flag, value bits of the source row at pos)
+                int js;
+                const bool ok = wm_value_src(f, i, m, js);
+                uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
+                rv[r] = f.has_dflt ? 1u : 0u;
+                if (live && ok) {
+                    bits = wm_decode(L.ov[L.k[wm_pad(js)] >> 12], f.asc, f.odt);
+                    rv[r] = 1u;
+                }
+                if (live) f.vout[s + pos[r]] = bits;
+            } else if (f.func == QEH_WIN_ROW_NUMBER) {
                 rv[r] = (uint32_t)i + 1u;
             } else if (f.func == QEH_WIN_NTILE) {
                 const int64_t q = m / f.param, rm = m % f.param, r0 = i;
@@ -1310,13 +1348,16 @@ __global__ __launch_bounds__(256) void k_wm2_csort_wg(WmShape sh, WmFunc f, cons
 
 // inverse of pass 2: replay each bucket's tiles, gather the results run by run (group order ->
 // pass-1 order)
-template <int DB>
+// VAL (value functions): the value bits move beside the flags (res2v -> res1v, staged in LDS).
+template <int DB, bool VAL = false>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                        const uint64_t *__restrict__ pstart, const uint16_t *__restrict__ i_kl,
-                                                       const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1) {
+                                                       const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1,
+                                                       const uint64_t *__restrict__ res2v, uint64_t *__restrict__ res1v) {
     __shared__ WmRankLds R;
     __shared__ uint64_t lpos[kWmDig];
     __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
+    __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
     const int64_t L = (int64_t)1 << sh.lb;
@@ -1355,12 +1396,17 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
-                st_r[s] = res2[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])];
+                const uint64_t src = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+                st_r[s] = res2[src];
+                if (VAL) st_v[s] = res2v[src];
             }
             wm_barrier();
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
-                if (live[j]) __builtin_nontemporal_store(st_r[slot[j]], res1 + t0 + woff + j * 64);
+                if (live[j]) {
+                    __builtin_nontemporal_store(st_r[slot[j]], res1 + t0 + woff + j * 64);
+                    if (VAL) __builtin_nontemporal_store(st_v[slot[j]], res1v + t0 + woff + j * 64);
+                }
             lpos[tid] += tcnt;
             wm_barrier();
         }
@@ -1370,12 +1416,17 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
 
 // inverse of pass 1: replay each workgroup's tiles, gather the results run by run and write them in
 // input order as Int64
-template <int KES, int DB>
+// VAL = 0: rank functions, out = Int64 results.  VAL = 4 / 8 (value functions): res1 holds valid
+// flags, res1v the value bits (gathered beside them through LDS), written in VAL bytes (zero when
+// NULL) plus a validity byte.
+template <int KES, int DB, int VAL = 0>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, const uint64_t *__restrict__ base,
-                                                       const uint16_t *__restrict__ res1, int64_t *__restrict__ out) {
+                                                       const uint16_t *__restrict__ res1, void *__restrict__ out,
+                                                       const uint64_t *__restrict__ res1v, uint8_t *__restrict__ valid8) {
     __shared__ WmRankLds R;
     __shared__ uint64_t lpos[kWmDig];
     __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
+    __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
     lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
@@ -1409,12 +1460,25 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
-            st_r[s] = res1[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])];
+            const uint64_t src = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+            st_r[s] = res1[src];
+            if (VAL) st_v[s] = res1v[src];
         }
         wm_barrier();
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (live[j]) __builtin_nontemporal_store((int64_t)st_r[slot[j]], out + t0 + woff + j * 64);
+        for (int j = 0; j < NJ; ++j) {
+            if (!live[j]) continue;
+            const int64_t i = t0 + woff + j * 64;
+            if constexpr (VAL == 0) {
+                __builtin_nontemporal_store((int64_t)st_r[slot[j]], (int64_t *)out + i);
+            } else {
+                const bool ok = st_r[slot[j]] != 0;
+                const uint64_t v = st_v[slot[j]];
+                if constexpr (VAL == 8) __builtin_nontemporal_store(ok ? v : 0ull, (uint64_t *)out + i);
+                else __builtin_nontemporal_store(ok ? (uint32_t)v : 0u, (uint32_t *)out + i);
+                valid8[i] = ok ? 1 : 0;
+            }
+        }
         lpos[tid] += tcnt;
         wm_barrier();
     }
@@ -1425,12 +1489,17 @@ __global__ void k_wm_set2(uint64_t *a, uint64_t *b, uint64_t v) {
 }
 
 // The id-free pipeline for the rank functions (shapes checked by window_msd).
+// Value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column, dflt = the
+// default's bits or null): the sort writes each row's value bits beside its valid flag and the
+// inverse passes move both.
 static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
-                       WmShape sh, qeh_column *out) {
+                       const int64_t *dflt, WmShape sh, qeh_column *out) {
     const int64_t n = sh.n;
     const int cus = ctx->props.multiProcessorCount;
     const int g1 = (int)((n + sh.span - 1) / sh.span);
-    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag;
+    const bool value_fn = func >= QEH_WIN_LAG;
+    const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
+    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     if (cnt1.alloc(ctx, nc1 * 4) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
@@ -1464,7 +1533,8 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_HIP(hipGetLastError());
     key1.reset();
     DevBuf fbl;  // groups the counting sort queues for the network: count, then group numbers
-    if (res2.alloc(ctx, n * 2) || fbl.alloc(ctx, (sh.nparts + 1) * 4)) return fail(QEH_E_OOM, "window: out of device memory");
+    if (res2.alloc(ctx, n * 2) || fbl.alloc(ctx, (sh.nparts + 1) * 4) || (value_fn && res2v.alloc(ctx, n * 8)))
+        return fail(QEH_E_OOM, "window: out of device memory");
     QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
     QEH_HIP(hipMemsetAsync(fbl.p, 0, 4, ctx->stream));
     WmFunc wf{};
@@ -1472,51 +1542,79 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     wf.param = param;
     wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
     wf.no_count = std::getenv("QEH_WM_NO_COUNT") ? 1 : 0;
+    wf.odt = order.dtype;
+    wf.asc = asc ? 1 : 0;
+    wf.has_dflt = dflt != nullptr;
+    if (dflt) wf.dflt = esz == 8 ? *dflt : (int64_t)(uint32_t)*dflt;
+    wf.vout = res2v.as<uint64_t>();
     const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
     {
         KernelTimer kt(ctx, "window_sort");
-        if (wf.no_count || wf.skip_sort) {
-            hipLaunchKernelGGL((k_wm2_sort<false, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
-                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
-            hipLaunchKernelGGL((k_wm2_sort<true, false>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
-                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
-        } else {
+        auto launch = [&](auto vf) {
+            constexpr bool VF = decltype(vf)::value;
+            if (wf.no_count || wf.skip_sort) {
+                hipLaunchKernelGGL((k_wm2_sort<false, false, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
+                hipLaunchKernelGGL((k_wm2_sort<true, false, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(), nullptr);
+                return;
+            }
             // counting sort, a workgroup per group, ranges of <= kWmCsMaxG groups per workgroup; then
             // the network for the queued (clustered) groups of both size classes
             const int64_t ncs = std::max<int64_t>(std::min<int64_t>((int64_t)cus * 16, sh.nparts),
                                                   (sh.nparts + kWmCsMaxG - 1) / kWmCsMaxG);
-            hipLaunchKernelGGL(k_wm2_csort_wg<4>, dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_csort_wg<4, VF>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
                                flag.as<uint32_t>());
-            hipLaunchKernelGGL(k_wm2_csort_wg<8>, dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_csort_wg<8, VF>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
                                flag.as<uint32_t>());
-            hipLaunchKernelGGL((k_wm2_sort<false, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_sort<false, true, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
                                fbl.as<uint32_t>());
-            hipLaunchKernelGGL((k_wm2_sort<true, true>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
+            hipLaunchKernelGGL((k_wm2_sort<true, true, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
                                fbl.as<uint32_t>());
-        }
+        };
+        if (value_fn) launch(std::true_type{});
+        else launch(std::false_type{});
     }
     QEH_HIP(hipGetLastError());
     uint32_t too_big = 0;
     QEH_TRY(read_small(ctx, &too_big, flag.p, 4));
     if (too_big) return kWindowMsdNotEligible;  // a group above 2048 rows / a long tie run: the LSD path
     key2.reset();
-    if (res1.alloc(ctx, n * 2)) return fail(QEH_E_OOM, "window: out of device memory");
-    QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, out));
+    if (res1.alloc(ctx, n * 2) || (value_fn && (res1v.alloc(ctx, n * 8) || valid8.alloc(ctx, n))))
+        return fail(QEH_E_OOM, "window: out of device memory");
+    QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
     {
         KernelTimer kt(ctx, "window_place");
-        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_inv2<10> : k_wm2_inv2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
-                           bst.as<uint64_t>(), pst.as<uint64_t>(), kl1.as<uint16_t>(), res2.as<uint16_t>(),
-                           res1.as<uint16_t>());
+        hipLaunchKernelGGL(value_fn ? (sh.lb == 10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
+                                    : (sh.lb == 10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
+                           dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
+                           kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(), res2v.as<uint64_t>(),
+                           res1v.as<uint64_t>());
         const bool d1i = wm_digit_bits(sh.nb) == 10;
-        hipLaunchKernelGGL(kes == 4 ? (d1i ? k_wm2_inv1<4, 10> : k_wm2_inv1<4, -1>) : (d1i ? k_wm2_inv1<8, 10> : k_wm2_inv1<8, -1>),
-                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, base1.as<uint64_t>(),
-                           res1.as<uint16_t>(), (int64_t *)out->values);
+#define QEH_WM_I1(V)                                                                                                     \
+    (kes == 4 ? (d1i ? k_wm2_inv1<4, 10, V> : k_wm2_inv1<4, -1, V>) : (d1i ? k_wm2_inv1<8, 10, V> : k_wm2_inv1<8, -1, V>))
+        hipLaunchKernelGGL(!value_fn ? QEH_WM_I1(0) : esz == 8 ? QEH_WM_I1(8) : QEH_WM_I1(4), dim3(g1), dim3(kWmBlock), 0,
+                           ctx->stream, kc, sh, base1.as<uint64_t>(), res1.as<uint16_t>(), out->values,
+                           res1v.as<uint64_t>(), valid8.as<uint8_t>());
+#undef QEH_WM_I1
     }
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    if (hipGetLastError() != hipSuccess) {
+        qeh_column_release(ctx, out);
+        return fail(QEH_E_HIP, "window: kernel launch failed");
+    }
+    if (value_fn) {
+        const int st = qeh_bytes_to_validity(ctx, valid8.as<uint8_t>(), n, out->validity);
+        if (st != QEH_OK) {
+            qeh_column_release(ctx, out);
+            return st;
+        }
+        out->null_count = -1;
+    }
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
         qeh_column_release(ctx, out);
         return fail(QEH_E_HIP, "window: kernel failed");
     }
@@ -1579,7 +1677,7 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     const int64_t nwin = ((n - 1) >> win_shift) + 1;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
 
-    if (!value_fn && !std::getenv("QEH_WM_IDS")) return window_noid(ctx, func, part, order, asc, param, sh, out);
+    if (!std::getenv("QEH_WM_IDS")) return window_noid(ctx, func, part, order, asc, param, dflt, sh, out);
     DevBuf cnt1, base1, key1, id1, kl1, key2, id2, pst, cnt5, base5, pa, pb, va, vb, valid8, flag;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
