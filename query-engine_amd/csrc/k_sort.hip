@@ -1707,8 +1707,8 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         else
             hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
                                (uint32_t)n_parts, ids.as<uint8_t>());
-        hipLaunchKernelGGL(k_rs_hist<uint8_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, 0,
-                           hist.as<uint32_t>(), nblocks);
+        hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
+                           hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));
@@ -1809,8 +1809,8 @@ extern "C" int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *co
         KernelTimer kt(ctx, "partition_move");
         hipLaunchKernelGGL(k_hash_ids8_pred, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
                            make_colref(kc), cs, terms, n, (uint32_t)n_parts, ids.as<uint8_t>());
-        hipLaunchKernelGGL(k_rs_hist<uint8_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, 0,
-                           hist.as<uint32_t>(), nblocks);
+        hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
+                           hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));

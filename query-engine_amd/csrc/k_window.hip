@@ -7,20 +7,19 @@
 // DENSE_RANK without, NTILE's first size % n buckets one row larger (:67-140); output aligned to
 // input order.  The LSD path of k_sort.hip sorts 40-bit (k, v) pair keys in five 8-bit passes
 // and scatters the numbers back with random 8-B stores; this path moves each row a bounded
-// number of times with coalesced writes:
-//   1. k_wm_hist1 + k_wm_pass1: a 1024-way partition of (order key, row id, low key bits) by the
-//      key's high bits (per-workgroup histograms, one scan, LDS-staged runs);
-//   2. k_wm_pass2: inside each bucket (one workgroup per bucket) a 1024-way partition by the
-//      key's low bits -- every PARTITION BY group is now contiguous, its start in pstart[];
-//   3. k_wm_sort: one wave per group sorts (order key, row id) in registers (bitonic network,
-//      lane-major layout: distances below the per-lane width are register swaps), computes the
-//      function, emits (row id, result) pairs in group order, and counts them per output window;
-//   4. k_wm_pass5a / k_wm_pass5b: the pairs are partitioned by row id into windows of 2^15 rows
-//      (window starts are exact: every row id occurs once);
-//   5. k_wm_place: a workgroup stages one window's results in LDS and writes its rows in order.
-// Partitions are ranked with LDS atomics (unordered within a tile): the sort compares
-// (order key, row id), so nothing depends on stability.  Groups above 2048 rows (skew) and
-// shapes outside the limits return kWindowMsdNotEligible and the caller takes the LSD path.
+// number of times with run-contiguous writes and no row ids:
+//   1. k_wm_hist1 + k_wm2_pass1: a stable 1024-way partition of (order key, low key bits) by the
+//      key's high bits (per-workgroup histograms, one scan, ballot-ranked LDS-staged runs);
+//   2. k_wm2_pass2: inside each bucket a stable partition by the key's low bits -- every PARTITION
+//      BY group is now contiguous (in input order), its start in pstart[];
+//   3. k_wm2_csort_wg: a workgroup per group ranks its rows by counting sort (exact ties by
+//      position in the group = input order) and writes the function's value at each row's own
+//      position; groups whose keys cluster go to the bitonic network kernel (k_wm2_sort);
+//   4. k_wm2_inv2 / k_wm2_inv1: the two partitions are replayed (the ranking is deterministic) and
+//      the results gathered back run by run, into pass-1 order and then input order.
+// Value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column) carry the value
+// bits beside a valid flag.  Groups above 2048 rows (skew) and shapes outside the limits return
+// kWindowMsdNotEligible and the caller takes the LSD path.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -36,7 +35,6 @@ constexpr int kWmBlock = 1024;                // partition passes: one workgroup
 constexpr int kWmTile = 8192;                 // rows per partition-pass tile (8 per thread)
 constexpr int kWmDig = 1024;                  // digits per partition pass
 constexpr int kWmSortBlock = 256;             // group sort: 4 waves
-constexpr int kWmWinBits = 15;                // output window = 2^15 rows (128 KB of u32 in LDS)
 
 // Workgroup barrier ordering LDS only: the next tile's global loads stay in flight across it
 // (__syncthreads would also drain vmcnt and serialise the prefetch).
@@ -55,14 +53,6 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t *ws
     }
     wm_barrier();
     return inc - v + wsum[wave];
-}
-
-// order key -> unsigned sortable 64-bit (ascending; descending flips every bit)
-__device__ __forceinline__ uint64_t wm_order_key(const ColRef &c, int64_t row, int asc) {
-    const int64_t x = load_i64(c, row);
-    const int64_t o = (c.dtype == QEH_DT_FLOAT32 || c.dtype == QEH_DT_FLOAT64) ? f64_order_key(as_f64(x)) : x;
-    const uint64_t u = (uint64_t)o ^ 0x8000000000000000ull;
-    return asc ? u : ~u;
 }
 
 // Typed element loads: the window kernels are instantiated per key / order-key element width, so the
@@ -142,160 +132,6 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
 }
 
-// Tile skeleton shared by the partition passes: rank the tile's rows by digit with LDS atomics,
-// scan the digit counts, stage the rows sorted by digit, write each digit's run at its running
-// position.  Rows of tile t + 1 are loaded (into registers) before tile t is staged.
-#define WM_TILE_RANK(NJ)                                                   \
-    _Pragma("unroll") for (int j = 0; j < NJ; ++j) rk[j] = live[j] ? atomicAdd(&cnt[d[j]], 1u) : 0u; \
-    wm_barrier();                                                          \
-    const uint32_t c_ = cnt[tid];                                          \
-    lofs[tid] = block_excl_scan1024(c_, wsum);                             \
-    wm_barrier();
-
-// ---- pass 1: partition (order key, row id, low key bits) by the high digit -------------------
-template <int KES, int OES>
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
-                                                       const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
-                                                       uint32_t *__restrict__ o_id, uint16_t *__restrict__ o_kl) {
-    __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
-    __shared__ uint64_t lpos[kWmDig];
-    __shared__ uint64_t st_key[kWmTile];
-    __shared__ uint32_t st_id[kWmTile];
-    __shared__ uint16_t st_kl[kWmTile], st_d[kWmTile];
-    const int tid = threadIdx.x;
-    cnt[tid] = 0;
-    lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
-    __syncthreads();
-    const uint32_t lmask = (1u << sh.lb) - 1u;
-    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-    uint64_t kv[8], ovv[8];
-    auto load = [&](int64_t t0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t i = t0 + j * kWmBlock + tid;
-            const int64_t ii = i < r1 ? i : r0;
-            kv[j] = wm_ld<KES>(key.values, ii);
-            ovv[j] = wm_ld<OES>(ord.values, ii);
-        }
-    };
-    if (r0 < r1) load(r0);
-    for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
-        uint32_t d[8], rk[8], kl[8];
-        uint64_t ok[8];
-        bool live[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            live[j] = t0 + j * kWmBlock + tid < r1;
-            const uint64_t kk = (uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin;
-            d[j] = (uint32_t)(kk >> sh.lb);
-            kl[j] = (uint32_t)kk & lmask;
-            ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
-        }
-        if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
-        WM_TILE_RANK(8)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (!live[j]) continue;
-            const uint32_t s = lofs[d[j]] + rk[j];
-            st_key[s] = ok[j];
-            st_id[s] = (uint32_t)(t0 + j * kWmBlock + tid);
-            st_kl[s] = (uint16_t)kl[j];
-            st_d[s] = (uint16_t)d[j];
-        }
-        wm_barrier();
-        const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
-        for (int s = tid; s < m; s += kWmBlock) {
-            const uint32_t dd = st_d[s];
-            const uint64_t p = lpos[dd] + (uint64_t)(s - (int)lofs[dd]);
-            o_key[p] = st_key[s];
-            o_id[p] = st_id[s];
-            o_kl[p] = st_kl[s];
-        }
-        wm_barrier();
-        lpos[tid] += c_;
-        cnt[tid] = 0;
-        wm_barrier();
-    }
-}
-
-// ---- pass 2: inside each bucket, partition by the low digit; group starts -> pstart ----------
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
-                                                       const uint64_t *__restrict__ i_key, const uint32_t *__restrict__ i_id,
-                                                       const uint16_t *__restrict__ i_kl, uint64_t *__restrict__ o_key,
-                                                       uint32_t *__restrict__ o_id, uint64_t *__restrict__ pstart) {
-    __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
-    __shared__ uint64_t lpos[kWmDig];
-    __shared__ uint64_t st_key[kWmTile];
-    __shared__ uint32_t st_id[kWmTile];
-    __shared__ uint16_t st_d[kWmTile];
-    const int tid = threadIdx.x;
-    const int64_t L = (int64_t)1 << sh.lb;
-    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
-        const uint64_t s0 = bstart[b], s1 = bstart[b + 1];
-        cnt[tid] = 0;
-        __syncthreads();
-        for (uint64_t i = s0 + tid; i < s1; i += kWmBlock) atomicAdd(&cnt[i_kl[i]], 1u);
-        __syncthreads();
-        {
-            const uint32_t c = cnt[tid];
-            const uint32_t ex = block_excl_scan1024(c, wsum);
-            const int64_t part = (int64_t)b * L + tid;
-            if (tid < L && part < sh.nparts) pstart[part] = s0 + ex;
-            lpos[tid] = s0 + ex;
-            cnt[tid] = 0;
-        }
-        __syncthreads();
-        uint64_t kx[8];
-        uint32_t ix[8], lx[8];
-        auto load = [&](uint64_t t0) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                const uint64_t ii = i < s1 ? i : s0;
-                kx[j] = i_key[ii];
-                ix[j] = i_id[ii];
-                lx[j] = i_kl[ii];
-            }
-        };
-        if (s0 < s1) load(s0);
-        for (uint64_t t0 = s0; t0 < s1; t0 += kWmTile) {
-            uint32_t d[8], rk[8], ids[8];
-            uint64_t keys[8];
-            bool live[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                live[j] = t0 + (uint64_t)(j * kWmBlock + tid) < s1;
-                d[j] = lx[j];
-                keys[j] = kx[j];
-                ids[j] = ix[j];
-            }
-            if (t0 + kWmTile < s1) load(t0 + kWmTile);
-            WM_TILE_RANK(8)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (!live[j]) continue;
-                const uint32_t s = lofs[d[j]] + rk[j];
-                st_key[s] = keys[j];
-                st_id[s] = ids[j];
-                st_d[s] = (uint16_t)d[j];
-            }
-            wm_barrier();
-            const int m = (int)std::min<uint64_t>(kWmTile, s1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                const uint64_t p = lpos[dd] + (uint64_t)(s - (int)lofs[dd]);
-                o_key[p] = st_key[s];
-                o_id[p] = st_id[s];
-            }
-            wm_barrier();
-            lpos[tid] += c_;
-            cnt[tid] = 0;
-            wm_barrier();
-        }
-        __syncthreads();
-    }
-}
-
 // ---- group sort: one wave per PARTITION BY group --------------------------------------------
 // A group of m <= 64 R rows is sorted by a 32-bit composite key: the top 21 significant bits of
 // (order key - the group's minimum) above the row's 11-bit position in the group.  The network
@@ -307,7 +143,6 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_pass2(WmShape sh, const uint64_
 struct WmFunc {
     int32_t func;      // QEH_WIN_* (ROW_NUMBER .. LAST_VALUE)
     int64_t param;     // NTILE buckets / LAG, LEAD offset
-    int32_t win_shift; // pass-5a digit = row id >> win_shift
     int32_t skip_sort; // QEH_WM_SKIP_SORT (experiments: load/emit cost without the network)
     int32_t no_count;  // QEH_WM_NO_COUNT (experiments: the bitonic network for every group)
     // value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column itself): the
@@ -334,7 +169,7 @@ __device__ __forceinline__ bool wm_value_src(const WmFunc &f, int i, int m, int 
     return true;
 }
 
-// order key (wm_order_key encoding) -> the column's value bits in its own width
+// order key (wm_order_bits encoding) -> the column's value bits in its own width
 __device__ __forceinline__ uint64_t wm_decode(uint64_t ok, int asc, int odt) {
     const uint64_t u = asc ? ok : ~ok;
     const int64_t o = (int64_t)(u ^ 0x8000000000000000ull);
@@ -402,316 +237,6 @@ struct WmWaveLds {
     uint32_t id[P];
     uint32_t k[P + P / 32];
 };
-
-template <int R, int P, bool VF>
-__device__ void wm_group(const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid, int64_t s, int m,
-                         const WmFunc &f, uint64_t *__restrict__ pairs, uint64_t *__restrict__ vals,
-                         uint32_t *__restrict__ whist, WmWaveLds<P> &L, uint32_t *__restrict__ too_big, int lane) {
-    // coalesced loads (register-major e = r * 64 + lane) into LDS; the group's min / max
-    wm_wave_sync();  // the previous group's LDS reads are done
-    uint64_t mn = ~0ull, mx = 0ull;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        if (e < m) {
-            const uint64_t o = gkey[s + e];
-            L.ov[e] = o;
-            L.id[e] = gid[s + e];
-            mn = o < mn ? o : mn;
-            mx = o > mx ? o : mx;
-        }
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
-    }
-    const uint64_t span = mx - mn;
-    const int sb = span ? 64 - __clzll((long long)span) : 0;
-    const int shift = sb > 21 ? sb - 21 : 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        L.k[wm_pad(e)] = e < m ? ((uint32_t)((L.ov[e] - mn) >> shift) << 11) | (uint32_t)e : 0xFFFFFFFFu;
-    }
-    wm_wave_sync();
-    if (!f.skip_sort) {
-        uint32_t k[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) k[r] = L.k[wm_pad(lane * R + r)];
-        bitonic_sort32<R, 2>(k, lane);
-#pragma unroll
-        for (int r = 0; r < R; ++r) L.k[wm_pad(lane * R + r)] = k[r];
-        wm_wave_sync();
-    }
-    // exact order inside runs of equal prefixes (insertion sort by (order key, row id))
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        if (e >= m) continue;
-        const uint32_t ke = L.k[wm_pad(e)] >> 11;
-        const bool start = e == 0 || (L.k[wm_pad(e - 1)] >> 11) != ke;
-        if (!start || e + 1 >= m || (L.k[wm_pad(e + 1)] >> 11) != ke) continue;
-        int len = 2;
-        while (e + len < m && (L.k[wm_pad(e + len)] >> 11) == ke) ++len;
-        if (len > 64) {
-            *too_big = 1u;
-            continue;
-        }
-        for (int a = 1; a < len; ++a) {
-            const uint32_t x = L.k[wm_pad(e + a)];
-            const uint64_t xo = L.ov[x & 2047];
-            const uint32_t xi = L.id[x & 2047];
-            int b = a - 1;
-            while (b >= 0) {
-                const uint32_t y = L.k[wm_pad(e + b)];
-                if (!wm_less(xo, xi, L.ov[y & 2047], L.id[y & 2047])) break;
-                L.k[wm_pad(e + b + 1)] = y;
-                --b;
-            }
-            L.k[wm_pad(e + b + 1)] = x;
-        }
-    }
-    wm_wave_sync();
-    // results in sorted order, register-major (coalesced emission)
-    uint32_t carry_rank = 0, carry_dense = 0;
-    uint64_t prev_ov = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = r * 64 + lane;
-        const bool live = e < m;
-        const uint32_t x = live ? L.k[wm_pad(e)] : 0u;
-        const uint32_t pos = x & 2047;
-        const uint64_t ov = live ? L.ov[pos] : 0ull;
-        const uint32_t rid = live ? L.id[pos] : 0u;
-        uint32_t res;
-        if (VF) {  // value functions: (valid flag, value of the source row)
-            int64_t es = e;
-            bool ok = true;
-            if (f.func == QEH_WIN_LAG) ok = f.param <= e, es = e - f.param;
-            else if (f.func == QEH_WIN_LEAD) ok = f.param < (int64_t)m - e, es = e + f.param;
-            else if (f.func == QEH_WIN_FIRST_VALUE) es = 0;
-            else es = m - 1;
-            uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
-            res = f.has_dflt ? 1u : 0u;
-            if (live && ok) {
-                bits = wm_decode(L.ov[L.k[wm_pad((int)es)] & 2047], f.asc, f.odt);
-                res = 1u;
-            }
-            if (live) vals[s + e] = bits;
-        } else if (f.func == QEH_WIN_ROW_NUMBER) {
-            res = (uint32_t)e + 1u;
-        } else if (f.func == QEH_WIN_NTILE) {
-            const int64_t q = m / f.param, rm = m % f.param, r0 = e;
-            res = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
-        } else {
-            uint64_t pv = __shfl_up(ov, 1, 64);
-            if (lane == 0) pv = prev_ov;
-            const uint32_t flag = (e == 0 || pv != ov) ? 1u : 0u;
-            if (f.func == QEH_WIN_RANK) {
-                uint32_t v = flag ? (uint32_t)e : 0u;  // last peer-group start at or before e
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t t = __shfl_up(v, d, 64);
-                    if (lane >= d) v = t > v ? t : v;
-                }
-                v = v > carry_rank ? v : carry_rank;
-                res = v + 1u;
-                carry_rank = __shfl(v, 63, 64);
-            } else {  // DENSE_RANK
-                const uint32_t v = wave_incl_scan(flag) + carry_dense;
-                res = v;
-                carry_dense = __shfl(v, 63, 64);
-            }
-            prev_ov = __shfl(ov, 63, 64);
-        }
-        if (live) {
-            pairs[s + e] = ((uint64_t)rid << 32) | res;
-            atomicAdd(&whist[rid >> f.win_shift], 1u);
-        }
-    }
-}
-
-// Workgroup w owns groups [g0, g1) (contiguous rows [pstart[g0], pstart[g1])); its waves take
-// the groups in turn.  Window histograms are added to counts[digit * grid + w] for pass 5a.
-// BIG = false: groups of <= 1024 rows; BIG = true: 1025..2048 rows, a kernel of its own so its
-// larger LDS area does not limit the common case.
-template <bool BIG, bool VF>
-__global__ __launch_bounds__(kWmSortBlock) void k_wm_sort(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
-                                                          const uint64_t *__restrict__ gkey, const uint32_t *__restrict__ gid,
-                                                          uint64_t *__restrict__ pairs, uint64_t *__restrict__ vals,
-                                                          uint32_t *__restrict__ counts, uint32_t *__restrict__ too_big) {
-    constexpr int P = BIG ? 2048 : 1024;
-    __shared__ uint32_t whist[kWmDig];
-    __shared__ WmWaveLds<P> wl[kWmSortBlock / 64];
-    for (int i = threadIdx.x; i < kWmDig; i += kWmSortBlock) whist[i] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t g0 = (int64_t)blockIdx.x * sh.nparts / gridDim.x, g1 = (int64_t)(blockIdx.x + 1) * sh.nparts / gridDim.x;
-    for (int64_t g = g0 + wave; g < g1; g += kWmSortBlock / 64) {
-        const int64_t s = (int64_t)pstart[g];
-        const int64_t m = (int64_t)pstart[g + 1] - s;
-        if (m <= 0) continue;
-        if (BIG) {
-            if (m <= 1024) continue;
-            if (m > 2048) {
-                if (lane == 0) *too_big = 1u;
-                continue;
-            }
-            wm_group<32, P, VF>(gkey, gid, s, (int)m, f, pairs, vals, whist, wl[wave], too_big, lane);
-        } else {
-            const int mi = (int)m;
-            if (mi > 1024) continue;
-            if (mi <= 64) wm_group<1, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
-            else if (mi <= 128) wm_group<2, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
-            else if (mi <= 256) wm_group<4, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
-            else if (mi <= 512) wm_group<8, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
-            else wm_group<16, P, VF>(gkey, gid, s, mi, f, pairs, vals, whist, wl[wave], too_big, lane);
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kWmDig; i += kWmSortBlock)
-        if (whist[i]) atomicAdd(&counts[(int64_t)i * gridDim.x + blockIdx.x], whist[i]);
-}
-
-// ---- pass 5a / 5b: pairs partitioned by row id ------------------------------------------------
-// 5a (global): digit = row id >> win_shift, over the row ranges of k_wm_sort's workgroups, at
-// positions from the scanned window histograms.  5b (segmented): window w holds exactly the row
-// ids [w << win_shift, (w + 1) << win_shift), so its region and every output window's place are
-// known without a histogram; digit = (row id >> wbits) within the window.  V: a value array
-// travels with the pairs (value functions; 4096-row tiles to fit the staging in LDS).
-template <bool SEG, bool V>
-__global__ __launch_bounds__(kWmBlock) void k_wm_pass5(WmShape sh, int nsort, int win_shift, int wbits, int64_t nwin,
-                                                       const uint64_t *__restrict__ pstart,
-                                                       const uint64_t *__restrict__ base, const uint64_t *__restrict__ in,
-                                                       const uint64_t *__restrict__ inv, uint64_t *__restrict__ out,
-                                                       uint64_t *__restrict__ outv) {
-    constexpr int NJ = V ? 4 : 8, TILE = NJ * kWmBlock;
-    __shared__ uint32_t cnt[kWmDig], lofs[kWmDig], wsum[16];
-    __shared__ uint64_t lpos[kWmDig];
-    __shared__ uint64_t st[TILE];
-    __shared__ uint64_t stv[V ? TILE : 1];
-    __shared__ uint16_t st_d[TILE];
-    const int tid = threadIdx.x;
-    const uint32_t dmask = SEG ? (1u << (win_shift - wbits)) - 1u : 0xFFFFFFFFu;
-    const int dshift = SEG ? wbits : win_shift;
-    const int64_t units = SEG ? nwin : nsort;
-    for (int64_t w = blockIdx.x; w < units; w += gridDim.x) {
-        uint64_t r0, r1;
-        if (SEG) {
-            r0 = (uint64_t)w << win_shift;
-            r1 = std::min<uint64_t>((uint64_t)sh.n, (uint64_t)(w + 1) << win_shift);
-            lpos[tid] = r0 + ((uint64_t)tid << wbits);
-        } else {
-            r0 = pstart[w * sh.nparts / nsort];
-            r1 = pstart[(w + 1) * sh.nparts / nsort];
-            lpos[tid] = base[(int64_t)tid * nsort + w];
-        }
-        cnt[tid] = 0;
-        __syncthreads();
-        uint64_t px[NJ], pv[NJ];
-        auto load = [&](uint64_t t0) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const uint64_t i = t0 + (uint64_t)(j * kWmBlock + tid);
-                const uint64_t ii = i < r1 ? i : r0;
-                px[j] = in[ii];
-                if (V) pv[j] = inv[ii];
-            }
-        };
-        if (r0 < r1) load(r0);
-        for (uint64_t t0 = r0; t0 < r1; t0 += TILE) {
-            uint32_t d[NJ], rk[NJ];
-            uint64_t v[NJ], vv[NJ];
-            bool live[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                live[j] = t0 + (uint64_t)(j * kWmBlock + tid) < r1;
-                v[j] = px[j];
-                vv[j] = V ? pv[j] : 0ull;
-                d[j] = (uint32_t)((v[j] >> 32) >> dshift) & dmask;
-            }
-            if (t0 + TILE < r1) load(t0 + TILE);
-            WM_TILE_RANK(NJ)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                if (!live[j]) continue;
-                const uint32_t s = lofs[d[j]] + rk[j];
-                st[s] = v[j];
-                if (V) stv[s] = vv[j];
-                st_d[s] = (uint16_t)d[j];
-            }
-            wm_barrier();
-            const int m = (int)std::min<uint64_t>(TILE, r1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                const uint64_t p = lpos[dd] + (uint64_t)(s - (int)lofs[dd]);
-                out[p] = st[s];
-                if (V) outv[p] = stv[s];
-            }
-            wm_barrier();
-            lpos[tid] += c_;
-            cnt[tid] = 0;
-            wm_barrier();
-        }
-        __syncthreads();
-    }
-}
-
-// ---- placement: one output window at a time through LDS, rows written in order ---------------
-// The next window's pairs are loaded while this window is written out.  Rank functions: the low
-// 32 bits of a pair are the Int64 result.  Value functions (V): the low bit of a pair is the
-// validity, the value comes from `vals`; ESZ-byte values plus one validity byte per row.
-template <bool V, int ESZ>
-__global__ __launch_bounds__(kWmBlock) void k_wm_place(int64_t n, int wbits, const uint64_t *__restrict__ pairs,
-                                                       const uint64_t *__restrict__ vals, void *__restrict__ out,
-                                                       uint8_t *__restrict__ valid8) {
-    constexpr int WMAX = V ? (1 << 14) : (1 << 15), PER = WMAX / kWmBlock;
-    __shared__ uint32_t buf[V ? 1 : WMAX];
-    __shared__ uint64_t bufv[V ? WMAX : 1];
-    __shared__ uint8_t bufok[V ? WMAX : 1];
-    const int64_t W = (int64_t)1 << wbits;
-    const int64_t nw = (n + W - 1) >> wbits;
-    uint64_t px[PER], pv[PER];
-    auto load = [&](int64_t w) {
-        const int64_t r0 = w << wbits, r1 = std::min<int64_t>(n, r0 + W);
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int64_t i = r0 + j * kWmBlock + threadIdx.x;
-            px[j] = i < r1 ? pairs[i] : ~0ull;
-            if (V) pv[j] = i < r1 ? vals[i] : 0ull;
-        }
-    };
-    if ((int64_t)blockIdx.x < nw) load(blockIdx.x);
-    for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const int64_t r0 = w << wbits, r1 = std::min<int64_t>(n, r0 + W);
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            if (px[j] == ~0ull) continue;
-            const uint32_t at = (uint32_t)(px[j] >> 32) - (uint32_t)r0;
-            if (V) {
-                bufv[at] = pv[j];
-                bufok[at] = (uint8_t)(px[j] & 1u);
-            } else {
-                buf[at] = (uint32_t)px[j];
-            }
-        }
-        if (w + gridDim.x < nw) load(w + gridDim.x);
-        wm_barrier();
-        for (int64_t i = r0 + threadIdx.x; i < r1; i += kWmBlock) {
-            if (!V) {
-                ((int64_t *)out)[i] = (int64_t)buf[i - r0];
-            } else {
-                const uint8_t ok = bufok[i - r0];
-                if (ESZ == 8) ((uint64_t *)out)[i] = ok ? bufv[i - r0] : 0ull;
-                else ((uint32_t *)out)[i] = ok ? (uint32_t)bufv[i - r0] : 0u;
-                valid8[i] = ok;
-            }
-        }
-        wm_barrier();
-    }
-}
 
 // ---- id-free pipeline (rank functions): stable passes replayed in reverse -------------------
 // ROW_NUMBER / RANK / DENSE_RANK / NTILE carry no row ids.  Both partition passes rank a tile's
@@ -1665,149 +1190,7 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     if (const char *e = std::getenv("QEH_WM_G1X")) g1x = std::max(1, std::atoi(e));
     const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * g1x, (n + kWmTile - 1) / kWmTile));
     sh.span = ((n + g1 - 1) / g1 + kWmTile - 1) / kWmTile * kWmTile;
-    // output windows of 2^wbits rows (the placement's LDS image); pass 5a digits = row id bits
-    // above the window, in at most two levels of 10 bits
-    const int wbits = value_fn ? 14 : kWmWinBits;
-    int nbits = 0;
-    while (nbits < 63 && ((uint64_t)(n - 1) >> nbits)) ++nbits;
-    const int above = std::max(0, nbits - wbits);
-    const int d2 = std::max(0, above - 10);                 // pass-5b digit bits
-    if (d2 > 10) return kWindowMsdNotEligible;
-    const int win_shift = wbits + d2;                       // pass-5a digit = id >> win_shift
-    const int64_t nwin = ((n - 1) >> win_shift) + 1;
-    const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-
-    if (!std::getenv("QEH_WM_IDS")) return window_noid(ctx, func, part, order, asc, param, dflt, sh, out);
-    DevBuf cnt1, base1, key1, id1, kl1, key2, id2, pst, cnt5, base5, pa, pb, va, vb, valid8, flag;
-    const int64_t nc1 = (int64_t)kWmDig * g1;
-    const int nsort = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 4, sh.nparts));
-    const int64_t nc5 = (int64_t)kWmDig * nsort;
-    if (cnt1.alloc(ctx, nc1 * 4) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || id1.alloc(ctx, n * 4) ||
-        kl1.alloc(ctx, n * 2) || key2.alloc(ctx, n * 8) || id2.alloc(ctx, n * 4) || pst.alloc(ctx, (sh.nparts + 1) * 8) ||
-        cnt5.alloc(ctx, nc5 * 4) || base5.alloc(ctx, (nc5 + 1) * 8) || flag.alloc(ctx, 8))
-        return fail(QEH_E_OOM, "window: out of device memory");
-    const ColRef kc = make_colref(part), oc = make_colref(order);
-    const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
-    const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-    {
-        KernelTimer kt(ctx, "window_partition");
-        hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
-        QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
-        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? k_wm_pass1<4, 4> : k_wm_pass1<4, 8>) : (oes == 4 ? k_wm_pass1<8, 4> : k_wm_pass1<8, 8>),
-                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, base1.as<uint64_t>(),
-                           key1.as<uint64_t>(), id1.as<uint32_t>(), kl1.as<uint16_t>());
-    }
-    QEH_HIP(hipGetLastError());
-    // bucket starts = the scanned bases of workgroup 0 per digit, then n
-    DevBuf bst;
-    if (bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8)) return fail(QEH_E_OOM, "window: out of device memory");
-    QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb, pst.as<uint64_t>() + sh.nparts,
-                       (uint64_t)n);
-    {
-        KernelTimer kt(ctx, "window_partition");
-        hipLaunchKernelGGL(k_wm_pass2, dim3(std::min(cus, sh.nb)), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(),
-                           key1.as<uint64_t>(), id1.as<uint32_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
-                           id2.as<uint32_t>(), pst.as<uint64_t>());
-    }
-    QEH_HIP(hipGetLastError());
-    key1.reset();
-    id1.reset();
-    kl1.reset();
-    if (pa.alloc(ctx, n * 8) || pb.alloc(ctx, n * 8)) return fail(QEH_E_OOM, "window: out of device memory");
-    if (value_fn && (va.alloc(ctx, n * 8) || vb.alloc(ctx, n * 8) || valid8.alloc(ctx, n)))
-        return fail(QEH_E_OOM, "window: out of device memory");
-    QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
-    QEH_HIP(hipMemsetAsync(cnt5.p, 0, (size_t)nc5 * 4, ctx->stream));
-    WmFunc wf{};
-    wf.func = func;
-    wf.param = param;
-    wf.win_shift = win_shift;
-    wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
-    wf.odt = order.dtype;
-    wf.asc = asc ? 1 : 0;
-    wf.has_dflt = dflt != nullptr;
-    if (dflt) wf.dflt = esz == 8 ? *dflt : (int64_t)(uint32_t)*dflt;
-    {
-        KernelTimer kt(ctx, "window_sort");
-#define QEH_WM_SORT(BIG, VF)                                                                                         \
-    hipLaunchKernelGGL((k_wm_sort<BIG, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf, pst.as<uint64_t>(), \
-                       key2.as<uint64_t>(), id2.as<uint32_t>(), pa.as<uint64_t>(), va.as<uint64_t>(), cnt5.as<uint32_t>(), \
-                       flag.as<uint32_t>())
-        if (value_fn) {
-            QEH_WM_SORT(false, true);
-            QEH_WM_SORT(true, true);
-        } else {
-            QEH_WM_SORT(false, false);
-            QEH_WM_SORT(true, false);
-        }
-#undef QEH_WM_SORT
-    }
-    QEH_HIP(hipGetLastError());
-    uint32_t too_big = 0;
-    QEH_TRY(read_small(ctx, &too_big, flag.p, 4));
-    if (too_big) return kWindowMsdNotEligible;  // a group above 2048 rows / a long tie run: the LSD path
-    key2.reset();
-    id2.reset();
-    QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
-    {
-        KernelTimer kt(ctx, "window_place");
-        const uint64_t *placed = pa.as<uint64_t>(), *placed_v = va.as<uint64_t>();
-        if (nwin > 1) {
-            QEH_TRY(exclusive_scan_u32(ctx, cnt5.as<uint32_t>(), base5.as<uint64_t>(), nc5, nullptr));
-            if (value_fn)
-                hipLaunchKernelGGL((k_wm_pass5<false, true>), dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh,
-                                   nsort, win_shift, wbits, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(),
-                                   va.as<uint64_t>(), pb.as<uint64_t>(), vb.as<uint64_t>());
-            else
-                hipLaunchKernelGGL((k_wm_pass5<false, false>), dim3(std::min(cus, nsort)), dim3(kWmBlock), 0, ctx->stream, sh,
-                                   nsort, win_shift, wbits, nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pa.as<uint64_t>(),
-                                   nullptr, pb.as<uint64_t>(), nullptr);
-            placed = pb.as<uint64_t>();
-            placed_v = vb.as<uint64_t>();
-            if (d2 > 0) {
-                const dim3 g5((unsigned)std::min<int64_t>(cus, nwin));
-                if (value_fn)
-                    hipLaunchKernelGGL((k_wm_pass5<true, true>), g5, dim3(kWmBlock), 0, ctx->stream, sh, nsort, win_shift, wbits,
-                                       nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pb.as<uint64_t>(), vb.as<uint64_t>(),
-                                       pa.as<uint64_t>(), va.as<uint64_t>());
-                else
-                    hipLaunchKernelGGL((k_wm_pass5<true, false>), g5, dim3(kWmBlock), 0, ctx->stream, sh, nsort, win_shift, wbits,
-                                       nwin, pst.as<uint64_t>(), base5.as<uint64_t>(), pb.as<uint64_t>(), nullptr,
-                                       pa.as<uint64_t>(), nullptr);
-                placed = pa.as<uint64_t>();
-                placed_v = va.as<uint64_t>();
-            }
-        }
-        const int64_t nw = (n + ((int64_t)1 << wbits) - 1) >> wbits;
-        const dim3 gp((unsigned)std::min<int64_t>((int64_t)cus * 2, nw));
-        if (!value_fn)
-            hipLaunchKernelGGL((k_wm_place<false, 8>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, nullptr, out->values,
-                               nullptr);
-        else if (esz == 8)
-            hipLaunchKernelGGL((k_wm_place<true, 8>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, placed_v, out->values,
-                               valid8.as<uint8_t>());
-        else
-            hipLaunchKernelGGL((k_wm_place<true, 4>), gp, dim3(kWmBlock), 0, ctx->stream, n, wbits, placed, placed_v, out->values,
-                               valid8.as<uint8_t>());
-    }
-    if (hipGetLastError() != hipSuccess) {
-        qeh_column_release(ctx, out);
-        return fail(QEH_E_HIP, "window: kernel launch failed");
-    }
-    if (value_fn) {
-        const int st = qeh_bytes_to_validity(ctx, valid8.as<uint8_t>(), n, out->validity);
-        if (st != QEH_OK) {
-            qeh_column_release(ctx, out);
-            return st;
-        }
-        out->null_count = -1;
-    }
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
-        qeh_column_release(ctx, out);
-        return fail(QEH_E_HIP, "window: stream synchronize failed");
-    }
-    return QEH_OK;
+    return window_noid(ctx, func, part, order, asc, param, dflt, sh, out);
 }
 
 }  // namespace qeh
