@@ -280,7 +280,8 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
             longest = std::max<int64_t>(longest, cols[i0 + q].length);
         }
         if (longest > 0)
-            hipLaunchKernelGGL(k_key_minmax_n, dim3(grid_for(ctx, longest, kBlock * 8, 1), nc), dim3(kBlock), 0, ctx->stream, j,
+            // four workgroups per CU: 64 KB of loads in flight per CU (one left the 1e9-row key at ~5 TB/s)
+            hipLaunchKernelGGL(k_key_minmax_n, dim3(grid_for(ctx, longest, kBlock * 8, 4), nc), dim3(kBlock), 0, ctx->stream, j,
                                mm.as<MinMax>() + i0);
     }
     QEH_HIP(hipGetLastError());
