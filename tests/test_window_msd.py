@@ -172,3 +172,33 @@ def test_msd_window_clustered_big_groups(ctx, monkeypatch, func, param):
     v[:700] = r.integers(0, 3, 700)
     got, want, ran = _run(ctx, func, k, v, True, param)
     assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param,default", [(W.Lag, 1, None), (W.Lead, 2, 9), (W.FirstValue, 0, None),
+                                                (W.LastValue, 0, None)])
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_value_functions_big_and_clustered_groups(ctx, monkeypatch, func, param, default, asc):
+    """Value functions over groups of 1025..2048 rows (the 2048-row counting sort), clustered groups
+    of both size classes (the network kernels' queue) and small spread groups, in one call."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(29)
+    n = 400_000
+    k = r.integers(0, 260, n).astype(np.int64)  # ~1540 rows per group
+    v = r.integers(-(2 ** 50), 2 ** 50, n).astype(np.int64)
+    v[k < 60] = r.integers(-20, 20, int((k < 60).sum()))  # clustered big groups
+    small = r.random(n) < 0.02
+    k[small] = 1000 + r.integers(0, 40, int(small.sum()))  # small groups, half of them clustered
+    v[small & (k < 1020)] = r.integers(0, 5, int((small & (k < 1020)).sum()))
+    d = None if default is None else np.int64(default)
+    ctx.timing(True)
+    ctx.timing_reset()
+    dv = ctx.upload(v)
+    got_v, got_m = ctx.window(func, [ctx.upload(k)], [dv], [asc], arg=dv, param=param, default=d).to_numpy()
+    ran = _msd_ran(ctx)
+    ctx.timing(False)
+    want_v, want_m = ob.window(func, [ob.HostCol(k)], [ob.HostCol(v)], [asc], arg=ob.HostCol(v), param=param,
+                               default=d)
+    assert ran
+    assert np.array_equal(got_m, want_m)
+    assert np.array_equal(got_v[want_m], want_v[want_m])
