@@ -26,18 +26,53 @@ struct MinMax {
 
 __device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, MinMax *out);
 
-__global__ __launch_bounds__(kBlock) void k_key_minmax(ColRef key, int64_t n, MinMax *out) { key_minmax_body(key, n, out); }
-
-// Several columns in one launch (blockIdx.y = column); k_minmax_init_n initialises their slots.
+// Several columns in one launch (blockIdx.y = column): each workgroup writes its partial to
+// part[column * gridDim.x + workgroup] and k_minmax_final reduces them -- same-address atomics from
+// every workgroup serialise at ~12 ns each (MI355X_MICROARCH.md, fanin), 74 us for 2 x 1024
+// workgroups against the 20 us the two 1e7-row build columns take to read.
 constexpr int kMinMaxCols = 4;
 struct MinMaxJob {
     ColRef c[kMinMaxCols];
     int64_t n[kMinMaxCols];
 };
-__global__ __launch_bounds__(kBlock) void k_key_minmax_n(MinMaxJob j, MinMax *out) {
-    key_minmax_body(j.c[blockIdx.y], j.n[blockIdx.y], out + blockIdx.y);
+__global__ __launch_bounds__(kBlock) void k_key_minmax_n(MinMaxJob j, MinMax *part) {
+    key_minmax_body(j.c[blockIdx.y], j.n[blockIdx.y], part + (int64_t)blockIdx.y * gridDim.x + blockIdx.x);
 }
 
+// blockIdx.x = column: reduce its nb partials into out[column]
+__global__ __launch_bounds__(kBlock) void k_minmax_final(const MinMax *__restrict__ part, int nb, MinMax *__restrict__ out) {
+    __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
+    __shared__ uint64_t scnt[kBlock / 64];
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    uint64_t cnt = 0;
+    for (int i = threadIdx.x; i < nb; i += kBlock) {
+        const MinMax q = part[(int64_t)blockIdx.x * nb + i];
+        mn = q.mn < mn ? q.mn : mn;
+        mx = q.mx > mx ? q.mx : mx;
+        cnt += q.cnt;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        const uint64_t c = __shfl_xor(cnt, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+        cnt += c;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) smn[w] = mn, smx[w] = mx, scnt[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < kBlock / 64; ++i) {
+            mn = smn[i] < mn ? smn[i] : mn;
+            mx = smx[i] > mx ? smx[i] : mx;
+            cnt += scnt[i];
+        }
+        out[blockIdx.x] = MinMax{mn, mx, cnt, 0u};
+    }
+}
+
+// One workgroup's (min, max, valid count) over its share of the rows, stored at *out.
 __device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, MinMax *out) {
     __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
     __shared__ uint64_t scnt[kBlock / 64];
@@ -87,34 +122,16 @@ __device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, Mi
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) smn[w] = mn, smx[w] = mx, scnt[w] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) {  // one set of atomics per workgroup
+    if (threadIdx.x == 0) {
         for (int i = 1; i < kBlock / 64; ++i) {
             mn = smn[i] < mn ? smn[i] : mn;
             mx = smx[i] > mx ? smx[i] : mx;
             cnt += scnt[i];
         }
-        atomicMin((long long *)&out->mn, (long long)mn);
-        atomicMax((long long *)&out->mx, (long long)mx);
-        atomicAdd((unsigned long long *)&out->cnt, (unsigned long long)cnt);
+        *out = MinMax{mn, mx, cnt, 0u};
     }
 }
 
-__global__ void k_minmax_init(MinMax *m) {
-    m->mn = INT64_MAX;
-    m->mx = INT64_MIN;
-    m->cnt = 0;
-    m->bad = 0;
-}
-
-__global__ void k_minmax_init_n(MinMax *m, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        m[i].mn = INT64_MAX;
-        m[i].mx = INT64_MIN;
-        m[i].cnt = 0;
-        m[i].bad = 0;
-    }
-}
 
 // ---- inserts -------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t payload_of(const RowPayload &rp, int64_t row) {
@@ -266,10 +283,13 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
     bool all = true;
     for (int i = 0; i < n && all; ++i) all = memo_get(ctx, cols[i], &mn[i], &mx[i], &valid[i]);
     if (all) return QEH_OK;
-    DevBuf mm;
+    DevBuf mm, part;
     QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
-    // one init and one reduction launch per group of up to four columns (blockIdx.y = column)
-    hipLaunchKernelGGL(k_minmax_init_n, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, mm.as<MinMax>(), n);
+    // one partial-reduction launch per group of up to four columns (blockIdx.y = column), then one
+    // final reduction per group; four workgroups per CU on long columns (64 KB of loads in flight
+    // per CU), one per CU below 2^26 rows
+    const int cus = ctx->props.multiProcessorCount;
+    QEH_TRY(part.alloc(ctx, sizeof(MinMax) * (size_t)kMinMaxCols * cus * 4));
     for (int i0 = 0; i0 < n; i0 += kMinMaxCols) {
         MinMaxJob j{};
         int64_t longest = 0;
@@ -279,10 +299,10 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
             j.n[q] = cols[i0 + q].length;
             longest = std::max<int64_t>(longest, cols[i0 + q].length);
         }
-        if (longest > 0)
-            // four workgroups per CU: 64 KB of loads in flight per CU (one left the 1e9-row key at ~5 TB/s)
-            hipLaunchKernelGGL(k_key_minmax_n, dim3(grid_for(ctx, longest, kBlock * 8, 4), nc), dim3(kBlock), 0, ctx->stream, j,
-                               mm.as<MinMax>() + i0);
+        const int nb = grid_for(ctx, std::max<int64_t>(longest, 1), kBlock * 8, longest >= ((int64_t)1 << 26) ? 4 : 1);
+        hipLaunchKernelGGL(k_key_minmax_n, dim3(nb, nc), dim3(kBlock), 0, ctx->stream, j, part.as<MinMax>());
+        hipLaunchKernelGGL(k_minmax_final, dim3(nc), dim3(kBlock), 0, ctx->stream, part.as<MinMax>(), nb,
+                           mm.as<MinMax>() + i0);
     }
     QEH_HIP(hipGetLastError());
     std::vector<MinMax> hm((size_t)n);
