@@ -1271,6 +1271,62 @@ __global__ void k_states_reduce(uint64_t *states, int64_t G, AggSpecs specs) {
     }
 }
 
+// Small group tables (G <= kCompactSmallG): fold the shard copies, flag the non-empty groups and
+// scan the flags in one workgroup -- one launch where the general path takes five (reduce,
+// flags, three scan kernels), ~4-5 us per dependent launch on the query's critical path.
+// pos[g] = non-empty groups before g; the count lands in total (the status words).
+constexpr int kCompactSmallG = 16384;
+__global__ __launch_bounds__(1024) void k_states_compact_small(uint64_t *__restrict__ states, int64_t Gs, int64_t G,
+                                                              AggSpecs specs, uint64_t *__restrict__ pos,
+                                                              uint64_t *__restrict__ total) {
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (specs.shards > 1) {
+        const int64_t words = (int64_t)specs.n_slots * Gs;
+        for (int64_t i = t; i < words; i += 1024) {
+            const int64_t slot = i / Gs;
+            int kind = -1;  // counts
+            for (int a = 0; a < specs.n; ++a)
+                if (specs.a[a].val_slot == slot) kind = specs.a[a].kind;
+            uint64_t acc = states[i];
+            for (int sh0 = 1; sh0 < specs.shards; sh0 += 4) {  // four shard loads in flight
+                uint64_t v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = sh0 + q < specs.shards ? states[i + (sh0 + q) * words] : 0ull;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (sh0 + q >= specs.shards) break;
+                    switch (kind) {
+                        case AK_SUM_F: acc = __builtin_bit_cast(uint64_t, as_f64(acc) + as_f64(v[q])); break;
+                        case AK_MIN: acc = (int64_t)v[q] < (int64_t)acc ? v[q] : acc; break;
+                        case AK_MAX: acc = (int64_t)v[q] > (int64_t)acc ? v[q] : acc; break;
+                        default: acc += v[q]; break;  // counts, wrapping int sums
+                    }
+                }
+            }
+            states[i] = acc;
+        }
+        __syncthreads();  // the row counts (slot 0) are folded before they are flagged
+    }
+    // thread t owns groups [t * per, (t + 1) * per)
+    const int64_t per = (G + 1023) / 1024, g0 = (int64_t)t * per, g1 = g0 + per < G ? g0 + per : G;
+    uint32_t c = 0;
+    for (int64_t g = g0; g < g1; ++g) c += states[g] != 0;
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - c, all = 0;
+    for (int w = 0; w < 16; ++w) {
+        base += w < wave ? wsum[w] : 0u;
+        all += wsum[w];
+    }
+    for (int64_t g = g0; g < g1; ++g) {
+        pos[g] = base;
+        base += states[g] != 0;
+    }
+    if (t == 0) *total = all;
+}
+
 // ---- finalize ------------------------------------------------------------------------
 __global__ void k_group_nonempty(const uint64_t *states, int64_t G, uint32_t *flags) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x)
@@ -2221,8 +2277,10 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         else launch_agg_rows<GM_GROUP>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>());
     }
     QEH_HIP(hipGetLastError());
+    // small tables with empty groups dropped: shards folded, flagged and scanned in compact() below
+    const bool small = drop_empty && G > 0 && Gs <= kCompactSmallG;
     auto reduce_shards = [&]() {
-        if (specs.shards > 1)
+        if (specs.shards > 1 && !small)
             hipLaunchKernelGGL(k_states_reduce, dim3(grid_for(ctx, specs.n_slots * Gs, kBlock, 8)), dim3(kBlock), 0,
                                ctx->stream, states.as<uint64_t>(), Gs, specs);
     };
@@ -2244,6 +2302,11 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     }
     auto compact = [&]() -> int {
         if (!posp) return QEH_OK;
+        if (small) {
+            hipLaunchKernelGGL(k_states_compact_small, dim3(1), dim3(1024), 0, ctx->stream, states.as<uint64_t>(), Gs, G,
+                               specs, pos.as<uint64_t>(), (uint64_t *)(errw.as<uint32_t>() + 2));
+            return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: compact launch failed");
+        }
         hipLaunchKernelGGL(k_group_nonempty, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
                            states.as<uint64_t>(), Gs, flags.as<uint32_t>());
         return exclusive_scan_u32_dev(ctx, flags.as<uint32_t>(), pos.as<uint64_t>(), G, (uint64_t *)(errw.as<uint32_t>() + 2));
