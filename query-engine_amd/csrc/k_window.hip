@@ -157,13 +157,16 @@ struct WmFunc {
 // Value functions at sorted index i of a group of m rows: the source row's sorted index (false when
 // the offset leaves the partition; LAST_VALUE spans the whole partition, as the reference's frame).
 __device__ __forceinline__ bool wm_value_src(const WmFunc &f, int i, int m, int &js) {
+    js = i;  // (param >= 0, checked by qeh_window; js is formed only inside the partition)
     if (f.func == QEH_WIN_LAG) {
+        if (f.param > i) return false;
         js = (int)(i - f.param);
-        return f.param <= i;
+        return true;
     }
     if (f.func == QEH_WIN_LEAD) {
+        if (f.param >= (int64_t)m - i) return false;
         js = (int)(i + f.param);
-        return f.param < (int64_t)m - i;
+        return true;
     }
     js = f.func == QEH_WIN_FIRST_VALUE ? 0 : m - 1;
     return true;

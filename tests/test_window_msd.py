@@ -202,3 +202,21 @@ def test_msd_value_functions_big_and_clustered_groups(ctx, monkeypatch, func, pa
     assert ran
     assert np.array_equal(got_m, want_m)
     assert np.array_equal(got_v[want_m], want_v[want_m])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.Lead, 2 ** 62), (W.Lag, 2 ** 62), (W.Lead, 0), (W.Lag, 5000)])
+def test_msd_value_functions_extreme_offsets(ctx, monkeypatch, func, param):
+    """Offsets far past every partition (all NULL / default) and offset 0 (the row itself)."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(31)
+    n = 100_000
+    k = r.integers(0, 300, n).astype(np.int64)
+    v = r.integers(-(2 ** 40), 2 ** 40, n).astype(np.int64)
+    for d in (None, np.int64(-7)):
+        dv = ctx.upload(v)
+        got_v, got_m = ctx.window(func, [ctx.upload(k)], [dv], [True], arg=dv, param=param, default=d).to_numpy()
+        want_v, want_m = ob.window(func, [ob.HostCol(k)], [ob.HostCol(v)], [True], arg=ob.HostCol(v), param=param,
+                                   default=d)
+        assert np.array_equal(got_m, want_m)
+        assert np.array_equal(got_v[want_m], want_v[want_m])
