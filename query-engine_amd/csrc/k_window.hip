@@ -671,7 +671,7 @@ struct WmGroupLds {
 };
 
 template <int E, bool VF>
-__global__ __launch_bounds__(256) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
+__global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                       const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
                                                       uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big) {
     constexpr int P = 256 * E, NB = E == 4 ? 11 : 12, LO = E == 4 ? 0 : 1024;  // groups of (LO, P] rows
