@@ -378,6 +378,10 @@ class DistributedExecutor:
         return self.ctx.hash_join_inner(p[probe_key_idx], p, b[build_key_idx], b)
 
     def _final(self, keys: Sequence[DeviceColumn], partials: Sequence[DeviceColumn], aggs: Sequence[Tuple[int, int]]):
+        if self.world == 1:
+            # one rank: the shuffle is the identity and every group's partial state is already its
+            # only one (the local aggregate emits each group once), so the final merge is the identity
+            return list(keys), list(partials), len(keys[0]) if keys else 0
         shuffled = self.shuffle(keys[0], list(keys) + list(partials))
         nk = len(keys)
         fk, fa, g = self.ctx.hash_aggregate(shuffled[:nk], shuffled[nk:],
@@ -606,8 +610,8 @@ class DistributedExecutor:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
         if self.world == 1:
-            # one partition: both hash exchanges are the identity, so the plan is the local fused
-            # operator on this rank's rows (its partial states still go through the final stage)
+            # one partition: both hash exchanges and the final merge are the identity, so the plan
+            # is the local fused operator on this rank's rows
             pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
                                                         build_group_keys, aggs)
             if g == 0:
