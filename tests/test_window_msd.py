@@ -220,3 +220,41 @@ def test_msd_value_functions_extreme_offsets(ctx, monkeypatch, func, param):
                                    default=d)
         assert np.array_equal(got_m, want_m)
         assert np.array_equal(got_v[want_m], want_v[want_m])
+
+
+@pytest.mark.gpu
+def test_row_number_full_size_properties(ctx):
+    """BASELINE config 5 at its full size (ROW_NUMBER() OVER (PARTITION BY k ORDER BY v), 1e9 rows,
+    k in [0, 2^20), generated in HBM), checked against independent torch computations on the
+    device: every group's numbers sum to m(m+1)/2 and lie in [1, m] (m = the group's row count from
+    bincount), and for 64 sampled groups the numbers equal those of a stable sort by (k, v, row)."""
+    import torch
+    from qe_hip import abi
+    from qe_hip.distributed import TYPESTR, _DeviceView
+    n, parts = 1_000_000_000, 1 << 20
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 7, n, parts)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    rn = ctx.row_number([k], [v], [True])
+
+    def view(col):
+        return torch.as_tensor(_DeviceView(col.c.values, len(col), TYPESTR[col.dtype], col), device="cuda")
+
+    tk, tv, tr = view(k), view(v), view(rn)
+    m = torch.bincount(tk, minlength=parts)
+    assert int(m.sum()) == n
+    assert int(tr.min()) >= 1 and bool((tr <= m[tk]).all())
+    assert int(tr.sum()) == int((m * (m + 1) // 2).sum())
+    sample = torch.randperm(parts, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))[:64]
+    idx = torch.nonzero(torch.isin(tk, sample)).squeeze(1)  # ascending row order
+    sk, sv = tk[idx], tv[idx]
+    o1 = torch.argsort(sv, stable=True)          # by v, ties by row
+    o2 = torch.argsort(sk[o1], stable=True)      # then by k
+    order = o1[o2]
+    ks = sk[order]
+    starts = torch.ones_like(ks, dtype=torch.bool)
+    starts[1:] = ks[1:] != ks[:-1]
+    pos = torch.arange(len(ks), device="cuda")
+    first = torch.cummax(torch.where(starts, pos, torch.zeros_like(pos)), 0).values
+    want = torch.empty_like(pos)
+    want[order] = pos - first + 1
+    assert torch.equal(tr[idx], want)
