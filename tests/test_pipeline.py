@@ -318,3 +318,33 @@ def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
                                           [ob.HostCol(dg)], AGGS)
     assert g == wg
     assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+def test_inner_join_full_size_properties(ctx):
+    """BASELINE config 3 at its full size (INNER join of 1e9 fact rows x 1e7 dim rows materialising
+    (f.v, d.a), generated in HBM; the slice path, rows in slice order), against independent torch
+    computations on the device: every fact row matches once (the dim keys are a permutation), the
+    output's Σ a equals Σ over fact rows of a[k] from a direct-indexed table, and the pairing of each
+    output v with its a holds (Σ a * (bits(v) & 0xFFFF) is exact in int64)."""
+    import torch
+    from qe_hip.distributed import TYPESTR, _DeviceView
+    n, nd = 1_000_000_000, 10_000_000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    fv = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, 1000)
+    p, b, rows = ctx.hash_join_inner(fk, [fv], dk, [da])
+    assert rows == n
+
+    def view(col, dt=None):
+        return torch.as_tensor(_DeviceView(col.c.values, len(col), TYPESTR[dt or col.dtype], col), device="cuda")
+
+    table = torch.empty(nd, dtype=torch.int64, device="cuda")
+    table[view(dk)] = view(da)
+    a_in = table[view(fk)]
+    a_out = view(b[0])
+    assert int(a_out.sum()) == int(a_in.sum())
+    lo_in = view(fv, abi.DT_INT64) & 0xFFFF
+    lo_out = view(p[0], abi.DT_INT64) & 0xFFFF
+    assert int((a_out * lo_out).sum()) == int((a_in * lo_in).sum())
