@@ -670,7 +670,10 @@ struct WmGroupLds {
     uint32_t ws[4], wf[4], wc[4], wt[4];
 };
 
-template <int E, bool VF>
+// FN: the window function as a compile-time constant (QEH_WIN_ROW_NUMBER .. NTILE; -1 = the value
+// functions, selected by f.func at run time) -- the per-row dispatch left a third of the kernel's
+// instructions scalar.
+template <int E, int FN>
 __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                       const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
                                                       uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big) {
@@ -815,7 +818,7 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
             const uint32_t x = live ? L.k[wm_pad(i)] : 0u;
             pos[r] = x & 4095u;
             rv[r] = 0u;
-            if (VF) {  // (valid flag, value bits of the source row at pos)
+            if constexpr (FN < 0) {  // (valid flag, value bits of the source row at pos)
                 int js;
                 const bool ok = wm_value_src(f, i, m, js);
                 uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
@@ -825,16 +828,16 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
                     rv[r] = 1u;
                 }
                 if (live) f.vout[s + pos[r]] = bits;
-            } else if (f.func == QEH_WIN_ROW_NUMBER) {
+            } else if constexpr (FN == QEH_WIN_ROW_NUMBER) {
                 rv[r] = (uint32_t)i + 1u;
-            } else if (f.func == QEH_WIN_NTILE) {
+            } else if constexpr (FN == QEH_WIN_NTILE) {
                 const int64_t q = m / f.param, rm = m % f.param, r0 = i;
                 rv[r] = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
             } else {
                 const uint64_t ov = live ? L.ov[x >> 12] : 0ull;
                 const uint64_t pv = (live && i > 0) ? L.ov[L.k[wm_pad(i - 1)] >> 12] : 0ull;
                 const uint32_t flag = (live && (i == 0 || pv != ov)) ? 1u : 0u;
-                if (f.func == QEH_WIN_RANK) {  // index of the last peer-group start at or before i
+                if constexpr (FN == QEH_WIN_RANK) {  // index of the last peer-group start at or before i
                     uint32_t v = flag ? (uint32_t)i : 0u;
 #pragma unroll
                     for (int d = 1; d < 64; d <<= 1) {
@@ -851,15 +854,15 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
                 }
             }
         }
-        if (f.func == QEH_WIN_RANK || f.func == QEH_WIN_DENSE_RANK) {  // (uniform) carries across waves
+        if constexpr (FN == QEH_WIN_RANK || FN == QEH_WIN_DENSE_RANK) {  // carries across waves
             if (lane == 0) L.wt[wave] = carry;
             wm_barrier();
             uint32_t c = 0;
 #pragma unroll
             for (int v = 0; v < 3; ++v)
-                if (v < wave) c = f.func == QEH_WIN_RANK ? max(c, L.wt[v]) : c + L.wt[v];
+                if (v < wave) c = FN == QEH_WIN_RANK ? max(c, L.wt[v]) : c + L.wt[v];
 #pragma unroll
-            for (int r = 0; r < E; ++r) rv[r] = f.func == QEH_WIN_RANK ? max(rv[r], c) + 1u : rv[r] + c;
+            for (int r = 0; r < E; ++r) rv[r] = FN == QEH_WIN_RANK ? max(rv[r], c) + 1u : rv[r] + c;
         }
 #pragma unroll
         for (int r = 0; r < E; ++r)
@@ -1091,12 +1094,20 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
             // the network for the queued (clustered) groups of both size classes
             const int64_t ncs = std::max<int64_t>(std::min<int64_t>((int64_t)cus * 16, sh.nparts),
                                                   (sh.nparts + kWmCsMaxG - 1) / kWmCsMaxG);
-            hipLaunchKernelGGL((k_wm2_csort_wg<4, VF>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
-                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
-                               flag.as<uint32_t>());
-            hipLaunchKernelGGL((k_wm2_csort_wg<8, VF>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
-                               pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
-                               flag.as<uint32_t>());
+            auto csort = [&](auto fn) {
+                constexpr int FN = decltype(fn)::value;
+                hipLaunchKernelGGL((k_wm2_csort_wg<4, FN>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                                   flag.as<uint32_t>());
+                hipLaunchKernelGGL((k_wm2_csort_wg<8, FN>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                                   flag.as<uint32_t>());
+            };
+            if (VF) csort(std::integral_constant<int, -1>{});
+            else if (func == QEH_WIN_ROW_NUMBER) csort(std::integral_constant<int, QEH_WIN_ROW_NUMBER>{});
+            else if (func == QEH_WIN_RANK) csort(std::integral_constant<int, QEH_WIN_RANK>{});
+            else if (func == QEH_WIN_DENSE_RANK) csort(std::integral_constant<int, QEH_WIN_DENSE_RANK>{});
+            else csort(std::integral_constant<int, QEH_WIN_NTILE>{});
             hipLaunchKernelGGL((k_wm2_sort<false, true, VF>), dim3(nsort), dim3(kWmSortBlock), 0, ctx->stream, sh, wf,
                                pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), flag.as<uint32_t>(),
                                fbl.as<uint32_t>());
