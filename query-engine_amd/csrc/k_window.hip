@@ -278,9 +278,9 @@ __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], cons
         uint64_t m = __ballot(live[j]);
 #pragma unroll
         for (int b = 0; b < (DB >= 0 ? DB : dbits); ++b) {
-            const uint32_t bit = (d[j] >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            const uint32_t rep = 0u - bit;  // all ones where the lane's bit is set
+            // all ones where the lane's bit b is set (one signed bitfield extract)
+            const uint32_t rep = (uint32_t)(__builtin_amdgcn_sbfe((int32_t)d[j], b, 1));
+            const uint64_t bb = __ballot(rep != 0u);
             m &= ~(bb ^ (((uint64_t)rep << 32) | rep));  // lanes whose bit b equals this lane's
         }
         const uint64_t below = m & below_mask;
