@@ -321,12 +321,12 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
                                                         const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
                                                         uint16_t *__restrict__ o_kl) {
     __shared__ WmRankLds R;
-    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
     __shared__ uint16_t st_kl[kWmTile], st_d[kWmTile];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
+    lpos[tid] = (uint32_t)base[(int64_t)tid * gridDim.x + blockIdx.x];
     __syncthreads();
     const int dbits = wm_digit_bits(sh.nb);
     const uint32_t lmask = (1u << sh.lb) - 1u;
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
-            const uint64_t p = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+            const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
             o_key[p] = st_key[s];
             o_kl[p] = st_kl[s];
         }
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
                                                         uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart) {
     __shared__ WmRankLds R;
-    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
     __shared__ uint16_t st_d[kWmTile];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             const uint32_t ex = block_excl_scan1024(R.lofs[tid], R.wsum);
             const int64_t part = (int64_t)b * L + tid;
             if (tid < L && part < sh.nparts) pstart[part] = (uint64_t)(s0 + ex);
-            lpos[tid] = (uint64_t)(s0 + ex);
+            lpos[tid] = (uint32_t)(s0 + ex);
         }
         __syncthreads();
         uint64_t kx[NJ];
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
-                o_key[lpos[dd] + (uint64_t)(s - (int)R.lofs[dd])] = st_key[s];
+                o_key[lpos[dd] + (uint32_t)s - R.lofs[dd]] = st_key[s];
             }
             wm_barrier();
             lpos[tid] += tcnt;
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
                                                        const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1,
                                                        const uint64_t *__restrict__ res2v, uint64_t *__restrict__ res1v) {
     __shared__ WmRankLds R;
-    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
     __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -899,7 +899,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
         {
             const int64_t part = (int64_t)b * L + tid;
-            lpos[tid] = (tid < L && part < sh.nparts) ? pstart[part] : 0ull;
+            lpos[tid] = (tid < L && part < sh.nparts) ? (uint32_t)pstart[part] : 0u;
         }
         __syncthreads();
         uint32_t lx[NJ];
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
-                const uint64_t src = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+                const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
                 st_r[s] = res2[src];
                 if (VAL) st_v[s] = res2v[src];
             }
@@ -956,12 +956,12 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
                                                        const uint16_t *__restrict__ res1, void *__restrict__ out,
                                                        const uint64_t *__restrict__ res1v, uint8_t *__restrict__ valid8) {
     __shared__ WmRankLds R;
-    __shared__ uint64_t lpos[kWmDig];
+    __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
     __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    lpos[tid] = base[(int64_t)tid * gridDim.x + blockIdx.x];
+    lpos[tid] = (uint32_t)base[(int64_t)tid * gridDim.x + blockIdx.x];
     __syncthreads();
     const int dbits = wm_digit_bits(sh.nb);
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
-            const uint64_t src = lpos[dd] + (uint64_t)(s - (int)R.lofs[dd]);
+            const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
             st_r[s] = res1[src];
             if (VAL) st_v[s] = res1v[src];
         }
