@@ -272,7 +272,6 @@ __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], cons
     for (int i = lane; i < kWmDig / 2; i += 64) wz[i] = 0u;
     wm_wave_sync();
     uint32_t r[NJ];
-    const uint64_t below_mask = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         uint64_t m = __ballot(live[j]);
@@ -283,14 +282,13 @@ __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], cons
             const uint64_t bb = __ballot(rep != 0u);
             m &= ~(bb ^ (((uint64_t)rep << 32) | rep));  // lanes whose bit b equals this lane's
         }
-        const uint64_t below = m & below_mask;
-        uint32_t old = 0;
-        if (live[j] && below == 0) {
-            old = R.wc[wave][d[j]];
-            R.wc[wave][d[j]] = (uint16_t)(old + (uint32_t)__popcll(m));
-        }
-        const int leader = live[j] ? __ffsll((long long)m) - 1 : lane;
-        r[j] = (uint32_t)__shfl((int)old, leader, 64) + (uint32_t)__popcll(below);
+        // every lane of a digit reads the digit's count (one LDS read, no broadcast from a leader);
+        // the digit's lowest lane then adds the digit's row count (the read instruction precedes
+        // the write in the wave's LDS order)
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t old = live[j] ? (uint32_t)R.wc[wave][d[j]] : 0u;
+        if (live[j] && below == 0) R.wc[wave][d[j]] = (uint16_t)(old + (uint32_t)__popcll(m));
+        r[j] = old + below;
         wm_wave_sync();
     }
     wm_barrier();
