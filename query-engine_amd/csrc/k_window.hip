@@ -364,6 +364,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
         }
         wm_barrier();
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+#pragma unroll 8
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
             const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
@@ -446,7 +447,8 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             }
             wm_barrier();
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
+    #pragma unroll 8
+        for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
                 o_key[lpos[dd] + (uint32_t)s - R.lofs[dd]] = st_key[s];
             }
@@ -924,7 +926,8 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
                 if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
             wm_barrier();
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
+    #pragma unroll 8
+        for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
                 const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
                 st_r[s] = res2[src];
@@ -988,6 +991,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
             if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
         wm_barrier();
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+#pragma unroll 8
         for (int s = tid; s < m; s += kWmBlock) {
             const uint32_t dd = st_d[s];
             const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
