@@ -419,6 +419,40 @@ int qo_filter(const qo_col *cols, int n_cols, const qeh_expr_node *nodes, int n_
 }
 
 /* ---- hashing of key tuples ----------------------------------------------- */
+static uint64_t mix(uint64_t k);
+
+/* partition.rs:151-212: per row, compute_row_hash (:292-316, NULL cells skip the hasher) and push
+ * the row onto partition (hash % n); the partitions are then taken in order (partition-major,
+ * input order inside each).  Hash: the device's (k_hash_ids_multi in k_sort.hip). */
+int qo_partition_hash(const qo_col *keys, int n_keys, int n_parts, int64_t *counts, uint32_t *out_perm) {
+    if (n_keys < 1 || n_parts < 1) return err(QEH_E_INVALID, "qo_partition_hash: bad argument");
+    const int64_t n = keys[0].length;
+    for (int j = 0; j < n_keys; ++j)
+        if (keys[j].dtype != QEH_DT_INT64 && keys[j].dtype != QEH_DT_INT32)
+            return err(QEH_E_UNSUPPORTED, "qo_partition_hash: Int32 / Int64 keys only");
+    uint32_t *part = malloc((size_t)(n > 0 ? n : 1) * sizeof(uint32_t));
+    for (int p = 0; p < n_parts; ++p) counts[p] = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (int j = 0; j < n_keys; ++j) {
+            const qo_col *c = &keys[j];
+            if (c->valid && !c->valid[r]) continue;
+            uint64_t v = c->dtype == QEH_DT_INT64 ? (uint64_t)((const int64_t *)c->values)[r]
+                                                  : (uint64_t)(int64_t)((const int32_t *)c->values)[r];
+            h = mix(h ^ (mix(v) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+        }
+        part[r] = (uint32_t)(h % (uint64_t)n_parts);
+        counts[part[r]]++;
+    }
+    int64_t *next = malloc((size_t)n_parts * sizeof(int64_t));
+    int64_t acc = 0;
+    for (int p = 0; p < n_parts; ++p) next[p] = acc, acc += counts[p];
+    for (int64_t r = 0; r < n; ++r) out_perm[next[part[r]]++] = (uint32_t)r;
+    free(next);
+    free(part);
+    return QEH_OK;
+}
+
 static uint64_t mix(uint64_t k) {
     k ^= k >> 33;
     k *= 0xff51afd7ed558ccdULL;

@@ -75,6 +75,12 @@ int qo_join_filter_aggregate_mt(const qo_col *probe_cols, int n_probe, int probe
                                 const qo_col *build_group_keys, int n_group_keys, const qeh_agg *aggs,
                                 int n_aggs, int threads, qo_col *out_keys, qo_col *out_aggs,
                                 int64_t *out_groups);
+/* Partitioner::partition_by_hash (query-distributed/src/partition.rs:151-212, compute_row_hash
+ * :292-316) over Int32 / Int64 key columns: every row goes to hash(row) % n_parts, rows keep input
+ * order inside a partition; out_perm = the partition-major row order, counts[p] = rows of p.
+ * The row hash is the device's (murmur3 fmix64 combine, NULL cells skipped), not SipHash: the
+ * hash is not observable in any query result. */
+int qo_partition_hash(const qo_col *keys, int n_keys, int n_parts, int64_t *counts, uint32_t *out_perm);
 int qo_sort_indices(const qo_col *keys, int n_keys, const int8_t *ascending, int64_t n_rows,
                     uint32_t *out_perm);
 int qo_sort_indices_nulls(const qo_col *keys, int n_keys, const int8_t *ascending, const int8_t *nulls_first,

@@ -1638,20 +1638,32 @@ struct BuildRanges {
 };
 
 // Phase A launched by qeh_join_filter_aggregate_prelaunch, waiting on the context for the call it
-// belongs to: the same probe columns, key and predicate (compared by identity / by value).
+// belongs to: the same probe columns, key, predicate and aggregates (compared by identity / by
+// value).  Phase A stages the aggregate input column it was planned with, so a call with other
+// aggregates (COUNT vs SUM(v), SUM over another column) must not adopt it.
 struct PendingSlice {
     SlicePre pre;
     std::vector<const void *> vals;
     std::vector<int64_t> offs, lens;
+    std::vector<int32_t> dtypes;
     int key_idx = -1;
     std::vector<uint8_t> pred;  // the predicate's serialised form (empty = none)
+    std::vector<int32_t> agg_fc;  // (func, column) of every aggregate
     BuildRanges br{};
     static std::vector<uint8_t> serialise(const qeh_expr *e);
-    bool matches(const qeh_column *cols, int n_cols, int key, const qeh_expr *predicate) const {
+    static std::vector<int32_t> agg_list(const qeh_agg *aggs, int n_aggs) {
+        std::vector<int32_t> v;
+        for (int i = 0; i < n_aggs; ++i) v.push_back(aggs[i].func), v.push_back(aggs[i].column);
+        return v;
+    }
+    bool matches(const qeh_column *cols, int n_cols, int key, const qeh_expr *predicate, const qeh_agg *aggs,
+                 int n_aggs) const {
         if (n_cols != (int)vals.size() || key != key_idx) return false;
         for (int i = 0; i < n_cols; ++i)
-            if (cols[i].values != vals[i] || cols[i].offset != offs[i] || cols[i].length != lens[i]) return false;
-        return serialise(predicate) == pred;
+            if (cols[i].values != vals[i] || cols[i].offset != offs[i] || cols[i].length != lens[i] ||
+                cols[i].dtype != dtypes[i])
+                return false;
+        return agg_list(aggs, n_aggs) == agg_fc && serialise(predicate) == pred;
     }
     void take(SlicePre *dst) {
         dst->launched = pre.launched;
@@ -2627,9 +2639,11 @@ extern "C" int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_colum
         p->vals.push_back(probe_cols[i].values);
         p->offs.push_back(probe_cols[i].offset);
         p->lens.push_back(probe_cols[i].length);
+        p->dtypes.push_back(probe_cols[i].dtype);
     }
     p->key_idx = probe_key_idx;
     p->pred = PendingSlice::serialise(predicate);
+    p->agg_fc = PendingSlice::agg_list(aggs, n_aggs);
     ctx->pending_slice = p;
     return QEH_OK;
 }
@@ -2671,7 +2685,7 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     SlicePre pre;
     std::shared_ptr<PendingSlice> pend = std::static_pointer_cast<PendingSlice>(ctx->pending_slice);
     ctx->pending_slice.reset();
-    if (pend && n_group_keys == 1 && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate)) {
+    if (pend && n_group_keys == 1 && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs)) {
         // adopt the phase A launched by qeh_join_filter_aggregate_prelaunch if the build columns that
         // arrived have exactly the ranges it was planned from
         const qeh_column both[2] = {*build_key, build_group_keys[0]};

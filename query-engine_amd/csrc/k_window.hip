@@ -261,8 +261,14 @@ struct WmRankLds {
     uint32_t wsum[16];
 };
 
-// Returns the tile's count of digit threadIdx.x.  DB >= 0: the digit width as a compile-time
-// constant (the ballot loop unrolls); DB < 0: `dbits` at run time.
+// Returns the tile's count of digit threadIdx.x.  DB >= 0: ballot matching with the digit width
+// as a compile-time constant (the ballot loop unrolls); DB == -1: ballot matching over `dbits`
+// bits at run time; DB == kWmAtomicRank: one LDS atomic per row on the wave's packed u16 counters
+// -- ds_add_rtn serves the lanes of one instruction that hit the same word in lane order
+// (tools/ubench/lds_order_ubench.hip checks exactly that), so the ranks are the same stable,
+// replayable ones at a handful of instructions per row instead of ~5 per digit bit.
+constexpr int kWmAtomicRank = -2;
+
 template <int NJ, int DB = -1>
 __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], const bool (&live)[NJ], int dbits,
                                                    uint32_t (&slot)[NJ], WmRankLds &R) {
@@ -272,24 +278,35 @@ __device__ __forceinline__ uint32_t wm_stable_rank(const uint32_t (&d)[NJ], cons
     for (int i = lane; i < kWmDig / 2; i += 64) wz[i] = 0u;
     wm_wave_sync();
     uint32_t r[NJ];
+    if constexpr (DB == kWmAtomicRank) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        uint64_t m = __ballot(live[j]);
-#pragma unroll
-        for (int b = 0; b < (DB >= 0 ? DB : dbits); ++b) {
-            // all ones where the lane's bit b is set (one signed bitfield extract)
-            const uint32_t rep = (uint32_t)(__builtin_amdgcn_sbfe((int32_t)d[j], b, 1));
-            const uint64_t bb = __ballot(rep != 0u);
-            m &= ~(bb ^ (((uint64_t)rep << 32) | rep));  // lanes whose bit b equals this lane's
+        for (int j = 0; j < NJ; ++j) {
+            r[j] = 0u;
+            if (live[j]) {
+                const uint32_t sh = (d[j] & 1u) * 16u;
+                r[j] = (atomicAdd(&wz[d[j] >> 1], 1u << sh) >> sh) & 0xFFFFu;
+            }
         }
-        // every lane of a digit reads the digit's count (one LDS read, no broadcast from a leader);
-        // the digit's lowest lane then adds the digit's row count (the read instruction precedes
-        // the write in the wave's LDS order)
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint32_t old = live[j] ? (uint32_t)R.wc[wave][d[j]] : 0u;
-        if (live[j] && below == 0) R.wc[wave][d[j]] = (uint16_t)(old + (uint32_t)__popcll(m));
-        r[j] = old + below;
-        wm_wave_sync();
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            uint64_t m = __ballot(live[j]);
+#pragma unroll
+            for (int b = 0; b < (DB >= 0 ? DB : dbits); ++b) {
+                // all ones where the lane's bit b is set (one signed bitfield extract)
+                const uint32_t rep = (uint32_t)(__builtin_amdgcn_sbfe((int32_t)d[j], b, 1));
+                const uint64_t bb = __ballot(rep != 0u);
+                m &= ~(bb ^ (((uint64_t)rep << 32) | rep));  // lanes whose bit b equals this lane's
+            }
+            // every lane of a digit reads the digit's count (one LDS read, no broadcast from a leader);
+            // the digit's lowest lane then adds the digit's row count (the read instruction precedes
+            // the write in the wave's LDS order)
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint32_t old = live[j] ? (uint32_t)R.wc[wave][d[j]] : 0u;
+            if (live[j] && below == 0) R.wc[wave][d[j]] = (uint16_t)(old + (uint32_t)__popcll(m));
+            r[j] = old + below;
+            wm_wave_sync();
+        }
     }
     wm_barrier();
     uint32_t tot = 0;
@@ -1042,6 +1059,8 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const ColRef kc = make_colref(part), oc = make_colref(order);
     const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
     const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
+    // stable tile ranking by LDS atomics (default) or by ballot matching (QEH_WM_BALLOT=1, A/B)
+    const bool at = std::getenv("QEH_WM_BALLOT") == nullptr;
     int gbx = 2;  // bucket workgroups per CU (pass 2 / its inverse)
     if (const char *e = std::getenv("QEH_WM_GBX")) gbx = std::max(1, std::atoi(e));
     const int gb = std::min(cus * gbx, sh.nb);
@@ -1050,17 +1069,17 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
         QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
         const bool d1 = wm_digit_bits(sh.nb) == 10;
-        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? (d1 ? k_wm2_pass1<4, 4, 10> : k_wm2_pass1<4, 4, -1>)
-                                                : (d1 ? k_wm2_pass1<4, 8, 10> : k_wm2_pass1<4, 8, -1>))
-                                    : (oes == 4 ? (d1 ? k_wm2_pass1<8, 4, 10> : k_wm2_pass1<8, 4, -1>)
-                                                : (d1 ? k_wm2_pass1<8, 8, 10> : k_wm2_pass1<8, 8, -1>)),
+#define QEH_WM_P1(K, O) (at ? k_wm2_pass1<K, O, kWmAtomicRank> : d1 ? k_wm2_pass1<K, O, 10> : k_wm2_pass1<K, O, -1>)
+        hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
+                                    : (oes == 4 ? QEH_WM_P1(8, 4) : QEH_WM_P1(8, 8)),
                            dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh,
                            base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
         // bucket starts = the scanned bases of workgroup 0 per digit, then n
         QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
-        hipLaunchKernelGGL(sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+#undef QEH_WM_P1
+        hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
                            bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
                            pst.as<uint64_t>());
     }
@@ -1131,14 +1150,15 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
     {
         KernelTimer kt(ctx, "window_place");
-        hipLaunchKernelGGL(value_fn ? (sh.lb == 10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
-                                    : (sh.lb == 10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
+        hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : sh.lb == 10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
+                                    : (at ? k_wm2_inv2<kWmAtomicRank, false> : sh.lb == 10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
                            dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
                            kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(), res2v.as<uint64_t>(),
                            res1v.as<uint64_t>());
         const bool d1i = wm_digit_bits(sh.nb) == 10;
 #define QEH_WM_I1(V)                                                                                                     \
-    (kes == 4 ? (d1i ? k_wm2_inv1<4, 10, V> : k_wm2_inv1<4, -1, V>) : (d1i ? k_wm2_inv1<8, 10, V> : k_wm2_inv1<8, -1, V>))
+    (kes == 4 ? (at ? k_wm2_inv1<4, kWmAtomicRank, V> : d1i ? k_wm2_inv1<4, 10, V> : k_wm2_inv1<4, -1, V>)                 \
+              : (at ? k_wm2_inv1<8, kWmAtomicRank, V> : d1i ? k_wm2_inv1<8, 10, V> : k_wm2_inv1<8, -1, V>))
         hipLaunchKernelGGL(!value_fn ? QEH_WM_I1(0) : esz == 8 ? QEH_WM_I1(8) : QEH_WM_I1(4), dim3(g1), dim3(kWmBlock), 0,
                            ctx->stream, kc, sh, base1.as<uint64_t>(), res1.as<uint16_t>(), out->values,
                            res1v.as<uint64_t>(), valid8.as<uint8_t>());

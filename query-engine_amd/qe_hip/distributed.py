@@ -25,6 +25,7 @@ and host tensors under "gloo" (CPU rehearsal of the same code path).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -59,12 +60,12 @@ def exchange(send_counts: torch.Tensor, payloads: Sequence[torch.Tensor], group=
     for i, p in enumerate(payloads):
         if i in byte_splits:
             j = keys.index(i)
-            pin = [int(x) for x in byte_splits[i]]
-            pout = [int(x) for x in M[:, world * (j + 1) + rank]]
+            S = M[:, world * (j + 1):world * (j + 2)]
         else:
-            pin = [int(x) for x in M[rank, :world]]
-            pout = [int(x) for x in M[:, rank]]
-        received.append(_all_to_all(p, pin, pout, group))
+            S = M[:, :world]
+        pin = [int(x) for x in S[rank]]
+        pout = [int(x) for x in S[:, rank]]
+        received.append(_all_to_all(p, pin, pout, _peak_remote(S), group))
     return recv_counts, received
 
 
@@ -83,15 +84,51 @@ def _allgather_meta_t(t: torch.Tensor, world: int, group=None) -> np.ndarray:
 # loses the second half of a world-1 all_to_all self-send once it passes ~1 GB
 # (tools/debug/a2a_big.py: 0.8 GB intact, 1.6 GB half wrong); large exchanges therefore never
 # self-send through RCCL and move in rounds of at most this many bytes per peer.
-A2A_CHUNK_BYTES = 256 << 20
+A2A_CHUNK_BYTES = int(os.environ.get("QEH_A2A_CHUNK_BYTES", 256 << 20))
 
 
-def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], group=None) -> torch.Tensor:
+def _peak_remote(splits: np.ndarray) -> int:
+    """Largest off-diagonal entry of a [world, world] split matrix (rows rank i sends to rank j):
+    the most any rank sends to another.  Every rank holds the same matrix (it comes from one
+    all_gather), so every rank derives the same round count from it."""
+    m = np.array(splits, np.int64, copy=True).reshape(len(splits), -1)
+    np.fill_diagonal(m, 0)
+    return int(m.max()) if m.size else 0
+
+
+def _a2a_rounds(pin: Sequence[int], pout: Sequence[int], me: int, row_bytes: int, chunk_bytes: int,
+                peak: int) -> List[List[Tuple[int, int, int, int]]]:
+    """The round plan of a chunked all-to-all (shared by every backend): rounds[t][r] =
+    (a, b, c, d) — rows [a, b) of the partition for rank r are sent and rows [c, d) of what rank r
+    sends here are received in round t (offsets inside the partitions).  At most chunk_bytes per
+    peer per round; the local partition (r == me) never takes part.  The round count comes from
+    `peak` (_peak_remote of the job-wide split matrix), not from this rank's own splits, so every
+    rank issues the same number of collectives — a rank with nothing left to move joins the later
+    rounds with empty slices (gloo's all-to-all is a collective every rank must enter)."""
+    world = len(pin)
+    cap = max(chunk_bytes // max(row_bytes, 1), 1)
+    n_rounds = (peak + cap - 1) // cap
+    rounds = []
+    for t in range(n_rounds):
+        plan = []
+        for r in range(world):
+            if r == me:
+                plan.append((0, 0, 0, 0))
+                continue
+            plan.append((min(t * cap, pin[r]), min((t + 1) * cap, pin[r]),
+                         min(t * cap, pout[r]), min((t + 1) * cap, pout[r])))
+        rounds.append(plan)
+    return rounds
+
+
+def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], peak: int, group=None) -> torch.Tensor:
     """Variable all-to-all of one partition-major payload: pin[r] leading rows go to rank r,
-    pout[r] rows arrive from rank r.  The local partition never goes through the collective
-    (one device copy, or the input itself at world size 1); under "nccl" the remote partitions
-    move as grouped send/recv (dist.all_to_all over views, ncclGroupStart/End) in rounds of at
-    most A2A_CHUNK_BYTES per peer; "gloo" (host tensors, rehearsal) uses all_to_all_single."""
+    pout[r] rows arrive from rank r; peak = _peak_remote of the job-wide split matrix.  The local partition never goes through the collective
+    (one copy, or the input itself at world size 1); the remote partitions move in the rounds of
+    _a2a_rounds (at most A2A_CHUNK_BYTES per peer each).  Only the collective of a round depends on
+    the backend: under "nccl" grouped send/recv of the views (dist.all_to_all over views,
+    ncclGroupStart/End, no packing); under "gloo" the round's slices are packed into one buffer for
+    all_to_all_single and unpacked into their places."""
     world = len(pin)
     me = dist.get_rank(group)
     if world == 1:
@@ -99,31 +136,25 @@ def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], group=
     p = p.contiguous()
     shape = tuple(p.shape[1:])
     out = torch.empty((sum(pout),) + shape, dtype=p.dtype, device=p.device)
-    if p.device.type != "cuda":
-        dist.all_to_all_single(out, p, output_split_sizes=list(pout), input_split_sizes=list(pin), group=group)
-        return out
     ioff = np.concatenate([[0], np.cumsum(pin)]).astype(np.int64)
     ooff = np.concatenate([[0], np.cumsum(pout)]).astype(np.int64)
     if pin[me]:
         out[ooff[me]:ooff[me] + pout[me]].copy_(p[ioff[me]:ioff[me] + pin[me]])
-    row_bytes = max(p.element_size() * int(np.prod(shape, dtype=np.int64)), 1)
-    cap = max(A2A_CHUNK_BYTES // row_bytes, 1)
-    rounds = max([(max(pin[r], pout[r]) + cap - 1) // cap for r in range(world) if r != me] + [0])
-    empty = p.new_empty((0,) + shape)
-    for t in range(rounds):
-        ins, outs = [], []
-        for r in range(world):
-            if r == me:
-                ins.append(empty)
-                outs.append(out.new_empty((0,) + shape))
-                continue
-            a = min(t * cap, pin[r])
-            b = min((t + 1) * cap, pin[r])
-            c = min(t * cap, pout[r])
-            d = min((t + 1) * cap, pout[r])
-            ins.append(p[ioff[r] + a:ioff[r] + b])
-            outs.append(out[ooff[r] + c:ooff[r] + d])
-        dist.all_to_all(outs, ins, group=group)
+    row_bytes = p.element_size() * int(np.prod(shape, dtype=np.int64))
+    grouped = dist.get_backend(group) == "nccl"
+    for plan in _a2a_rounds(pin, pout, me, row_bytes, A2A_CHUNK_BYTES, peak):
+        ins = [p[ioff[r] + a:ioff[r] + b] for r, (a, b, _, _) in enumerate(plan)]
+        outs = [out[ooff[r] + c:ooff[r] + d] for r, (_, _, c, d) in enumerate(plan)]
+        if grouped:
+            dist.all_to_all(outs, ins, group=group)
+        else:
+            recv = torch.empty((sum(o.shape[0] for o in outs),) + shape, dtype=p.dtype, device=p.device)
+            dist.all_to_all_single(recv, torch.cat(ins) if ins else p[:0], output_split_sizes=[o.shape[0] for o in outs],
+                                   input_split_sizes=[i.shape[0] for i in ins], group=group)
+            q = 0
+            for o in outs:
+                o.copy_(recv[q:q + o.shape[0]])
+                q += o.shape[0]
     return out
 
 
@@ -320,6 +351,7 @@ class DistributedExecutor:
         meta_t = torch.cat(meta) if meta else torch.zeros(0, dtype=torch.int64, device=self.device)
         M = _allgather_meta_t(meta_t, w, self.group)
         sin, sout = [int(x) for x in M[me, :w]], [int(x) for x in M[:, me]]
+        peak = _peak_remote(M[:, :w])
         nullable = M[:, w:w + len(cols)].max(axis=0) > 0 if len(cols) else np.zeros(0, bool)
         out = []
         for j, t in enumerate(cols):
@@ -330,14 +362,15 @@ class DistributedExecutor:
                 if t.dtype == abi.DT_UTF8 and q == 1:
                     u = utf8.index(j)
                     off = w + len(cols) + w * u
-                    vals.append(_all_to_all(ts[1], [int(x) for x in M[me, off:off + w]],
-                                            [int(x) for x in M[:, off + me]], self.group))
+                    S = M[:, off:off + w]
+                    vals.append(_all_to_all(ts[1], [int(x) for x in S[me]], [int(x) for x in S[:, me]],
+                                            _peak_remote(S), self.group))
                 else:
-                    vals.append(_all_to_all(ts[q], sin, sout, self.group))
+                    vals.append(_all_to_all(ts[q], sin, sout, peak, self.group))
             valid = None
             if nullable[j]:
                 vb = ts[nvals] if len(ts) > nvals else torch.ones(len(t), dtype=torch.uint8, device=self.device)
-                valid = _all_to_all(vb, sin, sout, self.group)
+                valid = _all_to_all(vb, sin, sout, peak, self.group)
             out.append(self._from_tensors(t.dtype, vals[0] if nvals == 1 else vals, valid))
         self._sync_torch()
         return out, sout
@@ -429,8 +462,10 @@ class DistributedExecutor:
         nullable = M[:, 1:].max(axis=0) > 0 if cols else []
         mx = max(rows) if rows else 0
         out = []
+        tens = [self._to_tensors(c) for c in cols]
+        self._sync()  # the views / validity bytes are produced on the library's queue
         for j, c in enumerate(cols):
-            ts = self._to_tensors(c)
+            ts = tens[j]
             vals = self._gather_padded(ts[0], n, mx, rows)
             valid = None
             if nullable[j]:
@@ -463,46 +498,69 @@ class DistributedExecutor:
         for f, _ in aggs:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
+        # which aggregate inputs may hold NULLs, agreed across ranks (each rank sees only its fact
+        # shard's bitmaps; the final stage's choice of collectives must be the same on every rank)
+        probe_flags = [1 if probe_cols[c].c.validity else 0 for _, c in aggs]
+        probe_nullable = None
         if build_sharded:
-            full = self._allgather_beside_phase_a(probe_cols, probe_key_idx, predicate, build_key,
-                                                  build_group_keys, aggs)
+            full, probe_nullable = self._allgather_beside_phase_a(probe_cols, probe_key_idx, predicate, build_key,
+                                                                  build_group_keys, aggs, probe_flags)
             if full is None:
                 full = self.allgather_columns([build_key] + list(build_group_keys))
             build_key, build_group_keys = full[0], full[1:]
+        if probe_nullable is None:
+            probe_nullable = self._agree_max(probe_flags)
         pk, pa_, g = self.ctx.join_filter_aggregate(probe_cols, probe_key_idx, predicate, build_key,
                                                     build_group_keys, aggs)
         if g == 0:
             pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
-        dense = self._final_dense(build_group_keys, probe_cols, pk, pa_, aggs)
+        dense = self._final_dense(build_group_keys, probe_nullable, pk, pa_, aggs)
         self.last_final = "dense" if dense is not None else "shuffle"
         if dense is not None:
             return dense
         return self._final(pk, pa_, aggs)
 
-    def _allgather_beside_phase_a(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs):
+    def _agree_max(self, flags: Sequence[int]) -> np.ndarray:
+        """Element-wise max of a small int vector over the ranks (one all_reduce; none at world 1)."""
+        f = np.asarray(flags, np.int64)
+        if self.world == 1 or len(f) == 0:
+            return f
+        t = torch.as_tensor(f, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t.cpu().numpy()
+
+    def _allgather_beside_phase_a(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs,
+                                  probe_flags: Sequence[int]):
         """The dimension all-gather overlapped with phase A of the fused operator: one small
-        all_gather of every shard's [rows, key min / max, group key min / max] gives the full build
-        side's ranges, the padded column all-gathers are issued asynchronously, phase A is launched
-        from the ranges (qeh_join_filter_aggregate_prelaunch) while they run, and only then does the
-        queue wait for them.  None when the shape does not allow it (the caller all-gathers first)."""
+        all_gather of every shard's [rows, key min / max, group key min / max, has-validity flags]
+        gives the full build side's ranges, the padded column all-gathers are issued asynchronously,
+        phase A is launched from the ranges (qeh_join_filter_aggregate_prelaunch) while they run, and
+        only then does the queue wait for them.  Returns (columns, agreed probe_flags); columns are
+        None when the shape does not allow it (the caller all-gathers first).  Every branch after
+        the small all_gather depends only on gathered values, so all ranks take the same one (a
+        bitmap on any rank's build shard sends every rank to allgather_columns)."""
         cols = [build_key] + list(build_group_keys)
         if (self.world == 1 or self.device != "cuda" or len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
-                or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32) or any(c.c.validity for c in cols)):
-            return None
+                or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32)):
+            return None, None
         n = len(build_key)
         ts = [self._to_tensors(c)[0] for c in cols]
+        self._sync()  # the shard columns may still be in flight on the library's queue
         big, small = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+        flags = torch.tensor([1 if any(c.c.validity for c in cols) else 0] + list(probe_flags), dtype=torch.int64,
+                             device=self.device)
         if n:
             kk, gg = torch.aminmax(ts[0]), torch.aminmax(ts[1].to(torch.int64))
-            st = torch.stack([torch.tensor(n, dtype=torch.int64, device=ts[0].device), kk.min, kk.max, gg.min, gg.max])
+            st = torch.cat([torch.stack([torch.tensor(n, dtype=torch.int64, device=ts[0].device), kk.min, kk.max,
+                                         gg.min, gg.max]), flags])
         else:
-            st = torch.tensor([0, big, small, big, small], dtype=torch.int64, device=self.device)
-        self._sync()
+            st = torch.cat([torch.tensor([0, big, small, big, small], dtype=torch.int64, device=self.device), flags])
         M = _allgather_meta_t(st, self.world, self.group)
+        agreed = M[:, 6:].max(axis=0)
         rows = [int(x) for x in M[:, 0]]
         total, mx = sum(rows), max(rows)
-        if total == 0:
-            return None
+        if total == 0 or M[:, 5].max() > 0:
+            return None, agreed
         live = M[M[:, 0] > 0]
         krange = [int(live[:, 1].min()), int(live[:, 2].max()), total]
         grange = [int(live[:, 3].min()), int(live[:, 4].max()), total]
@@ -524,11 +582,11 @@ class DistributedExecutor:
                 buf = torch.cat([buf[q * mx:q * mx + rows[q]] for q in range(self.world)])
             out.append(self._from_tensors(c.dtype, buf, None))
         self._sync_torch()
-        return out
+        return out, agreed
 
     DENSE_MAX_KEYS = 1 << 20
 
-    def _final_dense(self, build_group_keys, probe_cols, pk, pa_, aggs):
+    def _final_dense(self, build_group_keys, probe_nullable, pk, pa_, aggs):
         """Final aggregate of a broadcast join by all-reduce instead of a shuffle, when the single
         group key is a non-null integer column of the (replicated) dimension whose range spans at
         most DENSE_MAX_KEYS values: every rank scatters its partial states into dense arrays
@@ -537,16 +595,19 @@ class DistributedExecutor:
         rank keeps the groups with (key - min) % world == rank.  Same result as _final (partial
         states merged per group, each group on one rank) with one or two collectives and one host
         read (the key range) instead of a partition kernel, a metadata all_gather, an all-to-all
-        per column and a hash aggregate.  None when not applicable (the caller shuffles)."""
+        per column and a hash aggregate.  None when not applicable (the caller shuffles).
+        probe_nullable[j]: aggregate j's input has a bitmap on some rank (agreed across ranks); the
+        group column is the replicated dimension's, identical on every rank, so every rank decides
+        the same way."""
         if len(build_group_keys) != 1 or len(pk) != 1:
             return None
         gcol = build_group_keys[0]
         if gcol.dtype not in (abi.DT_INT64, abi.DT_INT32) or gcol.c.validity:
             return None  # (no NULL group key: the key comes from this column through an INNER join)
         kinds = []
-        for (f, c), col in zip(aggs, pa_):
+        for j, ((f, c), col) in enumerate(zip(aggs, pa_)):
             # partial states can be NULL only where an input value can (all-NULL group)
-            if f not in FINAL_OF or (f != AF.Count and probe_cols[c].c.validity):
+            if f not in FINAL_OF or (f != AF.Count and probe_nullable[j]):
                 return None
             if f in (AF.Min, AF.Max) and col.dtype not in (abi.DT_INT64, abi.DT_INT32):
                 return None  # float MIN / MAX keep the shuffle (total-order semantics)

@@ -67,6 +67,58 @@ def mode_exchange_bytes(rank, world):
     assert got == sorted(want)
 
 
+def mode_exchange_chunked(rank, world):
+    """The chunked all-to-all (distributed._all_to_all / _a2a_rounds, the logic the RCCL branch
+    shares) with A2A_CHUNK_BYTES tiny, so one payload moves in many rounds: uneven partitions,
+    zero partitions (rank 1 sends nothing to rank 0; the last rank has no rows at all), a 2-D
+    payload and a byte-split payload.  Received rows must equal what every source sent, in
+    source-rank-major, stable order."""
+    from qe_hip import distributed as D
+    D.A2A_CHUNK_BYTES = 40  # 5 int64 rows / 2 (3 x f32) rows / 40 bytes per peer per round
+
+    def shard(q):
+        r = np.random.default_rng(900 + q)
+        n = 0 if q == world - 1 else 37 + 53 * q
+        dest = r.integers(0, world, n)
+        if q == 1:
+            dest[dest == 0] = world - 1  # rank 1 -> rank 0: zero rows
+        k = (q * 100_000 + np.arange(n)).astype(np.int64)  # globally unique, source-ordered ids
+        w = r.random((n, 3)).astype(np.float32)
+        strs = [f"{q}:{i}" + "z" * int(r.integers(0, 30)) for i in range(n)]
+        return dest, k, w, strs
+
+    dest, k, w, strs = shard(rank)
+    order = np.argsort(dest, kind="stable")
+    counts = np.bincount(dest, minlength=world).astype(np.int64)
+    enc = [strs[i].encode() for i in order]
+    lens = np.array([len(b) for b in enc], np.int32)
+    data = np.frombuffer(b"".join(enc), np.uint8).copy() if enc else np.zeros(0, np.uint8)
+    bounds = np.concatenate([[0], np.cumsum(counts)])
+    cum = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    splits = [int(cum[bounds[q + 1]] - cum[bounds[q]]) for q in range(world)]
+    rc, (rk, rw, rl, rd) = exchange_host(torch.tensor(counts), [torch.from_numpy(k[order]), torch.from_numpy(w[order]),
+                                                                torch.from_numpy(lens), torch.from_numpy(data)],
+                                         byte_splits={3: splits})
+    want_k, want_w, want_s = [], [], []
+    for q in range(world):
+        dq, kq, wq, sq = shard(q)
+        sel = np.nonzero(dq == rank)[0]  # stable: source order inside each source
+        want_k.append(kq[sel])
+        want_w.append(wq[sel])
+        want_s += [sq[i] for i in sel]
+    assert np.array_equal(rk.numpy(), np.concatenate(want_k))
+    assert np.array_equal(rw.numpy(), np.concatenate(want_w).reshape(-1, 3))
+    raw = rd.numpy().tobytes()
+    c2 = np.concatenate([[0], np.cumsum(rl.numpy().astype(np.int64))])
+    assert [raw[c2[i]:c2[i + 1]].decode() for i in range(len(rl))] == want_s
+    assert int(rc.sum()) == len(want_s)
+
+
+def exchange_host(counts, payloads, byte_splits=None):
+    from qe_hip.distributed import exchange
+    return exchange(counts, payloads, byte_splits=byte_splits)
+
+
 def mode_gpu_exchange(rank, world):
     """DistributedExecutor.exchange: device Partitioner (Hash over Int64 + Utf8 keys, Range over
     Int64, Single) + all-to-all of Int64 / Float64 / Utf8 / Boolean columns with NULLs."""
@@ -384,7 +436,8 @@ def main():
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        {"exchange": mode_exchange, "exchange_bytes": mode_exchange_bytes, "gpu": mode_gpu,
+        {"exchange": mode_exchange, "exchange_bytes": mode_exchange_bytes, "exchange_chunked": mode_exchange_chunked,
+         "gpu": mode_gpu,
          "gpu_exchange": mode_gpu_exchange, "gpu_cfg4": mode_gpu_cfg4, "nccl1": mode_nccl1}[mode](rank, world)
         dist.barrier()
     finally:

@@ -232,6 +232,16 @@ def join_on(join_type: int, left: Sequence[HostCol], right: Sequence[HostCol], o
     return [_take(ol[i]) for i in range(len(left))], [_take(orr[i]) for i in range(len(right))], rows.value
 
 
+def partition_hash(keys: Sequence[HostCol], n_parts: int):
+    """(counts, partition-major row order) of Partitioner::partition_by_hash (qo_partition_hash)."""
+    n = len(keys[0].values)
+    counts = np.zeros(n_parts, np.int64)
+    perm = np.empty(max(n, 1), np.uint32)
+    _check(lib().qo_partition_hash(_arr(keys), len(keys), n_parts, counts.ctypes.data_as(C.c_void_p),
+                                   perm.ctypes.data_as(C.c_void_p)))
+    return counts, perm[:n]
+
+
 def sort_indices_nulls(keys: Sequence[HostCol], ascending: Sequence[bool], nulls_first: Sequence[bool]) -> np.ndarray:
     n = len(keys[0].values) if keys else 0
     out = np.empty(max(n, 1), np.uint32)

@@ -51,6 +51,42 @@ def test_exchange_variable_size_payloads_gloo_cpu(world):
     launch("exchange_bytes", world)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_chunked_rounds_gloo_cpu(world):
+    """The round / chunk / local-copy logic of the exchange (shared with the RCCL branch) with a
+    40-byte chunk: many rounds, uneven and zero partitions, a rank with no rows."""
+    launch("exchange_chunked", world)
+
+
+def test_a2a_round_plan_pairs_up():
+    """_a2a_rounds over random job-wide split matrices: every rank plans the same number of
+    rounds, in every round what rank i sends to rank j is exactly what j expects from i, and the
+    slices tile each remote partition once, in order."""
+    import numpy as np
+    from qe_hip.distributed import _a2a_rounds, _peak_remote
+    r = np.random.default_rng(5)
+    for _ in range(200):
+        world = int(r.integers(2, 6))
+        S = r.integers(0, 50, (world, world)) * (r.random((world, world)) > 0.3)
+        chunk, row_bytes = int(r.integers(1, 200)), int(r.choice([1, 4, 8, 24]))
+        peak = _peak_remote(S)
+        plans = [_a2a_rounds(list(S[i]), list(S[:, i]), i, row_bytes, chunk, peak) for i in range(world)]
+        assert len({len(p) for p in plans}) == 1
+        for i in range(world):
+            for j in range(world):
+                if i == j:
+                    assert all(rd[j] == (0, 0, 0, 0) for rd in plans[i])
+                    continue
+                sent = [(rd[j][0], rd[j][1]) for rd in plans[i]]
+                got = [(rd[i][2], rd[i][3]) for rd in plans[j]]
+                assert sent == got
+                pos = 0
+                for a, b in sent:
+                    assert a == pos or a == b
+                    pos = max(pos, b)
+                assert pos == S[i][j]
+
+
 @pytest.mark.gpu
 def test_device_exchange_two_ranks_on_one_gpu():
     """§8 f2: DistributedExecutor.exchange with the device Partitioner (Hash / Range / Single) over

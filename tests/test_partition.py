@@ -148,3 +148,88 @@ def test_filter_partition_hash_move_declines_general_predicates(ctx):
     with pytest.raises(abi.QehError) as ei:
         ctx.filter_partition_hash_move(cols, pred, 0, 2, [1])
     assert ei.value.status == abi.QEH_E_UNSUPPORTED
+
+
+def test_oracle_partition_hash_restates_partition_by_hash():
+    """qo_partition_hash (the oracle's partition.rs:151-212) against a numpy restatement of the
+    same row hash: per-partition counts, partition-major stable order, NULL keys hashed as an
+    empty key; rows are conserved (partition.rs:400-415)."""
+    import oracle_bind as ob
+    M = (1 << 64) - 1
+
+    def mix(k):
+        k ^= k >> 33
+        k = (k * 0xff51afd7ed558ccd) & M
+        k ^= k >> 33
+        k = (k * 0xc4ceb9fe1a85ec53) & M
+        return k ^ (k >> 33)
+
+    r = np.random.default_rng(8)
+    n = 3000
+    a = r.integers(-2**62, 2**62, n).astype(np.int64)
+    am = r.random(n) > 0.1
+    b = r.integers(-9, 9, n).astype(np.int32)
+    for keys, parts in (([ob.HostCol(a)], 8), ([ob.HostCol(a, am), ob.HostCol(b)], 5), ([ob.HostCol(b)], 1)):
+        counts, perm = ob.partition_hash(keys, parts)
+        ids = []
+        for i in range(n):
+            h = 0x9E3779B97F4A7C15
+            for c in keys:
+                if c.valid is not None and not c.valid[i]:
+                    continue
+                v = int(c.values[i]) & M
+                h = mix(h ^ ((mix(v) + 0x9E3779B97F4A7C15 + ((h << 6) & M) + (h >> 2)) & M))
+            ids.append(h % parts)
+        ids = np.array(ids)
+        assert np.array_equal(counts, np.bincount(ids, minlength=parts))
+        assert np.array_equal(perm, np.argsort(ids, kind="stable").astype(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nullable_key", [False, True])
+def test_partition_hash_move_8_ways_vs_oracle(ctx, nullable_key):
+    """Config 4's exchange pass against the oracle at 1e7 rows: qeh_partition_hash_move into 8
+    partitions == the oracle's partition_by_hash (partition.rs:151-212) order, counts and rows,
+    bit for bit (Int64 key with or without NULLs, Float64 and Int64 payloads)."""
+    import oracle_bind as ob
+    n, parts = 10_000_000, 8
+    r = np.random.default_rng(44)
+    k = r.integers(-10**12, 10**12, n).astype(np.int64)
+    km = (r.random(n) > 0.01) if nullable_key else None
+    v = r.random(n)
+    w = r.integers(-10**9, 10**9, n).astype(np.int64)
+    key = ctx.upload(k, km)
+    counts, moved = ctx.partition_hash_move([key], parts, [key, ctx.upload(v), ctx.upload(w)])
+    wc, perm = ob.partition_hash([ob.HostCol(k, km)], parts)
+    assert list(counts) == list(wc)
+    gk, gm = moved[0].to_numpy()
+    assert np.array_equal(gk[gm] if gm is not None else gk, k[perm][km[perm]] if km is not None else k[perm])
+    if km is not None:
+        assert np.array_equal(gm, km[perm])
+    assert np.array_equal(moved[1].to_numpy()[0], v[perm])
+    assert np.array_equal(moved[2].to_numpy()[0], w[perm])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("int32_key", [False, True])
+def test_filter_partition_hash_move_8_ways_vs_oracle(ctx, int32_key):
+    """Config 4's per-rank probe leg (qeh_filter_partition_hash_move: filter fused into the
+    8-way hash exchange pass) against the oracle at 1e7 rows: the oracle filter (executor.rs:
+    131-155) then the oracle partition_by_hash (partition.rs:151-212) give the same per-partition
+    counts and the same partition-major (k, v) rows, bit for bit."""
+    import oracle_bind as ob
+    from qe_hip import BinaryOp, binop, col, lit
+    n, parts = 10_000_000, 8
+    r = np.random.default_rng(45)
+    x = r.integers(0, 100, n).astype(np.int64)
+    k = r.integers(0, 10_000_000, n).astype(np.int32 if int32_key else np.int64)
+    v = r.random(n)
+    pred = binop(binop(col(0, "x"), BinaryOp.Greater, lit(49)), BinaryOp.And,
+                 binop(col(0, "x"), BinaryOp.LessEq, lit(97)))
+    counts, moved = ctx.filter_partition_hash_move([ctx.upload(x), ctx.upload(k), ctx.upload(v)], pred, 1, parts,
+                                                   [1, 2])
+    (fk, _), (fv, _) = ob.filter([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], pred, out_idx=[1, 2])[0]
+    wc, perm = ob.partition_hash([ob.HostCol(fk)], parts)
+    assert list(counts) == list(wc) and counts.sum() == int(((x > 49) & (x <= 97)).sum())
+    assert np.array_equal(moved[0].to_numpy()[0], fk[perm])
+    assert np.array_equal(moved[1].to_numpy()[0], fv[perm])

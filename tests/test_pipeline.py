@@ -286,12 +286,14 @@ def test_metric_full_size_properties(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hint", ["exact", "wrong_key_range", "wrong_group_range", "other_probe"])
+@pytest.mark.parametrize("hint", ["exact", "wrong_key_range", "wrong_group_range", "other_probe", "count_only_aggs",
+                                  "other_agg_column"])
 def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
     """qeh_join_filter_aggregate_prelaunch (phase A launched from caller-given build ranges while
     the build shards are in flight): the next fused call adopts it only when its probe columns and
-    the build columns' actual [min, max, count] match; otherwise it is discarded and the call
-    runs its own phase A.  The result equals the oracle's either way."""
+    the build columns' actual [min, max, count] match, and its aggregates are the call's (phase A
+    stages the aggregate input column: a COUNT-only prelaunch stages none); otherwise it is
+    discarded and the call runs its own phase A.  The result equals the oracle's either way."""
     n_fact, n_dim = 4_000_000, 4_000_000
     x, k, v, dk, dg = metric_data(n_fact, n_dim, 1024)
     probe = [ctx.upload(x), ctx.upload(k), ctx.upload(v)]
@@ -299,6 +301,11 @@ def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
     kr = [int(dk.min()), int(dk.max()), n_dim]
     gr = [int(dg.min()), int(dg.max()), n_dim]
     pre_probe = probe
+    pre_aggs = AGGS
+    if hint == "count_only_aggs":
+        pre_aggs = [(AF.Count, 2)]
+    elif hint == "other_agg_column":
+        pre_aggs = [(AF.Sum, 0), (AF.Count, 0)]
     if hint == "wrong_key_range":
         kr = [kr[0], kr[1] + 70_000, n_dim]
     elif hint == "wrong_group_range":
@@ -308,7 +315,7 @@ def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
     ctx.timing(True)
     ctx.timing_reset()
     try:
-        ctx.join_filter_aggregate_prelaunch(pre_probe, 1, PRED, AGGS, kr, gr)
+        ctx.join_filter_aggregate_prelaunch(pre_probe, 1, PRED, pre_aggs, kr, gr)
         gk, ga, g = ctx.join_filter_aggregate(probe, 1, PRED, bkey, [bg], AGGS)
         launches = ctx.kernel_time("slice_partition")[1]
     finally:

@@ -14,6 +14,8 @@
   merge   Merge::sorted of 8 partitions x 1.25e7 rows, ORDER BY k DESC NULLS LAST
   encode  pgwire DataRow text encoding of 1e7 result rows
   partition  device side of a hash Exchange, 1e8 rows into 8 partitions
+  cfg4leg    config 4's per-rank device leg at N = 8 (fused filter + 8-way exchange pass over 1e9
+             rows, the dim shard's exchange pass, the local join of what the rank receives)
 
 Prints one JSON line per config: rows/s, ms per run, algorithmic GB/s and
 fraction of 8 TB/s, and the oracle's rows/s on a bounded sample (1 thread).
@@ -352,6 +354,79 @@ def cfg_partition(ctx, scale):
          {"kernel_split_ms": kt, "max_partition_share": float(max(counts)) / n})
 
 
+def cfg4_leg(ctx, scale, world=8):
+    """BASELINE config 4's per-rank device leg at N = 8, on one GPU: what one rank of the
+    hash-partitioned plan runs besides the RCCL all-to-all (DistributedExecutor.
+    join_filter_aggregate_shuffle; partition.rs:151-212, planner.rs:200-249):
+      1. filter f.x > 49 fused into the 8-way hash exchange pass over its 1e9 fact rows
+         (qeh_filter_partition_hash_move: x, k, v read once, (k, v) of the selected rows written
+         partition-major);
+      2. the 8-way hash exchange pass over its dim shard (1e7 / 8 rows of (k, g));
+      3. the local fused join + partial aggregate over what the rank receives: the rows of ITS
+         partition from all 8 ranks — stood in for by 8 copies of this rank's partition 0 (same
+         size and key distribution: uniform keys send 1/8 of every rank's rows to each rank) —
+         against the dim keys of partition 0 (a sparse 1/8 of the key range).
+    Algorithmic bytes: 24 B read + 16 B written per selected row in (1), 32 B per dim row in (2),
+    16 B per received row in (3)."""
+    from qe_hip.partition import DeviceBatch  # noqa: F401  (same package the plan uses)
+    n, nd = int(1e9 * scale), 10_000_000
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dn = nd // world
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, dn, nd)
+    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, dn, 1024)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 1), (AF.Count, 1)]
+    # what rank 0 receives (built once, outside the timed legs)
+    pc, pm = ctx.filter_partition_hash_move([x, k, v], pred, 1, world, [1, 2])
+    selected = int(pc.sum())
+    recv_k = ctx.concat([ctx.slice(pm[0], 0, int(pc[0]))] * world)
+    recv_v = ctx.concat([ctx.slice(pm[1], 0, int(pc[0]))] * world)
+    for c in pm:
+        c.release()
+    full_dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    full_dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1024)
+    bc, bm = ctx.partition_hash_move([full_dk], world, [full_dk, full_dg])
+    bk0, bg0 = ctx.slice(bm[0], 0, int(bc[0])), ctx.slice(bm[1], 0, int(bc[0]))
+    recv = len(recv_k)
+
+    def leg1():
+        c, m = ctx.filter_partition_hash_move([x, k, v], pred, 1, world, [1, 2])
+        for q in m:
+            q.release()
+        return c
+
+    def leg2():
+        c, m = ctx.partition_hash_move([dk], world, [dk, dg])
+        for q in m:
+            q.release()
+        return c
+
+    def leg3():
+        gk, ga, g = ctx.join_filter_aggregate([recv_k, recv_v], 0, None, bk0, [bg0], aggs)
+        for q in gk + ga:
+            q.release()
+        return g
+    names = ["partition_move", "filter", "join_filter_aggregate", "slice_partition", "slice_probe", "join_build"]
+    w1, k1, _ = timed(ctx, leg1, 5, names)
+    w2, k2, _ = timed(ctx, leg2, 5, names)
+    w3, k3, g = timed(ctx, leg3, 5, names)
+    b1, b2, b3 = 24.0 * n + 16.0 * selected, 32.0 * dn, 16.0 * recv
+    kms1 = k1["partition_move"] + k1["filter"]
+    kms3 = k3["slice_partition"] + k3["slice_probe"] if k3["slice_partition"] else k3["join_filter_aggregate"]
+    legs = {"exchange_pass_fact": {"ms": kms1, "wall_ms": w1 * 1e3, "alg_bytes": b1, "frac_of_8TBs": b1 / (kms1 * 1e-3) / 1e9 / PEAK},
+            "exchange_pass_dim": {"ms": k2["partition_move"], "wall_ms": w2 * 1e3, "alg_bytes": b2},
+            "local_join": {"ms": kms3, "wall_ms": w3 * 1e3, "alg_bytes": b3, "rows": recv, "groups": g,
+                           "build_ms": k3["join_build"], "kernels": "slice" if k3["slice_partition"] else "single pass",
+                           "frac_of_8TBs": b3 / (kms3 * 1e-3) / 1e9 / PEAK}}
+    kms = kms1 + k2["partition_move"] + kms3
+    line(f"cfg4 per-rank device leg at N={world} (1e9 fact rows + 1/{world} dim per rank)", n, w1 + w2 + w3,
+         b1 + b2 + b3, kms, "k_hash_ids8_pred + k_part_scatter (fused filter + 8-way exchange), local fused join",
+         None, {"legs": legs, "selected": selected,
+                "note": "RCCL all-to-all time excluded (8-GPU runs are the driver's); wall = sum of the legs"})
+
+
 def cfg_filter(ctx, scale):
     n = int(5e8 * scale)
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
@@ -436,7 +511,8 @@ def main():
     for name in args.only.split(","):
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
-         "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window}[name](ctx, args.scale)
+         "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window,
+         "cfg4leg": cfg4_leg}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
