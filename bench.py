@@ -88,9 +88,10 @@ def host_threads() -> int:
 
 def cpu_baseline(args):
     """The metric query on the host CPU, same run, same box, two variants:
-      * 1 thread: the oracle's line-by-line restatement of the reference executor
-        (qo_join_filter_aggregate; executor.rs is single-threaded, rayon unused) over the full
-        dim table and the first `cpu-sample` fact rows;
+      * 1 thread: the oracle's intended-semantics hash join + filter + grouped aggregate
+        (qo_join_filter_aggregate: the reference's own executor.rs would take its Cartesian join
+        path and return no rows for this GROUP BY; executor.rs is single-threaded,
+        rayon unused) over the full dim table and the first `cpu-sample` fact rows;
       * all cores: qo_join_filter_aggregate_mt (OpenMP) over `cpu-sample-mt` fact rows.
     Both from oracle/_native/liboracle.so built with -march=native on this host when gcc is
     available (else the portable x86-64-v2 build).  `value` is the all-cores figure."""
@@ -123,8 +124,8 @@ def cpu_baseline(args):
     dt1 = time.perf_counter() - t0
     del f
     single = {"value": n1 / dt1, "cores": 1,
-              "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate (line-by-line restatement of executor.rs, "
-                        f"1 thread), {n1} fact rows x {args.dim} dim rows, build included, {dt1:.2f} s, {build}"}
+              "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate (intended-semantics hash join + filter + "
+                        f"group-by of the oracle, 1 thread), {n1} fact rows x {args.dim} dim rows, build included, {dt1:.2f} s, {build}"}
     nm = args.cpu_sample_mt
     f = fact(nm)
     ob.join_filter_aggregate_mt(f, 1, pred, ob.HostCol(dk), [ob.HostCol(dg)], aggs, threads)  # page in
@@ -133,8 +134,9 @@ def cpu_baseline(args):
     dtm = time.perf_counter() - t0
     del f
     out.update({"value": nm / dtm, "cores": threads,
-                "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate_mt (OpenMP, {threads} threads = this "
-                          f"process's CPU share of {os.cpu_count()} host CPUs), {nm} fact rows x {args.dim} dim rows, "
+                "sample": f"oracle/qe_oracle.c qo_join_filter_aggregate_mt (intended-semantics hash join of the "
+                          f"oracle, OpenMP, {threads} threads = the CPUs this process may use (affinity), not all "
+                          f"{os.cpu_count()} host CPUs), {nm} fact rows x {args.dim} dim rows, "
                           f"build included, {dtm:.2f} s, {build}",
                 "single_thread": single})
     return out

@@ -1289,12 +1289,15 @@ __global__ __launch_bounds__(1024) void k_states_compact_small(uint64_t *__restr
             for (int a = 0; a < specs.n; ++a)
                 if (specs.a[a].val_slot == slot) kind = specs.a[a].kind;
             uint64_t acc = states[i];
-            for (int sh0 = 1; sh0 < specs.shards; sh0 += 4) {  // four shard loads in flight
-                uint64_t v[4];
+            // sixteen shard loads in flight: one workgroup folds ~1 MB for 1024 groups x 64 shards,
+            // so it is bound by load round trips (four in flight: 32 us per query, profiles/r02)
+            constexpr int B = 16;
+            for (int sh0 = 1; sh0 < specs.shards; sh0 += B) {
+                uint64_t v[B];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = sh0 + q < specs.shards ? states[i + (sh0 + q) * words] : 0ull;
+                for (int q = 0; q < B; ++q) v[q] = sh0 + q < specs.shards ? states[i + (sh0 + q) * words] : 0ull;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < B; ++q) {
                     if (sh0 + q >= specs.shards) break;
                     switch (kind) {
                         case AK_SUM_F: acc = __builtin_bit_cast(uint64_t, as_f64(acc) + as_f64(v[q])); break;

@@ -177,6 +177,58 @@ __global__ void k_insert_direct16_xcd(ColRef key, int64_t n, RowPayload rp, Hash
     }
 }
 
+// The XCD-split insert in two steps, each key read once: k_xcd_lists appends every build row's
+// (key offset << 16 | payload + 1) to the list of its table range q = offset / span (one LDS rank per
+// row, one global cursor reservation per range per workgroup, ~1 K-entry contiguous runs per
+// range); k_insert_xcd_lists then has the workgroups of XCD q (b % 8 == q) drain list q, so range q
+// of the table is written only through XCD q's L2.  Lists hold up to n entries each (keys may all
+// fall into one range).
+constexpr int kXcdRows = 8;  // rows per thread in k_xcd_lists
+__global__ __launch_bounds__(kBlock) void k_xcd_lists(ColRef key, int64_t n, RowPayload rp, int64_t kmin, uint64_t span,
+                                                    uint64_t *__restrict__ lists, int64_t cap,
+                                                    unsigned long long *__restrict__ cursor) {
+    __shared__ uint32_t cnt[8];
+    __shared__ unsigned long long base[8];
+    for (int64_t t0 = (int64_t)blockIdx.x * kBlock * kXcdRows; t0 < n; t0 += (int64_t)gridDim.x * kBlock * kXcdRows) {
+        if (threadIdx.x < 8) cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        uint64_t e[kXcdRows];
+        uint32_t q[kXcdRows], rk[kXcdRows];
+#pragma unroll
+        for (int r = 0; r < kXcdRows; ++r) {
+            const int64_t i = t0 + (int64_t)r * kBlock + threadIdx.x;
+            q[r] = 8u;
+            e[r] = 0ull;
+            rk[r] = 0u;
+            if (i < n && col_valid(key, i)) {
+                const uint64_t o = (uint64_t)load_i64(key, i) - (uint64_t)kmin;
+                q[r] = (uint32_t)(o / span);
+                e[r] = (o << 16) | (uint64_t)(uint16_t)(payload_of(rp, i) + 1u);
+                rk[r] = atomicAdd(&cnt[q[r]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 8)
+            base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)cnt[threadIdx.x]) : 0ull;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kXcdRows; ++r)
+            if (q[r] < 8u) lists[(int64_t)q[r] * cap + (int64_t)base[q[r]] + rk[r]] = e[r];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_insert_xcd_lists(const uint64_t *__restrict__ lists, int64_t cap,
+                                                           const unsigned long long *__restrict__ cursor, HashTable t) {
+    const uint32_t q = blockIdx.x & 7u;
+    const int64_t nb = gridDim.x >> 3, m = (int64_t)cursor[q];
+    const uint64_t *l = lists + (int64_t)q * cap;
+    for (int64_t i = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x; i < m; i += nb * blockDim.x) {
+        const uint64_t e = __builtin_nontemporal_load(l + i);
+        t.payload16[e >> 16] = (uint16_t)(e & 0xFFFFu);
+    }
+}
+
 // Non-zero entries of a table of `n` words of `bytes` bytes (2 or 4), summed into *out.
 __global__ __launch_bounds__(kBlock) void k_count_nonzero(const void *__restrict__ table, uint64_t n, int bytes,
                                                           unsigned long long *out) {
@@ -389,9 +441,24 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
                 // alone it is slower (every workgroup reads all keys: 0.75 vs 0.52 ms for 1e7
                 // rows), beside 1e9 probe rows it disturbs phase A less (6.65-6.76 vs 6.85 ms per
                 // metric step, same box).  QEH_INSERT_XCD=0/1 overrides.
-                bool xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n;
-                if (const char *e = std::getenv("QEH_INSERT_XCD")) xcd = std::atoi(e) != 0;
-                if (xcd)
+                // QEH_INSERT_XCD=2 (default for the XCD split): keys partitioned into per-range lists
+                // once (k_xcd_lists), each list drained by one XCD; 1: every XCD's workgroups read
+                // all keys and keep their range's (8 key reads)
+                int xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n ? 2 : 0;
+                if (const char *e = std::getenv("QEH_INSERT_XCD")) xcd = std::atoi(e);
+                DevBuf lists, cursor;
+                if (xcd == 2 && (n > ((int64_t)1 << 28) || lists.alloc(ctx, (size_t)n * 8 * 8) != QEH_OK ||
+                                 cursor.alloc(ctx, 64) != QEH_OK))
+                    xcd = 1;
+                if (xcd == 2) {
+                    const uint64_t span = (range + 7) >> 3;
+                    QEH_HIP(hipMemsetAsync(cursor.p, 0, 64, ctx->stream));
+                    hipLaunchKernelGGL(k_xcd_lists, dim3(grid_for(ctx, n, kBlock * kXcdRows, 4)), dim3(kBlock), 0,
+                                       ctx->stream, kr, n, row_payload, t.kmin, span, lists.as<uint64_t>(), n,
+                                       cursor.as<unsigned long long>());
+                    hipLaunchKernelGGL(k_insert_xcd_lists, dim3(grid_for(ctx, n / 8 + 1, kBlock * 4, 4) * 8), dim3(kBlock),
+                                       0, ctx->stream, lists.as<uint64_t>(), n, cursor.as<unsigned long long>(), t);
+                } else if (xcd)
                     hipLaunchKernelGGL(k_insert_direct16_xcd, dim3(grid_for(ctx, n, kBlock * 4, 8) * 8), dim3(kBlock), 0,
                                        ctx->stream, kr, n, row_payload, t);
                 else

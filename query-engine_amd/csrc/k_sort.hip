@@ -165,8 +165,9 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
 template <typename KeyT>
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__ keys, int64_t n, int64_t seg,
                                                         int shift, uint32_t *__restrict__ hist, int nblocks) {
-    __shared__ uint32_t h[kRadix];
-    if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
+    constexpr int W = kRsThreads / 64;
+    __shared__ uint32_t h[W][kRadix];  // per-wave counters: one LDS atomic per row
+    for (int i = threadIdx.x; i < W * kRadix; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -182,12 +183,16 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__
         for (int j = 0; j < kRsIpt; ++j) {
             const bool live = base + j * 64 < hi;
             const uint32_t dg = (uint32_t)((k[j] >> shift) & (kRadix - 1));
-            const uint64_t peers = digit_peers(dg, live);  // one LDS atomic per distinct digit per wave
-            if (live && mbcnt(peers) == 0) atomicAdd(&h[dg], (uint32_t)popc64(peers));
+            if (live) atomicAdd(&h[wave][dg], 1u);
         }
     }
     __syncthreads();
-    if (threadIdx.x < kRadix) hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (threadIdx.x < kRadix) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) c += h[w][threadIdx.x];
+        hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = c;
+    }
 }
 
 // Histogram of a pass whose digits the previous scatter wrote as a byte stream
@@ -239,7 +244,9 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <typename KeyT>
+// AT: tile ranks by LDS atomics (ds_add_rtn serves one instruction's lanes in lane order, so the
+// rank is stable: tools/ubench/lds_order_ubench.hip), else by ballot peers (QEH_RS_BALLOT=1, A/B).
+template <typename KeyT, bool AT = true>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                            int nblocks, KeyT *__restrict__ keys_out,
@@ -286,10 +293,15 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
         for (int j = 0; j < kRsIpt; ++j) {
             const bool live = base + j * 64 < hi;
             const uint32_t dg = (uint32_t)((k[j] >> shift) & (kRadix - 1));
-            const uint64_t peers = digit_peers(dg, live);
-            const uint32_t before = wcnt[wave][dg];
-            rk[j] = before + mbcnt(peers);
-            if (live && mbcnt(peers) == 0) wcnt[wave][dg] = before + (uint32_t)popc64(peers);
+            if constexpr (AT) {
+                // LDS atomics serve the lanes of one instruction in lane order: the same stable rank
+                rk[j] = live ? atomicAdd(&wcnt[wave][dg], 1u) : 0u;
+            } else {
+                const uint64_t peers = digit_peers(dg, live);
+                const uint32_t before = wcnt[wave][dg];
+                rk[j] = before + mbcnt(peers);
+                if (live && mbcnt(peers) == 0) wcnt[wave][dg] = before + (uint32_t)popc64(peers);
+            }
         }
         lds_barrier();
         // thread t < 256 = digit t: wave starts inside the digit, tile total, scan -> loc
@@ -408,10 +420,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
 #pragma unroll
         for (int j = 0; j < kPmIpt; ++j) {
             const bool live = base + j * 64 < hi;
-            const uint64_t peers = digit_peers(dg[j], live);
-            const uint32_t before = wcnt[wave][dg[j]];
-            rk[j] = before + mbcnt(peers);
-            if (live && mbcnt(peers) == 0) wcnt[wave][dg[j]] = before + (uint32_t)popc64(peers);
+            rk[j] = live ? atomicAdd(&wcnt[wave][dg[j]], 1u) : 0u;  // stable (lane-ordered LDS atomics)
         }
         lds_barrier();
         uint32_t tot = 0, incl = 0;
@@ -467,6 +476,11 @@ struct RadixState {
     bool key32 = false;          // k[] currently holds 32-bit keys (column range fits 32 bits)
 };
 
+static bool rs_ballot() {
+    static const bool v = std::getenv("QEH_RS_BALLOT") != nullptr;
+    return v;
+}
+
 // Stable LSD passes over the low `bits` of the encoded keys in rs.
 template <typename KeyT>
 static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
@@ -494,9 +508,10 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         const bool next = multi && shift + kRadixBits < bits;
-        hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
-                           rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
-                           rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr, shift + kRadixBits);
+        auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
+        hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(),
+                           nblocks, rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr,
+                           shift + kRadixBits);
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
@@ -519,9 +534,9 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
                        hist.as<uint32_t>(), nblocks);
     QEH_HIP(hipGetLastError());
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
-    hipLaunchKernelGGL(k_rs_scatter<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(),
-                       rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks, rs.k[1 - c].as<KeyT>(),
-                       rs.v[1 - c].as<uint32_t>(), nullptr, 0);
+    auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
+    hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks,
+                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0);
     QEH_HIP(hipGetLastError());
     rs.cur = 1 - c;
     return QEH_OK;

@@ -177,12 +177,16 @@ FINAL_OF = {AF.Count: AF.Sum, AF.Sum: AF.Sum, AF.Min: AF.Min, AF.Max: AF.Max}
 
 
 class DistributedExecutor:
-    def __init__(self, ctx: Context, group=None):
+    def __init__(self, ctx: Context, group=None, device: Optional[str] = None):
+        """device: where payloads live during collectives — "cuda" under "nccl" (RCCL), "cpu" under
+        "gloo" by default.  device="cuda" with gloo keeps the device-tensor code paths (zero-copy
+        views, the overlapped dimension all-gather, the dense final aggregate) with gloo staging
+        through the host: the multi-rank rehearsal of the RCCL path on one GPU."""
         self.ctx = ctx
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        self.device = device or ("cuda" if dist.get_backend(group) == "nccl" else "cpu")
         self.last_final = None  # how the last broadcast join merged its partial states
 
     # ---- column <-> tensor ------------------------------------------------------

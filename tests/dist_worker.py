@@ -376,6 +376,98 @@ def mode_gpu_cfg4(rank, world):
     ctx.close()
 
 
+def mode_gpu_devtensors(rank, world):
+    """The RCCL path's device-tensor code with several ranks (two on one GPU): collectives over gloo
+    on CUDA tensors (DistributedExecutor(device="cuda")), the library on a torch stream as in the
+    bench.  Exercises what a host-tensor rehearsal skips: zero-copy column views as payloads, the
+    dimension all-gather overlapped with a prelaunched phase A (and its adoption), the dense
+    all-reduce final aggregate, validity flags agreed across ranks (only one rank's fact / dim shard
+    carries a bitmap), and the chunked all-to-all with a tiny chunk."""
+    import torch
+    import qe_hip
+    import oracle_bind as ob
+    from helpers import assert_grouped_equal
+    from qe_hip import AggregateFunction as AF, BinaryOp, binop, col, lit
+    from qe_hip import distributed as D
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    ctx = qe_hip.Context(0)
+    ctx.set_stream(s.cuda_stream)
+    dx = D.DistributedExecutor(ctx, device="cuda")
+    check_metric_plans(rank, world, dx, ctx)
+    # the metric shape at a size where the slice pipeline (phase A prelaunched beside the
+    # all-gather) runs, sharded fact and dim, dense final
+    n, nd = 3_000_000, 4_000_000
+    x = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 1, n, 100, row0=rank * n)
+    kk = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 2, n, nd, row0=rank * n)
+    vv = ob.generate(abi_gen("UNIT_F64"), 0x5EED, 3, n, row0=rank * n)
+    dk_all = ob.generate(abi_gen("PERMUTATION"), 0x5EED, 0, nd, nd)
+    dg_all = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 5, nd, 1024)
+    b = np.linspace(0, nd, world + 1).astype(int)
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
+        [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+        [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
+    launches = ctx.kernel_time("slice_partition")[1]
+    ctx.timing(False)
+    assert dx.last_final == "dense"
+    assert launches == 1, launches  # the prelaunched phase A was adopted (not re-run)
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        X = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 1, n * world, 100)
+        KK = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 2, n * world, nd)
+        VV = ob.generate(abi_gen("UNIT_F64"), 0x5EED, 3, n * world)
+        wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred,
+                                              ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
+        assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    # rank-local bitmaps: only rank 0's fact shard has NULLs in the aggregate input (every rank
+    # must then skip the dense final, which cannot carry all-NULL groups), only rank 1's dim key
+    # shard has a (NULL-free) bitmap (every rank must then skip the overlapped all-gather)
+    vmask = (np.random.default_rng(7).random(n) > 0.3) if rank == 0 else None
+    dkm = np.ones(b[rank + 1] - b[rank], bool) if rank == 1 else None
+    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
+        [ctx.upload(x), ctx.upload(kk), ctx.upload(vv, vmask)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]], dkm),
+        [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
+    assert dx.last_final == "shuffle"
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        VM = np.concatenate([np.random.default_rng(7).random(n) > 0.3] + [np.ones(n, bool)] * (world - 1))
+        wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV, VM)], 1, pred,
+                                              ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
+        assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    # chunked exchange on device tensors, one shard with a bitmap, a tiny chunk (many rounds)
+    D.A2A_CHUNK_BYTES = 4096
+    r = np.random.default_rng(40 + rank)
+    m = 20_000 + 17 * rank
+    a = r.integers(0, 50, m).astype(np.int64)
+    am = (r.random(m) > 0.2) if rank == 0 else None
+    v = r.random(m)
+    got = dx.gather_to_root(dx.shuffle(ctx.upload(a, am), [ctx.upload(a, am), ctx.upload(v)]))
+    if rank == 0:
+        from helpers import rows_of, _key
+        rows = []
+        for q in range(world):
+            rq = np.random.default_rng(40 + q)
+            mq = 20_000 + 17 * q
+            aq = rq.integers(0, 50, mq).astype(np.int64)
+            vm = (rq.random(mq) > 0.2) if q == 0 else np.ones(mq, bool)
+            vq = rq.random(mq)
+            rows += [(int(aq[i]) if vm[i] else None, float(vq[i])) for i in range(mq)]
+        assert sorted(rows_of(got), key=_key) == sorted(rows, key=_key)
+    torch.cuda.synchronize()
+    ctx.set_stream(0)
+    ctx.close()
+
+
+def abi_gen(name):
+    from qe_hip import abi
+    return getattr(abi, "GEN_" + name)
+
+
 def mode_nccl1(rank, world):
     """The RCCL path itself: world_size 1 over the "nccl" backend (device tensors through
     all_gather / all_to_all on the GPU): exchange, shuffle join, partial/final GROUP BY, the
@@ -438,7 +530,8 @@ def main():
     try:
         {"exchange": mode_exchange, "exchange_bytes": mode_exchange_bytes, "exchange_chunked": mode_exchange_chunked,
          "gpu": mode_gpu,
-         "gpu_exchange": mode_gpu_exchange, "gpu_cfg4": mode_gpu_cfg4, "nccl1": mode_nccl1}[mode](rank, world)
+         "gpu_exchange": mode_gpu_exchange, "gpu_cfg4": mode_gpu_cfg4, "nccl1": mode_nccl1,
+         "gpu_devtensors": mode_gpu_devtensors}[mode](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -123,6 +123,16 @@ def test_two_ranks_on_one_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_tensor_collectives_several_ranks_on_one_gpu(world):
+    """The RCCL path's device-tensor code at world size 2 and 3 (collectives over gloo on CUDA
+    tensors, ranks sharing one GPU): config 4's shuffle join and the sharded broadcast join with
+    the overlapped all-gather + adopted prelaunch and the dense final aggregate, vs the oracle;
+    validity agreed across ranks; the chunked all-to-all in many rounds."""
+    launch("gpu_devtensors", world, timeout=600)
+
+
+@pytest.mark.gpu
 def test_rccl_world_size_one():
     """The "nccl" backend (RCCL) with world_size 1 on the GPU: exchange, shuffle join,
     partial/final GROUP BY, the sharded broadcast join and config 4's shuffle join vs the oracle."""

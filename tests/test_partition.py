@@ -225,7 +225,7 @@ def test_filter_partition_hash_move_8_ways_vs_oracle(ctx, int32_key):
     k = r.integers(0, 10_000_000, n).astype(np.int32 if int32_key else np.int64)
     v = r.random(n)
     pred = binop(binop(col(0, "x"), BinaryOp.Greater, lit(49)), BinaryOp.And,
-                 binop(col(0, "x"), BinaryOp.LessEq, lit(97)))
+                 binop(col(0, "x"), BinaryOp.LessEqual, lit(97)))
     counts, moved = ctx.filter_partition_hash_move([ctx.upload(x), ctx.upload(k), ctx.upload(v)], pred, 1, parts,
                                                    [1, 2])
     (fk, _), (fv, _) = ob.filter([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], pred, out_idx=[1, 2])[0]
