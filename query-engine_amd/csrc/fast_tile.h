@@ -1,0 +1,80 @@
+// Fast-path column tiles shared by the fused join-aggregate (k_aggregate.hip) and the fused
+// filter + exchange pass (k_sort.hip): non-null 8-byte columns read as 16-B pairs, every load of a
+// tile issued before the term predicate is evaluated.
+#pragma once
+#include "agg.h"
+#include "device_common.h"
+#include "expr_device.h"
+
+namespace qeh {
+
+constexpr int kFastPairs = 4;
+constexpr int kFastR = 2 * kFastPairs;
+
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+struct FastIn {
+    const int64_t *key;
+    const int64_t *term[2];
+    int32_t term_dt[2];
+    const int64_t *acol[2];
+    int32_t agg_colslot[kMaxAggs];  // which acol an aggregate reads (-1: COUNT of a no-null column)
+};
+
+template <bool NT>
+__device__ __forceinline__ v2i64 ld2(const int64_t *p) {
+    if (NT) return __builtin_nontemporal_load((const v2i64 *)p);
+    return *(const v2i64 *)p;
+}
+
+// One 2048-row tile of the fast-path columns: every load (16-B pairs) issued
+// before the term predicate is evaluated.  Lane rows: base + j*128 + {0,1}.
+template <int NTERMS, int NACOL, bool NT>
+struct FastTile {
+    v2i64 key[kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
+    v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
+    uint32_t sel;
+    __device__ __forceinline__ void load(const FastIn &in, const PredTerms &terms, int64_t base) {
+        issue(in, base);
+        eval(in, terms);
+    }
+    // issue every load of the tile (no use of the data: they stay in flight)
+    __device__ __forceinline__ void issue(const FastIn &in, int64_t base) {
+#pragma unroll
+        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
+#pragma unroll
+        for (int c = 0; c < NACOL; ++c)
+#pragma unroll
+            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
+    }
+    // evaluate the term predicate into `sel`
+    __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
+        sel = (1u << kFastR) - 1u;
+#pragma unroll
+        for (int i = 0; i < NTERMS; ++i) {
+            const PredTerm pt = terms.t[i];
+            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+            uint32_t tr = 0;
+#pragma unroll
+            for (int r = 0; r < kFastR; ++r) {
+                int64_t v = tc[i][r >> 1][r & 1];
+                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
+                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            }
+            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
+            else sel &= tr;
+        }
+    }
+    __device__ __forceinline__ int64_t k(int r) const { return key[r >> 1][r & 1]; }
+    // value of row r for aggregate input slot `cs` (0 or 1)
+    __device__ __forceinline__ int64_t a(int cs, int r) const {
+        return (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
+    }
+};
+
+}  // namespace qeh

@@ -21,6 +21,7 @@
 
 #include "agg.h"
 #include "expr_device.h"
+#include "fast_tile.h"
 #include "ops.h"
 
 namespace qeh {
@@ -28,6 +29,7 @@ namespace qeh {
 constexpr int kAggR = 4;                           // rows per lane
 constexpr int kAggTile = kBlock * kAggR;           // rows per workgroup iteration
 constexpr size_t kLdsStateBudget = 48 * 1024;      // bytes of LDS state per workgroup
+constexpr int kFastTile = kBlock * kFastR;         // 2048 rows per fast-path workgroup iteration
 
 enum GidMode { GM_ZERO = 0, GM_JOIN = 1, GM_GROUP = 2, GM_LDSHASH = 3 };
 enum PredMode { PM_NONE = 0, PM_TERMS = 1, PM_PROG = 2 };
@@ -153,27 +155,6 @@ __global__ __launch_bounds__(kBlock) void k_agg_rows(ColSet cols, int64_t n, Pre
 // wave reads 1 KiB contiguous); all column loads of a tile are issued before
 // the predicate is evaluated, all table probes before any LDS update, so a
 // wave keeps 4 * (1 + terms + agg columns) HBM loads and 8 probes in flight.
-constexpr int kFastPairs = 4;
-constexpr int kFastR = 2 * kFastPairs;
-constexpr int kFastTile = kBlock * kFastR;  // 2048 rows per workgroup iteration
-
-typedef long long v2i64 __attribute__((ext_vector_type(2)));
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-
-struct FastIn {
-    const int64_t *key;
-    const int64_t *term[2];
-    int32_t term_dt[2];
-    const int64_t *acol[2];
-    int32_t agg_colslot[kMaxAggs];  // which acol an aggregate reads (-1: COUNT of a no-null column)
-};
-
-template <bool NT>
-__device__ __forceinline__ v2i64 ld2(const int64_t *p) {
-    if (NT) return __builtin_nontemporal_load((const v2i64 *)p);
-    return *(const v2i64 *)p;
-}
-
 __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, uint32_t &gid) {
     if (key < t.kmin || key > t.kmax) return false;
     if (t.kind == TK_DIRECT) {
@@ -207,55 +188,6 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
     }
     return false;
 }
-
-// One 2048-row tile of the fast-path columns: every load (16-B pairs) issued
-// before the term predicate is evaluated.  Lane rows: base + j*128 + {0,1}.
-template <int NTERMS, int NACOL, bool NT>
-struct FastTile {
-    v2i64 key[kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
-    v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
-    uint32_t sel;
-    __device__ __forceinline__ void load(const FastIn &in, const PredTerms &terms, int64_t base) {
-        issue(in, base);
-        eval(in, terms);
-    }
-    // issue every load of the tile (no use of the data: they stay in flight)
-    __device__ __forceinline__ void issue(const FastIn &in, int64_t base) {
-#pragma unroll
-        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
-#pragma unroll
-        for (int c = 0; c < NACOL; ++c)
-#pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
-    }
-    // evaluate the term predicate into `sel`
-    __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
-        sel = (1u << kFastR) - 1u;
-#pragma unroll
-        for (int i = 0; i < NTERMS; ++i) {
-            const PredTerm pt = terms.t[i];
-            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
-            uint32_t tr = 0;
-#pragma unroll
-            for (int r = 0; r < kFastR; ++r) {
-                int64_t v = tc[i][r >> 1][r & 1];
-                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
-                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
-            }
-            if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
-            else sel &= tr;
-        }
-    }
-    __device__ __forceinline__ int64_t k(int r) const { return key[r >> 1][r & 1]; }
-    // value of row r for aggregate input slot `cs` (0 or 1)
-    __device__ __forceinline__ int64_t a(int cs, int r) const {
-        return (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
-    }
-};
 
 // Apply one tile's rows (mask m, LDS state slot per row) to LDS states laid
 // out [value slot][stride] with row counts in slot 0.  Aggregate kinds are
@@ -1782,7 +1714,7 @@ static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, c
     if (g_bound <= 0 || g_bound >= 0xFFFF || (int64_t)specs.n_slots * g_bound > kSliceStateWords) return QEH_OK;
     const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1ull;
     // the DIRECT rule of build_join_table, and the slice path's own limits
-    if (range == 0 || range > 4 * (uint64_t)cnt + 1024 || range >= (1ull << 32)) return QEH_OK;
+    if (!direct_table_ok(range, (uint64_t)cnt, (uint64_t)g_bound)) return QEH_OK;
     uint64_t min_bytes = 6ull << 20;
     if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
     if (range * 2 < min_bytes) return QEH_OK;

@@ -410,7 +410,7 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
     const uint64_t range = (uint64_t)hm.mx - (uint64_t)hm.mn + 1ull;  // may wrap to 0 for the full int64 range
     const uint64_t nv = hm.cnt;
     int kind = force_kind >= 0 ? force_kind : forced_table_kind();
-    const bool direct_ok = range != 0 && range <= 4 * nv + 1024 && range < (1ull << 32) && payload_max < 0xFFFFFFFEull;
+    const bool direct_ok = direct_table_ok(range, nv, payload_max);
     const int pbits = bits_for(payload_max);
     const int kbits = range == 0 ? 64 : bits_for(range);  // key part holds 1..range
     const bool packed_ok = kbits + pbits <= 64;
@@ -441,10 +441,12 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
                 // alone it is slower (every workgroup reads all keys: 0.75 vs 0.52 ms for 1e7
                 // rows), beside 1e9 probe rows it disturbs phase A less (6.65-6.76 vs 6.85 ms per
                 // metric step, same box).  QEH_INSERT_XCD=0/1 overrides.
-                // QEH_INSERT_XCD=2 (default for the XCD split): keys partitioned into per-range lists
-                // once (k_xcd_lists), each list drained by one XCD; 1: every XCD's workgroups read
-                // all keys and keep their range's (8 key reads)
-                int xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n ? 2 : 0;
+                // QEH_INSERT_XCD=1 (default for the XCD split): every XCD's workgroups read all keys
+                // and keep their range's (8 key reads); 2: keys partitioned into per-range lists once
+                // (k_xcd_lists), each list drained by one XCD
+                // (measured: the list version cuts phase A's interference, 6.67 vs 6.82 ms of kernel
+                // time, but its two dependent kernels finish after phase A: 7.2 vs 7.0 ms per step)
+                int xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n ? 1 : 0;
                 if (const char *e = std::getenv("QEH_INSERT_XCD")) xcd = std::atoi(e);
                 DevBuf lists, cursor;
                 if (xcd == 2 && (n > ((int64_t)1 << 28) || lists.alloc(ctx, (size_t)n * 8 * 8) != QEH_OK ||

@@ -27,6 +27,7 @@
 #include "../../include/qeh_plan.h"
 #include "device_common.h"
 #include "expr_device.h"
+#include "fast_tile.h"
 #include "ops.h"
 
 namespace qeh {
@@ -463,6 +464,190 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
         }
         lds_barrier();
         if (t < kRadix) run[t] += tot_s[t];
+    }
+}
+
+// k_part_scatter for at most kPsDig partitions (an Exchange to the GPUs of one node, config 4's 8):
+// the same stable, run-contiguous placement with the bookkeeping sized to the partitions instead of
+// 256 digits (16 per-wave counters, a 16-lane scan), 8192-row tiles for up to two columns, and rows
+// with an id >= drop (the filtered-out rows) neither ranked nor staged, so the write loop covers only
+// the rows that move.
+constexpr int kPsDig = 16;
+template <int NC>
+__global__ __launch_bounds__(kRsThreads) void k_part_scatter_small(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
+                                                                   const uint64_t *__restrict__ offs, int nblocks, PmCols cols,
+                                                                   uint32_t drop) {
+    constexpr int W = kRsThreads / 64;
+    constexpr int IPT = NC <= 2 ? 8 : 4;
+    constexpr int TILE = kRsThreads * IPT;
+    __shared__ uint64_t s_val[NC > 0 ? NC : 1][TILE];
+    __shared__ uint8_t s_id[TILE];
+    __shared__ uint32_t wcnt[W][kPsDig];  // per-wave counts, then per-wave starts inside the partition
+    __shared__ uint32_t loc[kPsDig], tot_s[kPsDig + 1];
+    __shared__ uint64_t run[kPsDig];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (drop > (uint32_t)kPsDig) drop = kPsDig;
+    if (t < kPsDig) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    uint32_t dgn[IPT];
+    uint64_t vn[IPT][NC > 0 ? NC : 1];
+    auto load = [&](int64_t c0) {
+        const int64_t base = c0 + (int64_t)wave * 64 * IPT + lane;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = base + j * 64;
+            const int64_t ii = i < hi ? i : hi - 1;
+            dgn[j] = ids[ii];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) vn[j][c] = __builtin_nontemporal_load(&cols.src[c][ii]);
+        }
+    };
+    if (lo < hi) load(lo);
+    __syncthreads();  // run[]
+    for (int64_t c0 = lo; c0 < hi; c0 += TILE) {
+        if (t < W * kPsDig) (&wcnt[0][0])[t] = 0u;
+        const int64_t base = c0 + (int64_t)wave * 64 * IPT + lane;
+        uint32_t dg[IPT];
+        uint64_t v[IPT][NC > 0 ? NC : 1];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            dg[j] = dgn[j];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[j][c] = vn[j][c];
+        }
+        if (c0 + TILE < hi) load(c0 + TILE);
+        lds_barrier();
+        uint32_t rk[IPT];
+        bool mv[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            mv[j] = base + j * 64 < hi && dg[j] < drop;
+            rk[j] = mv[j] ? atomicAdd(&wcnt[wave][dg[j]], 1u) : 0u;  // stable (lane-ordered LDS atomics)
+        }
+        lds_barrier();
+        if (t < 64) {  // lane d < kPsDig: per-wave starts inside partition d, its tile total, the scan
+            uint32_t tot = 0;
+            if (lane < kPsDig) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t c = wcnt[w][lane];
+                    wcnt[w][lane] = tot;
+                    tot += c;
+                }
+            }
+            const uint32_t incl = wave_incl_scan(tot);
+            if (lane < kPsDig) loc[lane] = incl - tot, tot_s[lane] = tot;
+            if (lane == kPsDig - 1) tot_s[kPsDig] = incl;  // rows that move in this tile
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            if (mv[j]) {
+                const uint32_t p = loc[dg[j]] + wcnt[wave][dg[j]] + rk[j];
+                s_id[p] = (uint8_t)dg[j];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) s_val[c][p] = v[j][c];
+            }
+        }
+        lds_barrier();
+        const int cnt = (int)tot_s[kPsDig];
+        for (int p = t; p < cnt; p += kRsThreads) {
+            const uint32_t d = s_id[p];
+            const uint64_t pos = run[d] + (uint64_t)(p - (int)loc[d]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) cols.dst[c][pos] = s_val[c][p];
+        }
+        lds_barrier();
+        if (t < kPsDig) run[t] += tot_s[t];
+    }
+}
+
+// Filter + partition ids + per-segment histogram in one pass (config 4's probe side, fewer than
+// kPsDig partitions): block b streams its segment [b * seg, (b + 1) * seg) -- seg a multiple of the
+// 8192-row tile -- with FastTile's 16-B loads of the key and up to two term columns (every load of a
+// tile issued before the predicate), writes the ids as u16 pairs and counts them per partition in
+// byte-packed register counters, so no histogram pass re-reads the id stream.  The generic id pass
+// (k_hash_ids8_pred) evaluated the predicate and loaded the key in two dependent rounds of 4-row
+// loads (3.1 TB/s).  Rows past the last whole tile (the tail of the last segment) go row by row.
+__device__ __forceinline__ uint32_t part_of_key(int64_t k, uint32_t parts) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;  // k_hash_ids8's hash of one non-null key column
+    h = hash64(h ^ (hash64((uint64_t)k) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+    return (uint32_t)(h % parts);
+}
+
+template <int NTERMS>
+__global__ __launch_bounds__(kRsThreads) void k_ids_hist_pred(FastIn in, PredTerms terms, int64_t n, int64_t seg,
+                                                              uint32_t parts, uint8_t *__restrict__ ids,
+                                                              uint32_t *__restrict__ hist, int nblocks) {
+    constexpr int W = kRsThreads / 64, TILE = kRsThreads * kFastR;
+    __shared__ uint32_t wc[W][kPsDig];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    const int64_t full = hi > lo ? lo + (hi - lo) / TILE * TILE : lo;
+    uint32_t cnt[kPsDig];
+#pragma unroll
+    for (int d = 0; d < kPsDig; ++d) cnt[d] = 0u;
+    uint64_t acc[2] = {0ull, 0ull};  // byte counters of partitions 0-7 / 8-15 (flushed before 256)
+    auto flush = [&]() {
+#pragma unroll
+        for (int d = 0; d < kPsDig; ++d) cnt[d] += (uint32_t)(acc[d >> 3] >> (8 * (d & 7))) & 0xFFu;
+        acc[0] = acc[1] = 0ull;
+    };
+    FastTile<NTERMS, 0, true> ft;
+    int tiles = 0;
+    if (lo < full) ft.issue(in, lo + (int64_t)wave * 512 + 2 * lane);
+    for (int64_t t0 = lo; t0 < full; t0 += TILE) {
+        ft.eval(in, terms);
+        uint32_t id[kFastR];
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) id[r] = ((ft.sel >> r) & 1u) ? part_of_key(ft.k(r), parts) : parts;
+        if (t0 + TILE < full) ft.issue(in, t0 + TILE + (int64_t)wave * 512 + 2 * lane);
+        const int64_t base = t0 + (int64_t)wave * 512 + 2 * lane;
+#pragma unroll
+        for (int j = 0; j < kFastPairs; ++j) {
+            *(uint16_t *)(ids + base + j * 128) = (uint16_t)(id[2 * j] | (id[2 * j + 1] << 8));
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t d = id[2 * j + q];
+                const uint64_t one = 1ull << (8 * (d & 7));
+                acc[0] += d < 8 ? one : 0ull;
+                acc[1] += d < 8 ? 0ull : one;
+            }
+        }
+        if (++tiles == 31) {  // 31 tiles x 8 rows < 256 per byte counter
+            flush();
+            tiles = 0;
+        }
+    }
+    flush();
+    for (int64_t i = full + t; i < hi; i += kRsThreads) {  // ragged tail, one row per thread
+        bool ok = NTERMS == 0 || !terms.is_or;
+#pragma unroll
+        for (int q = 0; q < NTERMS; ++q) {
+            const PredTerm pt = terms.t[q];
+            int64_t v = in.term[q][i];
+            if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(in.term_dt[q] == QEH_DT_FLOAT64 ? as_f64(v) : (double)v);
+            const bool tr = cmp_i64(pt.op, v, pt.lit);
+            ok = terms.is_or ? (q == 0 ? tr : (ok || tr)) : (ok && tr);
+        }
+        const uint32_t d = ok ? part_of_key(in.key[i], parts) : parts;
+        ids[i] = (uint8_t)d;
+#pragma unroll
+        for (int e = 0; e < kPsDig; ++e) cnt[e] += d == (uint32_t)e ? 1u : 0u;
+    }
+#pragma unroll
+    for (int d = 0; d < kPsDig; ++d) {
+        uint32_t c = cnt[d];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) wc[wave][d] = c;
+    }
+    __syncthreads();
+    if (t < kPsDig) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) c += wc[w][t];
+        hist[(int64_t)t * nblocks + blockIdx.x] = c;  // digit-major, as k_rs_hist_u8
     }
 }
 
@@ -1730,26 +1915,46 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         for (int c = 0; c < n_cols; ++c)
             if (made[c]) qeh_column_release(ctx, &out_cols[c]);
     };
-    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
-                                               (int64_t)ctx->props.multiProcessorCount);
-    const int64_t seg = (n + nblocks - 1) / nblocks;
+    // one non-null, 16-B aligned Int64 key into at most kPsDig partitions: ids and per-segment
+    // histograms in one pass (k_ids_hist_pred without terms), segments of whole 8192-row tiles
+    const qeh_column &k0 = keys[0];
+    const bool fused = n_keys == 1 && n_parts <= kPsDig && k0.dtype == QEH_DT_INT64 &&
+                       (!k0.validity || k0.null_count == 0) &&
+                       (((uintptr_t)k0.values + (uintptr_t)k0.offset * 8) & 15) == 0 && !std::getenv("QEH_PM_GENERIC");
+    constexpr int64_t kFusedTile = (int64_t)kRsThreads * kFastR;
+    int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
+                                         (int64_t)ctx->props.multiProcessorCount);
+    int64_t seg = (n + nblocks - 1) / nblocks;
+    if (fused) {
+        seg = std::max<int64_t>((seg + kFusedTile - 1) / kFusedTile * kFusedTile, kFusedTile);
+        nblocks = (int)std::max<int64_t>((n + seg - 1) / seg, 1);
+    }
     DevBuf ids, hist, offs;
     QEH_TRY(ids.alloc(ctx, (size_t)std::max<int64_t>(n, 1)));
     QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
     QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
-    std::vector<uint32_t> h((size_t)kRadix * nblocks, 0);
+    const int ndig = fused ? kPsDig : kRadix;  // digits the histogram holds (digit-major)
+    std::vector<uint32_t> h((size_t)ndig * nblocks, 0);
     if (n > 0) {
         KernelTimer kt(ctx, "partition_move");
-        if (n_keys == 1 && keys[0].dtype == QEH_DT_INT64 && (!keys[0].validity || keys[0].null_count == 0))
-            hipLaunchKernelGGL(k_hash_ids8_i64, dim3(grid_for(ctx, (n + 7) / 8, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
-                               (const int64_t *)keys[0].values + keys[0].offset, n, (uint32_t)n_parts, ids.as<uint8_t>());
-        else
-            hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
-                               (uint32_t)n_parts, ids.as<uint8_t>());
-        hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
-                           hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
+        if (fused) {
+            FastIn fin{};
+            fin.key = (const int64_t *)k0.values + k0.offset;
+            hipLaunchKernelGGL(k_ids_hist_pred<0>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, fin, PredTerms{}, n,
+                               seg, (uint32_t)n_parts, ids.as<uint8_t>(), hist.as<uint32_t>(), nblocks);
+        } else {
+            if (n_keys == 1 && k0.dtype == QEH_DT_INT64 && (!k0.validity || k0.null_count == 0))
+                hipLaunchKernelGGL(k_hash_ids8_i64, dim3(grid_for(ctx, (n + 7) / 8, kBlock, 8)), dim3(kBlock), 0,
+                                   ctx->stream, (const int64_t *)k0.values + k0.offset, n, (uint32_t)n_parts,
+                                   ids.as<uint8_t>());
+            else
+                hipLaunchKernelGGL(k_hash_ids8, dim3(grid_for(ctx, n, kBlock * 8, 8)), dim3(kBlock), 0, ctx->stream, hk, n,
+                                   (uint32_t)n_parts, ids.as<uint8_t>());
+            hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
+                               hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
+        }
         QEH_HIP(hipGetLastError());
-        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)ndig * nblocks, nullptr));
         QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));
         for (int p = 0; p < n_parts; ++p)
             for (int b = 0; b < nblocks; ++b) counts[p] += h[(size_t)p * nblocks + b];
@@ -1759,6 +1964,7 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         if ((s = alloc_column(ctx, cols[c].dtype, n, false, &out_cols[c])) != QEH_OK) break;
         made[c] = 1;
     }
+    const bool small = n_parts <= kPsDig && !std::getenv("QEH_PM_GENERIC");
     for (size_t g = 0; s == QEH_OK && g < mv.size() && n > 0; g += kPmMaxCols) {
         PmCols pc{};
         const int nc = (int)std::min<size_t>(kPmMaxCols, mv.size() - g);
@@ -1770,8 +1976,14 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
         }
         KernelTimer kt(ctx, "partition_move");
 #define QEH_PM(NCV)                                                                                                        \
-    hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, \
-                       offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix)
+    do {                                                                                                               \
+        if (small)                                                                                                     \
+            hipLaunchKernelGGL(k_part_scatter_small<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
+                               ids.as<uint8_t>(), n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix);         \
+        else                                                                                                           \
+            hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
+                               n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix);                            \
+    } while (0)
         if (nc == 1) QEH_PM(1);
         else if (nc == 2) QEH_PM(2);
         else if (nc == 3) QEH_PM(3);
@@ -1835,23 +2047,57 @@ extern "C" int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *co
     ColSet cs;
     QEH_TRY(make_colset(cols, n_cols, &cs));
     std::fill(counts, counts + n_parts, 0);
-    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
-                                               (int64_t)ctx->props.multiProcessorCount);
-    const int64_t seg = (n + nblocks - 1) / nblocks;
+    // the fused id + histogram pass: fewer than kPsDig partitions, a non-null Int64 key and term
+    // columns that are non-null 8-byte, 16-B aligned (FastTile's loads)
+    auto fast_ok = [](const qeh_column &c) {
+        return (c.dtype == QEH_DT_INT64 || c.dtype == QEH_DT_FLOAT64) && (!c.validity || c.null_count == 0) &&
+               (((uintptr_t)c.values + (uintptr_t)c.offset * 8) & 15) == 0;
+    };
+    bool fused = n_parts < kPsDig && kc.dtype == QEH_DT_INT64 && fast_ok(kc) && terms.n <= 2 &&
+                 !std::getenv("QEH_PM_GENERIC");
+    FastIn fin{};
+    if (fused) {
+        fin.key = (const int64_t *)kc.values + kc.offset;
+        for (int i = 0; i < terms.n; ++i) {
+            const qeh_column &tc = cols[terms.t[i].col];
+            if (!fast_ok(tc)) fused = false;
+            fin.term[i] = (const int64_t *)tc.values + tc.offset;
+            fin.term_dt[i] = tc.dtype;
+        }
+    }
+    constexpr int64_t kFusedTile = (int64_t)kRsThreads * kFastR;
+    int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kPmTile - 1) / kPmTile, 1),
+                                         (int64_t)ctx->props.multiProcessorCount);
+    int64_t seg = (n + nblocks - 1) / nblocks;
+    if (fused) {  // segments of whole 8192-row tiles (16-B aligned pairs in every segment)
+        seg = std::max<int64_t>((seg + kFusedTile - 1) / kFusedTile * kFusedTile, kFusedTile);
+        nblocks = (int)std::max<int64_t>((n + seg - 1) / seg, 1);
+    }
     DevBuf ids, hist, offs;
     QEH_TRY(ids.alloc(ctx, (size_t)std::max<int64_t>(n, 1)));
     QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
     QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
-    std::vector<uint32_t> h((size_t)kRadix * nblocks, 0);
+    const int ndig = fused ? kPsDig : kRadix;  // digits the histogram holds (digit-major)
+    std::vector<uint32_t> h((size_t)ndig * nblocks, 0);
     int64_t kept = 0;
     if (n > 0) {
         KernelTimer kt(ctx, "partition_move");
-        hipLaunchKernelGGL(k_hash_ids8_pred, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
-                           make_colref(kc), cs, terms, n, (uint32_t)n_parts, ids.as<uint8_t>());
-        hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
-                           hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
+        if (fused) {
+#define QEH_IH(NT)                                                                                                      \
+    hipLaunchKernelGGL(k_ids_hist_pred<NT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, fin, terms, n, seg,      \
+                       (uint32_t)n_parts, ids.as<uint8_t>(), hist.as<uint32_t>(), nblocks)
+            if (terms.n == 0) QEH_IH(0);
+            else if (terms.n == 1) QEH_IH(1);
+            else QEH_IH(2);
+#undef QEH_IH
+        } else {
+            hipLaunchKernelGGL(k_hash_ids8_pred, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                               make_colref(kc), cs, terms, n, (uint32_t)n_parts, ids.as<uint8_t>());
+            hipLaunchKernelGGL(k_rs_hist_u8, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
+                               hist.as<uint32_t>(), nblocks);  // ids are a byte stream: 16 per load
+        }
         QEH_HIP(hipGetLastError());
-        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)ndig * nblocks, nullptr));
         QEH_TRY(read_small(ctx, h.data(), hist.p, h.size() * 4));
         for (int p = 0; p < n_parts; ++p)
             for (int b = 0; b < nblocks; ++b) counts[p] += h[(size_t)p * nblocks + b];
@@ -1869,9 +2115,16 @@ extern "C" int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *co
             pc.dst[q] = (uint64_t *)out_cols[q].values;
         }
         KernelTimer kt(ctx, "partition_move");
+        const bool small = n_parts < kPsDig && !std::getenv("QEH_PM_GENERIC");  // ids 0..n_parts (the drop id)
 #define QEH_FPM(NCV)                                                                                                       \
-    hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg, \
-                       offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts)
+    do {                                                                                                               \
+        if (small)                                                                                                     \
+            hipLaunchKernelGGL(k_part_scatter_small<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
+                               ids.as<uint8_t>(), n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts);        \
+        else                                                                                                           \
+            hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
+                               n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts);                           \
+    } while (0)
         if (n_move == 1) QEH_FPM(1);
         else if (n_move == 2) QEH_FPM(2);
         else if (n_move == 3) QEH_FPM(3);

@@ -809,15 +809,43 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
         uint32_t rank[E];
 #pragma unroll
         for (int r = 0; r < E; ++r) rank[r] = 0u;
+        // ROW_NUMBER / NTILE: rank among the bucket's rows by (order key, position); RANK: by order
+        // key alone (rows of earlier buckets all have smaller keys: buckets are key ranges)
+        constexpr bool kDirect = FN == QEH_WIN_ROW_NUMBER || FN == QEH_WIN_RANK || FN == QEH_WIN_NTILE;
         for (uint32_t j = 0; maxc > 1 && j < maxc; ++j) {
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 const uint32_t st = se[r] & 0xFFFFu, en = se[r] >> 16;
                 if (st + j < en) {
-                    const uint32_t q = L.k[wm_pad(st + j)];
-                    rank[r] += wm_less(L.ov[st + j], q, key[r], (uint32_t)(r * 256 + t)) ? 1u : 0u;
+                    if constexpr (FN == QEH_WIN_RANK) {
+                        rank[r] += L.ov[st + j] < key[r] ? 1u : 0u;
+                    } else {
+                        const uint32_t q = L.k[wm_pad(st + j)];
+                        rank[r] += wm_less(L.ov[st + j], q, key[r], (uint32_t)(r * 256 + t)) ? 1u : 0u;
+                    }
                 }
             }
+        }
+        if constexpr (kDirect) {
+            // the function's value follows from the row's sorted index (ROW_NUMBER, NTILE) or from
+            // the count of smaller keys (RANK) alone: written straight to the row's position in the
+            // group, without materialising the sorted order
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                const int e = r * 256 + t;
+                if (e >= m) continue;
+                const uint32_t i = (se[r] & 0xFFFFu) + rank[r];
+                uint32_t v;
+                if constexpr (FN == QEH_WIN_NTILE) {
+                    const int64_t q = m / f.param, rm = m % f.param, r0 = i;
+                    v = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
+                } else {
+                    v = i + 1u;
+                }
+                res[s + e] = (uint16_t)v;
+            }
+            wm_barrier();  // the group's LDS reads are done before the next group's writes
+            continue;
         }
         wm_barrier();  // every bucket read is done: L.k takes the sorted order
 #pragma unroll

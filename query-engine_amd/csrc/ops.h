@@ -1,5 +1,6 @@
 // Host-side helpers shared between operator translation units.
 #pragma once
+#include <cstdlib>
 
 #include <memory>
 #include <vector>
@@ -37,6 +38,20 @@ struct RowPayload {
     const int64_t *values = nullptr;  // payload = values[i] - bias (frame of reference)
     int64_t bias = 0;
 };
+// DIRECT (perfect-hash) join tables, one entry per key offset: for dense key ranges (<= 4 entries
+// per build row) always; for sparser ranges (<= 32 per row) when the entries are u16 and the table
+// stays <= 512 MB -- e.g. the key shard one rank receives in a hash exchange, 1/N of a dense range,
+// which then takes the LDS-slice pipeline instead of a linear-probing table whose every probe
+// misses L2 (QEH_DIRECT_SPARSE=0 turns the sparse case off).
+inline bool direct_table_ok(uint64_t range, uint64_t nv, uint64_t payload_max) {
+    if (range == 0 || range >= (1ull << 32) || payload_max >= 0xFFFFFFFEull) return false;
+    if (range <= 4 * nv + 1024) return true;
+    static const bool sparse = [] {
+        const char *e = std::getenv("QEH_DIRECT_SPARSE");
+        return !(e && e[0] == '0') && !std::getenv("QEH_NO_U16");
+    }();
+    return sparse && payload_max < 0xFFFFull && range <= 32 * nv && range * 2 <= (512ull << 20);
+}
 // min / max / valid count of an integer column (one synchronous read).
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid);
 // min / max / valid count of several integer columns, one synchronous read.
