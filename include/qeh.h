@@ -267,6 +267,30 @@ int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_column *probe_co
                                         int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
                                         int n_aggs, const int64_t *build_key_range, const int64_t *group_key_range);
 
+/* Broadcast join in table form (the distributed metric path at N > 1; the partial/final stage
+ * shape of distributed/planner.rs:200-249): instead of all-gathering the dimension and building the
+ * whole join table on every rank, each rank inserts its dimension shard into a DIRECT u16 table
+ * over the job-wide key range, the ranks sum their tables (RCCL all-reduce: keys are unique, so
+ * every entry has one writer), and the fused probe runs against the summed table.
+ *   qeh_direct_group_table_insert: table[key - key_min] = (group key - group_min) + 1 for every row
+ *     of this shard; `table` is caller-owned device memory of key_range u16 entries, zeroed by the
+ *     caller; keys must lie in [key_min, key_min + key_range) and group keys in
+ *     [group_min, group_min + 65534) (QEH_E_INVALID otherwise, nothing written out of range).
+ *   qeh_u16_count_nonzero: non-empty entries of such a table (the duplicate check after the sum:
+ *     fewer than the job's build rows means a key repeats, and the caller falls back).
+ *   qeh_join_filter_aggregate_table: qeh_join_filter_aggregate with that table as the join table;
+ *     group g = entry - 1 has key group_min + g (group_dtype Int64 / Int32); only non-empty groups
+ *     are returned.  Adopts a phase A prelaunched (qeh_join_filter_aggregate_prelaunch) for the
+ *     same probe columns, predicate, aggregates and key range. */
+int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
+                                  int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table);
+int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out);
+int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                                    const qeh_expr *predicate, const uint16_t *table, int64_t key_min,
+                                    uint64_t key_range, int64_t group_min, int64_t n_groups, int32_t group_dtype,
+                                    const qeh_agg *aggs, int n_aggs, qeh_column *out_keys, qeh_column *out_aggs,
+                                    int64_t *out_groups);
+
 /* Stable lexicographic sort -> permutation (UINT32 row ids) of the input.
  * Intended semantics of `Sort` (physical_plan.rs:40-44; executor.rs:290-297
  * is the identity): per-key ascending flag, NULLs first, floats totalOrder. */

@@ -2583,6 +2583,80 @@ extern "C" int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_colum
     return QEH_OK;
 }
 
+__global__ void k_seq_i64(int64_t *p, int64_t n, int64_t base, int as32) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (as32) ((int32_t *)p)[i] = (int32_t)(base + i);
+        else p[i] = base + i;
+    }
+}
+
+// The fused operator against a join table built elsewhere (the summed DIRECT u16 table of the
+// table-form broadcast join, include/qeh.h): group g = entry - 1, key group_min + g.  The group
+// keys are a synthesised column group_min + [0, G) with representative row g, so the aggregate and
+// finalize are qeh_join_filter_aggregate's own.
+extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                               int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
+                                               int64_t key_min, uint64_t key_range, int64_t group_min, int64_t n_groups,
+                                               int32_t group_dtype, const qeh_agg *aggs, int n_aggs, qeh_column *out_keys,
+                                               qeh_column *out_aggs, int64_t *out_groups) {
+    if (!ctx || !out_groups || !table || key_range == 0 || key_range >= (1ull << 32) || n_groups < 1 ||
+        n_groups >= 0xFFFE || (group_dtype != QEH_DT_INT64 && group_dtype != QEH_DT_INT32))
+        return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table: bad argument");
+    *out_groups = 0;
+    if (n_aggs == 0) return QEH_OK;
+    if (probe_key_idx < 0 || probe_key_idx >= n_probe_cols) return fail(QEH_E_INVALID, "probe key index out of range");
+    const int64_t n = probe_cols[0].length;
+    for (int i = 0; i < n_probe_cols; ++i)
+        if (probe_cols[i].length != n) return fail(QEH_E_INVALID, "probe columns have different lengths");
+    DeviceGuard dg(ctx->device);
+    ColSet cols;
+    QEH_TRY(make_colset(probe_cols, n_probe_cols, &cols));
+    std::vector<int32_t> dts(n_probe_cols);
+    std::vector<int> idx(n_probe_cols);
+    for (int i = 0; i < n_probe_cols; ++i) {
+        dts[i] = probe_cols[i].dtype;
+        idx[i] = i;
+    }
+    PredPlan pp;
+    QEH_TRY(plan_predicate(predicate, dts.data(), n_probe_cols, &pp));
+    AggSpecs specs;
+    QEH_TRY(plan_aggs(aggs, n_aggs, probe_cols, n_probe_cols, idx.data(), &specs));
+    if (probe_cols[probe_key_idx].dtype != QEH_DT_INT64 && probe_cols[probe_key_idx].dtype != QEH_DT_INT32)
+        return fail(QEH_E_UNSUPPORTED, "hash join keys must be Int32/Int64 on the device");
+    SlicePre pre;
+    std::shared_ptr<PendingSlice> pend = std::static_pointer_cast<PendingSlice>(ctx->pending_slice);
+    ctx->pending_slice.reset();
+    if (pend && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs)) pend->take(&pre);
+    pend.reset();  // not adopted: waits for its phase A, frees its regions
+    // (try_slice_join adopts `pre` only for this table's key range and tile count)
+    DevBuf gkeys, rep;
+    QEH_TRY(gkeys.alloc(ctx, (size_t)n_groups * 8));
+    QEH_TRY(rep.alloc(ctx, (size_t)n_groups * 4));
+    const int g = grid_for(ctx, n_groups, kBlock, 1);
+    hipLaunchKernelGGL(k_seq_i64, dim3(g), dim3(kBlock), 0, ctx->stream, gkeys.as<int64_t>(), n_groups, group_min,
+                       group_dtype == QEH_DT_INT32 ? 1 : 0);
+    hipLaunchKernelGGL(k_iota, dim3(g), dim3(kBlock), 0, ctx->stream, rep.as<uint32_t>(), n_groups);
+    QEH_HIP(hipGetLastError());
+    qeh_column kc{};
+    kc.dtype = group_dtype;
+    kc.length = n_groups;
+    kc.values = gkeys.p;
+    KeyCols keys{};
+    keys.n = 1;
+    keys.c[0] = make_colref(kc);
+    GidSource src{};
+    src.jt.kind = TK_DIRECT;
+    src.jt.payload16 = const_cast<uint16_t *>(table);
+    src.jt.kmin = key_min;
+    src.jt.kmax = (int64_t)((uint64_t)key_min + key_range - 1ull);
+    src.jt.range = key_range;
+    src.jt.unique = 1;
+    src.key_col = probe_key_idx;
+    const int32_t kd = group_dtype;
+    return aggregate_rows(ctx, GM_JOIN, cols, n, pp, src, specs, n_groups, keys, &kd, rep.as<uint32_t>(), true,
+                          "join_filter_aggregate", out_keys, out_aggs, out_groups, &pre);
+}
+
 extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
                                          int probe_key_idx, const qeh_expr *predicate, const qeh_column *build_key,
                                          const qeh_column *build_group_keys, int n_group_keys, const qeh_agg *aggs,

@@ -307,6 +307,69 @@ __global__ void k_wide_dups(ColRef key, int64_t n, HashTable t, uint32_t *dup) {
     }
 }
 
+// Broadcast join in table form (qeh_direct_group_table_insert): this rank's shard into the shared
+// DIRECT u16 table, entry = group slot + 1; out-of-range keys / group keys and NULL group keys flag
+// `bad` and are not written (NULL join keys never match and are skipped).
+__global__ void k_direct_group_insert(ColRef key, ColRef gkey, int64_t n, int64_t kmin, uint64_t range, int64_t gmin,
+                                      uint16_t *__restrict__ table, uint32_t *__restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        const uint64_t o = (uint64_t)load_i64(key, i) - (uint64_t)kmin;
+        const uint64_t g = (uint64_t)load_i64(gkey, i) - (uint64_t)gmin;
+        if (o >= range || !col_valid(gkey, i) || g >= 0xFFFEull) {
+            *bad = 1u;
+            continue;
+        }
+        table[o] = (uint16_t)(g + 1u);
+    }
+}
+
+extern "C" int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
+                                             int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table) {
+    if (!ctx || !build_key || !group_key || !table || key_range == 0)
+        return fail(QEH_E_INVALID, "qeh_direct_group_table_insert: bad argument");
+    if (build_key->length != group_key->length) return fail(QEH_E_INVALID, "build columns have different lengths");
+    for (const qeh_column *c : {build_key, group_key}) {
+        QEH_TRY(check_column(*c, "table build column"));
+        if (c->dtype != QEH_DT_INT64 && c->dtype != QEH_DT_INT32)
+            return fail(QEH_E_UNSUPPORTED, "table build columns must be Int32 / Int64");
+    }
+    DeviceGuard dg(ctx->device);
+    const int64_t n = build_key->length;
+    DevBuf bad;
+    QEH_TRY(bad.alloc(ctx, 8));
+    QEH_HIP(hipMemsetAsync(bad.p, 0, 8, ctx->stream));
+    if (n > 0) {
+        KernelTimer kt(ctx, "join_build");
+        hipLaunchKernelGGL(k_direct_group_insert, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                           make_colref(*build_key), make_colref(*group_key), n, key_min, key_range, group_min, table,
+                           bad.as<uint32_t>());
+        QEH_HIP(hipGetLastError());
+    }
+    uint32_t b = 0;
+    QEH_TRY(read_small(ctx, &b, bad.p, 4));
+    if (b) return fail(QEH_E_INVALID, "qeh_direct_group_table_insert: key or group key outside the given range (or NULL group key)");
+    return QEH_OK;
+}
+
+extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out) {
+    if (!ctx || !out || (n > 0 && !table)) return fail(QEH_E_INVALID, "qeh_u16_count_nonzero: bad argument");
+    DeviceGuard dg(ctx->device);
+    *out = 0;
+    if (n == 0) return QEH_OK;
+    DevBuf c;
+    QEH_TRY(c.alloc(ctx, 8));
+    QEH_HIP(hipMemsetAsync(c.p, 0, 8, ctx->stream));
+    const int gc = grid_for(ctx, (int64_t)(n / 8 + 1), kBlock * 4, 1);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)table, n, 2,
+                       c.as<unsigned long long>());
+    QEH_HIP(hipGetLastError());
+    unsigned long long v = 0;
+    QEH_TRY(read_small(ctx, &v, c.p, 8));
+    *out = (int64_t)v;
+    return QEH_OK;
+}
+
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid) {
     return columns_minmax(ctx, &col, 1, mn, mx, valid);
 }

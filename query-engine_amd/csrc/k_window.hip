@@ -92,6 +92,9 @@ struct WmShape {
     int32_t nb;        // buckets (high digits in use)
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
+    int32_t exp;       // QEH_WM_EXP (experiments only, results wrong): pass 1 / 2 bit 0 no key-bit stores,
+                       // bit 1 no order-key stores, bit 2 no write loop, bit 3 (with 2) no ranking
+    int32_t nts;       // QEH_WM_NTS: bit 0 pass 1, bit 1 pass 2 write their runs with non-temporal stores
 };
 
 // ---- pass 1: histogram of the high key digit per workgroup row range -------------------------
@@ -371,7 +374,13 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
             ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
-        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
+        uint32_t tcnt = 0;
+        if (sh.exp & 8) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) slot[j] = (uint32_t)(wave * 64 * NJ + j * 64 + lane);
+        } else {
+            tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             if (!live[j]) continue;
@@ -381,12 +390,19 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
         }
         wm_barrier();
         const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+        if (!(sh.exp & 4)) {
 #pragma unroll 8
-        for (int s = tid; s < m; s += kWmBlock) {
-            const uint32_t dd = st_d[s];
-            const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-            o_key[p] = st_key[s];
-            o_kl[p] = st_kl[s];
+            for (int s = tid; s < m; s += kWmBlock) {
+                const uint32_t dd = st_d[s];
+                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                if (sh.nts & 1) {
+                    if (!(sh.exp & 2)) __builtin_nontemporal_store(st_key[s], o_key + p);
+                    if (!(sh.exp & 1)) __builtin_nontemporal_store(st_kl[s], o_kl + p);
+                } else {
+                    if (!(sh.exp & 2)) o_key[p] = st_key[s];
+                    if (!(sh.exp & 1)) o_kl[p] = st_kl[s];
+                }
+            }
         }
         wm_barrier();
         lpos[tid] += tcnt;
@@ -467,7 +483,8 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     #pragma unroll 8
         for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
-                o_key[lpos[dd] + (uint32_t)s - R.lofs[dd]] = st_key[s];
+                if (sh.nts & 2) __builtin_nontemporal_store(st_key[s], o_key + lpos[dd] + (uint32_t)s - R.lofs[dd]);
+                else o_key[lpos[dd] + (uint32_t)s - R.lofs[dd]] = st_key[s];
             }
             wm_barrier();
             lpos[tid] += tcnt;
@@ -1107,11 +1124,16 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
 #undef QEH_WM_P1
+        if (!sh.exp)  // (experiment runs: pass 1 only)
         hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
                            bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
                            pst.as<uint64_t>());
     }
     QEH_HIP(hipGetLastError());
+    if (sh.exp) {  // experiment runs stop after the partition passes (their outputs are not valid)
+        QEH_HIP(hipStreamSynchronize(ctx->stream));
+        return fail(QEH_E_UNSUPPORTED, "QEH_WM_EXP: experiment run, partition passes only");
+    }
     key1.reset();
     DevBuf fbl;  // groups the counting sort queues for the network: count, then group numbers
     if (res2.alloc(ctx, n * 2) || fbl.alloc(ctx, (sh.nparts + 1) * 4) || (value_fn && res2v.alloc(ctx, n * 8)))
@@ -1248,6 +1270,8 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     }
     sh.nb = (int32_t)(((range - 1) >> sh.lb) + 1);
     sh.nparts = (int64_t)range;
+    if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
+    if (const char *e = std::getenv("QEH_WM_NTS")) sh.nts = std::atoi(e);
     const int cus = ctx->props.multiProcessorCount;
     // pass-1 workgroups (row spans): two per CU by default, so the replaying inverse pass (80 KB of
     // LDS) runs two per CU and one's barrier phases overlap the other's memory phases

@@ -83,6 +83,10 @@ SIGNATURES = {
     "qeh_join_filter_aggregate": (I, [P, COLP, I, I, EXPRP, COLP, COLP, I, AGGP, I, COLP, COLP,
                                       C.POINTER(I64)]),
     "qeh_join_filter_aggregate_prelaunch": (I, [P, COLP, I, I, EXPRP, AGGP, I, C.POINTER(I64), C.POINTER(I64)]),
+    "qeh_direct_group_table_insert": (I, [P, COLP, COLP, I64, U64, I64, P]),
+    "qeh_u16_count_nonzero": (I, [P, P, U64, C.POINTER(I64)]),
+    "qeh_join_filter_aggregate_table": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, I64, C.c_int32, AGGP, I, COLP, COLP,
+                                            C.POINTER(I64)]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_sort_indices_nulls": (I, [P, COLP, I, C.POINTER(C.c_int8), C.POINTER(C.c_int8), COLP]),
     "qeh_concat": (I, [P, COLP, I, COLP]),

@@ -366,6 +366,36 @@ class Context:
         return ([self._wrap(ok[i]) for i in range(len(build_group_keys))],
                 [self._wrap(oa[i]) for i in range(len(aggs))], g.value)
 
+    def direct_group_table_insert(self, build_key: DeviceColumn, group_key: DeviceColumn, key_min: int,
+                                  key_range: int, group_min: int, table_ptr: int) -> None:
+        """qeh_direct_group_table_insert: this shard's rows into the caller's zeroed u16 table."""
+        abi.check(self.lib.qeh_direct_group_table_insert(self.h, C.byref(build_key.c), C.byref(group_key.c), key_min,
+                                                         key_range, group_min, table_ptr))
+
+    def u16_count_nonzero(self, table_ptr: int, n: int) -> int:
+        out = C.c_int64()
+        abi.check(self.lib.qeh_u16_count_nonzero(self.h, table_ptr, n, C.byref(out)))
+        return out.value
+
+    def join_filter_aggregate_table(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                                    predicate: Optional[PhysicalExpr], table_ptr: int, key_min: int, key_range: int,
+                                    group_min: int, n_groups: int, group_dtype: int, aggs: Sequence[Tuple[int, int]]):
+        """qeh_join_filter_aggregate_table: the fused operator against a DIRECT u16 table of
+        (group slot + 1) entries (the table-form broadcast join)."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        ok = (abi.QehColumn * 1)()
+        oa = (abi.QehColumn * max(len(aggs), 1))()
+        g = C.c_int64()
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        abi.check(self.lib.qeh_join_filter_aggregate_table(self.h, cp, len(probe_cols), probe_key_idx,
+                                                           C.byref(e) if e is not None else None, table_ptr, key_min,
+                                                           key_range, group_min, n_groups, group_dtype, ca, len(aggs),
+                                                           ok, oa, C.byref(g)))
+        return [self._wrap(ok[0])], [self._wrap(oa[i]) for i in range(len(aggs))], g.value
+
     def join_filter_aggregate_prelaunch(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                                         predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],
                                         build_key_range: Sequence[int], group_key_range: Sequence[int]) -> None:

@@ -495,10 +495,17 @@ class DistributedExecutor:
     def join_filter_aggregate_broadcast(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
                                         aggs, build_sharded: bool = False):
         """Broadcast join (the BASELINE metric path): `probe_cols` = this rank's fact shard.
-        With build_sharded, `build_*` are this rank's shard of the dimension and are all-gathered
-        first (over RCCL under "nccl"); otherwise they are replicated already.  Then the fused
-        local pipeline, and the partial per-group states are shuffled by group key and merged on
-        the owning rank (partial/final aggregate, distributed/planner.rs:200-249)."""
+        With build_sharded, `build_*` are this rank's shard of the dimension.  Two forms:
+          * table (default when the shape allows it, _broadcast_table): every rank inserts its
+            dimension shard into a DIRECT u16 table over the job-wide key range and the ranks sum
+            the tables (one RCCL all-reduce of range x 2 B) -- each rank builds 1/N of the table
+            and receives a table, not the dimension;
+          * all-gather: the dimension shards are all-gathered (over RCCL under "nccl") and every
+            rank builds the whole table.
+        Otherwise `build_*` are replicated already.  Then the fused local pipeline, and the partial
+        per-group states are merged on the owning rank (partial/final aggregate,
+        distributed/planner.rs:200-249): one dense all-reduce for a bounded integer group key,
+        else a shuffle of the partial states."""
         for f, _ in aggs:
             if f not in FINAL_OF:
                 raise NotImplementedError("distributed AVG needs SUM+COUNT partials; compose it from them")
@@ -506,11 +513,22 @@ class DistributedExecutor:
         # shard's bitmaps; the final stage's choice of collectives must be the same on every rank)
         probe_flags = [1 if probe_cols[c].c.validity else 0 for _, c in aggs]
         probe_nullable = None
+        self.last_build = "replicated"
         if build_sharded:
-            full, probe_nullable = self._allgather_beside_phase_a(probe_cols, probe_key_idx, predicate, build_key,
-                                                                  build_group_keys, aggs, probe_flags)
+            st = self._build_stats(build_key, build_group_keys, probe_flags)
+            full = None
+            if st is not None:
+                probe_nullable = st["agreed"]
+                if not os.environ.get("QEH_NO_TABLE_BCAST"):
+                    out = self._broadcast_table(st, probe_cols, probe_key_idx, predicate, build_key, build_group_keys,
+                                                aggs, probe_nullable)
+                    if out is not None:
+                        self.last_build = "table"
+                        return out
+                full = self._allgather_beside_phase_a(st, probe_cols, probe_key_idx, predicate, aggs)
             if full is None:
                 full = self.allgather_columns([build_key] + list(build_group_keys))
+            self.last_build = "allgather"
             build_key, build_group_keys = full[0], full[1:]
         if probe_nullable is None:
             probe_nullable = self._agree_max(probe_flags)
@@ -518,7 +536,13 @@ class DistributedExecutor:
                                                     build_group_keys, aggs)
         if g == 0:
             pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
-        dense = self._final_dense(build_group_keys, probe_nullable, pk, pa_, aggs)
+        gcol = build_group_keys[0] if len(build_group_keys) == 1 else None
+        dense = None
+        if gcol is not None and gcol.dtype in (abi.DT_INT64, abi.DT_INT32) and not gcol.c.validity and len(gcol):
+            self._sync()
+            gk = self._to_tensors(gcol)[0]
+            lo, hi = (int(q) for q in torch.stack([gk.min().to(torch.int64), gk.max().to(torch.int64)]).tolist())
+            dense = self._final_dense(lo, hi, probe_nullable, pk, pa_, aggs)
         self.last_final = "dense" if dense is not None else "shuffle"
         if dense is not None:
             return dense
@@ -533,20 +557,16 @@ class DistributedExecutor:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t.cpu().numpy()
 
-    def _allgather_beside_phase_a(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs,
-                                  probe_flags: Sequence[int]):
-        """The dimension all-gather overlapped with phase A of the fused operator: one small
-        all_gather of every shard's [rows, key min / max, group key min / max, has-validity flags]
-        gives the full build side's ranges, the padded column all-gathers are issued asynchronously,
-        phase A is launched from the ranges (qeh_join_filter_aggregate_prelaunch) while they run, and
-        only then does the queue wait for them.  Returns (columns, agreed probe_flags); columns are
-        None when the shape does not allow it (the caller all-gathers first).  Every branch after
-        the small all_gather depends only on gathered values, so all ranks take the same one (a
-        bitmap on any rank's build shard sends every rank to allgather_columns)."""
+    def _build_stats(self, build_key, build_group_keys, probe_flags: Sequence[int]):
+        """One small all_gather of every dimension shard's [rows, key min / max, group key min / max,
+        has-bitmap] and the fact shard's aggregate-input bitmap flags: the job-wide ranges both
+        device broadcast forms plan from.  None when the shape is outside them (decided from
+        schema-level facts, identical on every rank).  Every later branch depends only on gathered
+        values, so all ranks take the same one."""
         cols = [build_key] + list(build_group_keys)
-        if (self.world == 1 or self.device != "cuda" or len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
+        if (self.device != "cuda" or len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
                 or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32)):
-            return None, None
+            return None
         n = len(build_key)
         ts = [self._to_tensors(c)[0] for c in cols]
         self._sync()  # the shard columns may still be in flight on the library's queue
@@ -560,14 +580,63 @@ class DistributedExecutor:
         else:
             st = torch.cat([torch.tensor([0, big, small, big, small], dtype=torch.int64, device=self.device), flags])
         M = _allgather_meta_t(st, self.world, self.group)
-        agreed = M[:, 6:].max(axis=0)
         rows = [int(x) for x in M[:, 0]]
-        total, mx = sum(rows), max(rows)
-        if total == 0 or M[:, 5].max() > 0:
-            return None, agreed
-        live = M[M[:, 0] > 0]
-        krange = [int(live[:, 1].min()), int(live[:, 2].max()), total]
-        grange = [int(live[:, 3].min()), int(live[:, 4].max()), total]
+        total = sum(rows)
+        out = {"M": M, "rows": rows, "total": total, "n": n, "ts": ts, "bitmap": bool(M[:, 5].max() > 0),
+               "agreed": M[:, 6:].max(axis=0), "gdtype": build_group_keys[0].dtype}
+        if total:
+            live = M[M[:, 0] > 0]
+            out["krange"] = [int(live[:, 1].min()), int(live[:, 2].max()), total]
+            out["grange"] = [int(live[:, 3].min()), int(live[:, 4].max()), total]
+        return out
+
+    def _broadcast_table(self, st, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs,
+                         probe_nullable):
+        """The table form of the broadcast join: phase A is launched from the job-wide key range
+        (qeh_join_filter_aggregate_prelaunch), this rank's dimension shard goes into a zeroed DIRECT
+        u16 table over that range (entry = group slot + 1, qeh_direct_group_table_insert), one RCCL
+        all-reduce sums the ranks' tables (unique keys: one writer per entry), and the fused probe
+        runs against the sum (qeh_join_filter_aggregate_table).  A repeated key shows as fewer
+        non-empty entries than build rows -- the same count on every rank, since every rank holds
+        the same summed table -- and returns None (the caller all-gathers instead).  None too when
+        the shape does not fit: NULLs, a key range above 4 x rows, more than 4096 groups."""
+        total = st["total"]
+        if st["bitmap"] or not total:
+            return None
+        kmin, kmax, _ = st["krange"]
+        gmin, gmax, _ = st["grange"]
+        R, G = kmax - kmin + 1, gmax - gmin + 1
+        if R > 4 * total + 1024 or R >= (1 << 31) or G > 4096 or self.world * (G + 1) >= (1 << 16):
+            return None
+        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"], st["grange"])
+        table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
+        self._sync_torch()  # zeroed before the library writes
+        if st["n"]:
+            self.ctx.direct_group_table_insert(build_key, build_group_keys[0], kmin, R, gmin, table.data_ptr())
+        self._sync()
+        if self.world > 1:
+            dist.all_reduce(table, op=dist.ReduceOp.SUM, group=self.group)  # u16 pairs: no carries (checked above)
+        self._sync_torch()
+        if self.ctx.u16_count_nonzero(table.data_ptr(), R) != total:
+            return None  # a build key repeats: the general path handles multi-match joins
+        pk, pa_, g = self.ctx.join_filter_aggregate_table(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
+                                                          R, gmin, G, st["gdtype"], aggs)
+        if g == 0:
+            pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
+        dense = self._final_dense(gmin, gmax, probe_nullable, pk, pa_, aggs)
+        self.last_final = "dense" if dense is not None else "shuffle"
+        return dense if dense is not None else self._final(pk, pa_, aggs)
+
+    def _allgather_beside_phase_a(self, st, probe_cols, probe_key_idx, predicate, aggs):
+        """The dimension all-gather overlapped with phase A of the fused operator: with the
+        job-wide ranges of _build_stats, the padded column all-gathers are issued asynchronously,
+        phase A is launched from the ranges (qeh_join_filter_aggregate_prelaunch) while they run,
+        and only then does the queue wait for them.  None when the shape does not allow it (the
+        caller all-gathers first)."""
+        if self.world == 1 or st["bitmap"] or not st["total"]:
+            return None
+        rows, n, ts = st["rows"], st["n"], st["ts"]
+        mx = max(rows)
         bufs, works = [], []
         for t in ts:
             if n < mx:
@@ -577,37 +646,34 @@ class DistributedExecutor:
             buf = torch.empty(self.world * mx, dtype=t.dtype, device=t.device)
             works.append(dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group, async_op=True))
             bufs.append(buf)
-        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, krange, grange)
+        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"], st["grange"])
         for w in works:
             w.wait()
         out = []
-        for c, buf in zip(cols, bufs):
+        dts = [abi.DT_INT64, st["gdtype"]]
+        for dt, buf in zip(dts, bufs):
             if any(r != mx for r in rows):
                 buf = torch.cat([buf[q * mx:q * mx + rows[q]] for q in range(self.world)])
-            out.append(self._from_tensors(c.dtype, buf, None))
+            out.append(self._from_tensors(dt, buf, None))
         self._sync_torch()
-        return out, agreed
+        return out
 
     DENSE_MAX_KEYS = 1 << 20
 
-    def _final_dense(self, build_group_keys, probe_nullable, pk, pa_, aggs):
+    def _final_dense(self, lo: int, hi: int, probe_nullable, pk, pa_, aggs):
         """Final aggregate of a broadcast join by all-reduce instead of a shuffle, when the single
-        group key is a non-null integer column of the (replicated) dimension whose range spans at
-        most DENSE_MAX_KEYS values: every rank scatters its partial states into dense arrays
-        indexed by key - min, one all_reduce per reduction op (SUM for float SUMs, COUNTs and a
+        group key is a non-null integer of the (whole) dimension whose job-wide range [lo, hi] spans
+        at most DENSE_MAX_KEYS values: every rank scatters its partial states into dense arrays
+        indexed by key - lo, one all_reduce per reduction op (SUM for float SUMs, COUNTs and a
         presence flag; SUM / MIN / MAX over int64 for integer aggregates) merges them, and each
-        rank keeps the groups with (key - min) % world == rank.  Same result as _final (partial
-        states merged per group, each group on one rank) with one or two collectives and one host
-        read (the key range) instead of a partition kernel, a metadata all_gather, an all-to-all
-        per column and a hash aggregate.  None when not applicable (the caller shuffles).
-        probe_nullable[j]: aggregate j's input has a bitmap on some rank (agreed across ranks); the
-        group column is the replicated dimension's, identical on every rank, so every rank decides
-        the same way."""
-        if len(build_group_keys) != 1 or len(pk) != 1:
+        rank keeps the groups with (key - lo) % world == rank.  Same result as _final (partial
+        states merged per group, each group on one rank) with one or two collectives instead of a
+        partition kernel, a metadata all_gather, an all-to-all per column and a hash aggregate.
+        None when not applicable (the caller shuffles).  probe_nullable[j]: aggregate j's input has
+        a bitmap on some rank (agreed across ranks); lo / hi are the same on every rank, so every
+        rank decides the same way."""
+        if len(pk) != 1:
             return None
-        gcol = build_group_keys[0]
-        if gcol.dtype not in (abi.DT_INT64, abi.DT_INT32) or gcol.c.validity:
-            return None  # (no NULL group key: the key comes from this column through an INNER join)
         kinds = []
         for j, ((f, c), col) in enumerate(zip(aggs, pa_)):
             # partial states can be NULL only where an input value can (all-NULL group)
@@ -616,14 +682,11 @@ class DistributedExecutor:
             if f in (AF.Min, AF.Max) and col.dtype not in (abi.DT_INT64, abi.DT_INT32):
                 return None  # float MIN / MAX keep the shuffle (total-order semantics)
             kinds.append(f)
-        self._sync()
-        gk = self._to_tensors(gcol)[0]
-        if gk.shape[0] == 0:
-            return None
-        lo, hi = (int(q) for q in torch.stack([gk.min().to(torch.int64), gk.max().to(torch.int64)]).tolist())
         R = hi - lo + 1
-        if R > self.DENSE_MAX_KEYS:
+        if R > self.DENSE_MAX_KEYS or R <= 0:
             return None
+        self._sync()
+        gk = self._to_tensors(pk[0])[0]
         dev = gk.device
         idx = self._to_tensors(pk[0])[0].to(torch.int64) - lo
         vals = [self._to_tensors(c)[0] for c in pa_]

@@ -338,6 +338,9 @@ def check_metric_plans(rank, world, dx, ctx):
             keys, aggs_out, ng = fn(fact, 1, pred, ctx.upload(dk), [ctx.upload(dg)], aggs)
             if name == "broadcast":
                 assert dx.last_final == final, (dx.last_final, final)
+                # the dimension repeats a key: the table form (device payloads) detects it and falls back
+                if dx.device == "cuda":
+                    assert dx.last_build == "allgather", dx.last_build
             res = dx.gather_to_root(keys + aggs_out)
             if rank == 0:
                 assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=floats), name
@@ -415,6 +418,7 @@ def mode_gpu_devtensors(rank, world):
     launches = ctx.kernel_time("slice_partition")[1]
     ctx.timing(False)
     assert dx.last_final == "dense"
+    assert dx.last_build == "table", dx.last_build  # each rank inserted its shard, the tables were summed
     assert launches == 1, launches  # the prelaunched phase A was adopted (not re-run)
     res = dx.gather_to_root(keys + aggs_out)
     if rank == 0:
@@ -433,6 +437,7 @@ def mode_gpu_devtensors(rank, world):
         [ctx.upload(x), ctx.upload(kk), ctx.upload(vv, vmask)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]], dkm),
         [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
     assert dx.last_final == "shuffle"
+    assert dx.last_build == "allgather"  # a bitmap on one rank's dimension shard: no table form
     res = dx.gather_to_root(keys + aggs_out)
     if rank == 0:
         VM = np.concatenate([np.random.default_rng(7).random(n) > 0.3] + [np.ones(n, bool)] * (world - 1))

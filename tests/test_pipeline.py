@@ -286,6 +286,45 @@ def test_metric_full_size_properties(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shards,dup", [(1, False), (3, False), (3, True)])
+def test_table_form_broadcast_join_vs_oracle(ctx, shards, dup):
+    """The table form of the distributed broadcast join on one device: every dimension shard is
+    inserted into its own zeroed DIRECT u16 table over the job-wide key range
+    (qeh_direct_group_table_insert), the tables are summed (the RCCL all-reduce's stand-in), the
+    non-empty count is the duplicate check (qeh_u16_count_nonzero), and the fused probe against the
+    sum (qeh_join_filter_aggregate_table) equals the oracle's join + filter + group-by."""
+    import torch
+    n_fact, n_dim = 5_000_000, 3_000_000
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 1000)
+    if dup:
+        dk[5] = dk[6]
+    kmin, R = int(dk.min()), int(dk.max() - dk.min() + 1)
+    gmin, G = int(dg.min()), int(dg.max() - dg.min() + 1)
+    b = np.linspace(0, n_dim, shards + 1).astype(int)
+    total = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")
+    for i in range(shards):
+        t = torch.zeros_like(total)
+        torch.cuda.synchronize()
+        ctx.direct_group_table_insert(ctx.upload(dk[b[i]:b[i + 1]]), ctx.upload(dg[b[i]:b[i + 1]]), kmin, R, gmin,
+                                      t.data_ptr())
+        total += t
+    torch.cuda.synchronize()
+    filled = ctx.u16_count_nonzero(total.data_ptr(), R)
+    if dup:
+        assert filled == n_dim - 1  # the repeated key is visible, so the caller falls back
+        return
+    assert filled == n_dim
+    gk, ga, g = ctx.join_filter_aggregate_table([ctx.upload(x), ctx.upload(k), ctx.upload(v)], 1, PRED,
+                                                total.data_ptr(), kmin, R, gmin, G, abi.DT_INT64, AGGS)
+    wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(dk),
+                                          [ob.HostCol(dg)], AGGS)
+    assert g == wg
+    assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
+    with pytest.raises(abi.QehError):  # a key outside the declared range is refused, nothing written
+        ctx.direct_group_table_insert(ctx.upload(dk[:10] + R), ctx.upload(dg[:10]), kmin, R, gmin, total.data_ptr())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("parts,rank", [(8, 3), (24, 0)])
 def test_sparse_direct_build_shard_vs_oracle(ctx, parts, rank):
     """The build side one rank of a hash-partitioned join receives (config 4 at N ranks): the dim
