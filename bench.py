@@ -13,11 +13,16 @@ the dim hash table, probe + filter + aggregate every fact row, finalize the
 groups, and for N>1 the RCCL exchanges.
 
 Default workload (the metric, strong scaling): 1e9 fact rows in total, split
-across the N GPUs (torchrun, one rank per GPU); the dim is sharded too and
-all-gathered over RCCL inside the step (broadcast join), the partial per-group
-states are shuffled by group key over RCCL all-to-all and merged on the owning
-rank (the reference's partial/final aggregate stage shape,
-crates/query-distributed/src/planner.rs:200-249).
+across the N GPUs (torchrun, one rank per GPU); the dim is sharded too.  Inside
+the step (broadcast join, DistributedExecutor.join_filter_aggregate_broadcast):
+each rank inserts its dim shard into a DIRECT u16 table over the job-wide key
+range and one RCCL all-reduce sums the tables (the table form; phase A of the
+probe runs meanwhile), the fused probe runs against the summed table, and the
+partial per-group states (1024 bounded integer group keys) are merged by one
+dense RCCL all-reduce, each rank keeping the groups it owns (the reference's
+partial/final aggregate stage shape, crates/query-distributed/src/planner.rs:
+200-249).  Shapes outside the table form all-gather the dim shards instead;
+group keys outside the dense bound shuffle their partial states by all-to-all.
 
 --workload cfg4 (BASELINE config 4, weak scaling): 1e9 fact rows per GPU; both
 sides hash-partitioned by the join key and exchanged over RCCL all-to-all
@@ -327,8 +332,9 @@ def main():
             workload = ("filter->hash-join->group-by (BASELINE metric query): SELECT d.g, SUM(f.v), COUNT(f.v) "
                         "FROM fact f JOIN dim d ON f.k = d.k WHERE f.x > 49 GROUP BY d.g")
             par = (f"fact {args.rows} rows split x{world} (strong scaling)"
-                   + (f", dim sharded x{world} and all-gathered over RCCL inside the step (broadcast join), partial "
-                      "states shuffled by RCCL all-to-all, final aggregate per owner rank" if dist else ""))
+                   + (f", dim sharded x{world}: shard tables summed by RCCL all-reduce inside the step (broadcast join, "
+                      "table form), partial states merged by a dense RCCL all-reduce, final aggregate per owner rank"
+                      if dist else ""))
         line = {
             "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
             "value": value,
@@ -365,6 +371,10 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "build_ms_per_step": kt["join_build"][0] / args.steps,
+            # N > 1 (or QEH_BENCH_FORCE_DIST): how the broadcast join got its table ("table": shard
+            # tables summed by all-reduce; "allgather": dim shards all-gathered) and merged its groups
+            "dist_build": getattr(dx, "last_build", None) if dx is not None and not cfg4 else None,
+            "dist_final": getattr(dx, "last_final", None) if dx is not None else None,
             "result_groups": groups,
             "result_rows_counted": counted,
             "result_check": "Σ COUNT == device filter count, Σ SUM(v) == device filtered Σ v (1e-6), groups == "

@@ -285,6 +285,22 @@ int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_column *probe_co
 int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
                                   int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table);
 int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out);
+/* [min, max, non-null count] of each Int32 / Int64 column (out[3 i .. 3 i + 2]; an all-NULL or empty
+ * column gives min > max), one synchronous read for all of them -- the job-wide build ranges of a
+ * distributed broadcast join are gathered from these. */
+int qeh_columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n_cols, int64_t *out);
+/* The dense final stage of a distributed broadcast join whose single group key is a bounded
+ * integer (the reference's partial/final aggregate, distributed/planner.rs:200-249): this rank's
+ * partial states (group keys + n_vals non-null value columns) scattered into f64 lanes
+ * [1 + n_vals][range] at key - key_min (lane 0 = 1.0 presence; values exact below 2^53), into
+ * caller-zeroed `out`; the caller sums the ranks' lanes (one RCCL all-reduce), then
+ * qeh_dense_states_take returns the groups this rank owns ((key - key_min) % world == rank) that
+ * are present, in key order, as key_dtype keys and out_dtypes[j] (Int64 / Float64) values. */
+int qeh_dense_states_f64(qeh_ctx *ctx, const qeh_column *keys, const qeh_column *vals, int n_vals, int64_t key_min,
+                         int64_t range, double *out);
+int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range, int world,
+                          int rank, int32_t key_dtype, const int32_t *out_dtypes, qeh_column *out_keys,
+                          qeh_column *out_vals, int64_t *out_groups);
 int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
                                     const qeh_expr *predicate, const uint16_t *table, int64_t key_min,
                                     uint64_t key_range, int64_t group_min, int64_t n_groups, int32_t group_dtype,

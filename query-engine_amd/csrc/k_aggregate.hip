@@ -1207,6 +1207,37 @@ __global__ void k_states_reduce(uint64_t *states, int64_t G, AggSpecs specs) {
 // scan the flags in one workgroup -- one launch where the general path takes five (reduce,
 // flags, three scan kernels), ~4-5 us per dependent launch on the query's critical path.
 // pos[g] = non-empty groups before g; the count lands in total (the status words).
+// Shard fold of small state tables by many workgroups (one word per thread, sixteen shard loads in
+// flight): states written by device-scope atomics live beyond the XCD L2s, so a single workgroup
+// folding 1024 groups x 64 shards waited ~40 us on load round trips (round-3 step trace).
+__global__ __launch_bounds__(256) void k_states_fold(uint64_t *__restrict__ states, int64_t Gs, AggSpecs specs) {
+    const int64_t words = (int64_t)specs.n_slots * Gs;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= words) return;
+    const int64_t slot = i / Gs;
+    int kind = -1;  // counts
+    for (int a = 0; a < specs.n; ++a)
+        if (specs.a[a].val_slot == slot) kind = specs.a[a].kind;
+    uint64_t acc = states[i];
+    constexpr int B = 16;
+    for (int sh0 = 1; sh0 < specs.shards; sh0 += B) {
+        uint64_t v[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) v[q] = sh0 + q < specs.shards ? states[i + (sh0 + q) * words] : 0ull;
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            if (sh0 + q >= specs.shards) break;
+            switch (kind) {
+                case AK_SUM_F: acc = __builtin_bit_cast(uint64_t, as_f64(acc) + as_f64(v[q])); break;
+                case AK_MIN: acc = (int64_t)v[q] < (int64_t)acc ? v[q] : acc; break;
+                case AK_MAX: acc = (int64_t)v[q] > (int64_t)acc ? v[q] : acc; break;
+                default: acc += v[q]; break;  // counts, wrapping int sums
+            }
+        }
+    }
+    states[i] = acc;
+}
+
 constexpr int kCompactSmallG = 16384;
 __global__ __launch_bounds__(1024) void k_states_compact_small(uint64_t *__restrict__ states, int64_t Gs, int64_t G,
                                                               AggSpecs specs, uint64_t *__restrict__ pos,
@@ -2250,8 +2281,15 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     auto compact = [&]() -> int {
         if (!posp) return QEH_OK;
         if (small) {
+            AggSpecs cs = specs;
+            if (specs.shards > 1 && !std::getenv("QEH_FOLD_ONE_WG")) {
+                const int64_t words = (int64_t)specs.n_slots * Gs;
+                hipLaunchKernelGGL(k_states_fold, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, ctx->stream,
+                                   states.as<uint64_t>(), Gs, specs);
+                cs.shards = 1;  // folded: the compact kernel only flags and scans
+            }
             hipLaunchKernelGGL(k_states_compact_small, dim3(1), dim3(1024), 0, ctx->stream, states.as<uint64_t>(), Gs, G,
-                               specs, pos.as<uint64_t>(), (uint64_t *)(errw.as<uint32_t>() + 2));
+                               cs, pos.as<uint64_t>(), (uint64_t *)(errw.as<uint32_t>() + 2));
             return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: compact launch failed");
         }
         hipLaunchKernelGGL(k_group_nonempty, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
@@ -2580,6 +2618,130 @@ extern "C" int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_colum
     p->pred = PendingSlice::serialise(predicate);
     p->agg_fc = PendingSlice::agg_list(aggs, n_aggs);
     ctx->pending_slice = p;
+    return QEH_OK;
+}
+
+// ---- dense partial states of a distributed broadcast join (qeh_dense_states_f64 / _take) ----
+struct DenseCols {
+    const void *vals[kMaxAggs];
+    int32_t dt[kMaxAggs];
+    int32_t n;
+};
+
+__global__ void k_dense_scatter(ColRef key, int64_t n, DenseCols dc, int64_t kmin, int64_t range,
+                                double *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = (uint64_t)load_i64(key, i) - (uint64_t)kmin;
+        if (o >= (uint64_t)range) continue;
+        out[o] = 1.0;
+        for (int j = 0; j < dc.n; ++j) {
+            double v;
+            if (dc.dt[j] == QEH_DT_FLOAT64) v = ((const double *)dc.vals[j])[i];
+            else if (dc.dt[j] == QEH_DT_INT32) v = (double)((const int32_t *)dc.vals[j])[i];
+            else v = (double)((const int64_t *)dc.vals[j])[i];
+            out[(int64_t)(j + 1) * range + (int64_t)o] = v;
+        }
+    }
+}
+
+// one workgroup: the owned slots o = rank + world * q with presence > 0, in key order
+__global__ __launch_bounds__(1024) void k_dense_take(const double *__restrict__ in, int64_t kmin, int64_t range, int world,
+                                                     int rank, int32_t key_dt, void *__restrict__ okeys, DenseCols oc,
+                                                     int64_t *__restrict__ total) {
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t owned = range > rank ? (range - rank + world - 1) / world : 0;
+    const int64_t per = (owned + 1023) / 1024, q0 = (int64_t)t * per, q1 = q0 + per < owned ? q0 + per : owned;
+    uint32_t c = 0;
+    for (int64_t q = q0; q < q1; ++q) c += in[rank + q * world] > 0.0;
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - c, all = 0;
+    for (int w = 0; w < 16; ++w) {
+        base += w < wave ? wsum[w] : 0u;
+        all += wsum[w];
+    }
+    for (int64_t q = q0; q < q1; ++q) {
+        const int64_t o = rank + q * world;
+        if (!(in[o] > 0.0)) continue;
+        const int64_t key = kmin + o;
+        if (key_dt == QEH_DT_INT32) ((int32_t *)okeys)[base] = (int32_t)key;
+        else ((int64_t *)okeys)[base] = key;
+        for (int j = 0; j < oc.n; ++j) {
+            const double v = in[(int64_t)(j + 1) * range + o];
+            if (oc.dt[j] == QEH_DT_FLOAT64) ((double *)oc.vals[j])[base] = v;
+            else ((int64_t *)oc.vals[j])[base] = (int64_t)v;
+        }
+        ++base;
+    }
+    if (t == 0) *total = all;
+}
+
+extern "C" int qeh_dense_states_f64(qeh_ctx *ctx, const qeh_column *keys, const qeh_column *vals, int n_vals,
+                                    int64_t key_min, int64_t range, double *out) {
+    if (!ctx || !keys || !out || n_vals < 0 || n_vals > kMaxAggs || (n_vals > 0 && !vals) || range <= 0)
+        return fail(QEH_E_INVALID, "qeh_dense_states_f64: bad argument");
+    QEH_TRY(check_column(*keys, "dense state key"));
+    if (keys->dtype != QEH_DT_INT64 && keys->dtype != QEH_DT_INT32) return fail(QEH_E_UNSUPPORTED, "dense state keys must be Int32 / Int64");
+    if (keys->validity && keys->null_count != 0) return fail(QEH_E_UNSUPPORTED, "dense state keys must be non-null");
+    DenseCols dc{};
+    dc.n = n_vals;
+    for (int j = 0; j < n_vals; ++j) {
+        QEH_TRY(check_column(vals[j], "dense state value"));
+        if (vals[j].length != keys->length) return fail(QEH_E_INVALID, "dense state columns have different lengths");
+        if ((vals[j].dtype != QEH_DT_INT64 && vals[j].dtype != QEH_DT_FLOAT64 && vals[j].dtype != QEH_DT_INT32) ||
+            (vals[j].validity && vals[j].null_count != 0))
+            return fail(QEH_E_UNSUPPORTED, "dense state values must be non-null Int32 / Int64 / Float64");
+        dc.vals[j] = (const char *)vals[j].values + (size_t)vals[j].offset * dtype_size(vals[j].dtype);
+        dc.dt[j] = vals[j].dtype;
+    }
+    DeviceGuard dg(ctx->device);
+    const int64_t n = keys->length;
+    if (n > 0)
+        hipLaunchKernelGGL(k_dense_scatter, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream, make_colref(*keys),
+                           n, dc, key_min, range, out);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+extern "C" int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range, int world,
+                                     int rank, int32_t key_dtype, const int32_t *out_dtypes, qeh_column *out_keys,
+                                     qeh_column *out_vals, int64_t *out_groups) {
+    if (!ctx || !in || !out_keys || !out_groups || n_vals < 0 || n_vals > kMaxAggs || (n_vals > 0 && (!out_vals || !out_dtypes)) ||
+        range <= 0 || world < 1 || rank < 0 || rank >= world || (key_dtype != QEH_DT_INT64 && key_dtype != QEH_DT_INT32))
+        return fail(QEH_E_INVALID, "qeh_dense_states_take: bad argument");
+    for (int j = 0; j < n_vals; ++j)
+        if (out_dtypes[j] != QEH_DT_INT64 && out_dtypes[j] != QEH_DT_FLOAT64)
+            return fail(QEH_E_UNSUPPORTED, "dense state outputs are Int64 / Float64");
+    DeviceGuard dg(ctx->device);
+    *out_groups = 0;
+    const int64_t cap = std::max<int64_t>((range + world - 1) / world, 1);
+    QEH_TRY(alloc_column(ctx, key_dtype, cap, false, out_keys));
+    DenseCols oc{};
+    oc.n = n_vals;
+    int made = 0, s = QEH_OK;
+    for (; made < n_vals; ++made) {
+        if ((s = alloc_column(ctx, out_dtypes[made], cap, false, &out_vals[made])) != QEH_OK) break;
+        oc.vals[made] = out_vals[made].values;
+        oc.dt[made] = out_dtypes[made];
+    }
+    DevBuf tot;
+    if (s == QEH_OK) s = tot.alloc(ctx, 8);
+    int64_t g = 0;
+    if (s == QEH_OK) {
+        hipLaunchKernelGGL(k_dense_take, dim3(1), dim3(1024), 0, ctx->stream, in, key_min, range, world, rank, key_dtype,
+                           out_keys->values, oc, tot.as<int64_t>());
+        s = hipGetLastError() == hipSuccess ? read_small(ctx, &g, tot.p, 8) : fail(QEH_E_HIP, "dense take launch failed");
+    }
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out_keys);
+        for (int j = 0; j < made; ++j) qeh_column_release(ctx, &out_vals[j]);
+        return s;
+    }
+    out_keys->length = g;
+    for (int j = 0; j < n_vals; ++j) out_vals[j].length = g;
+    *out_groups = g;
     return QEH_OK;
 }
 

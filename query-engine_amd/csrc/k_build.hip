@@ -352,6 +352,20 @@ extern "C" int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *bui
     return QEH_OK;
 }
 
+extern "C" int qeh_columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n_cols, int64_t *out) {
+    if (!ctx || !cols || !out || n_cols < 1) return fail(QEH_E_INVALID, "qeh_columns_minmax: bad argument");
+    for (int i = 0; i < n_cols; ++i) {
+        QEH_TRY(check_column(cols[i], "min/max column"));
+        if (cols[i].dtype != QEH_DT_INT64 && cols[i].dtype != QEH_DT_INT32)
+            return fail(QEH_E_UNSUPPORTED, "qeh_columns_minmax: Int32 / Int64 columns");
+    }
+    DeviceGuard dg(ctx->device);
+    std::vector<int64_t> mn(n_cols), mx(n_cols), cnt(n_cols);
+    QEH_TRY(columns_minmax(ctx, cols, n_cols, mn.data(), mx.data(), cnt.data()));
+    for (int i = 0; i < n_cols; ++i) out[3 * i] = mn[i], out[3 * i + 1] = mx[i], out[3 * i + 2] = cnt[i];
+    return QEH_OK;
+}
+
 extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out) {
     if (!ctx || !out || (n > 0 && !table)) return fail(QEH_E_INVALID, "qeh_u16_count_nonzero: bad argument");
     DeviceGuard dg(ctx->device);

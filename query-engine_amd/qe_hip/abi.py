@@ -85,6 +85,9 @@ SIGNATURES = {
     "qeh_join_filter_aggregate_prelaunch": (I, [P, COLP, I, I, EXPRP, AGGP, I, C.POINTER(I64), C.POINTER(I64)]),
     "qeh_direct_group_table_insert": (I, [P, COLP, COLP, I64, U64, I64, P]),
     "qeh_u16_count_nonzero": (I, [P, P, U64, C.POINTER(I64)]),
+    "qeh_columns_minmax": (I, [P, COLP, I, C.POINTER(I64)]),
+    "qeh_dense_states_f64": (I, [P, COLP, COLP, I, I64, I64, P]),
+    "qeh_dense_states_take": (I, [P, P, I, I64, I64, I, I, C.c_int32, C.POINTER(C.c_int32), COLP, COLP, C.POINTER(I64)]),
     "qeh_join_filter_aggregate_table": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, I64, C.c_int32, AGGP, I, COLP, COLP,
                                             C.POINTER(I64)]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),

@@ -372,6 +372,29 @@ class Context:
         abi.check(self.lib.qeh_direct_group_table_insert(self.h, C.byref(build_key.c), C.byref(group_key.c), key_min,
                                                          key_range, group_min, table_ptr))
 
+    def columns_minmax(self, cols: Sequence[DeviceColumn]) -> List[Tuple[int, int, int]]:
+        """qeh_columns_minmax: [(min, max, non-null count)] of Int32 / Int64 columns, one read."""
+        out = (C.c_int64 * (3 * len(cols)))()
+        abi.check(self.lib.qeh_columns_minmax(self.h, self._cols(cols), len(cols), out))
+        return [(out[3 * i], out[3 * i + 1], out[3 * i + 2]) for i in range(len(cols))]
+
+    def dense_states_f64(self, keys: DeviceColumn, vals: Sequence[DeviceColumn], key_min: int, key_range: int,
+                         out_ptr: int) -> None:
+        """qeh_dense_states_f64: partial states into f64 lanes [1 + len(vals)][key_range] (caller-zeroed)."""
+        abi.check(self.lib.qeh_dense_states_f64(self.h, C.byref(keys.c), self._cols(vals) if vals else None, len(vals),
+                                                key_min, key_range, out_ptr))
+
+    def dense_states_take(self, in_ptr: int, n_vals: int, key_min: int, key_range: int, world: int, rank: int,
+                          key_dtype: int, out_dtypes: Sequence[int]):
+        """qeh_dense_states_take: (keys, value columns, groups) this rank owns after the lane sum."""
+        ok = abi.QehColumn()
+        ov = (abi.QehColumn * max(n_vals, 1))()
+        dts = (C.c_int32 * max(n_vals, 1))(*out_dtypes)
+        g = C.c_int64()
+        abi.check(self.lib.qeh_dense_states_take(self.h, in_ptr, n_vals, key_min, key_range, world, rank, key_dtype,
+                                                 dts, C.byref(ok), ov, C.byref(g)))
+        return self._wrap(ok), [self._wrap(ov[i]) for i in range(n_vals)], g.value
+
     def u16_count_nonzero(self, table_ptr: int, n: int) -> int:
         out = C.c_int64()
         abi.check(self.lib.qeh_u16_count_nonzero(self.h, table_ptr, n, C.byref(out)))

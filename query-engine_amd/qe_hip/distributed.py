@@ -158,6 +158,18 @@ def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], peak: 
     return out
 
 
+def _without_bitmap(ctx: Context, col: DeviceColumn) -> DeviceColumn:
+    """A view of `col` without its validity bitmap (for columns known to hold no NULL)."""
+    c = abi.QehColumn()
+    C.pointer(c)[0] = col.c
+    c.owned = 0
+    c.validity = None
+    c.null_count = 0
+    d = DeviceColumn(ctx, c)
+    d.parent = col
+    return d
+
+
 class _DeviceView:
     """__cuda_array_interface__ over a library-owned device buffer: torch.as_tensor wraps it
     without a copy and keeps this object (and the column it references) alive."""
@@ -569,17 +581,14 @@ class DistributedExecutor:
             return None
         n = len(build_key)
         ts = [self._to_tensors(c)[0] for c in cols]
-        self._sync()  # the shard columns may still be in flight on the library's queue
         big, small = np.iinfo(np.int64).max, np.iinfo(np.int64).min
-        flags = torch.tensor([1 if any(c.c.validity for c in cols) else 0] + list(probe_flags), dtype=torch.int64,
-                             device=self.device)
-        if n:
-            kk, gg = torch.aminmax(ts[0]), torch.aminmax(ts[1].to(torch.int64))
-            st = torch.cat([torch.stack([torch.tensor(n, dtype=torch.int64, device=ts[0].device), kk.min, kk.max,
-                                         gg.min, gg.max]), flags])
+        flags = [1 if any(c.c.validity for c in cols) else 0] + list(probe_flags)
+        if n:  # one library min / max pass over both columns (one host read), not torch reductions
+            (kmn, kmx, _), (gmn, gmx, _) = self.ctx.columns_minmax(cols)
+            vals = [n, kmn, kmx, gmn, gmx] + flags
         else:
-            st = torch.cat([torch.tensor([0, big, small, big, small], dtype=torch.int64, device=self.device), flags])
-        M = _allgather_meta_t(st, self.world, self.group)
+            vals = [0, big, small, big, small] + flags
+        M = _allgather_meta(np.array(vals, np.int64), self.world, self.device, self.group)
         rows = [int(x) for x in M[:, 0]]
         total = sum(rows)
         out = {"M": M, "rows": rows, "total": total, "n": n, "ts": ts, "bitmap": bool(M[:, 5].max() > 0),
@@ -685,6 +694,21 @@ class DistributedExecutor:
         R = hi - lo + 1
         if R > self.DENSE_MAX_KEYS or R <= 0:
             return None
+        if (pk[0].dtype in (abi.DT_INT64, abi.DT_INT32) and not pk[0].c.validity
+                and all(f == AF.Count or (f == AF.Sum and c.dtype == abi.DT_FLOAT64) for f, c in zip(kinds, pa_))):
+            # every lane is a COUNT or a float SUM: exact in f64, so one lane buffer, one library scatter,
+            # one all-reduce and one library take (the torch path below issues ~15 small kernels)
+            lanes = torch.zeros((1 + len(pa_)) * R, dtype=torch.float64, device="cuda")
+            self._sync_torch()
+            # (SUM partials carry a bitmap but no NULL: every input is non-null, checked above)
+            self.ctx.dense_states_f64(pk[0], [_without_bitmap(self.ctx, c) for c in pa_], lo, R, lanes.data_ptr())
+            self._sync()
+            if self.world > 1:
+                dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+            self._sync_torch()
+            ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(pa_), lo, R, self.world, self.rank, pk[0].dtype,
+                                                   [c.dtype for c in pa_])
+            return [ok], ov, g
         self._sync()
         gk = self._to_tensors(pk[0])[0]
         dev = gk.device
