@@ -317,6 +317,24 @@ struct SliceRegions {
 };
 
 
+// Experiment switches for phase A's exchange stores (compile-time only, default 0 = the product):
+// 1 = cached value stores, 2 = cached stores folded into a 2^QEH_EXP_RING_LOG-item ring (wrong
+// results: prices the writes as if the exchange stayed on chip), 3 = no exchange stores.
+#ifndef QEH_EXP_A
+#define QEH_EXP_A 0
+#endif
+#ifndef QEH_EXP_RING_LOG
+#define QEH_EXP_RING_LOG 22
+#endif
+__device__ __forceinline__ uint64_t exa_o(uint64_t o) {
+    return QEH_EXP_A == 2 ? (o & ((1ull << QEH_EXP_RING_LOG) - 1ull)) : o;
+}
+template <typename T>
+__device__ __forceinline__ void exa_st(T v, T *p) {
+    if constexpr (QEH_EXP_A == 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // MODE 0: slices of the join key's offset (k - kmin) >> kSliceBits, items = 16-bit key offsets.
 // MODE 1: the group id is looked up here (any unique table layout) and rows are partitioned by
 // gid >> kGidSliceBits, items = gid & (2^kGidSliceBits - 1); `range` = number of groups.
@@ -457,20 +475,21 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                 }
                 const uint64_t dst = (uint64_t)pos[b] + kx;
                 const uint64_t o = abase[b] + dst;
-                if (dst >= hd[b] && dst + 1 < cap) {
-                    *(uint32_t *)(rg.key + o) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
+                if (QEH_EXP_A == 3 && kv[0] != 0x1357u) {
+                } else if (dst >= hd[b] && dst + 1 < cap) {
+                    *(uint32_t *)(rg.key + exa_o(o)) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
                     if (VC) {
                         v2i64 w;
                         w[0] = vv[0], w[1] = vv[1];
-                        __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                        exa_st(w, (v2i64 *)(rg.val + exa_o(o)));
                     }
                 } else {
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
                         if (dst + q < hd[b]) continue;  // placeholder ahead of the region's first item
                         if (dst + q < cap) {
-                            rg.key[o + q] = kv[q];
-                            if (VC) __builtin_nontemporal_store(vv[q], rg.val + o + q);
+                            rg.key[exa_o(o + q)] = kv[q];
+                            if (VC) exa_st(vv[q], rg.val + exa_o(o + q));
                         } else {
                             ovf = true;
                         }
