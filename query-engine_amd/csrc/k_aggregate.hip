@@ -310,48 +310,95 @@ struct SliceRegions {
     uint32_t *overflow;   // set when a region fills up (skewed probe keys)
     uint64_t cap;         // items per region, multiple of kSliceChunk
     int32_t F;            // slices
-    int32_t pair_flush;   // phase A: flush two items per lane (4-B key, 16-B value stores)
     // exact layout (materialising join): region (workgroup r, slice b) starts at
     // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
     const uint64_t *rbase;
 };
 
 
-// Experiment switches for phase A's exchange stores (compile-time only, default 0 = the product):
-// 1 = cached value stores, 2 = cached stores folded into a 2^QEH_EXP_RING_LOG-item ring (wrong
-// results: prices the writes as if the exchange stayed on chip), 3 = no exchange stores.
-#ifndef QEH_EXP_A
-#define QEH_EXP_A 0
-#endif
-#ifndef QEH_EXP_RING_LOG
-#define QEH_EXP_RING_LOG 22
-#endif
-__device__ __forceinline__ uint64_t exa_o(uint64_t o) {
-    return QEH_EXP_A == 2 ? (o & ((1ull << QEH_EXP_RING_LOG) - 1ull)) : o;
+// Phase A's shape when it is planned on the device (the prelaunch ahead of the build reads the build
+// key's range from device memory instead of waiting for the host: no host round trip between the
+// min/max kernels and phase A).  plan_slices is the one rule, evaluated on the device by
+// k_slice_plan and on the host to adopt the result; regions are allocated for the worst case and
+// the plan's cap divides them among grid x F regions.
+struct SlicePlan {
+    int64_t kmin;
+    uint64_t range;
+    uint64_t cap;
+    int32_t F;
+    int32_t ok;
+};
+struct SlicePlanIn {
+    uint64_t min_bytes;    // smallest table (bytes) worth the two-phase pipeline
+    uint64_t alloc_items;  // items allocated for all regions together
+    int32_t grid;
+    int32_t n_slots;
+    int32_t sparse_ok;     // direct_table_ok's sparse rule enabled
+};
+__host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t kmn, int64_t kmx, int64_t kcnt, int64_t gmn,
+                                                 int64_t gmx, int64_t gcnt) {
+    SlicePlan p{};
+    if (kcnt <= 0) return p;
+    // the group count is at most the group key's range (+ the NULL group)
+    const uint64_t gr = gcnt ? (uint64_t)gmx - (uint64_t)gmn + 1ull : 0;
+    const int64_t g_bound = (gr == 0 || gr > (1ull << 20)) ? -1 : (int64_t)gr + 1;
+    if (g_bound <= 0 || g_bound >= 0xFFFF || (int64_t)pi.n_slots * g_bound > kSliceStateWords) return p;
+    const uint64_t range = (uint64_t)kmx - (uint64_t)kmn + 1ull;
+    // the DIRECT rule of build_join_table, and the slice path's own limits
+    if (!direct_table_ok_with(range, (uint64_t)kcnt, (uint64_t)g_bound, pi.sparse_ok != 0)) return p;
+    if (range * 2 < pi.min_bytes) return p;
+    const uint64_t F = (range + kSliceKeys - 1) >> kSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return p;
+    p.kmin = kmn;
+    p.range = range;
+    p.F = (int32_t)F;
+    p.cap = pi.alloc_items / ((uint64_t)pi.grid * F) / kSliceChunk * kSliceChunk;
+    p.ok = p.cap >= (uint64_t)kSliceChunk;
+    return p;
 }
-template <typename T>
-__device__ __forceinline__ void exa_st(T v, T *p) {
-    if constexpr (QEH_EXP_A == 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
+// mm[0] = build key, mm[1] = group key ranges
+__global__ void k_slice_plan(const MinMax *__restrict__ mm, SlicePlanIn pi, SlicePlan *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        *out = plan_slices(pi, mm[0].mn, mm[0].mx, (int64_t)mm[0].cnt, mm[1].mn, mm[1].mx, (int64_t)mm[1].cnt);
 }
+
+// One whole chunk of phase A's flush, planned by the slice's owner thread while the tile is staged:
+// item x of the chunk (x < CH) comes from the carried items (c_key/c_v[coff + x]) when x < clim, else
+// from the staged tile (st_key/st_v[soff + x]); it lands at absolute item g + x when lo <= x < hi
+// (items below lo are placeholders ahead of an exact-layout region, items from hi on overflow it).
+struct __attribute__((aligned(16))) SliceChunk {
+    uint64_t g;
+    int32_t soff;
+    uint32_t pk;  // coff (13 bits) | clim << 13 | lo << 19 | hi << 25  (6 bits each)
+};
 
 // MODE 0: slices of the join key's offset (k - kmin) >> kSliceBits, items = 16-bit key offsets.
 // MODE 1: the group id is looked up here (any unique table layout) and rows are partitioned by
 // gid >> kGidSliceBits, items = gid & (2^kGidSliceBits - 1); `range` = number of groups.
+//
+// Three barriers per tile, software-pipelined: tile t's whole chunks are flushed at the top of
+// iteration t+1 while its loads are still arriving (no barrier after the flush: a wave that finishes
+// early goes on to rank its rows), and tile t's carries (the < CH items per slice left over) are
+// copied by waves 1-15 while wave 0 scans tile t+1's counts.  Counts, carried counts, write
+// positions and tile offsets are double-buffered by tile parity.
+//   [flush(t-1); eval + rank(t)] B1 [scan(t) | carry(t-1)] B2 [stage(t), plan chunks(t), issue(t+1)] B3
 template <int NTERMS, int NACOL, bool NT, int MODE = 0>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
-                                                                 int64_t n_tiles, SliceRegions rg, HashTable t) {
+                                                                 int64_t n_tiles, SliceRegions rg, HashTable t,
+                                                                 const SlicePlan *__restrict__ dplan = nullptr) {
     constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
+    if (dplan) {  // planned on the device: the shape comes from the build key's range in memory
+        const SlicePlan pl = *dplan;
+        if (!pl.ok) return;  // not the slice path: the host discards this launch
+        kmin = pl.kmin, range = pl.range;
+        rg.F = pl.F, rg.cap = pl.cap;
+    }
     constexpr int SB = MODE ? kGidSliceBits : kSliceBits;
     constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
-    // per-slice tile counts, carried item counts and region write positions are double-buffered:
-    // tile t reads one copy while the next tile's copy is written, so no barrier ends the tile
-    __shared__ uint32_t cntb[2][MAXF], cnb[2][MAXF], posb[2][MAXF], lofs[MAXF], mpre[MAXF], hd[MAXF];
-    uint32_t *cnt = cntb[0], *cn = cnb[0], *pos = posb[0];
-    uint32_t *cnt_n = cntb[1], *cn_n = cnb[1], *pos_n = posb[1];
+    __shared__ uint32_t cntb[2][MAXF], cnb[2][MAXF], posb[2][MAXF], lofsb[2][MAXF], mpre[MAXF], hd[MAXF];
     __shared__ uint64_t abase[MAXF];  // region start, aligned down to a whole chunk (exact layout)
     __shared__ uint32_t s_chunks;
-    __shared__ uint16_t chunk_slice[TILE / CH + MAXF];
+    __shared__ SliceChunk cdesc[TILE / CH + MAXF];
     __shared__ uint16_t st_key[TILE];
     __shared__ int64_t st_v[VC ? TILE : 1];
     __shared__ uint16_t c_key[MAXF * CH];
@@ -361,7 +408,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t region0 = (uint64_t)blockIdx.x * F;
     for (int i = tid; i < MAXF; i += kSliceBlock) {
-        cnt[i] = 0, cnt_n[i] = 0, pos[i] = 0, hd[i] = 0, abase[i] = 0;
+        cntb[0][i] = 0, cntb[1][i] = 0, posb[0][i] = 0, hd[i] = 0, abase[i] = 0;
         if (i < F) {
             // exact layout: regions start anywhere; chunks stay aligned to absolute multiples
             // of CH items by starting each region h = start % CH placeholder items early (never
@@ -370,14 +417,77 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             hd[i] = (uint32_t)(st % CH);
             abase[i] = st - hd[i];
         }
-        cn[i] = hd[i];
+        cnb[0][i] = hd[i];
     }
     __syncthreads();
     bool ovf = false;
+    // tile t-1's whole chunks (descriptors, staged items and the carries from before it): two
+    // consecutive items per lane, one chunk per quarter-wave (items sit at absolute multiples of
+    // CH, so even positions are 4-B / 16-B aligned)
+    auto flush = [&](uint32_t M) {
+        const uint32_t xl = (tid & (CH / 2 - 1)) * 2;
+        for (uint32_t c = tid / (CH / 2); c < M; c += kSliceBlock / (CH / 2)) {
+            const SliceChunk d = cdesc[c];
+            const uint32_t coff = d.pk & 8191u, clim = (d.pk >> 13) & 63u, lo = (d.pk >> 19) & 63u, hi = d.pk >> 25;
+            uint16_t kv[2];
+            int64_t vv[2] = {0, 0};
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t x = xl + q;
+                if (x < clim) {
+                    kv[q] = c_key[coff + x];
+                    if (VC) vv[q] = c_v[coff + x];
+                } else {
+                    kv[q] = st_key[d.soff + (int32_t)x];
+                    if (VC) vv[q] = st_v[d.soff + (int32_t)x];
+                }
+            }
+            const uint64_t o = d.g + xl;
+            if (lo == 0 && hi == (uint32_t)CH) {
+                *(uint32_t *)(rg.key + o) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
+                if (VC) {
+                    v2i64 w;
+                    w[0] = vv[0], w[1] = vv[1];
+                    __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    if (xl + q < lo || xl + q >= hi) continue;
+                    rg.key[o + q] = kv[q];
+                    if (VC) __builtin_nontemporal_store(vv[q], rg.val + o + q);
+                }
+            }
+        }
+    };
+    // carries after tile t-1 from the carries before it (cn_o), its counts (cnt_o) and offsets
+    // (lofs_o): appended when no whole chunk left, else the tile's last T % CH items
+    auto carry = [&](const uint32_t *cn_o, const uint32_t *cnt_o, const uint32_t *lofs_o, int p0, int stride) {
+        for (int p = p0; p < F * CH; p += stride) {
+            const int b = p / CH, kx = p % CH;
+            const uint32_t cb = cn_o[b], nb = cnt_o[b], T = cb + nb, L = T % CH;
+            int src = -1;
+            if (T < CH) {
+                if (kx >= (int)cb && kx < (int)T) src = (int)(lofs_o[b] + kx - cb);  // append
+            } else if (kx < (int)L) {
+                src = (int)(lofs_o[b] + nb - L + kx);  // the tile's last L items
+            }
+            if (src >= 0) {
+                c_key[b * CH + kx] = st_key[src];
+                if (VC) c_v[b * CH + kx] = st_v[src];
+            }
+        }
+    };
     FastTile<NTERMS, NACOL, NT> ft;
     int64_t tile = blockIdx.x;
+    int par = 0;
+    uint32_t m_prev = 0;
+    bool have_prev = false;
     if (tile < n_tiles) ft.issue(in, tile * TILE + (int64_t)wave * (64 * R) + 2 * lane);
     for (; tile < n_tiles; tile += gridDim.x) {
+        uint32_t *cnt = cntb[par], *cn = cnb[par], *pos = posb[par], *lofs = lofsb[par];
+        const int pq = par ^ 1;
+        if (have_prev) flush(m_prev);
         ft.eval(in, terms);
         uint32_t sel = ft.sel, off[R], rk[R];
         if constexpr (MODE == 1) {
@@ -405,7 +515,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         int64_t vcur[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) vcur[r] = VC ? ft.a(0, r) : 0;
-        lds_barrier();  // counts complete
+        lds_barrier();  // B1: counts complete, tile t-1 flushed
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged
             // counts (tile offsets) and of the whole chunks each slice flushes
@@ -433,8 +543,10 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                 mo += m3[q];
             }
             if (lane == 63) s_chunks = mi;
+        } else if (have_prev) {
+            carry(cnb[pq], cntb[pq], lofsb[pq], tid - 64, kSliceBlock - 64);
         }
-        lds_barrier();  // offsets ready
+        lds_barrier();  // B2: offsets ready, carries hold everything before tile t
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!((sel >> r) & 1)) continue;
@@ -443,107 +555,41 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             if (VC) st_v[s] = vcur[r];
         }
         if (tid < F) {
-            const uint32_t T = cn[tid] + cnt[tid], m = T / CH, m0 = mpre[tid];
-            for (uint32_t j = 0; j < m; ++j) chunk_slice[m0 + j] = (uint16_t)tid;
-            // next tile's state (its copies were last read before this tile's first barrier)
-            pos_n[tid] = pos[tid] + m * CH;
-            cn_n[tid] = T % CH;
-            cnt_n[tid] = 0;
+            // plan this slice's whole chunks; the next tile's state (its copies were last read by
+            // tile t-1's flush and carry, before B2)
+            const uint32_t cb = cn[tid], T = cb + cnt[tid], m = T / CH, m0 = mpre[tid];
+            const uint32_t lo0 = lofs[tid];
+            const uint64_t p0 = pos[tid], h = hd[tid], gb = abase[tid] + p0;
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint64_t ds = p0 + (uint64_t)j * CH;  // region item of the chunk's first slot
+                const uint32_t lo = h > ds ? (uint32_t)std::min<uint64_t>(h - ds, CH) : 0u;
+                const uint32_t hi = cap > ds ? (uint32_t)std::min<uint64_t>(cap - ds, CH) : 0u;
+                if (hi < (uint32_t)CH) ovf = true;
+                const uint32_t clim = j == 0 ? cb : 0u;
+                SliceChunk d;
+                d.g = gb + (uint64_t)j * CH;
+                d.soff = (int32_t)lo0 + (int32_t)(j * CH) - (int32_t)cb;
+                d.pk = (uint32_t)(tid * CH) | (clim << 13) | (lo << 19) | (hi << 25);
+                cdesc[m0 + j] = d;
+            }
+            posb[pq][tid] = (uint32_t)(p0 + (uint64_t)m * CH);
+            cnb[pq][tid] = T % CH;
+            cntb[pq][tid] = 0;
         }
         if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
-        lds_barrier();  // staged
-        if (rg.pair_flush) {
-            // whole chunks, two consecutive items per lane (one chunk per quarter-wave): the items
-            // of a chunk sit at absolute multiples of CH, so even positions are 4-B / 16-B aligned
-            const uint32_t M = s_chunks;
-            const uint32_t kx0 = (tid & (CH / 2 - 1)) * 2;
-            for (uint32_t c = tid / (CH / 2); c < M; c += kSliceBlock / (CH / 2)) {
-                const uint32_t b = chunk_slice[c];
-                const uint32_t kx = (c - mpre[b]) * CH + kx0, cb = cn[b];
-                uint16_t kv[2];
-                int64_t vv[2] = {0, 0};
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const uint32_t x = kx + q;
-                    if (x < cb) {
-                        kv[q] = c_key[b * CH + x];
-                        if (VC) vv[q] = c_v[b * CH + x];
-                    } else {
-                        kv[q] = st_key[lofs[b] + x - cb];
-                        if (VC) vv[q] = st_v[lofs[b] + x - cb];
-                    }
-                }
-                const uint64_t dst = (uint64_t)pos[b] + kx;
-                const uint64_t o = abase[b] + dst;
-                if (QEH_EXP_A == 3 && kv[0] != 0x1357u) {
-                } else if (dst >= hd[b] && dst + 1 < cap) {
-                    *(uint32_t *)(rg.key + exa_o(o)) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
-                    if (VC) {
-                        v2i64 w;
-                        w[0] = vv[0], w[1] = vv[1];
-                        exa_st(w, (v2i64 *)(rg.val + exa_o(o)));
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        if (dst + q < hd[b]) continue;  // placeholder ahead of the region's first item
-                        if (dst + q < cap) {
-                            rg.key[exa_o(o + q)] = kv[q];
-                            if (VC) exa_st(vv[q], rg.val + exa_o(o + q));
-                        } else {
-                            ovf = true;
-                        }
-                    }
-                }
-            }
-        } else {
-            // whole chunks: carried items first, then this tile's; one chunk per half-wave
-            const uint32_t M = s_chunks;
-            const uint32_t kx0 = tid & (CH - 1);
-            for (uint32_t c = tid / CH; c < M; c += kSliceBlock / CH) {
-                const uint32_t b = chunk_slice[c];
-                const uint32_t kx = (c - mpre[b]) * CH + kx0, cb = cn[b];
-                uint16_t kv;
-                int64_t vv = 0;
-                if (kx < cb) {
-                    kv = c_key[b * CH + kx];
-                    if (VC) vv = c_v[b * CH + kx];
-                } else {
-                    kv = st_key[lofs[b] + kx - cb];
-                    if (VC) vv = st_v[lofs[b] + kx - cb];
-                }
-                const uint64_t dst = (uint64_t)pos[b] + kx;
-                if (dst < hd[b]) {
-                    // placeholder ahead of the region's first item
-                } else if (dst < cap) {
-                    const uint64_t o = abase[b] + dst;
-                    rg.key[o] = kv;
-                    if (VC) __builtin_nontemporal_store(vv, rg.val + o);
-                } else {
-                    ovf = true;
-                }
-            }
-        }
-        lds_barrier();  // flushed: carries may be replaced
-        for (int p = tid; p < F * CH; p += kSliceBlock) {
-            const int b = p / CH, kx = p % CH;
-            const uint32_t cb = cn[b], nb = cnt[b], T = cb + nb, L = T % CH;
-            int src = -1;
-            if (T < CH) {
-                if (kx >= (int)cb && kx < (int)T) src = (int)(lofs[b] + kx - cb);  // append
-            } else if (kx < (int)L) {
-                src = (int)(lofs[b] + nb - L + kx);  // the tile's last L items
-            }
-            if (src >= 0) {
-                c_key[b * CH + kx] = st_key[src];
-                if (VC) c_v[b * CH + kx] = st_v[src];
-            }
-        }
-        lds_barrier();  // carries updated
-        uint32_t *t0 = cnt, *t1 = cn, *t2 = pos;
-        cnt = cnt_n, cn = cn_n, pos = pos_n;
-        cnt_n = t0, cn_n = t1, pos_n = t2;
+        lds_barrier();  // B3: staged, chunks planned
+        m_prev = s_chunks;
+        have_prev = true;
+        par = pq;
     }
+    if (have_prev) {
+        flush(m_prev);
+        lds_barrier();
+        const int pq = par ^ 1;  // the last tile's buffers
+        carry(cnb[pq], cntb[pq], lofsb[pq], tid, kSliceBlock);
+        lds_barrier();
+    }
+    const uint32_t *cn = cnb[par], *pos = posb[par];
     for (int p = tid; p < F * CH; p += kSliceBlock) {  // partial last chunks
         const int b = p / CH, kx = p % CH;
         if (kx >= (int)cn[b]) continue;
@@ -1601,7 +1647,7 @@ struct SlicePre {
     uint64_t range = 0;
     int grid = 0;
     int64_t n_tiles = 0;
-    DevBuf kbuf, vbuf, cbuf;
+    DevBuf kbuf, vbuf, cbuf, planbuf;
     SliceRegions rg{};
     hipEvent_t done = nullptr;
     ~SlicePre() {
@@ -1659,6 +1705,8 @@ struct PendingSlice {
         std::swap(dst->kbuf.p, pre.kbuf.p), std::swap(dst->kbuf.n, pre.kbuf.n), std::swap(dst->kbuf.ctx, pre.kbuf.ctx);
         std::swap(dst->vbuf.p, pre.vbuf.p), std::swap(dst->vbuf.n, pre.vbuf.n), std::swap(dst->vbuf.ctx, pre.vbuf.ctx);
         std::swap(dst->cbuf.p, pre.cbuf.p), std::swap(dst->cbuf.n, pre.cbuf.n), std::swap(dst->cbuf.ctx, pre.cbuf.ctx);
+        std::swap(dst->planbuf.p, pre.planbuf.p), std::swap(dst->planbuf.n, pre.planbuf.n),
+            std::swap(dst->planbuf.ctx, pre.planbuf.ctx);
         dst->rg = pre.rg;
         std::swap(dst->done, pre.done);
         pre.launched = false;
@@ -1696,19 +1744,18 @@ static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, i
 // gid_table != nullptr: MODE 1 (group-range slices, `range` = groups)
 static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol, int64_t kmin,
                                    uint64_t range, int64_t n_tiles, int grid, const SliceRegions &rg_in, hipStream_t stream,
-                                   const HashTable *gid_table = nullptr) {
+                                   const HashTable *gid_table = nullptr, const SlicePlan *dplan = nullptr) {
     const bool nt = fast_nt_mode() == 1;
     SliceRegions rg = rg_in;
-    rg.pair_flush = std::getenv("QEH_SLICE_SINGLE_FLUSH") ? 0 : 1;
     KernelTimer kta(ctx, "slice_partition", stream);
     const HashTable t = gid_table ? *gid_table : HashTable{};
 #define QEH_SA(NTV, NAV, NTB)                                                                                        \
     if (gid_table)                                                                                                   \
         hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 1>), dim3(grid), dim3(kSliceBlock), 0, stream, in,     \
-                           pp.terms, kmin, range, n_tiles, rg, t);                                                   \
+                           pp.terms, kmin, range, n_tiles, rg, t, nullptr);                                          \
     else                                                                                                             \
         hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB>), dim3(grid), dim3(kSliceBlock), 0, stream, in,        \
-                           pp.terms, kmin, range, n_tiles, rg, t)
+                           pp.terms, kmin, range, n_tiles, rg, t, dplan)
 #define QEH_SA_NA(NTV, NTB)                    \
     if (nacol == 0) { QEH_SA(NTV, 0, NTB); }   \
     else { QEH_SA(NTV, 1, NTB); }
@@ -1733,18 +1780,88 @@ static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, c
 
 // Launch phase A ahead of the build when the slice path is predictable from the build key's
 // range alone (and the group count is known to stay small).  Not launching is never an error.
+// The ranges' min/max kernels, the plan (k_slice_plan) and phase A are queued back to back -- phase A
+// reads its shape from device memory -- and the host reads the ranges back while phase A runs; it
+// adopts the launch when its own evaluation of the same plan says the slice path applies (phase A
+// returned at once otherwise).
 static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
                            int key_col, const qeh_column &build_key, const qeh_column &group_key, SlicePre *pre) {
     if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
     if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
-    if (n / kSliceTile == 0) return QEH_OK;
-    // build key and group key ranges in one read; the group count is at most the group key's range
-    // (+ the NULL group)
+    const int64_t n_tiles = n / kSliceTile;
+    if (n_tiles == 0) return QEH_OK;
     const qeh_column both[2] = {build_key, group_key};
+    if (std::getenv("QEH_HOST_PLAN")) {  // the ranges read back before phase A is launched
+        BuildRanges br;
+        QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
+        return slice_prelaunch_ranges(ctx, cols, n, pp, specs, key_col, br, pre);
+    }
+    FastIn in;
+    int nterms, nacol;
+    const bool fast = fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) && nacol <= 1;
+    hipStream_t side = fast ? aux_stream(ctx) : nullptr;
+    DevBuf mm;
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 + 16));
+    QEH_TRY(columns_minmax_launch(ctx, both, 2, mm.as<MinMax>()));
+    SlicePlanIn pi{};
+    bool launched = false;
+    if (side) {
+        pi.min_bytes = 6ull << 20;
+        if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
+        pi.grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+        pi.n_slots = specs.n_slots;
+        pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
+        const uint64_t tiles_per_wg = (uint64_t)((n_tiles + pi.grid - 1) / pi.grid);
+        // every row selected, keys uniform over the slices, +25 % (and per-region slack for the largest F)
+        pi.alloc_items = tiles_per_wg * pi.grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)pi.grid * kSliceMaxF * 288;
+        const uint64_t nreg_max = (uint64_t)pi.grid * kSliceMaxF;
+        hipEvent_t ready = nullptr;
+        if (pre->kbuf.alloc(ctx, pi.alloc_items * 2 + 64) == QEH_OK &&
+            (nacol == 0 || pre->vbuf.alloc(ctx, pi.alloc_items * 8 + 64) == QEH_OK) &&
+            pre->cbuf.alloc(ctx, nreg_max * 4 + 64) == QEH_OK && pre->planbuf.alloc(ctx, sizeof(SlicePlan)) == QEH_OK &&
+            hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventCreateWithFlags(&pre->done, hipEventDisableTiming) != hipSuccess) pre->done = nullptr;
+            if (pre->done) {
+                SliceRegions &rg = pre->rg;
+                rg = SliceRegions{};
+                rg.key = pre->kbuf.as<uint16_t>();
+                rg.val = nacol ? pre->vbuf.as<int64_t>() : nullptr;
+                rg.count = pre->cbuf.as<uint32_t>();
+                rg.overflow = rg.count + nreg_max;
+                QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
+                hipLaunchKernelGGL(k_slice_plan, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), pi,
+                                   pre->planbuf.as<SlicePlan>());
+                (void)hipEventRecord(ready, ctx->stream);  // inputs, the plan and the overflow reset
+                (void)hipStreamWaitEvent(side, ready, 0);
+                launch_slice_partition(ctx, in, pp, nterms, nacol, 0, 0, n_tiles, pi.grid, rg, side, nullptr,
+                                       pre->planbuf.as<SlicePlan>());
+                (void)hipEventRecord(pre->done, side);
+                launched = true;
+            }
+            (void)hipEventDestroy(ready);
+        }
+        if (hipGetLastError() != hipSuccess) return fail(QEH_E_HIP, "slice prelaunch failed");
+    }
     BuildRanges br;
-    QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
-    return slice_prelaunch_ranges(ctx, cols, n, pp, specs, key_col, br, pre);
+    QEH_TRY(columns_minmax_collect(ctx, both, 2, mm.as<MinMax>(), br.mn, br.mx, br.cnt));
+    if (!launched) return QEH_OK;
+    const SlicePlan pl = plan_slices(pi, br.mn[0], br.mx[0], br.cnt[0], br.mn[1], br.mx[1], br.cnt[1]);
+    if (!pl.ok) {  // phase A returned at once: release the worst-case regions now
+        (void)hipEventSynchronize(pre->done);
+        (void)hipEventDestroy(pre->done);
+        pre->done = nullptr;
+        pre->kbuf.reset(), pre->vbuf.reset(), pre->cbuf.reset(), pre->planbuf.reset();
+        return QEH_OK;
+    }
+    pre->rg.F = pl.F;
+    pre->rg.cap = pl.cap;
+    pre->launched = true;
+    pre->kmin = pl.kmin;
+    pre->range = pl.range;
+    pre->grid = pi.grid;
+    pre->n_tiles = n_tiles;
+    return QEH_OK;
 }
 
 static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
@@ -2086,10 +2203,10 @@ int slice_join_materialise(qeh_ctx *ctx, const qeh_column &probe_key, const qeh_
         KernelTimer kt(ctx, "join_probe");
         if (nt)
             hipLaunchKernelGGL((k_slice_partition<0, 1, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
-                               t.kmin, t.range, n_tiles, rg, HashTable{});
+                               t.kmin, t.range, n_tiles, rg, HashTable{}, nullptr);
         else
             hipLaunchKernelGGL((k_slice_partition<0, 1, false>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, none,
-                               t.kmin, t.range, n_tiles, rg, HashTable{});
+                               t.kmin, t.range, n_tiles, rg, HashTable{}, nullptr);
         hipLaunchKernelGGL(k_slice_join_inplace, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, amin, oa,
                            misses);
         if (hipGetLastError() != hipSuccess) st = fail(QEH_E_HIP, "slice join launch failed");
@@ -2316,8 +2433,65 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         return exclusive_scan_u32_dev(ctx, flags.as<uint32_t>(), pos.as<uint64_t>(), G, (uint64_t *)(errw.as<uint32_t>() + 2));
     };
     QEH_TRY(compact());
+
+    OutCols oc{};
+    const int nk = out_keys_src.n;
+    int made = 0;
+    auto cleanup = [&]() {
+        for (int i = 0; i < made; ++i) {
+            qeh_column *c = i < nk ? &out_keys[i] : &out_aggs[i - nk];
+            qeh_column_release(ctx, c);
+        }
+        made = 0;
+    };
+    // output columns with room for `rows` groups (their length is set once the count is known)
+    auto make_outputs = [&](uint64_t rows) -> int {
+        for (int i = 0; i < nk + specs.n; ++i) {
+            qeh_column *c = i < nk ? &out_keys[i] : &out_aggs[i - nk];
+            int dt;
+            bool nullable;
+            if (i < nk) {
+                dt = key_dtypes[i];
+                nullable = out_keys_src.c[i].validity != nullptr;
+            } else {
+                const AggSpec &sp = specs.a[i - nk];
+                dt = agg_output_type(sp.func, sp.in_type);
+                nullable = sp.func != QEH_AGG_COUNT;
+            }
+            int s = alloc_column(ctx, dt, (int64_t)rows, nullable, c);
+            if (s != QEH_OK) {
+                cleanup();
+                return s;
+            }
+            ++made;
+            if (nullable) QEH_HIP(hipMemsetAsync(c->validity, 0, ((rows + 63) / 64) * 8, ctx->stream));
+            if (dt == QEH_DT_BOOL) QEH_HIP(hipMemsetAsync(c->values, 0, ((rows + 63) / 64) * 8, ctx->stream));
+            oc.c[i].values = c->values;
+            oc.c[i].validity = (uint32_t *)c->validity;
+            oc.c[i].dtype = dt;
+        }
+        return QEH_OK;
+    };
+    auto finalize = [&]() -> int {
+        KernelTimer kt(ctx, "aggregate_finalize");
+        hipLaunchKernelGGL(k_finalize, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
+                           states.as<uint64_t>(), Gs, posp, out_keys_src, rep_row, specs, oc);
+        return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: finalize launch failed");
+    };
     uint32_t stw[4];
-    QEH_TRY(read_small(ctx, stw, errw.p, 16));  // one host round trip: error bits, overflow, group count
+    // Small group counts: the outputs are allocated for all G groups and finalized before the group
+    // count is known (k_finalize writes every non-empty group at its compacted position), so the
+    // status words are read once, after the last kernel -- one host round trip per call instead of two.
+    const bool early = G > 0 && Gs <= (1 << 20) && !std::getenv("QEH_FINALIZE_LATE");
+    if (early) {
+        QEH_TRY(make_outputs((uint64_t)Gs));
+        int s = finalize();
+        if (s == QEH_OK) s = read_small(ctx, stw, errw.p, 16);  // syncs: the finalize has run
+        if (s != QEH_OK || (ovf_pending && stw[1]) || stw[0]) cleanup();
+        QEH_TRY(s);
+    } else {
+        QEH_TRY(read_small(ctx, stw, errw.p, 16));  // one host round trip: error bits, overflow, group count
+    }
     if (ovf_pending && stw[1]) {
         // a slice region overflowed (probe keys skewed onto few slices): the single fused pass instead
         hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock),
@@ -2334,49 +2508,18 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     }
     QEH_TRY(kernel_error_status(stw[0], "aggregate"));
     if (posp) out_n = (uint64_t)stw[2] | ((uint64_t)stw[3] << 32);
-
-    OutCols oc{};
-    const int nk = out_keys_src.n;
-    int made = 0;
-    auto cleanup = [&]() {
-        for (int i = 0; i < made; ++i) {
-            qeh_column *c = i < nk ? &out_keys[i] : &out_aggs[i - nk];
-            qeh_column_release(ctx, c);
+    if (made == 0) {  // not finalized early (large G, or re-run after an overflow)
+        QEH_TRY(make_outputs(out_n));
+        if (G > 0 && out_n > 0) {
+            const int s = finalize();
+            if (s != QEH_OK) cleanup();
+            QEH_TRY(s);
         }
-    };
+        QEH_HIP(hipStreamSynchronize(ctx->stream));
+    }
     for (int i = 0; i < nk + specs.n; ++i) {
         qeh_column *c = i < nk ? &out_keys[i] : &out_aggs[i - nk];
-        int dt;
-        bool nullable;
-        if (i < nk) {
-            dt = key_dtypes[i];
-            nullable = out_keys_src.c[i].validity != nullptr;
-        } else {
-            const AggSpec &sp = specs.a[i - nk];
-            dt = agg_output_type(sp.func, sp.in_type);
-            nullable = sp.func != QEH_AGG_COUNT;
-        }
-        int s = alloc_column(ctx, dt, (int64_t)out_n, nullable, c);
-        if (s != QEH_OK) {
-            cleanup();
-            return s;
-        }
-        ++made;
-        if (nullable) QEH_HIP(hipMemsetAsync(c->validity, 0, ((out_n + 63) / 64) * 8, ctx->stream));
-        if (dt == QEH_DT_BOOL) QEH_HIP(hipMemsetAsync(c->values, 0, ((out_n + 63) / 64) * 8, ctx->stream));
-        oc.c[i].values = c->values;
-        oc.c[i].validity = (uint32_t *)c->validity;
-        oc.c[i].dtype = dt;
-    }
-    if (G > 0 && out_n > 0) {
-        KernelTimer kt(ctx, "aggregate_finalize");
-        hipLaunchKernelGGL(k_finalize, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
-                           states.as<uint64_t>(), Gs, posp, out_keys_src, rep_row, specs, oc);
-    }
-    QEH_HIP(hipGetLastError());
-    QEH_HIP(hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < nk + specs.n; ++i) {
-        qeh_column *c = i < nk ? &out_keys[i] : &out_aggs[i - nk];
+        c->length = (int64_t)out_n;
         c->null_count = c->validity ? -1 : 0;
     }
     *out_groups = (int64_t)out_n;

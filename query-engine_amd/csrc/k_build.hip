@@ -18,12 +18,6 @@ namespace qeh {
 static constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 
 // ---- key min/max over valid rows -------------------------------------------------
-struct MinMax {
-    int64_t mn, mx;
-    uint64_t cnt;
-    uint32_t bad;  // unsupported key type seen
-};
-
 __device__ __forceinline__ void key_minmax_body(const ColRef &key, int64_t n, MinMax *out);
 
 // Several columns in one launch (blockIdx.y = column): each workgroup writes its partial to
@@ -407,18 +401,12 @@ static void memo_put(qeh_ctx *ctx, const qeh_column &c, int64_t mn, int64_t mx, 
     ctx->mm_memo[ctx->mm_memo_n++] = {c.values, c.validity, c.offset, c.length, c.dtype, mn, mx, cnt};
 }
 
-// several columns, one synchronous read for all of them (none when every range is memoised)
-int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int64_t *mx, int64_t *valid) {
-    if (n <= 0) return QEH_OK;
-    bool all = true;
-    for (int i = 0; i < n && all; ++i) all = memo_get(ctx, cols[i], &mn[i], &mx[i], &valid[i]);
-    if (all) return QEH_OK;
-    DevBuf mm, part;
-    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
+int columns_minmax_launch(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *dev_out) {
     // one partial-reduction launch per group of up to four columns (blockIdx.y = column), then one
     // final reduction per group; four workgroups per CU on long columns (64 KB of loads in flight
     // per CU), one per CU below 2^26 rows
     const int cus = ctx->props.multiProcessorCount;
+    DevBuf part;  // stream-ordered pool: reusable once the kernels below have run
     QEH_TRY(part.alloc(ctx, sizeof(MinMax) * (size_t)kMinMaxCols * cus * 4));
     for (int i0 = 0; i0 < n; i0 += kMinMaxCols) {
         MinMaxJob j{};
@@ -431,12 +419,16 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
         }
         const int nb = grid_for(ctx, std::max<int64_t>(longest, 1), kBlock * 8, longest >= ((int64_t)1 << 26) ? 4 : 1);
         hipLaunchKernelGGL(k_key_minmax_n, dim3(nb, nc), dim3(kBlock), 0, ctx->stream, j, part.as<MinMax>());
-        hipLaunchKernelGGL(k_minmax_final, dim3(nc), dim3(kBlock), 0, ctx->stream, part.as<MinMax>(), nb,
-                           mm.as<MinMax>() + i0);
+        hipLaunchKernelGGL(k_minmax_final, dim3(nc), dim3(kBlock), 0, ctx->stream, part.as<MinMax>(), nb, dev_out + i0);
     }
     QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const MinMax *dev_out, int64_t *mn, int64_t *mx,
+                           int64_t *valid) {
     std::vector<MinMax> hm((size_t)n);
-    QEH_TRY(read_small(ctx, hm.data(), mm.p, sizeof(MinMax) * (size_t)n));
+    QEH_TRY(read_small(ctx, hm.data(), dev_out, sizeof(MinMax) * (size_t)n));
     for (int i = 0; i < n; ++i) {
         mn[i] = hm[i].mn;
         mx[i] = hm[i].mx;
@@ -444,6 +436,18 @@ int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int
         memo_put(ctx, cols[i], mn[i], mx[i], valid[i]);
     }
     return QEH_OK;
+}
+
+// several columns, one synchronous read for all of them (none when every range is memoised)
+int columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n, int64_t *mn, int64_t *mx, int64_t *valid) {
+    if (n <= 0) return QEH_OK;
+    bool all = true;
+    for (int i = 0; i < n && all; ++i) all = memo_get(ctx, cols[i], &mn[i], &mx[i], &valid[i]);
+    if (all) return QEH_OK;
+    DevBuf mm;
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * (size_t)n + 16));
+    QEH_TRY(columns_minmax_launch(ctx, cols, n, mm.as<MinMax>()));
+    return columns_minmax_collect(ctx, cols, n, mm.as<MinMax>(), mn, mx, valid);
 }
 
 static uint64_t next_pow2(uint64_t x) {

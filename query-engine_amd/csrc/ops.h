@@ -43,15 +43,32 @@ struct RowPayload {
 // stays <= 512 MB -- e.g. the key shard one rank receives in a hash exchange, 1/N of a dense range,
 // which then takes the LDS-slice pipeline instead of a linear-probing table whose every probe
 // misses L2 (QEH_DIRECT_SPARSE=0 turns the sparse case off).
-inline bool direct_table_ok(uint64_t range, uint64_t nv, uint64_t payload_max) {
+__host__ __device__ inline bool direct_table_ok_with(uint64_t range, uint64_t nv, uint64_t payload_max, bool sparse) {
     if (range == 0 || range >= (1ull << 32) || payload_max >= 0xFFFFFFFEull) return false;
     if (range <= 4 * nv + 1024) return true;
+    return sparse && payload_max < 0xFFFFull && range <= 32 * nv && range * 2 <= (512ull << 20);
+}
+inline bool direct_sparse_allowed() {
     static const bool sparse = [] {
         const char *e = std::getenv("QEH_DIRECT_SPARSE");
         return !(e && e[0] == '0') && !std::getenv("QEH_NO_U16");
     }();
-    return sparse && payload_max < 0xFFFFull && range <= 32 * nv && range * 2 <= (512ull << 20);
+    return sparse;
 }
+inline bool direct_table_ok(uint64_t range, uint64_t nv, uint64_t payload_max) {
+    return direct_table_ok_with(range, nv, payload_max, direct_sparse_allowed());
+}
+// Per-column [min, max, valid count] as the min/max kernels leave it in device memory.
+struct MinMax {
+    int64_t mn, mx;
+    uint64_t cnt;
+    uint32_t bad;  // unsupported key type seen
+};
+// The min/max kernels of `n` integer columns into dev_out[0..n) (no host sync), and the read-back of
+// such a result (one synchronous read; also memoised like columns_minmax).
+int columns_minmax_launch(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *dev_out);
+int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const MinMax *dev_out, int64_t *mn, int64_t *mx,
+                           int64_t *valid);
 // min / max / valid count of an integer column (one synchronous read).
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid);
 // min / max / valid count of several integer columns, one synchronous read.

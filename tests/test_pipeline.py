@@ -152,12 +152,16 @@ V_AGGS = [(AF.Sum, 2), (AF.Count, 2), (AF.Avg, 2), (AF.Min, 2), (AF.Max, 2)]  # 
     (400_000, 70_000, 300, 0, binop(col(0), BinaryOp.Greater, lit(20)) & binop(col(0), BinaryOp.Less, lit(80)),
      [(AF.Count, 2)]),                                            # two terms; COUNT only: keys-only exchange
 ])
-def test_slice_partitioned_probe(ctx, monkeypatch, n_fact, n_dim, groups, key0, pred, aggs):
+@pytest.mark.parametrize("host_plan", [False, True])
+def test_slice_partitioned_probe(ctx, monkeypatch, n_fact, n_dim, groups, key0, pred, aggs, host_plan):
     """Phase A (filter + stage by 64 Ki-key table slice + chunked region
     writes) / phase B (slice in LDS, LDS lookups and states), forced on small
     tables; misses below and above the key range; ragged tail by the generic
-    kernel."""
+    kernel.  Phase A planned on the device from the build key's range in memory (default) and
+    from the range read back first (QEH_HOST_PLAN)."""
     monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    if host_plan:
+        monkeypatch.setenv("QEH_HOST_PLAN", "1")
     x, k, v, dk, dg = metric_data(n_fact, n_dim, groups)
     k = k + key0
     dk = dk + key0
