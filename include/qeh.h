@@ -267,6 +267,15 @@ int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_column *probe_co
                                         int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
                                         int n_aggs, const int64_t *build_key_range, const int64_t *group_key_range);
 
+/* qeh_join_filter_aggregate_prelaunch with the build ranges still in device memory: `stats` = the
+ * ranks' qeh_broadcast_stats rows ([world][row_len], row_len >= 6, column 5 = has-bitmap) as an
+ * RCCL all-gather left them.  A plan kernel reduces them to the job-wide ranges and phase A reads its
+ * shape from that plan, so the host does not wait for the gather before phase A starts; the adopting
+ * call reads the plan back.  Launches nothing when the shape is outside the LDS-slice path. */
+int qeh_join_filter_aggregate_prelaunch_stats(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                              int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
+                                              int n_aggs, const int64_t *stats, int world, int row_len);
+
 /* Broadcast join in table form (the distributed metric path at N > 1; the partial/final stage
  * shape of distributed/planner.rs:200-249): instead of all-gathering the dimension and building the
  * whole join table on every rank, each rank inserts its dimension shard into a DIRECT u16 table
@@ -306,6 +315,22 @@ int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, 
                                     uint64_t key_range, int64_t group_min, int64_t n_groups, int32_t group_dtype,
                                     const qeh_agg *aggs, int n_aggs, qeh_column *out_keys, qeh_column *out_aggs,
                                     int64_t *out_groups);
+/* The same fused operator with the dense final stage's input as its output: instead of compacted
+ * group columns, f64 lanes [1 + n_aggs][n_groups] in caller-owned device memory (every entry
+ * written): lane 0 = the group's row count (> 0: present), lane 1 + j = aggregate j's partial state
+ * (COUNT, or SUM of a non-null Float64 column; QEH_E_UNSUPPORTED for others).  Summed over the
+ * ranks (RCCL all-reduce) they are qeh_dense_states_take's input -- the partial/final aggregate of
+ * distributed/planner.rs:200-249 without compacting, finalizing and re-scattering the partials. */
+int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                          int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
+                                          int64_t key_min, uint64_t key_range, int64_t n_groups, const qeh_agg *aggs,
+                                          int n_aggs, double *lanes);
+/* This dimension shard's broadcast-join statistics into device memory, no host wait:
+ * dev_out[0..4] = [rows, build key min, max, group key min, max] (min > max for an empty or all-NULL
+ * shard), dev_out[5 + i] = extra[i] (n_extra <= 16: flags the caller gathers with them).  The ranks
+ * all-gather these rows (RCCL) and read them back once, instead of a min/max read plus a gather. */
+int qeh_broadcast_stats(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key, const int64_t *extra,
+                        int n_extra, int64_t *dev_out);
 
 /* Stable lexicographic sort -> permutation (UINT32 row ids) of the input.
  * Intended semantics of `Sort` (physical_plan.rs:40-44; executor.rs:290-297

@@ -327,6 +327,7 @@ struct SlicePlan {
     uint64_t cap;
     int32_t F;
     int32_t ok;
+    int64_t src[6];  // the build ranges it was planned from: key min, max, count, group key min, max, count
 };
 struct SlicePlanIn {
     uint64_t min_bytes;    // smallest table (bytes) worth the two-phase pipeline
@@ -338,6 +339,7 @@ struct SlicePlanIn {
 __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t kmn, int64_t kmx, int64_t kcnt, int64_t gmn,
                                                  int64_t gmx, int64_t gcnt) {
     SlicePlan p{};
+    p.src[0] = kmn, p.src[1] = kmx, p.src[2] = kcnt, p.src[3] = gmn, p.src[4] = gmx, p.src[5] = gcnt;
     if (kcnt <= 0) return p;
     // the group count is at most the group key's range (+ the NULL group)
     const uint64_t gr = gcnt ? (uint64_t)gmx - (uint64_t)gmn + 1ull : 0;
@@ -360,6 +362,24 @@ __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t 
 __global__ void k_slice_plan(const MinMax *__restrict__ mm, SlicePlanIn pi, SlicePlan *out) {
     if (threadIdx.x == 0 && blockIdx.x == 0)
         *out = plan_slices(pi, mm[0].mn, mm[0].mx, (int64_t)mm[0].cnt, mm[1].mn, mm[1].mx, (int64_t)mm[1].cnt);
+}
+// The job-wide ranges from the gathered rows of qeh_broadcast_stats ([rows, key min, max, group key
+// min, max, has-bitmap, ...] per rank): min / max over the ranks with rows, counts = all rows; no
+// plan when any shard has a bitmap (the counts would not be the non-null counts).
+__global__ void k_slice_plan_stats(const int64_t *__restrict__ M, int world, int row_len, SlicePlanIn pi, SlicePlan *out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t tot = 0, kmn = INT64_MAX, kmx = INT64_MIN, gmn = INT64_MAX, gmx = INT64_MIN, bitmap = 0;
+    for (int r = 0; r < world; ++r) {
+        const int64_t *m = M + (int64_t)r * row_len;
+        bitmap |= m[5];
+        if (m[0] <= 0) continue;
+        tot += m[0];
+        kmn = m[1] < kmn ? m[1] : kmn, kmx = m[2] > kmx ? m[2] : kmx;
+        gmn = m[3] < gmn ? m[3] : gmn, gmx = m[4] > gmx ? m[4] : gmx;
+    }
+    SlicePlan p = plan_slices(pi, kmn, kmx, tot, gmn, gmx, tot);
+    if (bitmap || kmn > kmx || gmn > gmx) p.ok = 0;
+    *out = p;
 }
 
 // One whole chunk of phase A's flush, planned by the slice's owner thread while the tile is staged:
@@ -1303,6 +1323,36 @@ __global__ __launch_bounds__(256) void k_states_fold(uint64_t *__restrict__ stat
     states[i] = acc;
 }
 
+// lanes[0][g] = rows of group g, lanes[1 + j][g] = aggregate j's partial (COUNT or float SUM; the
+// caller checked the kinds), every shard copy folded in: one thread per lane entry, 16 shard loads
+// in flight
+__global__ __launch_bounds__(256) void k_states_lanes(const uint64_t *__restrict__ states, int64_t Gs, int64_t G,
+                                                      AggSpecs specs, double *__restrict__ lanes) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)(1 + specs.n) * G) return;
+    const int j = (int)(e / G) - 1;  // -1: the row-count lane
+    const int64_t g = e % G;
+    const bool fsum = j >= 0 && specs.a[j].kind == AK_SUM_F;
+    const int slot = j < 0 ? 0 : (fsum ? specs.a[j].val_slot : specs.a[j].cnt_slot);
+    const int64_t words = (int64_t)specs.n_slots * Gs;
+    const uint64_t *p = states + (int64_t)slot * Gs + g;
+    constexpr int B = 16;
+    double fv = 0.0;
+    uint64_t uv = 0;
+    for (int q0 = 0; q0 < specs.shards; q0 += B) {
+        uint64_t v[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) v[q] = q0 + q < specs.shards ? p[(int64_t)(q0 + q) * words] : 0ull;
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            if (q0 + q >= specs.shards) break;
+            if (fsum) fv += as_f64((int64_t)v[q]);
+            else uv += v[q];
+        }
+    }
+    lanes[e] = fsum ? fv : (double)uv;
+}
+
 constexpr int kCompactSmallG = 16384;
 __global__ __launch_bounds__(1024) void k_states_compact_small(uint64_t *__restrict__ states, int64_t Gs, int64_t G,
                                                               AggSpecs specs, uint64_t *__restrict__ pos,
@@ -1650,6 +1700,7 @@ struct SlicePre {
     DevBuf kbuf, vbuf, cbuf, planbuf;
     SliceRegions rg{};
     hipEvent_t done = nullptr;
+    bool dev_planned = false;  // launched from a plan in device memory, not yet read back (resolve_dev_plan)
     ~SlicePre() {
         if (done) {  // the buffers below must outlive the kernel
             (void)hipEventSynchronize(done);
@@ -1708,6 +1759,7 @@ struct PendingSlice {
         std::swap(dst->planbuf.p, pre.planbuf.p), std::swap(dst->planbuf.n, pre.planbuf.n),
             std::swap(dst->planbuf.ctx, pre.planbuf.ctx);
         dst->rg = pre.rg;
+        dst->dev_planned = pre.dev_planned;
         std::swap(dst->done, pre.done);
         pre.launched = false;
     }
@@ -1778,6 +1830,89 @@ static int64_t slice_chunk_tiles() {
 static int slice_prelaunch_ranges(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
                                   int key_col, const BuildRanges &br, SlicePre *pre);
 
+// Phase A launched from a plan in device memory: regions for the worst case, `launch_plan` queues the
+// plan kernel on the main queue (into pre->planbuf), phase A follows on the second queue.  Returns
+// whether it launched (*launched); pre->launched stays false until the plan is known on the host.
+template <class LaunchPlan>
+static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const AggSpecs &specs,
+                            int key_col, SlicePlanIn *pi, SlicePre *pre, LaunchPlan launch_plan, bool *launched) {
+    *launched = false;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 1) return QEH_OK;
+    const int64_t n_tiles = n / kSliceTile;
+    hipStream_t side = n_tiles ? aux_stream(ctx) : nullptr;
+    if (!side) return QEH_OK;
+    *pi = SlicePlanIn{};
+    pi->min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi->min_bytes = std::strtoull(e, nullptr, 10);
+    pi->grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    pi->n_slots = specs.n_slots;
+    pi->sparse_ok = direct_sparse_allowed() ? 1 : 0;
+    const uint64_t tiles_per_wg = (uint64_t)((n_tiles + pi->grid - 1) / pi->grid);
+    // every row selected, keys uniform over the slices, +25 % (and per-region slack for the largest F)
+    pi->alloc_items = tiles_per_wg * pi->grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)pi->grid * kSliceMaxF * 288;
+    const uint64_t nreg_max = (uint64_t)pi->grid * kSliceMaxF;
+    if (pre->kbuf.alloc(ctx, pi->alloc_items * 2 + 64) != QEH_OK ||
+        (nacol && pre->vbuf.alloc(ctx, pi->alloc_items * 8 + 64) != QEH_OK) ||
+        pre->cbuf.alloc(ctx, nreg_max * 4 + 64) != QEH_OK || pre->planbuf.alloc(ctx, sizeof(SlicePlan)) != QEH_OK)
+        return QEH_OK;
+    hipEvent_t ready = nullptr;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) return QEH_OK;
+    if (hipEventCreateWithFlags(&pre->done, hipEventDisableTiming) != hipSuccess) {
+        pre->done = nullptr;
+        (void)hipEventDestroy(ready);
+        return QEH_OK;
+    }
+    SliceRegions &rg = pre->rg;
+    rg = SliceRegions{};
+    rg.key = pre->kbuf.as<uint16_t>();
+    rg.val = nacol ? pre->vbuf.as<int64_t>() : nullptr;
+    rg.count = pre->cbuf.as<uint32_t>();
+    rg.overflow = rg.count + nreg_max;
+    QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
+    launch_plan(*pi, pre->planbuf.as<SlicePlan>());
+    (void)hipEventRecord(ready, ctx->stream);  // inputs, the plan and the overflow reset
+    (void)hipStreamWaitEvent(side, ready, 0);
+    launch_slice_partition(ctx, in, pp, nterms, nacol, 0, 0, n_tiles, pi->grid, rg, side, nullptr,
+                           pre->planbuf.as<SlicePlan>());
+    (void)hipEventRecord(pre->done, side);
+    (void)hipEventDestroy(ready);
+    if (hipGetLastError() != hipSuccess) return fail(QEH_E_HIP, "slice prelaunch failed");
+    pre->dev_planned = true;
+    pre->grid = pi->grid;
+    pre->n_tiles = n_tiles;
+    *launched = true;
+    return QEH_OK;
+}
+
+// A device-planned launch whose plan is `pl`: adopted (launched, shape set) when it planned the slice
+// path; else phase A returned at once and its worst-case regions are released now.
+static void settle_dev_plan(SlicePre *pre, const SlicePlan &pl) {
+    pre->dev_planned = false;
+    if (!pl.ok) {
+        (void)hipEventSynchronize(pre->done);
+        (void)hipEventDestroy(pre->done);
+        pre->done = nullptr;
+        pre->kbuf.reset(), pre->vbuf.reset(), pre->cbuf.reset(), pre->planbuf.reset();
+        return;
+    }
+    pre->rg.F = pl.F;
+    pre->rg.cap = pl.cap;
+    pre->launched = true;
+    pre->kmin = pl.kmin;
+    pre->range = pl.range;
+}
+
+// The plan of a device-planned launch read back (one small read; the plan kernel ran long before).
+static int resolve_dev_plan(qeh_ctx *ctx, SlicePre *pre, BuildRanges *br) {
+    SlicePlan pl{};
+    QEH_TRY(read_small(ctx, &pl, pre->planbuf.p, sizeof pl));
+    for (int q = 0; q < 2; ++q) br->mn[q] = pl.src[3 * q], br->mx[q] = pl.src[3 * q + 1], br->cnt[q] = pl.src[3 * q + 2];
+    settle_dev_plan(pre, pl);
+    return QEH_OK;
+}
+
 // Launch phase A ahead of the build when the slice path is predictable from the build key's
 // range alone (and the group count is known to stay small).  Not launching is never an error.
 // The ranges' min/max kernels, the plan (k_slice_plan) and phase A are queued back to back -- phase A
@@ -1789,78 +1924,27 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
     if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
-    const int64_t n_tiles = n / kSliceTile;
-    if (n_tiles == 0) return QEH_OK;
+    if (n / kSliceTile == 0) return QEH_OK;
     const qeh_column both[2] = {build_key, group_key};
     if (std::getenv("QEH_HOST_PLAN")) {  // the ranges read back before phase A is launched
         BuildRanges br;
         QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
         return slice_prelaunch_ranges(ctx, cols, n, pp, specs, key_col, br, pre);
     }
-    FastIn in;
-    int nterms, nacol;
-    const bool fast = fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) && nacol <= 1;
-    hipStream_t side = fast ? aux_stream(ctx) : nullptr;
     DevBuf mm;
     QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 + 16));
     QEH_TRY(columns_minmax_launch(ctx, both, 2, mm.as<MinMax>()));
-    SlicePlanIn pi{};
+    SlicePlanIn pi;
     bool launched = false;
-    if (side) {
-        pi.min_bytes = 6ull << 20;
-        if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
-        pi.grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
-        pi.n_slots = specs.n_slots;
-        pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
-        const uint64_t tiles_per_wg = (uint64_t)((n_tiles + pi.grid - 1) / pi.grid);
-        // every row selected, keys uniform over the slices, +25 % (and per-region slack for the largest F)
-        pi.alloc_items = tiles_per_wg * pi.grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)pi.grid * kSliceMaxF * 288;
-        const uint64_t nreg_max = (uint64_t)pi.grid * kSliceMaxF;
-        hipEvent_t ready = nullptr;
-        if (pre->kbuf.alloc(ctx, pi.alloc_items * 2 + 64) == QEH_OK &&
-            (nacol == 0 || pre->vbuf.alloc(ctx, pi.alloc_items * 8 + 64) == QEH_OK) &&
-            pre->cbuf.alloc(ctx, nreg_max * 4 + 64) == QEH_OK && pre->planbuf.alloc(ctx, sizeof(SlicePlan)) == QEH_OK &&
-            hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess) {
-            if (hipEventCreateWithFlags(&pre->done, hipEventDisableTiming) != hipSuccess) pre->done = nullptr;
-            if (pre->done) {
-                SliceRegions &rg = pre->rg;
-                rg = SliceRegions{};
-                rg.key = pre->kbuf.as<uint16_t>();
-                rg.val = nacol ? pre->vbuf.as<int64_t>() : nullptr;
-                rg.count = pre->cbuf.as<uint32_t>();
-                rg.overflow = rg.count + nreg_max;
-                QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
-                hipLaunchKernelGGL(k_slice_plan, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), pi,
-                                   pre->planbuf.as<SlicePlan>());
-                (void)hipEventRecord(ready, ctx->stream);  // inputs, the plan and the overflow reset
-                (void)hipStreamWaitEvent(side, ready, 0);
-                launch_slice_partition(ctx, in, pp, nterms, nacol, 0, 0, n_tiles, pi.grid, rg, side, nullptr,
-                                       pre->planbuf.as<SlicePlan>());
-                (void)hipEventRecord(pre->done, side);
-                launched = true;
-            }
-            (void)hipEventDestroy(ready);
-        }
-        if (hipGetLastError() != hipSuccess) return fail(QEH_E_HIP, "slice prelaunch failed");
-    }
-    BuildRanges br;
+    QEH_TRY(slice_launch_dev(
+        ctx, cols, n, pp, specs, key_col, &pi, pre,
+        [&](const SlicePlanIn &p, SlicePlan *out) {
+            hipLaunchKernelGGL(k_slice_plan, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), p, out);
+        },
+        &launched));
+    BuildRanges br;  // read while phase A runs (and memoised for the build)
     QEH_TRY(columns_minmax_collect(ctx, both, 2, mm.as<MinMax>(), br.mn, br.mx, br.cnt));
-    if (!launched) return QEH_OK;
-    const SlicePlan pl = plan_slices(pi, br.mn[0], br.mx[0], br.cnt[0], br.mn[1], br.mx[1], br.cnt[1]);
-    if (!pl.ok) {  // phase A returned at once: release the worst-case regions now
-        (void)hipEventSynchronize(pre->done);
-        (void)hipEventDestroy(pre->done);
-        pre->done = nullptr;
-        pre->kbuf.reset(), pre->vbuf.reset(), pre->cbuf.reset(), pre->planbuf.reset();
-        return QEH_OK;
-    }
-    pre->rg.F = pl.F;
-    pre->rg.cap = pl.cap;
-    pre->launched = true;
-    pre->kmin = pl.kmin;
-    pre->range = pl.range;
-    pre->grid = pi.grid;
-    pre->n_tiles = n_tiles;
+    if (launched) settle_dev_plan(pre, plan_slices(pi, br.mn[0], br.mx[0], br.cnt[0], br.mn[1], br.mx[1], br.cnt[1]));
     return QEH_OK;
 }
 
@@ -2332,7 +2416,8 @@ constexpr int kRetryBigger = 100;  // internal: group table too small
 static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, const PredPlan &pp,
                           const GidSource &src, const AggSpecs &specs_in, int64_t G, const KeyCols &out_keys_src,
                           const int32_t *key_dtypes, const uint32_t *rep_row, bool drop_empty, const char *kname,
-                          qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups, SlicePre *pre = nullptr) {
+                          qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups, SlicePre *pre = nullptr,
+                          double *lanes = nullptr) {
     DevBuf states, errw;
     const int64_t Gs = std::max<int64_t>(G, 1);
     AggSpecs specs = specs_in;
@@ -2403,6 +2488,34 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
         uint32_t of = 0;
         QEH_TRY(read_small(ctx, &of, src.gt.overflow, 4));
         if (of) return kRetryBigger;
+    }
+
+    if (lanes) {
+        // dense f64 lanes instead of compacted output columns (the distributed final stage sums them
+        // over the ranks): one host round trip for the status words, none for outputs
+        auto emit = [&]() -> int {
+            hipLaunchKernelGGL(k_states_lanes, dim3((unsigned)(((1 + specs.n) * G + 255) / 256)), dim3(256), 0, ctx->stream,
+                               states.as<uint64_t>(), Gs, G, specs, lanes);
+            return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: lanes launch failed");
+        };
+        if (G > 0) QEH_TRY(emit());
+        uint32_t stw[4];
+        QEH_TRY(read_small(ctx, stw, errw.p, 16));
+        if (ovf_pending && stw[1]) {
+            hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock),
+                               0, ctx->stream, states.as<uint64_t>(), Gs, specs);
+            QEH_HIP(hipMemsetAsync(errw.p, 0, 16, ctx->stream));
+            {
+                KernelTimer kt(ctx, kname);
+                join_fallback(grid, per_cu);
+            }
+            QEH_HIP(hipGetLastError());
+            if (G > 0) QEH_TRY(emit());
+            QEH_TRY(read_small(ctx, stw, errw.p, 16));
+        }
+        QEH_TRY(kernel_error_status(stw[0], "aggregate"));
+        *out_groups = G;
+        return QEH_OK;
     }
 
     // compact non-empty groups; the group count lands in the status words
@@ -2783,6 +2896,54 @@ extern "C" int qeh_join_filter_aggregate_prelaunch(qeh_ctx *ctx, const qeh_colum
     return QEH_OK;
 }
 
+extern "C" int qeh_join_filter_aggregate_prelaunch_stats(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                                         int probe_key_idx, const qeh_expr *predicate, const qeh_agg *aggs,
+                                                         int n_aggs, const int64_t *stats, int world, int row_len) {
+    if (!ctx || !probe_cols || n_probe_cols < 1 || !stats || world < 1 || row_len < 6 || (n_aggs > 0 && !aggs))
+        return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_prelaunch_stats: bad argument");
+    if (probe_key_idx < 0 || probe_key_idx >= n_probe_cols) return fail(QEH_E_INVALID, "probe key index out of range");
+    DeviceGuard dg(ctx->device);
+    ctx->pending_slice.reset();
+    if (n_aggs == 0 || std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
+    const int64_t n = probe_cols[0].length;
+    for (int i = 0; i < n_probe_cols; ++i)
+        if (probe_cols[i].length != n) return fail(QEH_E_INVALID, "probe columns have different lengths");
+    if (probe_cols[probe_key_idx].dtype != QEH_DT_INT64) return QEH_OK;
+    ColSet cols;
+    QEH_TRY(make_colset(probe_cols, n_probe_cols, &cols));
+    std::vector<int32_t> dts(n_probe_cols);
+    std::vector<int> idx(n_probe_cols);
+    for (int i = 0; i < n_probe_cols; ++i) {
+        dts[i] = probe_cols[i].dtype;
+        idx[i] = i;
+    }
+    PredPlan pp;
+    QEH_TRY(plan_predicate(predicate, dts.data(), n_probe_cols, &pp));
+    AggSpecs specs;
+    QEH_TRY(plan_aggs(aggs, n_aggs, probe_cols, n_probe_cols, idx.data(), &specs));
+    auto p = std::make_shared<PendingSlice>();
+    SlicePlanIn pi;
+    bool launched = false;
+    QEH_TRY(slice_launch_dev(
+        ctx, cols, n, pp, specs, probe_key_idx, &pi, &p->pre,
+        [&](const SlicePlanIn &q, SlicePlan *out) {
+            hipLaunchKernelGGL(k_slice_plan_stats, dim3(1), dim3(64), 0, ctx->stream, stats, world, row_len, q, out);
+        },
+        &launched));
+    if (!launched) return QEH_OK;
+    for (int i = 0; i < n_probe_cols; ++i) {
+        p->vals.push_back(probe_cols[i].values);
+        p->offs.push_back(probe_cols[i].offset);
+        p->lens.push_back(probe_cols[i].length);
+        p->dtypes.push_back(probe_cols[i].dtype);
+    }
+    p->key_idx = probe_key_idx;
+    p->pred = PendingSlice::serialise(predicate);
+    p->agg_fc = PendingSlice::agg_list(aggs, n_aggs);
+    ctx->pending_slice = p;
+    return QEH_OK;
+}
+
 // ---- dense partial states of a distributed broadcast join (qeh_dense_states_f64 / _take) ----
 struct DenseCols {
     const void *vals[kMaxAggs];
@@ -2918,11 +3079,11 @@ __global__ void k_seq_i64(int64_t *p, int64_t n, int64_t base, int as32) {
 // table-form broadcast join, include/qeh.h): group g = entry - 1, key group_min + g.  The group
 // keys are a synthesised column group_min + [0, G) with representative row g, so the aggregate and
 // finalize are qeh_join_filter_aggregate's own.
-extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
-                                               int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
-                                               int64_t key_min, uint64_t key_range, int64_t group_min, int64_t n_groups,
-                                               int32_t group_dtype, const qeh_agg *aggs, int n_aggs, qeh_column *out_keys,
-                                               qeh_column *out_aggs, int64_t *out_groups) {
+static int join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                                       const qeh_expr *predicate, const uint16_t *table, int64_t key_min,
+                                       uint64_t key_range, int64_t group_min, int64_t n_groups, int32_t group_dtype,
+                                       const qeh_agg *aggs, int n_aggs, qeh_column *out_keys, qeh_column *out_aggs,
+                                       int64_t *out_groups, double *lanes) {
     if (!ctx || !out_groups || !table || key_range == 0 || key_range >= (1ull << 32) || n_groups < 1 ||
         n_groups >= 0xFFFE || (group_dtype != QEH_DT_INT64 && group_dtype != QEH_DT_INT32))
         return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table: bad argument");
@@ -2950,7 +3111,10 @@ extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *p
     SlicePre pre;
     std::shared_ptr<PendingSlice> pend = std::static_pointer_cast<PendingSlice>(ctx->pending_slice);
     ctx->pending_slice.reset();
-    if (pend && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs)) pend->take(&pre);
+    if (pend && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs)) {
+        if (pend->pre.dev_planned) QEH_TRY(resolve_dev_plan(ctx, &pend->pre, &pend->br));
+        pend->take(&pre);
+    }
     pend.reset();  // not adopted: waits for its phase A, frees its regions
     // (try_slice_join adopts `pre` only for this table's key range and tile count)
     DevBuf gkeys, rep;
@@ -2977,8 +3141,34 @@ extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *p
     src.jt.unique = 1;
     src.key_col = probe_key_idx;
     const int32_t kd = group_dtype;
+    if (lanes)
+        for (int a = 0; a < specs.n; ++a)
+            if (!((specs.a[a].kind == AK_SUM_F && specs.a[a].func == QEH_AGG_SUM && specs.a[a].cnt_slot == 0) ||
+                  (specs.a[a].kind == AK_COUNT && specs.a[a].func == QEH_AGG_COUNT)))
+                return fail(QEH_E_UNSUPPORTED, "dense lanes carry COUNT and non-null float SUM aggregates only");
     return aggregate_rows(ctx, GM_JOIN, cols, n, pp, src, specs, n_groups, keys, &kd, rep.as<uint32_t>(), true,
-                          "join_filter_aggregate", out_keys, out_aggs, out_groups, &pre);
+                          "join_filter_aggregate", out_keys, out_aggs, out_groups, &pre, lanes);
+}
+
+extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                               int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
+                                               int64_t key_min, uint64_t key_range, int64_t group_min, int64_t n_groups,
+                                               int32_t group_dtype, const qeh_agg *aggs, int n_aggs, qeh_column *out_keys,
+                                               qeh_column *out_aggs, int64_t *out_groups) {
+    return join_filter_aggregate_table(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, table, key_min, key_range,
+                                       group_min, n_groups, group_dtype, aggs, n_aggs, out_keys, out_aggs, out_groups,
+                                       nullptr);
+}
+
+extern "C" int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                                     int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
+                                                     int64_t key_min, uint64_t key_range, int64_t n_groups,
+                                                     const qeh_agg *aggs, int n_aggs, double *lanes) {
+    if (!lanes) return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table_lanes: bad argument");
+    if (n_aggs == 0) return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table_lanes: no aggregates");
+    int64_t g = 0;
+    return join_filter_aggregate_table(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, table, key_min, key_range,
+                                       0, n_groups, QEH_DT_INT64, aggs, n_aggs, nullptr, nullptr, &g, lanes);
 }
 
 extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
@@ -3019,11 +3209,12 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
     std::shared_ptr<PendingSlice> pend = std::static_pointer_cast<PendingSlice>(ctx->pending_slice);
     ctx->pending_slice.reset();
     if (pend && n_group_keys == 1 && pend->matches(probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs)) {
-        // adopt the phase A launched by qeh_join_filter_aggregate_prelaunch if the build columns that
-        // arrived have exactly the ranges it was planned from
+        // adopt the phase A launched by qeh_join_filter_aggregate_prelaunch(_stats) if the build columns
+        // that arrived have exactly the ranges it was planned from
+        if (pend->pre.dev_planned) QEH_TRY(resolve_dev_plan(ctx, &pend->pre, &pend->br));
         const qeh_column both[2] = {*build_key, build_group_keys[0]};
         BuildRanges br;
-        if (build_key->dtype == QEH_DT_INT64 &&
+        if (pend->pre.launched && build_key->dtype == QEH_DT_INT64 &&
             (build_group_keys[0].dtype == QEH_DT_INT64 || build_group_keys[0].dtype == QEH_DT_INT32)) {
             QEH_TRY(columns_minmax(ctx, both, 2, br.mn, br.mx, br.cnt));
             if (br == pend->br) pend->take(&pre);

@@ -360,6 +360,45 @@ extern "C" int qeh_columns_minmax(qeh_ctx *ctx, const qeh_column *cols, int n_co
     return QEH_OK;
 }
 
+struct StatsExtra {
+    int64_t v[16];
+    int32_t n;
+};
+__global__ void k_bcast_stats(const MinMax *__restrict__ mm, int64_t rows, StatsExtra ex, int64_t *__restrict__ out) {
+    const int t = threadIdx.x;
+    if (t == 0) {
+        out[0] = rows;
+        out[1] = rows ? mm[0].mn : INT64_MAX;
+        out[2] = rows ? mm[0].mx : INT64_MIN;
+        out[3] = rows ? mm[1].mn : INT64_MAX;
+        out[4] = rows ? mm[1].mx : INT64_MIN;
+    }
+    if (t < ex.n) out[5 + t] = ex.v[t];
+}
+
+extern "C" int qeh_broadcast_stats(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
+                                   const int64_t *extra, int n_extra, int64_t *dev_out) {
+    if (!ctx || !build_key || !group_key || !dev_out || n_extra < 0 || n_extra > 16 || (n_extra > 0 && !extra))
+        return fail(QEH_E_INVALID, "qeh_broadcast_stats: bad argument");
+    const qeh_column both[2] = {*build_key, *group_key};
+    for (int i = 0; i < 2; ++i) {
+        QEH_TRY(check_column(both[i], "broadcast stats column"));
+        if (both[i].dtype != QEH_DT_INT64 && both[i].dtype != QEH_DT_INT32)
+            return fail(QEH_E_UNSUPPORTED, "qeh_broadcast_stats: Int32 / Int64 columns");
+    }
+    if (build_key->length != group_key->length) return fail(QEH_E_INVALID, "qeh_broadcast_stats: columns have different lengths");
+    DeviceGuard dg(ctx->device);
+    DevBuf mm;  // stream-ordered reuse: read by k_bcast_stats before any later allocation's kernels
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 + 16));
+    if (build_key->length > 0) QEH_TRY(columns_minmax_launch(ctx, both, 2, mm.as<MinMax>()));
+    StatsExtra ex{};
+    ex.n = n_extra;
+    for (int i = 0; i < n_extra; ++i) ex.v[i] = extra[i];
+    hipLaunchKernelGGL(k_bcast_stats, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), build_key->length, ex, dev_out);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
 extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out) {
     if (!ctx || !out || (n > 0 && !table)) return fail(QEH_E_INVALID, "qeh_u16_count_nonzero: bad argument");
     DeviceGuard dg(ctx->device);

@@ -419,6 +419,44 @@ class Context:
                                                            ok, oa, C.byref(g)))
         return [self._wrap(ok[0])], [self._wrap(oa[i]) for i in range(len(aggs))], g.value
 
+    def join_filter_aggregate_table_lanes(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                                          predicate: Optional[PhysicalExpr], table_ptr: int, key_min: int,
+                                          key_range: int, n_groups: int, aggs: Sequence[Tuple[int, int]],
+                                          lanes_ptr: int) -> None:
+        """qeh_join_filter_aggregate_table_lanes: the table-form fused operator writing the dense
+        final stage's f64 lanes [1 + len(aggs)][n_groups] (row counts, then COUNT / float SUM partials)."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        abi.check(self.lib.qeh_join_filter_aggregate_table_lanes(self.h, cp, len(probe_cols), probe_key_idx,
+                                                                 C.byref(e) if e is not None else None, table_ptr,
+                                                                 key_min, key_range, n_groups, ca, len(aggs),
+                                                                 lanes_ptr))
+
+    def broadcast_stats(self, build_key: DeviceColumn, group_key: DeviceColumn, extra: Sequence[int],
+                        out_ptr: int) -> None:
+        """qeh_broadcast_stats: [rows, key min, max, group min, max, *extra] of this dimension shard
+        into device memory (no host wait)."""
+        ex = (C.c_int64 * max(len(extra), 1))(*[int(q) for q in extra])
+        abi.check(self.lib.qeh_broadcast_stats(self.h, C.byref(build_key.c), C.byref(group_key.c), ex, len(extra),
+                                               out_ptr))
+
+    def join_filter_aggregate_prelaunch_stats(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                                              predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],
+                                              stats_ptr: int, world: int, row_len: int) -> None:
+        """qeh_join_filter_aggregate_prelaunch_stats: phase A planned on the device from the gathered
+        qeh_broadcast_stats rows (no host wait); the adopting call reads the plan back."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        abi.check(self.lib.qeh_join_filter_aggregate_prelaunch_stats(self.h, cp, len(probe_cols), probe_key_idx,
+                                                                     C.byref(e) if e is not None else None, ca,
+                                                                     len(aggs), stats_ptr, world, row_len))
+
     def join_filter_aggregate_prelaunch(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                                         predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],
                                         build_key_range: Sequence[int], group_key_range: Sequence[int]) -> None:

@@ -527,7 +527,8 @@ class DistributedExecutor:
         probe_nullable = None
         self.last_build = "replicated"
         if build_sharded:
-            st = self._build_stats(build_key, build_group_keys, probe_flags)
+            st = self._build_stats(build_key, build_group_keys, probe_flags,
+                                   probe=(probe_cols, probe_key_idx, predicate, aggs))
             full = None
             if st is not None:
                 probe_nullable = st["agreed"]
@@ -569,7 +570,7 @@ class DistributedExecutor:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t.cpu().numpy()
 
-    def _build_stats(self, build_key, build_group_keys, probe_flags: Sequence[int]):
+    def _build_stats(self, build_key, build_group_keys, probe_flags: Sequence[int], probe=None):
         """One small all_gather of every dimension shard's [rows, key min / max, group key min / max,
         has-bitmap] and the fact shard's aggregate-input bitmap flags: the job-wide ranges both
         device broadcast forms plan from.  None when the shape is outside them (decided from
@@ -581,18 +582,29 @@ class DistributedExecutor:
             return None
         n = len(build_key)
         ts = [self._to_tensors(c)[0] for c in cols]
-        big, small = np.iinfo(np.int64).max, np.iinfo(np.int64).min
         flags = [1 if any(c.c.validity for c in cols) else 0] + list(probe_flags)
-        if n:  # one library min / max pass over both columns (one host read), not torch reductions
-            (kmn, kmx, _), (gmn, gmx, _) = self.ctx.columns_minmax(cols)
-            vals = [n, kmn, kmx, gmn, gmx] + flags
-        else:
-            vals = [0, big, small, big, small] + flags
-        M = _allgather_meta(np.array(vals, np.int64), self.world, self.device, self.group)
+        # [rows, key min / max, group key min / max, flags] written on the device by one library call
+        # (min / max kernels, no host wait), gathered over the ranks, read back once
+        row = torch.empty(5 + len(flags), dtype=torch.int64, device="cuda")
+        self._sync_torch()
+        self.ctx.broadcast_stats(build_key, build_group_keys[0], flags, row.data_ptr())
+        self._sync()
+        if self.world > 1:
+            out = torch.empty(self.world * row.numel(), dtype=torch.int64, device="cuda")
+            dist.all_gather_into_tensor(out, row, group=self.group)
+            row = out
+        prelaunched = False
+        if probe is not None and not os.environ.get("QEH_HOST_PLAN"):
+            # phase A planned on the device from the gathered rows: it starts while the host reads them
+            self._sync_torch()
+            self.ctx.join_filter_aggregate_prelaunch_stats(*probe, row.data_ptr(), self.world, 5 + len(flags))
+            prelaunched = True
+        M = row.cpu().numpy().reshape(self.world, -1)
         rows = [int(x) for x in M[:, 0]]
         total = sum(rows)
         out = {"M": M, "rows": rows, "total": total, "n": n, "ts": ts, "bitmap": bool(M[:, 5].max() > 0),
-               "agreed": M[:, 6:].max(axis=0), "gdtype": build_group_keys[0].dtype}
+               "agreed": M[:, 6:].max(axis=0), "gdtype": build_group_keys[0].dtype, "prelaunched": prelaunched,
+               "stats_dev": row}
         if total:
             live = M[M[:, 0] > 0]
             out["krange"] = [int(live[:, 1].min()), int(live[:, 2].max()), total]
@@ -617,7 +629,9 @@ class DistributedExecutor:
         R, G = kmax - kmin + 1, gmax - gmin + 1
         if R > 4 * total + 1024 or R >= (1 << 31) or G > 4096 or self.world * (G + 1) >= (1 << 16):
             return None
-        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"], st["grange"])
+        if not st["prelaunched"]:
+            self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"],
+                                                     st["grange"])
         table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
         self._sync_torch()  # zeroed before the library writes
         if st["n"]:
@@ -628,6 +642,24 @@ class DistributedExecutor:
         self._sync_torch()
         if self.ctx.u16_count_nonzero(table.data_ptr(), R) != total:
             return None  # a build key repeats: the general path handles multi-match joins
+        if (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
+                and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
+                        for j, (f, c) in enumerate(aggs))):
+            # the fused operator writes the dense final stage's lanes itself (row counts, COUNT / float
+            # SUM partials per group slot): no compaction, output columns or re-scatter of the partials
+            lanes = torch.empty((1 + len(aggs)) * G, dtype=torch.float64, device="cuda")
+            self._sync_torch()
+            self.ctx.join_filter_aggregate_table_lanes(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin, R,
+                                                       G, aggs, lanes.data_ptr())
+            self._sync()
+            if self.world > 1:
+                dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+            self._sync_torch()
+            ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank,
+                                                   st["gdtype"],
+                                                   [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
+            self.last_final = "dense"
+            return [ok], ov, g
         pk, pa_, g = self.ctx.join_filter_aggregate_table(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
                                                           R, gmin, G, st["gdtype"], aggs)
         if g == 0:
@@ -655,7 +687,9 @@ class DistributedExecutor:
             buf = torch.empty(self.world * mx, dtype=t.dtype, device=t.device)
             works.append(dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group, async_op=True))
             bufs.append(buf)
-        self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"], st["grange"])
+        if not st["prelaunched"]:
+            self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"],
+                                                     st["grange"])
         for w in works:
             w.wait()
         out = []

@@ -324,6 +324,33 @@ def test_table_form_broadcast_join_vs_oracle(ctx, shards, dup):
                                           [ob.HostCol(dg)], AGGS)
     assert g == wg
     assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
+    # the lanes form (qeh_join_filter_aggregate_table_lanes): row counts and the COUNT / float SUM
+    # partials of every group slot, then the dense take (world 1) == the compacted groups
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
+    lanes = torch.full((3 * G,), -7.0, dtype=torch.float64, device="cuda")  # every entry must be written
+    torch.cuda.synchronize()
+    ctx.join_filter_aggregate_table_lanes([ctx.upload(x), ctx.upload(k), ctx.upload(v)], 1, PRED, total.data_ptr(),
+                                          kmin, R, G, aggs, lanes.data_ptr())
+    ln = lanes.cpu().numpy().reshape(3, G)
+    assert (ln >= 0).all() and np.array_equal(ln[0], ln[2])
+    want = {int(kk): (float(sv), int(cv)) for kk, sv, cv in zip(wk[0][0], wa[0][0], wa[1][0])}
+    got = {gmin + i: (ln[1][i], int(ln[2][i])) for i in range(G) if ln[0][i] > 0}
+    assert got.keys() == want.keys()
+    for kk, (sv, cv) in want.items():
+        assert got[kk][1] == cv and abs(got[kk][0] - sv) <= 1e-9 * max(abs(sv), 1.0)
+    ok, ov, tg = ctx.dense_states_take(lanes.data_ptr(), 2, gmin, G, 1, 0, abi.DT_INT64, [abi.DT_FLOAT64, abi.DT_INT64])
+    assert tg == wg
+    assert_grouped_equal([ok.to_numpy()], [c.to_numpy() for c in ov], wk, wa, float_aggs=[0])
+    # this shard's stats row on the device (qeh_broadcast_stats) == the host min / max
+    row = torch.zeros(7, dtype=torch.int64, device="cuda")
+    ctx.broadcast_stats(ctx.upload(dk), ctx.upload(dg), [1, 0], row.data_ptr())
+    assert row.cpu().tolist() == [n_dim, int(dk.min()), int(dk.max()), int(dg.min()), int(dg.max()), 1, 0]
+    ctx.broadcast_stats(ctx.upload(dk[:0]), ctx.upload(dg[:0]), [0, 1], row.data_ptr())
+    big, small = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+    assert row.cpu().tolist() == [0, big, small, big, small, 0, 1]
+    with pytest.raises(abi.QehError):  # MIN is not a lane aggregate
+        ctx.join_filter_aggregate_table_lanes([ctx.upload(x), ctx.upload(k), ctx.upload(v)], 1, PRED, total.data_ptr(),
+                                              kmin, R, G, [(AF.Min, 2)], lanes.data_ptr())
     with pytest.raises(abi.QehError):  # a key outside the declared range is refused, nothing written
         ctx.direct_group_table_insert(ctx.upload(dk[:10] + R), ctx.upload(dg[:10]), kmin, R, gmin, total.data_ptr())
 
