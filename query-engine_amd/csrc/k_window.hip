@@ -410,17 +410,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
 }
 
 // pass 2: inside each bucket, stable partition by the low digit; group starts -> pstart
-// Pass 2 also leaves, for each bucket, the run positions at the first tile of each of kWmInvChunks
-// equal tile ranges (snap[(bucket * kWmInvChunks + c) * L + digit]) -- where the XCD-cooperative
-// inverse (k_wm2_inv2c) starts its workgroups' replays.
-constexpr int kWmInvChunks = 64;  // inverse-2 workgroups per XCD (two per CU)
-__host__ __device__ inline int64_t wm_chunk_tile(int64_t c, int64_t T) { return c * T / kWmInvChunks; }
-
 template <int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
-                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart,
-                                                        uint32_t *__restrict__ snap) {
+                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
@@ -467,15 +460,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             }
         };
         if (s0 < s1) load(s0);
-        const int64_t T = (s1 - s0 + kWmTile - 1) / kWmTile;
-        int64_t c_next = 0;  // next chunk whose first tile's positions are recorded
         for (int64_t t0 = s0; t0 < s1; t0 += kWmTile) {
-            if (snap) {
-                const int64_t t = (t0 - s0) / kWmTile;
-                for (; c_next < kWmInvChunks && wm_chunk_tile(c_next, T) <= t; ++c_next)
-                    if (wm_chunk_tile(c_next, T) == t && tid < L)
-                        snap[((int64_t)b * kWmInvChunks + c_next) * L + tid] = lpos[tid];
-            }
             uint32_t d[NJ], slot[NJ];
             uint64_t keys[NJ];
             bool live[NJ];
@@ -1024,111 +1009,6 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
     }
 }
 
-// XCD-cooperative inverse of pass 2: the workgroups of one XCD (b % 8, dispatched round-robin over
-// the XCDs) take the buckets q with q % 8 == XCD together, each replaying one of kWmInvChunks tile
-// ranges from the run positions pass 2 recorded there -- so one bucket's results (2 B per row, ~2 MB)
-// are read through that XCD's L2 while all its tiles are replayed, instead of every workgroup
-// streaming its own bucket and fetching each result line once per tile that touches it.
-template <int DB, bool VAL = false>
-__global__ __launch_bounds__(kWmBlock) void k_wm2_inv2c(WmShape sh, const uint64_t *__restrict__ bstart,
-                                                        const uint32_t *__restrict__ snap, const uint16_t *__restrict__ i_kl,
-                                                        const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1,
-                                                        const uint64_t *__restrict__ res2v, uint64_t *__restrict__ res1v) {
-    __shared__ WmRankLds R;
-    __shared__ uint32_t lpos[kWmDig];
-    __shared__ uint16_t st_d[kWmTile], st_r[kWmTile];
-    __shared__ uint64_t st_v[VAL ? kWmTile : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int NJ = kWmTile / kWmBlock;
-    const int64_t L = (int64_t)1 << sh.lb;
-    const int dbits = sh.lb;
-    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    const int xcd = blockIdx.x & 7, c = blockIdx.x >> 3;  // gridDim.x = 8 * kWmInvChunks
-    // this workgroup's tile ranges, one per bucket q = xcd (mod 8), walked as one sequence: the next
-    // tile's loads (and at a range's last tile the next range's start positions) are issued before the
-    // current tile's LDS phases, across range boundaries too
-    struct Range {
-        int b;
-        int64_t e0, e1;  // rows of the range
-    };
-    auto next_range = [&](int b) -> Range {
-        for (; b < sh.nb; b += 8) {
-            const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
-            const int64_t T = (s1 - s0 + kWmTile - 1) / kWmTile;
-            const int64_t ta = wm_chunk_tile(c, T), tb = wm_chunk_tile(c + 1, T);
-            if (ta < tb) return Range{b, s0 + ta * kWmTile, std::min<int64_t>(s1, s0 + tb * kWmTile)};
-        }
-        return Range{sh.nb, 0, 0};
-    };
-    uint32_t lx[NJ];
-    auto load = [&](const Range &r, int64_t t0) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int64_t i = t0 + woff + j * 64;
-            lx[j] = __builtin_nontemporal_load(i_kl + (i < r.e1 ? i : r.e0));
-        }
-    };
-    auto snap_of = [&](const Range &r) -> uint32_t {
-        return tid < L ? snap[((int64_t)r.b * kWmInvChunks + c) * L + tid] : 0u;
-    };
-    Range cur = next_range(xcd);
-    if (cur.b >= sh.nb) return;
-    load(cur, cur.e0);
-    uint32_t snapv = snap_of(cur);
-    int64_t t0 = cur.e0;
-    bool fresh = true;  // first tile of the range: start positions from snapv
-    while (true) {
-        if (fresh) {
-            lpos[tid] = snapv;
-            __syncthreads();
-            fresh = false;
-        }
-        uint32_t d[NJ], slot[NJ];
-        bool live[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            live[j] = t0 + woff + j * 64 < cur.e1;
-            d[j] = lx[j];
-        }
-        Range nxt = cur;
-        int64_t nt0 = t0 + kWmTile;
-        if (nt0 >= cur.e1) {
-            nxt = next_range(cur.b + 8);
-            nt0 = nxt.e0;
-        }
-        if (nxt.b < sh.nb) {
-            load(nxt, nt0);
-            if (nxt.b != cur.b) snapv = snap_of(nxt);
-        }
-        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
-        wm_barrier();
-        const int m = (int)std::min<int64_t>(kWmTile, cur.e1 - t0);
-#pragma unroll 8
-        for (int s = tid; s < m; s += kWmBlock) {
-            const uint32_t dd = st_d[s];
-            const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
-            st_r[s] = res2[src];
-            if (VAL) st_v[s] = res2v[src];
-        }
-        wm_barrier();
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (live[j]) {
-                __builtin_nontemporal_store(st_r[slot[j]], res1 + t0 + woff + j * 64);
-                if (VAL) __builtin_nontemporal_store(st_v[slot[j]], res1v + t0 + woff + j * 64);
-            }
-        lpos[tid] += tcnt;
-        wm_barrier();
-        if (nxt.b >= sh.nb) break;
-        fresh = nxt.b != cur.b;
-        cur = nxt;
-        t0 = nt0;
-    }
-}
-
 // inverse of pass 1: replay each workgroup's tiles, gather the results run by run and write them in
 // input order as Int64
 // VAL = 0: rank functions, out = Int64 results.  VAL = 4 / 8 (value functions): res1 holds valid
@@ -1215,11 +1095,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int g1 = (int)((n + sh.span - 1) / sh.span);
     const bool value_fn = func >= QEH_WIN_LAG;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, snap;
-    // the XCD-cooperative inverse of pass 2 (QEH_WM_INV2C=1; default: one workgroup per bucket)
-    const bool coop = std::getenv("QEH_WM_INV2C") && std::atoi(std::getenv("QEH_WM_INV2C")) == 1;
-    if (coop && snap.alloc(ctx, (size_t)sh.nb * kWmInvChunks * ((size_t)1 << sh.lb) * 4))
-        return fail(QEH_E_OOM, "window: out of device memory");
+    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     if (cnt1.alloc(ctx, nc1 * 4) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
@@ -1251,7 +1127,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         if (!sh.exp)  // (experiment runs: pass 1 only)
         hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
                            bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
-                           pst.as<uint64_t>(), coop ? snap.as<uint32_t>() : nullptr);
+                           pst.as<uint64_t>());
     }
     QEH_HIP(hipGetLastError());
     if (sh.exp) {  // experiment runs stop after the partition passes (their outputs are not valid)
@@ -1324,13 +1200,6 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
     {
         KernelTimer kt(ctx, "window_place");
-        if (coop)
-            hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2c<kWmAtomicRank, true> : sh.lb == 10 ? k_wm2_inv2c<10, true> : k_wm2_inv2c<-1, true>)
-                                        : (at ? k_wm2_inv2c<kWmAtomicRank, false> : sh.lb == 10 ? k_wm2_inv2c<10, false> : k_wm2_inv2c<-1, false>),
-                               dim3(8 * kWmInvChunks), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), snap.as<uint32_t>(),
-                               kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(), res2v.as<uint64_t>(),
-                               res1v.as<uint64_t>());
-        else
         hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : sh.lb == 10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
                                     : (at ? k_wm2_inv2<kWmAtomicRank, false> : sh.lb == 10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
                            dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
