@@ -668,7 +668,9 @@ __device__ __forceinline__ void slice_states_init(uint64_t *lst, int64_t stride,
 // range of 2^kGidSliceBits groups, whose states live in LDS while the workgroup drains that slice
 // and are merged into the global states when it moves on.
 // PF: the next 512 items of a region are loaded while this chunk is looked up and aggregated.
-template <int NACOL, bool IDENT = false, bool PF = false>
+// PV: items loaded two per lane (a 4-B key pair and a 16-B value pair per load; 128 items per wave
+// load instead of 64) -- half the load instructions for the same bytes.
+template <int NACOL, bool IDENT = false, bool PF = false, bool PV = false>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
                                                              AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
     constexpr int VC = NACOL > 0 ? 1 : 0;
@@ -732,13 +734,34 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             const int64_t *vp = VC ? rg.val + reg * rg.cap : nullptr;
             uint32_t en[8];
             int64_t vn[8];
+            // item of register j (the masks below use the same map)
+            auto item = [&](uint32_t i0, int j) -> uint32_t {
+                return PV ? i0 + (uint32_t)(j >> 1) * 128 + 2 * lane + (uint32_t)(j & 1) : i0 + (uint32_t)j * 64 + lane;
+            };
             auto ld = [&](uint32_t i0) {
+                if constexpr (PV) {
+                    // pairs start at even items; a pair past the count reads inside the region buffer
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t i = i0 + j * 64 + lane;
-                    const uint32_t ii = i < n_r ? i : 0u;
-                    en[j] = __builtin_nontemporal_load(kp + ii);
-                    vn[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i = item(i0, 2 * j);
+                        const uint32_t ii = i < n_r ? i : 0u;
+                        const uint32_t kk = __builtin_nontemporal_load((const uint32_t *)(kp + ii));
+                        en[2 * j] = kk & 0xFFFFu, en[2 * j + 1] = kk >> 16;
+                        if (VC) {
+                            const v2i64 w = __builtin_nontemporal_load((const v2i64 *)(vp + ii));
+                            vn[2 * j] = w[0], vn[2 * j + 1] = w[1];
+                        } else {
+                            vn[2 * j] = vn[2 * j + 1] = 0;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint32_t i = item(i0, j);
+                        const uint32_t ii = i < n_r ? i : 0u;
+                        en[j] = __builtin_nontemporal_load(kp + ii);
+                        vn[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
+                    }
                 }
             };
             if (PF && n_r) ld(0);
@@ -751,7 +774,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                 if (PF && i0 + 64 * 8 < n_r) ld(i0 + 64 * 8);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    e[j] = (i0 + j * 64 + lane < n_r) ? (IDENT ? e[j] + 1u : (uint32_t)tslice[e[j]]) : 0u;
+                    e[j] = (item(i0, j) < n_r) ? (IDENT ? e[j] + 1u : (uint32_t)tslice[e[j]]) : 0u;
                 // aggregate kinds are uniform: switch once per aggregate, then
                 // issue the 8 items' LDS atomics back to back
 #pragma unroll
@@ -2016,9 +2039,16 @@ static void launch_slice_probe(qeh_ctx *ctx, const SliceRegions &rg, int nreg, c
     KernelTimer ktb(ctx, "slice_probe");
     const int gridB = ctx->props.multiProcessorCount;
     const bool pf = slice_probe_prefetch();
+    static const bool pv = std::getenv("QEH_SLICE_B_PAIRS") && std::atoi(std::getenv("QEH_SLICE_B_PAIRS")) == 1;
 #define QEH_SB(NAV, PFV)                                                                                           \
-    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, 0, t, \
-                       in, specs, G, states)
+    do {                                                                                                           \
+        if (pv)                                                                                                    \
+            hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, \
+                               nreg, 0, t, in, specs, G, states);                                            \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, nreg, \
+                               0, t, in, specs, G, states);                                                  \
+    } while (0)
     if (nacol == 0) {
         if (pf) QEH_SB(0, true);
         else QEH_SB(0, false);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase A / phase B kernel times of the metric query (1e9 x 1e7) for several builds of the library,
 alternating builds in rounds (results are not checked: experiment builds may compute garbage).
-usage: python tools/r3/exp_slice.py [--rows N] [--steps K] [--rounds R] lib1.so lib2.so ..."""
+usage: python tools/r3/exp_slice.py [--rows N] [--steps K] [--rounds R] lib1.so[:ENV=V,ENV2=V2] ..."""
 import argparse
 import os
 import subprocess
@@ -51,12 +51,17 @@ def main():
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     for r in range(a.rounds):
-        for lib in a.libs:
+        for spec in a.libs:
+            lib, _, envs = spec.partition(":")
+            env = dict(os.environ)
+            for kv in filter(None, envs.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             p = os.path.join(ROOT, "query-engine_amd", lib) if not os.path.isabs(lib) else lib
             code = CHILD % {"root": ROOT, "lib": p, "rows": a.rows, "steps": a.steps}
-            out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+            out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
             line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-400:]
-            print(f"round {r} {line}", flush=True)
+            print(f"round {r} [{envs}] {line}", flush=True)
             if out.returncode != 0:
                 sys.exit(out.returncode)
 
