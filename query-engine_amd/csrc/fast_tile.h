@@ -30,10 +30,12 @@ __device__ __forceinline__ v2i64 ld2(const int64_t *p) {
 
 // One 2048-row tile of the fast-path columns: every load (16-B pairs) issued
 // before the term predicate is evaluated.  Lane rows: base + j*128 + {0,1}.
-template <int NTERMS, int NACOL, bool NT>
+// P: row pairs per lane (kFastPairs; the two-value-column slice pass uses 2).
+template <int NTERMS, int NACOL, bool NT, int P = kFastPairs>
 struct FastTile {
-    v2i64 key[kFastPairs], ac[NACOL > 0 ? NACOL : 1][kFastPairs];
-    v2i64 tc[NTERMS > 0 ? NTERMS : 1][kFastPairs];
+    static constexpr int R = 2 * P;
+    v2i64 key[P], ac[NACOL > 0 ? NACOL : 1][P];
+    v2i64 tc[NTERMS > 0 ? NTERMS : 1][P];
     uint32_t sel;
     __device__ __forceinline__ void load(const FastIn &in, const PredTerms &terms, int64_t base) {
         issue(in, base);
@@ -42,26 +44,26 @@ struct FastTile {
     // issue every load of the tile (no use of the data: they stay in flight)
     __device__ __forceinline__ void issue(const FastIn &in, int64_t base) {
 #pragma unroll
-        for (int j = 0; j < kFastPairs; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
+        for (int j = 0; j < P; ++j) key[j] = ld2<NT>(in.key + base + j * 128);
 #pragma unroll
         for (int i = 0; i < NTERMS; ++i)
 #pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
+            for (int j = 0; j < P; ++j) tc[i][j] = ld2<NT>(in.term[i] + base + j * 128);
 #pragma unroll
         for (int c = 0; c < NACOL; ++c)
 #pragma unroll
-            for (int j = 0; j < kFastPairs; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
+            for (int j = 0; j < P; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
     }
     // evaluate the term predicate into `sel`
     __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
-        sel = (1u << kFastR) - 1u;
+        sel = (1u << R) - 1u;
 #pragma unroll
         for (int i = 0; i < NTERMS; ++i) {
             const PredTerm pt = terms.t[i];
             const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
             uint32_t tr = 0;
 #pragma unroll
-            for (int r = 0; r < kFastR; ++r) {
+            for (int r = 0; r < R; ++r) {
                 int64_t v = tc[i][r >> 1][r & 1];
                 if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
                 if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;

@@ -305,7 +305,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 struct SliceRegions {
     uint16_t *key;        // [grid][F][cap] key - kmin - slice * 2^16
-    int64_t *val;         // [grid][F][cap] aggregate input (NACOL == 1)
+    int64_t *val;         // [grid][F][cap] aggregate input (NACOL >= 1)
+    int64_t *val2;        // [grid][F][cap] second aggregate input (NACOL == 2)
     uint32_t *count;      // [grid][F]
     uint32_t *overflow;   // set when a region fills up (skewed probe keys)
     uint64_t cap;         // items per region, multiple of kSliceChunk
@@ -402,11 +403,21 @@ struct __attribute__((aligned(16))) SliceChunk {
 // copied by waves 1-15 while wave 0 scans tile t+1's counts.  Counts, carried counts, write
 // positions and tile offsets are double-buffered by tile parity.
 //   [flush(t-1); eval + rank(t)] B1 [scan(t) | carry(t-1)] B2 [stage(t), plan chunks(t), issue(t+1)] B3
+// NACOL = 2 (two aggregate columns, 18-B items) stages half tiles (P = 2 pairs per lane, 4096 rows)
+// and flushes 16-item chunks, so staging and carries fit one CU's LDS.
+template <int NACOL>
+struct SliceShape {
+    static constexpr int P = NACOL > 1 ? 2 : kFastPairs;
+    static constexpr int CH = NACOL > 1 ? 16 : kSliceChunk;
+    static constexpr int TILE = kSliceBlock * 2 * P;
+};
+
 template <int NTERMS, int NACOL, bool NT, int MODE = 0>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
                                                                  int64_t n_tiles, SliceRegions rg, HashTable t,
                                                                  const SlicePlan *__restrict__ dplan = nullptr) {
-    constexpr int R = kFastR, TILE = kSliceTile, CH = kSliceChunk, MAXF = kSliceMaxF;
+    constexpr int P = SliceShape<NACOL>::P, R = 2 * P, TILE = SliceShape<NACOL>::TILE, CH = SliceShape<NACOL>::CH;
+    constexpr int MAXF = kSliceMaxF;
     if (dplan) {  // planned on the device: the shape comes from the build key's range in memory
         const SlicePlan pl = *dplan;
         if (!pl.ok) return;  // not the slice path: the host discards this launch
@@ -414,15 +425,17 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         rg.F = pl.F, rg.cap = pl.cap;
     }
     constexpr int SB = MODE ? kGidSliceBits : kSliceBits;
-    constexpr int VC = NACOL > 0 ? 1 : 0;  // staged value columns
+    constexpr int VC = NACOL;               // staged value columns
+    constexpr int VS = VC > 0 ? VC : 1;
     __shared__ uint32_t cntb[2][MAXF], cnb[2][MAXF], posb[2][MAXF], lofsb[2][MAXF], mpre[MAXF], hd[MAXF];
     __shared__ uint64_t abase[MAXF];  // region start, aligned down to a whole chunk (exact layout)
     __shared__ uint32_t s_chunks;
     __shared__ SliceChunk cdesc[TILE / CH + MAXF];
     __shared__ uint16_t st_key[TILE];
-    __shared__ int64_t st_v[VC ? TILE : 1];
+    __shared__ int64_t st_v[VS][VC ? TILE : 1];
     __shared__ uint16_t c_key[MAXF * CH];
-    __shared__ int64_t c_v[VC ? MAXF * CH : 1];
+    __shared__ int64_t c_v[VS][VC ? MAXF * CH : 1];
+    int64_t *const vout[2] = {rg.val, rg.val2};
     const int F = rg.F;
     const uint64_t cap = rg.cap;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -450,32 +463,36 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             const SliceChunk d = cdesc[c];
             const uint32_t coff = d.pk & 8191u, clim = (d.pk >> 13) & 63u, lo = (d.pk >> 19) & 63u, hi = d.pk >> 25;
             uint16_t kv[2];
-            int64_t vv[2] = {0, 0};
+            int64_t vv[VS][2] = {};
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t x = xl + q;
                 if (x < clim) {
                     kv[q] = c_key[coff + x];
-                    if (VC) vv[q] = c_v[coff + x];
+#pragma unroll
+                    for (int u = 0; u < VC; ++u) vv[u][q] = c_v[u][coff + x];
                 } else {
                     kv[q] = st_key[d.soff + (int32_t)x];
-                    if (VC) vv[q] = st_v[d.soff + (int32_t)x];
+#pragma unroll
+                    for (int u = 0; u < VC; ++u) vv[u][q] = st_v[u][d.soff + (int32_t)x];
                 }
             }
             const uint64_t o = d.g + xl;
             if (lo == 0 && hi == (uint32_t)CH) {
                 *(uint32_t *)(rg.key + o) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
-                if (VC) {
+#pragma unroll
+                for (int u = 0; u < VC; ++u) {
                     v2i64 w;
-                    w[0] = vv[0], w[1] = vv[1];
-                    __builtin_nontemporal_store(w, (v2i64 *)(rg.val + o));
+                    w[0] = vv[u][0], w[1] = vv[u][1];
+                    __builtin_nontemporal_store(w, (v2i64 *)(vout[u] + o));
                 }
             } else {
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     if (xl + q < lo || xl + q >= hi) continue;
                     rg.key[o + q] = kv[q];
-                    if (VC) __builtin_nontemporal_store(vv[q], rg.val + o + q);
+#pragma unroll
+                    for (int u = 0; u < VC; ++u) __builtin_nontemporal_store(vv[u][q], vout[u] + o + q);
                 }
             }
         }
@@ -494,11 +511,12 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             }
             if (src >= 0) {
                 c_key[b * CH + kx] = st_key[src];
-                if (VC) c_v[b * CH + kx] = st_v[src];
+#pragma unroll
+                for (int u = 0; u < VC; ++u) c_v[u][b * CH + kx] = st_v[u][src];
             }
         }
     };
-    FastTile<NTERMS, NACOL, NT> ft;
+    FastTile<NTERMS, NACOL, NT, P> ft;
     int64_t tile = blockIdx.x;
     int par = 0;
     uint32_t m_prev = 0;
@@ -532,9 +550,11 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                 else sel &= ~(1u << r);
             }
         }
-        int64_t vcur[R];
+        int64_t vcur[VS][R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) vcur[r] = VC ? ft.a(0, r) : 0;
+        for (int u = 0; u < VS; ++u)
+#pragma unroll
+            for (int r = 0; r < R; ++r) vcur[u][r] = VC ? ft.a(u, r) : 0;
         lds_barrier();  // B1: counts complete, tile t-1 flushed
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged
@@ -572,7 +592,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             if (!((sel >> r) & 1)) continue;
             const uint32_t s = lofs[off[r] >> SB] + rk[r];
             st_key[s] = (uint16_t)(off[r] & ((1u << SB) - 1u));
-            if (VC) st_v[s] = vcur[r];
+#pragma unroll
+            for (int u = 0; u < VC; ++u) st_v[u][s] = vcur[u][r];
         }
         if (tid < F) {
             // plan this slice's whole chunks; the next tile's state (its copies were last read by
@@ -618,7 +639,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         if (dst < cap) {
             const uint64_t o = abase[b] + dst;
             rg.key[o] = c_key[b * CH + kx];
-            if (VC) rg.val[o] = c_v[b * CH + kx];
+#pragma unroll
+            for (int u = 0; u < VC; ++u) vout[u][o] = c_v[u][b * CH + kx];
         } else {
             ovf = true;
         }
@@ -732,8 +754,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             const uint32_t n_r = rg.count[reg];
             const uint16_t *kp = rg.key + reg * rg.cap;
             const int64_t *vp = VC ? rg.val + reg * rg.cap : nullptr;
+            const int64_t *vp2 = NACOL > 1 ? rg.val2 + reg * rg.cap : nullptr;
             uint32_t en[8];
-            int64_t vn[8];
+            int64_t vn[8], vn2[NACOL > 1 ? 8 : 1];
             // item of register j (the masks below use the same map)
             auto item = [&](uint32_t i0, int j) -> uint32_t {
                 return PV ? i0 + (uint32_t)(j >> 1) * 128 + 2 * lane + (uint32_t)(j & 1) : i0 + (uint32_t)j * 64 + lane;
@@ -761,16 +784,21 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                         const uint32_t ii = i < n_r ? i : 0u;
                         en[j] = __builtin_nontemporal_load(kp + ii);
                         vn[j] = VC ? __builtin_nontemporal_load(vp + ii) : 0;
+                        if constexpr (NACOL > 1) vn2[j] = __builtin_nontemporal_load(vp2 + ii);
                     }
                 }
             };
             if (PF && n_r) ld(0);
             for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
                 uint32_t e[8];
-                int64_t v[8];
+                int64_t v[8], v2[NACOL > 1 ? 8 : 1];
                 if (!PF) ld(i0);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) e[j] = en[j], v[j] = vn[j];
+                if constexpr (NACOL > 1) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v2[j] = vn2[j];
+                }
                 if (PF && i0 + 64 * 8 < n_r) ld(i0 + 64 * 8);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
@@ -783,22 +811,27 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
                 for (int a = 0; a < specs.n; ++a) {
                     const AggSpec sp = specs.a[a];
                     uint64_t *st = lst + (int64_t)sp.val_slot * stride - 1;  // indexed by entry = gid + 1
+                    const bool second = NACOL > 1 && in.agg_colslot[a] == 1;  // uniform
+                    auto val = [&](int j) -> int64_t {
+                        if constexpr (NACOL > 1) return second ? v2[j] : v[j];
+                        return v[j];
+                    };
                     switch (sp.kind) {
                         case AK_SUM_F:
 #pragma unroll
                             for (int j = 0; j < 8; ++j)
-                                if (e[j]) atomicAdd((double *)&st[e[j]], as_f64(v[j]));
+                                if (e[j]) atomicAdd((double *)&st[e[j]], as_f64(val(j)));
                             break;
                         case AK_SUM_I:
 #pragma unroll
                             for (int j = 0; j < 8; ++j)
-                                if (e[j]) atomicAdd((unsigned long long *)&st[e[j]], (unsigned long long)v[j]);
+                                if (e[j]) atomicAdd((unsigned long long *)&st[e[j]], (unsigned long long)val(j));
                             break;
                         case AK_MIN:
                         case AK_MAX:
 #pragma unroll
                             for (int j = 0; j < 8; ++j)
-                                if (e[j]) agg_apply<true>(sp.kind, &st[e[j]], agg_input(sp.kind, sp.in_type, v[j]));
+                                if (e[j]) agg_apply<true>(sp.kind, &st[e[j]], agg_input(sp.kind, sp.in_type, val(j)));
                             break;
                         default: break;  // COUNT: the row count slot
                     }
@@ -1720,7 +1753,7 @@ struct SlicePre {
     uint64_t range = 0;
     int grid = 0;
     int64_t n_tiles = 0;
-    DevBuf kbuf, vbuf, cbuf, planbuf;
+    DevBuf kbuf, vbuf, cbuf, planbuf, vbuf2;
     SliceRegions rg{};
     hipEvent_t done = nullptr;
     bool dev_planned = false;  // launched from a plan in device memory, not yet read back (resolve_dev_plan)
@@ -1781,6 +1814,7 @@ struct PendingSlice {
         std::swap(dst->cbuf.p, pre.cbuf.p), std::swap(dst->cbuf.n, pre.cbuf.n), std::swap(dst->cbuf.ctx, pre.cbuf.ctx);
         std::swap(dst->planbuf.p, pre.planbuf.p), std::swap(dst->planbuf.n, pre.planbuf.n),
             std::swap(dst->planbuf.ctx, pre.planbuf.ctx);
+        std::swap(dst->vbuf2.p, pre.vbuf2.p), std::swap(dst->vbuf2.n, pre.vbuf2.n), std::swap(dst->vbuf2.ctx, pre.vbuf2.ctx);
         dst->rg = pre.rg;
         dst->dev_planned = pre.dev_planned;
         std::swap(dst->done, pre.done);
@@ -1798,17 +1832,20 @@ std::vector<uint8_t> PendingSlice::serialise(const qeh_expr *e) {
 
 // regions sized for every row selected with keys uniform over the slices, +25 %
 static bool slice_regions(qeh_ctx *ctx, int64_t n_tiles, int grid, uint64_t F, int nacol, DevBuf *kbuf, DevBuf *vbuf,
-                          DevBuf *cbuf, SliceRegions *rg, hipStream_t stream) {
+                          DevBuf *cbuf, SliceRegions *rg, hipStream_t stream, int64_t tile_rows = kSliceTile,
+                          DevBuf *vbuf2 = nullptr) {
     const int64_t tiles_per_wg = (n_tiles + grid - 1) / grid;
-    uint64_t cap = (uint64_t)((double)tiles_per_wg * kSliceTile / (double)F * 1.25) + 256;
+    uint64_t cap = (uint64_t)((double)tiles_per_wg * tile_rows / (double)F * 1.25) + 256;
     cap = (cap + kSliceChunk - 1) / kSliceChunk * kSliceChunk;
     const uint64_t nreg = (uint64_t)grid * F;
     if (kbuf->alloc(ctx, nreg * cap * 2 + 64) != QEH_OK) return false;
     if (nacol && vbuf->alloc(ctx, nreg * cap * 8 + 64) != QEH_OK) return false;
+    if (nacol > 1 && (!vbuf2 || vbuf2->alloc(ctx, nreg * cap * 8 + 64) != QEH_OK)) return false;
     if (cbuf->alloc(ctx, nreg * 4 + 64) != QEH_OK) return false;
     *rg = SliceRegions{};
     rg->key = kbuf->as<uint16_t>();
     rg->val = nacol ? vbuf->as<int64_t>() : nullptr;
+    rg->val2 = nacol > 1 ? vbuf2->as<int64_t>() : nullptr;
     rg->count = cbuf->as<uint32_t>();
     rg->overflow = rg->count + nreg;
     rg->cap = cap;
@@ -1833,7 +1870,8 @@ static void launch_slice_partition(qeh_ctx *ctx, const FastIn &in, const PredPla
                            pp.terms, kmin, range, n_tiles, rg, t, dplan)
 #define QEH_SA_NA(NTV, NTB)                    \
     if (nacol == 0) { QEH_SA(NTV, 0, NTB); }   \
-    else { QEH_SA(NTV, 1, NTB); }
+    else if (nacol == 1) { QEH_SA(NTV, 1, NTB); } \
+    else { QEH_SA(NTV, 2, NTB); }
 #define QEH_SA_NT(NTB)                         \
     if (nterms == 0) { QEH_SA_NA(0, NTB) }     \
     else if (nterms == 1) { QEH_SA_NA(1, NTB) } \
@@ -1862,8 +1900,11 @@ static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const P
     *launched = false;
     FastIn in;
     int nterms, nacol;
-    if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 1) return QEH_OK;
-    const int64_t n_tiles = n / kSliceTile;
+    if (!fast_cols_eligible(cols, pp, key_col, specs, &in, &nterms, &nacol) || nacol > 2 ||
+        (nacol == 2 && std::getenv("QEH_NO_SLICE_AGG2")))
+        return QEH_OK;
+    const int64_t tile_rows = nacol == 2 ? (int64_t)SliceShape<2>::TILE : (int64_t)kSliceTile;
+    const int64_t n_tiles = n / tile_rows;
     hipStream_t side = n_tiles ? aux_stream(ctx) : nullptr;
     if (!side) return QEH_OK;
     *pi = SlicePlanIn{};
@@ -1874,10 +1915,11 @@ static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const P
     pi->sparse_ok = direct_sparse_allowed() ? 1 : 0;
     const uint64_t tiles_per_wg = (uint64_t)((n_tiles + pi->grid - 1) / pi->grid);
     // every row selected, keys uniform over the slices, +25 % (and per-region slack for the largest F)
-    pi->alloc_items = tiles_per_wg * pi->grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)pi->grid * kSliceMaxF * 288;
+    pi->alloc_items = tiles_per_wg * pi->grid * (uint64_t)tile_rows * 5 / 4 + (uint64_t)pi->grid * kSliceMaxF * 288;
     const uint64_t nreg_max = (uint64_t)pi->grid * kSliceMaxF;
     if (pre->kbuf.alloc(ctx, pi->alloc_items * 2 + 64) != QEH_OK ||
         (nacol && pre->vbuf.alloc(ctx, pi->alloc_items * 8 + 64) != QEH_OK) ||
+        (nacol > 1 && pre->vbuf2.alloc(ctx, pi->alloc_items * 8 + 64) != QEH_OK) ||
         pre->cbuf.alloc(ctx, nreg_max * 4 + 64) != QEH_OK || pre->planbuf.alloc(ctx, sizeof(SlicePlan)) != QEH_OK)
         return QEH_OK;
     hipEvent_t ready = nullptr;
@@ -1891,6 +1933,7 @@ static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const P
     rg = SliceRegions{};
     rg.key = pre->kbuf.as<uint16_t>();
     rg.val = nacol ? pre->vbuf.as<int64_t>() : nullptr;
+    rg.val2 = nacol > 1 ? pre->vbuf2.as<int64_t>() : nullptr;
     rg.count = pre->cbuf.as<uint32_t>();
     rg.overflow = rg.count + nreg_max;
     QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
@@ -1911,13 +1954,19 @@ static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const P
 
 // A device-planned launch whose plan is `pl`: adopted (launched, shape set) when it planned the slice
 // path; else phase A returned at once and its worst-case regions are released now.
-static void settle_dev_plan(SlicePre *pre, const SlicePlan &pl) {
+static void settle_dev_plan(qeh_ctx *ctx, SlicePre *pre, const SlicePlan &pl) {
     pre->dev_planned = false;
     if (!pl.ok) {
+        // the launch returned at once: its timing record is not a phase A
+        for (auto it = ctx->timing_pending.rbegin(); it != ctx->timing_pending.rend(); ++it)
+            if (it->name == "slice_partition") {
+                it->name = "slice_partition_declined";
+                break;
+            }
         (void)hipEventSynchronize(pre->done);
         (void)hipEventDestroy(pre->done);
         pre->done = nullptr;
-        pre->kbuf.reset(), pre->vbuf.reset(), pre->cbuf.reset(), pre->planbuf.reset();
+        pre->kbuf.reset(), pre->vbuf.reset(), pre->cbuf.reset(), pre->planbuf.reset(), pre->vbuf2.reset();
         return;
     }
     pre->rg.F = pl.F;
@@ -1932,7 +1981,7 @@ static int resolve_dev_plan(qeh_ctx *ctx, SlicePre *pre, BuildRanges *br) {
     SlicePlan pl{};
     QEH_TRY(read_small(ctx, &pl, pre->planbuf.p, sizeof pl));
     for (int q = 0; q < 2; ++q) br->mn[q] = pl.src[3 * q], br->mx[q] = pl.src[3 * q + 1], br->cnt[q] = pl.src[3 * q + 2];
-    settle_dev_plan(pre, pl);
+    settle_dev_plan(ctx, pre, pl);
     return QEH_OK;
 }
 
@@ -1947,7 +1996,7 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
     if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_OVERLAP") || slice_chunk_tiles() > 0) return QEH_OK;
     if (cols.c[key_col].dtype != QEH_DT_INT64 || build_key.dtype != QEH_DT_INT64) return QEH_OK;
     if (group_key.dtype != QEH_DT_INT64 && group_key.dtype != QEH_DT_INT32) return QEH_OK;
-    if (n / kSliceTile == 0) return QEH_OK;
+    if (n / SliceShape<2>::TILE == 0) return QEH_OK;
     const qeh_column both[2] = {build_key, group_key};
     if (std::getenv("QEH_HOST_PLAN")) {  // the ranges read back before phase A is launched
         BuildRanges br;
@@ -1967,7 +2016,7 @@ static int slice_prelaunch(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pr
         &launched));
     BuildRanges br;  // read while phase A runs (and memoised for the build)
     QEH_TRY(columns_minmax_collect(ctx, both, 2, mm.as<MinMax>(), br.mn, br.mx, br.cnt));
-    if (launched) settle_dev_plan(pre, plan_slices(pi, br.mn[0], br.mx[0], br.cnt[0], br.mn[1], br.mx[1], br.cnt[1]));
+    if (launched) settle_dev_plan(ctx, pre, plan_slices(pi, br.mn[0], br.mx[0], br.cnt[0], br.mn[1], br.mx[1], br.cnt[1]));
     return QEH_OK;
 }
 
@@ -2073,7 +2122,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     int nterms, nacol;
     if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol)) return 0;
     const HashTable &t = src.jt;
-    if (t.kind != TK_DIRECT || !t.payload16 || nacol > 1) return 0;
+    if (t.kind != TK_DIRECT || !t.payload16 || nacol > 2 || (nacol == 2 && std::getenv("QEH_NO_SLICE_AGG2"))) return 0;
     if ((int64_t)specs.n_slots * G > kSliceStateWords) return 0;
     const uint64_t F = (t.range + kSliceKeys - 1) >> kSliceBits;
     if (F == 0 || F > (uint64_t)kSliceMaxF) return 0;
@@ -2081,12 +2130,14 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     uint64_t min_bytes = 6ull << 20;
     if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
     if (table_bytes(t) < min_bytes) return 0;
-    const int64_t n_tiles = n / kSliceTile;
+    // two aggregate columns: half tiles (SliceShape<2>)
+    const int64_t tile_rows = nacol == 2 ? (int64_t)SliceShape<2>::TILE : (int64_t)kSliceTile;
+    const int64_t n_tiles = n / tile_rows;
     if (n_tiles == 0) return 0;
     int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
     bool tail_done = false;
     hipEvent_t tail_ev = nullptr;
-    DevBuf kbuf, vbuf, cbuf;
+    DevBuf kbuf, vbuf, cbuf, vbuf2;
     SliceRegions rg{};
     if (pre && pre->launched && pre->kmin == t.kmin && pre->range == t.range && pre->n_tiles == n_tiles) {
         grid = pre->grid;  // phase A's workgroups = regions per slice
@@ -2098,8 +2149,8 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         // Phase B waits for phase A only; the tail runs on the second queue beside phase B (both
         // merge into the global states with atomics) and the main queue waits for it after phase B.
         if (std::getenv("QEH_TAIL_BESIDE")) {
-            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
-        } else if (n > n_tiles * kSliceTile) {
+            launch_tail(ctx, cols, n, n_tiles * tile_rows, pp, src, specs, G, states, err, lds_bytes);
+        } else if (n > n_tiles * tile_rows) {
             hipStream_t side = aux_stream(ctx), main = ctx->stream;
             hipEvent_t built;
             if (hipEventCreateWithFlags(&built, hipEventDisableTiming) != hipSuccess) return 0;
@@ -2112,7 +2163,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
             (void)hipStreamWaitEvent(side, built, 0);
             (void)hipEventDestroy(built);
             ctx->stream = side;
-            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+            launch_tail(ctx, cols, n, n_tiles * tile_rows, pp, src, specs, G, states, err, lds_bytes);
             ctx->stream = main;
             (void)hipEventRecord(tail_ev, side);
         }
@@ -2120,7 +2171,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         if (hipStreamWaitEvent(ctx->stream, pre->done, 0) != hipSuccess) return 0;
     } else {
         const int64_t chunk = slice_chunk_tiles();
-        if (chunk > 0 && chunk < n_tiles) {
+        if (chunk > 0 && chunk < n_tiles && nacol < 2) {
             // chunked pipeline: phase A and phase B alternate over chunks of `chunk` tiles; each
             // chunk's exchange (plain stores) is read back by its phase B from the Infinity Cache
             const int gridc = (int)std::min<int64_t>(ctx->props.multiProcessorCount, chunk);
@@ -2139,7 +2190,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
                 launch_slice_probe(ctx, rg, g, t, ic, specs, G, states, nacol);
             }
             if (hipGetLastError() != hipSuccess) return 0;
-            launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+            launch_tail(ctx, cols, n, n_tiles * tile_rows, pp, src, specs, G, states, err, lds_bytes);
             uint32_t of = 0;
             if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
             if (of) {
@@ -2149,7 +2200,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
             }
             return 1;
         }
-        if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
+        if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream, tile_rows, &vbuf2)) return 0;
         launch_slice_partition(ctx, in, pp, nterms, nacol, t.kmin, t.range, n_tiles, grid, rg, ctx->stream);
     }
     {
@@ -2158,15 +2209,25 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         int splits = 0;
         if (const char *e = std::getenv("QEH_SLICE_SPLITS")) splits = std::atoi(e);
         const bool pf = slice_probe_prefetch();
+        static const bool pv = std::getenv("QEH_SLICE_B_PAIRS") && std::atoi(std::getenv("QEH_SLICE_B_PAIRS")) == 1;
 #define QEH_SB(NAV, PFV)                                                                                              \
-    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, splits, \
-                       t, in, specs, G, states)
+    do {                                                                                                              \
+        if (pv)                                                                                                       \
+            hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, \
+                               grid, splits, t, in, specs, G, states);                                          \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, \
+                               splits, t, in, specs, G, states);                                                \
+    } while (0)
         if (nacol == 0) {
             if (pf) QEH_SB(0, true);
             else QEH_SB(0, false);
-        } else {
+        } else if (nacol == 1) {
             if (pf) QEH_SB(1, true);
             else QEH_SB(1, false);
+        } else {
+            if (pf) QEH_SB(2, true);
+            else QEH_SB(2, false);
         }
 #undef QEH_SB
     }
@@ -2175,7 +2236,7 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         (void)hipEventDestroy(tail_ev);
     }
     if (hipGetLastError() != hipSuccess) return 0;
-    if (!tail_done) launch_tail(ctx, cols, n, n_tiles * kSliceTile, pp, src, specs, G, states, err, lds_bytes);
+    if (!tail_done) launch_tail(ctx, cols, n, n_tiles * tile_rows, pp, src, specs, G, states, err, lds_bytes);
     if (ovf_copy) {
         if (hipMemcpyAsync(ovf_copy, rg.overflow, 4, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) return -1;
         return 2;

@@ -173,6 +173,30 @@ def test_slice_partitioned_probe(ctx, monkeypatch, n_fact, n_dim, groups, key0, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_fact,n_dim,key0", [(1_000_003, 300_001, -12_345), (600_000, 70_000, 0)])
+def test_slice_two_aggregate_columns(ctx, monkeypatch, n_fact, n_dim, key0):
+    """Two aggregate input columns on the LDS-slice pipeline (18-B items: half tiles, 16-item
+    chunks): SUM / MIN / MAX over a float and an integer column, COUNT; misses, ragged tail."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    rng = np.random.default_rng(17)
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 512)
+    k = k + key0
+    dk = dk + key0
+    k[::89] = key0 - 1 - k[::89]
+    w = rng.integers(-(1 << 40), 1 << 40, n_fact)
+    probe = [(x, None), (k, None), (v, None), (w, None)]
+    aggs = [(AF.Sum, 2), (AF.Sum, 3), (AF.Count, 2), (AF.Min, 3), (AF.Max, 2)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+        assert ctx.kernel_time("slice_probe")[1] == 1  # the slice pipeline ran (not the single pass)
+    finally:
+        ctx.timing(False)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
 def test_slice_probe_metric_table_default_threshold(ctx):
     """The BASELINE shape at 1/50 scale: 20M fact rows x 10M-key dim (20 MB u16
     table), slice path chosen by default."""
