@@ -138,7 +138,8 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # QEH_LIB_PATH: an experiment build of the library in place of the in-tree one (A/B runs)
+    p = path or os.environ.get("QEH_LIB_PATH") or LIB_PATH
     # One HIP runtime per process: torch's wheel bundles its own libamdhip64
     # (same soname, libamdhip64.so.7).  If libqeh.so loaded /opt/rocm's copy
     # first, a later `import torch` would load a second runtime that finds no
