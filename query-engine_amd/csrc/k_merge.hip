@@ -192,6 +192,21 @@ extern "C" int qeh_merge_sorted(qeh_ctx *ctx, const qeh_column *parts, int n_par
         *out_rows = n;
         return QEH_OK;
     }
+    if (n_keys == 1 && n_cols == 2) {
+        // one key and one 8-byte payload: the payload rides through the radix passes (no gathers)
+        const int kj = key_idx[0], vj = 1 - key_idx[0];
+        qeh_column ok{}, ov{};
+        const int ps = sort_pairs_payload(ctx, cat[kj], cat[vj], ascending ? ascending[0] != 0 : true,
+                                          nulls_first ? nulls_first[0] != 0 : true, &ok, &ov);
+        if (ps != kPayloadSortNotEligible) {
+            release_cat();
+            QEH_TRY(ps);
+            out[kj] = ok;
+            out[vj] = ov;
+            *out_rows = n;
+            return QEH_OK;
+        }
+    }
     std::vector<qeh_column> keys(n_keys);
     for (int k = 0; k < n_keys; ++k) keys[k] = cat[key_idx[k]];
     qeh_column perm{};

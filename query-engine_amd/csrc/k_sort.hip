@@ -247,16 +247,17 @@ __device__ __forceinline__ void lds_barrier() {
 
 // AT: tile ranks by LDS atomics (ds_add_rtn serves one instruction's lanes in lane order, so the
 // rank is stable: tools/ubench/lds_order_ubench.hip), else by ballot peers (QEH_RS_BALLOT=1, A/B).
-template <typename KeyT, bool AT = true>
-__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
+// ValT: the carried value -- a u32 row id, or (qeh_merge_sorted's payload sort) an 8-B payload.
+template <typename KeyT, bool AT = true, typename ValT = uint32_t>
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const ValT *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                            int nblocks, KeyT *__restrict__ keys_out,
-                                                           uint32_t *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
+                                                           ValT *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
                                                            int nshift) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
     __shared__ KeyT s_keys[kRsSTile];
-    __shared__ uint32_t s_vals[kRsSTile];
+    __shared__ ValT s_vals[kRsSTile];
     __shared__ uint32_t wcnt[W][kRadix];  // per-wave digit counts, then per-wave start inside the digit
     __shared__ uint32_t loc[kRadix];      // tile-local start of each digit
     __shared__ uint32_t tot_s[kRadix];
@@ -266,11 +267,11 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
     KeyT k[kRsIpt];
-    uint32_t v[kRsIpt];
+    ValT v[kRsIpt];
     // loads are unconditional (indices clamped into [lo, hi)): no branches around
     // them, so the compiler's wait counts stay exact and the prefetch really
     // stays in flight across the ranking of the current tile
-    auto load_tile = [&](int64_t c0, KeyT *kk, uint32_t *vv) {
+    auto load_tile = [&](int64_t c0, KeyT *kk, ValT *vv) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     for (int64_t c0 = lo; c0 < hi; c0 += kRsSTile) {
         for (int i = t; i < W * kRadix; i += kRsThreads) (&wcnt[0][0])[i] = 0;
         KeyT kn[kRsIpt];
-        uint32_t vn[kRsIpt];
+        ValT vn[kRsIpt];
         const int64_t c1 = c0 + kRsSTile;
         load_tile(c1 < hi ? c1 : c0, kn, vn);  // in flight while this tile is ranked and written
         lds_barrier();
@@ -1346,6 +1347,122 @@ extern "C" int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys
     QEH_TRY(alloc_column(ctx, QEH_DT_UINT32, n, false, out_perm));
     if (n > 0) QEH_HIP(hipMemcpyAsync(out_perm->values, rs.v[rs.cur].p, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     QEH_HIP(hipStreamSynchronize(ctx->stream));
+    return QEH_OK;
+}
+
+// ---- payload-carrying sort (qeh_merge_sorted of one Int64 / Int32 key and one 8-byte column) ----
+// The key is encoded as in sort_by_column (asc: x - mn, desc: mx - x; NULL = 0 below every value
+// code when NULLs go first, or above them when last) and sorted with the payload itself as the carried
+// value, so no permutation is gathered afterwards: the sorted key column is decoded from the sorted
+// codes, and the last pass writes the payload straight into the output column.
+__global__ void k_encode_kv(ColRef c, int64_t n, int64_t mn, int64_t mx, int asc, uint64_t bias, uint64_t null_code,
+                            uint64_t *__restrict__ keys) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t k = null_code;
+        if (col_valid(c, i)) {
+            const int64_t x = load_i64(c, i);
+            k = asc ? (uint64_t)x - (uint64_t)mn + bias : (uint64_t)mx - (uint64_t)x + bias;
+        }
+        keys[i] = k;
+    }
+}
+
+// codes -> key values (Int64 / Int32) and the validity bitmap: one row per lane (coalesced), each
+// wave's 64 validity bits from one ballot (blockDim and the grid stride are multiples of 64)
+__global__ void k_decode_keys(const uint64_t *__restrict__ keys, int64_t n, int64_t mn, int64_t mx, int asc, uint64_t bias,
+                              uint64_t null_code, int dt, void *__restrict__ out, uint64_t *__restrict__ valid) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n; i += stride) {
+        const bool in = i < n;
+        const uint64_t k = in ? keys[i] : null_code;
+        const bool ok = in && k != null_code;
+        const int64_t x = ok ? (asc ? (int64_t)(k - bias + (uint64_t)mn) : (int64_t)((uint64_t)mx - (k - bias))) : 0;
+        if (in) {
+            if (dt == QEH_DT_INT32) ((int32_t *)out)[i] = (int32_t)x;
+            else ((int64_t *)out)[i] = x;
+        }
+        const uint64_t m = __ballot(ok);
+        if (valid && lane == 0) valid[i >> 6] = m;
+    }
+}
+
+int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_column &val, bool asc, bool nulls_first,
+                            qeh_column *out_key, qeh_column *out_val) {
+    const int64_t n = key.length;
+    if (std::getenv("QEH_NO_PAYLOAD_SORT") || n <= 1 || n >= ((int64_t)1 << 32) || val.length != n) return kPayloadSortNotEligible;
+    if (key.dtype != QEH_DT_INT64 && key.dtype != QEH_DT_INT32) return kPayloadSortNotEligible;
+    if ((val.dtype != QEH_DT_INT64 && val.dtype != QEH_DT_FLOAT64) || (val.validity && val.null_count != 0))
+        return kPayloadSortNotEligible;
+    const ColRef kc = make_colref(key);
+    DevBuf st;
+    QEH_TRY(st.alloc(ctx, sizeof(KeyStats)));
+    KeyStats ks{};
+    {
+        KernelTimer kt(ctx, "sort_encode");
+        hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, st.as<KeyStats>());
+        hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kc, nullptr, n,
+                           st.as<KeyStats>());
+    }
+    QEH_TRY(read_small(ctx, &ks, st.p, sizeof ks));
+    const bool any_valid = ks.mn <= ks.mx;
+    const int64_t mn = any_valid ? ks.mn : 0, mx = any_valid ? ks.mx : 0;
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn;  // value codes 0 .. range (+ bias)
+    const bool nullable = key.validity && key.null_count != 0;
+    const uint64_t bias = nullable && nulls_first ? 1 : 0;
+    const uint64_t null_code = nullable && nulls_first ? 0 : range + 1;  // (no NULLs: never produced)
+    int bits = 1;
+    while (bits < 64 && ((range + 1) >> bits) != 0) ++bits;
+    const int npass = (bits + kRadixBits - 1) / kRadixBits;
+    // ping-pong buffers; the payload buffer the last pass writes is the output column's values
+    QEH_TRY(alloc_column(ctx, val.dtype, n, false, out_val));
+    DevBuf kb[2], vtmp, hist, offs;
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)ctx->props.multiProcessorCount);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    int s = QEH_OK;
+    if (kb[0].alloc(ctx, n * 8) || kb[1].alloc(ctx, n * 8) || vtmp.alloc(ctx, n * 8) ||
+        hist.alloc(ctx, (size_t)kRadix * nblocks * 4) || offs.alloc(ctx, (size_t)kRadix * nblocks * 8))
+        s = fail(QEH_E_OOM, "payload sort: out of device memory");
+    // pass p reads buffer p % 2 and writes (p + 1) % 2; the last pass writes the output column
+    uint64_t *vb[2];
+    vb[npass % 2] = (uint64_t *)out_val->values;
+    vb[(npass + 1) % 2] = vtmp.as<uint64_t>();
+    if (s == QEH_OK) {
+        KernelTimer kt(ctx, "sort_encode");
+        hipLaunchKernelGGL(k_encode_kv, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream, kc, n, mn, mx,
+                           asc ? 1 : 0, bias, null_code, kb[0].as<uint64_t>());
+        const char *vsrc = (const char *)val.values + (size_t)val.offset * 8;
+        if (hipMemcpyAsync(vb[0], vsrc, (size_t)n * 8, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+            s = fail(QEH_E_HIP, "payload sort: copy failed");
+    }
+    for (int p = 0; p < npass && s == QEH_OK; ++p) {
+        KernelTimer kt(ctx, "radix_pass");
+        const int c = p & 1, shift = p * kRadixBits;
+        hipLaunchKernelGGL(k_rs_hist<uint64_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), n, seg,
+                           shift, hist.as<uint32_t>(), nblocks);
+        s = exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr);
+        if (s != QEH_OK) break;
+        hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
+                           kb[c].as<uint64_t>(), vb[c], n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
+                           vb[1 - c], nullptr, 0);
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: pass launch failed");
+    }
+    if (s == QEH_OK) s = alloc_column(ctx, key.dtype, n, nullable, out_key);
+    if (s == QEH_OK) {
+        KernelTimer kt(ctx, "sort_encode");
+        hipLaunchKernelGGL(k_decode_keys, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
+                           kb[npass % 2].as<uint64_t>(), n, mn, mx, asc ? 1 : 0, bias, null_code, key.dtype, out_key->values,
+                           nullable ? (uint64_t *)out_key->validity : nullptr);
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: decode launch failed");
+        if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "payload sort failed");
+        if (s != QEH_OK) qeh_column_release(ctx, out_key);
+    }
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out_val);
+        return s;
+    }
+    out_key->null_count = nullable ? -1 : 0;
+    out_val->null_count = 0;
     return QEH_OK;
 }
 

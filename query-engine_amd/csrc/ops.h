@@ -69,6 +69,12 @@ struct MinMax {
 int columns_minmax_launch(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *dev_out);
 int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const MinMax *dev_out, int64_t *mn, int64_t *mx,
                            int64_t *valid);
+// Stable sort of (one Int64 / Int32 key, one non-null 8-byte payload) carrying the payload through
+// the radix passes (no gather): the sorted key and payload columns.  kPayloadSortNotEligible when
+// the shapes do not fit (nothing allocated).
+constexpr int kPayloadSortNotEligible = -3;
+int sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_column &val, bool asc, bool nulls_first,
+                       qeh_column *out_key, qeh_column *out_val);
 // min / max / valid count of an integer column (one synchronous read).
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid);
 // min / max / valid count of several integer columns, one synchronous read.
