@@ -803,6 +803,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     e[j] = (item(i0, j) < n_r) ? (IDENT ? e[j] + 1u : (uint32_t)tslice[e[j]]) : 0u;
+
                 // aggregate kinds are uniform: switch once per aggregate, then
                 // issue the 8 items' LDS atomics back to back
 #pragma unroll
