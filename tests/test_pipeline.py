@@ -477,3 +477,54 @@ def test_inner_join_full_size_properties(ctx):
     lo_in = view(fv, abi.DT_INT64) & 0xFFFF
     lo_out = view(p[0], abi.DT_INT64) & 0xFFFF
     assert int((a_out * lo_out).sum()) == int((a_in * lo_in).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["table_lanes", "plain_call", "other_probe", "bitmap_flag", "two_rank_rows"])
+def test_prelaunch_from_device_stats(ctx, case):
+    """qeh_join_filter_aggregate_prelaunch_stats: phase A planned on the device from gathered
+    qeh_broadcast_stats rows (no host read before it starts).  Adopted by the table-form lanes call and
+    by a plain fused call whose build has exactly the planned ranges (one phase A in the kernel
+    timers); discarded for other probe columns; declined when a row flags a bitmap (the plan kernel
+    returns at once and is not counted as a phase A).  Results equal the oracle's in every case."""
+    import torch
+    n_fact, n_dim = 4_000_000, 4_000_000
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 1024)
+    probe = [ctx.upload(x), ctx.upload(k), ctx.upload(v)]
+    bkey, bg = ctx.upload(dk), ctx.upload(dg)
+    rows = torch.zeros(2, 7, dtype=torch.int64, device="cuda")
+    if case == "two_rank_rows":  # two shards' rows: the plan reduces them to the job-wide ranges
+        h = n_dim // 2
+        ctx.broadcast_stats(ctx.upload(dk[:h]), ctx.upload(dg[:h]), [0, 0], rows[0].data_ptr())
+        ctx.broadcast_stats(ctx.upload(dk[h:]), ctx.upload(dg[h:]), [0, 0], rows[1].data_ptr())
+        world = 2
+    else:
+        ctx.broadcast_stats(bkey, bg, [1 if case == "bitmap_flag" else 0, 0], rows[0].data_ptr())
+        world = 1
+    torch.cuda.synchronize()
+    pre_probe = [ctx.upload(x), ctx.upload(k), ctx.upload(v)] if case == "other_probe" else probe
+    wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(dk),
+                                          [ob.HostCol(dg)], AGGS)
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        ctx.join_filter_aggregate_prelaunch_stats(pre_probe, 1, PRED, AGGS, rows.data_ptr(), world, 7)
+        if case == "table_lanes":
+            kmin, R = int(dk.min()), int(dk.max() - dk.min() + 1)
+            gmin, G = int(dg.min()), int(dg.max() - dg.min() + 1)
+            table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            ctx.direct_group_table_insert(bkey, bg, kmin, R, gmin, table.data_ptr())
+            lanes = torch.empty(3 * G, dtype=torch.float64, device="cuda")
+            ctx.join_filter_aggregate_table_lanes(probe, 1, PRED, table.data_ptr(), kmin, R, G, AGGS, lanes.data_ptr())
+            ok, ov, g = ctx.dense_states_take(lanes.data_ptr(), 2, gmin, G, 1, 0, abi.DT_INT64,
+                                              [abi.DT_FLOAT64, abi.DT_INT64])
+            gk, ga = [ok], ov
+        else:
+            gk, ga, g = ctx.join_filter_aggregate(probe, 1, PRED, bkey, [bg], AGGS)
+        launches = ctx.kernel_time("slice_partition")[1]
+    finally:
+        ctx.timing(False)
+    assert launches == (2 if case == "other_probe" else 1)
+    assert g == wg
+    assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
