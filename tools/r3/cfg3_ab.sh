@@ -4,7 +4,7 @@ set -o pipefail
 R="$GRAFT_REPO_ROOT"; O=$R/gpurun_out/r3/${1:-cfg3ab}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 i=0
-for lib in "" "$R/query-engine_amd/libqeh_old.so"; do
+for lib in "" "$R/query-engine_amd/${OLD:-libqeh_old.so}"; do
   i=$((i+1))
   QEH_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt$i -o kt -- \
       python3 $R/tools/bench_configs.py --only ${CFG:-cfg3} > $O/kt$i.log 2>&1 || { tail -5 $O/kt$i.log; exit 1; }
