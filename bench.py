@@ -180,6 +180,17 @@ def main():
     # query at N = 1 is the local operator, at N > 1 the broadcast join over RCCL
     # QEH_BENCH_FORCE_DIST=1: the N > 1 plan at N = 1 (measures its fixed per-step overhead)
     dist = world > 1 or cfg4 or bool(os.environ.get("QEH_BENCH_FORCE_DIST"))
+    # QEH_BENCH_RANK_OF="r/W": rehearse rank r's share of an N = W metric run on one GPU -- its fact
+    # rows and its dim shard through the distributed plan at world size 1 (the RCCL table all-reduce
+    # has one member, so its xGMI time is not in the step); checked against the local operator over
+    # the same dim shard instead of the full-join properties
+    rehearse = os.environ.get("QEH_BENCH_RANK_OF")
+    if rehearse:
+        rr, ww = (int(q) for q in rehearse.split("/"))
+        assert world == 1 and not cfg4 and 0 <= rr < ww, "QEH_BENCH_RANK_OF: one process, metric workload, r < W"
+        dist = True
+        # the rank's 1/W of the dim spans the whole key range: let the table form take it, as the job's W shards would
+        os.environ.setdefault("QEH_TABLE_MAX_SPARSITY", str(4 * ww))
     import torch
     if dist:
         import torch.distributed as tdist
@@ -207,6 +218,9 @@ def main():
     if cfg4:  # weak scaling: `rows` fact rows on every GPU
         row0, n = rank * args.rows, args.rows
         total_rows = args.rows * world
+    elif rehearse:
+        row0, n = shard(args.rows, ww, rr)
+        total_rows = n
     else:     # strong scaling: `rows` fact rows in total, split across the GPUs
         row0, n = shard(args.rows, world, rank)
         total_rows = args.rows
@@ -215,7 +229,7 @@ def main():
     v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n, row0=row0)
     # the dimension: whole on one GPU; sharded across ranks for N > 1 / config 4 (each rank
     # holds rows [d0, d0 + dn) of the same table) and moved by RCCL inside the step
-    d0, dn = shard(nd, world, rank) if dist else (0, nd)
+    d0, dn = shard(nd, ww, rr) if rehearse else shard(nd, world, rank) if dist else (0, nd)
     dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, dn, nd, row0=d0)
     dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, dn, args.groups, row0=d0)
     ctx.sync()
@@ -270,9 +284,15 @@ def main():
     counts, _ = ga[1].to_numpy()
     sums, _ = ga[0].to_numpy()
     counted, groups, vsum = int(counts.sum()), int(g), float(sums.sum())
-    fx, want_rows = ctx.filter([x, v], pred, out_idx=[1])
-    _, want_sum_cols, _ = ctx.hash_aggregate([], fx, [(AF.Sum, 0)])
-    want_sum = float(want_sum_cols[0].to_numpy()[0][0]) if want_rows else 0.0
+    if rehearse:  # the local operator over the same fact rows and dim shard
+        _, lga, lg = ctx.join_filter_aggregate([x, k, v], 1, pred, dk, [dg], aggs)
+        want_rows, want_sum = int(lga[1].to_numpy()[0].sum()), float(lga[0].to_numpy()[0].sum())
+        assert int(lg) == groups, f"{groups} groups, the local operator {int(lg)}"
+        args.groups = groups  # every group of the shard, checked against the local operator above
+    else:
+        fx, want_rows = ctx.filter([x, v], pred, out_idx=[1])
+        _, want_sum_cols, _ = ctx.hash_aggregate([], fx, [(AF.Sum, 0)])
+        want_sum = float(want_sum_cols[0].to_numpy()[0][0]) if want_rows else 0.0
     if dist:
         t = torch.tensor([counted, groups, want_rows], device=cdev, dtype=torch.int64)
         tdist.all_reduce(t)
@@ -322,7 +342,7 @@ def main():
             traffic = None
 
     if rank == 0:
-        cpu = cpu_baseline(args) if world == 1 and not cfg4 else None  # the CPU baseline is an N=1 figure
+        cpu = cpu_baseline(args) if world == 1 and not cfg4 and not rehearse else None  # an N=1 figure
         if cfg4:
             workload = ("BASELINE config 4: hash-partitioned join + aggregate (filter f.x > 49, both sides "
                         "hash-partitioned by the join key over RCCL all-to-all, local fused join + partial "
@@ -335,6 +355,10 @@ def main():
                    + (f", dim sharded x{world}: shard tables summed by RCCL all-reduce inside the step (broadcast join, "
                       "table form), partial states merged by a dense RCCL all-reduce, final aggregate per owner rank"
                       if dist else ""))
+        if rehearse:
+            par = (f"rehearsal of rank {rr} of {ww} at world size 1: fact rows [{row0}, {row0 + n}), dim rows "
+                   f"[{d0}, {d0 + dn}) through the broadcast join's table form (the RCCL all-reduce of the shard "
+                   "tables has one member: its xGMI time is not in the step)")
         line = {
             "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
             "value": value,
@@ -377,8 +401,10 @@ def main():
             "dist_final": getattr(dx, "last_final", None) if dx is not None else None,
             "result_groups": groups,
             "result_rows_counted": counted,
-            "result_check": "Σ COUNT == device filter count, Σ SUM(v) == device filtered Σ v (1e-6), groups == "
-                            f"{args.groups}: passed",
+            "result_check": ("Σ COUNT, Σ SUM(v) (1e-6) and groups == the local operator over the same dim shard: passed"
+                             if rehearse else
+                             "Σ COUNT == device filter count, Σ SUM(v) == device filtered Σ v (1e-6), groups == "
+                             f"{args.groups}: passed"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -627,7 +627,10 @@ class DistributedExecutor:
         kmin, kmax, _ = st["krange"]
         gmin, gmax, _ = st["grange"]
         R, G = kmax - kmin + 1, gmax - gmin + 1
-        if R > 4 * total + 1024 or R >= (1 << 31) or G > 4096 or self.world * (G + 1) >= (1 << 16):
+        # QEH_TABLE_MAX_SPARSITY: key range per build row allowed (bench.py's one-rank rehearsal holds 1/N
+        # of the rows over the whole range)
+        sparsity = float(os.environ.get("QEH_TABLE_MAX_SPARSITY", "4"))
+        if R > sparsity * total + 1024 or R >= (1 << 31) or G > 4096 or self.world * (G + 1) >= (1 << 16):
             return None
         if not st["prelaunched"]:
             self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"],
