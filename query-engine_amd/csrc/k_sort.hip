@@ -245,15 +245,25 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// The payload sort's last pass writes the decoded key column itself (DEC): code -> Int64 / Int32 value
+// as k_encode_kv's inverse, and one valid byte per row for the bitmap packed afterwards.
+struct RsDecode {
+    int64_t mn, mx;
+    uint64_t bias, null_code;
+    int32_t asc, dt;
+    void *out;
+    uint8_t *validb;  // nullable key: 1 = value, 0 = NULL (else nullptr)
+};
+
 // AT: tile ranks by LDS atomics (ds_add_rtn serves one instruction's lanes in lane order, so the
 // rank is stable: tools/ubench/lds_order_ubench.hip), else by ballot peers (QEH_RS_BALLOT=1, A/B).
 // ValT: the carried value -- a u32 row id, or (qeh_merge_sorted's payload sort) an 8-B payload.
-template <typename KeyT, bool AT = true, typename ValT = uint32_t>
+template <typename KeyT, bool AT = true, typename ValT = uint32_t, bool DEC = false>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const ValT *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                            int nblocks, KeyT *__restrict__ keys_out,
                                                            ValT *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
-                                                           int nshift) {
+                                                           int nshift, RsDecode dec) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
     __shared__ KeyT s_keys[kRsSTile];
@@ -342,7 +352,18 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
             const KeyT key = s_keys[p];
             const uint32_t dg = (uint32_t)((key >> shift) & (kRadix - 1));
             const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
-            keys_out[pos] = key;
+            if constexpr (DEC) {
+                const uint64_t c = (uint64_t)key;
+                const bool ok = c != dec.null_code;
+                const int64_t x = ok ? (dec.asc ? (int64_t)(c - dec.bias + (uint64_t)dec.mn)
+                                               : (int64_t)((uint64_t)dec.mx - (c - dec.bias)))
+                                     : 0;
+                if (dec.dt == QEH_DT_INT32) ((int32_t *)dec.out)[pos] = (int32_t)x;
+                else ((int64_t *)dec.out)[pos] = x;
+                if (dec.validb) dec.validb[pos] = ok ? 1 : 0;
+            } else {
+                keys_out[pos] = key;
+            }
             vals_out[pos] = s_vals[p];
             if (nd_out) nd_out[pos] = (uint8_t)(key >> nshift);  // the next pass's digit (its histogram input)
         }
@@ -697,7 +718,7 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
         auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
         hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(),
                            nblocks, rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr,
-                           shift + kRadixBits);
+                           shift + kRadixBits, RsDecode{});
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
@@ -722,7 +743,7 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
     auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
     hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks,
-                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0);
+                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{});
     QEH_HIP(hipGetLastError());
     rs.cur = 1 - c;
     return QEH_OK;
@@ -1367,23 +1388,30 @@ __global__ void k_encode_kv(ColRef c, int64_t n, int64_t mn, int64_t mx, int asc
     }
 }
 
-// codes -> key values (Int64 / Int32) and the validity bitmap: one row per lane (coalesced), each
-// wave's 64 validity bits from one ballot (blockDim and the grid stride are multiples of 64)
-__global__ void k_decode_keys(const uint64_t *__restrict__ keys, int64_t n, int64_t mn, int64_t mx, int asc, uint64_t bias,
-                              uint64_t null_code, int dt, void *__restrict__ out, uint64_t *__restrict__ valid) {
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n; i += stride) {
-        const bool in = i < n;
-        const uint64_t k = in ? keys[i] : null_code;
-        const bool ok = in && k != null_code;
-        const int64_t x = ok ? (asc ? (int64_t)(k - bias + (uint64_t)mn) : (int64_t)((uint64_t)mx - (k - bias))) : 0;
-        if (in) {
-            if (dt == QEH_DT_INT32) ((int32_t *)out)[i] = (int32_t)x;
-            else ((int64_t *)out)[i] = x;
+// valid bytes (the last pass's, one per row, each 0 or 1) -> the key's validity bitmap: one 64-row word
+// per thread from four 16-B loads (bit i of a dword's 4 flags = bit 8 i of the dword)
+__global__ void k_pack_valid(const uint8_t *__restrict__ vb, int64_t n, uint64_t *__restrict__ valid) {
+    typedef unsigned int v4u32p __attribute__((ext_vector_type(4)));
+    const int64_t nw = (n + 63) >> 6;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r0 = w << 6;
+        uint64_t m = 0;
+        if (r0 + 64 <= n) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const v4u32p x = __builtin_nontemporal_load((const v4u32p *)(vb + r0) + q);
+                const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t y = d[t];
+                    const uint32_t b4 = (y & 1u) | ((y >> 7) & 2u) | ((y >> 14) & 4u) | ((y >> 21) & 8u);
+                    m |= (uint64_t)b4 << (q * 16 + t * 4);
+                }
+            }
+        } else {
+            for (int64_t i = r0; i < n; ++i) m |= (uint64_t)(vb[i] != 0) << (i - r0);
         }
-        const uint64_t m = __ballot(ok);
-        if (valid && lane == 0) valid[i >> 6] = m;
+        valid[w] = m;
     }
 }
 
@@ -1414,16 +1442,23 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     int bits = 1;
     while (bits < 64 && ((range + 1) >> bits) != 0) ++bits;
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
-    // ping-pong buffers; the payload buffer the last pass writes is the output column's values
+    // ping-pong buffers; pass 0 reads the payload column itself, the last pass writes the output
+    // columns: the payload, and the key decoded from its codes (+ one valid byte per row when nullable)
     QEH_TRY(alloc_column(ctx, val.dtype, n, false, out_val));
-    DevBuf kb[2], vtmp, hist, offs;
+    int s = alloc_column(ctx, key.dtype, n, nullable, out_key);
+    if (s != QEH_OK) {
+        qeh_column_release(ctx, out_val);
+        return s;
+    }
+    DevBuf kb[2], vtmp, hist, offs, validb;
     const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)ctx->props.multiProcessorCount);
     const int64_t seg = (n + nblocks - 1) / nblocks;
-    int s = QEH_OK;
     if (kb[0].alloc(ctx, n * 8) || kb[1].alloc(ctx, n * 8) || vtmp.alloc(ctx, n * 8) ||
-        hist.alloc(ctx, (size_t)kRadix * nblocks * 4) || offs.alloc(ctx, (size_t)kRadix * nblocks * 8))
+        hist.alloc(ctx, (size_t)kRadix * nblocks * 4) || offs.alloc(ctx, (size_t)kRadix * nblocks * 8) ||
+        (nullable && validb.alloc(ctx, n)))
         s = fail(QEH_E_OOM, "payload sort: out of device memory");
-    // pass p reads buffer p % 2 and writes (p + 1) % 2; the last pass writes the output column
+    // pass p reads buffer p % 2 (pass 0: the input column) and writes (p + 1) % 2
+    const uint64_t *vsrc = (const uint64_t *)((const char *)val.values + (size_t)val.offset * 8);
     uint64_t *vb[2];
     vb[npass % 2] = (uint64_t *)out_val->values;
     vb[(npass + 1) % 2] = vtmp.as<uint64_t>();
@@ -1431,10 +1466,8 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
         KernelTimer kt(ctx, "sort_encode");
         hipLaunchKernelGGL(k_encode_kv, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream, kc, n, mn, mx,
                            asc ? 1 : 0, bias, null_code, kb[0].as<uint64_t>());
-        const char *vsrc = (const char *)val.values + (size_t)val.offset * 8;
-        if (hipMemcpyAsync(vb[0], vsrc, (size_t)n * 8, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
-            s = fail(QEH_E_HIP, "payload sort: copy failed");
     }
+    RsDecode dec{mn, mx, bias, null_code, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
     for (int p = 0; p < npass && s == QEH_OK; ++p) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = p & 1, shift = p * kRadixBits;
@@ -1442,22 +1475,26 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
                            shift, hist.as<uint32_t>(), nblocks);
         s = exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr);
         if (s != QEH_OK) break;
-        hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
-                           kb[c].as<uint64_t>(), vb[c], n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
-                           vb[1 - c], nullptr, 0);
+        const uint64_t *vin = p == 0 ? vsrc : vb[c];
+        if (p + 1 < npass)
+            hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
+                               kb[c].as<uint64_t>(), vin, n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
+                               vb[1 - c], nullptr, 0, RsDecode{});
+        else
+            hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t, true>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
+                               kb[c].as<uint64_t>(), vin, n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
+                               vb[1 - c], nullptr, 0, dec);
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: pass launch failed");
     }
-    if (s == QEH_OK) s = alloc_column(ctx, key.dtype, n, nullable, out_key);
-    if (s == QEH_OK) {
+    if (s == QEH_OK && nullable) {
         KernelTimer kt(ctx, "sort_encode");
-        hipLaunchKernelGGL(k_decode_keys, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream,
-                           kb[npass % 2].as<uint64_t>(), n, mn, mx, asc ? 1 : 0, bias, null_code, key.dtype, out_key->values,
-                           nullable ? (uint64_t *)out_key->validity : nullptr);
-        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: decode launch failed");
-        if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "payload sort failed");
-        if (s != QEH_OK) qeh_column_release(ctx, out_key);
+        hipLaunchKernelGGL(k_pack_valid, dim3(grid_for(ctx, (n + 63) / 64, kBlock, 8)), dim3(kBlock), 0, ctx->stream, validb.as<uint8_t>(),
+                           n, (uint64_t *)out_key->validity);
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: validity launch failed");
     }
+    if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "payload sort failed");
     if (s != QEH_OK) {
+        qeh_column_release(ctx, out_key);
         qeh_column_release(ctx, out_val);
         return s;
     }
