@@ -163,9 +163,30 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
     return peers;
 }
 
-template <typename KeyT>
+// The payload sort's first pass reads the raw key column and encodes on load (KES = 4 / 8: Int32 /
+// Int64 values) instead of a separate encode pass; KES = 0 reads the codes.
+struct RsEncode {
+    ColRef c;
+    int64_t mn, mx;
+    uint64_t bias, null_code;
+    int32_t asc;
+};
+
+template <int KES, typename KeyT>
+__device__ __forceinline__ KeyT rs_load_key(const KeyT *__restrict__ keys, const RsEncode &e, int64_t i) {
+    if constexpr (KES == 0) {
+        return __builtin_nontemporal_load(&keys[i]);
+    } else {
+        const int64_t x = KES == 4 ? (int64_t)__builtin_nontemporal_load((const int32_t *)e.c.values + i)
+                                   : __builtin_nontemporal_load((const int64_t *)e.c.values + i);
+        const uint64_t code = e.asc ? (uint64_t)x - (uint64_t)e.mn + e.bias : (uint64_t)e.mx - (uint64_t)x + e.bias;
+        return (KeyT)(col_valid(e.c, i) ? code : e.null_code);
+    }
+}
+
+template <typename KeyT, int KES = 0>
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__ keys, int64_t n, int64_t seg,
-                                                        int shift, uint32_t *__restrict__ hist, int nblocks) {
+                                                        int shift, uint32_t *__restrict__ hist, int nblocks, RsEncode enc) {
     constexpr int W = kRsThreads / 64;
     __shared__ uint32_t h[W][kRadix];  // per-wave counters: one LDS atomic per row
     for (int i = threadIdx.x; i < W * kRadix; i += kRsThreads) (&h[0][0])[i] = 0;
@@ -178,7 +199,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
-            k[j] = __builtin_nontemporal_load(&keys[i < hi ? i : hi - 1]);
+            k[j] = rs_load_key<KES>(keys, enc, i < hi ? i : hi - 1);
         }
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
@@ -246,7 +267,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // The payload sort's last pass writes the decoded key column itself (DEC): code -> Int64 / Int32 value
-// as k_encode_kv's inverse, and one valid byte per row for the bitmap packed afterwards.
+// as rs_load_key's inverse, and one valid byte per row for the bitmap packed afterwards.
 struct RsDecode {
     int64_t mn, mx;
     uint64_t bias, null_code;
@@ -258,12 +279,12 @@ struct RsDecode {
 // AT: tile ranks by LDS atomics (ds_add_rtn serves one instruction's lanes in lane order, so the
 // rank is stable: tools/ubench/lds_order_ubench.hip), else by ballot peers (QEH_RS_BALLOT=1, A/B).
 // ValT: the carried value -- a u32 row id, or (qeh_merge_sorted's payload sort) an 8-B payload.
-template <typename KeyT, bool AT = true, typename ValT = uint32_t, bool DEC = false>
+template <typename KeyT, bool AT = true, typename ValT = uint32_t, bool DEC = false, int KES = 0>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const ValT *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
                                                            int nblocks, KeyT *__restrict__ keys_out,
                                                            ValT *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
-                                                           int nshift, RsDecode dec) {
+                                                           int nshift, RsDecode dec, RsEncode enc) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
     __shared__ KeyT s_keys[kRsSTile];
@@ -287,7 +308,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
             const int64_t ii = i < hi ? i : hi - 1;
-            kk[j] = __builtin_nontemporal_load(&keys[ii]);
+            kk[j] = rs_load_key<KES>(keys, enc, ii);
             vv[j] = __builtin_nontemporal_load(&vals[ii]);
         }
     };
@@ -711,14 +732,14 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
                                hist.as<uint32_t>(), nblocks);
         else
             hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg,
-                               shift, hist.as<uint32_t>(), nblocks);
+                               shift, hist.as<uint32_t>(), nblocks, RsEncode{});
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         const bool next = multi && shift + kRadixBits < bits;
         auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
         hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(),
                            nblocks, rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr,
-                           shift + kRadixBits, RsDecode{});
+                           shift + kRadixBits, RsDecode{}, RsEncode{});
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
@@ -738,12 +759,12 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
     KernelTimer kt(ctx, "radix_pass");
     const int c = rs.cur;
     hipLaunchKernelGGL(k_rs_hist<KeyT>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), n, seg, shift,
-                       hist.as<uint32_t>(), nblocks);
+                       hist.as<uint32_t>(), nblocks, RsEncode{});
     QEH_HIP(hipGetLastError());
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
     auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
     hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks,
-                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{});
+                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{}, RsEncode{});
     QEH_HIP(hipGetLastError());
     rs.cur = 1 - c;
     return QEH_OK;
@@ -1376,17 +1397,6 @@ extern "C" int qeh_sort_indices(qeh_ctx *ctx, const qeh_column *keys, int n_keys
 // code when NULLs go first, or above them when last) and sorted with the payload itself as the carried
 // value, so no permutation is gathered afterwards: the sorted key column is decoded from the sorted
 // codes, and the last pass writes the payload straight into the output column.
-__global__ void k_encode_kv(ColRef c, int64_t n, int64_t mn, int64_t mx, int asc, uint64_t bias, uint64_t null_code,
-                            uint64_t *__restrict__ keys) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t k = null_code;
-        if (col_valid(c, i)) {
-            const int64_t x = load_i64(c, i);
-            k = asc ? (uint64_t)x - (uint64_t)mn + bias : (uint64_t)mx - (uint64_t)x + bias;
-        }
-        keys[i] = k;
-    }
-}
 
 // valid bytes (the last pass's, one per row, each 0 or 1) -> the key's validity bitmap: one 64-row word
 // per thread from four 16-B loads (bit i of a dword's 4 flags = bit 8 i of the dword)
@@ -1462,28 +1472,25 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     uint64_t *vb[2];
     vb[npass % 2] = (uint64_t *)out_val->values;
     vb[(npass + 1) % 2] = vtmp.as<uint64_t>();
-    if (s == QEH_OK) {
-        KernelTimer kt(ctx, "sort_encode");
-        hipLaunchKernelGGL(k_encode_kv, dim3(grid_for(ctx, n, kBlock, 8)), dim3(kBlock), 0, ctx->stream, kc, n, mn, mx,
-                           asc ? 1 : 0, bias, null_code, kb[0].as<uint64_t>());
-    }
-    RsDecode dec{mn, mx, bias, null_code, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
+    // pass 0 encodes the key column on load (histogram and scatter), the last pass decodes on store
+    const RsEncode enc{kc, mn, mx, bias, null_code, asc ? 1 : 0};
+    const RsDecode dec{mn, mx, bias, null_code, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
+    const bool k32 = key.dtype == QEH_DT_INT32;
     for (int p = 0; p < npass && s == QEH_OK; ++p) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = p & 1, shift = p * kRadixBits;
-        hipLaunchKernelGGL(k_rs_hist<uint64_t>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), n, seg,
-                           shift, hist.as<uint32_t>(), nblocks);
+        const bool first = p == 0, last = p + 1 == npass;
+        auto hk = !first ? k_rs_hist<uint64_t, 0> : k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
+        hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), n, seg, shift,
+                           hist.as<uint32_t>(), nblocks, enc);
         s = exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr);
         if (s != QEH_OK) break;
-        const uint64_t *vin = p == 0 ? vsrc : vb[c];
-        if (p + 1 < npass)
-            hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
-                               kb[c].as<uint64_t>(), vin, n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
-                               vb[1 - c], nullptr, 0, RsDecode{});
-        else
-            hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t, true>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,
-                               kb[c].as<uint64_t>(), vin, n, seg, shift, offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(),
-                               vb[1 - c], nullptr, 0, dec);
+        const uint64_t *vin = first ? vsrc : vb[c];
+        auto sk = first ? (last ? (k32 ? k_rs_scatter<uint64_t, true, uint64_t, true, 4> : k_rs_scatter<uint64_t, true, uint64_t, true, 8>)
+                                : (k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4> : k_rs_scatter<uint64_t, true, uint64_t, false, 8>))
+                        : (last ? k_rs_scatter<uint64_t, true, uint64_t, true, 0> : k_rs_scatter<uint64_t, true, uint64_t, false, 0>);
+        hipLaunchKernelGGL(sk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), vin, n, seg, shift,
+                           offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(), vb[1 - c], nullptr, 0, dec, enc);
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: pass launch failed");
     }
     if (s == QEH_OK && nullable) {

@@ -109,13 +109,15 @@ def test_sort_indices_nulls_vs_oracle(ctx, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt,asc,nf,nulls,key_col", [
-    (np.int64, False, False, True, 0),   # the Merge::sorted bench shape: k DESC NULLS LAST, v payload
-    (np.int64, True, True, True, 1),     # key second, NULLs first
-    (np.int32, True, False, False, 0),   # Int32 key, no NULLs
-    (np.int64, False, True, False, 1),
+@pytest.mark.parametrize("dt,asc,nf,nulls,key_col,span", [
+    (np.int64, False, False, True, 0, 5000),   # the Merge::sorted bench shape: k DESC NULLS LAST, v payload
+    (np.int64, True, True, True, 1, 5000),     # key second, NULLs first
+    (np.int32, True, False, False, 0, 5000),   # Int32 key, no NULLs
+    (np.int64, False, True, False, 1, 5000),
+    (np.int32, False, True, True, 0, 100),     # one radix pass: encode on load and decode on store together
+    (np.int64, True, False, True, 1, 2 ** 40),  # five passes
 ])
-def test_merge_sorted_key_payload_pairs_vs_oracle(ctx, dt, asc, nf, nulls, key_col):
+def test_merge_sorted_key_payload_pairs_vs_oracle(ctx, dt, asc, nf, nulls, key_col, span):
     """One sort key and one 8-byte payload: the payload rides through the radix passes (no gather)
     and the key column is decoded from the sorted codes.  Stable (ties keep the concatenation order),
     NULL placement, negative keys, several tiles and ragged partitions; equal to the oracle's stable
@@ -123,7 +125,7 @@ def test_merge_sorted_key_payload_pairs_vs_oracle(ctx, dt, asc, nf, nulls, key_c
     rng = np.random.default_rng(7 + key_col)
     sizes = [70_001, 0, 33_333, 9]
     n = sum(sizes)
-    k = rng.integers(-5000, 5000, n).astype(dt)  # many ties
+    k = rng.integers(-span, span, n).astype(dt)  # many ties at the small spans
     kv = rng.random(n) > 0.1 if nulls else np.ones(n, bool)
     v = rng.random(n)
     bounds = np.concatenate([[0], np.cumsum(sizes)])

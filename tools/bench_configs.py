@@ -282,7 +282,7 @@ def cfg_merge(ctx, scale):
     dt = time.perf_counter() - t0
     cpu = {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"{m} rows sort, {dt:.2f} s"}
     line("Merge::sorted 8 x 1.25e7 rows, ORDER BY k DESC NULLS LAST", n, wall, 32.0 * n, sum(kt.values()),
-         "k_rs_hist/k_rs_scatter + gathers", cpu, kt)
+         "k_rs_hist/k_rs_scatter carrying the payload (encode on load in pass 0, decode on store in the last)", cpu, kt)
 
 
 def cfg_encode(ctx, scale):
