@@ -1208,6 +1208,25 @@ class Executor {
             *out = in;
             return QEH_OK;
         }
+        const int kj = nd.n_exprs == 1 && in.cols.size() == 2 ? expr_as_column(&nd.exprs[0]) : -1;
+        if (kj == 0 || kj == 1) {
+            // a key column and one 8-byte payload: the payload rides through the radix passes (no
+            // permutation, no gathers); NULL keys first, as qeh_sort_indices
+            qeh_column ok{}, ov{};
+            const int ps = sort_pairs_payload(ctx_, in.cols[kj].c, in.cols[1 - kj].c,
+                                              nd.ascending ? nd.ascending[0] != 0 : true, true, &ok, &ov);
+            if (ps != kPayloadSortNotEligible) {
+                QEH_TRY(ps);
+                Col k = own(ctx_, ok), v = own(ctx_, ov);
+                out->fields = in.fields;
+                out->cols.assign(2, Col{});
+                out->cols[kj] = k;
+                out->cols[1 - kj] = v;
+                out->rows = in.rows;
+                out->batches = in.batches;
+                return QEH_OK;
+            }
+        }
         std::vector<Col> keys;
         for (int i = 0; i < nd.n_exprs; ++i) {
             Col c;

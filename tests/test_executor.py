@@ -166,6 +166,28 @@ def test_sort_limit_subquery_window(qx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("key_col,asc,key_dt,nulls", [(0, True, pa.int64(), True), (1, False, pa.int32(), False),
+                                                      (0, False, pa.int64(), False)])
+def test_sort_key_and_payload_columns(qx, monkeypatch, key_col, asc, key_dt, nulls):
+    """Sort of a two-column table by one Int key column: the payload column rides through the radix
+    passes (no permutation, no gathers); stable, NULL keys first -- equal to the oracle's stable sort
+    and to the permutation path (QEH_NO_PAYLOAD_SORT=1)."""
+    r = np.random.default_rng(11 + key_col)
+    n = 90_001
+    k = pa.array(r.integers(-3000, 3000, n), key_dt, mask=(r.random(n) < 0.07) if nulls else None)
+    v = pa.array(r.random(n))
+    t = pa.table({"t.k": k, "t.v": v} if key_col == 0 else {"t.v": v, "t.k": k})
+    plan = Sort(Scan(source(t, 3)), [Column("t.k", key_col)], [asc])
+    got = as_cols(qx.execute(plan))
+    kc = as_cols([t.combine_chunks().to_batches()[0]])[key_col]
+    perm = ob.sort_indices([ob.HostCol(kc[0].astype(np.int64), kc[1])], [asc])
+    want = t.take(pa.array(perm))
+    assert rows_of(got) == rows_of(as_cols(want.to_batches()))
+    monkeypatch.setenv("QEH_NO_PAYLOAD_SORT", "1")
+    assert rows_of(as_cols(qx.execute(plan))) == rows_of(got)
+
+
+@pytest.mark.gpu
 def test_projection_join_and_errors(qx):
     a = pa.table({"a.id": np.arange(100, dtype=np.int64), "a.x": np.arange(100, dtype=np.int64) * 2})
     b = pa.table({"b.id": np.arange(0, 200, 2, dtype=np.int64), "b.name": [f"n{i}" for i in range(100)]})
