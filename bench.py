@@ -330,14 +330,22 @@ def main():
         avg_probe_ms = probe_ms / max(probe_launches, 1)
         kernel_name = "k_join_agg_fast (HIP events 'join_filter_aggregate')"
         kernel_split = None
-    alg_bytes = 24.0 * n  # x, k, v read once per fact row of this GPU
+    # x, k, v read once per fact row of this GPU (24 B) + the dim's k, g read once
+    # per dim row this GPU builds from (16 B; at N = 1 the whole 1e7-row dim: 24.16 GB per step)
+    alg_bytes = 24.0 * n + 16.0 * dn
     achieved = alg_bytes / (avg_probe_ms * 1e-3) / 1e9
-    traffic = None
+    # roofline.traffic is not measured in this run (PMC counters need their own rocprofv3 passes):
+    # it is read from the committed record of such a run (tools/profile.sh -> tools/pmc_traffic.py),
+    # used only when that record is for the same shape, and labelled with where it came from
+    traffic, traffic_source = None, None
     if os.path.exists(args.traffic_json) and not dist:
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("rows") == n and tj.get("kernel") == "join_filter_aggregate":
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_source = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                  f"passes of a separate run ({tj.get('source', 'tools/profile.sh')}), FETCH_SIZE x2 "
+                                  "(gfx950 wide-read correction) + WRITE_SIZE per query, not measured in this run")
         except Exception:
             traffic = None
 
@@ -387,6 +395,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel": kernel_name,
                 "kernel_ms": avg_probe_ms,
                 "kernel_split_ms": kernel_split,

@@ -135,6 +135,10 @@ int qeh_abi_version(void);
 const char *qeh_last_error(void);
 
 int qeh_init(int device, qeh_ctx **out);
+/* 1 when the device serves the lanes of one returning LDS atomic in lane order (the stable tile
+ * ranking of the sort, exchange and window passes relies on it; checked once per process by a
+ * self-test kernel, else those passes rank by ballot matching), 0 otherwise. */
+int qeh_lds_atomic_rank_ok(qeh_ctx *ctx);
 int qeh_shutdown(qeh_ctx *ctx);
 /* Run on a caller-owned hipStream_t (e.g. torch's current stream); NULL =
  * the context's own stream. */

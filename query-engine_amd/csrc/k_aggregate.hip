@@ -555,6 +555,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         for (int u = 0; u < VS; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) vcur[u][r] = VC ? ft.a(u, r) : 0;
+#ifdef QEH_EXP_EARLY_ISSUE
+        if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
+#endif
         lds_barrier();  // B1: counts complete, tile t-1 flushed
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged
@@ -617,7 +620,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             cnb[pq][tid] = T % CH;
             cntb[pq][tid] = 0;
         }
+#ifndef QEH_EXP_EARLY_ISSUE
         if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
+#endif
         lds_barrier();  // B3: staged, chunks planned
         m_prev = s_chunks;
         have_prev = true;

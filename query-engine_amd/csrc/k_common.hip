@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "device_common.h"
@@ -373,4 +374,95 @@ extern "C" int qeh_bytes_to_validity(qeh_ctx *ctx, const uint8_t *bytes, int64_t
                        bytes, n, (uint64_t *)out_bitmap);
     QEH_HIP(hipGetLastError());
     return QEH_OK;
+}
+
+namespace qeh {
+
+// ---- self-check of the stable LDS-atomic tile ranking -----------------------------------------
+// The stable partition passes (k_rs_scatter, k_part_scatter_small, the window passes) rank a tile's
+// rows per digit with one returning LDS atomic per row; that rank is stable only if ds_add_rtn serves
+// the lanes of one instruction that hit the same word in lane order.  This kernel checks exactly that
+// on the running device, in both forms the passes use (a u32 counter per digit, and two u16 counters
+// packed per word), against ranks computed by ballot matching; the host falls back to the ballot
+// ranking when any rank differs.
+namespace {
+constexpr int kRcBlock = 512, kRcRounds = 8, kRcDig = 1024;
+__device__ __forceinline__ uint32_t rc_digit(int pat, int w, int j, int lane) {
+    uint64_t z = ((uint64_t)pat << 48) ^ ((uint64_t)w << 24) ^ ((uint64_t)j << 8) ^ (uint64_t)lane;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint32_t masks[4] = {kRcDig - 1, 63u, 3u, 0u};  // uniform, narrow, hot and single-digit patterns
+    return (uint32_t)z & masks[pat & 3];
+}
+}  // namespace
+
+__global__ __launch_bounds__(kRcBlock) void k_lds_rank_check(uint32_t *__restrict__ bad) {
+    __shared__ uint32_t c32[kRcBlock / 64][kRcDig];       // u32 counter per digit (k_rs_scatter form)
+    __shared__ uint32_t c16[kRcBlock / 64][kRcDig / 2];   // u16 halves packed per word (window form)
+    __shared__ uint32_t ref[kRcBlock / 64][kRcDig];       // rows of each digit ranked so far (ballot)
+    __shared__ uint32_t nbad;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) nbad = 0;
+    uint32_t miss = 0;
+    for (int pat = 0; pat < 4; ++pat) {
+        for (int i = lane; i < kRcDig; i += 64) c32[wave][i] = 0, ref[wave][i] = 0;
+        for (int i = lane; i < kRcDig / 2; i += 64) c16[wave][i] = 0;
+        __syncthreads();
+        for (int j = 0; j < kRcRounds; ++j) {
+            const uint32_t d = rc_digit(pat, blockIdx.x * (kRcBlock / 64) + wave, j, lane);
+            const uint32_t r32 = atomicAdd(&c32[wave][d], 1u);
+            const uint32_t sh = (d & 1u) * 16u;
+            const uint32_t r16 = (atomicAdd(&c16[wave][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
+            // lanes of this round with the same digit, by ballot over the digit bits
+            uint64_t m = ~0ull;
+            for (int b = 0; b < 10; ++b) {
+                const uint64_t bl = __ballot(((d >> b) & 1u) != 0);
+                m &= ((d >> b) & 1u) ? bl : ~bl;
+            }
+            const uint32_t before = ref[wave][d];
+            const uint32_t want = before + mbcnt(m);
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // every lane read ref before the group's last lane updates it
+            __builtin_amdgcn_wave_barrier();
+            if (mbcnt(m) + 1u == (uint32_t)popc64(m)) ref[wave][d] = before + (uint32_t)popc64(m);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            miss += (r32 != want) + (r16 != want);
+        }
+        __syncthreads();
+    }
+    if (miss) atomicAdd(&nbad, miss);
+    __syncthreads();
+    if (threadIdx.x == 0) bad[blockIdx.x] = nbad;
+}
+
+// true when the device ranks stably by LDS atomics; checked once per process (first caller's device)
+bool lds_atomic_rank_ok(qeh_ctx *ctx) {
+    static int state = -1;  // -1 unknown, 0 fall back to ballot, 1 atomics are lane-ordered
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (state >= 0) return state == 1;
+    state = 0;
+    constexpr int blocks = 64;
+    DevBuf bad;
+    if (bad.alloc(ctx, blocks * 4) != QEH_OK) return false;
+    hipLaunchKernelGGL(k_lds_rank_check, dim3(blocks), dim3(kRcBlock), 0, ctx->stream, bad.as<uint32_t>());
+    uint32_t h[blocks];
+    if (hipGetLastError() != hipSuccess || hipMemcpyAsync(h, bad.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return false;
+    uint64_t tot = 0;
+    for (int i = 0; i < blocks; ++i) tot += h[i];
+    state = tot == 0 ? 1 : 0;
+    return state == 1;
+}
+
+}  // namespace qeh
+
+extern "C" int qeh_lds_atomic_rank_ok(qeh_ctx *ctx) {
+    using namespace qeh;
+    if (!ctx) return fail(QEH_E_INVALID, "qeh_lds_atomic_rank_ok: bad argument");
+    DeviceGuard dg(ctx->device);
+    return lds_atomic_rank_ok(ctx) ? 1 : 0;
 }

@@ -163,6 +163,22 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t dg, bool live) {
     return peers;
 }
 
+// Stable rank of this lane's row among the rows of digit dg ranked so far by this wave (wc = the
+// wave's counters): one returning LDS atomic when the device serves a wave's lanes in lane order
+// (AT, the default after the lds_atomic_rank_ok self-check), else ballot peers; dead lanes get 0.
+template <bool AT>
+__device__ __forceinline__ uint32_t tile_rank(uint32_t *wc, uint32_t dg, bool live) {
+    if constexpr (AT) {
+        return live ? atomicAdd(&wc[dg], 1u) : 0u;
+    } else {
+        const uint32_t d = live ? dg : 0u;
+        const uint64_t peers = digit_peers(d, live);
+        const uint32_t before = wc[d];
+        if (live && mbcnt(peers) == 0) wc[d] = before + (uint32_t)popc64(peers);
+        return live ? before + mbcnt(peers) : 0u;
+    }
+}
+
 // The payload sort's first pass reads the raw key column and encodes on load (KES = 4 / 8: Int32 /
 // Int64 values) instead of a separate encode pass; KES = 0 reads the codes.
 struct RsEncode {
@@ -414,7 +430,7 @@ struct PmCols {
 
 // Rows whose id is >= `drop` (the filtered-out rows of a fused filter + exchange) are ranked last
 // and not written.
-template <int NC>
+template <int NC, bool AT = true>
 __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
                                                              const uint64_t *__restrict__ offs, int nblocks, PmCols cols,
                                                              uint32_t drop) {
@@ -464,7 +480,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
 #pragma unroll
         for (int j = 0; j < kPmIpt; ++j) {
             const bool live = base + j * 64 < hi;
-            rk[j] = live ? atomicAdd(&wcnt[wave][dg[j]], 1u) : 0u;  // stable (lane-ordered LDS atomics)
+            rk[j] = tile_rank<AT>(wcnt[wave], dg[j], live);  // stable
         }
         lds_barrier();
         uint32_t tot = 0, incl = 0;
@@ -516,7 +532,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter(const uint8_t *__re
 // with an id >= drop (the filtered-out rows) neither ranked nor staged, so the write loop covers only
 // the rows that move.
 constexpr int kPsDig = 16;
-template <int NC>
+template <int NC, bool AT = true>
 __global__ __launch_bounds__(kRsThreads) void k_part_scatter_small(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
                                                                    const uint64_t *__restrict__ offs, int nblocks, PmCols cols,
                                                                    uint32_t drop) {
@@ -565,7 +581,7 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter_small(const uint8_t
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             mv[j] = base + j * 64 < hi && dg[j] < drop;
-            rk[j] = mv[j] ? atomicAdd(&wcnt[wave][dg[j]], 1u) : 0u;  // stable (lane-ordered LDS atomics)
+            rk[j] = tile_rank<AT>(wcnt[wave], dg[j], mv[j]);  // stable
         }
         lds_barrier();
         if (t < 64) {  // lane d < kPsDig: per-wave starts inside partition d, its tile total, the scan
@@ -704,9 +720,10 @@ struct RadixState {
     bool key32 = false;          // k[] currently holds 32-bit keys (column range fits 32 bits)
 };
 
-static bool rs_ballot() {
-    static const bool v = std::getenv("QEH_RS_BALLOT") != nullptr;
-    return v;
+// ballot ranking when asked for (QEH_RS_BALLOT=1, A/B) or when the device's LDS atomics failed the
+// lane-order self-check (lds_atomic_rank_ok)
+static bool rs_ballot(qeh_ctx *ctx) {
+    return std::getenv("QEH_RS_BALLOT") != nullptr || !lds_atomic_rank_ok(ctx);
 }
 
 // Stable LSD passes over the low `bits` of the encoded keys in rs.
@@ -736,7 +753,7 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
         QEH_HIP(hipGetLastError());
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         const bool next = multi && shift + kRadixBits < bits;
-        auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
+        auto scat = rs_ballot(ctx) ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
         hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(),
                            nblocks, rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr,
                            shift + kRadixBits, RsDecode{}, RsEncode{});
@@ -762,7 +779,7 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
                        hist.as<uint32_t>(), nblocks, RsEncode{});
     QEH_HIP(hipGetLastError());
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
-    auto scat = rs_ballot() ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
+    auto scat = rs_ballot(ctx) ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
     hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks,
                        rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{}, RsEncode{});
     QEH_HIP(hipGetLastError());
@@ -1430,6 +1447,7 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     const int64_t n = key.length;
     if (std::getenv("QEH_NO_PAYLOAD_SORT") || n <= 1 || n >= ((int64_t)1 << 32) || val.length != n) return kPayloadSortNotEligible;
     if (key.dtype != QEH_DT_INT64 && key.dtype != QEH_DT_INT32) return kPayloadSortNotEligible;
+    if (rs_ballot(ctx)) return kPayloadSortNotEligible;  // its passes rank by LDS atomics only
     if ((val.dtype != QEH_DT_INT64 && val.dtype != QEH_DT_FLOAT64) || (val.validity && val.null_count != 0))
         return kPayloadSortNotEligible;
     const ColRef kc = make_colref(key);
@@ -1449,8 +1467,12 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     const bool nullable = key.validity && key.null_count != 0;
     const uint64_t bias = nullable && nulls_first ? 1 : 0;
     const uint64_t null_code = nullable && nulls_first ? 0 : range + 1;  // (no NULLs: never produced)
+    // the largest code: range (+ 1 for the NULL code when nullable); a nullable key spanning the
+    // whole Int64 range has no free code left, so it takes the permutation sort
+    if (nullable && range == UINT64_MAX) return kPayloadSortNotEligible;
+    const uint64_t max_code = range + (nullable ? 1 : 0);
     int bits = 1;
-    while (bits < 64 && ((range + 1) >> bits) != 0) ++bits;
+    while (bits < 64 && (max_code >> bits) != 0) ++bits;
     const int npass = (bits + kRadixBits - 1) / kRadixBits;
     // ping-pong buffers; pass 0 reads the payload column itself, the last pass writes the output
     // columns: the payload, and the key decoded from its codes (+ one valid byte per row when nullable)
@@ -2136,19 +2158,20 @@ extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int
             pc.dst[q] = (uint64_t *)out_cols[mv[g + q]].values;
         }
         KernelTimer kt(ctx, "partition_move");
-#define QEH_PM(NCV)                                                                                                        \
+#define QEH_PM(NCV, AT)                                                                                                       \
     do {                                                                                                               \
         if (small)                                                                                                     \
-            hipLaunchKernelGGL(k_part_scatter_small<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
+            hipLaunchKernelGGL((k_part_scatter_small<NCV, AT>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
                                ids.as<uint8_t>(), n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix);         \
         else                                                                                                           \
-            hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
+            hipLaunchKernelGGL((k_part_scatter<NCV, AT>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
                                n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)kRadix);                            \
     } while (0)
-        if (nc == 1) QEH_PM(1);
-        else if (nc == 2) QEH_PM(2);
-        else if (nc == 3) QEH_PM(3);
-        else QEH_PM(4);
+        const bool ballot = rs_ballot(ctx);
+        if (nc == 1) { if (ballot) QEH_PM(1, false); else QEH_PM(1, true); }
+        else if (nc == 2) { if (ballot) QEH_PM(2, false); else QEH_PM(2, true); }
+        else if (nc == 3) { if (ballot) QEH_PM(3, false); else QEH_PM(3, true); }
+        else { if (ballot) QEH_PM(4, false); else QEH_PM(4, true); }
 #undef QEH_PM
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "partition move launch failed");
     }
@@ -2277,19 +2300,20 @@ extern "C" int qeh_filter_partition_hash_move(qeh_ctx *ctx, const qeh_column *co
         }
         KernelTimer kt(ctx, "partition_move");
         const bool small = n_parts < kPsDig && !std::getenv("QEH_PM_GENERIC");  // ids 0..n_parts (the drop id)
-#define QEH_FPM(NCV)                                                                                                       \
+#define QEH_FPM(NCV, AT)                                                                                                      \
     do {                                                                                                               \
         if (small)                                                                                                     \
-            hipLaunchKernelGGL(k_part_scatter_small<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
+            hipLaunchKernelGGL((k_part_scatter_small<NCV, AT>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream,             \
                                ids.as<uint8_t>(), n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts);        \
         else                                                                                                           \
-            hipLaunchKernelGGL(k_part_scatter<NCV>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
+            hipLaunchKernelGGL((k_part_scatter<NCV, AT>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), \
                                n, seg, offs.as<uint64_t>(), nblocks, pc, (uint32_t)n_parts);                           \
     } while (0)
-        if (n_move == 1) QEH_FPM(1);
-        else if (n_move == 2) QEH_FPM(2);
-        else if (n_move == 3) QEH_FPM(3);
-        else QEH_FPM(4);
+        const bool ballot = rs_ballot(ctx);
+        if (n_move == 1) { if (ballot) QEH_FPM(1, false); else QEH_FPM(1, true); }
+        else if (n_move == 2) { if (ballot) QEH_FPM(2, false); else QEH_FPM(2, true); }
+        else if (n_move == 3) { if (ballot) QEH_FPM(3, false); else QEH_FPM(3, true); }
+        else { if (ballot) QEH_FPM(4, false); else QEH_FPM(4, true); }
 #undef QEH_FPM
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "filter-partition move launch failed");
     }

@@ -1105,7 +1105,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
     const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
     // stable tile ranking by LDS atomics (default) or by ballot matching (QEH_WM_BALLOT=1, A/B)
-    const bool at = std::getenv("QEH_WM_BALLOT") == nullptr;
+    const bool at = std::getenv("QEH_WM_BALLOT") == nullptr && lds_atomic_rank_ok(ctx);
     int gbx = 2;  // bucket workgroups per CU (pass 2 / its inverse)
     if (const char *e = std::getenv("QEH_WM_GBX")) gbx = std::max(1, std::atoi(e));
     const int gb = std::min(cus * gbx, sh.nb);

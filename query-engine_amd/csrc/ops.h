@@ -157,5 +157,7 @@ int kernel_error_status(uint32_t err, const char *op);
 
 // Environment knob for forcing a table layout in tests ("direct"/"packed"/"wide").
 int forced_table_kind();
+// the device ranks a tile's rows stably by returning LDS atomics (checked once per process)
+bool lds_atomic_rank_ok(qeh_ctx *ctx);
 
 }  // namespace qeh

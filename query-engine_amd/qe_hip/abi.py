@@ -56,6 +56,7 @@ SIGNATURES = {
     "qeh_last_error": (C.c_char_p, []),
     "qeh_init": (I, [I, C.POINTER(P)]),
     "qeh_shutdown": (I, [P]),
+    "qeh_lds_atomic_rank_ok": (I, [P]),
     "qeh_set_stream": (I, [P, P]),
     "qeh_get_stream": (P, [P]),
     "qeh_synchronize": (I, [P]),

@@ -149,6 +149,14 @@ class Context:
     def d2h(self, dst: np.ndarray, src: int, nbytes: int) -> None:
         abi.check(self.lib.qeh_memcpy_d2h(self.h, dst.ctypes.data, src, nbytes))
 
+    def lds_atomic_rank_ok(self) -> bool:
+        """Whether the device ranks a tile's rows stably by LDS atomics (else the sort, exchange
+        and window passes rank by ballot matching); a once-per-process self-check kernel."""
+        s = self.lib.qeh_lds_atomic_rank_ok(self.h)
+        if s < 0:
+            abi.check(s)
+        return s == 1
+
     def sync(self) -> None:
         abi.check(self.lib.qeh_synchronize(self.h))
 

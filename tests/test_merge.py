@@ -143,3 +143,31 @@ def test_merge_sorted_key_payload_pairs_vs_oracle(ctx, dt, asc, nf, nulls, key_c
     assert np.array_equal(gk[gm], k[perm][kv[perm]])
     assert np.array_equal(gv, v[perm])  # bit-exact payload, stable order
     assert cols[key_col].dtype == (abi.DT_INT32 if dt == np.int32 else abi.DT_INT64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("asc,nf,nulls", [(True, False, False), (False, True, False), (True, True, True),
+                                          (False, False, True)])
+def test_merge_sorted_payload_full_range_keys(ctx, asc, nf, nulls):
+    """Keys spanning the whole Int64 range (INT64_MIN and INT64_MAX present): the payload sort needs all
+    64 key bits (eight passes); with NULLs there is no free code left, so the permutation sort runs.
+    Either way the result equals the oracle's stable sort (range + 1 used to wrap to 0)."""
+    r = np.random.default_rng(11)
+    n = 50_001
+    k = r.integers(-(2 ** 63), 2 ** 63 - 1, n, dtype=np.int64)
+    k[:4] = [-(2 ** 63), 2 ** 63 - 1, -(2 ** 63), 0]
+    k[-3:] = [2 ** 63 - 1, -1, -(2 ** 63)]
+    kv = r.random(n) > 0.2 if nulls else np.ones(n, bool)
+    kv[:4] = True
+    v = r.random(n)
+    half = n // 2
+    parts = [[ctx.upload(k[a:b], kv[a:b]) if nulls else ctx.upload(k[a:b]), ctx.upload(v[a:b])]
+             for a, b in ((0, half), (half, n))]
+    cols, rows = ctx.merge_sorted(parts, [0], [asc], [nf])
+    assert rows == n
+    perm = ob.sort_indices_nulls([ob.HostCol(k, kv)], [asc], [nf])
+    gk, gm = host(cols[0])
+    gv, _ = host(cols[1])
+    assert np.array_equal(gm, kv[perm])
+    assert np.array_equal(gk[gm], k[perm][kv[perm]])
+    assert np.array_equal(gv, v[perm])

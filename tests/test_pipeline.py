@@ -284,6 +284,61 @@ def test_group_range_slices(ctx, groups, skew):
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[])
 
 
+def _host_threads():
+    import os
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n)
+
+
+@pytest.mark.gpu
+def test_config2_full_size_vs_oracle(ctx):
+    """BASELINE config 2 at its full size (1e8 rows, the shape tools/bench_configs.py times):
+    SELECT k, SUM(v), COUNT(v), SUM(vi) FROM t WHERE x > 49 GROUP BY k through the device operator
+    (qeh_filter_aggregate) against the oracle's filter + grouped aggregate over the same counter-based
+    columns generated on the host: COUNT and the Int64 SUM bit-exact, SUM(v) within 1e-6."""
+    n = 100_000_000
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 2), (AF.Count, 2), (AF.Sum, 3)]
+    gen = [(abi.GEN_UNIFORM_MOD, 1, 100, 0), (abi.GEN_UNIFORM_MOD, 2, 1024, 0), (abi.GEN_UNIT_F64, 3, 0, 0),
+           (abi.GEN_UNIFORM_MOD, 4, 2 ** 21, -(2 ** 20))]
+    dev = [ctx.generate(kd, SEED, c, n, m, lo=lo) for kd, c, m, lo in gen]
+    gk, ga, g = ctx.filter_aggregate(dev, pred, [1], aggs)
+    got_k = [c.to_numpy() for c in gk]
+    got_a = [c.to_numpy() for c in ga]
+    del dev
+    host = [ob.HostCol(ob.generate(kd, SEED, c, n, m, lo=lo)) for kd, c, m, lo in gen]
+    fc, rows, _ = ob.filter(host, pred)
+    del host
+    fh = [ob.HostCol(v, m) for v, m in fc]
+    wk, wa, wg, _ = ob.hash_aggregate([fh[1]], fh, aggs)
+    assert g == wg == 1024
+    assert_grouped_equal(got_k, got_a, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+def test_metric_full_size_vs_oracle(ctx):
+    """The BASELINE metric query at its full size (1e9 fact rows x 1e7 dim rows) against the oracle
+    itself (its OpenMP restatement of the intended-semantics hash join + filter + group-by over the
+    same counter-based columns generated on the host): every group's COUNT bit-exact, SUM(v) within
+    1e-6 relative."""
+    n, nd, groups = 1_000_000_000, 10_000_000, 1024
+    dev = [ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100), ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd),
+           ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)]
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, groups)
+    gk, ga, g = ctx.join_filter_aggregate(dev, 1, PRED, dk, [dg], AGGS)
+    got_k = [c.to_numpy() for c in gk]
+    got_a = [c.to_numpy() for c in ga]
+    del dev, dk, dg
+    x, k, v, hdk, hdg = metric_data(n, nd, groups)
+    wk, wa, wg = ob.join_filter_aggregate_mt([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(hdk),
+                                             [ob.HostCol(hdg)], AGGS, _host_threads())
+    del x, k, v
+    assert g == wg == groups
+    assert_grouped_equal(got_k, got_a, wk, wa, float_aggs=[0])
+
+
 @pytest.mark.gpu
 def test_metric_full_size_properties(ctx):
     """The BASELINE metric query at its full size (1e9 fact rows x 1e7 dim rows, generated in HBM):

@@ -412,19 +412,29 @@ def cfg4_leg(ctx, scale, world=8):
     w1, k1, _ = timed(ctx, leg1, 5, names)
     w2, k2, _ = timed(ctx, leg2, 5, names)
     w3, k3, g = timed(ctx, leg3, 5, names)
+    # bytes each leg moves through HBM (intermediates included: the exchange's writes and re-reads)
     b1, b2, b3 = 24.0 * n + 16.0 * selected, 32.0 * dn, 16.0 * recv
     kms1 = k1["partition_move"] + k1["filter"]
     kms3 = k3["slice_partition"] + k3["slice_probe"] if k3["slice_partition"] else k3["join_filter_aggregate"]
-    legs = {"exchange_pass_fact": {"ms": kms1, "wall_ms": w1 * 1e3, "alg_bytes": b1, "frac_of_8TBs": b1 / (kms1 * 1e-3) / 1e9 / PEAK},
-            "exchange_pass_dim": {"ms": k2["partition_move"], "wall_ms": w2 * 1e3, "alg_bytes": b2},
-            "local_join": {"ms": kms3, "wall_ms": w3 * 1e3, "alg_bytes": b3, "rows": recv, "groups": g,
+    legs = {"exchange_pass_fact": {"ms": kms1, "wall_ms": w1 * 1e3, "hbm_bytes_moved": b1,
+                                   "moved_GBs": b1 / (kms1 * 1e-3) / 1e9},
+            "exchange_pass_dim": {"ms": k2["partition_move"], "wall_ms": w2 * 1e3, "hbm_bytes_moved": b2},
+            "local_join": {"ms": kms3, "wall_ms": w3 * 1e3, "hbm_bytes_moved": b3, "rows": recv, "groups": g,
                            "build_ms": k3["join_build"], "kernels": "slice" if k3["slice_partition"] else "single pass",
-                           "frac_of_8TBs": b3 / (kms3 * 1e-3) / 1e9 / PEAK}}
+                           "moved_GBs": b3 / (kms3 * 1e-3) / 1e9}}
     kms = kms1 + k2["partition_move"] + kms3
+    # the per-GPU algorithmic bytes of config 4 are the metric's (24 B per fact row
+    # + 16 B per dim row read once, intermediates excluded); the exchange is reported separately
+    alg = 24.0 * n + 16.0 * nd
+    xgmi = (world - 1) / world * (16.0 * selected + 16.0 * dn)
     line(f"cfg4 per-rank device leg at N={world} (1e9 fact rows + 1/{world} dim per rank)", n, w1 + w2 + w3,
-         b1 + b2 + b3, kms, "k_hash_ids8_pred + k_part_scatter (fused filter + 8-way exchange), local fused join",
-         None, {"legs": legs, "selected": selected,
-                "note": "RCCL all-to-all time excluded (8-GPU runs are the driver's); wall = sum of the legs"})
+         alg, kms, "k_hash_ids8_pred + k_part_scatter (fused filter + 8-way exchange), local fused join",
+         None, {"legs": legs, "selected": selected, "exchange_hbm_bytes": b1 + b2 + b3 - 24.0 * n - 16.0 * dn,
+                "xgmi_bytes_per_rank": xgmi,
+                "note": "frac on SURVEY §8(d)'s 24 B / fact row + 16 B / dim row; the exchange's HBM writes and "
+                        "re-reads are in exchange_hbm_bytes, the bytes leaving the rank over xGMI in "
+                        "xgmi_bytes_per_rank; RCCL all-to-all time excluded (8-GPU runs are the driver's); "
+                        "wall = sum of the legs"})
 
 
 def cfg_filter(ctx, scale):

@@ -60,7 +60,7 @@ def main(d):
 PIPELINE = ("k_slice_partition", "k_slice_probe", "k_join_agg_fast", "k_agg_rows<1")
 
 
-def emit(summary, stats, path, rows):
+def emit(summary, stats, path, rows, source):
     """Per-launch HBM bytes and average durations of the probe pipeline's kernels."""
     comp, dur = {}, {}
     for k, v in summary.items():
@@ -71,6 +71,7 @@ def emit(summary, stats, path, rows):
         if any(p in k for p in PIPELINE):
             dur[k] = float(r.get("AverageNs", 0) or 0) / 1e6
     out = {"rows": rows, "kernel": "join_filter_aggregate", "hbm_bytes_per_launch": sum(comp.values()),
+           "source": source,
            "components_hbm_bytes": comp, "components_avg_ms": dur,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, mean per dispatch, summed over the "
                    "pipeline's kernels (one dispatch each per query)"}
@@ -87,4 +88,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     summary, stats = main(a.dir)
     if a.emit:
-        emit(summary, stats, a.emit, a.rows)
+        emit(summary, stats, a.emit, a.rows, "tools/profile.sh run " + os.path.basename(os.path.abspath(a.dir)))
