@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
             const uint64_t pos = run[dg] + (uint64_t)(p - (int)loc[dg]);
             if constexpr (DEC) {
                 const uint64_t c = (uint64_t)key;
-                const bool ok = c != dec.null_code;
+                const bool ok = !dec.validb || c != dec.null_code;  // no NULLs: every code is a value
                 const int64_t x = ok ? (dec.asc ? (int64_t)(c - dec.bias + (uint64_t)dec.mn)
                                                : (int64_t)((uint64_t)dec.mx - (c - dec.bias)))
                                      : 0;
