@@ -267,7 +267,8 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    names = ["join_filter_aggregate", "slice_partition", "slice_probe", "join_build", "filter", "partition_move"]
+    names = ["join_filter_aggregate", "slice_partition", "slice_probe", "join_build", "fused_build", "filter",
+             "partition_move"]
     kt = {nm: ctx.kernel_time(nm) for nm in names}
     ctx.timing(False)
 
@@ -403,7 +404,8 @@ def main():
                 "operator_main_queue_ms": probe_ms / max(probe_launches, 1),
                 "alg_bytes_per_launch": alg_bytes,
             },
-            "build_ms_per_step": kt["join_build"][0] / args.steps,
+            # the build: the dim grouped by slice before phase A (fused pipeline), or the table insert
+            "build_ms_per_step": (kt["join_build"][0] + kt["fused_build"][0]) / args.steps,
             # N > 1 (or QEH_BENCH_FORCE_DIST): how the broadcast join got its table ("table": shard
             # tables summed by all-reduce; "allgather": dim shards all-gathered) and merged its groups
             "dist_build": getattr(dx, "last_build", None) if dx is not None and not cfg4 else None,

@@ -54,6 +54,28 @@ struct FastTile {
 #pragma unroll
             for (int j = 0; j < P; ++j) ac[c][j] = ld2<NT>(in.acol[c] + base + j * 128);
     }
+    // a partial last tile: rows at and past `lim` are not read (8-B loads, zeros in their place);
+    // the caller masks them out of `sel` after eval (tail_mask)
+    __device__ __forceinline__ void issue_tail(const FastIn &in, int64_t base, int64_t lim) {
+        auto ld1 = [&](const int64_t *p, int64_t r) -> int64_t { return r < lim ? p[r] : 0; };
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t r = base + j * 128;
+            key[j][0] = ld1(in.key, r), key[j][1] = ld1(in.key, r + 1);
+#pragma unroll
+            for (int i = 0; i < NTERMS; ++i) tc[i][j][0] = ld1(in.term[i], r), tc[i][j][1] = ld1(in.term[i], r + 1);
+#pragma unroll
+            for (int c = 0; c < NACOL; ++c) ac[c][j][0] = ld1(in.acol[c], r), ac[c][j][1] = ld1(in.acol[c], r + 1);
+        }
+    }
+    // bit r set when row r of the lane (base + (r >> 1) * 128 + (r & 1)) is below `lim`
+    __device__ __forceinline__ static uint32_t tail_mask(int64_t base, int64_t lim) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (base + (r >> 1) * 128 + (r & 1) < lim) m |= 1u << r;
+        return m;
+    }
     // evaluate the term predicate into `sel`
     __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
         sel = (1u << R) - 1u;

@@ -293,6 +293,7 @@ constexpr int kSliceMaxF = 160;                  // slices: key range <= 160 * 6
 constexpr int kSliceBlock = 1024;                // one workgroup per CU in both phases
 constexpr int kSliceTile = kSliceBlock * kFastR;  // 8192 probe rows per phase-A iteration
 constexpr int kSliceChunk = 32;                  // items per flushed chunk
+constexpr int kMaxSliceGrid = 256;               // phase-A workgroups of the fused pipeline (one per CU)
 constexpr int kSliceStateWords = 3584;           // phase-B LDS aggregate states (n_slots * G)
 // Group-range slices (G too large for LDS states): phase A looks the group id up and partitions
 // by gid >> kGidSliceBits; phase B aggregates one range of 2^kGidSliceBits groups in LDS.
@@ -383,6 +384,39 @@ __global__ void k_slice_plan_stats(const int64_t *__restrict__ M, int world, int
     *out = p;
 }
 
+// The fused pipeline's plan (qeh_join_filter_aggregate with one bounded integer group key): the slice
+// shape of the build key's range plus the group key's range -- the join table's entries are group
+// slots (g - gmin + 1) instead of dense group ids, so the build needs no group table first.
+struct FusedPlan {
+    SlicePlan sp;      // sp.ok: every condition of the fused pipeline holds
+    int64_t gmin;      // group slot s <-> group key gmin + s
+    int64_t ngroups;   // gmax - gmin + 1
+    uint64_t dcap;     // build rows per (phase-A workgroup, slice) region, a multiple of 4
+};
+// Phase A's prologue in the fused pipeline: the build rows grouped by slice into per-(workgroup,
+// slice) regions (items = key offset << 16 | group slot + 1), and the output group keys.
+struct FusedPro {
+    const int64_t *dk;     // build key (Int64, no NULLs)
+    ColRef dg;             // group key (Int64 / Int32, no NULLs)
+    int64_t nd;
+    uint32_t *ditems;      // [grid][F][dcap]
+    uint32_t *dcount;      // [grid][F]
+    uint32_t *status;      // [1]: a region overflowed (probe or build rows)
+    void *gkeys;           // output group keys: gmin + i for i < G (Int32 when as32)
+    uint32_t *rep;         // i (the finalize's representative rows)
+    int64_t G;
+    int32_t as32;
+    const FusedPlan *plan;
+};
+// Phase B's view of the build rows (DIM): slice b's rows are items[(r * F + b) * dcap ..] for every
+// phase-A workgroup r, count[r * F + b] of them.
+struct DimSlices {
+    const uint32_t *items;
+    const uint32_t *count;
+    uint32_t *dup;     // set when two build rows share a key
+    const FusedPlan *plan;
+};
+
 // One whole chunk of phase A's flush, planned by the slice's owner thread while the tile is staged:
 // item x of the chunk (x < CH) comes from the carried items (c_key/c_v[coff + x]) when x < clim, else
 // from the staged tile (st_key/st_v[soff + x]); it lands at absolute item g + x when lo <= x < hi
@@ -412,10 +446,65 @@ struct SliceShape {
     static constexpr int TILE = kSliceBlock * 2 * P;
 };
 
-template <int NTERMS, int NACOL, bool NT, int MODE = 0>
+// Phase A's prologue in the fused pipeline (before the first tile's loads): the output group keys,
+// then this workgroup's share of the build rows, each into its slice's region (LDS atomics on dcnt
+// give the positions; no order inside a region is needed).  Not inlined: its registers stay out of
+// the tile loop's allocation.
+__device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int F, int64_t kmin, uint32_t *dcnt) {
+    const int tid = threadIdx.x;
+    const FusedPlan fpl = *fp.plan;
+    for (int i = tid; i < F; i += kSliceBlock) dcnt[i] = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kSliceBlock + tid; i < fp.G; i += (int64_t)gridDim.x * kSliceBlock) {
+        if (fp.as32) ((int32_t *)fp.gkeys)[i] = (int32_t)(fpl.gmin + i);
+        else ((int64_t *)fp.gkeys)[i] = fpl.gmin + i;
+        fp.rep[i] = (uint32_t)i;
+    }
+    __syncthreads();
+    const int64_t chunk = (fp.nd + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * chunk, hi = lo + chunk < fp.nd ? lo + chunk : fp.nd;
+    uint32_t *dreg = fp.ditems + (uint64_t)blockIdx.x * F * fpl.dcap;
+    bool dovf = false;
+    constexpr int DR = 8;
+    for (int64_t i0 = lo + tid; i0 < hi; i0 += DR * kSliceBlock) {
+        int64_t kk[DR], gg[DR];
+#pragma unroll
+        for (int q = 0; q < DR; ++q) {
+            const int64_t i = i0 + (int64_t)q * kSliceBlock;
+            kk[q] = i < hi ? fp.dk[i] : kmin;
+            gg[q] = i < hi ? load_i64(fp.dg, i) : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < DR; ++q) {
+            if (i0 + (int64_t)q * kSliceBlock >= hi) continue;
+            const uint64_t o = (uint64_t)kk[q] - (uint64_t)kmin;
+            const uint32_t b = (uint32_t)(o >> kSliceBits);
+            const uint32_t r = atomicAdd(&dcnt[b], 1u);
+            if (r < fpl.dcap)
+                dreg[(uint64_t)b * fpl.dcap + r] =
+                    ((uint32_t)(o & (kSliceKeys - 1)) << 16) | ((uint32_t)((uint64_t)gg[q] - (uint64_t)fpl.gmin) + 1u);
+            else
+                dovf = true;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < F; i += kSliceBlock) {
+        fp.dcount[(uint64_t)blockIdx.x * F + i] = dcnt[i] < fpl.dcap ? dcnt[i] : (uint32_t)fpl.dcap;
+        dovf |= dcnt[i] > fpl.dcap;
+    }
+    if (dovf) fp.status[1] = 1u;
+}
+
+// EARLY: the next tile's loads are issued right after this tile's rows are ranked (its registers are
+// free from then on), so they stay in flight across the scan, staging and flush phases; it takes every
+// VGPR of the SIMD (nothing else fits beside phase A), so only the fused pipeline, whose build runs
+// before phase A, uses it (the prelaunched phase A of the other paths keeps room for the build).
+// tail_rows > 0: one more, partial tile of that many rows after the n_tiles full ones (fused pipeline;
+// the other paths run their ragged tail through the generic kernel).
+template <int NTERMS, int NACOL, bool NT, int MODE = 0, bool EARLY = false>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
                                                                  int64_t n_tiles, SliceRegions rg, HashTable t,
-                                                                 const SlicePlan *__restrict__ dplan = nullptr) {
+                                                                 const SlicePlan *__restrict__ dplan = nullptr,
+                                                                 int64_t tail_rows = 0, FusedPro fp = FusedPro{}) {
     constexpr int P = SliceShape<NACOL>::P, R = 2 * P, TILE = SliceShape<NACOL>::TILE, CH = SliceShape<NACOL>::CH;
     constexpr int MAXF = kSliceMaxF;
     if (dplan) {  // planned on the device: the shape comes from the build key's range in memory
@@ -521,13 +610,25 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     int par = 0;
     uint32_t m_prev = 0;
     bool have_prev = false;
-    if (tile < n_tiles) ft.issue(in, tile * TILE + (int64_t)wave * (64 * R) + 2 * lane);
-    for (; tile < n_tiles; tile += gridDim.x) {
+    // the partial last tile only in the fused pipeline (EARLY): the other paths keep their registers
+    const int64_t n_all = n_tiles + (EARLY && tail_rows > 0 ? 1 : 0), lim = n_tiles * TILE + tail_rows;
+    auto issue_tile = [&](int64_t tl) {
+        const int64_t b = tl * TILE + (int64_t)wave * (64 * R) + 2 * lane;
+        if (!EARLY || tl < n_tiles) ft.issue(in, b);
+        else ft.issue_tail(in, b, lim);
+    };
+    if constexpr (EARLY) {
+        __shared__ uint32_t dcnt[MAXF];
+        fused_prologue(fp, F, kmin, dcnt);
+    }
+    if (tile < n_all) issue_tile(tile);
+    for (; tile < n_all; tile += gridDim.x) {
         uint32_t *cnt = cntb[par], *cn = cnb[par], *pos = posb[par], *lofs = lofsb[par];
         const int pq = par ^ 1;
         if (have_prev) flush(m_prev);
         ft.eval(in, terms);
         uint32_t sel = ft.sel, off[R], rk[R];
+        if (EARLY && tile >= n_tiles) sel &= decltype(ft)::tail_mask(tile * TILE + (int64_t)wave * (64 * R) + 2 * lane, lim);
         if constexpr (MODE == 1) {
             // all probes first (independent loads in flight), then the LDS ranks
 #pragma unroll
@@ -555,9 +656,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         for (int u = 0; u < VS; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) vcur[u][r] = VC ? ft.a(u, r) : 0;
-#ifdef QEH_EXP_EARLY_ISSUE
-        if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
-#endif
+        if (EARLY && tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
         lds_barrier();  // B1: counts complete, tile t-1 flushed
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged
@@ -620,9 +719,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             cnb[pq][tid] = T % CH;
             cntb[pq][tid] = 0;
         }
-#ifndef QEH_EXP_EARLY_ISSUE
-        if (tile + gridDim.x < n_tiles) ft.issue(in, (tile + gridDim.x) * TILE + (int64_t)wave * (64 * R) + 2 * lane);
-#endif
+        if (!EARLY && tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
         lds_barrier();  // B3: staged, chunks planned
         m_prev = s_chunks;
         have_prev = true;
@@ -697,13 +794,25 @@ __device__ __forceinline__ void slice_states_init(uint64_t *lst, int64_t stride,
 // PF: the next 512 items of a region are loaded while this chunk is looked up and aggregated.
 // PV: items loaded two per lane (a 4-B key pair and a 16-B value pair per load; 128 items per wave
 // load instead of 64) -- half the load instructions for the same bytes.
-template <int NACOL, bool IDENT = false, bool PF = false, bool PV = false>
+// DIM (fused pipeline): there is no join table in memory; slice b's entries are built in LDS from the
+// build rows phase A's prologue grouped by slice (entry = group slot + 1 at the key offset), with a
+// duplicate build key flagged in *dim.dup, and the shape (F, cap) comes from the device plan.
+template <int NACOL, bool IDENT = false, bool PF = false, bool PV = false, bool DIM = false>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, int nreg, int splits, HashTable t, FastIn in,
-                                                             AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all) {
+                                                             AggSpecs specs, int64_t G, uint64_t *__restrict__ gstates_all,
+                                                             DimSlices dim = DimSlices{}) {
     constexpr int VC = NACOL > 0 ? 1 : 0;
     __shared__ __attribute__((aligned(16))) uint16_t tslice[IDENT ? 8 : kSliceKeys];
     __shared__ uint64_t lst[IDENT ? kGidStateWords : kSliceStateWords];
+    __shared__ uint32_t rcnt[DIM ? kMaxSliceGrid : 1];  // DIM: the build-row counts of the slice's regions
     uint32_t *lcnt = (uint32_t *)lst;
+    uint64_t dcap = 0;
+    if constexpr (DIM) {
+        const FusedPlan pl = *dim.plan;
+        if (!pl.sp.ok) return;
+        rg.F = pl.sp.F, rg.cap = pl.sp.cap;
+        dcap = pl.dcap;
+    }
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int W = kSliceBlock / 64;
@@ -738,7 +847,51 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             }
             cur_b = b;
         }
-        if (!IDENT && b != cur_b) {
+        if (DIM && b != cur_b) {
+            cur_b = b;
+            uint32_t *tw = (uint32_t *)tslice;
+            for (int i = tid; i < kSliceKeys / 2; i += kSliceBlock) tw[i] = 0u;
+            for (int r = tid; r < nreg; r += kSliceBlock) rcnt[r] = dim.count[(uint64_t)r * F + b];
+            __syncthreads();
+            // slice b's build rows: every wave takes 8 regions at a time, lane j their items 4j..4j+3
+            uint32_t dup = 0;
+            for (int r0 = wave * 8; r0 < nreg; r0 += W * 8) {
+                v4u32 w[8];
+                uint32_t cq[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int r = r0 + q;
+                    cq[q] = r < nreg ? rcnt[r] : 0u;
+                    w[q] = (uint32_t)lane * 4 < cq[q] ? *(const v4u32 *)(dim.items + ((uint64_t)r * F + b) * dcap + lane * 4)
+                                                      : v4u32{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if ((uint32_t)lane * 4 + e >= cq[q]) break;  // past the region's rows
+                        const uint32_t it = w[q][e];
+                        const uint32_t off = it >> 16, sh = (off & 1u) * 16u;
+                        dup |= (atomicOr(&tw[off >> 1], (it & 0xFFFFu) << sh) >> sh) & 0xFFFFu;
+                    }
+                // regions with more than 256 rows (build keys crowded into one slice)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int r = r0 + q;
+                    const uint32_t c = r < nreg ? rcnt[r] : 0u;
+                    for (uint32_t i = 256 + (uint32_t)lane * 4; i < c; i += 256) {
+                        const v4u32 x = *(const v4u32 *)(dim.items + ((uint64_t)r * F + b) * dcap + i);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            if (i + e >= c) break;
+                            const uint32_t off = x[e] >> 16, sh = (off & 1u) * 16u;
+                            dup |= (atomicOr(&tw[off >> 1], (x[e] & 0xFFFFu) << sh) >> sh) & 0xFFFFu;
+                        }
+                    }
+                }
+            }
+            if (dup) *dim.dup = 1u;
+        } else if (!DIM && !IDENT && b != cur_b) {
             cur_b = b;
             const uint64_t k0 = (uint64_t)b << kSliceBits;
             const uint64_t nk = t.range - k0 < (uint64_t)kSliceKeys ? t.range - k0 : (uint64_t)kSliceKeys;
@@ -856,6 +1009,28 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     } else {
         slice_states_flush(lst, stride, 0, G, specs, G, gstates);
     }
+}
+
+// ---- fused pipeline: the plan -----------------------------------------------------------------
+// The build rows (key, group key) take the probe rows' route: phase A's prologue groups them by slice
+// (4-B items), and phase B builds each slice's entries in LDS from them instead of loading a join table
+// from HBM.  No table is written, there are no scattered 2-B stores (the XCD-split insert read every
+// key 8 times, 1.2 GB per query), and nothing of the build runs beside phase A.
+// mm[0] = build key, mm[1] = group key ranges; nd = build rows (no NULLs allowed); dim_items = the
+// build-row region buffer's size in items; st = the status words (zeroed here, [5] = the verdict).
+__global__ void k_fused_plan(const MinMax *__restrict__ mm, SlicePlanIn pi, int64_t g_cap, int64_t nd, uint64_t dim_items,
+                             FusedPlan *out, uint32_t *__restrict__ st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    FusedPlan p{};
+    p.sp = plan_slices(pi, mm[0].mn, mm[0].mx, (int64_t)mm[0].cnt, mm[1].mn, mm[1].mx, (int64_t)mm[1].cnt);
+    const bool full = (int64_t)mm[0].cnt == nd && (int64_t)mm[1].cnt == nd && !mm[0].bad && !mm[1].bad;
+    p.gmin = mm[1].mn;
+    p.ngroups = full ? (int64_t)((uint64_t)mm[1].mx - (uint64_t)mm[1].mn + 1ull) : 0;
+    p.dcap = p.sp.F > 0 ? dim_items / ((uint64_t)pi.grid * p.sp.F) / 4 * 4 : 0;
+    p.sp.ok = p.sp.ok && full && p.ngroups >= 1 && p.ngroups <= g_cap && p.ngroups < 0xFFFF && p.dcap >= 4;
+    *out = p;
+    for (int i = 0; i < 8; ++i) st[i] = 0u;
+    st[5] = p.sp.ok ? 1u : 0u;
 }
 
 // ---- LDS-slice materialising INNER join (BASELINE config 3) -----------------------------
@@ -3268,6 +3443,211 @@ extern "C" int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_col
                                        0, n_groups, QEH_DT_INT64, aggs, n_aggs, nullptr, nullptr, &g, lanes);
 }
 
+// ---- the fused pipeline (one bounded integer group key, unique Int64 build keys) ----------------
+// Everything on the main queue, one host round trip per query (the status words after the finalize):
+//   build key / group key min-max -> k_fused_plan (slice shape, group slots, status words zeroed)
+//   -> states zeroed -> phase A (prologue: output group keys and the build rows grouped by slice into
+//   per-(workgroup, slice) regions, 4 B each; then the probe rows with EARLY loads and the ragged tail
+//   as a partial last tile) -> phase B (each slice's entries built in LDS from its build rows,
+//   duplicate keys flagged) -> fold / compact / finalize.
+// Returns kFusedNotEligible when the shape does not qualify (checked on the host) or the device plan,
+// a region overflow or a duplicate build key rejected the run (outputs released): the caller runs
+// the general path.
+constexpr int kFusedNotEligible = -4;
+
+static void launch_slice_partition_early(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol,
+                                         int64_t n_tiles, int64_t tail_rows, int grid, const SliceRegions &rg,
+                                         const SlicePlan *dplan, const FusedPro &fp) {
+    const bool nt = fast_nt_mode() == 1;
+    KernelTimer kta(ctx, "slice_partition");
+    const HashTable t{};
+#define QEH_SE(NTV, NAV, NTB)                                                                                            \
+    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,  \
+                       pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
+#define QEH_SE_NA(NTV, NTB)                 \
+    if (nacol == 0) { QEH_SE(NTV, 0, NTB); } \
+    else { QEH_SE(NTV, 1, NTB); }
+#define QEH_SE_NT(NTB)                         \
+    if (nterms == 0) { QEH_SE_NA(0, NTB) }     \
+    else if (nterms == 1) { QEH_SE_NA(1, NTB) } \
+    else { QEH_SE_NA(2, NTB) }
+    if (nt) { QEH_SE_NT(true) } else { QEH_SE_NT(false) }
+#undef QEH_SE_NT
+#undef QEH_SE_NA
+#undef QEH_SE
+}
+
+static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp,
+                                       const AggSpecs &specs_in, int key_col, const qeh_column &bk, const qeh_column &gk,
+                                       qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups) {
+    if (std::getenv("QEH_NO_FUSED") || std::getenv("QEH_NO_SLICES")) return kFusedNotEligible;
+    const bool bk_nulls = bk.validity && bk.null_count != 0, gk_nulls = gk.validity && gk.null_count != 0;
+    if (bk.dtype != QEH_DT_INT64 || bk_nulls || (gk.dtype != QEH_DT_INT64 && gk.dtype != QEH_DT_INT32) || gk_nulls)
+        return kFusedNotEligible;
+    const int64_t nd = bk.length;
+    if (nd <= 0 || nd >= ((int64_t)1 << 32) || gk.length != nd) return kFusedNotEligible;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 1) return kFusedNotEligible;
+    const int64_t n_tiles = n / kSliceTile, tail = n - n_tiles * kSliceTile;
+    if (n_tiles == 0) return kFusedNotEligible;
+    AggSpecs specs = specs_in;
+    const int64_t g_cap = std::min<int64_t>(kSliceStateWords / std::max(specs.n_slots, 1), 0xFFFE);
+    const int64_t Gs = g_cap;  // states and outputs for every possible slot; empty slots are dropped
+    specs.shards = 1;
+    while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
+    if (std::getenv("QEH_NO_SHARDS")) specs.shards = 1;
+    const int64_t n_all = n_tiles + (tail ? 1 : 0);
+    const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all, (int64_t)kMaxSliceGrid});
+    const uint64_t tiles_per_wg = (uint64_t)((n_all + grid - 1) / grid);
+
+    DevBuf mm, plan, ditems, dcount, kbuf, vbuf, cbuf, states, errw, gkeys, rep, pos;
+    SlicePlanIn pi{};
+    pi.min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
+    pi.grid = grid;
+    pi.n_slots = specs.n_slots;
+    pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
+    pi.alloc_items = tiles_per_wg * grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)grid * kSliceMaxF * 288;
+    // build rows: uniform keys over the slices, +25 %, and per-region slack
+    const uint64_t dim_items = (uint64_t)nd * 5 / 4 + (uint64_t)grid * kSliceMaxF * 64;
+    const uint64_t nreg_max = (uint64_t)grid * kSliceMaxF;
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 + 16));
+    QEH_TRY(plan.alloc(ctx, sizeof(FusedPlan)));
+    QEH_TRY(ditems.alloc(ctx, dim_items * 4 + 64));
+    QEH_TRY(dcount.alloc(ctx, nreg_max * 4 + 64));
+    QEH_TRY(kbuf.alloc(ctx, pi.alloc_items * 2 + 64));
+    if (nacol) QEH_TRY(vbuf.alloc(ctx, pi.alloc_items * 8 + 64));
+    QEH_TRY(cbuf.alloc(ctx, nreg_max * 4 + 64));
+    QEH_TRY(states.alloc(ctx, (size_t)specs.shards * specs.n_slots * Gs * 8));
+    // status words (zeroed by k_fused_plan): [0] kernel error bits, [1] region overflow, [2..3] groups,
+    // [4] duplicate build key, [5] the device plan's verdict
+    QEH_TRY(errw.alloc(ctx, 32));
+    QEH_TRY(gkeys.alloc(ctx, (size_t)Gs * 8));
+    QEH_TRY(rep.alloc(ctx, (size_t)Gs * 4));
+    QEH_TRY(pos.alloc(ctx, (size_t)Gs * 8));
+    uint32_t *st = errw.as<uint32_t>();
+    SliceRegions rg{};
+    rg.key = kbuf.as<uint16_t>();
+    rg.val = nacol ? vbuf.as<int64_t>() : nullptr;
+    rg.count = cbuf.as<uint32_t>();
+    rg.overflow = st + 1;
+    FusedPlan *dplan = plan.as<FusedPlan>();
+    {
+        KernelTimer kt(ctx, "fused_build");
+        const qeh_column both[2] = {bk, gk};
+        QEH_TRY(columns_minmax_launch(ctx, both, 2, mm.as<MinMax>()));
+        hipLaunchKernelGGL(k_fused_plan, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), pi, g_cap, nd, dim_items, dplan, st);
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock), 0,
+                           ctx->stream, states.as<uint64_t>(), Gs, specs);
+    }
+    QEH_HIP(hipGetLastError());
+    FusedPro fp{};
+    fp.dk = (const int64_t *)bk.values + bk.offset;
+    fp.dg = make_colref(gk);
+    fp.nd = nd;
+    fp.ditems = ditems.as<uint32_t>();
+    fp.dcount = dcount.as<uint32_t>();
+    fp.status = st;
+    fp.gkeys = gkeys.p;
+    fp.rep = rep.as<uint32_t>();
+    fp.G = Gs;
+    fp.as32 = gk.dtype == QEH_DT_INT32 ? 1 : 0;
+    fp.plan = dplan;
+    launch_slice_partition_early(ctx, in, pp, nterms, nacol, n_tiles, tail, grid, rg, &dplan->sp, fp);
+    {
+        KernelTimer ktb(ctx, "slice_probe");
+        DimSlices dim{ditems.as<uint32_t>(), dcount.as<uint32_t>(), st + 4, dplan};
+        const bool pf = slice_probe_prefetch();
+        const int gridB = ctx->props.multiProcessorCount;
+        const HashTable t{};
+#define QEH_SD(NAV, PFV)                                                                                                   \
+    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, \
+                       grid, 0, t, in, specs, Gs, states.as<uint64_t>(), dim)
+        if (nacol == 0) {
+            if (pf) QEH_SD(0, true);
+            else QEH_SD(0, false);
+        } else {
+            if (pf) QEH_SD(1, true);
+            else QEH_SD(1, false);
+        }
+#undef QEH_SD
+    }
+    QEH_HIP(hipGetLastError());
+    // fold the shard copies, flag / scan the non-empty slots (the group count into st[2..3]), finalize
+    {
+        AggSpecs cs = specs;
+        if (specs.shards > 1) {
+            const int64_t words = (int64_t)specs.n_slots * Gs;
+            hipLaunchKernelGGL(k_states_fold, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, ctx->stream,
+                               states.as<uint64_t>(), Gs, specs);
+            cs.shards = 1;
+        }
+        hipLaunchKernelGGL(k_states_compact_small, dim3(1), dim3(1024), 0, ctx->stream, states.as<uint64_t>(), Gs, Gs, cs,
+                           pos.as<uint64_t>(), (uint64_t *)(st + 2));
+        specs.shards = cs.shards;
+    }
+    QEH_HIP(hipGetLastError());
+    qeh_column kc{};
+    kc.dtype = gk.dtype;
+    kc.length = Gs;
+    kc.values = gkeys.p;
+    KeyCols keys{};
+    keys.n = 1;
+    keys.c[0] = make_colref(kc);
+    OutCols oc{};
+    int made = 0;
+    auto cleanup = [&]() {
+        for (int i = 0; i < made; ++i) qeh_column_release(ctx, i == 0 ? &out_keys[0] : &out_aggs[i - 1]);
+        made = 0;
+    };
+    for (int i = 0; i < 1 + specs.n; ++i) {
+        qeh_column *c = i == 0 ? &out_keys[0] : &out_aggs[i - 1];
+        int dt;
+        bool nullable;
+        if (i == 0) {
+            dt = gk.dtype;
+            nullable = false;
+        } else {
+            const AggSpec &sp = specs.a[i - 1];
+            dt = agg_output_type(sp.func, sp.in_type);
+            nullable = sp.func != QEH_AGG_COUNT;
+        }
+        const int s = alloc_column(ctx, dt, Gs, nullable, c);
+        if (s != QEH_OK) {
+            cleanup();
+            return s;
+        }
+        ++made;
+        if (nullable) QEH_HIP(hipMemsetAsync(c->validity, 0, ((Gs + 63) / 64) * 8, ctx->stream));
+        oc.c[i].values = c->values;
+        oc.c[i].validity = (uint32_t *)c->validity;
+        oc.c[i].dtype = dt;
+    }
+    {
+        KernelTimer kt(ctx, "aggregate_finalize");
+        hipLaunchKernelGGL(k_finalize, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream, states.as<uint64_t>(),
+                           Gs, pos.as<uint64_t>(), keys, rep.as<uint32_t>(), specs, oc);
+    }
+    uint32_t sw[8];
+    int s = hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "fused join-aggregate: launch failed");
+    if (s == QEH_OK) s = read_small(ctx, sw, errw.p, 32);  // the one host round trip of the query
+    if (s == QEH_OK && !sw[0] && (!sw[5] || sw[1] || sw[4])) s = kFusedNotEligible;  // plan, overflow, duplicates
+    if (s == QEH_OK) s = kernel_error_status(sw[0], "aggregate");
+    if (s != QEH_OK) {
+        cleanup();
+        return s;
+    }
+    const int64_t out_n = (int64_t)((uint64_t)sw[2] | ((uint64_t)sw[3] << 32));
+    for (int i = 0; i < 1 + specs.n; ++i) {
+        qeh_column *c = i == 0 ? &out_keys[0] : &out_aggs[i - 1];
+        c->length = out_n;
+        c->null_count = c->validity ? -1 : 0;
+    }
+    *out_groups = out_n;
+    return QEH_OK;
+}
+
 extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
                                          int probe_key_idx, const qeh_expr *predicate, const qeh_column *build_key,
                                          const qeh_column *build_group_keys, int n_group_keys, const qeh_agg *aggs,
@@ -3318,8 +3698,12 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
         }
     }
     pend.reset();  // not adopted: waits for its phase A, frees its regions
-    if (!pre.launched && n_group_keys == 1)
+    if (!pre.launched && n_group_keys == 1) {
+        const int fs = fused_join_filter_aggregate(ctx, cols, n, pp, specs, probe_key_idx, *build_key, build_group_keys[0],
+                                                   out_keys, out_aggs, out_groups);
+        if (fs != kFusedNotEligible) return fs;
         QEH_TRY(slice_prelaunch(ctx, cols, n, pp, specs, probe_key_idx, *build_key, build_group_keys[0], &pre));
+    }
     // build side: dense group ids of the build rows, then the join table with gid payloads
     GroupTable gt;
     DevBuf slot_of_row;

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r4a; mkdir -p $O
 timeout -k 10 120 tools/ubench/floor_ubench 1000000000 5 > $O/floor.txt 2>&1 || { echo floor failed; cat $O/floor.txt; exit 1; }
 cat $O/floor.txt
-timeout -k 10 400 python3 tools/r3/exp_slice.py --rounds 3 libqeh.so libqeh_exp1.so > $O/early.txt 2>&1 || { echo ab failed; cat $O/early.txt; exit 1; }
+timeout -k 10 400 python3 tools/exp_slice.py --rounds 3 libqeh.so libqeh_exp1.so > $O/early.txt 2>&1 || { echo ab failed; cat $O/early.txt; exit 1; }
 cat $O/early.txt
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_lds_rank.py \
     tests/test_merge.py "tests/test_pipeline.py::test_config2_full_size_vs_oracle" \

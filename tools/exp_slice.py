@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Phase A / phase B kernel times of the metric query (1e9 x 1e7) for several builds of the library,
 alternating builds in rounds (results are not checked: experiment builds may compute garbage).
-usage: python tools/r3/exp_slice.py [--rows N] [--steps K] [--rounds R] lib1.so[:ENV=V,ENV2=V2] ..."""
+usage: python tools/exp_slice.py [--rows N] [--steps K] [--rounds R] lib1.so[:ENV=V,ENV2=V2] ..."""
 import argparse
 import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r'''
 import os, sys, time, json
