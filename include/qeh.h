@@ -298,6 +298,9 @@ int qeh_join_filter_aggregate_prelaunch_stats(qeh_ctx *ctx, const qeh_column *pr
 int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
                                   int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table);
 int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out);
+/* The same count into device memory (*dev_out, 8 B, overwritten), no host wait: the distributed step
+ * reads it with its final results instead of stalling the queue between the table sum and the probe. */
+int qeh_u16_count_nonzero_dev(qeh_ctx *ctx, const uint16_t *table, uint64_t n, uint64_t *dev_out);
 /* [min, max, non-null count] of each Int32 / Int64 column (out[3 i .. 3 i + 2]; an all-NULL or empty
  * column gives min > max), one synchronous read for all of them -- the job-wide build ranges of a
  * distributed broadcast join are gathered from these. */
@@ -329,6 +332,14 @@ int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_column *probe_
                                           int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
                                           int64_t key_min, uint64_t key_range, int64_t n_groups, const qeh_agg *aggs,
                                           int n_aggs, double *lanes);
+/* ..._lanes without a host wait: the operator's status words go to dev_status[0..3] (device memory;
+ * [0] kernel error bits, [1] a slice region overflowed -- then the lanes are incomplete) and the call
+ * returns as soon as its kernels are queued; the caller reads the words with its final results and,
+ * when either is set, runs qeh_join_filter_aggregate_table_lanes (which recovers) instead. */
+int qeh_join_filter_aggregate_table_lanes_async(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                                int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
+                                                int64_t key_min, uint64_t key_range, int64_t n_groups,
+                                                const qeh_agg *aggs, int n_aggs, double *lanes, uint32_t *dev_status);
 /* This dimension shard's broadcast-join statistics into device memory, no host wait:
  * dev_out[0..4] = [rows, build key min, max, group key min, max] (min > max for an empty or all-NULL
  * shard), dev_out[5 + i] = extra[i] (n_extra <= 16: flags the caller gathers with them).  The ranks

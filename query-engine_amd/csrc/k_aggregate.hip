@@ -337,6 +337,7 @@ struct SlicePlanIn {
     int32_t grid;
     int32_t n_slots;
     int32_t sparse_ok;     // direct_table_ok's sparse rule enabled
+    int32_t chunk;         // items per flushed chunk (regions are whole chunks); 0 = kSliceChunk
 };
 __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t kmn, int64_t kmx, int64_t kcnt, int64_t gmn,
                                                  int64_t gmx, int64_t gcnt) {
@@ -356,8 +357,9 @@ __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t 
     p.kmin = kmn;
     p.range = range;
     p.F = (int32_t)F;
-    p.cap = pi.alloc_items / ((uint64_t)pi.grid * F) / kSliceChunk * kSliceChunk;
-    p.ok = p.cap >= (uint64_t)kSliceChunk;
+    const uint64_t ch = pi.chunk > 0 ? (uint64_t)pi.chunk : (uint64_t)kSliceChunk;
+    p.cap = pi.alloc_items / ((uint64_t)pi.grid * F) / ch * ch;
+    p.ok = p.cap >= ch;
     return p;
 }
 // mm[0] = build key, mm[1] = group key ranges
@@ -424,7 +426,7 @@ struct DimSlices {
 struct __attribute__((aligned(16))) SliceChunk {
     uint64_t g;
     int32_t soff;
-    uint32_t pk;  // coff (13 bits) | clim << 13 | lo << 19 | hi << 25  (6 bits each)
+    uint32_t pk;  // slice (8 bits; its carries start at slice * CH) | clim << 8 | lo << 15 | hi << 22 (7 bits each)
 };
 
 // MODE 0: slices of the join key's offset (k - kmin) >> kSliceBits, items = 16-bit key offsets.
@@ -439,10 +441,19 @@ struct __attribute__((aligned(16))) SliceChunk {
 //   [flush(t-1); eval + rank(t)] B1 [scan(t) | carry(t-1)] B2 [stage(t), plan chunks(t), issue(t+1)] B3
 // NACOL = 2 (two aggregate columns, 18-B items) stages half tiles (P = 2 pairs per lane, 4096 rows)
 // and flushes 16-item chunks, so staging and carries fit one CU's LDS.
-template <int NACOL>
+// EARLY (the fused pipeline) may take its own tile and chunk (QEH_EARLY_PAIRS / QEH_EARLY_CHUNK at
+// build time): 64-item chunks (128 B of keys + 512 B of values, whole lines) with 4096-row tiles keep
+// the carries and the staging in one CU's LDS.
+#ifndef QEH_EARLY_PAIRS
+#define QEH_EARLY_PAIRS kFastPairs
+#endif
+#ifndef QEH_EARLY_CHUNK
+#define QEH_EARLY_CHUNK kSliceChunk
+#endif
+template <int NACOL, bool EARLY = false>
 struct SliceShape {
-    static constexpr int P = NACOL > 1 ? 2 : kFastPairs;
-    static constexpr int CH = NACOL > 1 ? 16 : kSliceChunk;
+    static constexpr int P = NACOL > 1 ? 2 : (EARLY ? QEH_EARLY_PAIRS : kFastPairs);
+    static constexpr int CH = NACOL > 1 ? 16 : (EARLY ? QEH_EARLY_CHUNK : kSliceChunk);
     static constexpr int TILE = kSliceBlock * 2 * P;
 };
 
@@ -505,7 +516,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                                                                  int64_t n_tiles, SliceRegions rg, HashTable t,
                                                                  const SlicePlan *__restrict__ dplan = nullptr,
                                                                  int64_t tail_rows = 0, FusedPro fp = FusedPro{}) {
-    constexpr int P = SliceShape<NACOL>::P, R = 2 * P, TILE = SliceShape<NACOL>::TILE, CH = SliceShape<NACOL>::CH;
+    using Shape = SliceShape<NACOL, EARLY>;
+    constexpr int P = Shape::P, R = 2 * P, TILE = Shape::TILE, CH = Shape::CH;
     constexpr int MAXF = kSliceMaxF;
     if (dplan) {  // planned on the device: the shape comes from the build key's range in memory
         const SlicePlan pl = *dplan;
@@ -524,6 +536,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     __shared__ int64_t st_v[VS][VC ? TILE : 1];
     __shared__ uint16_t c_key[MAXF * CH];
     __shared__ int64_t c_v[VS][VC ? MAXF * CH : 1];
+    __shared__ uint8_t st_b[EARLY ? TILE : 1];  // EARLY: slice of each staged item (the per-item carry)
     int64_t *const vout[2] = {rg.val, rg.val2};
     const int F = rg.F;
     const uint64_t cap = rg.cap;
@@ -550,7 +563,8 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         const uint32_t xl = (tid & (CH / 2 - 1)) * 2;
         for (uint32_t c = tid / (CH / 2); c < M; c += kSliceBlock / (CH / 2)) {
             const SliceChunk d = cdesc[c];
-            const uint32_t coff = d.pk & 8191u, clim = (d.pk >> 13) & 63u, lo = (d.pk >> 19) & 63u, hi = d.pk >> 25;
+            const uint32_t coff = (d.pk & 255u) * CH, clim = (d.pk >> 8) & 127u, lo = (d.pk >> 15) & 127u,
+                           hi = (d.pk >> 22) & 127u;
             uint16_t kv[2];
             int64_t vv[VS][2] = {};
 #pragma unroll
@@ -589,6 +603,25 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     // carries after tile t-1 from the carries before it (cn_o), its counts (cnt_o) and offsets
     // (lofs_o): appended when no whole chunk left, else the tile's last T % CH items
     auto carry = [&](const uint32_t *cn_o, const uint32_t *cnt_o, const uint32_t *lofs_o, int p0, int stride) {
+        if constexpr (EARLY) {
+            // one pass over the staged items (the tile's selected rows) instead of every (slice, slot):
+            // item j of slice b's segment is carried when no whole chunk was left (appended after the
+            // cb carried before) or when it is among the segment's last T % CH items
+            const uint32_t total = lofs_o[F - 1] + cnt_o[F - 1];
+            for (uint32_t si = (uint32_t)p0; si < total; si += (uint32_t)stride) {
+                const int b = st_b[si];
+                const uint32_t cb = cn_o[b], nb = cnt_o[b], T = cb + nb, L = T % CH, j = si - lofs_o[b];
+                int dst = -1;
+                if (T < CH) dst = (int)(cb + j);
+                else if (j >= nb - L) dst = (int)(j - (nb - L));
+                if (dst >= 0) {
+                    c_key[b * CH + dst] = st_key[si];
+#pragma unroll
+                    for (int u = 0; u < VC; ++u) c_v[u][b * CH + dst] = st_v[u][si];
+                }
+            }
+            return;
+        }
         for (int p = p0; p < F * CH; p += stride) {
             const int b = p / CH, kx = p % CH;
             const uint32_t cb = cn_o[b], nb = cnt_o[b], T = cb + nb, L = T % CH;
@@ -694,6 +727,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             if (!((sel >> r) & 1)) continue;
             const uint32_t s = lofs[off[r] >> SB] + rk[r];
             st_key[s] = (uint16_t)(off[r] & ((1u << SB) - 1u));
+            if constexpr (EARLY) st_b[s] = (uint8_t)(off[r] >> SB);
 #pragma unroll
             for (int u = 0; u < VC; ++u) st_v[u][s] = vcur[u][r];
         }
@@ -712,7 +746,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
                 SliceChunk d;
                 d.g = gb + (uint64_t)j * CH;
                 d.soff = (int32_t)lo0 + (int32_t)(j * CH) - (int32_t)cb;
-                d.pk = (uint32_t)(tid * CH) | (clim << 13) | (lo << 19) | (hi << 25);
+                d.pk = (uint32_t)tid | (clim << 8) | (lo << 15) | (hi << 22);
                 cdesc[m0 + j] = d;
             }
             posb[pq][tid] = (uint32_t)(p0 + (uint64_t)m * CH);
@@ -1018,9 +1052,59 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
 // key 8 times, 1.2 GB per query), and nothing of the build runs beside phase A.
 // mm[0] = build key, mm[1] = group key ranges; nd = build rows (no NULLs allowed); dim_items = the
 // build-row region buffer's size in items; st = the status words (zeroed here, [5] = the verdict).
-__global__ void k_fused_plan(const MinMax *__restrict__ mm, SlicePlanIn pi, int64_t g_cap, int64_t nd, uint64_t dim_items,
-                             FusedPlan *out, uint32_t *__restrict__ st) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One launch ahead of phase A: workgroup 0 reduces the build key / group key partial min / max
+// (part[c * nb + w], c = 0 key, 1 group key) and writes the plan and the zeroed status words; every
+// workgroup initialises its share of the aggregate states.
+__global__ __launch_bounds__(1024) void k_fused_plan(const MinMax *__restrict__ part, int nb, SlicePlanIn pi, int64_t g_cap,
+                                                     int64_t nd, uint64_t dim_items, FusedPlan *out, uint32_t *__restrict__ st,
+                                                     uint64_t *__restrict__ states, int64_t G, AggSpecs specs) {
+    const int64_t words = (int64_t)specs.shards * specs.n_slots * G;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t slot = (i / G) % specs.n_slots;
+        uint64_t v = 0;
+        for (int a = 0; a < specs.n; ++a)
+            if (specs.a[a].val_slot == slot) v = (uint64_t)agg_init_value(specs.a[a].kind);
+        states[i] = v;
+    }
+    if (blockIdx.x != 0) return;
+    __shared__ MinMax sm[2][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int c = 0; c < 2; ++c) {
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        uint64_t cnt = 0;
+        uint32_t bad = 0;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+            const MinMax q = part[(int64_t)c * nb + i];
+            mn = q.mn < mn ? q.mn : mn;
+            mx = q.mx > mx ? q.mx : mx;
+            cnt += q.cnt;
+            bad |= q.bad;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const int64_t a = __shfl_xor(mn, d, 64), b2 = __shfl_xor(mx, d, 64);
+            const uint64_t cc = __shfl_xor(cnt, d, 64);
+            const uint32_t bb = __shfl_xor(bad, d, 64);
+            mn = a < mn ? a : mn;
+            mx = b2 > mx ? b2 : mx;
+            cnt += cc;
+            bad |= bb;
+        }
+        if (lane == 0) sm[c][wave] = MinMax{mn, mx, cnt, bad};
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    MinMax mm[2];
+    for (int c = 0; c < 2; ++c) {
+        mm[c] = sm[c][0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            const MinMax q = sm[c][w];
+            mm[c].mn = q.mn < mm[c].mn ? q.mn : mm[c].mn;
+            mm[c].mx = q.mx > mm[c].mx ? q.mx : mm[c].mx;
+            mm[c].cnt += q.cnt;
+            mm[c].bad |= q.bad;
+        }
+    }
     FusedPlan p{};
     p.sp = plan_slices(pi, mm[0].mn, mm[0].mx, (int64_t)mm[0].cnt, mm[1].mn, mm[1].mx, (int64_t)mm[1].cnt);
     const bool full = (int64_t)mm[0].cnt == nd && (int64_t)mm[1].cnt == nd && !mm[0].bad && !mm[1].bad;
@@ -1714,6 +1798,76 @@ __global__ void k_finalize(const uint64_t *__restrict__ states, int64_t G, const
             }
         }
     }
+}
+
+// After phase B (shard copies folded): one workgroup compacts the non-empty group slots, writes the
+// output keys, aggregates and validity words (zeroed here first) and the group count (*total).
+__global__ __launch_bounds__(1024) void k_fused_finish(const uint64_t *__restrict__ states, int64_t G, KeyCols keys,
+                                                       const uint32_t *__restrict__ rep, AggSpecs specs, OutCols outs,
+                                                       uint64_t *__restrict__ total) {
+    __shared__ uint32_t pos[kSliceStateWords];
+    __shared__ uint32_t vbits[kMaxGroupKeys + kMaxAggs][kSliceStateWords / 32];  // validity, built in LDS
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int nout = keys.n + specs.n;
+    const int64_t vwords = (G + 31) / 32;
+    for (int c = 0; c < nout; ++c)
+        for (int64_t w = t; w < vwords; w += blockDim.x) vbits[c][w] = 0u;
+    const int64_t per = (G + 1023) / 1024, g0 = (int64_t)t * per, g1 = g0 + per < G ? g0 + per : G;
+    uint32_t c = 0;
+    for (int64_t g = g0; g < g1; ++g) c += states[g] != 0;
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - c, all = 0;
+    for (int w = 0; w < 16; ++w) {
+        base += w < wave ? wsum[w] : 0u;
+        all += wsum[w];
+    }
+    for (int64_t g = g0; g < g1; ++g) {
+        pos[g] = base;
+        base += states[g] != 0;
+    }
+    if (t == 0) *total = all;
+    __syncthreads();  // validity bits zeroed, positions known
+    // values by plain stores, validity bits in LDS (written out once below)
+    auto put = [&](int c, int64_t p, int64_t payload, bool valid) {
+        OutCol o = outs.c[c];
+        if (o.validity && valid) atomicOr(&vbits[c][p >> 5], 1u << (p & 31));
+        o.validity = nullptr;
+        write_value(o, p, payload, true);
+    };
+    for (int64_t g = t; g < G; g += blockDim.x) {
+        const uint64_t rows = states[g];
+        if (!rows) continue;
+        const int64_t p = pos[g];
+        for (int k = 0; k < keys.n; ++k) {
+            const int64_t r = rep[g];
+            put(k, p, load_i64(keys.c[k], r), col_valid(keys.c[k], r));
+        }
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            const uint64_t cnt = sp.cnt_slot ? states[(int64_t)sp.cnt_slot * G + g] : rows;
+            const int64_t v = sp.kind == AK_COUNT ? 0 : (int64_t)states[(int64_t)sp.val_slot * G + g];
+            const int o = keys.n + a;
+            const bool i32 = sp.in_type == QEH_DT_INT32;
+            const bool flt = sp.in_type == QEH_DT_FLOAT32 || sp.in_type == QEH_DT_FLOAT64;
+            switch (sp.func) {
+                case QEH_AGG_COUNT: put(o, p, (int64_t)cnt, true); break;
+                case QEH_AGG_SUM: put(o, p, i32 ? (int64_t)(int32_t)v : v, cnt != 0); break;
+                case QEH_AGG_AVG: {
+                    double sm = flt ? as_f64(v) : (double)(i32 ? (int64_t)(int32_t)v : v);
+                    put(o, p, f64_bits(cnt ? sm / (double)cnt : 0.0), cnt != 0);
+                    break;
+                }
+                default: put(o, p, flt ? f64_bits(f64_from_order_key(v)) : v, cnt != 0); break;
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < nout; ++c)
+        if (outs.c[c].validity)
+            for (int64_t w = t; w < vwords; w += blockDim.x) outs.c[c].validity[w] = vbits[c][w];
 }
 
 // ---- host helpers ----------------------------------------------------------------------
@@ -2689,7 +2843,7 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
                           const GidSource &src, const AggSpecs &specs_in, int64_t G, const KeyCols &out_keys_src,
                           const int32_t *key_dtypes, const uint32_t *rep_row, bool drop_empty, const char *kname,
                           qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups, SlicePre *pre = nullptr,
-                          double *lanes = nullptr) {
+                          double *lanes = nullptr, uint32_t *dev_status = nullptr) {
     DevBuf states, errw;
     const int64_t Gs = std::max<int64_t>(G, 1);
     AggSpecs specs = specs_in;
@@ -2771,6 +2925,11 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
             return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: lanes launch failed");
         };
         if (G > 0) QEH_TRY(emit());
+        if (dev_status) {  // the caller reads the status words later (and recovers from an overflow)
+            QEH_HIP(hipMemcpyAsync(dev_status, errw.p, 16, hipMemcpyDeviceToDevice, ctx->stream));
+            *out_groups = G;
+            return QEH_OK;
+        }
         uint32_t stw[4];
         QEH_TRY(read_small(ctx, stw, errw.p, 16));
         if (ovf_pending && stw[1]) {
@@ -3355,7 +3514,7 @@ static int join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_col
                                        const qeh_expr *predicate, const uint16_t *table, int64_t key_min,
                                        uint64_t key_range, int64_t group_min, int64_t n_groups, int32_t group_dtype,
                                        const qeh_agg *aggs, int n_aggs, qeh_column *out_keys, qeh_column *out_aggs,
-                                       int64_t *out_groups, double *lanes) {
+                                       int64_t *out_groups, double *lanes, uint32_t *dev_status = nullptr) {
     if (!ctx || !out_groups || !table || key_range == 0 || key_range >= (1ull << 32) || n_groups < 1 ||
         n_groups >= 0xFFFE || (group_dtype != QEH_DT_INT64 && group_dtype != QEH_DT_INT32))
         return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table: bad argument");
@@ -3419,7 +3578,7 @@ static int join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_col
                   (specs.a[a].kind == AK_COUNT && specs.a[a].func == QEH_AGG_COUNT)))
                 return fail(QEH_E_UNSUPPORTED, "dense lanes carry COUNT and non-null float SUM aggregates only");
     return aggregate_rows(ctx, GM_JOIN, cols, n, pp, src, specs, n_groups, keys, &kd, rep.as<uint32_t>(), true,
-                          "join_filter_aggregate", out_keys, out_aggs, out_groups, &pre, lanes);
+                          "join_filter_aggregate", out_keys, out_aggs, out_groups, &pre, lanes, dev_status);
 }
 
 extern "C" int qeh_join_filter_aggregate_table(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
@@ -3441,6 +3600,18 @@ extern "C" int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_col
     int64_t g = 0;
     return join_filter_aggregate_table(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, table, key_min, key_range,
                                        0, n_groups, QEH_DT_INT64, aggs, n_aggs, nullptr, nullptr, &g, lanes);
+}
+
+extern "C" int qeh_join_filter_aggregate_table_lanes_async(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
+                                                           int probe_key_idx, const qeh_expr *predicate,
+                                                           const uint16_t *table, int64_t key_min, uint64_t key_range,
+                                                           int64_t n_groups, const qeh_agg *aggs, int n_aggs, double *lanes,
+                                                           uint32_t *dev_status) {
+    if (!lanes || !dev_status) return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table_lanes_async: bad argument");
+    if (n_aggs == 0) return fail(QEH_E_INVALID, "qeh_join_filter_aggregate_table_lanes_async: no aggregates");
+    int64_t g = 0;
+    return join_filter_aggregate_table(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, table, key_min, key_range,
+                                       0, n_groups, QEH_DT_INT64, aggs, n_aggs, nullptr, nullptr, &g, lanes, dev_status);
 }
 
 // ---- the fused pipeline (one bounded integer group key, unique Int64 build keys) ----------------
@@ -3489,7 +3660,9 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     FastIn in;
     int nterms, nacol;
     if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 1) return kFusedNotEligible;
-    const int64_t n_tiles = n / kSliceTile, tail = n - n_tiles * kSliceTile;
+    const int64_t tile_rows = nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE;
+    const int chunk = nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH;
+    const int64_t n_tiles = n / tile_rows, tail = n - n_tiles * tile_rows;
     if (n_tiles == 0) return kFusedNotEligible;
     AggSpecs specs = specs_in;
     const int64_t g_cap = std::min<int64_t>(kSliceStateWords / std::max(specs.n_slots, 1), 0xFFFE);
@@ -3501,18 +3674,19 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all, (int64_t)kMaxSliceGrid});
     const uint64_t tiles_per_wg = (uint64_t)((n_all + grid - 1) / grid);
 
-    DevBuf mm, plan, ditems, dcount, kbuf, vbuf, cbuf, states, errw, gkeys, rep, pos;
+    DevBuf mm, plan, ditems, dcount, kbuf, vbuf, cbuf, states, errw, gkeys, rep;
     SlicePlanIn pi{};
     pi.min_bytes = 6ull << 20;
     if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
     pi.grid = grid;
     pi.n_slots = specs.n_slots;
     pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
-    pi.alloc_items = tiles_per_wg * grid * (uint64_t)kSliceTile * 5 / 4 + (uint64_t)grid * kSliceMaxF * 288;
+    pi.chunk = chunk;
+    pi.alloc_items = tiles_per_wg * grid * (uint64_t)tile_rows * 5 / 4 + (uint64_t)grid * kSliceMaxF * (256 + 2 * chunk);
     // build rows: uniform keys over the slices, +25 %, and per-region slack
     const uint64_t dim_items = (uint64_t)nd * 5 / 4 + (uint64_t)grid * kSliceMaxF * 64;
     const uint64_t nreg_max = (uint64_t)grid * kSliceMaxF;
-    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 + 16));
+    QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 * (size_t)minmax_partials_max_blocks(ctx) + 16));  // the partials
     QEH_TRY(plan.alloc(ctx, sizeof(FusedPlan)));
     QEH_TRY(ditems.alloc(ctx, dim_items * 4 + 64));
     QEH_TRY(dcount.alloc(ctx, nreg_max * 4 + 64));
@@ -3525,7 +3699,6 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     QEH_TRY(errw.alloc(ctx, 32));
     QEH_TRY(gkeys.alloc(ctx, (size_t)Gs * 8));
     QEH_TRY(rep.alloc(ctx, (size_t)Gs * 4));
-    QEH_TRY(pos.alloc(ctx, (size_t)Gs * 8));
     uint32_t *st = errw.as<uint32_t>();
     SliceRegions rg{};
     rg.key = kbuf.as<uint16_t>();
@@ -3536,10 +3709,12 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     {
         KernelTimer kt(ctx, "fused_build");
         const qeh_column both[2] = {bk, gk};
-        QEH_TRY(columns_minmax_launch(ctx, both, 2, mm.as<MinMax>()));
-        hipLaunchKernelGGL(k_fused_plan, dim3(1), dim3(64), 0, ctx->stream, mm.as<MinMax>(), pi, g_cap, nd, dim_items, dplan, st);
-        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * Gs, kBlock * 4, 8)), dim3(kBlock), 0,
-                           ctx->stream, states.as<uint64_t>(), Gs, specs);
+        int nb = 0;
+        QEH_TRY(columns_minmax_partials(ctx, both, 2, mm.as<MinMax>(), &nb));
+        const int gp = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->props.multiProcessorCount,
+                                                                   (specs.shards * specs.n_slots * Gs + 4095) / 4096));
+        hipLaunchKernelGGL(k_fused_plan, dim3(gp), dim3(1024), 0, ctx->stream, mm.as<MinMax>(), nb, pi, g_cap, nd, dim_items,
+                           dplan, st, states.as<uint64_t>(), Gs, specs);
     }
     QEH_HIP(hipGetLastError());
     FusedPro fp{};
@@ -3561,31 +3736,29 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
         const bool pf = slice_probe_prefetch();
         const int gridB = ctx->props.multiProcessorCount;
         const HashTable t{};
-#define QEH_SD(NAV, PFV)                                                                                                   \
-    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, \
+        static const bool pv = std::getenv("QEH_FUSED_PV") && std::atoi(std::getenv("QEH_FUSED_PV")) == 1;
+#define QEH_SD(NAV, PFV, PVV)                                                                                              \
+    hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, PVV, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg,   \
                        grid, 0, t, in, specs, Gs, states.as<uint64_t>(), dim)
         if (nacol == 0) {
-            if (pf) QEH_SD(0, true);
-            else QEH_SD(0, false);
+            if (pf) QEH_SD(0, true, false);
+            else QEH_SD(0, false, false);
+        } else if (pv) {
+            if (pf) QEH_SD(1, true, true);
+            else QEH_SD(1, false, true);
         } else {
-            if (pf) QEH_SD(1, true);
-            else QEH_SD(1, false);
+            if (pf) QEH_SD(1, true, false);
+            else QEH_SD(1, false, false);
         }
 #undef QEH_SD
     }
     QEH_HIP(hipGetLastError());
-    // fold the shard copies, flag / scan the non-empty slots (the group count into st[2..3]), finalize
-    {
-        AggSpecs cs = specs;
-        if (specs.shards > 1) {
-            const int64_t words = (int64_t)specs.n_slots * Gs;
-            hipLaunchKernelGGL(k_states_fold, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, ctx->stream,
-                               states.as<uint64_t>(), Gs, specs);
-            cs.shards = 1;
-        }
-        hipLaunchKernelGGL(k_states_compact_small, dim3(1), dim3(1024), 0, ctx->stream, states.as<uint64_t>(), Gs, Gs, cs,
-                           pos.as<uint64_t>(), (uint64_t *)(st + 2));
-        specs.shards = cs.shards;
+    // fold the shard copies (when there are several), then one workgroup compacts, writes the outputs
+    // and the group count (st[2..3])
+    if (specs.shards > 1) {
+        const int64_t words = (int64_t)specs.n_slots * Gs;
+        hipLaunchKernelGGL(k_states_fold, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, ctx->stream,
+                           states.as<uint64_t>(), Gs, specs);
     }
     QEH_HIP(hipGetLastError());
     qeh_column kc{};
@@ -3619,15 +3792,14 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
             return s;
         }
         ++made;
-        if (nullable) QEH_HIP(hipMemsetAsync(c->validity, 0, ((Gs + 63) / 64) * 8, ctx->stream));
         oc.c[i].values = c->values;
         oc.c[i].validity = (uint32_t *)c->validity;
         oc.c[i].dtype = dt;
     }
     {
         KernelTimer kt(ctx, "aggregate_finalize");
-        hipLaunchKernelGGL(k_finalize, dim3(grid_for(ctx, Gs, kBlock, 8)), dim3(kBlock), 0, ctx->stream, states.as<uint64_t>(),
-                           Gs, pos.as<uint64_t>(), keys, rep.as<uint32_t>(), specs, oc);
+        hipLaunchKernelGGL(k_fused_finish, dim3(1), dim3(1024), 0, ctx->stream, states.as<uint64_t>(), Gs, keys,
+                           rep.as<uint32_t>(), specs, oc, (uint64_t *)(st + 2));
     }
     uint32_t sw[8];
     int s = hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "fused join-aggregate: launch failed");

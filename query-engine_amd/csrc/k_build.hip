@@ -417,6 +417,18 @@ extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64
     return QEH_OK;
 }
 
+extern "C" int qeh_u16_count_nonzero_dev(qeh_ctx *ctx, const uint16_t *table, uint64_t n, uint64_t *dev_out) {
+    if (!ctx || !dev_out || (n > 0 && !table)) return fail(QEH_E_INVALID, "qeh_u16_count_nonzero_dev: bad argument");
+    DeviceGuard dg(ctx->device);
+    QEH_HIP(hipMemsetAsync(dev_out, 0, 8, ctx->stream));
+    if (n == 0) return QEH_OK;
+    const int gc = grid_for(ctx, (int64_t)(n / 8 + 1), kBlock * 4, 1);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)table, n, 2,
+                       (unsigned long long *)dev_out);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
 int column_minmax(qeh_ctx *ctx, const qeh_column &col, int64_t *mn, int64_t *mx, int64_t *valid) {
     return columns_minmax(ctx, &col, 1, mn, mx, valid);
 }
@@ -463,6 +475,25 @@ int columns_minmax_launch(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *d
     QEH_HIP(hipGetLastError());
     return QEH_OK;
 }
+
+// The partial min / max of up to kMinMaxCols columns only (part[column * nb + workgroup], nb workgroups
+// per column): for callers that reduce the partials in a kernel of their own.
+int columns_minmax_partials(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *part, int *nb_out) {
+    if (n < 1 || n > kMinMaxCols) return fail(QEH_E_INVALID, "columns_minmax_partials: 1..4 columns");
+    MinMaxJob j{};
+    int64_t longest = 0;
+    for (int q = 0; q < n; ++q) {
+        j.c[q] = make_colref(cols[q]);
+        j.n[q] = cols[q].length;
+        longest = std::max<int64_t>(longest, cols[q].length);
+    }
+    const int nb = grid_for(ctx, std::max<int64_t>(longest, 1), kBlock * 8, longest >= ((int64_t)1 << 26) ? 4 : 1);
+    hipLaunchKernelGGL(k_key_minmax_n, dim3(nb, n), dim3(kBlock), 0, ctx->stream, j, part);
+    QEH_HIP(hipGetLastError());
+    *nb_out = nb;
+    return QEH_OK;
+}
+int minmax_partials_max_blocks(qeh_ctx *ctx) { return ctx->props.multiProcessorCount * 4; }
 
 int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const MinMax *dev_out, int64_t *mn, int64_t *mx,
                            int64_t *valid) {

@@ -67,6 +67,9 @@ struct MinMax {
 // The min/max kernels of `n` integer columns into dev_out[0..n) (no host sync), and the read-back of
 // such a result (one synchronous read; also memoised like columns_minmax).
 int columns_minmax_launch(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *dev_out);
+// only the per-workgroup partials (part[column * *nb + workgroup], at most minmax_partials_max_blocks per column)
+int columns_minmax_partials(qeh_ctx *ctx, const qeh_column *cols, int n, MinMax *part, int *nb);
+int minmax_partials_max_blocks(qeh_ctx *ctx);
 int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const MinMax *dev_out, int64_t *mn, int64_t *mx,
                            int64_t *valid);
 // Stable sort of (one Int64 / Int32 key, one non-null 8-byte payload) carrying the payload through

@@ -86,12 +86,14 @@ SIGNATURES = {
     "qeh_join_filter_aggregate_prelaunch": (I, [P, COLP, I, I, EXPRP, AGGP, I, C.POINTER(I64), C.POINTER(I64)]),
     "qeh_direct_group_table_insert": (I, [P, COLP, COLP, I64, U64, I64, P]),
     "qeh_u16_count_nonzero": (I, [P, P, U64, C.POINTER(I64)]),
+    "qeh_u16_count_nonzero_dev": (I, [P, P, U64, P]),
     "qeh_columns_minmax": (I, [P, COLP, I, C.POINTER(I64)]),
     "qeh_dense_states_f64": (I, [P, COLP, COLP, I, I64, I64, P]),
     "qeh_dense_states_take": (I, [P, P, I, I64, I64, I, I, C.c_int32, C.POINTER(C.c_int32), COLP, COLP, C.POINTER(I64)]),
     "qeh_join_filter_aggregate_table": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, I64, C.c_int32, AGGP, I, COLP, COLP,
                                             C.POINTER(I64)]),
     "qeh_join_filter_aggregate_table_lanes": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, AGGP, I, P]),
+    "qeh_join_filter_aggregate_table_lanes_async": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, AGGP, I, P, P]),
     "qeh_broadcast_stats": (I, [P, COLP, COLP, C.POINTER(I64), I, P]),
     "qeh_join_filter_aggregate_prelaunch_stats": (I, [P, COLP, I, I, EXPRP, AGGP, I, P, I, I]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),
@@ -155,7 +157,7 @@ def load(path: str | None = None) -> C.CDLL:
                            "(there is no CPU fallback)")
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
-        if os.environ.get("QEH_LIB_PATH") and not hasattr(lib, name):
+        if (path or os.environ.get("QEH_LIB_PATH")) and not hasattr(lib, name):
             continue  # an older experiment build: calls into what it lacks fail where they are made
         fn = getattr(lib, name)
         fn.restype = res

@@ -443,6 +443,26 @@ class Context:
                                                                  key_min, key_range, n_groups, ca, len(aggs),
                                                                  lanes_ptr))
 
+    def join_filter_aggregate_table_lanes_async(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                                                predicate: Optional[PhysicalExpr], table_ptr: int, key_min: int,
+                                                key_range: int, n_groups: int, aggs: Sequence[Tuple[int, int]],
+                                                lanes_ptr: int, status_ptr: int) -> None:
+        """qeh_join_filter_aggregate_table_lanes_async: as ..._lanes, but its status words (error bits,
+        region overflow) go to device memory at status_ptr and nothing waits on the host."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        abi.check(self.lib.qeh_join_filter_aggregate_table_lanes_async(self.h, cp, len(probe_cols), probe_key_idx,
+                                                                       C.byref(e) if e is not None else None, table_ptr,
+                                                                       key_min, key_range, n_groups, ca, len(aggs),
+                                                                       lanes_ptr, status_ptr))
+
+    def u16_count_nonzero_dev(self, table_ptr: int, n: int, out_ptr: int) -> None:
+        """qeh_u16_count_nonzero_dev: the non-empty entries of a u16 table into device memory (8 B)."""
+        abi.check(self.lib.qeh_u16_count_nonzero_dev(self.h, table_ptr, n, out_ptr))
+
     def broadcast_stats(self, build_key: DeviceColumn, group_key: DeviceColumn, extra: Sequence[int],
                         out_ptr: int) -> None:
         """qeh_broadcast_stats: [rows, key min, max, group min, max, *extra] of this dimension shard

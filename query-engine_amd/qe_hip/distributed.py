@@ -643,11 +643,50 @@ class DistributedExecutor:
         if self.world > 1:
             dist.all_reduce(table, op=dist.ReduceOp.SUM, group=self.group)  # u16 pairs: no carries (checked above)
         self._sync_torch()
+        lanes_ok = (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
+                    and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
+                            for j, (f, c) in enumerate(aggs)))
+        if lanes_ok and not os.environ.get("QEH_SYNC_TABLE_CHECK"):
+            # no host wait until the final states: the duplicate check (non-empty entries of the summed
+            # table, the same on every rank) and the operator's status words (error bits, a slice region
+            # overflow on this rank) stay on the device; the status rides the lanes' all-reduce as one
+            # extra lane, so every rank sees every rank's flags and all take the same branch below
+            chk = torch.empty(2, dtype=torch.int64, device="cuda")
+            status = torch.zeros(4, dtype=torch.int32, device="cuda")
+            lanes = torch.empty((1 + len(aggs)) * G + 1, dtype=torch.float64, device="cuda")
+            self._sync_torch()
+            self.ctx.u16_count_nonzero_dev(table.data_ptr(), R, chk.data_ptr())
+            self.ctx.join_filter_aggregate_table_lanes_async(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
+                                                             R, G, aggs, lanes.data_ptr(), status.data_ptr())
+            self._sync()
+            lanes[-1] = (status[:2] != 0).any().to(torch.float64)
+            if self.world > 1:
+                dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+            chk[1] = lanes[-1].to(torch.int64)
+            self._sync_torch()
+            ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank,
+                                                   st["gdtype"],
+                                                   [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
+            nz, bad = (int(q) for q in chk.tolist())
+            if nz != total:
+                return None  # a build key repeats: the general path handles multi-match joins
+            if bad:  # some rank's operator overflowed a slice region (or failed): redo it with the checks inline
+                lanes = torch.empty((1 + len(aggs)) * G, dtype=torch.float64, device="cuda")
+                self._sync_torch()
+                self.ctx.join_filter_aggregate_table_lanes(probe_cols, probe_key_idx, predicate, table.data_ptr(),
+                                                           kmin, R, G, aggs, lanes.data_ptr())
+                self._sync()
+                if self.world > 1:
+                    dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+                self._sync_torch()
+                ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank,
+                                                       st["gdtype"],
+                                                       [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
+            self.last_final = "dense"
+            return [ok], ov, g
         if self.ctx.u16_count_nonzero(table.data_ptr(), R) != total:
             return None  # a build key repeats: the general path handles multi-match joins
-        if (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
-                and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
-                        for j, (f, c) in enumerate(aggs))):
+        if lanes_ok:
             # the fused operator writes the dense final stage's lanes itself (row counts, COUNT / float
             # SUM partials per group slot): no compaction, output columns or re-scatter of the partials
             lanes = torch.empty((1 + len(aggs)) * G, dtype=torch.float64, device="cuda")
