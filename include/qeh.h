@@ -429,6 +429,14 @@ int qeh_partition_hash(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_p
  * columns are moved by a single tile-ranked pass; other columns through the permutation. */
 int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts, const qeh_column *cols,
                             int n_cols, int64_t *counts, qeh_column *out_cols);
+/* The reverse of qeh_partition_hash_move over one non-null Int64 key into at most 16 partitions:
+ * out_cols[c][i] = moved[c][p(i)], p(i) = row i's position in the stable partition-major order the
+ * move produces (rows of lower partitions, then the rows of its own partition before it) -- results
+ * computed on moved rows (a distributed window function's numbers, returned by the reverse
+ * all-to-all) back into input order in one streaming pass.  1..2 non-null Int64 / Float64 columns of
+ * the key's length. */
+int qeh_partition_hash_unmove(qeh_ctx *ctx, const qeh_column *key, int n_parts, const qeh_column *moved, int n_cols,
+                              qeh_column *out_cols);
 
 /* FilterExec followed by the hash Exchange of a shuffle stage (executor.rs:131-155, then
  * partition.rs:151-212 / operators.rs:15-73; config 4's probe side), fused: rows of `cols` whose

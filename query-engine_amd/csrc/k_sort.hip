@@ -621,6 +621,70 @@ __global__ __launch_bounds__(kRsThreads) void k_part_scatter_small(const uint8_t
     }
 }
 
+// The inverse of k_part_scatter_small (qeh_partition_hash_unmove): the same stable ranking of each
+// tile's rows by partition, but every row reads its value from the partition-major column at the
+// position the forward move gave it (run start + its rank in the partition) and writes it at its own
+// input position.  A stable partition places row i at (rows of lower partitions) + (rows of its
+// partition before i) whatever the tiling, so this reproduces any stable forward move.
+template <int NC, bool AT = true>
+__global__ __launch_bounds__(kRsThreads) void k_part_gather_small(const uint8_t *__restrict__ ids, int64_t n, int64_t seg,
+                                                                  const uint64_t *__restrict__ offs, int nblocks, PmCols cols) {
+    constexpr int W = kRsThreads / 64;
+    constexpr int IPT = 8;
+    constexpr int TILE = kRsThreads * IPT;
+    __shared__ uint32_t wcnt[W][kPsDig];
+    __shared__ uint32_t tot_s[kPsDig];
+    __shared__ uint64_t run[kPsDig];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (t < kPsDig) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    __syncthreads();  // run[]
+    for (int64_t c0 = lo; c0 < hi; c0 += TILE) {
+        if (t < W * kPsDig) (&wcnt[0][0])[t] = 0u;
+        const int64_t base = c0 + (int64_t)wave * 64 * IPT + lane;
+        uint32_t dg[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = base + j * 64;
+            dg[j] = ids[i < hi ? i : hi - 1];
+        }
+        lds_barrier();
+        uint32_t rk[IPT];
+        bool live[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            live[j] = base + j * 64 < hi;
+            rk[j] = tile_rank<AT>(wcnt[wave], dg[j], live[j]);  // stable, as the forward move
+        }
+        lds_barrier();
+        if (t < kPsDig) {  // thread d: per-wave starts inside partition d, its tile total
+            uint32_t tot = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = wcnt[w][t];
+                wcnt[w][t] = tot;
+                tot += c;
+            }
+            tot_s[t] = tot;
+        }
+        lds_barrier();
+        uint64_t v[IPT][NC];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint64_t pos = live[j] ? run[dg[j]] + wcnt[wave][dg[j]] + rk[j] : 0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[j][c] = live[j] ? cols.src[c][pos] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (live[j])
+#pragma unroll
+                for (int c = 0; c < NC; ++c) __builtin_nontemporal_store(v[j][c], &cols.dst[c][base + j * 64]);
+        lds_barrier();
+        if (t < kPsDig) run[t] += tot_s[t];
+    }
+}
+
 // Filter + partition ids + per-segment histogram in one pass (config 4's probe side, fewer than
 // kPsDig partitions): block b streams its segment [b * seg, (b + 1) * seg) -- seg a multiple of the
 // 8192-row tile -- with FastTile's 16-B loads of the key and up to two term columns (every load of a
@@ -2074,6 +2138,67 @@ static int make_hash_keys(const qeh_column *keys, int n_keys, HashKeys *hk, int6
 // Exchange's device side in one pass: partition ids, per-segment histograms, then the payload
 // columns moved to partition-major order (k_part_scatter).  Columns that are not non-null
 // 8-byte go through the permutation + gather path.
+// qeh_partition_hash_unmove: out_cols[c][i] = moved[c][position of row i in the stable partition-major
+// order of qeh_partition_hash_move over the same key] -- the reverse of an Exchange's move, for results
+// computed on the partition-major rows (distributed window functions return them into input order).
+extern "C" int qeh_partition_hash_unmove(qeh_ctx *ctx, const qeh_column *key, int n_parts, const qeh_column *moved,
+                                         int n_cols, qeh_column *out_cols) {
+    if (!ctx || !key || !moved || !out_cols || n_cols < 1 || n_cols > 2 || n_parts < 1 || n_parts > kPsDig)
+        return fail(QEH_E_INVALID, "qeh_partition_hash_unmove: bad argument (1..2 columns, 1..16 partitions)");
+    DeviceGuard dg(ctx->device);
+    const int64_t n = key->length;
+    QEH_TRY(check_column(*key, "partition key"));
+    if (key->dtype != QEH_DT_INT64 || (key->validity && key->null_count != 0) ||
+        (((uintptr_t)key->values + (uintptr_t)key->offset * 8) & 15) != 0)
+        return fail(QEH_E_UNSUPPORTED, "qeh_partition_hash_unmove: one non-null, 16-B aligned Int64 key");
+    for (int c = 0; c < n_cols; ++c) {
+        QEH_TRY(check_column(moved[c], "moved column"));
+        if (moved[c].length != n || (moved[c].dtype != QEH_DT_INT64 && moved[c].dtype != QEH_DT_FLOAT64) ||
+            (moved[c].validity && moved[c].null_count != 0))
+            return fail(QEH_E_UNSUPPORTED, "qeh_partition_hash_unmove: non-null Int64 / Float64 columns of the key's length");
+    }
+    constexpr int64_t kFusedTile = (int64_t)kRsThreads * kFastR;
+    int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kFusedTile - 1) / kFusedTile, 1), (int64_t)ctx->props.multiProcessorCount);
+    int64_t seg = (n + nblocks - 1) / nblocks;
+    seg = std::max<int64_t>((seg + kFusedTile - 1) / kFusedTile * kFusedTile, kFusedTile);
+    nblocks = (int)std::max<int64_t>((n + seg - 1) / seg, 1);
+    int made = 0, s = QEH_OK;
+    for (; made < n_cols; ++made)
+        if ((s = alloc_column(ctx, moved[made].dtype, n, false, &out_cols[made])) != QEH_OK) break;
+    if (s == QEH_OK && n > 0) {
+        DevBuf ids, hist, offs;
+        if (ids.alloc(ctx, (size_t)n) || hist.alloc(ctx, (size_t)kPsDig * nblocks * 4) ||
+            offs.alloc(ctx, (size_t)kPsDig * nblocks * 8))
+            s = fail(QEH_E_OOM, "partition unmove: out of device memory");
+        KernelTimer kt(ctx, "partition_move");
+        if (s == QEH_OK) {
+            FastIn fin{};
+            fin.key = (const int64_t *)key->values + key->offset;
+            hipLaunchKernelGGL(k_ids_hist_pred<0>, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, fin, PredTerms{}, n, seg,
+                               (uint32_t)n_parts, ids.as<uint8_t>(), hist.as<uint32_t>(), nblocks);
+            s = exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kPsDig * nblocks, nullptr);
+        }
+        if (s == QEH_OK) {
+            PmCols pc{};
+            pc.n = n_cols;
+            for (int c = 0; c < n_cols; ++c) {
+                pc.src[c] = (const uint64_t *)moved[c].values + moved[c].offset;
+                pc.dst[c] = (uint64_t *)out_cols[c].values;
+            }
+            const bool ballot = rs_ballot(ctx);
+            auto kf = n_cols == 1 ? (ballot ? k_part_gather_small<1, false> : k_part_gather_small<1, true>)
+                                  : (ballot ? k_part_gather_small<2, false> : k_part_gather_small<2, true>);
+            hipLaunchKernelGGL(kf, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, ids.as<uint8_t>(), n, seg,
+                               offs.as<uint64_t>(), nblocks, pc);
+            if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "partition unmove launch failed");
+        }
+        if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "partition unmove failed");
+    }
+    if (s != QEH_OK)
+        for (int c = 0; c < made; ++c) qeh_column_release(ctx, &out_cols[c]);
+    return s;
+}
+
 extern "C" int qeh_partition_hash_move(qeh_ctx *ctx, const qeh_column *keys, int n_keys, int n_parts,
                                        const qeh_column *cols, int n_cols, int64_t *counts, qeh_column *out_cols) {
     if (!ctx || !keys || n_keys < 1 || n_keys > kMaxCols || !counts || n_parts < 1 || n_parts > kRadix || n_cols < 0 ||

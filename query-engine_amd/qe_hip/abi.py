@@ -108,6 +108,7 @@ SIGNATURES = {
     "qeh_partition_hash": (I, [P, COLP, I, I, C.POINTER(I64), COLP]),
     "qeh_partition_range": (I, [P, COLP, C.POINTER(I64), I, C.POINTER(I64), COLP]),
     "qeh_partition_hash_move": (I, [P, COLP, I, I, COLP, I, C.POINTER(I64), COLP]),
+    "qeh_partition_hash_unmove": (I, [P, COLP, I, COLP, I, COLP]),
     "qeh_filter_partition_hash_move": (I, [P, COLP, I, EXPRP, I, I, C.POINTER(C.c_int32), I, C.POINTER(I64), COLP]),
     "qeh_take": (I, [P, COLP, COLP, COLP]),
     "qeh_row_number": (I, [P, COLP, I, COLP, I, C.POINTER(C.c_int8), COLP]),

@@ -582,6 +582,13 @@ class Context:
                                                    len(cols), counts, out))
         return np.array(counts[:], np.int64), [self._wrap(out[i]) for i in range(len(cols))]
 
+    def partition_hash_unmove(self, key: DeviceColumn, n_parts: int, moved: Sequence[DeviceColumn]) -> List[DeviceColumn]:
+        """qeh_partition_hash_unmove: columns in partition-major order (as partition_hash_move over `key`
+        left them) back into the key's input order."""
+        out = (abi.QehColumn * max(len(moved), 1))()
+        abi.check(self.lib.qeh_partition_hash_unmove(self.h, C.byref(key.c), n_parts, self._cols(moved), len(moved), out))
+        return [self._wrap(out[i]) for i in range(len(moved))]
+
     def filter_partition_hash_move(self, cols: Sequence[DeviceColumn], predicate: PhysicalExpr, key_idx: int,
                                    n_parts: int, move_idx: Sequence[int]):
         """qeh_filter_partition_hash_move: (counts, cols[move_idx] of the qualifying rows in

@@ -35,6 +35,7 @@ import torch.distributed as dist
 from . import abi
 from .device import NP_OF, Context, DeviceColumn, order_keys
 from .expr import AggregateFunction as AF
+from .plan import WindowFunctionType as W
 
 TORCH_OF = {abi.DT_INT64: torch.int64, abi.DT_FLOAT64: torch.float64, abi.DT_INT32: torch.int32,
             abi.DT_FLOAT32: torch.float32, abi.DT_UINT32: torch.int32}
@@ -874,6 +875,30 @@ class DistributedExecutor:
             pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
         return self._final(pk, pa_, aggs)
 
+    def _moved_shuffle_ok(self, part_keys, cols) -> bool:
+        """The fused window shuffle applies: one non-null 16-B aligned Int64 PARTITION BY key, every
+        moved column a non-null Int64 / Float64, at most 16 ranks (QEH_DIST_WINDOW_PERM=1: the
+        permutation + take / scatter form)."""
+        if len(part_keys) != 1 or self.world > 16 or os.environ.get("QEH_DIST_WINDOW_PERM"):
+            return False
+        k = part_keys[0].c
+        if k.dtype != abi.DT_INT64 or (k.validity and k.null_count != 0) or ((k.values or 0) + k.offset * 8) % 16:
+            return False
+        return all(c.dtype in (abi.DT_INT64, abi.DT_FLOAT64) and not (c.c.validity and c.c.null_count != 0) for c in cols)
+
+    def _moved_window(self, part_keys, cols, local_fn) -> DeviceColumn:
+        """The window shuffle as two streaming passes instead of a permutation, a take per column and a
+        scatter: qeh_partition_hash_move carries (key, order keys, argument) to their rank in one pass,
+        the rank computes the function on what it received (source-rank-major = global input order,
+        stable within a source), the reverse all-to-all returns each source's rows in the order it sent
+        them, and qeh_partition_hash_unmove puts them back into input order (the same stable ranking,
+        gathering instead of scattering)."""
+        counts, moved = self.ctx.partition_hash_move([part_keys[0]], self.world, cols)
+        recv, recv_counts = self._exchange_columns(moved, counts)
+        res = local_fn(recv)
+        back, _ = self._exchange_columns([res], recv_counts)
+        return self.ctx.partition_hash_unmove(part_keys[0], self.world, [back[0]])[0]
+
     def row_number(self, part_keys: Sequence[DeviceColumn], order_keys: Sequence[DeviceColumn],
                    ascending: Sequence[bool]) -> DeviceColumn:
         """ROW_NUMBER() OVER (PARTITION BY .. ORDER BY ..) over rank-sharded rows
@@ -881,7 +906,13 @@ class DistributedExecutor:
         partition key, so each PARTITION BY group lives on one rank and is numbered
         there (received order = source-rank-major, stable within a source, i.e. the
         global input order that breaks ties); the numbers go back by the reverse
-        all-to-all and are scattered into this rank's input order."""
+        all-to-all into this rank's input order (_moved_window, or a permutation and
+        a scatter for shapes it does not take)."""
+        cols = list(part_keys) + list(order_keys)
+        if self._moved_shuffle_ok(part_keys, cols):
+            npk = len(part_keys)
+            return self._moved_window(part_keys, cols,
+                                      lambda recv: self.ctx.row_number(recv[:npk], recv[npk:], list(ascending)))
         counts, perm = self.ctx.hash_partition(part_keys[0], self.world)
         cols = list(part_keys) + list(order_keys)
         recv, recv_counts = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
@@ -899,8 +930,14 @@ class DistributedExecutor:
         through the inverse permutation (the results of LAG/LEAD/… carry NULLs)."""
         if not part_keys:
             raise ValueError("distributed window functions need a PARTITION BY key")
-        counts, perm = self.ctx.hash_partition(part_keys[0], self.world)
         cols = list(part_keys) + list(order_keys) + ([arg] if arg is not None else [])
+        npk, nok = len(part_keys), len(order_keys)
+        if func in (W.RowNumber, W.Rank, W.DenseRank, W.Ntile) and self._moved_shuffle_ok(part_keys, cols):
+            # non-null Int64 results: back through the moved route
+            return self._moved_window(part_keys, cols, lambda recv: self.ctx.window(
+                func, recv[:npk], recv[npk:npk + nok], list(ascending),
+                arg=recv[npk + nok] if arg is not None else None, param=param, default=default))
+        counts, perm = self.ctx.hash_partition(part_keys[0], self.world)
         recv, recv_counts = self._exchange_columns([self.ctx.take(c, perm) for c in cols], counts)
         npk, nok = len(part_keys), len(order_keys)
         res = self.ctx.window(func, recv[:npk], recv[npk:npk + nok], list(ascending),

@@ -279,6 +279,16 @@ def mode_gpu(rank, world):
                                      param=2, default=0.25)
         assert np.array_equal(res[1][1], want_ok)
         assert np.array_equal(res[1][0][want_ok], want_lv[want_ok])
+    # --- the moved route (non-null Int64 PARTITION BY and ORDER BY keys): partition_hash_move carries the
+    # rows, partition_hash_unmove returns the numbers into input order -- ROW_NUMBER, DENSE_RANK, NTILE
+    rn2 = dx.row_number([ctx.upload(wk_)], [ctx.upload(wv_)], [True])
+    dr2 = dx.window(WF.DenseRank, [ctx.upload(wk_)], [ctx.upload(wv_)], [False])
+    nt2 = dx.window(WF.Ntile, [ctx.upload(wk_)], [ctx.upload(wv_)], [True], param=3)
+    res = dx.gather_to_root([rn2, dr2, nt2])
+    if rank == 0:
+        assert np.array_equal(res[0][0], ob.row_number([ob.HostCol(K)], [ob.HostCol(V)], [True]))
+        assert np.array_equal(res[1][0], ob.window(WF.DenseRank, [ob.HostCol(K)], [ob.HostCol(V)], [False])[0])
+        assert np.array_equal(res[2][0], ob.window(WF.Ntile, [ob.HostCol(K)], [ob.HostCol(V)], [True], param=3)[0])
     # --- distributed ORDER BY (sampled range partition, stable local sort)
     def srt(r):
         g = np.random.default_rng(90 + r)

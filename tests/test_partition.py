@@ -235,3 +235,20 @@ def test_filter_partition_hash_move_8_ways_vs_oracle(ctx, int32_key):
     if not int32_key:
         assert np.array_equal(moved[0].to_numpy()[0], fk[perm])
     assert np.array_equal(moved[-1].to_numpy()[0], fv[perm])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", [(1, 2), (8191, 3), (8192 * 5 + 17, 8), (2_000_003, 16)])
+def test_partition_hash_unmove_inverts_move(ctx, n, parts):
+    """qeh_partition_hash_unmove(move(x)) == x: the reverse of the stable hash move, for any row count
+    (ragged segments and tiles) and up to 16 partitions; and it places a column computed on the moved
+    rows (here the moved row ids) back at each row's input position."""
+    r = np.random.default_rng(n + parts)
+    k = r.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    v = r.random(n)
+    rowid = np.arange(n, dtype=np.int64)
+    counts, moved = ctx.partition_hash_move([ctx.upload(k)], parts, [ctx.upload(k), ctx.upload(v), ctx.upload(rowid)])
+    assert int(counts.sum()) == n
+    back = ctx.partition_hash_unmove(ctx.upload(k), parts, [moved[1], moved[2]])
+    assert np.array_equal(back[0].to_numpy()[0], v)
+    assert np.array_equal(back[1].to_numpy()[0], rowid)
