@@ -293,7 +293,7 @@ constexpr int kSliceMaxF = 160;                  // slices: key range <= 160 * 6
 constexpr int kSliceBlock = 1024;                // one workgroup per CU in both phases
 constexpr int kSliceTile = kSliceBlock * kFastR;  // 8192 probe rows per phase-A iteration
 constexpr int kSliceChunk = 32;                  // items per flushed chunk
-constexpr int kMaxSliceGrid = 256;               // phase-A workgroups of the fused pipeline (one per CU)
+constexpr int kMaxSliceGrid = 512;               // phase-A workgroups of the fused pipeline (one or two per CU)
 constexpr int kSliceStateWords = 3584;           // phase-B LDS aggregate states (n_slots * G)
 // Group-range slices (G too large for LDS states): phase A looks the group id up and partitions
 // by gid >> kGidSliceBits; phase B aggregates one range of 2^kGidSliceBits groups in LDS.
@@ -445,27 +445,38 @@ struct __attribute__((aligned(16))) SliceChunk {
 // build time): 64-item chunks (128 B of keys + 512 B of values, whole lines) with 4096-row tiles keep
 // the carries and the staging in one CU's LDS.
 #ifndef QEH_EARLY_PAIRS
-#define QEH_EARLY_PAIRS kFastPairs
+#define QEH_EARLY_PAIRS 2
 #endif
 #ifndef QEH_EARLY_CHUNK
-#define QEH_EARLY_CHUNK kSliceChunk
+#define QEH_EARLY_CHUNK 64
 #endif
-template <int NACOL, bool EARLY = false>
+// NTH = 512 (fused pipeline, QEH_FUSED_2WG): two co-resident 512-thread workgroups per CU, each with
+// 1024-row tiles and 32-item chunks (72 KB of LDS), so one workgroup's rank / scan / stage phases run
+// while the other's loads stream.
+#ifndef QEH_EARLY2_PAIRS
+#define QEH_EARLY2_PAIRS 1
+#endif
+#ifndef QEH_EARLY2_CHUNK
+#define QEH_EARLY2_CHUNK 32
+#endif
+template <int NACOL, bool EARLY = false, int NTH = kSliceBlock>
 struct SliceShape {
-    static constexpr int P = NACOL > 1 ? 2 : (EARLY ? QEH_EARLY_PAIRS : kFastPairs);
-    static constexpr int CH = NACOL > 1 ? 16 : (EARLY ? QEH_EARLY_CHUNK : kSliceChunk);
-    static constexpr int TILE = kSliceBlock * 2 * P;
+    static constexpr bool HALF = EARLY && NTH < kSliceBlock;
+    static constexpr int P = NACOL > 1 ? 2 : (HALF ? QEH_EARLY2_PAIRS : EARLY ? QEH_EARLY_PAIRS : kFastPairs);
+    static constexpr int CH = NACOL > 1 ? 16 : (HALF ? QEH_EARLY2_CHUNK : EARLY ? QEH_EARLY_CHUNK : kSliceChunk);
+    static constexpr int TILE = NTH * 2 * P;
 };
 
 // Phase A's prologue in the fused pipeline (before the first tile's loads): the output group keys,
 // then this workgroup's share of the build rows, each into its slice's region (LDS atomics on dcnt
 // give the positions; no order inside a region is needed).  Not inlined: its registers stay out of
 // the tile loop's allocation.
+template <int NTH>
 __device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int F, int64_t kmin, uint32_t *dcnt) {
     const int tid = threadIdx.x;
     const FusedPlan fpl = *fp.plan;
-    for (int i = tid; i < F; i += kSliceBlock) dcnt[i] = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kSliceBlock + tid; i < fp.G; i += (int64_t)gridDim.x * kSliceBlock) {
+    for (int i = tid; i < F; i += NTH) dcnt[i] = 0;
+    for (int64_t i = (int64_t)blockIdx.x * NTH + tid; i < fp.G; i += (int64_t)gridDim.x * NTH) {
         if (fp.as32) ((int32_t *)fp.gkeys)[i] = (int32_t)(fpl.gmin + i);
         else ((int64_t *)fp.gkeys)[i] = fpl.gmin + i;
         fp.rep[i] = (uint32_t)i;
@@ -476,17 +487,17 @@ __device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int
     uint32_t *dreg = fp.ditems + (uint64_t)blockIdx.x * F * fpl.dcap;
     bool dovf = false;
     constexpr int DR = 8;
-    for (int64_t i0 = lo + tid; i0 < hi; i0 += DR * kSliceBlock) {
+    for (int64_t i0 = lo + tid; i0 < hi; i0 += DR * NTH) {
         int64_t kk[DR], gg[DR];
 #pragma unroll
         for (int q = 0; q < DR; ++q) {
-            const int64_t i = i0 + (int64_t)q * kSliceBlock;
+            const int64_t i = i0 + (int64_t)q * NTH;
             kk[q] = i < hi ? fp.dk[i] : kmin;
             gg[q] = i < hi ? load_i64(fp.dg, i) : 0;
         }
 #pragma unroll
         for (int q = 0; q < DR; ++q) {
-            if (i0 + (int64_t)q * kSliceBlock >= hi) continue;
+            if (i0 + (int64_t)q * NTH >= hi) continue;
             const uint64_t o = (uint64_t)kk[q] - (uint64_t)kmin;
             const uint32_t b = (uint32_t)(o >> kSliceBits);
             const uint32_t r = atomicAdd(&dcnt[b], 1u);
@@ -498,7 +509,7 @@ __device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int
         }
     }
     __syncthreads();
-    for (int i = tid; i < F; i += kSliceBlock) {
+    for (int i = tid; i < F; i += NTH) {
         fp.dcount[(uint64_t)blockIdx.x * F + i] = dcnt[i] < fpl.dcap ? dcnt[i] : (uint32_t)fpl.dcap;
         dovf |= dcnt[i] > fpl.dcap;
     }
@@ -511,12 +522,12 @@ __device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int
 // before phase A, uses it (the prelaunched phase A of the other paths keeps room for the build).
 // tail_rows > 0: one more, partial tile of that many rows after the n_tiles full ones (fused pipeline;
 // the other paths run their ragged tail through the generic kernel).
-template <int NTERMS, int NACOL, bool NT, int MODE = 0, bool EARLY = false>
-__global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
+template <int NTERMS, int NACOL, bool NT, int MODE = 0, bool EARLY = false, int NTH = kSliceBlock>
+__global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms terms, int64_t kmin, uint64_t range,
                                                                  int64_t n_tiles, SliceRegions rg, HashTable t,
                                                                  const SlicePlan *__restrict__ dplan = nullptr,
                                                                  int64_t tail_rows = 0, FusedPro fp = FusedPro{}) {
-    using Shape = SliceShape<NACOL, EARLY>;
+    using Shape = SliceShape<NACOL, EARLY, NTH>;
     constexpr int P = Shape::P, R = 2 * P, TILE = Shape::TILE, CH = Shape::CH;
     constexpr int MAXF = kSliceMaxF;
     if (dplan) {  // planned on the device: the shape comes from the build key's range in memory
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     const uint64_t cap = rg.cap;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t region0 = (uint64_t)blockIdx.x * F;
-    for (int i = tid; i < MAXF; i += kSliceBlock) {
+    for (int i = tid; i < MAXF; i += NTH) {
         cntb[0][i] = 0, cntb[1][i] = 0, posb[0][i] = 0, hd[i] = 0, abase[i] = 0;
         if (i < F) {
             // exact layout: regions start anywhere; chunks stay aligned to absolute multiples
@@ -561,7 +572,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     // CH, so even positions are 4-B / 16-B aligned)
     auto flush = [&](uint32_t M) {
         const uint32_t xl = (tid & (CH / 2 - 1)) * 2;
-        for (uint32_t c = tid / (CH / 2); c < M; c += kSliceBlock / (CH / 2)) {
+        for (uint32_t c = tid / (CH / 2); c < M; c += NTH / (CH / 2)) {
             const SliceChunk d = cdesc[c];
             const uint32_t coff = (d.pk & 255u) * CH, clim = (d.pk >> 8) & 127u, lo = (d.pk >> 15) & 127u,
                            hi = (d.pk >> 22) & 127u;
@@ -652,7 +663,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
     };
     if constexpr (EARLY) {
         __shared__ uint32_t dcnt[MAXF];
-        fused_prologue(fp, F, kmin, dcnt);
+        fused_prologue<NTH>(fp, F, kmin, dcnt);
     }
     if (tile < n_all) issue_tile(tile);
     for (; tile < n_all; tile += gridDim.x) {
@@ -719,7 +730,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
             }
             if (lane == 63) s_chunks = mi;
         } else if (have_prev) {
-            carry(cnb[pq], cntb[pq], lofsb[pq], tid - 64, kSliceBlock - 64);
+            carry(cnb[pq], cntb[pq], lofsb[pq], tid - 64, NTH - 64);
         }
         lds_barrier();  // B2: offsets ready, carries hold everything before tile t
 #pragma unroll
@@ -763,11 +774,11 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         flush(m_prev);
         lds_barrier();
         const int pq = par ^ 1;  // the last tile's buffers
-        carry(cnb[pq], cntb[pq], lofsb[pq], tid, kSliceBlock);
+        carry(cnb[pq], cntb[pq], lofsb[pq], tid, NTH);
         lds_barrier();
     }
     const uint32_t *cn = cnb[par], *pos = posb[par];
-    for (int p = tid; p < F * CH; p += kSliceBlock) {  // partial last chunks
+    for (int p = tid; p < F * CH; p += NTH) {  // partial last chunks
         const int b = p / CH, kx = p % CH;
         if (kx >= (int)cn[b]) continue;
         const uint64_t dst = (uint64_t)pos[b] + kx;
@@ -782,10 +793,162 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_partition(FastIn in, Pred
         }
     }
     if (ovf) *rg.overflow = 1u;
-    for (int b = tid; b < F; b += kSliceBlock) {
+    for (int b = tid; b < F; b += NTH) {
         const uint64_t n = (uint64_t)pos[b] + cn[b];
         rg.count[region0 + b] = (uint32_t)((n < cap ? n : cap) - hd[b]);
     }
+}
+
+// Phase A of the fused pipeline without staging (QEH_FUSED_RING=1): every selected row takes its
+// position in its slice's region from one LDS atomic on the slice's item count (no order inside a
+// region is needed), and is written straight into the slice's LDS rings -- keys into a 128-entry ring
+// flushed in 64-key (128-B) chunks, values into a 64-entry ring flushed in 32-value (256-B) chunks.
+// After a barrier the waves flush every whole chunk of their own slices (a quarter-wave per slice),
+// then a second barrier frees the ring slots: two barriers per tile, no scan, no staging copy, no
+// carry pass.  A row whose ring slot is still taken (more rows for one slice in one tile than the
+// ring has free, i.e. skewed keys) is stored straight to its region position instead; the chunk it
+// shares with ring items is then written from the ring past that direct prefix (dk / dv: where the
+// ring part of the window's first chunk starts).
+constexpr int kRingK = 128, kRingKC = 64, kRingV = 64, kRingVC = 32;
+#ifndef QEH_RING_PAIRS
+#define QEH_RING_PAIRS 4
+#endif
+constexpr int kRingPairs = QEH_RING_PAIRS;  // row pairs per lane: 8192-row tiles
+// Measured against the staged kernel (profiles/r04/ab_ring_vs_staged.txt, A/B x3 on one box): equal
+// within the box's drift (phase A 5.06-5.38 vs 5.05-5.36 ms; 4096-row tiles 0.05-0.1 ms slower), i.e.
+// the staging, carry and scan work is hidden under the stream and phase A sits at the mixed
+// read/write rate of its 29 GB; kept as an option, the staged kernel stays the default.
+template <int NTERMS, int NACOL, bool NT, int P>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_ring(FastIn in, PredTerms terms, int64_t n_tiles, SliceRegions rg,
+                                                            const SlicePlan *__restrict__ dplan, int64_t tail_rows,
+                                                            FusedPro fp) {
+    static_assert(NACOL <= 1, "one value column");
+    constexpr int R = 2 * P, TILE = kSliceBlock * R, MAXF = kSliceMaxF;
+    const SlicePlan pl = *dplan;
+    if (!pl.ok) return;
+    const int64_t kmin = pl.kmin;
+    const uint64_t range = pl.range, cap = pl.cap;
+    const int F = pl.F;
+    __shared__ uint32_t head[MAXF], fk[MAXF], fv[MAXF], dk[MAXF], dv[MAXF];
+    __shared__ uint16_t ring_k[MAXF * kRingK];
+    __shared__ int64_t ring_v[NACOL ? MAXF * kRingV : 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t region0 = (uint64_t)blockIdx.x * F;
+    {
+        __shared__ uint32_t dcnt[MAXF];
+        fused_prologue<kSliceBlock>(fp, F, kmin, dcnt);
+    }
+    for (int i = tid; i < MAXF; i += kSliceBlock) head[i] = 0, fk[i] = 0, fv[i] = 0, dk[i] = 0, dv[i] = 0;
+    __syncthreads();
+    bool ovf = false;
+    FastTile<NTERMS, NACOL, NT, P> ft;
+    const int64_t n_all = n_tiles + (tail_rows > 0 ? 1 : 0), lim = n_tiles * TILE + tail_rows;
+    auto issue_tile = [&](int64_t tl) {
+        const int64_t b = tl * TILE + (int64_t)wave * (64 * R) + 2 * lane;
+        if (tl < n_tiles) ft.issue(in, b);
+        else ft.issue_tail(in, b, lim);
+    };
+    // whole chunks of slice b below its count h, from the ring window [f, f + RS) (chunks past the
+    // window were stored directly); items below d were stored directly too
+    const int q16 = lane & 15;
+    auto flush_slice = [&](int b) {
+        const uint32_t h = head[b];
+        const uint64_t base = (region0 + b) * cap;
+        {
+            const uint32_t f = fk[b], d = dk[b];
+            uint32_t c0 = f;
+            for (; c0 + kRingKC <= h && c0 < f + kRingK; c0 += kRingKC) {
+                const uint32_t r0 = c0 + 4 * q16;
+                if (r0 + 4 > cap) { ovf = true; continue; }
+                const uint16_t *src = ring_k + b * kRingK + (r0 & (kRingK - 1));
+                if (r0 >= d) {
+                    *(uint2 *)(rg.key + base + r0) = *(const uint2 *)src;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (r0 + j >= d) rg.key[base + r0 + j] = src[j];
+                }
+            }
+            const uint32_t fn = h / kRingKC * kRingKC;
+            if (fn != f) {
+                // the new window's first chunk [fn, h): stored directly when it lay past the old window
+                const uint32_t dn = fn >= f + kRingK ? h : fn;
+                if (q16 == 0) fk[b] = fn, dk[b] = dn;
+            }
+        }
+        if constexpr (NACOL > 0) {
+            const uint32_t f = fv[b], d = dv[b];
+            uint32_t c0 = f;
+            for (; c0 + kRingVC <= h && c0 < f + kRingV; c0 += kRingVC) {
+                const uint32_t r0 = c0 + 2 * q16;
+                if (r0 + 2 > cap) { ovf = true; continue; }
+                const int64_t *src = ring_v + b * kRingV + (r0 & (kRingV - 1));
+                if (r0 >= d) {
+                    __builtin_nontemporal_store(*(const v2i64 *)src, (v2i64 *)(rg.val + base + r0));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        if (r0 + j >= d) __builtin_nontemporal_store(src[j], rg.val + base + r0 + j);
+                }
+            }
+            const uint32_t fn = h / kRingVC * kRingVC;
+            if (fn != f) {
+                const uint32_t dn = fn >= f + kRingV ? h : fn;
+                if (q16 == 0) fv[b] = fn, dv[b] = dn;
+            }
+        }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < n_all) issue_tile(tile);
+    for (; tile < n_all; tile += gridDim.x) {
+        ft.eval(in, terms);
+        uint32_t sel = ft.sel;
+        if (tile >= n_tiles) sel &= decltype(ft)::tail_mask(tile * TILE + (int64_t)wave * (64 * R) + 2 * lane, lim);
+        uint32_t off[R], pos[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t o = (uint64_t)ft.k(r) - (uint64_t)kmin;  // out of range -> huge, dropped
+            off[r] = (uint32_t)o;
+            pos[r] = 0;
+            if (((sel >> r) & 1) && o < range) pos[r] = atomicAdd(&head[(uint32_t)o >> kSliceBits], 1u);
+            else sel &= ~(1u << r);
+        }
+        int64_t vcur[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) vcur[r] = NACOL ? ft.a(0, r) : 0;
+        if (tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!((sel >> r) & 1)) continue;
+            const uint32_t b = off[r] >> kSliceBits, ps = pos[r];
+            if (ps >= cap) { ovf = true; continue; }
+            const uint16_t kv = (uint16_t)(off[r] & (kSliceKeys - 1));
+            if (ps < fk[b] + kRingK) ring_k[b * kRingK + (ps & (kRingK - 1))] = kv;
+            else rg.key[(region0 + b) * cap + ps] = kv;
+            if constexpr (NACOL > 0) {
+                if (ps < fv[b] + kRingV) ring_v[b * kRingV + (ps & (kRingV - 1))] = vcur[r];
+                else __builtin_nontemporal_store(vcur[r], rg.val + (region0 + b) * cap + ps);
+            }
+        }
+        lds_barrier();  // B1: this tile's items are in the rings
+        for (int b = wave * 4 + (lane >> 4); b < F; b += kSliceBlock / 16) flush_slice(b);
+        lds_barrier();  // B2: whole chunks written, windows moved
+    }
+    // the partial last chunks: ring items at and past d
+    for (int p = tid; p < F * kRingK; p += kSliceBlock) {
+        const int b = p / kRingK, x = p % kRingK;
+        const uint32_t h = head[b], r = fk[b] + x;
+        if (r < h && r >= dk[b] && r < cap) rg.key[(region0 + b) * cap + r] = ring_k[b * kRingK + (r & (kRingK - 1))];
+    }
+    if constexpr (NACOL > 0) {
+        for (int p = tid; p < F * kRingV; p += kSliceBlock) {
+            const int b = p / kRingV, x = p % kRingV;
+            const uint32_t h = head[b], r = fv[b] + x;
+            if (r < h && r >= dv[b] && r < cap) rg.val[(region0 + b) * cap + r] = ring_v[b * kRingV + (r & (kRingV - 1))];
+        }
+    }
+    if (ovf) *rg.overflow = 1u;
+    for (int b = tid; b < F; b += kSliceBlock) rg.count[region0 + b] = (uint32_t)(head[b] < cap ? head[b] : cap);
 }
 
 // Phase B.  Region slots are enumerated slice-major (slot = b * nreg + r);
@@ -3628,13 +3791,34 @@ constexpr int kFusedNotEligible = -4;
 
 static void launch_slice_partition_early(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol,
                                          int64_t n_tiles, int64_t tail_rows, int grid, const SliceRegions &rg,
-                                         const SlicePlan *dplan, const FusedPro &fp) {
+                                         const SlicePlan *dplan, const FusedPro &fp, bool two, bool ring) {
     const bool nt = fast_nt_mode() == 1;
     KernelTimer kta(ctx, "slice_partition");
     const HashTable t{};
+    if (ring) {
+#define QEH_SR(NTV, NAV, NTB)                                                                                            \
+    hipLaunchKernelGGL((k_slice_ring<NTV, NAV, NTB, kRingPairs>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,     \
+                       pp.terms, n_tiles, rg, dplan, tail_rows, fp)
+#define QEH_SR_NA(NTV, NTB)                 \
+    if (nacol == 0) { QEH_SR(NTV, 0, NTB); } \
+    else { QEH_SR(NTV, 1, NTB); }
+#define QEH_SR_NT(NTB)                         \
+    if (nterms == 0) { QEH_SR_NA(0, NTB) }     \
+    else if (nterms == 1) { QEH_SR_NA(1, NTB) } \
+    else { QEH_SR_NA(2, NTB) }
+        if (nt) { QEH_SR_NT(true) } else { QEH_SR_NT(false) }
+#undef QEH_SR_NT
+#undef QEH_SR_NA
+#undef QEH_SR
+        return;
+    }
 #define QEH_SE(NTV, NAV, NTB)                                                                                            \
-    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,  \
-                       pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
+    if (two)                                                                                                              \
+        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true, kSliceBlock / 2>), dim3(grid), dim3(kSliceBlock / 2), \
+                           0, ctx->stream, in, pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp);                       \
+    else                                                                                                                  \
+        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
+                           pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
 #define QEH_SE_NA(NTV, NTB)                 \
     if (nacol == 0) { QEH_SE(NTV, 0, NTB); } \
     else { QEH_SE(NTV, 1, NTB); }
@@ -3660,18 +3844,31 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     FastIn in;
     int nterms, nacol;
     if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 1) return kFusedNotEligible;
-    const int64_t tile_rows = nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE;
-    const int chunk = nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH;
+    // phase A: the staged kernel with one 1024-thread or two 512-thread workgroups per CU
+    // (QEH_FUSED_2WG=1), or the ring kernel (QEH_FUSED_RING=1)
+    const bool ring = std::getenv("QEH_FUSED_RING") && std::atoi(std::getenv("QEH_FUSED_RING")) == 1;
+    const bool two = !ring && std::getenv("QEH_FUSED_2WG") && std::atoi(std::getenv("QEH_FUSED_2WG")) == 1;
+    constexpr int H = kSliceBlock / 2;
+    const int64_t tile_rows = ring ? (int64_t)kSliceBlock * 2 * kRingPairs
+                              : two ? (nacol ? SliceShape<1, true, H>::TILE : SliceShape<0, true, H>::TILE)
+                                    : (nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE);
+    const int chunk = ring ? kRingKC
+                      : two ? (nacol ? SliceShape<1, true, H>::CH : SliceShape<0, true, H>::CH)
+                            : (nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH);
     const int64_t n_tiles = n / tile_rows, tail = n - n_tiles * tile_rows;
     if (n_tiles == 0) return kFusedNotEligible;
     AggSpecs specs = specs_in;
     const int64_t g_cap = std::min<int64_t>(kSliceStateWords / std::max(specs.n_slots, 1), 0xFFFE);
     const int64_t Gs = g_cap;  // states and outputs for every possible slot; empty slots are dropped
+    // one copy of the states: phase B folds each slice's LDS states into them once per workgroup, so
+    // same-address contention is low and the shard fold launch is not worth its place in the chain
+    // (A/B on one box, profiles/r04/ab_early_shape.txt); QEH_FUSED_SHARDS=1 restores the copies
     specs.shards = 1;
-    while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
-    if (std::getenv("QEH_NO_SHARDS")) specs.shards = 1;
+    if (std::getenv("QEH_FUSED_SHARDS"))
+        while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
     const int64_t n_all = n_tiles + (tail ? 1 : 0);
-    const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all, (int64_t)kMaxSliceGrid});
+    const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount * (two ? 2 : 1), n_all,
+                                             (int64_t)kMaxSliceGrid});
     const uint64_t tiles_per_wg = (uint64_t)((n_all + grid - 1) / grid);
 
     DevBuf mm, plan, ditems, dcount, kbuf, vbuf, cbuf, states, errw, gkeys, rep;
@@ -3729,14 +3926,15 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     fp.G = Gs;
     fp.as32 = gk.dtype == QEH_DT_INT32 ? 1 : 0;
     fp.plan = dplan;
-    launch_slice_partition_early(ctx, in, pp, nterms, nacol, n_tiles, tail, grid, rg, &dplan->sp, fp);
+    launch_slice_partition_early(ctx, in, pp, nterms, nacol, n_tiles, tail, grid, rg, &dplan->sp, fp, two, ring);
     {
         KernelTimer ktb(ctx, "slice_probe");
         DimSlices dim{ditems.as<uint32_t>(), dcount.as<uint32_t>(), st + 4, dplan};
         const bool pf = slice_probe_prefetch();
         const int gridB = ctx->props.multiProcessorCount;
         const HashTable t{};
-        static const bool pv = std::getenv("QEH_FUSED_PV") && std::atoi(std::getenv("QEH_FUSED_PV")) == 1;
+        // items loaded two per lane (PV, default; QEH_FUSED_PV=0: one per lane)
+        static const bool pv = !(std::getenv("QEH_FUSED_PV") && std::atoi(std::getenv("QEH_FUSED_PV")) == 0);
 #define QEH_SD(NAV, PFV, PVV)                                                                                              \
     hipLaunchKernelGGL((k_slice_probe<NAV, false, PFV, PVV, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg,   \
                        grid, 0, t, in, specs, Gs, states.as<uint64_t>(), dim)

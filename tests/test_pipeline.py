@@ -215,11 +215,13 @@ def test_fused_pipeline_vs_oracle(ctx, monkeypatch, n_fact, gdt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["dup_keys", "skewed_probe", "groups_too_many", "count_only", "min_max"])
+@pytest.mark.parametrize("case", ["dup_keys", "skewed_probe", "groups_too_many", "count_only", "min_max", "ring_overflow",
+                                  "ring_overflow_count"])
 def test_fused_pipeline_fallbacks_and_shapes(ctx, monkeypatch, case):
     """Cases the fused pipeline rejects on the device (duplicate build keys, a region overflow from
     probe keys skewed onto one slice, more groups than its LDS states) fall back to the general path
-    and stay equal to the oracle; COUNT-only (no value items) and MIN / MAX run fused."""
+    and stay equal to the oracle; COUNT-only (no value items), MIN / MAX and skew that overflows phase
+    A's rings but not its regions run fused."""
     monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
     n_fact, n_dim, groups = 600_000, 150_000, 512
     x, k, v, dk, dg = metric_data(n_fact, n_dim, groups)
@@ -236,6 +238,13 @@ def test_fused_pipeline_fallbacks_and_shapes(ctx, monkeypatch, case):
         want_fused = False
     elif case == "count_only":
         aggs = [(AF.Count, 2)]
+    elif case.startswith("ring_overflow"):
+        # 30 % of the probe rows in the first slice: hundreds of rows per slice per tile, far more than
+        # phase A's LDS rings hold, so most items are stored straight to their region positions
+        # (the region capacity still holds them: the run stays fused)
+        k[np.random.default_rng(5).random(n_fact) < 0.3] %= 1000
+        if case == "ring_overflow_count":
+            aggs = [(AF.Count, 2), (AF.Count, 0)]
     else:
         aggs = [(AF.Min, 2), (AF.Max, 2), (AF.Avg, 2), (AF.Count, 0)]
     probe = [(x, None), (k, None), (v, None)]
@@ -245,6 +254,25 @@ def test_fused_pipeline_fallbacks_and_shapes(ctx, monkeypatch, case):
     if want_fused:
         assert ran
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[j for j, (f, c) in enumerate(aggs) if f in (AF.Sum, AF.Avg)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["QEH_FUSED_RING", "QEH_FUSED_2WG"])
+@pytest.mark.parametrize("skew", [False, True])
+def test_fused_phase_a_variants(ctx, monkeypatch, variant, skew):
+    """The fused pipeline's optional phase-A kernels (the ring kernel without staging, and the staged
+    kernel as two 512-thread workgroups per CU) against the oracle, with uniform keys and with 30 %
+    of the probe rows on one slice (the ring kernel's direct stores past a full ring)."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    monkeypatch.setenv(variant, "1")
+    n_fact, n_dim, groups = 1_000_003, 400_000, 600
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, groups)
+    if skew:
+        k[np.random.default_rng(9).random(n_fact) < 0.3] %= 5000
+    probe = [(x, None), (k, None), (v, None)]
+    (gk, ga, wk, wa), ran = _fused_ran(ctx, lambda: run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS))
+    assert ran
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
 
 
 @pytest.mark.gpu

@@ -14,6 +14,8 @@
   merge   Merge::sorted of 8 partitions x 1.25e7 rows, ORDER BY k DESC NULLS LAST
   encode  pgwire DataRow text encoding of 1e7 result rows
   partition  device side of a hash Exchange, 1e8 rows into 8 partitions
+  cfg5leg    config 5's per-rank device leg at N = 8 (8-way exchange pass, local ROW_NUMBER over the
+             received rows, the unmove pass that returns the numbers to input order)
   cfg4leg    config 4's per-rank device leg at N = 8 (fused filter + 8-way exchange pass over 1e9
              rows, the dim shard's exchange pass, the local join of what the rank receives)
 
@@ -437,6 +439,71 @@ def cfg4_leg(ctx, scale, world=8):
                         "wall = sum of the legs"})
 
 
+def cfg5_leg(ctx, scale, world=8):
+    """BASELINE config 5's per-rank device leg at N = 8, on one GPU: what one rank of the distributed
+    ROW_NUMBER() OVER (PARTITION BY k ORDER BY v) runs besides the two RCCL all-to-alls
+    (DistributedExecutor.row_number -> _moved_window; window.rs:32-226 on each rank):
+      1. the 8-way hash exchange pass over the rank's 1.25e8 rows (qeh_partition_hash_move: k, v read
+         once, written partition-major);
+      2. the local ROW_NUMBER over what the rank receives: partition 0 of every rank's rows (the
+         1e9-row table is generated whole and each rank's 1/8 moved, so the received rows are the real
+         ones, source-rank-major);
+      3. the reverse pass (qeh_partition_hash_unmove): the row numbers that come back, partition-major,
+         gathered into the rank's input order.
+    Algorithmic bytes: 16 B read + 8 B written per row of the rank."""
+    n = int(1e9 * scale)
+    nr = n // world
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 20)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    rk, rv = ctx.slice(k, 0, nr), ctx.slice(v, 0, nr)  # rank 0's rows
+    recv_k, recv_v = [], []
+    for r in range(world):  # what rank 0 receives: partition 0 of every rank's rows, source-rank-major
+        c, m = ctx.partition_hash_move([ctx.slice(k, r * nr, nr)], world, [ctx.slice(k, r * nr, nr), ctx.slice(v, r * nr, nr)])
+        recv_k.append(ctx.concat([ctx.slice(m[0], 0, int(c[0]))]))
+        recv_v.append(ctx.concat([ctx.slice(m[1], 0, int(c[0]))]))
+        for q in m:
+            q.release()
+    rk_all, rv_all = ctx.concat(recv_k), ctx.concat(recv_v)
+    for q in recv_k + recv_v:
+        q.release()
+    recv = len(rk_all)
+    counts0, m0 = ctx.partition_hash_move([rk], world, [rk])
+    m0[0].release()
+    back = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 9, nr, 2 ** 30)  # stands in for the returned numbers
+
+    def leg1():
+        c, m = ctx.partition_hash_move([rk], world, [rk, rv])
+        for q in m:
+            q.release()
+        return c
+
+    def leg2():
+        rn = ctx.row_number([rk_all], [rv_all], [True])
+        rn.release()
+
+    def leg3():
+        out = ctx.partition_hash_unmove(rk, world, [back])
+        for q in out:
+            q.release()
+    names = ["partition_move", "radix_pass", "sort_encode", "row_number", "window_partition", "window_sort",
+             "window_place"]
+    w1, k1, _ = timed(ctx, leg1, 5, names)
+    w2, k2, _ = timed(ctx, leg2, 3, names)
+    w3, k3, _ = timed(ctx, leg3, 5, names)
+    kms2 = sum(v_ for n_, v_ in k2.items() if n_ != "partition_move")
+    legs = {"exchange_pass": {"ms": k1["partition_move"], "wall_ms": w1 * 1e3, "hbm_bytes_moved": 32.0 * nr},
+            "local_row_number": {"ms": kms2, "wall_ms": w2 * 1e3, "rows": recv, "kernels": {n_: v_ for n_, v_ in k2.items() if v_}},
+            "unmove_pass": {"ms": k3["partition_move"], "wall_ms": w3 * 1e3, "hbm_bytes_moved": 17.0 * nr}}
+    kms = k1["partition_move"] + kms2 + k3["partition_move"]
+    xgmi = (world - 1) / world * (16.0 * nr + 8.0 * recv)
+    line(f"cfg5 per-rank device leg at N={world} (ROW_NUMBER, 1e9 rows, 1/{world} per rank)", nr, w1 + w2 + w3,
+         24.0 * nr, kms, "k_part_scatter_small (exchange), k_window passes (local ROW_NUMBER), k_part_gather_small (unmove)",
+         None, {"legs": legs, "received_rows": recv, "rank0_partition_counts": [int(q) for q in counts0],
+                "xgmi_bytes_per_rank": xgmi,
+                "note": "frac on SURVEY §8(d)'s 24 B per row of the rank; RCCL all-to-all time excluded (8-GPU runs "
+                        "are the driver's); wall = sum of the legs"})
+
+
 def cfg_filter(ctx, scale):
     n = int(5e8 * scale)
     x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
@@ -522,7 +589,7 @@ def main():
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
          "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window,
-         "cfg4leg": cfg4_leg}[name](ctx, args.scale)
+         "cfg4leg": cfg4_leg, "cfg5leg": cfg5_leg}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()

@@ -15,7 +15,7 @@ timeout -k 10 600 python3 tools/exp_slice.py --rounds 3 libqeh_base.so libqeh_c3
 cat $O/ab.txt; [ $rc = 0 ] || exit $rc
 timeout -k 10 120 python3 tools/probes/host_overhead.py > $O/host.txt 2>&1 && QEH_NO_FUSED=1 timeout -k 10 120 python3 tools/probes/host_overhead.py >> $O/host.txt 2>&1
 cat $O/host.txt
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_distributed.py > $O/dist.txt 2>&1 || { echo dist tests failed; tail -30 $O/dist.txt; exit 1; }
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_distributed.py tests/test_partition.py > $O/dist.txt 2>&1 || { echo dist tests failed; tail -30 $O/dist.txt; exit 1; }
 tail -2 $O/dist.txt
 for m in "" "QEH_SYNC_TABLE_CHECK=1"; do
   env $m QEH_BENCH_RANK_OF=0/8 timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --cpu-sample 0 > $O/rank08.json 2>$O/rank08.err || { tail $O/rank08.err; exit 1; }
