@@ -295,12 +295,17 @@ struct RsDecode {
 // AT: tile ranks by LDS atomics (ds_add_rtn serves one instruction's lanes in lane order, so the
 // rank is stable: tools/ubench/lds_order_ubench.hip), else by ballot peers (QEH_RS_BALLOT=1, A/B).
 // ValT: the carried value -- a u32 row id, or (qeh_merge_sorted's payload sort) an 8-B payload.
-template <typename KeyT, bool AT = true, typename ValT = uint32_t, bool DEC = false, int KES = 0>
+// SEG (the MSD payload sort's second pass): block b's rows [lo, hi) and its offsets come from a
+// segment table (lo, hi, hb, nbb per block): offsets[hb + digit * nbb], so every block stays inside
+// one first-pass bucket and the scan orders (bucket, digit, block).
+template <typename KeyT, bool AT = true, typename ValT = uint32_t, bool DEC = false, int KES = 0, bool SEG = false,
+          typename KOutT = KeyT>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restrict__ keys, const ValT *__restrict__ vals,
                                                            int64_t n, int64_t seg, int shift, const uint64_t *__restrict__ offs,
-                                                           int nblocks, KeyT *__restrict__ keys_out,
+                                                           int nblocks, KOutT *__restrict__ keys_out,
                                                            ValT *__restrict__ vals_out, uint8_t *__restrict__ nd_out,
-                                                           int nshift, RsDecode dec, RsEncode enc) {
+                                                           int nshift, RsDecode dec, RsEncode enc,
+                                                           const int64_t *__restrict__ segtab = nullptr) {
     constexpr int W = kRsThreads / 64;
     constexpr int DW = kRadix / 64;       // waves that own one digit per lane in the bookkeeping
     __shared__ KeyT s_keys[kRsSTile];
@@ -311,8 +316,15 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     __shared__ uint32_t wsum[DW];
     __shared__ uint64_t run[kRadix];      // global position of the block's next element of each digit
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
-    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    int64_t lo, hi;
+    if constexpr (SEG) {
+        const int64_t *e = segtab + 4 * (int64_t)blockIdx.x;
+        lo = e[0], hi = e[1];
+        if (t < kRadix) run[t] = offs[e[2] + (int64_t)t * e[3]];
+    } else {
+        if (t < kRadix) run[t] = offs[(int64_t)t * nblocks + blockIdx.x];
+        lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    }
     KeyT k[kRsIpt];
     ValT v[kRsIpt];
     // loads are unconditional (indices clamped into [lo, hi)): no branches around
@@ -399,7 +411,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
                 else ((int64_t *)dec.out)[pos] = x;
                 if (dec.validb) dec.validb[pos] = ok ? 1 : 0;
             } else {
-                keys_out[pos] = key;
+                keys_out[pos] = (KOutT)key;  // (KOutT narrower: the low code bits the next stage needs)
             }
             vals_out[pos] = s_vals[p];
             if (nd_out) nd_out[pos] = (uint8_t)(key >> nshift);  // the next pass's digit (its histogram input)
@@ -820,7 +832,7 @@ static int radix_passes_t(qeh_ctx *ctx, RadixState &rs, int bits) {
         auto scat = rs_ballot(ctx) ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
         hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(),
                            nblocks, rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), next ? nd.as<uint8_t>() : nullptr,
-                           shift + kRadixBits, RsDecode{}, RsEncode{});
+                           shift + kRadixBits, RsDecode{}, RsEncode{}, nullptr);
         QEH_HIP(hipGetLastError());
         rs.cur = 1 - c;
     }
@@ -845,7 +857,7 @@ static int radix_pass_at(qeh_ctx *ctx, RadixState &rs, int shift) {
     QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
     auto scat = rs_ballot(ctx) ? k_rs_scatter<KeyT, false> : k_rs_scatter<KeyT, true>;
     hipLaunchKernelGGL(scat, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, rs.k[c].as<KeyT>(), rs.v[c].as<uint32_t>(), n, seg, shift, offs.as<uint64_t>(), nblocks,
-                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{}, RsEncode{});
+                       rs.k[1 - c].as<KeyT>(), rs.v[1 - c].as<uint32_t>(), nullptr, 0, RsDecode{}, RsEncode{}, nullptr);
     QEH_HIP(hipGetLastError());
     rs.cur = 1 - c;
     return QEH_OK;
@@ -1506,6 +1518,277 @@ __global__ void k_pack_valid(const uint8_t *__restrict__ vb, int64_t n, uint64_t
     }
 }
 
+// ---- MSD payload sort ----------------------------------------------------------------------
+// Codes of 24..45 bits over >= 2^20 rows: two stable 256-way passes on the top 16 bits (k_rs_scatter
+// over the whole array, then the same scatter inside every first-pass bucket: SEG blocks never straddle
+// a bucket and the scan orders (bucket, digit, block)), then one workgroup per sub-bucket sorts its
+// rows by the remaining low bits in LDS -- stable 8-bit LDS passes over (low code, row) pairs, ranks
+// by lane-ordered LDS atomics as the global passes -- and writes the decoded key, the payload
+// (gathered inside the sub-bucket) and the valid byte.  Three passes over the rows instead of
+// ceil(bits / 8) hist + scatter pairs.  A sub-bucket above kMsdCap rows is copied through when its
+// codes are all equal (the NULLs, a repeated key), else the caller redoes the sort on the LSD path.
+constexpr int kMsdCap = 4096;
+constexpr int kMsdThreads = 256;
+constexpr int kMsdBits = 16;  // code bits the two global passes consume
+constexpr uint32_t kMsdMaxBig = 255;  // sub-buckets above kMsdCap rows handled by k_msd_big
+constexpr int kMsdLdsBits = 9;        // digit of the in-LDS passes: 25 low bits in three passes
+constexpr int kMsdMaxLow = 29;        // low code bits the LDS sort packs beside a 12-bit row index
+
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist_u8_seg(const uint8_t *__restrict__ dg, const int64_t *__restrict__ segtab,
+                                                               uint32_t *__restrict__ hist) {
+    constexpr int W = kRsThreads / 64;
+    __shared__ uint32_t h[W][kRadix];
+    for (int i = threadIdx.x; i < W * kRadix; i += kRsThreads) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t *e = segtab + 4 * (int64_t)blockIdx.x;
+    const int64_t lo = e[0], hi = e[1];
+    const int wave = threadIdx.x >> 6;
+    const int64_t a = std::min<int64_t>(hi, (lo + 15) & ~(int64_t)15), b = std::max<int64_t>(a, hi & ~(int64_t)15);
+    for (int64_t i = lo + threadIdx.x; i < a; i += kRsThreads) atomicAdd(&h[wave][dg[i]], 1u);
+    for (int64_t i = b + threadIdx.x; i < hi; i += kRsThreads) atomicAdd(&h[wave][dg[i]], 1u);
+    for (int64_t i = a + 16 * (int64_t)threadIdx.x; i < b; i += 16 * (int64_t)kRsThreads) {
+        typedef unsigned int v4u32s __attribute__((ext_vector_type(4)));
+        const v4u32s w = __builtin_nontemporal_load((const v4u32s *)(dg + i));
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(&h[wave][(ws[q] >> (8 * r)) & 0xff], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kRadix) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) c += h[w][threadIdx.x];
+        hist[e[2] + (int64_t)threadIdx.x * e[3]] = c;
+    }
+}
+
+// sub-bucket (bucket b, digit d) starts: the scanned second-pass offset of the bucket's first block
+// (btab per bucket: hist base, blocks, start); sb[65536] = n
+__global__ void k_msd_sbstart(const uint64_t *__restrict__ offs2, const int64_t *__restrict__ btab, int64_t n,
+                              uint64_t *__restrict__ sb) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id > kRadix * kRadix) return;
+    if (id == kRadix * kRadix) {
+        sb[id] = (uint64_t)n;
+        return;
+    }
+    const int b = id >> kRadixBits, d = id & (kRadix - 1);
+    const int64_t base = btab[3 * b], nb = btab[3 * b + 1];
+    sb[id] = nb ? offs2[base * kRadix + (int64_t)d * nb] : (uint64_t)btab[3 * b + 2];
+}
+
+__device__ __forceinline__ void msd_emit(const RsDecode &dec, uint64_t *__restrict__ vout, int64_t pos, uint64_t c,
+                                         uint64_t val) {
+    const bool ok = !dec.validb || c != dec.null_code;
+    const int64_t x = ok ? (dec.asc ? (int64_t)(c - dec.bias + (uint64_t)dec.mn) : (int64_t)((uint64_t)dec.mx - (c - dec.bias)))
+                         : 0;
+    if (dec.dt == QEH_DT_INT32) ((int32_t *)dec.out)[pos] = (int32_t)x;
+    else ((int64_t *)dec.out)[pos] = x;
+    if (dec.validb) dec.validb[pos] = ok ? 1 : 0;
+    vout[pos] = val;
+}
+
+// one workgroup per sub-bucket (blockIdx.x = bucket << 8 | digit): the codes here share their top 16
+// bits; pass 2 left their low 32 bits.  Rows e = wave * 64 J + j * 64 + lane keep input order in
+// (wave, j, lane).  The first LDS pass ranks (low code, row e) and leaves packed words
+// (remaining code bits << 12 | e), so the later passes move one dword per row (lbits <= 29).
+__global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__restrict__ codes, const uint64_t *__restrict__ vin,
+                                                              const uint64_t *__restrict__ sb, int lbits, RsDecode dec,
+                                                              uint64_t *__restrict__ vout, uint32_t *__restrict__ flag,
+                                                              uint32_t *__restrict__ big) {
+    constexpr int W = kMsdThreads / 64, J = kMsdCap / kMsdThreads;
+    constexpr int DB = kMsdLdsBits, ND = 1 << DB, DPT = ND / kMsdThreads;  // digits per thread in the scan
+    constexpr int IB = 12;                                                 // row bits (kMsdCap = 2^12)
+    static_assert(kMsdCap == 1 << IB, "row index bits");
+    __shared__ uint32_t buf[2][kMsdCap];
+    __shared__ uint32_t wc[W][ND];
+    __shared__ uint32_t loc[ND], wsum[W];
+    const int64_t s0 = (int64_t)sb[blockIdx.x], s1 = (int64_t)sb[blockIdx.x + 1];
+    const int64_t m = s1 - s0;
+    if (m <= 0) return;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    if (m > kMsdCap) {  // k_msd_big takes it, with the whole grid
+        if (t == 0) {
+            const uint32_t q = atomicAdd(big, 1u);
+            if (q < kMsdMaxBig) big[1 + q] = blockIdx.x;
+            else atomicOr(flag, 1u);
+        }
+        return;
+    }
+    const int mm = (int)m;
+    const uint64_t hi_code = (uint64_t)blockIdx.x << lbits;
+    const uint32_t lmask = lbits >= 32 ? 0xFFFFFFFFu : ((1u << lbits) - 1u);
+    for (int e = t; e < mm; e += kMsdThreads) buf[0][e] = codes[s0 + e] & lmask;
+    int cur = 0;
+    for (int sh = 0; sh < lbits; sh += DB) {
+        const bool first = sh == 0;
+        for (int i = t; i < W * ND; i += kMsdThreads) (&wc[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t kk[J], rk[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int e = wave * 64 * J + j * 64 + lane;
+            const bool live = e < mm;
+            kk[j] = live ? buf[cur][e] : 0u;
+            // the first pass reads raw low codes; later passes packed words (digit above the row bits)
+            const uint32_t dg = first ? (kk[j] & (ND - 1)) : ((kk[j] >> IB) & (ND - 1));
+            rk[j] = live ? atomicAdd(&wc[wave][dg], 1u) : 0u;
+        }
+        __syncthreads();
+        // thread t owns digits t * DPT .. + DPT - 1: wave starts inside each digit, then one scan
+        uint32_t dt[DPT], tot = 0;
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) {
+            const int d = t * DPT + q;
+            uint32_t c0 = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = wc[w][d];
+                wc[w][d] = c0;
+                c0 += c;
+            }
+            dt[q] = c0;
+            tot += c0;
+        }
+        const uint32_t inc = wave_incl_scan(tot);
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wb = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) wb += w < wave ? wsum[w] : 0u;
+        uint32_t run = wb + inc - tot;
+#pragma unroll
+        for (int q = 0; q < DPT; ++q) {
+            loc[t * DPT + q] = run;
+            run += dt[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int e = wave * 64 * J + j * 64 + lane;
+            if (e >= mm) continue;
+            const uint32_t dg = first ? (kk[j] & (ND - 1)) : ((kk[j] >> IB) & (ND - 1));
+            const uint32_t p = loc[dg] + wc[wave][dg] + rk[j];
+            // packed: the code bits above this pass's digit, then the row
+            buf[cur ^ 1][p] = first ? (((kk[j] >> DB) << IB) | (uint32_t)e)
+                                    : ((((kk[j] >> IB) >> DB) << IB) | (kk[j] & (kMsdCap - 1)));
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // every pass ran (lbits > 0): buf holds rows in code order; the code is re-read from the row
+    for (int e = t; e < mm; e += kMsdThreads) {
+        const uint32_t r = buf[cur][e] & (kMsdCap - 1);
+        msd_emit(dec, vout, s0 + e, hi_code | (codes[s0 + r] & lmask), vin[s0 + r]);
+    }
+}
+
+// The sub-buckets above kMsdCap rows (big[0] of them, ids in big[1..]), every workgroup of the grid on
+// each in turn: rows whose codes all equal the first one (the NULLs, one repeated key) are already in
+// order and are copied through; any other code sets the redo flag (the LSD passes then rewrite all).
+__global__ __launch_bounds__(256) void k_msd_big(const uint32_t *__restrict__ codes, const uint64_t *__restrict__ vin,
+                                                 const uint64_t *__restrict__ sb, int lbits, RsDecode dec, uint64_t *__restrict__ vout,
+                                                 uint32_t *__restrict__ flag, const uint32_t *__restrict__ big) {
+    const uint32_t nbig = big[0] < kMsdMaxBig ? big[0] : kMsdMaxBig;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (uint32_t q = 0; q < nbig; ++q) {
+        const uint32_t id = big[1 + q];
+        const int64_t s0 = (int64_t)sb[id], s1 = (int64_t)sb[id + 1];
+        const uint32_t c0 = codes[s0];
+        const uint64_t full = ((uint64_t)id << lbits) | c0;
+        bool bad = false;
+        for (int64_t i = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < s1; i += stride) {
+            if (codes[i] != c0) bad = true;
+            else msd_emit(dec, vout, i, full, vin[i]);
+        }
+        if (bad) atomicOr(flag, 1u);
+    }
+}
+
+// Returns QEH_OK (outputs written, validity bytes in validb) or kMsdRedo (a sub-bucket too large to
+// sort in LDS: the caller runs the LSD passes over the same buffers).
+constexpr int kMsdRedo = -5;
+static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_t *vsrc, int64_t n, int bits, const RsEncode &enc,
+                              const RsDecode &dec, uint64_t *kb0, uint64_t *kb1, uint64_t *vtmp, uint64_t *vout) {
+    const bool k32 = key.dtype == QEH_DT_INT32;
+    const int cus = ctx->props.multiProcessorCount;
+    const int nblocks = (int)std::min<int64_t>(std::max<int64_t>((n + kRsSTile - 1) / kRsSTile, 1), (int64_t)cus);
+    const int64_t seg = (n + nblocks - 1) / nblocks;
+    const int shift1 = bits - kRadixBits, shift2 = bits - kMsdBits;
+    DevBuf hist, offs, nd, vtmp2, tabd, btabd, sbd, flag;
+    QEH_TRY(hist.alloc(ctx, (size_t)kRadix * nblocks * 4));
+    QEH_TRY(offs.alloc(ctx, (size_t)kRadix * nblocks * 8));
+    QEH_TRY(nd.alloc(ctx, (size_t)n + 16));
+    QEH_TRY(vtmp2.alloc(ctx, (size_t)n * 8));
+    QEH_TRY(sbd.alloc(ctx, ((size_t)kRadix * kRadix + 1) * 8));
+    QEH_TRY(flag.alloc(ctx, 8 + 4 * (kMsdMaxBig + 1)));
+    {
+        KernelTimer kt(ctx, "radix_pass");
+        auto hk = k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
+        hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, n, seg, shift1, hist.as<uint32_t>(), nblocks, enc);
+        QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
+        auto sk = k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4> : k_rs_scatter<uint64_t, true, uint64_t, false, 8>;
+        hipLaunchKernelGGL(sk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, vsrc, n, seg, shift1, offs.as<uint64_t>(),
+                           nblocks, kb1, vtmp, nd.as<uint8_t>(), shift2, dec, enc, nullptr);
+        QEH_HIP(hipGetLastError());
+    }
+    // the buckets' starts (the scanned offsets of block 0), then blocks of <= S rows inside each bucket
+    std::vector<uint64_t> bst(kRadix + 1);
+    QEH_HIP(hipMemcpy2DAsync(bst.data(), 8, offs.p, (size_t)nblocks * 8, 8, kRadix, hipMemcpyDeviceToHost, ctx->stream));
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
+    bst[kRadix] = (uint64_t)n;
+    // ~4 blocks per CU: the buckets differ in size, so many shorter blocks balance the last round
+    const int64_t S = std::max<int64_t>(kRsSTile, ((n + 4 * cus - 1) / (4 * cus) + kRsSTile - 1) / kRsSTile * kRsSTile);
+    std::vector<int64_t> tab, btab;
+    int64_t base = 0;
+    for (int b = 0; b < kRadix; ++b) {
+        const int64_t lo = (int64_t)bst[b], hi = (int64_t)bst[b + 1], size = hi - lo;
+        const int64_t nb = size > 0 ? (size + S - 1) / S : 0;
+        for (int64_t j = 0; j < nb; ++j) {
+            tab.push_back(lo + j * S);
+            tab.push_back(std::min<int64_t>(lo + (j + 1) * S, hi));
+            tab.push_back(base * kRadix + j);
+            tab.push_back(nb);
+        }
+        btab.push_back(base);
+        btab.push_back(nb);
+        btab.push_back(lo);
+        base += nb;
+    }
+    const int64_t B = base;
+    QEH_TRY(tabd.alloc(ctx, tab.size() * 8));
+    QEH_TRY(btabd.alloc(ctx, btab.size() * 8));
+    QEH_HIP(hipMemcpyAsync(tabd.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    QEH_HIP(hipMemcpyAsync(btabd.p, btab.data(), btab.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    DevBuf hist2, offs2;
+    QEH_TRY(hist2.alloc(ctx, (size_t)kRadix * B * 4));
+    QEH_TRY(offs2.alloc(ctx, (size_t)kRadix * B * 8));
+    {
+        KernelTimer kt(ctx, "radix_pass");
+        hipLaunchKernelGGL(k_rs_hist_u8_seg, dim3((unsigned)B), dim3(kRsThreads), 0, ctx->stream, nd.as<uint8_t>(), tabd.as<int64_t>(),
+                           hist2.as<uint32_t>());
+        QEH_TRY(exclusive_scan_u32(ctx, hist2.as<uint32_t>(), offs2.as<uint64_t>(), (int64_t)kRadix * B, nullptr));
+        uint32_t *codes2 = (uint32_t *)kb0;  // the low 32 code bits: all the LDS sort needs (lbits <= 29)
+        hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t, false, 0, true, uint32_t>), dim3((unsigned)B), dim3(kRsThreads), 0,
+                           ctx->stream, kb1, vtmp, n, 0, shift2, offs2.as<uint64_t>(), (int)B, codes2, vtmp2.as<uint64_t>(), nullptr, 0,
+                           dec, enc, tabd.as<int64_t>());
+        hipLaunchKernelGGL(k_msd_sbstart, dim3((kRadix * kRadix + 256) / 256), dim3(256), 0, ctx->stream, offs2.as<uint64_t>(),
+                           btabd.as<int64_t>(), n, sbd.as<uint64_t>());
+        QEH_HIP(hipMemsetAsync(flag.p, 0, 16, ctx->stream));
+        uint32_t *bigl = flag.as<uint32_t>() + 2;
+        hipLaunchKernelGGL(k_msd_lds_sort, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2, vtmp2.as<uint64_t>(),
+                           sbd.as<uint64_t>(), shift2, dec, vout, flag.as<uint32_t>(), bigl);
+        hipLaunchKernelGGL(k_msd_big, dim3(cus * 4), dim3(256), 0, ctx->stream, codes2, vtmp2.as<uint64_t>(), sbd.as<uint64_t>(),
+                           shift2, dec, vout, flag.as<uint32_t>(), bigl);
+        QEH_HIP(hipGetLastError());
+    }
+    uint32_t redo = 0;
+    QEH_TRY(read_small(ctx, &redo, flag.p, 4));
+    return redo ? kMsdRedo : QEH_OK;
+}
+
 int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_column &val, bool asc, bool nulls_first,
                             qeh_column *out_key, qeh_column *out_val) {
     const int64_t n = key.length;
@@ -1562,7 +1845,35 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     const RsEncode enc{kc, mn, mx, bias, null_code, asc ? 1 : 0};
     const RsDecode dec{mn, mx, bias, null_code, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
     const bool k32 = key.dtype == QEH_DT_INT32;
-    for (int p = 0; p < npass && s == QEH_OK; ++p) {
+    // codes of 24..45 bits over many rows: the MSD passes (three passes over the rows); a sub-bucket
+    // too large for its LDS sort sends the job on to the LSD passes below.  The NULL code gets a
+    // sub-bucket (top 16 bits) of its own: the first one (NULLS FIRST: values biased past it) or the
+    // one after the largest value's, so the NULLs are copied through instead of sharing an LDS sort.
+    int mbits = 0;
+    uint64_t mbias = 0, mnull = 0;
+    if (s == QEH_OK && bits >= 24 && n >= ((int64_t)1 << 20) && !std::getenv("QEH_NO_MSD_SORT") &&
+        range < (1ull << (kMsdBits + kMsdMaxLow))) {
+        for (int bm = std::max(24, bits); bm <= kMsdBits + kMsdMaxLow && !mbits; ++bm) {
+            const int s2 = bm - kMsdBits;
+            const uint64_t top = range >> s2;  // the largest value's sub-bucket (unbiased)
+            if (!nullable) mbits = bm;
+            else if (top + 1 < (1ull << kMsdBits)) {
+                mbits = bm;
+                if (nulls_first) mbias = 1ull << s2, mnull = 0;
+                else mnull = (top + 1) << s2;
+            }
+        }
+    }
+    bool done = false;
+    if (mbits) {
+        const RsEncode encm{kc, mn, mx, mbias, mnull, asc ? 1 : 0};
+        const RsDecode decm{mn, mx, mbias, mnull, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
+        const int r = msd_payload_passes(ctx, key, vsrc, n, mbits, encm, decm, kb[0].as<uint64_t>(), kb[1].as<uint64_t>(),
+                                         vtmp.as<uint64_t>(), (uint64_t *)out_val->values);
+        if (r == QEH_OK) done = true;
+        else if (r != kMsdRedo) s = r;
+    }
+    for (int p = 0; p < npass && s == QEH_OK && !done; ++p) {
         KernelTimer kt(ctx, "radix_pass");
         const int c = p & 1, shift = p * kRadixBits;
         const bool first = p == 0, last = p + 1 == npass;
@@ -1576,7 +1887,7 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
                                 : (k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4> : k_rs_scatter<uint64_t, true, uint64_t, false, 8>))
                         : (last ? k_rs_scatter<uint64_t, true, uint64_t, true, 0> : k_rs_scatter<uint64_t, true, uint64_t, false, 0>);
         hipLaunchKernelGGL(sk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), vin, n, seg, shift,
-                           offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(), vb[1 - c], nullptr, 0, dec, enc);
+                           offs.as<uint64_t>(), nblocks, kb[1 - c].as<uint64_t>(), vb[1 - c], nullptr, 0, dec, enc, nullptr);
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "payload sort: pass launch failed");
     }
     if (s == QEH_OK && nullable) {

@@ -594,13 +594,21 @@ class DistributedExecutor:
             out = torch.empty(self.world * row.numel(), dtype=torch.int64, device="cuda")
             dist.all_gather_into_tensor(out, row, group=self.group)
             row = out
+        # the rows' copy to the host is queued ahead of phase A: a copy queued behind it would wait for
+        # phase A's workgroups to leave the CUs (the copy engine's blit kernel needs a CU), so the host
+        # would sit idle for the whole of phase A before it could queue the build and phase B
+        row_host = torch.empty(row.numel(), dtype=torch.int64, pin_memory=True)
+        row_host.copy_(row, non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record()
         prelaunched = False
         if probe is not None and not os.environ.get("QEH_HOST_PLAN"):
             # phase A planned on the device from the gathered rows: it starts while the host reads them
             self._sync_torch()
             self.ctx.join_filter_aggregate_prelaunch_stats(*probe, row.data_ptr(), self.world, 5 + len(flags))
             prelaunched = True
-        M = row.cpu().numpy().reshape(self.world, -1)
+        copied.synchronize()
+        M = row_host.numpy().reshape(self.world, -1)
         rows = [int(x) for x in M[:, 0]]
         total = sum(rows)
         out = {"M": M, "rows": rows, "total": total, "n": n, "ts": ts, "bitmap": bool(M[:, 5].max() > 0),

@@ -171,3 +171,54 @@ def test_merge_sorted_payload_full_range_keys(ctx, asc, nf, nulls):
     assert np.array_equal(gm, kv[perm])
     assert np.array_equal(gk[gm], k[perm][kv[perm]])
     assert np.array_equal(gv, v[perm])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bench_shape", "ties_25_bits", "skew_redo", "constant_big", "int32_full", "asc_nulls_first",
+                                  "45_bits"])
+def test_merge_sorted_msd_payload_vs_oracle(ctx, monkeypatch, case):
+    """The MSD payload sort (codes of 24..48 bits over >= 2^20 rows: two global 256-way passes on the top
+    16 bits, then an LDS sort per sub-bucket): equal to the oracle's stable sort and to the LSD passes
+    (QEH_NO_MSD_SORT=1) -- the Merge::sorted bench shape, many ties, a sub-bucket too large for LDS
+    (the LSD redo), a large sub-bucket of one repeated key (copied through), Int32 keys over their
+    whole range, NULLs first, 45-bit codes (the widest the LDS sort packs)."""
+    r = np.random.default_rng(23)
+    n = (1 << 20) + 12_345
+    dt, asc, nf, nulls = np.int64, False, False, True
+    k = r.integers(0, 2 ** 40, n, dtype=np.int64)
+    if case == "ties_25_bits":
+        k = r.integers(-(2 ** 23), 2 ** 23, n, dtype=np.int64)
+        asc = True
+    elif case == "skew_redo":
+        k[r.random(n) < 0.3] %= 100_000  # one sub-bucket of ~300K distinct-ish keys
+    elif case == "constant_big":
+        k[r.random(n) < 0.2] = 123_456_789_012
+        asc = True
+    elif case == "int32_full":
+        k = r.integers(-(2 ** 31), 2 ** 31 - 1, n, dtype=np.int64).astype(np.int32)
+        k[:2] = [-(2 ** 31), 2 ** 31 - 1]
+        dt, nulls = np.int32, False
+    elif case == "asc_nulls_first":
+        asc, nf = True, True
+    elif case == "45_bits":
+        k = r.integers(-(2 ** 43), 2 ** 43, n, dtype=np.int64)
+        nulls = False
+    kv = r.random(n) > 0.05 if nulls else np.ones(n, bool)
+    v = r.random(n)
+    cuts = [0, n // 3, n // 3 + 7, n]
+    parts = [[ctx.upload(k[a:b], kv[a:b]) if nulls else ctx.upload(k[a:b]), ctx.upload(v[a:b])] for a, b in zip(cuts[:-1], cuts[1:])]
+    perm = ob.sort_indices_nulls([ob.HostCol(k.astype(np.int64), kv)], [asc], [nf])
+    outs = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("QEH_NO_MSD_SORT", env)
+        cols, rows = ctx.merge_sorted(parts, [0], [asc], [nf])
+        assert rows == n
+        gk, gm = host(cols[0])
+        gv, _ = host(cols[1])
+        assert np.array_equal(gm, kv[perm])
+        assert np.array_equal(gk[gm], k[perm][kv[perm]])
+        assert np.array_equal(gv, v[perm])
+        assert cols[0].dtype == (abi.DT_INT32 if dt == np.int32 else abi.DT_INT64)
+        outs.append(gv)
+    assert np.array_equal(outs[0], outs[1])
