@@ -297,6 +297,11 @@ int qeh_join_filter_aggregate_prelaunch_stats(qeh_ctx *ctx, const qeh_column *pr
  *     same probe columns, predicate, aggregates and key range. */
 int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
                                   int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table);
+/* The same insert without the range check's host wait: rows outside the ranges are skipped (not an
+ * error), which the caller's non-empty count (qeh_u16_count_nonzero_dev) then shows as missing rows.
+ * The distributed step queues it while phase A runs. */
+int qeh_direct_group_table_insert_async(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
+                                        int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table);
 int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out);
 /* The same count into device memory (*dev_out, 8 B, overwritten), no host wait: the distributed step
  * reads it with its final results instead of stalling the queue between the table sum and the probe. */

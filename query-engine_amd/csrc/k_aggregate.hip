@@ -2255,10 +2255,15 @@ struct SlicePre {
     SliceRegions rg{};
     hipEvent_t done = nullptr;
     bool dev_planned = false;  // launched from a plan in device memory, not yet read back (resolve_dev_plan)
+    hipEvent_t plan_copied = nullptr;  // the plan's copy into ctx->pinned_plan (queued ahead of phase A)
     ~SlicePre() {
         if (done) {  // the buffers below must outlive the kernel
             (void)hipEventSynchronize(done);
             (void)hipEventDestroy(done);
+        }
+        if (plan_copied) {
+            (void)hipEventSynchronize(plan_copied);
+            (void)hipEventDestroy(plan_copied);
         }
     }
 };
@@ -2436,6 +2441,17 @@ static int slice_launch_dev(qeh_ctx *ctx, const ColSet &cols, int64_t n, const P
     rg.overflow = rg.count + nreg_max;
     QEH_HIP(hipMemsetAsync(rg.overflow, 0, 4, ctx->stream));
     launch_plan(*pi, pre->planbuf.as<SlicePlan>());
+    // the plan's host copy goes ahead of phase A: a copy queued behind it would wait for phase A's
+    // workgroups to leave the CUs, and with it the host that reads the plan
+    if (!ctx->pinned_plan && hipHostMalloc(&ctx->pinned_plan, sizeof(SlicePlan), hipHostMallocDefault) != hipSuccess)
+        ctx->pinned_plan = nullptr;
+    if (ctx->pinned_plan && hipEventCreateWithFlags(&pre->plan_copied, hipEventDisableTiming) == hipSuccess) {
+        if (hipMemcpyAsync(ctx->pinned_plan, pre->planbuf.p, sizeof(SlicePlan), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipEventRecord(pre->plan_copied, ctx->stream) != hipSuccess) {
+            (void)hipEventDestroy(pre->plan_copied);
+            pre->plan_copied = nullptr;
+        }
+    }
     (void)hipEventRecord(ready, ctx->stream);  // inputs, the plan and the overflow reset
     (void)hipStreamWaitEvent(side, ready, 0);
     launch_slice_partition(ctx, in, pp, nterms, nacol, 0, 0, n_tiles, pi->grid, rg, side, nullptr,
@@ -2477,7 +2493,14 @@ static void settle_dev_plan(qeh_ctx *ctx, SlicePre *pre, const SlicePlan &pl) {
 // The plan of a device-planned launch read back (one small read; the plan kernel ran long before).
 static int resolve_dev_plan(qeh_ctx *ctx, SlicePre *pre, BuildRanges *br) {
     SlicePlan pl{};
-    QEH_TRY(read_small(ctx, &pl, pre->planbuf.p, sizeof pl));
+    if (pre->plan_copied) {  // copied ahead of phase A: wait for that copy only
+        QEH_HIP(hipEventSynchronize(pre->plan_copied));
+        (void)hipEventDestroy(pre->plan_copied);
+        pre->plan_copied = nullptr;
+        std::memcpy(&pl, ctx->pinned_plan, sizeof pl);
+    } else {
+        QEH_TRY(read_small(ctx, &pl, pre->planbuf.p, sizeof pl));
+    }
     for (int q = 0; q < 2; ++q) br->mn[q] = pl.src[3 * q], br->mx[q] = pl.src[3 * q + 1], br->cnt[q] = pl.src[3 * q + 2];
     settle_dev_plan(ctx, pre, pl);
     return QEH_OK;

@@ -318,8 +318,21 @@ __global__ void k_direct_group_insert(ColRef key, ColRef gkey, int64_t n, int64_
     }
 }
 
+static int direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key, int64_t key_min,
+                                     uint64_t key_range, int64_t group_min, uint16_t *table, bool check);
+
 extern "C" int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
                                              int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table) {
+    return direct_group_table_insert(ctx, build_key, group_key, key_min, key_range, group_min, table, true);
+}
+
+extern "C" int qeh_direct_group_table_insert_async(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key,
+                                                   int64_t key_min, uint64_t key_range, int64_t group_min, uint16_t *table) {
+    return direct_group_table_insert(ctx, build_key, group_key, key_min, key_range, group_min, table, false);
+}
+
+static int direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key, int64_t key_min,
+                                     uint64_t key_range, int64_t group_min, uint16_t *table, bool check) {
     if (!ctx || !build_key || !group_key || !table || key_range == 0)
         return fail(QEH_E_INVALID, "qeh_direct_group_table_insert: bad argument");
     if (build_key->length != group_key->length) return fail(QEH_E_INVALID, "build columns have different lengths");
@@ -339,6 +352,10 @@ extern "C" int qeh_direct_group_table_insert(qeh_ctx *ctx, const qeh_column *bui
                            make_colref(*build_key), make_colref(*group_key), n, key_min, key_range, group_min, table,
                            bad.as<uint32_t>());
         QEH_HIP(hipGetLastError());
+    }
+    if (!check) {  // rows outside the range are skipped: the caller's non-empty count shows them
+        // (the flag buffer is freed to the pool in stream order)
+        return QEH_OK;
     }
     uint32_t b = 0;
     QEH_TRY(read_small(ctx, &b, bad.p, 4));

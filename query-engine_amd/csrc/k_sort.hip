@@ -1528,7 +1528,7 @@ __global__ void k_pack_valid(const uint8_t *__restrict__ vb, int64_t n, uint64_t
 // ceil(bits / 8) hist + scatter pairs.  A sub-bucket above kMsdCap rows is copied through when its
 // codes are all equal (the NULLs, a repeated key), else the caller redoes the sort on the LSD path.
 constexpr int kMsdCap = 4096;
-constexpr int kMsdThreads = 256;
+constexpr int kMsdThreads = 512;
 constexpr int kMsdBits = 16;  // code bits the two global passes consume
 constexpr uint32_t kMsdMaxBig = 255;  // sub-buckets above kMsdCap rows handled by k_msd_big
 constexpr int kMsdLdsBits = 9;        // digit of the in-LDS passes: 25 low bits in three passes
@@ -1600,6 +1600,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
                                                               uint32_t *__restrict__ big) {
     constexpr int W = kMsdThreads / 64, J = kMsdCap / kMsdThreads;
     constexpr int DB = kMsdLdsBits, ND = 1 << DB, DPT = ND / kMsdThreads;  // digits per thread in the scan
+    static_assert(DPT >= 1, "one digit per thread at least");
     constexpr int IB = 12;                                                 // row bits (kMsdCap = 2^12)
     static_assert(kMsdCap == 1 << IB, "row index bits");
     __shared__ uint32_t buf[2][kMsdCap];

@@ -82,6 +82,9 @@ struct qeh_ctx {
     // pinned host staging for small device->host results
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
+    // pinned host copy of a device-planned phase A's plan (queued ahead of phase A, so reading it
+    // back does not wait behind work queued after phase A)
+    void *pinned_plan = nullptr;
     // timing
     bool timing = false;
     std::vector<qeh::TimingRecord> timing_pending;

@@ -233,6 +233,7 @@ int qeh_shutdown(qeh_ctx *ctx) {
     }
     for (auto e : ctx->event_free) hipEventDestroy(e);
     if (ctx->scratch) ctx->pool->free(ctx->scratch);
+    if (ctx->pinned_plan) hipHostFree(ctx->pinned_plan);
     if (ctx->pinned) hipHostFree(ctx->pinned);
     ctx->pending_slice.reset();  // waits for a prelaunched phase A; its buffers go back to the pool
     ctx->source_cache.reset();  // its columns go back to the pool first

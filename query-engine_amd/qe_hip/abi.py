@@ -85,6 +85,7 @@ SIGNATURES = {
                                       C.POINTER(I64)]),
     "qeh_join_filter_aggregate_prelaunch": (I, [P, COLP, I, I, EXPRP, AGGP, I, C.POINTER(I64), C.POINTER(I64)]),
     "qeh_direct_group_table_insert": (I, [P, COLP, COLP, I64, U64, I64, P]),
+    "qeh_direct_group_table_insert_async": (I, [P, COLP, COLP, I64, U64, I64, P]),
     "qeh_u16_count_nonzero": (I, [P, P, U64, C.POINTER(I64)]),
     "qeh_u16_count_nonzero_dev": (I, [P, P, U64, P]),
     "qeh_columns_minmax": (I, [P, COLP, I, C.POINTER(I64)]),

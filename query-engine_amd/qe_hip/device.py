@@ -375,10 +375,11 @@ class Context:
                 [self._wrap(oa[i]) for i in range(len(aggs))], g.value)
 
     def direct_group_table_insert(self, build_key: DeviceColumn, group_key: DeviceColumn, key_min: int,
-                                  key_range: int, group_min: int, table_ptr: int) -> None:
-        """qeh_direct_group_table_insert: this shard's rows into the caller's zeroed u16 table."""
-        abi.check(self.lib.qeh_direct_group_table_insert(self.h, C.byref(build_key.c), C.byref(group_key.c), key_min,
-                                                         key_range, group_min, table_ptr))
+                                  key_range: int, group_min: int, table_ptr: int, check: bool = True) -> None:
+        """qeh_direct_group_table_insert: this shard's rows into the caller's zeroed u16 table
+        (check=False: qeh_direct_group_table_insert_async, no host wait; out-of-range rows skipped)."""
+        fn = self.lib.qeh_direct_group_table_insert if check else self.lib.qeh_direct_group_table_insert_async
+        abi.check(fn(self.h, C.byref(build_key.c), C.byref(group_key.c), key_min, key_range, group_min, table_ptr))
 
     def columns_minmax(self, cols: Sequence[DeviceColumn]) -> List[Tuple[int, int, int]]:
         """qeh_columns_minmax: [(min, max, non-null count)] of Int32 / Int64 columns, one read."""

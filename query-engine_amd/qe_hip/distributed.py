@@ -646,16 +646,20 @@ class DistributedExecutor:
                                                      st["grange"])
         table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
         self._sync_torch()  # zeroed before the library writes
+        lanes_ok = (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
+                    and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
+                            for j, (f, c) in enumerate(aggs)))
+        no_wait = lanes_ok and not os.environ.get("QEH_SYNC_TABLE_CHECK")
         if st["n"]:
-            self.ctx.direct_group_table_insert(build_key, build_group_keys[0], kmin, R, gmin, table.data_ptr())
+            # the ranges are the job's own min / max, so every row is in range; the no-wait form skips
+            # the range check's host read (a row it skipped would show in the non-empty count below)
+            self.ctx.direct_group_table_insert(build_key, build_group_keys[0], kmin, R, gmin, table.data_ptr(),
+                                               check=not no_wait)
         self._sync()
         if self.world > 1:
             dist.all_reduce(table, op=dist.ReduceOp.SUM, group=self.group)  # u16 pairs: no carries (checked above)
         self._sync_torch()
-        lanes_ok = (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
-                    and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
-                            for j, (f, c) in enumerate(aggs)))
-        if lanes_ok and not os.environ.get("QEH_SYNC_TABLE_CHECK"):
+        if no_wait:
             # no host wait until the final states: the duplicate check (non-empty entries of the summed
             # table, the same on every rank) and the operator's status words (error bits, a slice region
             # overflow on this rank) stay on the device; the status rides the lanes' all-reduce as one
