@@ -3859,6 +3859,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
                                        const AggSpecs &specs_in, int key_col, const qeh_column &bk, const qeh_column &gk,
                                        qeh_column *out_keys, qeh_column *out_aggs, int64_t *out_groups) {
     if (std::getenv("QEH_NO_FUSED") || std::getenv("QEH_NO_SLICES")) return kFusedNotEligible;
+    const size_t timing_mark = ctx->timing_pending.size();
     const bool bk_nulls = bk.validity && bk.null_count != 0, gk_nulls = gk.validity && gk.null_count != 0;
     if (bk.dtype != QEH_DT_INT64 || bk_nulls || (gk.dtype != QEH_DT_INT64 && gk.dtype != QEH_DT_INT32) || gk_nulls)
         return kFusedNotEligible;
@@ -4026,6 +4027,11 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     int s = hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "fused join-aggregate: launch failed");
     if (s == QEH_OK) s = read_small(ctx, sw, errw.p, 32);  // the one host round trip of the query
     if (s == QEH_OK && !sw[0] && (!sw[5] || sw[1] || sw[4])) s = kFusedNotEligible;  // plan, overflow, duplicates
+    if (s == kFusedNotEligible && !sw[5]) {
+        // the device plan declined: every kernel of this call returned at once, so its timing records
+        // are not a query's phases (the general path that follows records its own)
+        for (size_t i = timing_mark; i < ctx->timing_pending.size(); ++i) ctx->timing_pending[i].name += "_declined";
+    }
     if (s == QEH_OK) s = kernel_error_status(sw[0], "aggregate");
     if (s != QEH_OK) {
         cleanup();
