@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/qeh_plan.h"
 #include "device_common.h"
@@ -88,6 +89,8 @@ typedef unsigned int v4u32w __attribute__((ext_vector_type(4)));
 struct WmShape {
     int64_t n;
     int64_t kmin;
+    uint64_t kmask;    // key offset = (k - kmin) & kmask: all ones, or 2^20 - 1 with kmin = 0 (keys mod 2^20,
+                       // one-to-one over any key range <= 2^20, so the histogram needs no minimum first)
     int32_t lb;        // low key bits (pass 2 digit); high digit = (k - kmin) >> lb
     int32_t nb;        // buckets (high digits in use)
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     while (a0 < r1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
     const int64_t body = (r1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
     auto one = [&](uint64_t raw) {
-        const uint64_t kk = (uint64_t)wm_key_val(raw, key.dtype) - (uint64_t)sh.kmin;
+        const uint64_t kk = ((uint64_t)wm_key_val(raw, key.dtype) - (uint64_t)sh.kmin) & sh.kmask;
         atomicAdd(&h[kk >> sh.lb], 1u);
     };
     for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
@@ -133,6 +136,67 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, u
     for (int64_t i = a0 + body + threadIdx.x; i < r1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
     __syncthreads();
     counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
+}
+
+// The key's min / max (per-workgroup partials) and pass 1's histogram in one read of the key: the
+// histogram is taken on the key mod 2^20 (kmin = 0, kmask = 2^20 - 1, 1024 digits of 10 bits), which
+// is pass 1's digit for every key range of 2^19 .. 2^20 keys (config 5's shape) whatever its minimum;
+// other ranges histogram again with their own shape.
+struct WmMinMax {
+    int64_t mn, mx;
+};
+template <int KES>
+__global__ __launch_bounds__(kWmBlock) void k_wm_minmax_hist1(ColRef key, WmShape sh, uint32_t *__restrict__ counts,
+                                                              WmMinMax *__restrict__ part) {
+    __shared__ uint32_t h[kWmDig];
+    __shared__ int64_t smn[kWmBlock / 64], smx[kWmBlock / 64];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
+    constexpr int PER = 16 / KES, U = 4;
+    const char *kp = (const char *)key.values;
+    int64_t a0 = r0;
+    while (a0 < r1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
+    const int64_t body = (r1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    auto one = [&](uint64_t raw) {
+        const int64_t x = wm_key_val(raw, key.dtype);
+        mn = x < mn ? x : mn;
+        mx = x > mx ? x : mx;
+        atomicAdd(&h[(((uint64_t)x - (uint64_t)sh.kmin) & sh.kmask) >> sh.lb], 1u);
+    };
+    for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
+        v4u32w w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load((const v4u32w *)(kp + (i + (int64_t)u * kWmBlock * PER) * KES));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (KES == 8) {
+                one((uint64_t)w[u][0] | ((uint64_t)w[u][1] << 32));
+                one((uint64_t)w[u][2] | ((uint64_t)w[u][3] << 32));
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) one((uint64_t)w[u][q]);
+            }
+        }
+    }
+    for (int64_t i = r0 + threadIdx.x; i < a0; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+    for (int64_t i = a0 + body + threadIdx.x; i < r1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) smn[wave] = mn, smx[wave] = mx;
+    __syncthreads();
+    counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWmBlock / 64; ++w) mn = smn[w] < mn ? smn[w] : mn, mx = smx[w] > mx ? smx[w] : mx;
+        mn = smn[0] < mn ? smn[0] : mn, mx = smx[0] > mx ? smx[0] : mx;
+        part[blockIdx.x] = WmMinMax{mn, mx};
+    }
 }
 
 // ---- group sort: one wave per PARTITION BY group --------------------------------------------
@@ -368,7 +432,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             live[j] = t0 + woff + j * 64 < r1;
-            const uint64_t kk = (uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin;
+            const uint64_t kk = ((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) & sh.kmask;
             d[j] = (uint32_t)(kk >> sh.lb);
             kl[j] = (uint32_t)kk & lmask;
             ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
@@ -1044,7 +1108,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             live[j] = t0 + woff + j * 64 < r1;
-            d[j] = (uint32_t)(((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) >> sh.lb);
+            d[j] = (uint32_t)((((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) & sh.kmask) >> sh.lb);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);
         const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
@@ -1089,7 +1153,7 @@ __global__ void k_wm_set2(uint64_t *a, uint64_t *b, uint64_t v) {
 // default's bits or null): the sort writes each row's value bits beside its valid flag and the
 // inverse passes move both.
 static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
-                       const int64_t *dflt, WmShape sh, qeh_column *out) {
+                       const int64_t *dflt, WmShape sh, qeh_column *out, DevBuf *pre_counts = nullptr) {
     const int64_t n = sh.n;
     const int cus = ctx->props.multiProcessorCount;
     const int g1 = (int)((n + sh.span - 1) / sh.span);
@@ -1097,7 +1161,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
     DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8;
     const int64_t nc1 = (int64_t)kWmDig * g1;
-    if (cnt1.alloc(ctx, nc1 * 4) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
+    if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
         flag.alloc(ctx, 8))
         return fail(QEH_E_OOM, "window: out of device memory");
@@ -1111,8 +1175,11 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int gb = std::min(cus * gbx, sh.nb);
     {
         KernelTimer kt(ctx, "window_partition");
-        hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh, cnt1.as<uint32_t>());
-        QEH_TRY(exclusive_scan_u32(ctx, cnt1.as<uint32_t>(), base1.as<uint64_t>(), nc1, nullptr));
+        const uint32_t *counts = pre_counts ? pre_counts->as<uint32_t>() : cnt1.as<uint32_t>();
+        if (!pre_counts)
+            hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh,
+                               cnt1.as<uint32_t>());
+        QEH_TRY(exclusive_scan_u32(ctx, counts, base1.as<uint64_t>(), nc1, nullptr));
         const bool d1 = wm_digit_bits(sh.nb) == 10;
 #define QEH_WM_P1(K, O) (at ? k_wm2_pass1<K, O, kWmAtomicRank> : d1 ? k_wm2_pass1<K, O, 10> : k_wm2_pass1<K, O, -1>)
         hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
@@ -1253,16 +1320,41 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         order.dtype != QEH_DT_FLOAT32)
         return kWindowMsdNotEligible;
     if ((part.validity && part.null_count != 0) || (order.validity && order.null_count != 0)) return kWindowMsdNotEligible;
-    int64_t kmin, kmax, kval;
-    QEH_TRY(column_minmax(ctx, part, &kmin, &kmax, &kval));
-    if (kval != n) return kWindowMsdNotEligible;
+    const int cus = ctx->props.multiProcessorCount;
+    // pass-1 workgroups (row spans): two per CU by default, so the replaying inverse pass (80 KB of
+    // LDS) runs two per CU and one's barrier phases overlap the other's memory phases
+    int g1x = 2;
+    if (const char *e = std::getenv("QEH_WM_G1X")) g1x = std::max(1, std::atoi(e));
+    const int g1w = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * g1x, (n + kWmTile - 1) / kWmTile));
+    const int64_t span = ((n + g1w - 1) / g1w + kWmTile - 1) / kWmTile * kWmTile;
+    const int g1 = (int)((n + span - 1) / span);  // window_noid's pass-1 grid (histogram layout)
+    // the key's min / max and the 20-bit shape's pass-1 histogram in one read (k_wm_minmax_hist1)
+    WmShape sh{};
+    sh.n = n;
+    sh.span = span;
+    sh.kmin = 0;
+    sh.kmask = (1ull << 20) - 1;
+    sh.lb = 10;
+    DevBuf pre, mmp;
+    QEH_TRY(pre.alloc(ctx, (size_t)kWmDig * g1 * 4));
+    QEH_TRY(mmp.alloc(ctx, sizeof(WmMinMax) * (size_t)g1));
+    {
+        KernelTimer kt(ctx, "window_partition");
+        hipLaunchKernelGGL(part.dtype == QEH_DT_INT32 ? k_wm_minmax_hist1<4> : k_wm_minmax_hist1<8>, dim3(g1), dim3(kWmBlock), 0,
+                           ctx->stream, make_colref(part), sh, pre.as<uint32_t>(), mmp.as<WmMinMax>());
+        QEH_HIP(hipGetLastError());
+    }
+    std::vector<WmMinMax> mmh(g1);
+    QEH_TRY(read_small(ctx, mmh.data(), mmp.p, sizeof(WmMinMax) * (size_t)g1));
+    int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+    for (const WmMinMax &q : mmh) kmin = q.mn < kmin ? q.mn : kmin, kmax = q.mx > kmax ? q.mx : kmax;
     const uint64_t range = (uint64_t)kmax - (uint64_t)kmin + 1ull;
     if (range == 0 || range > (1ull << 20)) return kWindowMsdNotEligible;
     int bits = 0;
     while (bits < 64 && ((range - 1) >> bits)) ++bits;
-    WmShape sh{};
-    sh.n = n;
+    const bool folded = bits == 20 && !std::getenv("QEH_WM_LB") && !std::getenv("QEH_WM_NO_FOLD");
     sh.kmin = kmin;
+    sh.kmask = ~0ull;
     sh.lb = bits > 10 ? bits - 10 : 0;
     if (const char *e = std::getenv("QEH_WM_LB")) {  // experiments: digit split between the passes
         const int lb = std::atoi(e);
@@ -1270,16 +1362,16 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     }
     sh.nb = (int32_t)(((range - 1) >> sh.lb) + 1);
     sh.nparts = (int64_t)range;
+    if (folded) {  // groups = keys mod 2^20 (some empty): the histogram already taken is pass 1's
+        sh.kmin = 0;
+        sh.kmask = (1ull << 20) - 1;
+        sh.lb = 10;
+        sh.nb = kWmDig;
+        sh.nparts = (int64_t)1 << 20;
+    }
     if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
     if (const char *e = std::getenv("QEH_WM_NTS")) sh.nts = std::atoi(e);
-    const int cus = ctx->props.multiProcessorCount;
-    // pass-1 workgroups (row spans): two per CU by default, so the replaying inverse pass (80 KB of
-    // LDS) runs two per CU and one's barrier phases overlap the other's memory phases
-    int g1x = 2;
-    if (const char *e = std::getenv("QEH_WM_G1X")) g1x = std::max(1, std::atoi(e));
-    const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * g1x, (n + kWmTile - 1) / kWmTile));
-    sh.span = ((n + g1 - 1) / g1 + kWmTile - 1) / kWmTile * kWmTile;
-    return window_noid(ctx, func, part, order, asc, param, dflt, sh, out);
+    return window_noid(ctx, func, part, order, asc, param, dflt, sh, out, folded ? &pre : nullptr);
 }
 
 }  // namespace qeh
