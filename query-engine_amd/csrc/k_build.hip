@@ -616,8 +616,10 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
                 // time, but its two dependent kernels finish after phase A: 7.2 vs 7.0 ms per step)
                 int xcd = range * 2 >= (4ull << 20) && ctx->build_beside_rows >= 32 * n ? 1 : 0;
                 if (const char *e = std::getenv("QEH_INSERT_XCD")) xcd = std::atoi(e);
+                // the eight lists are sized for every row each (64 B per build row): opt-in only, and
+                // capped at 2^24 build rows (1 GB of lists) so it cannot crowd a large probe's memory
                 DevBuf lists, cursor;
-                if (xcd == 2 && (n > ((int64_t)1 << 28) || lists.alloc(ctx, (size_t)n * 8 * 8) != QEH_OK ||
+                if (xcd == 2 && (n > ((int64_t)1 << 24) || lists.alloc(ctx, (size_t)n * 8 * 8) != QEH_OK ||
                                  cursor.alloc(ctx, 64) != QEH_OK))
                     xcd = 1;
                 if (xcd == 2) {
