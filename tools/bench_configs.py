@@ -223,6 +223,29 @@ def cfg_window(ctx, scale):
         line(f"window {name} 1e9", n, wall, alg * n, sum(kt.values()), "radix sort + k_seg_start/k_window_out", cpu, kt)
 
 
+def cfg_window_lsd(ctx, scale):
+    """The shapes the partitioning path does not take, on the LSD path (k_sort.hip): ROW_NUMBER() and
+    RANK() OVER (PARTITION BY k ORDER BY v) with k over 2^24 values (beyond the path's 2^20-key bound),
+    and ROW_NUMBER over two PARTITION BY keys, 1e9 rows.  Algorithmic bytes: 16 B read + 8 B written
+    per row (24 B with the second key)."""
+    from qe_hip.plan import WindowFunctionType as W
+    n = int(1e9 * scale)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 24)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    names = ["radix_pass", "sort_encode", "row_number", "window", "window_partition", "window_sort", "window_place", "gather"]
+    for label, fn, alg in [
+            ("ROW_NUMBER, k over 2^24", lambda: ctx.row_number([k], [v], [True]).release(), 24.0),
+            ("RANK, k over 2^24", lambda: ctx.window(W.Rank, [k], [v], [True]).release(), 24.0)]:
+        wall, kt, _ = timed(ctx, fn, 2, names)
+        line(f"window LSD path {label} 1e9", n, wall, alg * n, sum(kt.values()), "k_encode_pair + radix passes + scans + scatter", None,
+             {"kernel_split_ms": {q: w for q, w in kt.items() if w}})
+    k2 = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 9, n, 64)
+    kk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 16)
+    wall, kt, _ = timed(ctx, lambda: ctx.row_number([kk, k2], [v], [True]).release(), 2, names)
+    line("window LSD path ROW_NUMBER, PARTITION BY (k, k2) 1e9", n, wall, 32.0 * n, sum(kt.values()),
+         "radix passes + scans + scatter", None, {"kernel_split_ms": {q: w for q, w in kt.items() if w}})
+
+
 def cfg_outer(ctx, scale, jt=1):
     """LEFT (jt=1) / FULL (jt=3) join, 2e8 probe rows (keys uniform over twice the dim key range,
     so half find no match) x 1e7 dim rows, materialising (f.v, d.a).  Algorithmic bytes: 16 B probe
@@ -589,7 +612,8 @@ def main():
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
          "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window,
-         "cfg4leg": cfg4_leg, "cfg5leg": cfg5_leg}[name](ctx, args.scale)
+         "cfg4leg": cfg4_leg, "cfg5leg": cfg5_leg,
+         "window_lsd": cfg_window_lsd}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))
     ctx.close()
