@@ -1967,8 +1967,9 @@ extern "C" int qeh_row_number(qeh_ctx *ctx, const qeh_column *part_keys, int n_p
     }
     int64_t n;
     QEH_TRY(check_sort_keys(all.data(), (int)all.size(), &n));
-    if (n_part == 1 && n_order == 1) {  // one bounded partition key: partition instead of sorting
-        const int s = window_msd(ctx, QEH_WIN_ROW_NUMBER, part_keys[0], order_keys[0], asc[1] != 0, 0, nullptr, nullptr, out_rn);
+    if (n_part >= 1 && n_order == 1) {  // bounded integer partition keys: partition instead of sorting
+        const int s = window_msd_keys(ctx, QEH_WIN_ROW_NUMBER, part_keys, n_part, order_keys[0], asc[n_part] != 0, 0, nullptr,
+                                      nullptr, out_rn);
         if (s != kWindowMsdNotEligible) return s;
     }
     RadixState rs;
@@ -2201,8 +2202,8 @@ extern "C" int qeh_window(qeh_ctx *ctx, int32_t func, const qeh_column *part_key
     }
     if (func == QEH_WIN_ROW_NUMBER && !all.empty())  // the dedicated path (pair-key sort, no peer state)
         return qeh_row_number(ctx, part_keys, n_part, order_keys, n_order, ascending, out);
-    if (n_part == 1 && n_order == 1) {  // one bounded partition key: partition instead of sorting
-        const int s = window_msd(ctx, func, part_keys[0], order_keys[0], asc[1] != 0, param, arg, dflt, out);
+    if (n_part >= 1 && n_order == 1) {  // bounded integer partition keys: partition instead of sorting
+        const int s = window_msd_keys(ctx, func, part_keys, n_part, order_keys[0], asc[n_part] != 0, param, arg, dflt, out);
         if (s != kWindowMsdNotEligible) return s;
     }
     const int odt = value_fn ? arg->dtype : QEH_DT_INT64;

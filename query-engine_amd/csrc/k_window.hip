@@ -92,6 +92,8 @@ struct WmShape {
     uint64_t kmask;    // key offset = (k - kmin) & kmask: all ones, or 2^20 - 1 with kmin = 0 (keys mod 2^20,
                        // one-to-one over any key range <= 2^20, so the histogram needs no minimum first)
     int32_t lb;        // low key bits (pass 2 digit); high digit = (k - kmin) >> lb
+    int32_t sb;        // sub-key bits (key ranges above 2^20): pass 2's digit is the low bits >> sb, and a
+                       // "group" is 2^sb consecutive keys, told apart by the group sort (ks below)
     int32_t nb;        // buckets (high digits in use)
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
@@ -477,15 +479,17 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
 template <int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
-                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart) {
+                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart,
+                                                        uint8_t *__restrict__ o_ks) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
     __shared__ uint16_t st_d[kWmTile];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    const int64_t L = (int64_t)1 << sh.lb;
-    const int dbits = sh.lb;
+    const int sbits = sh.sb;
+    const int64_t L = (int64_t)1 << (sh.lb - sbits);
+    const int dbits = sh.lb - sbits;
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
     for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
@@ -493,14 +497,14 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
         __syncthreads();
         {  // the bucket's low-digit counts: 8 digits per 16-B load, aligned body, scalar edges
             const int64_t a0 = std::min<int64_t>(s1, (s0 + 7) & ~(int64_t)7), a1 = std::max<int64_t>(a0, s1 & ~(int64_t)7);
-            for (int64_t i = s0 + tid; i < a0; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
-            for (int64_t i = a1 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i]], 1u);
+            for (int64_t i = s0 + tid; i < a0; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i] >> sbits], 1u);
+            for (int64_t i = a1 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i] >> sbits], 1u);
             for (int64_t i = a0 + (int64_t)tid * 8; i < a1; i += (int64_t)kWmBlock * 8) {
                 const v4u32w w = __builtin_nontemporal_load((const v4u32w *)(i_kl + i));
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    atomicAdd(&R.lofs[w[q] & 0xFFFFu], 1u);
-                    atomicAdd(&R.lofs[w[q] >> 16], 1u);
+                    atomicAdd(&R.lofs[(w[q] & 0xFFFFu) >> sbits], 1u);
+                    atomicAdd(&R.lofs[(w[q] >> 16) >> sbits], 1u);
                 }
             }
         }
@@ -528,10 +532,12 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             uint32_t d[NJ], slot[NJ];
             uint64_t keys[NJ];
             bool live[NJ];
+            uint32_t ksub[NJ];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 live[j] = t0 + woff + j * 64 < s1;
-                d[j] = lx[j];
+                d[j] = lx[j] >> sbits;
+                ksub[j] = lx[j] & ((1u << sbits) - 1u);
                 keys[j] = kx[j];
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
@@ -540,15 +546,17 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
             for (int j = 0; j < NJ; ++j) {
                 if (!live[j]) continue;
                 st_key[slot[j]] = keys[j];
-                st_d[slot[j]] = (uint16_t)d[j];
+                st_d[slot[j]] = (uint16_t)(d[j] | (ksub[j] << 10));  // digit (10 bits) | sub-key (<= 4 bits)
             }
             wm_barrier();
             const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
     #pragma unroll 8
         for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                if (sh.nts & 2) __builtin_nontemporal_store(st_key[s], o_key + lpos[dd] + (uint32_t)s - R.lofs[dd]);
-                else o_key[lpos[dd] + (uint32_t)s - R.lofs[dd]] = st_key[s];
+                const uint32_t dd = st_d[s] & 1023u;
+                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                if (sh.nts & 2) __builtin_nontemporal_store(st_key[s], o_key + p);
+                else o_key[p] = st_key[s];
+                if (sbits) o_ks[p] = (uint8_t)(st_d[s] >> 10);
             }
             wm_barrier();
             lpos[tid] += tcnt;
@@ -767,15 +775,21 @@ struct WmGroupLds {
     uint64_t bnd[kWmCsMaxG + 1];
     uint64_t mm[8];           // per-wave min / max
     uint32_t ws[4], wf[4], wc[4], wt[4];
+    uint32_t subc[16], subst[16];  // SUB: rows per sub-key, then the sub-keys' starts in the sorted group
 };
 
 // FN: the window function as a compile-time constant (QEH_WIN_ROW_NUMBER .. NTILE; -1 = the value
 // functions, selected by f.func at run time) -- the per-row dispatch left a third of the kernel's
 // instructions scalar.
-template <int E, int FN>
+// SUB (key ranges above 2^20, sh.sb > 0): a group holds 2^sb consecutive keys, told apart by gks (the
+// key's low sb bits): the buckets are (sub-key, order-key range), so a row's sorted index minus its
+// sub-key's start is its index inside its own PARTITION BY group (ROW_NUMBER, RANK, NTILE only).
+template <int E, int FN, bool SUB = false>
 __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                       const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
-                                                      uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big) {
+                                                      uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big,
+                                                      const uint8_t *__restrict__ gks) {
+    static_assert(!SUB || FN == QEH_WIN_ROW_NUMBER || FN == QEH_WIN_RANK || FN == QEH_WIN_NTILE, "sub-keys: direct functions");
     constexpr int P = 256 * E, NB = E == 4 ? 11 : 12, LO = E == 4 ? 0 : 1024;  // groups of (LO, P] rows
     static_assert((1 << NB) == 2 * P, "two buckets per row of capacity");
     __shared__ WmGroupLds<E> L;
@@ -784,6 +798,7 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
     for (int64_t i = t; i <= g1 - g0; i += 256) L.bnd[i] = pstart[g0 + i];
     __syncthreads();
     uint64_t keyN[E];
+    uint32_t ksN[SUB ? E : 1];
     auto issue = [&](int64_t gi) {
         const int64_t s = (int64_t)L.bnd[gi - g0];
         const int m = (int)((int64_t)L.bnd[gi - g0 + 1] - s);
@@ -791,6 +806,7 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
         for (int r = 0; r < E; ++r) {
             const int e = r * 256 + t;
             keyN[r] = (m > LO && m <= P && e < m) ? __builtin_nontemporal_load(gkey + s + e) : 0ull;
+            if constexpr (SUB) ksN[r] = (m > LO && m <= P && e < m) ? (uint32_t)gks[s + e] : 0u;
         }
     };
     if (g0 < g1) issue(g0);
@@ -798,8 +814,13 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
         const int64_t s = (int64_t)L.bnd[g - g0];
         const int m = (int)((int64_t)L.bnd[g - g0 + 1] - s);
         uint64_t key[E];
+        uint32_t ks[SUB ? E : 1];
 #pragma unroll
         for (int r = 0; r < E; ++r) key[r] = keyN[r];
+        if constexpr (SUB) {
+#pragma unroll
+            for (int r = 0; r < E; ++r) ks[r] = ksN[r];
+        }
         if (g + 1 < g1) issue(g + 1);
         if (m > P && E == 8 && t == 0) *too_big = 1u;  // above 2048 rows: the caller takes the LSD path
         if (m <= LO || m > P) continue;  // (uniform) empty, or the other kernel's size class
@@ -817,19 +838,26 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
             mx = b > mx ? b : mx;
         }
         if (lane == 0) L.mm[wave] = mn, L.mm[4 + wave] = mx;
+        if (SUB && t < 16) L.subc[t] = 0u;
         wm_barrier();
         mn = min(min(L.mm[0], L.mm[1]), min(L.mm[2], L.mm[3]));
         mx = max(max(L.mm[4], L.mm[5]), max(L.mm[6], L.mm[7]));
         const uint64_t span = mx - mn;
         const int sb = span ? 64 - __clzll((long long)span) : 0;
-        const int shift = sb > NB ? sb - NB : 0;
+        const int NBV = SUB ? NB - sh.sb : NB;  // bucket bits of the order key (the sub-key takes sh.sb)
+        const int shift = sb > NBV ? sb - NBV : 0;
         uint32_t se[E], sl[E];  // bucket, then start | end << 16; arrival, then slot
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int e = r * 256 + t;
             se[r] = sl[r] = 0u;
             if (e < m) {
-                const uint32_t bk = (uint32_t)((key[r] - mn) >> shift), sh16 = (bk & 1u) * 16u;
+                uint32_t bk = (uint32_t)((key[r] - mn) >> shift);
+                if constexpr (SUB) {
+                    bk |= ks[r] << NBV;
+                    atomicAdd(&L.subc[ks[r]], 1u);
+                }
+                const uint32_t sh16 = (bk & 1u) * 16u;
                 const uint32_t old = atomicAdd(&L.cnt[bk >> 1], 1u << sh16);
                 se[r] = bk;
                 sl[r] = (old >> sh16) & 0xFFFFu;
@@ -850,9 +878,19 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
             if (lane == 63) L.ws[wave] = incl, L.wf[wave] = wbig ? 1u : 0u;
             wm_barrier();
             if (L.wf[0] | L.wf[1] | L.wf[2] | L.wf[3]) {  // (uniform) clustered keys: the network sorts it
-                if (t == 0) fb[1 + atomicAdd(&fb[0], 1u)] = (uint32_t)g;
+                if (t == 0) {
+                    if (SUB) *too_big = 1u;  // (the network knows no sub-keys: the LSD path takes the job)
+                    else fb[1 + atomicAdd(&fb[0], 1u)] = (uint32_t)g;
+                }
                 wm_barrier();  // every thread has read the flags before the next group writes them
                 continue;
+            }
+            if (SUB && t == 0) {  // sub-key starts in the group's sorted order (counts complete since the barrier)
+                uint32_t run = 0;
+                for (int q = 0; q < 16; ++q) {
+                    L.subst[q] = run;
+                    run += L.subc[q];
+                }
             }
             uint32_t run = incl - tot;
 #pragma unroll
@@ -915,10 +953,15 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
             for (int r = 0; r < E; ++r) {
                 const int e = r * 256 + t;
                 if (e >= m) continue;
-                const uint32_t i = (se[r] & 0xFFFFu) + rank[r];
+                uint32_t i = (se[r] & 0xFFFFu) + rank[r];
+                int64_t mg = m;  // rows of the row's PARTITION BY group
+                if constexpr (SUB) {
+                    i -= L.subst[ks[r]];
+                    mg = L.subc[ks[r]];
+                }
                 uint32_t v;
                 if constexpr (FN == QEH_WIN_NTILE) {
-                    const int64_t q = m / f.param, rm = m % f.param, r0 = i;
+                    const int64_t q = mg / f.param, rm = mg % f.param, r0 = i;
                     v = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
                 } else {
                     v = i + 1u;
@@ -1018,8 +1061,8 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
     __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    const int64_t L = (int64_t)1 << sh.lb;
-    const int dbits = sh.lb;
+    const int64_t L = (int64_t)1 << (sh.lb - sh.sb);
+    const int dbits = sh.lb - sh.sb;
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
     for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
@@ -1043,7 +1086,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 live[j] = t0 + woff + j * 64 < s1;
-                d[j] = lx[j];
+                d[j] = lx[j] >> sh.sb;
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
             const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
@@ -1159,11 +1202,11 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int g1 = (int)((n + sh.span - 1) / sh.span);
     const bool value_fn = func >= QEH_WIN_LAG;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8;
+    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
-        flag.alloc(ctx, 8))
+        flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)))
         return fail(QEH_E_OOM, "window: out of device memory");
     const ColRef kc = make_colref(part), oc = make_colref(order);
     const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
@@ -1192,9 +1235,9 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
 #undef QEH_WM_P1
         if (!sh.exp)  // (experiment runs: pass 1 only)
-        hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+        hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
                            bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
-                           pst.as<uint64_t>());
+                           pst.as<uint64_t>(), ks2.as<uint8_t>());
     }
     QEH_HIP(hipGetLastError());
     if (sh.exp) {  // experiment runs stop after the partition passes (their outputs are not valid)
@@ -1237,11 +1280,27 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                 constexpr int FN = decltype(fn)::value;
                 hipLaunchKernelGGL((k_wm2_csort_wg<4, FN>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
                                    pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
-                                   flag.as<uint32_t>());
+                                   flag.as<uint32_t>(), nullptr);
                 hipLaunchKernelGGL((k_wm2_csort_wg<8, FN>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
                                    pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
-                                   flag.as<uint32_t>());
+                                   flag.as<uint32_t>(), nullptr);
             };
+            // groups of 2^sb keys (sh.sb > 0): the sub-key-aware sort, direct functions only
+            auto csort_sub = [&](auto fn) {
+                constexpr int FN = decltype(fn)::value;
+                hipLaunchKernelGGL((k_wm2_csort_wg<4, FN, true>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                                   flag.as<uint32_t>(), ks2.as<uint8_t>());
+                hipLaunchKernelGGL((k_wm2_csort_wg<8, FN, true>), dim3((unsigned)ncs), dim3(256), 0, ctx->stream, sh, wf,
+                                   pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
+                                   flag.as<uint32_t>(), ks2.as<uint8_t>());
+            };
+            if (!VF && sh.sb) {
+                if (func == QEH_WIN_ROW_NUMBER) csort_sub(std::integral_constant<int, QEH_WIN_ROW_NUMBER>{});
+                else if (func == QEH_WIN_RANK) csort_sub(std::integral_constant<int, QEH_WIN_RANK>{});
+                else csort_sub(std::integral_constant<int, QEH_WIN_NTILE>{});
+                return;  // (nothing was queued for the network)
+            }
             if (VF) csort(std::integral_constant<int, -1>{});
             else if (func == QEH_WIN_ROW_NUMBER) csort(std::integral_constant<int, QEH_WIN_ROW_NUMBER>{});
             else if (func == QEH_WIN_RANK) csort(std::integral_constant<int, QEH_WIN_RANK>{});
@@ -1267,8 +1326,9 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     QEH_TRY(alloc_column(ctx, value_fn ? order.dtype : QEH_DT_INT64, n, value_fn, out));
     {
         KernelTimer kt(ctx, "window_place");
-        hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : sh.lb == 10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
-                                    : (at ? k_wm2_inv2<kWmAtomicRank, false> : sh.lb == 10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
+        const bool d10 = sh.lb - sh.sb == 10;
+        hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : d10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
+                                    : (at ? k_wm2_inv2<kWmAtomicRank, false> : d10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
                            dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
                            kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(), res2v.as<uint64_t>(),
                            res1v.as<uint64_t>());
@@ -1349,19 +1409,24 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     int64_t kmin = INT64_MAX, kmax = INT64_MIN;
     for (const WmMinMax &q : mmh) kmin = q.mn < kmin ? q.mn : kmin, kmax = q.mx > kmax ? q.mx : kmax;
     const uint64_t range = (uint64_t)kmax - (uint64_t)kmin + 1ull;
-    if (range == 0 || range > (1ull << 20)) return kWindowMsdNotEligible;
+    // up to 2^20 keys: a group per key; up to 2^24 for ROW_NUMBER / RANK / NTILE: a group per 2^sb
+    // consecutive keys, told apart inside the group sort
+    const bool sub_ok = (func == QEH_WIN_ROW_NUMBER || func == QEH_WIN_RANK || func == QEH_WIN_NTILE) &&
+                        !std::getenv("QEH_WM_NO_SUB");
+    if (range == 0 || range > (1ull << (sub_ok ? 24 : 20))) return kWindowMsdNotEligible;
     int bits = 0;
     while (bits < 64 && ((range - 1) >> bits)) ++bits;
     const bool folded = bits == 20 && !std::getenv("QEH_WM_LB") && !std::getenv("QEH_WM_NO_FOLD");
     sh.kmin = kmin;
     sh.kmask = ~0ull;
     sh.lb = bits > 10 ? bits - 10 : 0;
+    sh.sb = bits > 20 ? bits - 20 : 0;
     if (const char *e = std::getenv("QEH_WM_LB")) {  // experiments: digit split between the passes
         const int lb = std::atoi(e);
-        if (lb >= sh.lb && lb <= 10 && lb <= bits) sh.lb = lb;
+        if (!sh.sb && lb >= sh.lb && lb <= 10 && lb <= bits) sh.lb = lb;
     }
     sh.nb = (int32_t)(((range - 1) >> sh.lb) + 1);
-    sh.nparts = (int64_t)range;
+    sh.nparts = (int64_t)(((range - 1) >> sh.sb) + 1);  // groups (of 2^sb keys)
     if (folded) {  // groups = keys mod 2^20 (some empty): the histogram already taken is pass 1's
         sh.kmin = 0;
         sh.kmask = (1ull << 20) - 1;
@@ -1372,6 +1437,67 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
     if (const char *e = std::getenv("QEH_WM_NTS")) sh.nts = std::atoi(e);
     return window_noid(ctx, func, part, order, asc, param, dflt, sh, out, folded ? &pre : nullptr);
+}
+
+
+// composite[i] = sum_j (k_j[i] - mn_j) * mul_j (mixed radix, the first key most significant)
+struct WmKeys {
+    ColRef c[4];
+    int64_t mn[4], mul[4];
+    int32_t n;
+};
+__global__ void k_wm_composite(WmKeys ks, int64_t n, int64_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t v = 0;
+        for (int j = 0; j < ks.n; ++j) v += ((uint64_t)load_i64(ks.c[j], i) - (uint64_t)ks.mn[j]) * (uint64_t)ks.mul[j];
+        out[i] = (int64_t)v;
+    }
+}
+
+int window_msd_keys(qeh_ctx *ctx, int func, const qeh_column *parts, int n_part, const qeh_column &order, bool asc,
+                    int64_t param, const qeh_column *arg, const int64_t *dflt, qeh_column *out) {
+    if (n_part == 1) return window_msd(ctx, func, parts[0], order, asc, param, arg, dflt, out);
+    if (n_part < 2 || n_part > 4 || std::getenv("QEH_NO_WINDOW_MSD")) return kWindowMsdNotEligible;
+    const int64_t n = parts[0].length;
+    if (!msd_forced() && n < ((int64_t)1 << 20)) return kWindowMsdNotEligible;
+    const bool sub_ok = func == QEH_WIN_ROW_NUMBER || func == QEH_WIN_RANK || func == QEH_WIN_NTILE;
+    const uint64_t bound = 1ull << (sub_ok ? 24 : 20);
+    WmKeys ks{};
+    ks.n = n_part;
+    uint64_t prod = 1, rng[4] = {};
+    for (int j = 0; j < n_part; ++j) {
+        const qeh_column &c = parts[j];
+        if (c.length != n || (c.dtype != QEH_DT_INT64 && c.dtype != QEH_DT_INT32) || (c.validity && c.null_count != 0))
+            return kWindowMsdNotEligible;
+        int64_t mn, mx, cnt;
+        QEH_TRY(column_minmax(ctx, c, &mn, &mx, &cnt));
+        if (cnt != n) return kWindowMsdNotEligible;
+        rng[j] = (uint64_t)mx - (uint64_t)mn + 1ull;
+        if (rng[j] == 0 || rng[j] > bound || prod * rng[j] > bound) return kWindowMsdNotEligible;
+        ks.c[j] = make_colref(c);
+        ks.mn[j] = mn;
+        prod *= rng[j];
+    }
+    // multipliers: the product of the ranges of the keys after j (the last key least significant)
+    uint64_t m = 1;
+    for (int j = n_part - 1; j >= 0; --j) {
+        ks.mul[j] = (int64_t)m;
+        m *= rng[j];
+    }
+    qeh_column comp{};
+    QEH_TRY(alloc_column(ctx, QEH_DT_INT64, n, false, &comp));
+    {
+        KernelTimer kt(ctx, "window_partition");
+        hipLaunchKernelGGL(k_wm_composite, dim3(grid_for(ctx, n, 256 * 8, 8)), dim3(256), 0, ctx->stream, ks, n,
+                           (int64_t *)comp.values);
+    }
+    if (hipGetLastError() != hipSuccess) {
+        qeh_column_release(ctx, &comp);
+        return fail(QEH_E_HIP, "window: composite key launch failed");
+    }
+    const int s = window_msd(ctx, func, comp, order, asc, param, arg, dflt, out);
+    qeh_column_release(ctx, &comp);
+    return s;
 }
 
 }  // namespace qeh

@@ -154,6 +154,10 @@ constexpr int kWindowMsdNotEligible = -1;
 // LAG / LEAD / FIRST_VALUE / LAST_VALUE when `arg` is the ORDER BY column itself.
 int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
                const qeh_column *arg, const int64_t *dflt, qeh_column *out);
+// Several integer PARTITION BY keys (2..4): their mixed-radix composite (one Int64 column, the keys'
+// ranges multiplied) takes window_msd when the product of the ranges is within its key bound.
+int window_msd_keys(qeh_ctx *ctx, int func, const qeh_column *parts, int n_part, const qeh_column &order, bool asc,
+                    int64_t param, const qeh_column *arg, const int64_t *dflt, qeh_column *out);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);

@@ -258,3 +258,65 @@ def test_row_number_full_size_properties(ctx):
     want = torch.empty_like(pos)
     want[order] = pos - first + 1
     assert torch.equal(tr[idx], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.Ntile, 3)])
+@pytest.mark.parametrize("n,parts,k0", [(300_001, (1 << 20) + 5, -7), (2_000_000, 1 << 22, 1 << 40), (1_500_000, 1 << 24, -(1 << 30))])
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_window_sub_keys_vs_oracle(ctx, monkeypatch, func, param, n, parts, k0, asc):
+    """Key ranges above 2^20 (up to 2^24) for ROW_NUMBER / RANK / NTILE: a group holds 2^sb consecutive
+    keys and the group sort buckets by (sub-key, order key), numbering each sub-key's rows from 1."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(n + parts)
+    k = r.integers(0, parts, n).astype(np.int64) + k0
+    k[:2] = [k0, k0 + parts - 1]  # the whole range present
+    v = r.integers(-40, 40, n).astype(np.int64)  # ties: RANK peers, input-order tiebreak
+    got, want, ran = _run(ctx, func, k, v, asc, param)
+    assert ran
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_msd_window_sub_keys_fallbacks(ctx, monkeypatch):
+    """Above 2^20 keys: DENSE_RANK is not taken (LSD path), a group above 2048 rows falls back; both
+    stay equal to the oracle."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(12)
+    n = 400_000
+    k = r.integers(0, 1 << 22, n).astype(np.int64)
+    v = r.integers(-5, 5, n).astype(np.int64)
+    got, want, ran = _run(ctx, W.DenseRank, k, v, True)
+    assert not ran and np.array_equal(got, want)
+    k[:5000] = 777  # one group of > 2048 rows
+    got, want, _ = _run(ctx, W.RowNumber, k, v, True)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.DenseRank, 0), (W.Ntile, 4)])
+@pytest.mark.parametrize("ranges", [(64, 4096), (100, 50, 30), (3000, 2000)])
+def test_msd_window_several_partition_keys(ctx, monkeypatch, func, param, ranges):
+    """PARTITION BY two or three integer keys: their mixed-radix composite takes the partitioning path
+    when the product of the ranges fits it (2^20 keys, 2^24 for ROW_NUMBER / RANK / NTILE), else the
+    LSD path; equal to the oracle either way."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(sum(ranges))
+    n = 500_000
+    ks = [(r.integers(0, q, n) - q // 3).astype(np.int64 if i % 2 == 0 else np.int32) for i, q in enumerate(ranges)]
+    v = r.integers(-30, 30, n).astype(np.int64)
+    ctx.timing(True)
+    ctx.timing_reset()
+    dk = [ctx.upload(k) for k in ks]
+    hk = [ob.HostCol(k.astype(np.int64)) for k in ks]
+    if func == W.RowNumber:
+        got = ctx.row_number(dk, [ctx.upload(v)], [True]).to_numpy()[0]
+        want = ob.row_number(hk, [ob.HostCol(v)], [True])
+    else:
+        got = ctx.window(func, dk, [ctx.upload(v)], [True], param=param).to_numpy()[0]
+        want, _ = ob.window(func, hk, [ob.HostCol(v)], [True], param=param)
+    ran = _msd_ran(ctx)
+    ctx.timing(False)
+    prod = int(np.prod(ranges))
+    assert ran == (prod <= (1 << (24 if func != W.DenseRank else 20)))
+    assert np.array_equal(got, want)

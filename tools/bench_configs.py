@@ -224,10 +224,11 @@ def cfg_window(ctx, scale):
 
 
 def cfg_window_lsd(ctx, scale):
-    """The shapes the partitioning path does not take, on the LSD path (k_sort.hip): ROW_NUMBER() and
-    RANK() OVER (PARTITION BY k ORDER BY v) with k over 2^24 values (beyond the path's 2^20-key bound),
-    and ROW_NUMBER over two PARTITION BY keys, 1e9 rows.  Algorithmic bytes: 16 B read + 8 B written
-    per row (24 B with the second key)."""
+    """Window shapes beyond config 5's: ROW_NUMBER() and RANK() OVER (PARTITION BY k ORDER BY v) with k
+    over 2^24 values (groups of 16 consecutive keys in the partitioning path), and ROW_NUMBER over two
+    PARTITION BY keys (64 x 2^16 values: their composite key takes the same path), 1e9 rows.
+    QEH_WM_NO_SUB=1 / QEH_NO_WINDOW_MSD=1 give the LSD path for comparison.  Algorithmic bytes: 16 B read
+    + 8 B written per row (24 B read with the second key)."""
     from qe_hip.plan import WindowFunctionType as W
     n = int(1e9 * scale)
     k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 24)
@@ -237,13 +238,15 @@ def cfg_window_lsd(ctx, scale):
             ("ROW_NUMBER, k over 2^24", lambda: ctx.row_number([k], [v], [True]).release(), 24.0),
             ("RANK, k over 2^24", lambda: ctx.window(W.Rank, [k], [v], [True]).release(), 24.0)]:
         wall, kt, _ = timed(ctx, fn, 2, names)
-        line(f"window LSD path {label} 1e9", n, wall, alg * n, sum(kt.values()), "k_encode_pair + radix passes + scans + scatter", None,
+        path = "partitioning path" if kt["window_sort"] else "LSD path"
+        line(f"window {label} 1e9 ({path})", n, wall, alg * n, sum(kt.values()), path, None,
              {"kernel_split_ms": {q: w for q, w in kt.items() if w}})
     k2 = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 9, n, 64)
     kk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 16)
     wall, kt, _ = timed(ctx, lambda: ctx.row_number([kk, k2], [v], [True]).release(), 2, names)
-    line("window LSD path ROW_NUMBER, PARTITION BY (k, k2) 1e9", n, wall, 32.0 * n, sum(kt.values()),
-         "radix passes + scans + scatter", None, {"kernel_split_ms": {q: w for q, w in kt.items() if w}})
+    path = "partitioning path, composite key" if kt["window_sort"] else "LSD path"
+    line(f"window ROW_NUMBER, PARTITION BY (k, k2) 1e9 ({path})", n, wall, 32.0 * n, sum(kt.values()), path, None,
+         {"kernel_split_ms": {q: w for q, w in kt.items() if w}})
 
 
 def cfg_outer(ctx, scale, jt=1):
