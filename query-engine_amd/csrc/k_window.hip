@@ -783,13 +783,13 @@ struct WmGroupLds {
 // instructions scalar.
 // SUB (key ranges above 2^20, sh.sb > 0): a group holds 2^sb consecutive keys, told apart by gks (the
 // key's low sb bits): the buckets are (sub-key, order-key range), so a row's sorted index minus its
-// sub-key's start is its index inside its own PARTITION BY group (ROW_NUMBER, RANK, NTILE only).
+// sub-key's start is its index inside its own PARTITION BY group, and the sub-key's row count its
+// size (the sorted entries carry the sub-key for DENSE_RANK's group starts and the value functions).
 template <int E, int FN, bool SUB = false>
 __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh, WmFunc f, const uint64_t *__restrict__ pstart,
                                                       const uint64_t *__restrict__ gkey, uint16_t *__restrict__ res,
                                                       uint32_t *__restrict__ fb, uint32_t *__restrict__ too_big,
                                                       const uint8_t *__restrict__ gks) {
-    static_assert(!SUB || FN == QEH_WIN_ROW_NUMBER || FN == QEH_WIN_RANK || FN == QEH_WIN_NTILE, "sub-keys: direct functions");
     constexpr int P = 256 * E, NB = E == 4 ? 11 : 12, LO = E == 4 ? 0 : 1024;  // groups of (LO, P] rows
     static_assert((1 << NB) == 2 * P, "two buckets per row of capacity");
     __shared__ WmGroupLds<E> L;
@@ -975,7 +975,7 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int e = r * 256 + t;
-            if (e < m) L.k[wm_pad((se[r] & 0xFFFFu) + rank[r])] = (uint32_t)e | (sl[r] << 12);
+            if (e < m) L.k[wm_pad((se[r] & 0xFFFFu) + rank[r])] = (uint32_t)e | (sl[r] << 12) | (SUB ? ks[r] << 24 : 0u);
         }
         wm_barrier();
         // the function: wave w takes sorted indices [64 E w, 64 E (w + 1)) in E steps of 64
@@ -988,13 +988,16 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
             const uint32_t x = live ? L.k[wm_pad(i)] : 0u;
             pos[r] = x & 4095u;
             rv[r] = 0u;
+            // SUB: the row's own PARTITION BY group is its sub-key's run [sst, sst + mg) of the sorted group
+            const uint32_t sst = SUB ? L.subst[x >> 24] : 0u;
+            const int mg = SUB ? (int)L.subc[x >> 24] : m;
             if constexpr (FN < 0) {  // (valid flag, value bits of the source row at pos)
                 int js;
-                const bool ok = wm_value_src(f, i, m, js);
+                const bool ok = wm_value_src(f, i - (int)sst, mg, js);
                 uint64_t bits = f.has_dflt ? (uint64_t)f.dflt : 0ull;
                 rv[r] = f.has_dflt ? 1u : 0u;
                 if (live && ok) {
-                    bits = wm_decode(L.ov[L.k[wm_pad(js)] >> 12], f.asc, f.odt);
+                    bits = wm_decode(L.ov[(L.k[wm_pad(js + (int)sst)] >> 12) & 4095u], f.asc, f.odt);
                     rv[r] = 1u;
                 }
                 if (live) f.vout[s + pos[r]] = bits;
@@ -1004,9 +1007,9 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
                 const int64_t q = m / f.param, rm = m % f.param, r0 = i;
                 rv[r] = (uint32_t)(r0 < rm * (q + 1) ? r0 / (q + 1) + 1 : rm + (r0 - rm * (q + 1)) / (q > 0 ? q : 1) + 1);
             } else {
-                const uint64_t ov = live ? L.ov[x >> 12] : 0ull;
-                const uint64_t pv = (live && i > 0) ? L.ov[L.k[wm_pad(i - 1)] >> 12] : 0ull;
-                const uint32_t flag = (live && (i == 0 || pv != ov)) ? 1u : 0u;
+                const uint64_t ov = live ? L.ov[(x >> 12) & 4095u] : 0ull;
+                const uint64_t pv = (live && i > 0) ? L.ov[(L.k[wm_pad(i - 1)] >> 12) & 4095u] : 0ull;
+                const uint32_t flag = (live && (i == (int)sst || pv != ov)) ? 1u : 0u;
                 if constexpr (FN == QEH_WIN_RANK) {  // index of the last peer-group start at or before i
                     uint32_t v = flag ? (uint32_t)i : 0u;
 #pragma unroll
@@ -1033,6 +1036,22 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
                 if (v < wave) c = FN == QEH_WIN_RANK ? max(c, L.wt[v]) : c + L.wt[v];
 #pragma unroll
             for (int r = 0; r < E; ++r) rv[r] = FN == QEH_WIN_RANK ? max(rv[r], c) + 1u : rv[r] + c;
+            if constexpr (SUB && FN == QEH_WIN_DENSE_RANK) {
+                // rv = peer-group starts up to i across the whole group; a row's DENSE_RANK counts them
+                // from its sub-key's first row (every order-key read is done: L.ov takes the counts)
+                uint32_t *pc = (uint32_t *)L.ov;
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    const int i = wave * 64 * E + r * 64 + lane;
+                    if (i < m) pc[i] = rv[r];
+                }
+                wm_barrier();
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    const int i = wave * 64 * E + r * 64 + lane;
+                    if (i < m) rv[r] = rv[r] - pc[L.subst[L.k[wm_pad(i)] >> 24]] + 1u;
+                }
+            }
         }
 #pragma unroll
         for (int r = 0; r < E; ++r)
@@ -1295,9 +1314,11 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                                    pst.as<uint64_t>(), key2.as<uint64_t>(), res2.as<uint16_t>(), fbl.as<uint32_t>(),
                                    flag.as<uint32_t>(), ks2.as<uint8_t>());
             };
-            if (!VF && sh.sb) {
-                if (func == QEH_WIN_ROW_NUMBER) csort_sub(std::integral_constant<int, QEH_WIN_ROW_NUMBER>{});
+            if (sh.sb) {
+                if (VF) csort_sub(std::integral_constant<int, -1>{});
+                else if (func == QEH_WIN_ROW_NUMBER) csort_sub(std::integral_constant<int, QEH_WIN_ROW_NUMBER>{});
                 else if (func == QEH_WIN_RANK) csort_sub(std::integral_constant<int, QEH_WIN_RANK>{});
+                else if (func == QEH_WIN_DENSE_RANK) csort_sub(std::integral_constant<int, QEH_WIN_DENSE_RANK>{});
                 else csort_sub(std::integral_constant<int, QEH_WIN_NTILE>{});
                 return;  // (nothing was queued for the network)
             }
@@ -1409,10 +1430,9 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     int64_t kmin = INT64_MAX, kmax = INT64_MIN;
     for (const WmMinMax &q : mmh) kmin = q.mn < kmin ? q.mn : kmin, kmax = q.mx > kmax ? q.mx : kmax;
     const uint64_t range = (uint64_t)kmax - (uint64_t)kmin + 1ull;
-    // up to 2^20 keys: a group per key; up to 2^24 for ROW_NUMBER / RANK / NTILE: a group per 2^sb
-    // consecutive keys, told apart inside the group sort
-    const bool sub_ok = (func == QEH_WIN_ROW_NUMBER || func == QEH_WIN_RANK || func == QEH_WIN_NTILE) &&
-                        !std::getenv("QEH_WM_NO_SUB");
+    // up to 2^20 keys: a group per key; up to 2^24: a group per 2^sb consecutive keys, told apart inside
+    // the group sort
+    const bool sub_ok = !std::getenv("QEH_WM_NO_SUB");
     if (range == 0 || range > (1ull << (sub_ok ? 24 : 20))) return kWindowMsdNotEligible;
     int bits = 0;
     while (bits < 64 && ((range - 1) >> bits)) ++bits;
@@ -1460,8 +1480,7 @@ int window_msd_keys(qeh_ctx *ctx, int func, const qeh_column *parts, int n_part,
     if (n_part < 2 || n_part > 4 || std::getenv("QEH_NO_WINDOW_MSD")) return kWindowMsdNotEligible;
     const int64_t n = parts[0].length;
     if (!msd_forced() && n < ((int64_t)1 << 20)) return kWindowMsdNotEligible;
-    const bool sub_ok = func == QEH_WIN_ROW_NUMBER || func == QEH_WIN_RANK || func == QEH_WIN_NTILE;
-    const uint64_t bound = 1ull << (sub_ok ? 24 : 20);
+    const uint64_t bound = 1ull << (std::getenv("QEH_WM_NO_SUB") ? 20 : 24);
     WmKeys ks{};
     ks.n = n_part;
     uint64_t prod = 1, rng[4] = {};

@@ -175,7 +175,10 @@ def test_slice_partitioned_probe(ctx, monkeypatch, n_fact, n_dim, groups, key0, 
     ctx.timing_reset()
     try:
         gk, ga, wk, wa = run_both(ctx, probe, 1, pred, (dk, None), [(dg, None)], aggs)
-        assert (ctx.kernel_time("fused_build")[1] > 0) == fused
+        # the fused pipeline was tried (its launches are recorded as *_declined when its device plan
+        # turned the shape down, e.g. more aggregate states than its LDS holds)
+        tried = ctx.kernel_time("fused_build")[1] + ctx.kernel_time("fused_build_declined")[1]
+        assert (tried > 0) == fused
     finally:
         ctx.timing(False)
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[j for j, (f, c) in enumerate(aggs) if f in (AF.Sum, AF.Avg)])

@@ -278,19 +278,55 @@ def test_msd_window_sub_keys_vs_oracle(ctx, monkeypatch, func, param, n, parts, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_window_sub_keys_dense_rank(ctx, monkeypatch, asc):
+    """DENSE_RANK over key ranges above 2^20: peer-group starts counted from each sub-key's first row."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(12)
+    n = 1_200_000
+    k = r.integers(0, 1 << 22, n).astype(np.int64) - 5
+    v = r.integers(-5, 5, n).astype(np.int64)
+    got, want, ran = _run(ctx, W.DenseRank, k, v, asc)
+    assert ran and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("func,param,default", [(W.Lag, 1, None), (W.Lead, 2, -5), (W.FirstValue, 0, None),
+                                                (W.LastValue, 0, None)])
+@pytest.mark.parametrize("asc", [True, False])
+def test_msd_value_functions_sub_keys(ctx, monkeypatch, func, param, default, asc):
+    """LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column over key ranges above 2^20: the
+    source row is found inside the row's own sub-key run."""
+    monkeypatch.setenv("QEH_WINDOW_MSD", "1")
+    r = np.random.default_rng(13)
+    n = 900_000
+    k = r.integers(0, (1 << 21) + 3, n).astype(np.int64)
+    v = r.integers(-50, 50, n).astype(np.int64)
+    d = None if default is None else np.int64(default)
+    ctx.timing(True)
+    ctx.timing_reset()
+    dv = ctx.upload(v)
+    got_v, got_m = ctx.window(func, [ctx.upload(k)], [dv], [asc], arg=dv, param=param, default=d).to_numpy()
+    ran = _msd_ran(ctx)
+    ctx.timing(False)
+    want_v, want_m = ob.window(func, [ob.HostCol(k)], [ob.HostCol(v)], [asc], arg=ob.HostCol(v), param=param, default=d)
+    assert ran
+    assert np.array_equal(got_m, want_m)
+    assert np.array_equal(got_v[want_m], want_v[want_m])
+
+
+@pytest.mark.gpu
 def test_msd_window_sub_keys_fallbacks(ctx, monkeypatch):
-    """Above 2^20 keys: DENSE_RANK is not taken (LSD path), a group above 2048 rows falls back; both
-    stay equal to the oracle."""
+    """Above 2^20 keys, a group above 2048 rows falls back to the LSD path and stays equal to the oracle."""
     monkeypatch.setenv("QEH_WINDOW_MSD", "1")
     r = np.random.default_rng(12)
     n = 400_000
     k = r.integers(0, 1 << 22, n).astype(np.int64)
     v = r.integers(-5, 5, n).astype(np.int64)
-    got, want, ran = _run(ctx, W.DenseRank, k, v, True)
-    assert not ran and np.array_equal(got, want)
     k[:5000] = 777  # one group of > 2048 rows
-    got, want, _ = _run(ctx, W.RowNumber, k, v, True)
-    assert np.array_equal(got, want)
+    for func in (W.RowNumber, W.DenseRank):
+        got, want, _ = _run(ctx, func, k, v, True)
+        assert np.array_equal(got, want)
 
 
 @pytest.mark.gpu
@@ -317,6 +353,5 @@ def test_msd_window_several_partition_keys(ctx, monkeypatch, func, param, ranges
         want, _ = ob.window(func, hk, [ob.HostCol(v)], [True], param=param)
     ran = _msd_ran(ctx)
     ctx.timing(False)
-    prod = int(np.prod(ranges))
-    assert ran == (prod <= (1 << (24 if func != W.DenseRank else 20)))
+    assert ran == (int(np.prod(ranges)) <= (1 << 24))
     assert np.array_equal(got, want)
