@@ -338,9 +338,12 @@ int qeh_join_filter_aggregate_table_lanes(qeh_ctx *ctx, const qeh_column *probe_
                                           int64_t key_min, uint64_t key_range, int64_t n_groups, const qeh_agg *aggs,
                                           int n_aggs, double *lanes);
 /* ..._lanes without a host wait: the operator's status words go to dev_status[0..3] (device memory;
- * [0] kernel error bits, [1] a slice region overflowed -- then the lanes are incomplete) and the call
- * returns as soon as its kernels are queued; the caller reads the words with its final results and,
- * when either is set, runs qeh_join_filter_aggregate_table_lanes (which recovers) instead. */
+ * [0] kernel error bits, [1] a slice region overflowed -- then the lanes are incomplete), and one more
+ * lane after the (1 + n_aggs) * n_groups ones, lanes[(1 + n_aggs) * n_groups] = 1.0 when either is set
+ * (else 0.0; `lanes` holds (1 + n_aggs) * n_groups + 1 doubles), so an all-reduce of the lanes carries
+ * every rank's flag.  The call returns as soon as its kernels are queued; the caller reads the flag
+ * with its final results and, when it is set, runs qeh_join_filter_aggregate_table_lanes (which
+ * recovers) instead. */
 int qeh_join_filter_aggregate_table_lanes_async(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
                                                 int probe_key_idx, const qeh_expr *predicate, const uint16_t *table,
                                                 int64_t key_min, uint64_t key_range, int64_t n_groups,

@@ -1810,9 +1810,13 @@ __global__ __launch_bounds__(256) void k_states_fold(uint64_t *__restrict__ stat
 // lanes[0][g] = rows of group g, lanes[1 + j][g] = aggregate j's partial (COUNT or float SUM; the
 // caller checked the kinds), every shard copy folded in: one thread per lane entry, 16 shard loads
 // in flight
+// status (the no-wait form): lanes[(1 + n) * G] = 1 when the operator's error or overflow word is set,
+// so the caller's all-reduce of the lanes carries every rank's flag.
 __global__ __launch_bounds__(256) void k_states_lanes(const uint64_t *__restrict__ states, int64_t Gs, int64_t G,
-                                                      AggSpecs specs, double *__restrict__ lanes) {
+                                                      AggSpecs specs, double *__restrict__ lanes,
+                                                      const uint32_t *__restrict__ status) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e == 0 && status) lanes[(int64_t)(1 + specs.n) * G] = (status[0] | status[1]) ? 1.0 : 0.0;
     if (e >= (int64_t)(1 + specs.n) * G) return;
     const int j = (int)(e / G) - 1;  // -1: the row-count lane
     const int64_t g = e % G;
@@ -3105,17 +3109,19 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     if (lanes) {
         // dense f64 lanes instead of compacted output columns (the distributed final stage sums them
         // over the ranks): one host round trip for the status words, none for outputs
-        auto emit = [&]() -> int {
-            hipLaunchKernelGGL(k_states_lanes, dim3((unsigned)(((1 + specs.n) * G + 255) / 256)), dim3(256), 0, ctx->stream,
-                               states.as<uint64_t>(), Gs, G, specs, lanes);
+        auto emit = [&](const uint32_t *status) -> int {
+            const int64_t ne = std::max<int64_t>((1 + specs.n) * G, 1);
+            hipLaunchKernelGGL(k_states_lanes, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, ctx->stream,
+                               states.as<uint64_t>(), Gs, G, specs, lanes, status);
             return hipGetLastError() == hipSuccess ? QEH_OK : fail(QEH_E_HIP, "aggregate: lanes launch failed");
         };
-        if (G > 0) QEH_TRY(emit());
-        if (dev_status) {  // the caller reads the status words later (and recovers from an overflow)
+        if (dev_status) {  // the caller reads the status later (and recovers from an overflow)
+            QEH_TRY(emit(errw.as<uint32_t>()));  // + the status lane
             QEH_HIP(hipMemcpyAsync(dev_status, errw.p, 16, hipMemcpyDeviceToDevice, ctx->stream));
             *out_groups = G;
             return QEH_OK;
         }
+        if (G > 0) QEH_TRY(emit(nullptr));
         uint32_t stw[4];
         QEH_TRY(read_small(ctx, stw, errw.p, 16));
         if (ovf_pending && stw[1]) {
@@ -3127,7 +3133,7 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
                 join_fallback(grid, per_cu);
             }
             QEH_HIP(hipGetLastError());
-            if (G > 0) QEH_TRY(emit());
+            if (G > 0) QEH_TRY(emit(nullptr));
             QEH_TRY(read_small(ctx, stw, errw.p, 16));
         }
         QEH_TRY(kernel_error_status(stw[0], "aggregate"));

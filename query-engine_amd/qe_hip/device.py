@@ -449,7 +449,9 @@ class Context:
                                                 key_range: int, n_groups: int, aggs: Sequence[Tuple[int, int]],
                                                 lanes_ptr: int, status_ptr: int) -> None:
         """qeh_join_filter_aggregate_table_lanes_async: as ..._lanes, but its status words (error bits,
-        region overflow) go to device memory at status_ptr and nothing waits on the host."""
+        region overflow) go to device memory at status_ptr, one more lane after the (1 + aggs) * n_groups
+        ones is 1.0 when either is set (lanes_ptr holds (1 + aggs) * n_groups + 1 doubles), and nothing
+        waits on the host."""
         cp = self._cols(probe_cols)
         ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
         e = keep = None

@@ -664,23 +664,22 @@ class DistributedExecutor:
             # table, the same on every rank) and the operator's status words (error bits, a slice region
             # overflow on this rank) stay on the device; the status rides the lanes' all-reduce as one
             # extra lane, so every rank sees every rank's flags and all take the same branch below
-            chk = torch.empty(2, dtype=torch.int64, device="cuda")
-            status = torch.zeros(4, dtype=torch.int32, device="cuda")
+            chk = torch.empty(1, dtype=torch.int64, device="cuda")
+            status = torch.empty(4, dtype=torch.int32, device="cuda")
+            # (1 + aggregates) lanes per group slot + the status lane the library writes last
             lanes = torch.empty((1 + len(aggs)) * G + 1, dtype=torch.float64, device="cuda")
             self._sync_torch()
             self.ctx.u16_count_nonzero_dev(table.data_ptr(), R, chk.data_ptr())
             self.ctx.join_filter_aggregate_table_lanes_async(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
                                                              R, G, aggs, lanes.data_ptr(), status.data_ptr())
             self._sync()
-            lanes[-1] = (status[:2] != 0).any().to(torch.float64)
             if self.world > 1:
                 dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
-            chk[1] = lanes[-1].to(torch.int64)
             self._sync_torch()
             ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank,
                                                    st["gdtype"],
                                                    [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
-            nz, bad = (int(q) for q in chk.tolist())
+            nz, bad = int(chk.item()), float(lanes[-1].item()) != 0.0
             if nz != total:
                 return None  # a build key repeats: the general path handles multi-match joins
             if bad:  # some rank's operator overflowed a slice region (or failed): redo it with the checks inline

@@ -312,5 +312,17 @@ timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke
 tail -3 $O/smoke.txt
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t>"; exit 2; }
+r4u() {
+# the status lane written by the lanes kernel (no torch ops between the probe and the lanes all-reduce)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4u; mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_distributed.py tests/test_pipeline.py -k "dist or table or rank" > $O/tests.txt 2>&1 || { echo "tests failed"; tail -30 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt
+for m in "" "QEH_SYNC_TABLE_CHECK=1" "" "QEH_SYNC_TABLE_CHECK=1"; do
+  env $m QEH_BENCH_RANK_OF=0/8 timeout -k 10 200 python3 bench.py --steps 30 --warmup 3 --cpu-sample 0 > $O/rank08.out 2>$O/rank08.err || { tail $O/rank08.err; exit 1; }
+  echo "[$m] $(tail -1 $O/rank08.out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), d["roofline"]["kernel_split_ms"])')"
+done
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u>"; exit 2; }
 "$1"
