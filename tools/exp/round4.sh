@@ -324,5 +324,17 @@ for m in "" "QEH_SYNC_TABLE_CHECK=1" "" "QEH_SYNC_TABLE_CHECK=1"; do
 done
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u>"; exit 2; }
+r4v() {
+# the window path's pipelined inverse pass 1: parity, then config 5 / LAG A/B against the serial kernel
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4v; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_window_msd.py tests/test_lds_rank.py tests/test_join_sort_window.py > $O/tests.txt 2>&1 || { echo "tests failed"; tail -40 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt
+for m in "" "QEH_WM_INV1_SERIAL=1" "" "QEH_WM_INV1_SERIAL=1"; do
+  env $m timeout -k 10 300 python3 -u tools/bench_configs.py --only cfg5,window > $O/cfg5.jsonl 2>$O/cfg5.err || { tail $O/cfg5.err; exit 1; }
+  echo "[$m] $(python3 -c 'import json,sys; print([(json.loads(l)["config"][:22], round(json.loads(l)["kernel_ms"],2), round(json.loads(l).get("window_place",0),2)) for l in open(sys.argv[1])])' $O/cfg5.jsonl)"
+done
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v>"; exit 2; }
 "$1"
