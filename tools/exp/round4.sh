@@ -336,5 +336,15 @@ for m in "" "QEH_WM_INV1_SERIAL=1" "" "QEH_WM_INV1_SERIAL=1"; do
 done
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v>"; exit 2; }
+r4w() {
+# the final tree: bench line (default run, as the driver runs it), twice
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4w; mkdir -p $O
+for i in 1 2; do
+  timeout -k 10 300 python3 bench.py > $O/bench_$i.json 2>$O/bench_$i.err || { tail $O/bench_$i.err; exit 1; }
+  python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(round(d["ms_per_step"],3), round(d["value"]/1e9,1), round(d["roofline"]["frac"],3), d["roofline"]["kernel_split_ms"], d["cpu_baseline"]["value"])' $O/bench_$i.json
+done
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w>"; exit 2; }
 "$1"
