@@ -3848,9 +3848,14 @@ static void launch_slice_partition_early(qeh_ctx *ctx, const FastIn &in, const P
     else                                                                                                                  \
         hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
                            pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
+// two aggregate columns (18-B items: half tiles, 16-item chunks), one 1024-thread workgroup per CU
+#define QEH_SE2(NTV, NTB)                                                                                                 \
+    hipLaunchKernelGGL((k_slice_partition<NTV, 2, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,     \
+                       pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
 #define QEH_SE_NA(NTV, NTB)                 \
     if (nacol == 0) { QEH_SE(NTV, 0, NTB); } \
-    else { QEH_SE(NTV, 1, NTB); }
+    else if (nacol == 1) { QEH_SE(NTV, 1, NTB); } \
+    else { QEH_SE2(NTV, NTB); }
 #define QEH_SE_NT(NTB)                         \
     if (nterms == 0) { QEH_SE_NA(0, NTB) }     \
     else if (nterms == 1) { QEH_SE_NA(1, NTB) } \
@@ -3858,6 +3863,7 @@ static void launch_slice_partition_early(qeh_ctx *ctx, const FastIn &in, const P
     if (nt) { QEH_SE_NT(true) } else { QEH_SE_NT(false) }
 #undef QEH_SE_NT
 #undef QEH_SE_NA
+#undef QEH_SE2
 #undef QEH_SE
 }
 
@@ -3873,16 +3879,21 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     if (nd <= 0 || nd >= ((int64_t)1 << 32) || gk.length != nd) return kFusedNotEligible;
     FastIn in;
     int nterms, nacol;
-    if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 1) return kFusedNotEligible;
+    if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 2 ||
+        (nacol == 2 && std::getenv("QEH_NO_FUSED_AGG2")))
+        return kFusedNotEligible;
     // phase A: the staged kernel with one 1024-thread or two 512-thread workgroups per CU
-    // (QEH_FUSED_2WG=1), or the ring kernel (QEH_FUSED_RING=1)
-    const bool ring = std::getenv("QEH_FUSED_RING") && std::atoi(std::getenv("QEH_FUSED_RING")) == 1;
-    const bool two = !ring && std::getenv("QEH_FUSED_2WG") && std::atoi(std::getenv("QEH_FUSED_2WG")) == 1;
+    // (QEH_FUSED_2WG=1), or the ring kernel (QEH_FUSED_RING=1); two aggregate columns take the staged
+    // kernel with 18-B items
+    const bool ring = nacol < 2 && std::getenv("QEH_FUSED_RING") && std::atoi(std::getenv("QEH_FUSED_RING")) == 1;
+    const bool two = nacol < 2 && !ring && std::getenv("QEH_FUSED_2WG") && std::atoi(std::getenv("QEH_FUSED_2WG")) == 1;
     constexpr int H = kSliceBlock / 2;
     const int64_t tile_rows = ring ? (int64_t)kSliceBlock * 2 * kRingPairs
+                              : nacol == 2 ? (int64_t)SliceShape<2, true>::TILE
                               : two ? (nacol ? SliceShape<1, true, H>::TILE : SliceShape<0, true, H>::TILE)
                                     : (nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE);
     const int chunk = ring ? kRingKC
+                      : nacol == 2 ? SliceShape<2, true>::CH
                       : two ? (nacol ? SliceShape<1, true, H>::CH : SliceShape<0, true, H>::CH)
                             : (nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH);
     const int64_t n_tiles = n / tile_rows, tail = n - n_tiles * tile_rows;
@@ -3901,7 +3912,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
                                              (int64_t)kMaxSliceGrid});
     const uint64_t tiles_per_wg = (uint64_t)((n_all + grid - 1) / grid);
 
-    DevBuf mm, plan, ditems, dcount, kbuf, vbuf, cbuf, states, errw, gkeys, rep;
+    DevBuf mm, plan, ditems, dcount, kbuf, vbuf, vbuf2, cbuf, states, errw, gkeys, rep;
     SlicePlanIn pi{};
     pi.min_bytes = 6ull << 20;
     if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
@@ -3919,6 +3930,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     QEH_TRY(dcount.alloc(ctx, nreg_max * 4 + 64));
     QEH_TRY(kbuf.alloc(ctx, pi.alloc_items * 2 + 64));
     if (nacol) QEH_TRY(vbuf.alloc(ctx, pi.alloc_items * 8 + 64));
+    if (nacol > 1) QEH_TRY(vbuf2.alloc(ctx, pi.alloc_items * 8 + 64));
     QEH_TRY(cbuf.alloc(ctx, nreg_max * 4 + 64));
     QEH_TRY(states.alloc(ctx, (size_t)specs.shards * specs.n_slots * Gs * 8));
     // status words (zeroed by k_fused_plan): [0] kernel error bits, [1] region overflow, [2..3] groups,
@@ -3930,6 +3942,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     SliceRegions rg{};
     rg.key = kbuf.as<uint16_t>();
     rg.val = nacol ? vbuf.as<int64_t>() : nullptr;
+    rg.val2 = nacol > 1 ? vbuf2.as<int64_t>() : nullptr;
     rg.count = cbuf.as<uint32_t>();
     rg.overflow = st + 1;
     FusedPlan *dplan = plan.as<FusedPlan>();
@@ -3971,6 +3984,9 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
         if (nacol == 0) {
             if (pf) QEH_SD(0, true, false);
             else QEH_SD(0, false, false);
+        } else if (nacol == 2) {  // (item pairs carry one value column: two columns load per item)
+            if (pf) QEH_SD(2, true, false);
+            else QEH_SD(2, false, false);
         } else if (pv) {
             if (pf) QEH_SD(1, true, true);
             else QEH_SD(1, false, true);

@@ -279,6 +279,26 @@ def test_fused_phase_a_variants(ctx, monkeypatch, variant, skew):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_fact,n_dim,key0", [(1_000_003, 300_001, -12_345), (2_500_007, 70_000, 0)])
+def test_fused_two_aggregate_columns(ctx, monkeypatch, n_fact, n_dim, key0):
+    """Two aggregate input columns on the fused pipeline (18-B items, half tiles, 16-item chunks, the
+    build grouped in phase A's prologue): SUM / MIN / MAX over a float and an integer column, COUNT;
+    misses, ragged tail; equal to the oracle, and the fused kernels ran."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    rng = np.random.default_rng(19)
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 512)
+    k = k + key0
+    dk = dk + key0
+    k[::89] = key0 - 1 - k[::89]
+    w = rng.integers(-(1 << 40), 1 << 40, n_fact)
+    probe = [(x, None), (k, None), (v, None), (w, None)]
+    aggs = [(AF.Sum, 2), (AF.Sum, 3), (AF.Count, 2), (AF.Min, 3), (AF.Max, 2)]
+    (gk, ga, wk, wa), ran = _fused_ran(ctx, lambda: run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs))
+    assert ran
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n_fact,n_dim,key0", [(1_000_003, 300_001, -12_345), (600_000, 70_000, 0)])
 def test_slice_two_aggregate_columns(ctx, monkeypatch, n_fact, n_dim, key0):
     """Two aggregate input columns on the LDS-slice pipeline (18-B items: half tiles, 16-item

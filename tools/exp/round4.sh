@@ -346,5 +346,17 @@ for i in 1 2; do
 done
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w>"; exit 2; }
+r4x() {
+# the fused pipeline with two aggregate columns: parity, then the agg2 shape A/B against the prelaunch path
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4x; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_pipeline.py > $O/tests.txt 2>&1 || { echo "tests failed"; tail -40 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt
+for m in "" "QEH_NO_FUSED_AGG2=1" "" "QEH_NO_FUSED_AGG2=1"; do
+  env $m timeout -k 10 300 python3 -u -c "import sys; sys.argv=['x','--only','shapes']; sys.path.insert(0,'tools'); import bench_configs as b; b.cfg_metric_shapes.__defaults__ = (('agg2',),); b.main()" > $O/agg2.jsonl 2>$O/agg2.err || { tail $O/agg2.err; exit 1; }
+  echo "[$m] $(python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(round(d["ms_per_run"],2), round(d["kernel_ms"],2), round(d["frac_of_8TBs"],3), d["dominant_kernel"])' $O/agg2.jsonl)"
+done
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x>"; exit 2; }
 "$1"
