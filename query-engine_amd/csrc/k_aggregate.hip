@@ -1208,6 +1208,117 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     }
 }
 
+// Phase B of the key-window pipeline (group states too large for LDS, join key range within the slice
+// shape): the group is a function of the join key, so rows are aggregated per KEY first and each key's
+// partial state is merged into its group's global states once -- 1e7 merges instead of one global
+// atomic per row and aggregate, and no group-id gather in phase A (try_gid_slices' MODE 1 read a
+// 40-MB table at random: 11.8 of the 12.6 ms of the 2^17-group query).
+// Per-key states of a whole 2^16-key slice do not fit LDS, so a slice is split into nw windows of ws
+// keys (ws * (4 + 8 * value slots) bytes of LDS: a u32 row count and the value slots per key), one per
+// workgroup of a group of nw workgroups that all read the slice's items and keep those of their
+// window.  The group's workgroups sit on one XCD (workgroup x runs on XCD x % 8) and walk the regions
+// in the same order, so each item line comes from HBM once and from that XCD's L2 the other nw - 1
+// times (r04 counters: 39.5M HBM read requests = the items once, 82 % L2 hits): the L2 -> CU traffic
+// is what bounds the kernel, hence the compact states and the fewest windows that fit.
+// Work units: slices [0, full) whole, then each remaining slice split into `tparts` parts of its
+// regions, so the last round of units is short instead of leaving most groups idle (two groups holding
+// partials of one key each merge theirs: the merges are memory-side atomics, ~0.5 ms per 1e7 keys, so
+// only the tail is split).  gridDim.x = 8 * (groups per XCD) * nw.
+constexpr int kKeyAggWords = 20400;  // LDS words of k_slice_keyagg's states (163200 B)
+template <int NACOL>
+__global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, int nreg, HashTable t, AggSpecs specs,
+                                                              int64_t G, uint64_t *__restrict__ gstates_all, int nw, int ws,
+                                                              int full, int tparts) {
+    __shared__ uint64_t lbuf[kKeyAggWords];
+    uint32_t *lcnt = (uint32_t *)lbuf;                 // [ws] row counts
+    uint64_t *lval = lbuf + ((uint32_t)ws + 1u) / 2u;  // [slot - 1][ws] value slots
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int W = kSliceBlock / 64;
+    const int gpx = (int)gridDim.x / 8 / nw;  // groups per XCD
+    const int xcd = (int)blockIdx.x & 7, x = (int)blockIdx.x >> 3;
+    const int grp = xcd * gpx + x / nw, ngrp = 8 * gpx;
+    const uint32_t lo = (uint32_t)(x % nw) * (uint32_t)ws;  // this workgroup's keys: [lo, lo + ws) of the slice
+    auto init = [&]() {
+        for (int i = tid; i < ws; i += kSliceBlock) lcnt[i] = 0u;
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind == AK_COUNT) continue;
+            const uint64_t v0 = (uint64_t)agg_init_value(sp.kind);
+            for (int i = tid; i < ws; i += kSliceBlock) lval[(int64_t)(sp.val_slot - 1) * ws + i] = v0;
+        }
+    };
+    init();
+    const int units = full + (rg.F - full) * tparts;
+    for (int u = grp; u < units; u += ngrp) {
+        const int tu = u - full;
+        const int b = tu < 0 ? u : full + tu / tparts, parts = tu < 0 ? 1 : tparts, part = tu < 0 ? 0 : tu % tparts;
+        const int r0 = part * nreg / parts, r1 = (part + 1) * nreg / parts;
+        __syncthreads();
+        for (int r = r0 + wave; r < r1; r += W) {
+            const uint64_t reg = (uint64_t)r * rg.F + b;
+            const uint32_t n_r = rg.count[reg];
+            const uint16_t *kp = rg.key + reg * rg.cap;
+            const int64_t *vp = NACOL ? rg.val + reg * rg.cap : nullptr;
+            for (uint32_t i0 = 0; i0 < n_r; i0 += 64 * 8) {
+                uint32_t e[8];
+                int64_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t i = i0 + (uint32_t)j * 64 + lane;
+                    const uint32_t ii = i < n_r ? i : 0u;
+                    const uint32_t k = (uint32_t)kp[ii] - lo;  // below the window -> huge
+                    v[j] = NACOL ? vp[ii] : 0;
+                    e[j] = (i < n_r && k < (uint32_t)ws) ? k + 1u : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (e[j]) atomicAdd(lcnt + (e[j] - 1u), 1u);
+                for (int a = 0; a < specs.n; ++a) {
+                    const AggSpec sp = specs.a[a];
+                    if (sp.kind == AK_COUNT) continue;  // the row count
+                    uint64_t *st = lval + (int64_t)(sp.val_slot - 1) * ws - 1;  // indexed by entry = key + 1
+                    switch (sp.kind) {
+                        case AK_SUM_F:
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) atomicAdd((double *)&st[e[j]], as_f64(v[j]));
+                            break;
+                        case AK_SUM_I:
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) atomicAdd((unsigned long long *)&st[e[j]], (unsigned long long)v[j]);
+                            break;
+                        default:  // MIN / MAX
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                if (e[j]) agg_apply<true>(sp.kind, &st[e[j]], agg_input(sp.kind, sp.in_type, v[j]));
+                            break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // the window's keys with rows: their group from the join table, one merge per key
+        const uint64_t k0 = ((uint64_t)b << kSliceBits) + lo;
+        for (int i = tid; i < ws; i += kSliceBlock) {
+            const uint64_t rows = lcnt[i];
+            if (!rows || k0 + i >= t.range) continue;
+            const uint32_t ent = t.payload16 ? (uint32_t)t.payload16[k0 + i] : t.payload[k0 + i];
+            if (!ent) continue;  // no build row with this key
+            const int64_t g = (int64_t)ent - 1;
+            atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
+            for (int a = 0; a < specs.n; ++a) {
+                const AggSpec sp = specs.a[a];
+                if (sp.kind != AK_COUNT)
+                    agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lval[(int64_t)(sp.val_slot - 1) * ws + i]);
+            }
+        }
+        __syncthreads();
+        init();
+    }
+}
+
 // ---- fused pipeline: the plan -----------------------------------------------------------------
 // The build rows (key, group key) take the probe rows' route: phase A's prologue groups them by slice
 // (4-B items), and phase B builds each slice's entries in LDS from them instead of loading a join table
@@ -2776,6 +2887,71 @@ static int try_slice_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     return 1;
 }
 
+// Key-window slices (k_slice_keyagg) for joins whose group states do not fit LDS but whose build key
+// range fits the slice shape (a direct table, entries of any width): phase A as for the LDS-state
+// pipeline, phase B aggregates per join key.  Returns 1 when it ran; 0 when not eligible or a region
+// overflowed, with the states re-initialised.
+static int try_key_slices(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
+                          const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err) {
+    if (std::getenv("QEH_NO_SLICES") || std::getenv("QEH_NO_KEY_SLICES")) return 0;
+    FastIn in;
+    int nterms, nacol;
+    if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol) || nacol > 1) return 0;
+    const HashTable &t = src.jt;
+    if (t.kind != TK_DIRECT || !t.unique) return 0;
+    // windows: the fewest whose per-key states (u32 count + 8 B per value slot) fit the LDS words
+    const int64_t per_key = 4 + 8 * (int64_t)(specs.n_slots - 1);
+    const int64_t ws_max = (int64_t)kKeyAggWords * 8 / per_key / 2 * 2;
+    const int nw = (int)((kSliceKeys + ws_max - 1) / ws_max);
+    const int ws = (int)(((kSliceKeys + nw - 1) / nw + 1) / 2 * 2);
+    const int gpx = ctx->props.multiProcessorCount / 8 / nw;  // groups of nw workgroups per XCD
+    if (gpx == 0 || (int64_t)ws * per_key > (int64_t)kKeyAggWords * 8) return 0;
+    const int gridB = 8 * gpx * nw;
+    const uint64_t F = (t.range + kSliceKeys - 1) >> kSliceBits;
+    if (F == 0 || F > (uint64_t)kSliceMaxF) return 0;
+    uint64_t min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) min_bytes = std::strtoull(e, nullptr, 10);
+    if (table_bytes(t) < min_bytes) return 0;
+    const int64_t n_tiles = n / kSliceTile;
+    if (n_tiles == 0) return 0;
+    const int grid = (int)std::min<int64_t>(ctx->props.multiProcessorCount, n_tiles);
+    DevBuf kbuf, vbuf, cbuf;
+    SliceRegions rg{};
+    if (!slice_regions(ctx, n_tiles, grid, F, nacol, &kbuf, &vbuf, &cbuf, &rg, ctx->stream)) return 0;
+    launch_slice_partition(ctx, in, pp, nterms, nacol, t.kmin, t.range, n_tiles, grid, rg, ctx->stream);
+    {
+        KernelTimer ktb(ctx, "slice_keyagg");
+        // whole slices for the full rounds of the 8 * gpx groups; the slices left over split so that the
+        // last round has about one part per group (QEH_KEYAGG_TAIL=0: whole slices only)
+        const int ngrp = 8 * gpx;
+        int full = (int)F / ngrp * ngrp, tparts = 1;
+        if ((int)F > full) tparts = std::max(1, std::min(grid, ngrp / ((int)F - full)));
+        if (const char *e = std::getenv("QEH_KEYAGG_TAIL"))
+            if (std::atoi(e) == 0) full = (int)F, tparts = 1;
+        if (nacol == 0)
+            hipLaunchKernelGGL(k_slice_keyagg<0>, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, specs, G,
+                               states, nw, ws, full, tparts);
+        else
+            hipLaunchKernelGGL(k_slice_keyagg<1>, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, specs, G,
+                               states, nw, ws, full, tparts);
+    }
+    const int64_t done = n_tiles * kSliceTile;
+    if (done < n) {  // ragged tail: generic kernel, global states
+        ColSet tail = cols;
+        for (int i = 0; i < cols.n; ++i) tail.c[i] = advance(cols.c[i], done);
+        launch_agg_rows<GM_JOIN>(ctx, pp.mode, false, 1, 0, tail, n - done, pp, src, specs, G, states, err);
+    }
+    if (hipGetLastError() != hipSuccess) return 0;
+    uint32_t of = 0;
+    if (read_small(ctx, &of, rg.overflow, 4) != QEH_OK) return 0;
+    if (of) {
+        hipLaunchKernelGGL(k_states_init, dim3(grid_for(ctx, specs.shards * specs.n_slots * G, kBlock * 4, 8)), dim3(kBlock), 0,
+                           ctx->stream, states, G, specs);
+        return 0;
+    }
+    return 1;
+}
+
 // Group-range slices for joins whose group states do not fit LDS (G > kSliceStateWords /
 // n_slots): phase A (MODE 1) looks each selected row's group id up in the join table and
 // partitions the rows by gid >> kGidSliceBits; phase B (IDENT) aggregates each range of
@@ -3051,7 +3227,8 @@ static int aggregate_rows(qeh_ctx *ctx, int gm, const ColSet &cols, int64_t n, c
     const bool lds = lds_bytes <= kLdsStateBudget;
     // fused join-aggregate when the LDS-slice pipeline does not run (or overflowed)
     auto join_fallback = [&](int grid, int per_cu) {
-        if (!lds && try_gid_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>()) == 1) {
+        if (!lds && (try_key_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>()) == 1 ||
+                     try_gid_slices(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>()) == 1)) {
         } else if (!(lds && try_fast_join(ctx, cols, n, pp, src, specs, Gs, states.as<uint64_t>(), errw.as<uint32_t>(),
                                           lds_bytes, per_cu)))
             launch_agg_rows<GM_JOIN>(ctx, pp.mode, lds, grid, lds ? lds_bytes : 0, cols, n, pp, src, specs, Gs,

@@ -387,12 +387,19 @@ def test_metric_widened_shapes_1e7(ctx, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("groups,skew", [(40_000, False), (1 << 17, False), (300_001, False), (1 << 17, True)])
-def test_group_range_slices(ctx, groups, skew):
-    """More groups than LDS states hold: phase A looks the group id up and partitions the rows by
-    group range, phase B aggregates each range of 4096 groups in LDS (k_slice_partition MODE 1 +
-    k_slice_probe IDENT).  Integer SUM, MIN, MAX and COUNT bit-exact;
-    a group range holding most rows overflows its regions and the generic kernel answers.
-    (The float SUM case is test_metric_widened_shapes_1e7[g17].)"""
+@pytest.mark.parametrize("path", ["gid", "key"])
+def test_group_range_slices(ctx, monkeypatch, groups, skew, path):
+    """More groups than LDS states hold.  gid: phase A looks the group id up and partitions the rows
+    by group range, phase B aggregates each range of 4096 groups in LDS (k_slice_partition MODE 1 +
+    k_slice_probe IDENT); a group range holding most rows overflows its regions and the generic
+    kernel answers.  key: phase A partitions by join key, phase B aggregates per key in LDS windows
+    and merges each key into its group once (k_slice_keyagg; 4 state slots -> 4096-key windows).
+    Integer SUM, MIN, MAX and COUNT bit-exact.  (The float SUM case is
+    test_metric_widened_shapes_1e7[g17].)"""
+    if path == "gid":
+        monkeypatch.setenv("QEH_NO_KEY_SLICES", "1")
+    else:
+        monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
     n, nd = 3_000_000, 400_000
     x, k, v, dk, dg = metric_data(n, nd, groups)
     if skew:
@@ -405,9 +412,35 @@ def test_group_range_slices(ctx, groups, skew):
     ctx.timing_reset()
     gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
     ran = ctx.kernel_time("slice_partition")[1] > 0
+    keyagg = ctx.kernel_time("slice_keyagg")[1] > 0
     ctx.timing(False)
-    assert ran
+    assert ran and keyagg == (path == "key")
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", ["", "0"])
+def test_key_slices_count_and_parts(ctx, monkeypatch, tail):
+    """k_slice_keyagg with COUNT only (no value column: 2 windows of 32768 keys) and with float SUM +
+    COUNT (5 windows of 13108 keys); the slices past the full rounds split into region parts (each part
+    merges its own per-key partials) or not (QEH_KEYAGG_TAIL=0); 2^17 groups, keys outside the build
+    range, equal to the oracle."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    if tail:
+        monkeypatch.setenv("QEH_KEYAGG_TAIL", tail)
+    n, nd = 2_500_000, 300_000
+    x, k, v, dk, dg = metric_data(n, nd, 1 << 17)
+    k = k.copy()
+    k[::97] += nd  # no build row
+    probe = [(x, None), (k, None), (v, None)]
+    for aggs in ([(AF.Count, 0)], [(AF.Sum, 2), (AF.Count, 2)]):
+        ctx.timing(True)
+        ctx.timing_reset()
+        gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+        ran = ctx.kernel_time("slice_keyagg")[1] > 0
+        ctx.timing(False)
+        assert ran
+        assert_grouped_equal(gk, ga, wk, wa, float_aggs=float_idx(aggs, probe))
 
 
 def _host_threads():

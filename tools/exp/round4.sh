@@ -358,5 +358,44 @@ for m in "" "QEH_NO_FUSED_AGG2=1" "" "QEH_NO_FUSED_AGG2=1"; do
 done
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x>"; exit 2; }
+r4y() {
+# key-window slices (k_slice_keyagg) for the 2^17-group shape: parity, then A/B against the group-range slices
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4y; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_pipeline.py -k "group_range or widened" > $O/tests.txt 2>&1 || { echo "tests failed"; tail -40 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt
+for m in "" "QEH_NO_KEY_SLICES=1" ""; do
+  env $m timeout -k 10 300 python3 -u -c "import sys; sys.argv=['x','--only','shapes']; sys.path.insert(0,'tools'); import bench_configs as b; b.cfg_metric_shapes.__defaults__ = (('g17',),); b.main()" > $O/g17.jsonl 2>$O/g17.err || { tail $O/g17.err; exit 1; }
+  echo "[$m] $(python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(round(d["ms_per_run"],2), round(d["kernel_ms"],2), round(d["frac_of_8TBs"],3), d["dominant_kernel"], {k: round(v, 3) for k, v in d["kernel_split_ms"].items()})' $O/g17.jsonl)"
+done
+}
+
+r4z() {
+# k_slice_keyagg variants (LS: workgroup walks regions in turn, PF: prefetch) on the 2^17-group shape, then L2 hits
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4z; mkdir -p $O
+G17="import sys; sys.argv=['x','--only','shapes']; sys.path.insert(0,'tools'); import bench_configs as b; b.cfg_metric_shapes.__defaults__ = (('g17',),); b.main()"
+for v in ${R4Z_VARS:-0 1 2 3 0}; do
+  QEH_KEYAGG_TAIL=$v timeout -k 10 300 python3 -u -c "$G17" > $O/g17.jsonl 2>$O/g17.err || { tail $O/g17.err; exit 1; }
+  echo "[var $v] $(python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(round(d["ms_per_run"],2), round(d["kernel_ms"],2), round(d["frac_of_8TBs"],3), {k: round(v, 3) for k, v in d["kernel_split_ms"].items() if v})' $O/g17.jsonl)"
+done
+[ -n "$R4Z_NOPMC" ] && return 0
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d $O/pmc -o pmc --output-format csv -- python3 -u -c "$G17" > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
+python3 - $O <<'PY'
+import csv, glob, sys, collections
+f = glob.glob(sys.argv[1] + "/pmc/**/*counter_collection.csv", recursive=True)
+acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
+for path in f:
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"][:60]
+        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        if r["Counter_Name"] == "TCC_HIT_sum": n[k] += 1
+for k, d in acc.items():
+    if "slice" in k:
+        print(k, n[k], {c: round(v / n[k] / 1e6, 2) for c, v in d.items()}, "hit", round(d["TCC_HIT_sum"] / max(1, d["TCC_HIT_sum"] + d["TCC_MISS_sum"]), 3))
+PY
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x r4y r4z>"; exit 2; }
 "$1"
