@@ -397,5 +397,20 @@ for k, d in acc.items():
 PY
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x r4y r4z>"; exit 2; }
+r4f2() {
+# full GPU suite on the final tree, the three widened metric shapes, and the 2^17-group shape's kernel stats
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4f2; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.txt 2>&1 || { echo "tests failed"; tail -30 $O/gpu_tests.txt; exit 1; }
+tail -1 $O/gpu_tests.txt
+timeout -k 10 300 python3 -u tools/bench_configs.py --only shapes > $O/shapes.jsonl 2>$O/shapes.err || { tail $O/shapes.err; exit 1; }
+python3 -c 'import json,sys; [print(d["config"], round(d["ms_per_run"],2), round(d["kernel_ms"],2), round(d["frac_of_8TBs"],3), d["dominant_kernel"]) for d in map(json.loads, open(sys.argv[1]))]' $O/shapes.jsonl
+G17="import sys; sys.argv=['x','--only','shapes']; sys.path.insert(0,'tools'); import bench_configs as b; b.cfg_metric_shapes.__defaults__ = (('g17',),); b.main()"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/g17prof -o g17 --output-format csv -- python3 -u -c "$G17" > $O/g17prof.log 2>&1 || { tail $O/g17prof.log; exit 1; }
+find $O/g17prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/g17_kernel_stats.csv
+head -6 $O/g17_kernel_stats.csv | cut -c1-200
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x r4y r4z r4f2>"; exit 2; }
 "$1"
