@@ -443,6 +443,21 @@ def test_key_slices_count_and_parts(ctx, monkeypatch, tail):
         assert_grouped_equal(gk, ga, wk, wa, float_aggs=float_idx(aggs, probe))
 
 
+@pytest.mark.gpu
+def test_key_slices_skewed_keys_fall_back(ctx, monkeypatch):
+    """Three quarters of the probe rows on one join key: phase A's regions for that slice overflow,
+    the key-window path re-initialises the states and declines, and the query still equals the oracle
+    (group-range slices or the generic kernel answer)."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    n, nd = 2_000_000, 300_000
+    x, k, v, dk, dg = metric_data(n, nd, 1 << 17)
+    k = k.copy()
+    k[: n * 3 // 4] = 12_345
+    probe = [(x, None), (k, None), (v, None)]
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS)
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
 def _host_threads():
     import os
     n = len(os.sched_getaffinity(0))
