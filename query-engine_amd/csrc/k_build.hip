@@ -345,7 +345,9 @@ static int direct_group_table_insert(qeh_ctx *ctx, const qeh_column *build_key, 
     const int64_t n = build_key->length;
     DevBuf bad;
     QEH_TRY(bad.alloc(ctx, 8));
-    QEH_HIP(hipMemsetAsync(bad.p, 0, 8, ctx->stream));
+    // the async form never reads the flag: no memset, whose blit kernel queued beside a running phase A
+    // waited for its CUs (0.63 ms) and held the insert behind it
+    if (check) QEH_HIP(hipMemsetAsync(bad.p, 0, 8, ctx->stream));
     if (n > 0) {
         KernelTimer kt(ctx, "join_build");
         hipLaunchKernelGGL(k_direct_group_insert, dim3(grid_for(ctx, n, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,

@@ -582,7 +582,6 @@ class DistributedExecutor:
                 or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32)):
             return None
         n = len(build_key)
-        ts = [self._to_tensors(c)[0] for c in cols]
         flags = [1 if any(c.c.validity for c in cols) else 0] + list(probe_flags)
         # [rows, key min / max, group key min / max, flags] written on the device by one library call
         # (min / max kernels, no host wait), gathered over the ranks, read back once
@@ -597,23 +596,35 @@ class DistributedExecutor:
         # the rows' copy to the host is queued ahead of phase A: a copy queued behind it would wait for
         # phase A's workgroups to leave the CUs (the copy engine's blit kernel needs a CU), so the host
         # would sit idle for the whole of phase A before it could queue the build and phase B
-        row_host = torch.empty(row.numel(), dtype=torch.int64, pin_memory=True)
+        # (one pinned buffer per row size, reused every step: M below is copied out of it)
+        pinned = getattr(self, "_stats_pinned", None)
+        if pinned is None or pinned.numel() != row.numel():
+            pinned = self._stats_pinned = torch.empty(row.numel(), dtype=torch.int64, pin_memory=True)
+        row_host = pinned
         row_host.copy_(row, non_blocking=True)
         copied = torch.cuda.Event()
         copied.record()
         prelaunched = False
+        # the table form's u16 table of the previous step, zeroed here -- ahead of phase A on the queue --
+        # for this step to reuse when its key range is the same: zeroed behind phase A it waited for
+        # phase A's CUs (0.67 ms for 20 MB), and the table insert, its count and phase B's set-up with it
+        table_zeroed = False
+        tc = getattr(self, "_table_cache", None)
+        if tc is not None and probe is not None and not os.environ.get("QEH_NO_TABLE_CACHE"):
+            tc.zero_()
+            table_zeroed = True
         if probe is not None and not os.environ.get("QEH_HOST_PLAN"):
             # phase A planned on the device from the gathered rows: it starts while the host reads them
             self._sync_torch()
             self.ctx.join_filter_aggregate_prelaunch_stats(*probe, row.data_ptr(), self.world, 5 + len(flags))
             prelaunched = True
         copied.synchronize()
-        M = row_host.numpy().reshape(self.world, -1)
+        M = row_host.numpy().reshape(self.world, -1).copy()
         rows = [int(x) for x in M[:, 0]]
         total = sum(rows)
-        out = {"M": M, "rows": rows, "total": total, "n": n, "ts": ts, "bitmap": bool(M[:, 5].max() > 0),
+        out = {"M": M, "rows": rows, "total": total, "n": n, "cols": cols, "bitmap": bool(M[:, 5].max() > 0),
                "agreed": M[:, 6:].max(axis=0), "gdtype": build_group_keys[0].dtype, "prelaunched": prelaunched,
-               "stats_dev": row}
+               "stats_dev": row, "table_zeroed": table_zeroed}
         if total:
             live = M[M[:, 0] > 0]
             out["krange"] = [int(live[:, 1].min()), int(live[:, 2].max()), total]
@@ -644,7 +655,13 @@ class DistributedExecutor:
         if not st["prelaunched"]:
             self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"],
                                                      st["grange"])
-        table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
+        tc = getattr(self, "_table_cache", None)
+        if st.get("table_zeroed") and tc is not None and tc.numel() == (R + 1) // 2:
+            table = tc  # zeroed ahead of phase A in _build_stats
+        else:
+            table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
+            if not os.environ.get("QEH_NO_TABLE_CACHE"):
+                self._table_cache = table
         self._sync_torch()  # zeroed before the library writes
         lanes_ok = (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
                     and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
@@ -664,12 +681,15 @@ class DistributedExecutor:
             # table, the same on every rank) and the operator's status words (error bits, a slice region
             # overflow on this rank) stay on the device; the status rides the lanes' all-reduce as one
             # extra lane, so every rank sees every rank's flags and all take the same branch below
-            chk = torch.empty(1, dtype=torch.int64, device="cuda")
             status = torch.empty(4, dtype=torch.int32, device="cuda")
-            # (1 + aggregates) lanes per group slot + the status lane the library writes last
-            lanes = torch.empty((1 + len(aggs)) * G + 1, dtype=torch.float64, device="cuda")
+            # (1 + aggregates) lanes per group slot + the status lane the library writes last, then one
+            # word outside the all-reduced lanes for the table's non-empty count (int64 bits): the two
+            # checks come back in one 16-B read, with no torch kernels between the step's end and it
+            nl = (1 + len(aggs)) * G + 1
+            lanes_buf = torch.empty(nl + 1, dtype=torch.float64, device="cuda")
+            lanes = lanes_buf[:nl]
             self._sync_torch()
-            self.ctx.u16_count_nonzero_dev(table.data_ptr(), R, chk.data_ptr())
+            self.ctx.u16_count_nonzero_dev(table.data_ptr(), R, lanes_buf[nl:].data_ptr())
             self.ctx.join_filter_aggregate_table_lanes_async(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
                                                              R, G, aggs, lanes.data_ptr(), status.data_ptr())
             self._sync()
@@ -679,7 +699,8 @@ class DistributedExecutor:
             ok, ov, g = self.ctx.dense_states_take(lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank,
                                                    st["gdtype"],
                                                    [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
-            nz, bad = int(chk.item()), float(lanes[-1].item()) != 0.0
+            tail = lanes_buf[nl - 1:].cpu().numpy()  # [status lane, non-empty count]
+            nz, bad = int(tail[1:].view(np.int64)[0]), float(tail[0]) != 0.0
             if nz != total:
                 return None  # a build key repeats: the general path handles multi-match joins
             if bad:  # some rank's operator overflowed a slice region (or failed): redo it with the checks inline
@@ -730,7 +751,8 @@ class DistributedExecutor:
         caller all-gathers first)."""
         if self.world == 1 or st["bitmap"] or not st["total"]:
             return None
-        rows, n, ts = st["rows"], st["n"], st["ts"]
+        rows, n = st["rows"], st["n"]
+        ts = [self._to_tensors(c)[0] for c in st["cols"]]
         mx = max(rows)
         bufs, works = [], []
         for t in ts:
