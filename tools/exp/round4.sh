@@ -412,5 +412,17 @@ find $O/g17prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/g17_ke
 head -6 $O/g17_kernel_stats.csv | cut -c1-200
 }
 
-[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x r4y r4z r4f2>"; exit 2; }
+r4end() {
+# last tree: GPU suite, smoke, the default bench line
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4end; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.txt 2>&1 || { echo "tests failed"; tail -30 $O/gpu_tests.txt; exit 1; }
+tail -1 $O/gpu_tests.txt
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail $O/smoke.txt; exit 1; }
+tail -2 $O/smoke.txt
+timeout -k 10 400 python3 bench.py > $O/bench.out 2>$O/bench.err || { tail $O/bench.err; exit 1; }
+tail -1 $O/bench.out | cut -c1-400
+}
+
+[ -n "$1" ] || { echo "usage: $0 <session: r4a r4b r4c r4d r4e r4f r4g r4h r4i r4j r4k r4l r4m r4n r4o r4p r4q r4r r4s r4t r4u r4v r4w r4x r4y r4z r4f2 r4end>"; exit 2; }
 "$1"
