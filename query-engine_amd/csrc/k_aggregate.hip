@@ -1224,14 +1224,18 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
 // regions, so the last round of units is short instead of leaving most groups idle (two groups holding
 // partials of one key each merge theirs: the merges are memory-side atomics, ~0.5 ms per 1e7 keys, so
 // only the tail is split).  gridDim.x = 8 * (groups per XCD) * nw.
-constexpr int kKeyAggWords = 20400;  // LDS words of k_slice_keyagg's states (163200 B)
-template <int NACOL>
+// C16: u16 row counts (two per LDS dword, returned atomics catch a count passing 65535 and flag the
+// regions' overflow word, so the host falls back): SUM + COUNT fit 4 windows of 16384 keys, COUNT alone
+// one window per slice.
+constexpr int kKeyAggWords = 20480;  // LDS words of k_slice_keyagg's states (163840 B, all of a CU's LDS)
+template <int NACOL, bool C16 = false>
 __global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, int nreg, HashTable t, AggSpecs specs,
                                                               int64_t G, uint64_t *__restrict__ gstates_all, int nw, int ws,
                                                               int full, int tparts) {
     __shared__ uint64_t lbuf[kKeyAggWords];
-    uint32_t *lcnt = (uint32_t *)lbuf;                 // [ws] row counts
-    uint64_t *lval = lbuf + ((uint32_t)ws + 1u) / 2u;  // [slot - 1][ws] value slots
+    uint32_t *lcnt = (uint32_t *)lbuf;  // [ws] row counts (C16: [ws / 2] dwords of two)
+    uint64_t *lval = lbuf + (C16 ? ((uint32_t)ws + 3u) / 4u : ((uint32_t)ws + 1u) / 2u);  // [slot - 1][ws] value slots
+    bool ovf = false;
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int W = kSliceBlock / 64;
@@ -1240,7 +1244,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, i
     const int grp = xcd * gpx + x / nw, ngrp = 8 * gpx;
     const uint32_t lo = (uint32_t)(x % nw) * (uint32_t)ws;  // this workgroup's keys: [lo, lo + ws) of the slice
     auto init = [&]() {
-        for (int i = tid; i < ws; i += kSliceBlock) lcnt[i] = 0u;
+        for (int i = tid; i < (C16 ? (ws + 1) / 2 : ws); i += kSliceBlock) lcnt[i] = 0u;
         for (int a = 0; a < specs.n; ++a) {
             const AggSpec sp = specs.a[a];
             if (sp.kind == AK_COUNT) continue;
@@ -1272,8 +1276,16 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, i
                     e[j] = (i < n_r && k < (uint32_t)ws) ? k + 1u : 0u;
                 }
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (e[j]) atomicAdd(lcnt + (e[j] - 1u), 1u);
+                for (int j = 0; j < 8; ++j) {
+                    if (!e[j]) continue;
+                    if constexpr (C16) {
+                        const uint32_t sh = ((e[j] - 1u) & 1u) * 16u;
+                        const uint32_t old = atomicAdd(lcnt + ((e[j] - 1u) >> 1), 1u << sh);
+                        ovf |= ((old >> sh) & 0xFFFFu) == 0xFFFFu;  // this add carried into the neighbour
+                    } else {
+                        atomicAdd(lcnt + (e[j] - 1u), 1u);
+                    }
+                }
                 for (int a = 0; a < specs.n; ++a) {
                     const AggSpec sp = specs.a[a];
                     if (sp.kind == AK_COUNT) continue;  // the row count
@@ -1302,7 +1314,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, i
         // the window's keys with rows: their group from the join table, one merge per key
         const uint64_t k0 = ((uint64_t)b << kSliceBits) + lo;
         for (int i = tid; i < ws; i += kSliceBlock) {
-            const uint64_t rows = lcnt[i];
+            const uint64_t rows = C16 ? (lcnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu : lcnt[i];
             if (!rows || k0 + i >= t.range) continue;
             const uint32_t ent = t.payload16 ? (uint32_t)t.payload16[k0 + i] : t.payload[k0 + i];
             if (!ent) continue;  // no build row with this key
@@ -1317,6 +1329,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_keyagg(SliceRegions rg, i
         __syncthreads();
         init();
     }
+    if (C16 && ovf) *rg.overflow = 1u;
 }
 
 // ---- fused pipeline: the plan -----------------------------------------------------------------
@@ -2900,10 +2913,13 @@ static int try_key_slices(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     const HashTable &t = src.jt;
     if (t.kind != TK_DIRECT || !t.unique) return 0;
     // windows: the fewest whose per-key states (u32 count + 8 B per value slot) fit the LDS words
-    const int64_t per_key = 4 + 8 * (int64_t)(specs.n_slots - 1);
-    const int64_t ws_max = (int64_t)kKeyAggWords * 8 / per_key / 2 * 2;
-    const int nw = (int)((kSliceKeys + ws_max - 1) / ws_max);
-    const int ws = (int)(((kSliceKeys + nw - 1) / nw + 1) / 2 * 2);
+    // (u16 counts when they save a window: QEH_KEYAGG_C16=0 keeps u32)
+    auto windows = [&](int cb) { return (int)((kSliceKeys + (int64_t)kKeyAggWords * 8 / (cb + 8 * (int64_t)(specs.n_slots - 1)) / 4 * 4 - 1) /
+                                              ((int64_t)kKeyAggWords * 8 / (cb + 8 * (int64_t)(specs.n_slots - 1)) / 4 * 4)); };
+    const bool c16 = windows(2) < windows(4) && !(std::getenv("QEH_KEYAGG_C16") && std::atoi(std::getenv("QEH_KEYAGG_C16")) == 0);
+    const int64_t per_key = (c16 ? 2 : 4) + 8 * (int64_t)(specs.n_slots - 1);
+    const int nw = windows(c16 ? 2 : 4);
+    const int ws = (int)(((kSliceKeys + nw - 1) / nw + 3) / 4 * 4);
     const int gpx = ctx->props.multiProcessorCount / 8 / nw;  // groups of nw workgroups per XCD
     if (gpx == 0 || (int64_t)ws * per_key > (int64_t)kKeyAggWords * 8) return 0;
     const int gridB = 8 * gpx * nw;
@@ -2928,12 +2944,17 @@ static int try_key_slices(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
         if ((int)F > full) tparts = std::max(1, std::min(grid, ngrp / ((int)F - full)));
         if (const char *e = std::getenv("QEH_KEYAGG_TAIL"))
             if (std::atoi(e) == 0) full = (int)F, tparts = 1;
-        if (nacol == 0)
-            hipLaunchKernelGGL(k_slice_keyagg<0>, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, specs, G,
-                               states, nw, ws, full, tparts);
-        else
-            hipLaunchKernelGGL(k_slice_keyagg<1>, dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, specs, G,
-                               states, nw, ws, full, tparts);
+#define QEH_KA(NAV, C16V)                                                                                            \
+    hipLaunchKernelGGL((k_slice_keyagg<NAV, C16V>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream, rg, grid, t, specs, G, \
+                       states, nw, ws, full, tparts)
+        if (nacol == 0) {
+            if (c16) QEH_KA(0, true);
+            else QEH_KA(0, false);
+        } else {
+            if (c16) QEH_KA(1, true);
+            else QEH_KA(1, false);
+        }
+#undef QEH_KA
     }
     const int64_t done = n_tiles * kSliceTile;
     if (done < n) {  // ragged tail: generic kernel, global states

@@ -458,6 +458,30 @@ def test_key_slices_skewed_keys_fall_back(ctx, monkeypatch):
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("c16", ["", "0"])
+def test_key_slices_count_overflow(ctx, monkeypatch, c16):
+    """One slice (a 60000-key build range), 1e6 probe rows on one key: no phase-A region overflows, but
+    the key's row count passes 65535 in one window -- the u16 counts (SUM + COUNT: 4 windows of 16384
+    keys) flag it and the query falls back; with u32 counts (QEH_KEYAGG_C16=0) the window path answers.
+    Equal to the oracle either way."""
+    monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
+    if c16:
+        monkeypatch.setenv("QEH_KEYAGG_C16", c16)
+    n, nd = 3_000_000, 60_000
+    x, k, v, dk, dg = metric_data(n, nd, 1 << 17)
+    k = k.copy()
+    k[:1_000_000] = 777
+    probe = [(x, None), (k, None), (v, None)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], AGGS)
+    ran = ctx.kernel_time("slice_keyagg")[1] > 0
+    ctx.timing(False)
+    assert ran
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
 def _host_threads():
     import os
     n = len(os.sched_getaffinity(0))

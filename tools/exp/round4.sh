@@ -376,7 +376,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r4z; mkdir -p $O
 G17="import sys; sys.argv=['x','--only','shapes']; sys.path.insert(0,'tools'); import bench_configs as b; b.cfg_metric_shapes.__defaults__ = (('g17',),); b.main()"
 for v in ${R4Z_VARS:-0 1 2 3 0}; do
-  QEH_KEYAGG_TAIL=$v timeout -k 10 300 python3 -u -c "$G17" > $O/g17.jsonl 2>$O/g17.err || { tail $O/g17.err; exit 1; }
+  QEH_KEYAGG_C16=$v timeout -k 10 300 python3 -u -c "$G17" > $O/g17.jsonl 2>$O/g17.err || { tail $O/g17.err; exit 1; }
   echo "[var $v] $(python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(round(d["ms_per_run"],2), round(d["kernel_ms"],2), round(d["frac_of_8TBs"],3), {k: round(v, 3) for k, v in d["kernel_split_ms"].items() if v})' $O/g17.jsonl)"
 done
 [ -n "$R4Z_NOPMC" ] && return 0
