@@ -306,6 +306,12 @@ int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64
 /* The same count into device memory (*dev_out, 8 B, overwritten), no host wait: the distributed step
  * reads it with its final results instead of stalling the queue between the table sum and the probe. */
 int qeh_u16_count_nonzero_dev(qeh_ctx *ctx, const uint16_t *table, uint64_t n, uint64_t *dev_out);
+/* The no-wait duplicate check of the summed table: *dev_out = entries in [1, max_entry] (8 B,
+ * overwritten), and every entry above max_entry is cleared in place, so a probe queued behind it reads
+ * such a key as a miss instead of indexing group state max_entry or beyond.  A build key held by two
+ * ranks sums to a larger entry (or to a wrong one); either way the count falls below the job's build
+ * rows and the caller discards the probe's result.  max_entry = the group slots G (1..65535). */
+int qeh_u16_table_check_dev(qeh_ctx *ctx, uint16_t *table, uint64_t n, uint32_t max_entry, uint64_t *dev_out);
 /* [min, max, non-null count] of each Int32 / Int64 column (out[3 i .. 3 i + 2]; an all-NULL or empty
  * column gives min > max), one synchronous read for all of them -- the job-wide build ranges of a
  * distributed broadcast join are gathered from these. */

@@ -20,6 +20,19 @@ struct ExprRegs {
 };
 
 // Evaluate compare on int64 payloads (ints, bools or totalOrder keys).
+// op (D_EQ..D_GE) as a truth table over the three outcomes: bit 0 = result when a < b, bit 1 when
+// a == b, bit 2 when a > b
+__host__ __device__ __forceinline__ uint32_t cmp_truth_table(int op) {
+    switch (op) {
+        case D_EQ: return 2u;
+        case D_NE: return 5u;
+        case D_LT: return 1u;
+        case D_LE: return 3u;
+        case D_GT: return 4u;
+        default: return 6u;  // D_GE
+    }
+}
+
 __device__ __forceinline__ bool cmp_i64(int op, int64_t a, int64_t b) {
     switch (op) {
         case D_EQ: return a == b;

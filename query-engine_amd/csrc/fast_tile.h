@@ -76,20 +76,36 @@ struct FastTile {
             if (base + (r >> 1) * 128 + (r & 1) < lim) m |= 1u << r;
         return m;
     }
-    // evaluate the term predicate into `sel`
+    // evaluate the term predicate into `sel`.  The comparison is branch-free: the (wave-uniform)
+    // operator becomes a 3-bit truth table over {a < b, a == b, a > b}, so a row costs two 64-bit
+    // compares and two selects instead of a scalar branch tree per row (the switch of cmp_i64 was
+    // lowered into ~20 SALU per row inside the tile loop); the Float64 order-key conversion runs only
+    // in the uniform branch of a float comparison.
+    __device__ __forceinline__ static uint32_t term_bits(const int64_t (&v)[R], int64_t lit, uint32_t tt) {
+        const uint32_t t_lt = tt & 1u, t_eq = (tt >> 1) & 1u, t_gt = tt >> 2;
+        uint32_t tr = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t b = v[r] < lit ? t_lt : (v[r] > lit ? t_gt : t_eq);
+            tr |= b << r;
+        }
+        return tr;
+    }
     __device__ __forceinline__ void eval(const FastIn &in, const PredTerms &terms) {
         sel = (1u << R) - 1u;
 #pragma unroll
         for (int i = 0; i < NTERMS; ++i) {
             const PredTerm pt = terms.t[i];
-            const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
-            uint32_t tr = 0;
+            const uint32_t tt = cmp_truth_table(pt.op);
+            int64_t v[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int64_t v = tc[i][r >> 1][r & 1];
-                if (pt.ctype == QEH_DT_FLOAT64) v = f64_order_key(fcol ? as_f64(v) : (double)v);
-                if (cmp_i64(pt.op, v, pt.lit)) tr |= 1u << r;
+            for (int r = 0; r < R; ++r) v[r] = tc[i][r >> 1][r & 1];
+            if (pt.ctype == QEH_DT_FLOAT64) {  // uniform
+                const bool fcol = in.term_dt[i] == QEH_DT_FLOAT64;
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = f64_order_key(fcol ? as_f64(v[r]) : (double)v[r]);
             }
+            const uint32_t tr = term_bits(v, pt.lit, tt);
             if (NTERMS > 1 && terms.is_or) sel = (i == 0) ? tr : (sel | tr);
             else sel &= tr;
         }

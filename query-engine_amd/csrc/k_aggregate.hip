@@ -447,6 +447,11 @@ struct __attribute__((aligned(16))) SliceChunk {
 #ifndef QEH_EARLY_PAIRS
 #define QEH_EARLY_PAIRS 2
 #endif
+// 1: tile t-1's flush after tile t's rows are ranked (and, EARLY, tile t+1's loads issued); 0: at the
+// top of the iteration, before tile t's loads are waited for (the round-4 order)
+#ifndef QEH_SLICE_FLUSH_LATE
+#define QEH_SLICE_FLUSH_LATE 1
+#endif
 #ifndef QEH_EARLY_CHUNK
 #define QEH_EARLY_CHUNK 64
 #endif
@@ -669,7 +674,7 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
     for (; tile < n_all; tile += gridDim.x) {
         uint32_t *cnt = cntb[par], *cn = cnb[par], *pos = posb[par], *lofs = lofsb[par];
         const int pq = par ^ 1;
-        if (have_prev) flush(m_prev);
+        if (!QEH_SLICE_FLUSH_LATE && have_prev) flush(m_prev);
         ft.eval(in, terms);
         uint32_t sel = ft.sel, off[R], rk[R];
         if (EARLY && tile >= n_tiles) sel &= decltype(ft)::tail_mask(tile * TILE + (int64_t)wave * (64 * R) + 2 * lane, lim);
@@ -701,6 +706,11 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
 #pragma unroll
             for (int r = 0; r < R; ++r) vcur[u][r] = VC ? ft.a(u, r) : 0;
         if (EARLY && tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
+        // tile t-1's chunks go out after this tile's loads were waited for (and the next tile's
+        // issued): flushed at the top of the iteration, the stores sat in front of the loop head's
+        // s_waitcnt vmcnt(0) -- vmcnt counts stores too, so every tile waited for its own flush's
+        // write round trip before it could evaluate its rows
+        if (QEH_SLICE_FLUSH_LATE && have_prev) flush(m_prev);
         lds_barrier();  // B1: counts complete, tile t-1 flushed
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged

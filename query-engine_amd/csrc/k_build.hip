@@ -224,25 +224,45 @@ __global__ __launch_bounds__(kBlock) void k_insert_xcd_lists(const uint64_t *__r
 }
 
 // Non-zero entries of a table of `n` words of `bytes` bytes (2 or 4), summed into *out.
-__global__ __launch_bounds__(kBlock) void k_count_nonzero(const void *__restrict__ table, uint64_t n, int bytes,
-                                                          unsigned long long *out) {
+// max_entry > 0 (u16 tables only): entries above it are not counted and are cleared in place, so a
+// probe of the table afterwards reads them as misses -- a summed table of the distributed table form
+// holds world x (G + 1) where a build key sits on two ranks, and the probe kernels index group states
+// with entry - 1 unchecked (the caller's count < rows then sends the query to the general path).
+__global__ __launch_bounds__(kBlock) void k_count_nonzero(void *__restrict__ table, uint64_t n, int bytes,
+                                                          unsigned long long *out, uint32_t max_entry = 0) {
     __shared__ uint64_t part[kBlock / 64];
     uint64_t c = 0;
     const uint64_t words = bytes == 2 ? n / 8 : n / 4;  // 16-B chunks
-    const uint4 *v = (const uint4 *)table;
+    uint4 *v = (uint4 *)table;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 q = v[i];
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        bool cleared = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (bytes == 2) c += ((w[j] & 0xFFFFu) != 0u) + ((w[j] >> 16) != 0u);
-            else c += w[j] != 0u;
+            if (bytes == 2) {
+                uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
+                if (max_entry && lo > max_entry) lo = 0, cleared = true;
+                if (max_entry && hi > max_entry) hi = 0, cleared = true;
+                c += (lo != 0u) + (hi != 0u);
+                w[j] = lo | (hi << 16);
+            } else {
+                c += w[j] != 0u;
+            }
         }
+        if (cleared) v[i] = uint4{w[0], w[1], w[2], w[3]};
     }
     if (blockIdx.x == 0) {  // ragged tail
         const uint64_t done = bytes == 2 ? words * 8 : words * 4;
-        for (uint64_t i = done + threadIdx.x; i < n; i += blockDim.x)
-            c += bytes == 2 ? ((const uint16_t *)table)[i] != 0 : ((const uint32_t *)table)[i] != 0u;
+        for (uint64_t i = done + threadIdx.x; i < n; i += blockDim.x) {
+            if (bytes == 2) {
+                uint16_t *e = (uint16_t *)table + i;
+                if (max_entry && *e > max_entry) *e = 0;
+                c += *e != 0;
+            } else {
+                c += ((const uint32_t *)table)[i] != 0u;
+            }
+        }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
@@ -427,8 +447,8 @@ extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64
     QEH_TRY(c.alloc(ctx, 8));
     QEH_HIP(hipMemsetAsync(c.p, 0, 8, ctx->stream));
     const int gc = grid_for(ctx, (int64_t)(n / 8 + 1), kBlock * 4, 1);
-    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)table, n, 2,
-                       c.as<unsigned long long>());
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)table, n, 2,
+                       c.as<unsigned long long>(), 0u);
     QEH_HIP(hipGetLastError());
     unsigned long long v = 0;
     QEH_TRY(read_small(ctx, &v, c.p, 8));
@@ -442,8 +462,21 @@ extern "C" int qeh_u16_count_nonzero_dev(qeh_ctx *ctx, const uint16_t *table, ui
     QEH_HIP(hipMemsetAsync(dev_out, 0, 8, ctx->stream));
     if (n == 0) return QEH_OK;
     const int gc = grid_for(ctx, (int64_t)(n / 8 + 1), kBlock * 4, 1);
-    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)table, n, 2,
-                       (unsigned long long *)dev_out);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)table, n, 2,
+                       (unsigned long long *)dev_out, 0u);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+extern "C" int qeh_u16_table_check_dev(qeh_ctx *ctx, uint16_t *table, uint64_t n, uint32_t max_entry, uint64_t *dev_out) {
+    if (!ctx || !dev_out || (n > 0 && !table) || max_entry == 0 || max_entry > 0xFFFFu)
+        return fail(QEH_E_INVALID, "qeh_u16_table_check_dev: bad argument");
+    DeviceGuard dg(ctx->device);
+    QEH_HIP(hipMemsetAsync(dev_out, 0, 8, ctx->stream));
+    if (n == 0) return QEH_OK;
+    const int gc = grid_for(ctx, (int64_t)(n / 8 + 1), kBlock * 4, 1);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)table, n, 2,
+                       (unsigned long long *)dev_out, max_entry);
     QEH_HIP(hipGetLastError());
     return QEH_OK;
 }
@@ -637,15 +670,15 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
                                        ctx->stream, kr, n, row_payload, t);
                 else
                     hipLaunchKernelGGL(k_insert_direct16, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
-                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)t.payload16, range, 2,
-                                   nz);
+                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)t.payload16, range, 2,
+                                   nz, 0u);
             } else {
                 QEH_TRY(out->payload.alloc(ctx, range * 4 + 16));
                 t.payload = out->payload.as<uint32_t>();
                 QEH_HIP(hipMemsetAsync(t.payload, 0, range * 4 + 16, ctx->stream));
                 hipLaunchKernelGGL(k_insert_direct, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
-                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (const void *)t.payload, range, 4,
-                                   nz);
+                hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)t.payload, range, 4,
+                                   nz, 0u);
             }
         }
         QEH_HIP(hipGetLastError());

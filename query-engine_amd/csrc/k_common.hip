@@ -439,11 +439,14 @@ __global__ __launch_bounds__(kRcBlock) void k_lds_rank_check(uint32_t *__restric
 
 // true when the device ranks stably by LDS atomics; checked once per process (first caller's device)
 bool lds_atomic_rank_ok(qeh_ctx *ctx) {
-    static int state = -1;  // -1 unknown, 0 fall back to ballot, 1 atomics are lane-ordered
+    // cached per device, and only once the check kernel has run to the end: a failed allocation,
+    // launch or sync returns false for this call and leaves the next call to retry
+    constexpr int kMaxDev = 64;
+    static int state[kMaxDev];  // 0 unknown, 1 fall back to ballot, 2 atomics are lane-ordered
     static std::mutex mu;
     std::lock_guard<std::mutex> lk(mu);
-    if (state >= 0) return state == 1;
-    state = 0;
+    const int dev = ctx->device >= 0 && ctx->device < kMaxDev ? ctx->device : 0;
+    if (state[dev]) return state[dev] == 2;
     constexpr int blocks = 64;
     DevBuf bad;
     if (bad.alloc(ctx, blocks * 4) != QEH_OK) return false;
@@ -454,8 +457,8 @@ bool lds_atomic_rank_ok(qeh_ctx *ctx) {
         return false;
     uint64_t tot = 0;
     for (int i = 0; i < blocks; ++i) tot += h[i];
-    state = tot == 0 ? 1 : 0;
-    return state == 1;
+    state[dev] = tot == 0 ? 2 : 1;
+    return state[dev] == 2;
 }
 
 }  // namespace qeh

@@ -233,9 +233,12 @@ int qeh_shutdown(qeh_ctx *ctx) {
     }
     for (auto e : ctx->event_free) hipEventDestroy(e);
     if (ctx->scratch) ctx->pool->free(ctx->scratch);
+    // a prelaunched phase A may still have its plan's copy into pinned_plan queued: wait for it (and
+    // return its buffers to the pool) before the pinned buffers go
+    ctx->pending_slice.reset();
+    if (ctx->aux_stream) hipStreamSynchronize(ctx->aux_stream);
     if (ctx->pinned_plan) hipHostFree(ctx->pinned_plan);
     if (ctx->pinned) hipHostFree(ctx->pinned);
-    ctx->pending_slice.reset();  // waits for a prelaunched phase A; its buffers go back to the pool
     ctx->source_cache.reset();  // its columns go back to the pool first
     delete ctx->pool;
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);

@@ -88,6 +88,7 @@ SIGNATURES = {
     "qeh_direct_group_table_insert_async": (I, [P, COLP, COLP, I64, U64, I64, P]),
     "qeh_u16_count_nonzero": (I, [P, P, U64, C.POINTER(I64)]),
     "qeh_u16_count_nonzero_dev": (I, [P, P, U64, P]),
+    "qeh_u16_table_check_dev": (I, [P, P, U64, C.c_uint32, P]),
     "qeh_columns_minmax": (I, [P, COLP, I, C.POINTER(I64)]),
     "qeh_dense_states_f64": (I, [P, COLP, COLP, I, I64, I64, P]),
     "qeh_dense_states_take": (I, [P, P, I, I64, I64, I, I, C.c_int32, C.POINTER(C.c_int32), COLP, COLP, C.POINTER(I64)]),

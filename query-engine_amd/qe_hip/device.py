@@ -466,6 +466,11 @@ class Context:
         """qeh_u16_count_nonzero_dev: the non-empty entries of a u16 table into device memory (8 B)."""
         abi.check(self.lib.qeh_u16_count_nonzero_dev(self.h, table_ptr, n, out_ptr))
 
+    def u16_table_check_dev(self, table_ptr: int, n: int, max_entry: int, out_ptr: int) -> None:
+        """qeh_u16_table_check_dev: entries in [1, max_entry] counted into device memory (8 B); entries
+        above max_entry cleared in place (a later probe reads them as misses)."""
+        abi.check(self.lib.qeh_u16_table_check_dev(self.h, table_ptr, n, max_entry, out_ptr))
+
     def broadcast_stats(self, build_key: DeviceColumn, group_key: DeviceColumn, extra: Sequence[int],
                         out_ptr: int) -> None:
         """qeh_broadcast_stats: [rows, key min, max, group min, max, *extra] of this dimension shard

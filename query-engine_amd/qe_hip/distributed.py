@@ -651,6 +651,8 @@ class DistributedExecutor:
         # of the rows over the whole range)
         sparsity = float(os.environ.get("QEH_TABLE_MAX_SPARSITY", "4"))
         if R > sparsity * total + 1024 or R >= (1 << 31) or G > 4096 or self.world * (G + 1) >= (1 << 16):
+            # declined: drop the cached table so later steps stop zeroing it (and its memory is freed)
+            self._table_cache = None
             return None
         if not st["prelaunched"]:
             self.ctx.join_filter_aggregate_prelaunch(probe_cols, probe_key_idx, predicate, aggs, st["krange"],
@@ -660,8 +662,9 @@ class DistributedExecutor:
             table = tc  # zeroed ahead of phase A in _build_stats
         else:
             table = torch.zeros((R + 1) // 2, dtype=torch.int32, device="cuda")  # R u16 entries (+1 pad)
-            if not os.environ.get("QEH_NO_TABLE_CACHE"):
-                self._table_cache = table
+            # cached for the next step (zeroed ahead of its phase A) up to TABLE_CACHE_MAX_BYTES
+            cache = not os.environ.get("QEH_NO_TABLE_CACHE") and R * 2 <= self.TABLE_CACHE_MAX_BYTES
+            self._table_cache = table if cache else None
         self._sync_torch()  # zeroed before the library writes
         lanes_ok = (G <= self.DENSE_MAX_KEYS and not os.environ.get("QEH_NO_TABLE_LANES")
                     and all((f == AF.Count or (f == AF.Sum and probe_cols[c].dtype == abi.DT_FLOAT64 and not probe_nullable[j]))
@@ -689,7 +692,9 @@ class DistributedExecutor:
             lanes_buf = torch.empty(nl + 1, dtype=torch.float64, device="cuda")
             lanes = lanes_buf[:nl]
             self._sync_torch()
-            self.ctx.u16_count_nonzero_dev(table.data_ptr(), R, lanes_buf[nl:].data_ptr())
+            # entries above G (a build key on two ranks sums to world x its entry) are cleared before
+            # the probe reads the table: the kernels index group states with entry - 1 unchecked
+            self.ctx.u16_table_check_dev(table.data_ptr(), R, G, lanes_buf[nl:].data_ptr())
             self.ctx.join_filter_aggregate_table_lanes_async(probe_cols, probe_key_idx, predicate, table.data_ptr(), kmin,
                                                              R, G, aggs, lanes.data_ptr(), status.data_ptr())
             self._sync()
@@ -701,9 +706,11 @@ class DistributedExecutor:
                                                    [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
             tail = lanes_buf[nl - 1:].cpu().numpy()  # [status lane, non-empty count]
             nz, bad = int(tail[1:].view(np.int64)[0]), float(tail[0]) != 0.0
+            self.last_table_redo = False
             if nz != total:
                 return None  # a build key repeats: the general path handles multi-match joins
             if bad:  # some rank's operator overflowed a slice region (or failed): redo it with the checks inline
+                self.last_table_redo = True
                 lanes = torch.empty((1 + len(aggs)) * G, dtype=torch.float64, device="cuda")
                 self._sync_torch()
                 self.ctx.join_filter_aggregate_table_lanes(probe_cols, probe_key_idx, predicate, table.data_ptr(),
@@ -778,6 +785,7 @@ class DistributedExecutor:
         return out
 
     DENSE_MAX_KEYS = 1 << 20
+    TABLE_CACHE_MAX_BYTES = 256 << 20  # the table form's u16 table kept for the next step up to this size
 
     def _final_dense(self, lo: int, hi: int, probe_nullable, pk, pa_, aggs):
         """Final aggregate of a broadcast join by all-reduce instead of a shuffle, when the single

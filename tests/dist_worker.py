@@ -438,6 +438,41 @@ def mode_gpu_devtensors(rank, world):
         wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred,
                                               ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
         assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    fact = [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)]
+    # a build key held by two ranks (rank 0 and the last rank) with SUM + COUNT: the no-wait table
+    # form sums the two entries to one above G (both group slots >= G / 2), which the table check
+    # clears before the probe reads it; the non-empty count then falls short on every rank and every
+    # rank falls back to the all-gather form (multi-match join) -- vs the oracle's join
+    lo0, hi0 = b[0], b[1]
+    lo1, hi1 = b[world - 1], b[world]
+    i0 = lo0 + int(np.nonzero(dg_all[lo0:hi0] >= 700)[0][0])
+    i1 = lo1 + int(np.nonzero(dg_all[lo1:hi1] >= 700)[0][0])
+    dk_dup = dk_all.copy()
+    dk_dup[i1] = dk_dup[i0]
+    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
+        fact, 1, pred, ctx.upload(dk_dup[b[rank]:b[rank + 1]]), [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs,
+        build_sharded=True)
+    assert dx.last_build == "allgather", dx.last_build
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        dk_, da_, _ = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred,
+                                               ob.HostCol(dk_dup), [ob.HostCol(dg_all)], aggs)
+        assert_grouped_equal(res[:1], res[1:], dk_, da_, float_aggs=[0])
+    # probe keys crowded into one 2^16-key slice: the prelaunched phase A overflows its regions on
+    # every rank, the status lane of the lanes' all-reduce tells every rank, and every rank redoes the
+    # probe with the checks inline (the synchronous lanes call) -- vs the oracle
+    ksk = (kk % 60_000).astype(np.int64)
+    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
+        [ctx.upload(x), ctx.upload(ksk), ctx.upload(vv)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+        [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
+    assert dx.last_build == "table", dx.last_build
+    assert dx.last_table_redo, "the region overflow did not reach the redo branch"
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        KSK = (KK % 60_000).astype(np.int64)
+        sk_, sa_, _ = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KSK), ob.HostCol(VV)], 1, pred,
+                                               ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
+        assert_grouped_equal(res[:1], res[1:], sk_, sa_, float_aggs=[0])
     # rank-local bitmaps: only rank 0's fact shard has NULLs in the aggregate input (every rank
     # must then skip the dense final, which cannot carry all-NULL groups), only rank 1's dim key
     # shard has a (NULL-free) bitmap (every rank must then skip the overlapped all-gather)

@@ -123,13 +123,16 @@ def test_two_ranks_on_one_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_device_tensor_collectives_several_ranks_on_one_gpu(world):
-    """The RCCL path's device-tensor code at world size 2 and 3 (collectives over gloo on CUDA
-    tensors, ranks sharing one GPU): config 4's shuffle join and the sharded broadcast join with
-    the overlapped all-gather + adopted prelaunch and the dense final aggregate, vs the oracle;
-    validity agreed across ranks; the chunked all-to-all in many rounds."""
-    launch("gpu_devtensors", world, timeout=600)
+    """The RCCL path's device-tensor code at world size 2, 3 and 8 (collectives over gloo on CUDA
+    tensors, ranks sharing one GPU; 8 = one node's ranks, so config 4's 8-way round plan and HIP legs
+    run with eight ranks): config 4's shuffle join and the sharded broadcast join with the
+    overlapped all-gather + adopted prelaunch and the dense final aggregate, vs the oracle; a build
+    key on two ranks (the table form's check clears the summed entry, every rank falls back); probe
+    keys crowded into one slice (every rank takes the overflow redo); validity agreed across ranks;
+    the chunked all-to-all in many rounds."""
+    launch("gpu_devtensors", world, timeout=900)
 
 
 @pytest.mark.gpu

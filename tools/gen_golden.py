@@ -193,8 +193,65 @@ def main():
         "schema": ["employees.name: Utf8", "employees.age: Int64"],
         "rows": [[n, a] for n, a in zip(ans["name"].to_pylist(), ans["age"].to_pylist())],
     }
+    employees_departments(manifest)
     json.dump(manifest, open(os.path.join(OUT, "manifest.json"), "w"), indent=1)
     print(json.dumps(manifest["fixtures"]["employees"]))
+
+
+# Known answers on the reference's own data/employees.csv and data/departments.csv, joined on dept_id:
+# the only reference-held input that exercises the join and group-by operators.  The rows below were
+# derived by hand from the two files (6 employees, Frank's dept_id is the literal text NULL -- read as a
+# NULL, which never matches; read as the text "NULL" by a reader that keeps it, it equals no department
+# id either, so the answer is the same; department 104 has no employee), then checked against
+# pyarrow's hash join and group_by when this script runs.
+EMP_DEPT = {
+    "inner": {
+        "query": "SELECT e.name, d.dept_name FROM employees e JOIN departments d ON e.dept_id = d.dept_id",
+        "rows": [["Alice", "Engineering"], ["Bob", "Sales"], ["Charlie", "Engineering"], ["Diana", "HR"],
+                 ["Eve", "Sales"]]},
+    "left": {
+        "query": "SELECT e.name, d.dept_name FROM employees e LEFT JOIN departments d ON e.dept_id = d.dept_id",
+        "rows": [["Alice", "Engineering"], ["Bob", "Sales"], ["Charlie", "Engineering"], ["Diana", "HR"],
+                 ["Eve", "Sales"], ["Frank", None]]},
+    "right": {
+        "query": "SELECT e.name, d.dept_name FROM employees e RIGHT JOIN departments d ON e.dept_id = d.dept_id",
+        "rows": [["Alice", "Engineering"], ["Bob", "Sales"], ["Charlie", "Engineering"], ["Diana", "HR"],
+                 ["Eve", "Sales"], [None, "Marketing"]]},
+    "full": {
+        "query": "SELECT e.name, d.dept_name FROM employees e FULL JOIN departments d ON e.dept_id = d.dept_id",
+        "rows": [["Alice", "Engineering"], ["Bob", "Sales"], ["Charlie", "Engineering"], ["Diana", "HR"],
+                 ["Eve", "Sales"], ["Frank", None], [None, "Marketing"]]},
+    "group_by_dept": {
+        "query": "SELECT dept_id, COUNT(salary), SUM(salary), AVG(salary) FROM employees GROUP BY dept_id",
+        "rows": [[101, 2, 170000, 85000.0], [102, 2, 175000, 87500.0], [103, 1, 80000, 80000.0],
+                 [None, 1, 78000, 78000.0]]},
+    "join_filter_group_by": {
+        "query": "SELECT d.dept_id, COUNT(e.salary), SUM(e.salary) FROM employees e JOIN departments d "
+                 "ON e.dept_id = d.dept_id WHERE e.age > 25 GROUP BY d.dept_id",
+        "rows": [[101, 1, 95000], [102, 2, 175000], [103, 1, 80000]]},
+}
+
+
+def employees_departments(manifest):
+    src = "/root/reference/data/departments.csv"
+    dst = os.path.join(OUT, "departments.csv")
+    if os.path.exists(src):
+        shutil.copyfile(src, dst)
+    emp = pacsv.read_csv(os.path.join(OUT, "employees.csv"))
+    dep = pacsv.read_csv(dst)
+    def rows(t, cols):
+        return sorted([list(r) for r in zip(*[t[c].to_pylist() for c in cols])], key=repr)
+    for how, name in (("inner", "inner"), ("left outer", "left"), ("right outer", "right"), ("full outer", "full")):
+        j = emp.join(dep, "dept_id", join_type=how)
+        assert rows(j, ["name", "dept_name"]) == sorted(EMP_DEPT[name]["rows"], key=repr), name
+    g = emp.group_by("dept_id").aggregate([("salary", "count"), ("salary", "sum"), ("salary", "mean")])
+    assert rows(g, ["dept_id", "salary_count", "salary_sum", "salary_mean"]) == \
+        sorted(EMP_DEPT["group_by_dept"]["rows"], key=repr)
+    j = emp.filter(pc.greater(emp["age"], 25)).join(dep, "dept_id", join_type="inner")
+    g = j.group_by("dept_id").aggregate([("salary", "count"), ("salary", "sum")])
+    assert rows(g, ["dept_id", "salary_count", "salary_sum"]) == sorted(EMP_DEPT["join_filter_group_by"]["rows"], key=repr)
+    manifest["fixtures"]["employees_departments"] = dict(EMP_DEPT, inputs=["employees.csv", "departments.csv"],
+                                                         key="dept_id")
 
 
 if __name__ == "__main__":
