@@ -361,6 +361,45 @@ int qeh_join_filter_aggregate_table_lanes_async(qeh_ctx *ctx, const qeh_column *
 int qeh_broadcast_stats(qeh_ctx *ctx, const qeh_column *build_key, const qeh_column *group_key, const int64_t *extra,
                         int n_extra, int64_t *dev_out);
 
+/* The items form of the distributed broadcast join (the BASELINE metric at N > 1; replaces the
+ * table form's all-reduced 2-B-per-key table).  Distributed HashJoinExec + HashAggregateExec
+ * (query-distributed/src/planner.rs:200-249 over query-executor/src/executor.rs:157-190, 363-381):
+ *   qeh_fused_items_begin: plans the fused pipeline from the gathered qeh_broadcast_stats rows
+ *     (stats_dev[world][row_len], device memory) and queues phase A over this rank's fact shard
+ *     (probe_cols) -- no host wait; *handle is opaque.  COUNT and non-null Float64 SUM aggregates over
+ *     at most one aggregate column, a column-literal predicate list (QEH_E_UNSUPPORTED otherwise).
+ *   qeh_fused_items_build: this rank's dimension rows (one non-null Int64 key, one non-null integer
+ *     group key) grouped by 2^16-key slice by n_blocks workgroups, each into its own span of `span` u32
+ *     (span >= ceil(rows / n_blocks) + 640, a multiple of 4; items: caller-owned device memory of
+ *     n_blocks * span u32): span w's slice b has offs[w * 322 + 161 + b] items from
+ *     items[w * span + offs[w * 322 + b]] (a multiple of 4); offs holds n_blocks * 322 u32.
+ *   (caller: all-gather items and offs over the ranks, rank-major; every rank uses the same n_blocks
+ *     and span)
+ *   qeh_fused_items_finish: phase B over the n_regions = world * n_blocks gathered spans (region r at
+ *     items + r * span, its offs at offs + r * 322; n_regions <= 512) and the dense final stage's
+ *     lanes as qeh_join_filter_aggregate_table_lanes_async writes them for group keys
+ *     group_min + [0, n_groups) ((1 + n_aggs) * n_groups + 1 doubles; the last = 1.0 when the plan
+ *     declined the shape, a key lies outside the gathered ranges, a key repeats -- on any rank -- or a
+ *     kernel failed: the caller then takes another form).  Frees the handle.
+ *   qeh_fused_items_abort: waits for the queued work and frees the handle (a rank that does not finish). */
+int qeh_fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                          const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev, int world,
+                          int row_len, void **handle);
+int qeh_fused_items_build(qeh_ctx *ctx, void *handle, const qeh_column *build_key, const qeh_column *group_key,
+                          int n_blocks, uint64_t span, uint32_t *items, uint32_t *offs);
+int qeh_fused_items_finish(qeh_ctx *ctx, void *handle, const uint32_t *items, uint64_t span, const uint32_t *offs,
+                           int n_regions, int64_t n_groups, double *lanes);
+int qeh_fused_items_abort(qeh_ctx *ctx, void *handle);
+/* qeh_dense_states_take that also returns the status lane after the (1 + n_vals) * range lanes (the
+ * no-wait forms' flag) in *status, from the same host read as the group count. */
+int qeh_dense_states_take_status(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range,
+                                 int world, int rank, int32_t key_dtype, const int32_t *out_dtypes,
+                                 qeh_column *out_keys, qeh_column *out_vals, int64_t *out_groups, double *status);
+/* qeh_fused_items_begin's shape checks only (QEH_OK or QEH_E_UNSUPPORTED; nothing queued): the flag
+ * every rank contributes to the gathered stats before any rank's choice of collectives depends on it. */
+int qeh_fused_items_check(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                          const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs);
+
 /* Stable lexicographic sort -> permutation (UINT32 row ids) of the input.
  * Intended semantics of `Sort` (physical_plan.rs:40-44; executor.rs:290-297
  * is the identity): per-key ascending flag, NULLs first, floats totalOrder. */

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <type_traits>
 
 #include "agg.h"
@@ -417,6 +418,14 @@ struct DimSlices {
     const uint32_t *count;
     uint32_t *dup;     // set when two build rows share a key
     const FusedPlan *plan;
+    // the items form of the distributed broadcast join: the build rows come grouped by slice from the
+    // ranks instead of from phase A's prologue -- nreg > 0 regions (every rank's build spans), region r's
+    // items at items + r * rstride, with o = offs + r * 2 * (kSliceMaxF + 1): slice b's o[S + 1 + b] items
+    // at o[b] (a multiple of 4)
+    int32_t nreg;
+    int32_t _pad;
+    uint64_t rstride;
+    const uint32_t *offs;
 };
 
 // One whole chunk of phase A's flush, planned by the slice's owner thread while the tile is staged:
@@ -514,12 +523,35 @@ __device__ __attribute__((noinline)) void fused_prologue(const FusedPro &fp, int
         }
     }
     __syncthreads();
-    for (int i = tid; i < F; i += NTH) {
-        fp.dcount[(uint64_t)blockIdx.x * F + i] = dcnt[i] < fpl.dcap ? dcnt[i] : (uint32_t)fpl.dcap;
-        dovf |= dcnt[i] > fpl.dcap;
-    }
+    if (fp.dcount)  // (the items form: no build rows here)
+        for (int i = tid; i < F; i += NTH) {
+            fp.dcount[(uint64_t)blockIdx.x * F + i] = dcnt[i] < fpl.dcap ? dcnt[i] : (uint32_t)fpl.dcap;
+            dovf |= dcnt[i] > fpl.dcap;
+        }
     if (dovf) fp.status[1] = 1u;
 }
+
+// Diagnostic build only (-DQEH_PA_STAMPS=1; the default build has no stamp): every wave of the fused
+// phase A accumulates the shader-clock cycles of each phase of its tile loop and writes them, with
+// its tile count and the s_memtime / s_memrealtime bounds of the loop, to qeh_pa_stamps (plain vector
+// stores from lane 0), which qeh_debug_pa_stamps copies out.
+#ifndef QEH_PA_STAMPS
+#define QEH_PA_STAMPS 0
+#endif
+#if QEH_PA_STAMPS
+constexpr int kPaStampWords = 16;
+__device__ uint64_t qeh_pa_stamps[kMaxSliceGrid * 16 * kPaStampWords];
+#define PA_STAMP(i)                                          \
+    do {                                                     \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+        pa_acc[i] += t_ - pa_prev;                           \
+        pa_prev = t_;                                        \
+    } while (0)
+#else
+#define PA_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
 
 // EARLY: the next tile's loads are issued right after this tile's rows are ranked (its registers are
 // free from then on), so they stay in flight across the scan, staging and flush phases; it takes every
@@ -671,10 +703,20 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
         fused_prologue<NTH>(fp, F, kmin, dcnt);
     }
     if (tile < n_all) issue_tile(tile);
+#if QEH_PA_STAMPS
+    uint64_t pa_acc[10] = {};
+    const uint64_t pa_t0 = __builtin_amdgcn_s_memtime(), pa_r0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t pa_prev = pa_t0;
+#endif
     for (; tile < n_all; tile += gridDim.x) {
         uint32_t *cnt = cntb[par], *cn = cnb[par], *pos = posb[par], *lofs = lofsb[par];
         const int pq = par ^ 1;
         if (!QEH_SLICE_FLUSH_LATE && have_prev) flush(m_prev);
+#if QEH_PA_STAMPS
+        PA_STAMP(9);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's loads (and older stores)
+        PA_STAMP(0);
+#endif
         ft.eval(in, terms);
         uint32_t sel = ft.sel, off[R], rk[R];
         if (EARLY && tile >= n_tiles) sel &= decltype(ft)::tail_mask(tile * TILE + (int64_t)wave * (64 * R) + 2 * lane, lim);
@@ -705,13 +747,16 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
         for (int u = 0; u < VS; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) vcur[u][r] = VC ? ft.a(u, r) : 0;
+        PA_STAMP(1);
         if (EARLY && tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
         // tile t-1's chunks go out after this tile's loads were waited for (and the next tile's
         // issued): flushed at the top of the iteration, the stores sat in front of the loop head's
         // s_waitcnt vmcnt(0) -- vmcnt counts stores too, so every tile waited for its own flush's
         // write round trip before it could evaluate its rows
         if (QEH_SLICE_FLUSH_LATE && have_prev) flush(m_prev);
+        PA_STAMP(2);
         lds_barrier();  // B1: counts complete, tile t-1 flushed
+        PA_STAMP(3);
         if (wave == 0) {
             // three consecutive slices per lane: exclusive scans of the staged
             // counts (tile offsets) and of the whole chunks each slice flushes
@@ -742,7 +787,9 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
         } else if (have_prev) {
             carry(cnb[pq], cntb[pq], lofsb[pq], tid - 64, NTH - 64);
         }
+        PA_STAMP(4);
         lds_barrier();  // B2: offsets ready, carries hold everything before tile t
+        PA_STAMP(5);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!((sel >> r) & 1)) continue;
@@ -775,11 +822,24 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
             cntb[pq][tid] = 0;
         }
         if (!EARLY && tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
+        PA_STAMP(6);
         lds_barrier();  // B3: staged, chunks planned
+        PA_STAMP(7);
         m_prev = s_chunks;
         have_prev = true;
         par = pq;
+#if QEH_PA_STAMPS
+        pa_acc[8] += 1;
+#endif
     }
+#if QEH_PA_STAMPS
+    if (EARLY && lane == 0) {
+        uint64_t *o = qeh_pa_stamps + ((uint64_t)blockIdx.x * (NTH / 64) + wave) * kPaStampWords;
+        for (int i = 0; i < 10; ++i) o[i] = pa_acc[i];
+        o[10] = __builtin_amdgcn_s_memtime() - pa_t0;
+        o[11] = __builtin_amdgcn_s_memrealtime() - pa_r0;
+    }
+#endif
     if (have_prev) {
         flush(m_prev);
         lds_barrier();
@@ -1012,6 +1072,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     __shared__ __attribute__((aligned(16))) uint16_t tslice[IDENT ? 8 : kSliceKeys];
     __shared__ uint64_t lst[IDENT ? kGidStateWords : kSliceStateWords];
     __shared__ uint32_t rcnt[DIM ? kMaxSliceGrid : 1];  // DIM: the build-row counts of the slice's regions
+    __shared__ uint32_t rbase[DIM ? kMaxSliceGrid : 1];  // DIM: where they start (items, < 2^32)
     uint32_t *lcnt = (uint32_t *)lst;
     uint64_t dcap = 0;
     if constexpr (DIM) {
@@ -1058,18 +1119,29 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             cur_b = b;
             uint32_t *tw = (uint32_t *)tslice;
             for (int i = tid; i < kSliceKeys / 2; i += kSliceBlock) tw[i] = 0u;
-            for (int r = tid; r < nreg; r += kSliceBlock) rcnt[r] = dim.count[(uint64_t)r * F + b];
+            // build-row regions of the slice: one per phase-A workgroup, or (items form) one per rank
+            const int dn = dim.nreg ? dim.nreg : nreg;
+            for (int r = tid; r < dn; r += kSliceBlock) {
+                if (dim.nreg) {
+                    const uint32_t *o = dim.offs + (uint64_t)r * 2 * (kSliceMaxF + 1);
+                    rcnt[r] = o[kSliceMaxF + 1 + b];
+                    rbase[r] = (uint32_t)((uint64_t)r * dim.rstride + o[b]);
+                } else {
+                    rcnt[r] = dim.count[(uint64_t)r * F + b];
+                    rbase[r] = (uint32_t)(((uint64_t)r * F + b) * dcap);
+                }
+            }
             __syncthreads();
             // slice b's build rows: every wave takes 8 regions at a time, lane j their items 4j..4j+3
             uint32_t dup = 0;
-            for (int r0 = wave * 8; r0 < nreg; r0 += W * 8) {
+            for (int r0 = wave * 8; r0 < dn; r0 += W * 8) {
                 v4u32 w[8];
                 uint32_t cq[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int r = r0 + q;
-                    cq[q] = r < nreg ? rcnt[r] : 0u;
-                    w[q] = (uint32_t)lane * 4 < cq[q] ? *(const v4u32 *)(dim.items + ((uint64_t)r * F + b) * dcap + lane * 4)
+                    cq[q] = r < dn ? rcnt[r] : 0u;
+                    w[q] = (uint32_t)lane * 4 < cq[q] ? *(const v4u32 *)(dim.items + (uint64_t)rbase[r] + lane * 4)
                                                       : v4u32{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
@@ -1085,9 +1157,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int r = r0 + q;
-                    const uint32_t c = r < nreg ? rcnt[r] : 0u;
+                    const uint32_t c = r < dn ? rcnt[r] : 0u;
                     for (uint32_t i = 256 + (uint32_t)lane * 4; i < c; i += 256) {
-                        const v4u32 x = *(const v4u32 *)(dim.items + ((uint64_t)r * F + b) * dcap + i);
+                        const v4u32 x = *(const v4u32 *)(dim.items + (uint64_t)rbase[r] + i);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             if (i + e >= c) break;
@@ -1946,11 +2018,15 @@ __global__ __launch_bounds__(256) void k_states_fold(uint64_t *__restrict__ stat
 // in flight
 // status (the no-wait form): lanes[(1 + n) * G] = 1 when the operator's error or overflow word is set,
 // so the caller's all-reduce of the lanes carries every rank's flag.
+// fused: the fused pipeline's status words -- a duplicate build key (status[4]) or a declined plan
+// (!status[5]) also set the status lane.
 __global__ __launch_bounds__(256) void k_states_lanes(const uint64_t *__restrict__ states, int64_t Gs, int64_t G,
                                                       AggSpecs specs, double *__restrict__ lanes,
-                                                      const uint32_t *__restrict__ status) {
+                                                      const uint32_t *__restrict__ status, int fused = 0) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e == 0 && status) lanes[(int64_t)(1 + specs.n) * G] = (status[0] | status[1]) ? 1.0 : 0.0;
+    if (e == 0 && status)
+        lanes[(int64_t)(1 + specs.n) * G] =
+            (status[0] | status[1] | (fused ? (status[4] | (status[5] ? 0u : 1u)) : 0u)) ? 1.0 : 0.0;
     if (e >= (int64_t)(1 + specs.n) * G) return;
     const int j = (int)(e / G) - 1;  // -1: the row-count lane
     const int64_t g = e % G;
@@ -3801,7 +3877,7 @@ __global__ void k_dense_scatter(ColRef key, int64_t n, DenseCols dc, int64_t kmi
 // one workgroup: the owned slots o = rank + world * q with presence > 0, in key order
 __global__ __launch_bounds__(1024) void k_dense_take(const double *__restrict__ in, int64_t kmin, int64_t range, int world,
                                                      int rank, int32_t key_dt, void *__restrict__ okeys, DenseCols oc,
-                                                     int64_t *__restrict__ total) {
+                                                     int64_t *__restrict__ total, int with_status = 0) {
     __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int64_t owned = range > rank ? (range - rank + world - 1) / world : 0;
@@ -3829,7 +3905,11 @@ __global__ __launch_bounds__(1024) void k_dense_take(const double *__restrict__ 
         }
         ++base;
     }
-    if (t == 0) *total = all;
+    if (t == 0) {
+        total[0] = all;
+        // the status lane after the (1 + n) * range lanes (the no-wait forms), in the same read
+        if (with_status) total[1] = __builtin_bit_cast(int64_t, in[(int64_t)(1 + oc.n) * range]);
+    }
 }
 
 extern "C" int qeh_dense_states_f64(qeh_ctx *ctx, const qeh_column *keys, const qeh_column *vals, int n_vals,
@@ -3859,9 +3939,9 @@ extern "C" int qeh_dense_states_f64(qeh_ctx *ctx, const qeh_column *keys, const 
     return QEH_OK;
 }
 
-extern "C" int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range, int world,
-                                     int rank, int32_t key_dtype, const int32_t *out_dtypes, qeh_column *out_keys,
-                                     qeh_column *out_vals, int64_t *out_groups) {
+static int dense_states_take(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range, int world,
+                             int rank, int32_t key_dtype, const int32_t *out_dtypes, qeh_column *out_keys,
+                             qeh_column *out_vals, int64_t *out_groups, double *status) {
     if (!ctx || !in || !out_keys || !out_groups || n_vals < 0 || n_vals > kMaxAggs || (n_vals > 0 && (!out_vals || !out_dtypes)) ||
         range <= 0 || world < 1 || rank < 0 || rank >= world || (key_dtype != QEH_DT_INT64 && key_dtype != QEH_DT_INT32))
         return fail(QEH_E_INVALID, "qeh_dense_states_take: bad argument");
@@ -3881,12 +3961,15 @@ extern "C" int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals,
         oc.dt[made] = out_dtypes[made];
     }
     DevBuf tot;
-    if (s == QEH_OK) s = tot.alloc(ctx, 8);
-    int64_t g = 0;
+    if (s == QEH_OK) s = tot.alloc(ctx, 16);
+    int64_t g = 0, gs[2] = {0, 0};
     if (s == QEH_OK) {
         hipLaunchKernelGGL(k_dense_take, dim3(1), dim3(1024), 0, ctx->stream, in, key_min, range, world, rank, key_dtype,
-                           out_keys->values, oc, tot.as<int64_t>());
-        s = hipGetLastError() == hipSuccess ? read_small(ctx, &g, tot.p, 8) : fail(QEH_E_HIP, "dense take launch failed");
+                           out_keys->values, oc, tot.as<int64_t>(), status ? 1 : 0);
+        s = hipGetLastError() == hipSuccess ? read_small(ctx, gs, tot.p, status ? 16 : 8)
+                                            : fail(QEH_E_HIP, "dense take launch failed");
+        g = gs[0];
+        if (status) *status = __builtin_bit_cast(double, gs[1]);
     }
     if (s != QEH_OK) {
         qeh_column_release(ctx, out_keys);
@@ -3897,6 +3980,22 @@ extern "C" int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals,
     for (int j = 0; j < n_vals; ++j) out_vals[j].length = g;
     *out_groups = g;
     return QEH_OK;
+}
+
+extern "C" int qeh_dense_states_take(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range, int world,
+                                     int rank, int32_t key_dtype, const int32_t *out_dtypes, qeh_column *out_keys,
+                                     qeh_column *out_vals, int64_t *out_groups) {
+    return dense_states_take(ctx, in, n_vals, key_min, range, world, rank, key_dtype, out_dtypes, out_keys, out_vals,
+                             out_groups, nullptr);
+}
+
+extern "C" int qeh_dense_states_take_status(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range,
+                                            int world, int rank, int32_t key_dtype, const int32_t *out_dtypes,
+                                            qeh_column *out_keys, qeh_column *out_vals, int64_t *out_groups,
+                                            double *status) {
+    if (!status) return fail(QEH_E_INVALID, "qeh_dense_states_take_status: bad argument");
+    return dense_states_take(ctx, in, n_vals, key_min, range, world, rank, key_dtype, out_dtypes, out_keys, out_vals,
+                             out_groups, status);
 }
 
 __global__ void k_seq_i64(int64_t *p, int64_t n, int64_t base, int as32) {
@@ -4131,6 +4230,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     pi.alloc_items = tiles_per_wg * grid * (uint64_t)tile_rows * 5 / 4 + (uint64_t)grid * kSliceMaxF * (256 + 2 * chunk);
     // build rows: uniform keys over the slices, +25 %, and per-region slack
     const uint64_t dim_items = (uint64_t)nd * 5 / 4 + (uint64_t)grid * kSliceMaxF * 64;
+    if (dim_items >= (1ull << 32)) return kFusedNotEligible;  // phase B's region bases are 32-bit
     const uint64_t nreg_max = (uint64_t)grid * kSliceMaxF;
     QEH_TRY(mm.alloc(ctx, sizeof(MinMax) * 2 * (size_t)minmax_partials_max_blocks(ctx) + 16));  // the partials
     QEH_TRY(plan.alloc(ctx, sizeof(FusedPlan)));
@@ -4277,6 +4377,304 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     return QEH_OK;
 }
 
+// ---- the items form of the distributed broadcast join (BASELINE metric at N > 1) ---------------
+// The fused pipeline with the build side sharded over the ranks: every rank groups ITS dimension rows by
+// slice into 4-B items (key offset << 16 | group slot + 1) -- what phase A's prologue does with the
+// whole dimension at N = 1 -- the caller all-gathers the item regions (4 B per dimension row over the
+// wire, one region per rank and slice), and phase B builds each slice's LDS entries from the regions of
+// every rank.  Phase A needs only the job-wide key range, which the plan takes from the gathered stats
+// rows on the device (qeh_broadcast_stats), so it is launched before the host has read them:
+//   qeh_fused_items_begin  plan + states + phase A (the EARLY kernel, no build rows in its prologue)
+//   qeh_fused_items_build  this rank's build rows grouped by slice into caller buffers
+//   (caller: all-gather of the items and counts)
+//   qeh_fused_items_finish phase B over the gathered regions, then the dense final stage's lanes
+// It replaces the table form's 2-B-per-key table insert, its all-reduce and the table's HBM reads in
+// phase B; phase A is the fused pipeline's kernel (its loads issued a tile ahead) instead of the
+// prelaunched kernel that keeps room for a build beside it.  A duplicate key (on any rank), a region
+// overflow or a declined plan shows in the status lane of the lanes (every rank sees every rank's).
+
+// The fused plan from the gathered stats rows ([rows, key min, max, group key min, max, has-bitmap,
+// ...] per rank); states initialised, status words zeroed ([5] = the plan's verdict).
+__global__ __launch_bounds__(1024) void k_fused_plan_stats(const int64_t *__restrict__ M, int world, int row_len,
+                                                           SlicePlanIn pi, int64_t g_cap, FusedPlan *out,
+                                                           uint32_t *__restrict__ st, uint64_t *__restrict__ states,
+                                                           int64_t G, AggSpecs specs) {
+    const int64_t words = (int64_t)specs.shards * specs.n_slots * G;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t slot = (i / G) % specs.n_slots;
+        uint64_t v = 0;
+        for (int a = 0; a < specs.n; ++a)
+            if (specs.a[a].val_slot == slot) v = (uint64_t)agg_init_value(specs.a[a].kind);
+        states[i] = v;
+    }
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int64_t tot = 0, kmn = INT64_MAX, kmx = INT64_MIN, gmn = INT64_MAX, gmx = INT64_MIN, bitmap = 0;
+    for (int r = 0; r < world; ++r) {
+        const int64_t *m = M + (int64_t)r * row_len;
+        bitmap |= m[5];
+        if (m[0] <= 0) continue;
+        tot += m[0];
+        kmn = m[1] < kmn ? m[1] : kmn, kmx = m[2] > kmx ? m[2] : kmx;
+        gmn = m[3] < gmn ? m[3] : gmn, gmx = m[4] > gmx ? m[4] : gmx;
+    }
+    FusedPlan p{};
+    p.sp = plan_slices(pi, kmn, kmx, tot, gmn, gmx, tot);
+    const bool live = !bitmap && tot > 0 && kmn <= kmx && gmn <= gmx;
+    p.gmin = gmn;
+    p.ngroups = live ? (int64_t)((uint64_t)gmx - (uint64_t)gmn + 1ull) : 0;
+    p.dcap = 0;  // the build regions' capacity comes with the gathered items
+    p.sp.ok = p.sp.ok && live && p.ngroups >= 1 && p.ngroups <= g_cap && p.ngroups < 0xFFFF;
+    *out = p;
+    for (int i = 0; i < 8; ++i) st[i] = 0u;
+    st[5] = p.sp.ok ? 1u : 0u;
+}
+
+// This rank's build rows grouped by slice, no global atomics (reserving ranges in one count word per
+// slice from every workgroup serialised on those words) and no compaction: workgroup w takes rows
+// [w * per, (w + 1) * per) (per = ceil(rows / gridDim.x)), counts them per slice in LDS, and writes them
+// slice-major into its own span items[w * span ..], each slice's run starting at a multiple of 4 (phase
+// B's 16-B loads) -- item = (key - kmin) mod 2^16 << 16 | (group key - gmin) + 1 -- with
+// offs[w * 2 (S + 1) + b] = run start and offs[w * 2 (S + 1) + S + 1 + b] = run rows.  span >= per + 4 S.
+// A key or group key outside the plan's ranges sets st[1] (the caller falls back).
+__device__ __forceinline__ uint32_t dim_item(const FusedPlan &pl, int64_t k, int64_t g, uint32_t &it) {
+    const uint64_t o = (uint64_t)k - (uint64_t)pl.sp.kmin;
+    const uint64_t gs = (uint64_t)g - (uint64_t)pl.gmin;
+    if (o >= pl.sp.range || gs >= (uint64_t)pl.ngroups) return 0xFFFFFFFFu;
+    it = ((uint32_t)(o & (kSliceKeys - 1)) << 16) | ((uint32_t)gs + 1u);
+    return (uint32_t)(o >> kSliceBits);
+}
+__global__ __launch_bounds__(1024) void k_dim_items(const int64_t *__restrict__ dk, ColRef dg, int64_t nd, uint64_t span,
+                                                    const FusedPlan *__restrict__ plan, uint32_t *__restrict__ items,
+                                                    uint32_t *__restrict__ offs, uint32_t *__restrict__ st) {
+    constexpr int DR = 8, S = kSliceMaxF;
+    __shared__ uint32_t lc[S], ls[S];
+    const int tid = threadIdx.x;
+    const FusedPlan pl = *plan;
+    for (int i = tid; i < S; i += 1024) lc[i] = 0u;
+    __syncthreads();
+    const int64_t per = (nd + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = lo + per < nd ? lo + per : nd;
+    bool bad = false;
+    auto pass = [&](bool place) {
+        for (int64_t c0 = lo; c0 < hi; c0 += 1024 * DR) {
+            int64_t kk[DR], gg[DR];
+#pragma unroll
+            for (int q = 0; q < DR; ++q) {
+                const int64_t i = c0 + (int64_t)q * 1024 + tid;
+                kk[q] = i < hi ? dk[i] : 0;
+                gg[q] = i < hi ? load_i64(dg, i) : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < DR; ++q) {
+                if (c0 + (int64_t)q * 1024 + tid >= hi) continue;
+                uint32_t it;
+                const uint32_t b = dim_item(pl, kk[q], gg[q], it);
+                if (b == 0xFFFFFFFFu) bad = true;
+                else if (place) items[(uint64_t)blockIdx.x * span + atomicAdd(&ls[b], 1u)] = it;
+                else atomicAdd(&lc[b], 1u);
+            }
+        }
+    };
+    if (pl.sp.ok) pass(false);  // slice counts
+    __syncthreads();
+    uint32_t *o = offs + (uint64_t)blockIdx.x * 2 * (S + 1);
+    if (tid < 64) {  // run starts: exclusive scan of the counts padded to multiples of 4 (3 slices a lane)
+        const int lane = tid;
+        uint32_t c3[3], t = 0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int b = lane * 3 + q;
+            c3[q] = b < S ? (lc[b] + 3u) & ~3u : 0u;
+            t += c3[q];
+        }
+        uint32_t incl = t;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t a = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += a;
+        }
+        uint32_t run = incl - t;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int b = lane * 3 + q;
+            if (b < S) ls[b] = run;
+            run += c3[q];
+        }
+        if (lane == 63) o[S] = incl;
+    }
+    __syncthreads();
+    for (int b = tid; b < S; b += 1024) o[b] = ls[b], o[S + 1 + b] = lc[b];
+    __syncthreads();
+    if (pl.sp.ok) pass(true);  // the same rows again (L2), placed
+    if (bad) st[1] = 1u;
+}
+
+struct FusedItems {
+    DevBuf plan, kbuf, vbuf, cbuf, states, errw;
+    SliceRegions rg{};
+    FastIn in{};
+    AggSpecs specs{};
+    int nacol = 0, grid = 0;
+    int64_t Gs = 0;
+};
+
+// begin's checks (check_only: nothing allocated or launched -- the caller's agreement flag)
+static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                             const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev,
+                             int world, int row_len, void **handle, bool check_only) {
+    if (!ctx || (!check_only && (!handle || !stats_dev || world < 1 || row_len < 6)) || n_aggs < 1 || n_probe_cols < 1 ||
+        probe_key_idx < 0 || probe_key_idx >= n_probe_cols)
+        return fail(QEH_E_INVALID, "qeh_fused_items_begin: bad argument");
+    if (handle) *handle = nullptr;
+    DeviceGuard dg(ctx->device);
+    const int64_t n = probe_cols[0].length;
+    for (int i = 0; i < n_probe_cols; ++i)
+        if (probe_cols[i].length != n) return fail(QEH_E_INVALID, "probe columns have different lengths");
+    ColSet cols;
+    QEH_TRY(make_colset(probe_cols, n_probe_cols, &cols));
+    std::vector<int32_t> dts(n_probe_cols);
+    std::vector<int> idx(n_probe_cols);
+    for (int i = 0; i < n_probe_cols; ++i) dts[i] = probe_cols[i].dtype, idx[i] = i;
+    PredPlan pp;
+    QEH_TRY(plan_predicate(predicate, dts.data(), n_probe_cols, &pp));
+    auto fi = std::make_unique<FusedItems>();
+    QEH_TRY(plan_aggs(aggs, n_aggs, probe_cols, n_probe_cols, idx.data(), &fi->specs));
+    for (int a = 0; a < fi->specs.n; ++a)
+        if (!((fi->specs.a[a].kind == AK_SUM_F && fi->specs.a[a].func == QEH_AGG_SUM && fi->specs.a[a].cnt_slot == 0) ||
+              (fi->specs.a[a].kind == AK_COUNT && fi->specs.a[a].func == QEH_AGG_COUNT)))
+            return fail(QEH_E_UNSUPPORTED, "qeh_fused_items_begin: COUNT and non-null float SUM aggregates only");
+    int nterms = 0;
+    if (!fast_cols_eligible(cols, pp, probe_key_idx, fi->specs, &fi->in, &nterms, &fi->nacol) || fi->nacol > 1)
+        return fail(QEH_E_UNSUPPORTED, "qeh_fused_items_begin: probe columns outside the fused pipeline's shapes");
+    if (check_only) return QEH_OK;
+    const int64_t tile_rows = fi->nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE;
+    const int chunk = fi->nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH;
+    const int64_t n_tiles = n / tile_rows, tail = n - n_tiles * tile_rows, n_all = n_tiles + (tail ? 1 : 0);
+    AggSpecs &specs = fi->specs;
+    specs.shards = 1;
+    fi->Gs = std::min<int64_t>(kSliceStateWords / std::max(specs.n_slots, 1), 0xFFFE);
+    fi->grid = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all,
+                                                            (int64_t)kMaxSliceGrid}));
+    const uint64_t tiles_per_wg = (uint64_t)((n_all + fi->grid - 1) / fi->grid);
+    SlicePlanIn pi{};
+    pi.min_bytes = 6ull << 20;
+    if (const char *e = std::getenv("QEH_SLICE_MIN_BYTES")) pi.min_bytes = std::strtoull(e, nullptr, 10);
+    pi.grid = fi->grid;
+    pi.n_slots = specs.n_slots;
+    pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
+    pi.chunk = chunk;
+    pi.alloc_items = tiles_per_wg * fi->grid * (uint64_t)tile_rows * 5 / 4 + (uint64_t)fi->grid * kSliceMaxF * (256 + 2 * chunk);
+    const uint64_t nreg_max = (uint64_t)fi->grid * kSliceMaxF;
+    QEH_TRY(fi->plan.alloc(ctx, sizeof(FusedPlan)));
+    QEH_TRY(fi->kbuf.alloc(ctx, pi.alloc_items * 2 + 64));
+    if (fi->nacol) QEH_TRY(fi->vbuf.alloc(ctx, pi.alloc_items * 8 + 64));
+    QEH_TRY(fi->cbuf.alloc(ctx, nreg_max * 4 + 64));
+    QEH_TRY(fi->states.alloc(ctx, (size_t)specs.n_slots * fi->Gs * 8));
+    QEH_TRY(fi->errw.alloc(ctx, 32));
+    uint32_t *st = fi->errw.as<uint32_t>();
+    fi->rg.key = fi->kbuf.as<uint16_t>();
+    fi->rg.val = fi->nacol ? fi->vbuf.as<int64_t>() : nullptr;
+    fi->rg.count = fi->cbuf.as<uint32_t>();
+    fi->rg.overflow = st + 1;
+    FusedPlan *dplan = fi->plan.as<FusedPlan>();
+    {
+        KernelTimer kt(ctx, "fused_build");
+        const int gp = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->props.multiProcessorCount,
+                                                                   (specs.n_slots * fi->Gs + 4095) / 4096));
+        hipLaunchKernelGGL(k_fused_plan_stats, dim3(gp), dim3(1024), 0, ctx->stream, stats_dev, world, row_len, pi, fi->Gs,
+                           dplan, st, fi->states.as<uint64_t>(), fi->Gs, specs);
+    }
+    QEH_HIP(hipGetLastError());
+    FusedPro fp{};  // no build rows in the prologue: they arrive gathered by slice
+    fp.status = st;
+    fp.plan = dplan;
+    if (n_tiles > 0 || tail > 0)
+        launch_slice_partition_early(ctx, fi->in, pp, nterms, fi->nacol, n_tiles, tail, fi->grid, fi->rg, &dplan->sp, fp,
+                                     false, false);
+    QEH_HIP(hipGetLastError());
+    *handle = fi.release();
+    return QEH_OK;
+}
+
+extern "C" int qeh_fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                                     const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev,
+                                     int world, int row_len, void **handle) {
+    return fused_items_begin(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs, stats_dev, world, row_len,
+                             handle, false);
+}
+
+extern "C" int qeh_fused_items_check(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                                     const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs) {
+    return fused_items_begin(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs, nullptr, 0, 0, nullptr,
+                             true);
+}
+
+extern "C" int qeh_fused_items_build(qeh_ctx *ctx, void *handle, const qeh_column *build_key, const qeh_column *group_key,
+                                     int n_blocks, uint64_t span, uint32_t *items, uint32_t *offs) {
+    if (!ctx || !handle || !build_key || !group_key || !offs || !items || n_blocks < 1 || n_blocks > kMaxSliceGrid ||
+        (span & 3))
+        return fail(QEH_E_INVALID, "qeh_fused_items_build: bad argument (1..512 blocks, span a multiple of 4)");
+    FusedItems *fi = (FusedItems *)handle;
+    DeviceGuard dg(ctx->device);
+    if (build_key->dtype != QEH_DT_INT64 || (build_key->validity && build_key->null_count != 0) ||
+        (group_key->dtype != QEH_DT_INT64 && group_key->dtype != QEH_DT_INT32) ||
+        (group_key->validity && group_key->null_count != 0) || group_key->length != build_key->length)
+        return fail(QEH_E_UNSUPPORTED, "qeh_fused_items_build: one non-null Int64 key and one non-null integer group key");
+    const int64_t nd = build_key->length;
+    if ((uint64_t)((nd + n_blocks - 1) / n_blocks) + 4ull * kSliceMaxF > span)
+        return fail(QEH_E_INVALID, "qeh_fused_items_build: span below ceil(rows / n_blocks) + 640");
+    KernelTimer kt(ctx, "fused_build");
+    hipLaunchKernelGGL(k_dim_items, dim3(n_blocks), dim3(1024), 0, ctx->stream,
+                       (const int64_t *)build_key->values + build_key->offset, make_colref(*group_key), nd, span,
+                       fi->plan.as<FusedPlan>(), items, offs, fi->errw.as<uint32_t>());
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+extern "C" int qeh_fused_items_finish(qeh_ctx *ctx, void *handle, const uint32_t *items, uint64_t span,
+                                      const uint32_t *offs, int n_regions, int64_t n_groups, double *lanes) {
+    const int world = n_regions;
+    if (!ctx || !handle || !offs || !lanes || world < 1 || world > kMaxSliceGrid || n_groups < 1 || (span & 3) ||
+        (uint64_t)world * span >= (1ull << 32))
+        return fail(QEH_E_INVALID, "qeh_fused_items_finish: bad argument");
+    std::unique_ptr<FusedItems> fi((FusedItems *)handle);  // freed here: its buffers' users are queued ahead
+    DeviceGuard dg(ctx->device);
+    if (n_groups > fi->Gs) return fail(QEH_E_UNSUPPORTED, "qeh_fused_items_finish: more groups than the states hold");
+    uint32_t *st = fi->errw.as<uint32_t>();
+    {
+        KernelTimer ktb(ctx, "slice_probe");
+        DimSlices dim{items, nullptr, st + 4, fi->plan.as<FusedPlan>(), world, 0, span, offs};
+        const int gridB = ctx->props.multiProcessorCount;
+        const HashTable t{};
+        const bool pf = slice_probe_prefetch();
+        if (fi->nacol == 0) {
+            if (pf) hipLaunchKernelGGL((k_slice_probe<0, false, true, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                       fi->rg, fi->grid, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+            else hipLaunchKernelGGL((k_slice_probe<0, false, false, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                    fi->rg, fi->grid, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+        } else {
+            if (pf) hipLaunchKernelGGL((k_slice_probe<1, false, true, true, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                       fi->rg, fi->grid, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+            else hipLaunchKernelGGL((k_slice_probe<1, false, false, true, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                    fi->rg, fi->grid, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+        }
+    }
+    QEH_HIP(hipGetLastError());
+    const int64_t ne = (int64_t)(1 + fi->specs.n) * n_groups;
+    hipLaunchKernelGGL(k_states_lanes, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, ctx->stream,
+                       (const uint64_t *)fi->states.as<uint64_t>(), fi->Gs, n_groups, fi->specs, lanes, (const uint32_t *)st, 1);
+    QEH_HIP(hipGetLastError());
+    return QEH_OK;
+}
+
+extern "C" int qeh_fused_items_abort(qeh_ctx *ctx, void *handle) {
+    if (!ctx || !handle) return QEH_OK;
+    DeviceGuard dg(ctx->device);
+    std::unique_ptr<FusedItems> fi((FusedItems *)handle);
+    QEH_HIP(hipStreamSynchronize(ctx->stream));  // its phase A may still be running
+    return QEH_OK;
+}
+
 extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols,
                                          int probe_key_idx, const qeh_expr *predicate, const qeh_column *build_key,
                                          const qeh_column *build_group_keys, int n_group_keys, const qeh_agg *aggs,
@@ -4354,3 +4752,12 @@ extern "C" int qeh_join_filter_aggregate(qeh_ctx *ctx, const qeh_column *probe_c
                           gt.rep_row.as<uint32_t>(), true, "join_filter_aggregate", out_keys, out_aggs, out_groups,
                           &pre);
 }
+
+#if QEH_PA_STAMPS
+// diagnostic build only: the per-wave phase cycles of the last fused phase A (see QEH_PA_STAMPS)
+extern "C" int qeh_debug_pa_stamps(uint64_t *out, uint64_t n_words) {
+    using namespace qeh;
+    const uint64_t w = std::min<uint64_t>(n_words, (uint64_t)kMaxSliceGrid * 16 * kPaStampWords);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(qeh_pa_stamps), w * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

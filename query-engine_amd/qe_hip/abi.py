@@ -92,11 +92,18 @@ SIGNATURES = {
     "qeh_columns_minmax": (I, [P, COLP, I, C.POINTER(I64)]),
     "qeh_dense_states_f64": (I, [P, COLP, COLP, I, I64, I64, P]),
     "qeh_dense_states_take": (I, [P, P, I, I64, I64, I, I, C.c_int32, C.POINTER(C.c_int32), COLP, COLP, C.POINTER(I64)]),
+    "qeh_dense_states_take_status": (I, [P, P, I, I64, I64, I, I, C.c_int32, C.POINTER(C.c_int32), COLP, COLP,
+                                         C.POINTER(I64), C.POINTER(C.c_double)]),
     "qeh_join_filter_aggregate_table": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, I64, C.c_int32, AGGP, I, COLP, COLP,
                                             C.POINTER(I64)]),
     "qeh_join_filter_aggregate_table_lanes": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, AGGP, I, P]),
     "qeh_join_filter_aggregate_table_lanes_async": (I, [P, COLP, I, I, EXPRP, P, I64, U64, I64, AGGP, I, P, P]),
     "qeh_broadcast_stats": (I, [P, COLP, COLP, C.POINTER(I64), I, P]),
+    "qeh_fused_items_begin": (I, [P, COLP, I, I, EXPRP, AGGP, I, P, I, I, C.POINTER(P)]),
+    "qeh_fused_items_build": (I, [P, P, COLP, COLP, I, U64, P, P]),
+    "qeh_fused_items_finish": (I, [P, P, P, U64, P, I, I64, P]),
+    "qeh_fused_items_abort": (I, [P, P]),
+    "qeh_fused_items_check": (I, [P, COLP, I, I, EXPRP, AGGP, I]),
     "qeh_join_filter_aggregate_prelaunch_stats": (I, [P, COLP, I, I, EXPRP, AGGP, I, P, I, I]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),
     "qeh_sort_indices_nulls": (I, [P, COLP, I, C.POINTER(C.c_int8), C.POINTER(C.c_int8), COLP]),

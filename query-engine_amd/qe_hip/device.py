@@ -404,6 +404,18 @@ class Context:
                                                  dts, C.byref(ok), ov, C.byref(g)))
         return self._wrap(ok), [self._wrap(ov[i]) for i in range(n_vals)], g.value
 
+    def dense_states_take_status(self, in_ptr: int, n_vals: int, key_min: int, key_range: int, world: int, rank: int,
+                                 key_dtype: int, out_dtypes: Sequence[int]):
+        """qeh_dense_states_take_status: dense_states_take + the status lane, one host read."""
+        ok = abi.QehColumn()
+        ov = (abi.QehColumn * max(n_vals, 1))()
+        dts = (C.c_int32 * max(n_vals, 1))(*out_dtypes)
+        g = C.c_int64()
+        st = C.c_double()
+        abi.check(self.lib.qeh_dense_states_take_status(self.h, in_ptr, n_vals, key_min, key_range, world, rank,
+                                                        key_dtype, dts, C.byref(ok), ov, C.byref(g), C.byref(st)))
+        return self._wrap(ok), [self._wrap(ov[i]) for i in range(n_vals)], g.value, st.value
+
     def u16_count_nonzero(self, table_ptr: int, n: int) -> int:
         out = C.c_int64()
         abi.check(self.lib.qeh_u16_count_nonzero(self.h, table_ptr, n, C.byref(out)))
@@ -478,6 +490,65 @@ class Context:
         ex = (C.c_int64 * max(len(extra), 1))(*[int(q) for q in extra])
         abi.check(self.lib.qeh_broadcast_stats(self.h, C.byref(build_key.c), C.byref(group_key.c), ex, len(extra),
                                                out_ptr))
+
+    # the items form of the distributed broadcast join (include/qeh.h qeh_fused_items_*)
+    FUSED_ITEMS_SLICES = 160  # slices the item buffers hold (kSliceMaxF)
+
+    def fused_items_begin(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                          predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]], stats_ptr: int,
+                          world: int, row_len: int) -> int:
+        """qeh_fused_items_begin: plan from the gathered stats rows + phase A queued; returns the handle.
+        Raises QehError(QEH_E_UNSUPPORTED) for shapes outside the items form."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        h = C.c_void_p()
+        abi.check(self.lib.qeh_fused_items_begin(self.h, cp, len(probe_cols), probe_key_idx,
+                                                 C.byref(e) if e is not None else None, ca, len(aggs), stats_ptr, world,
+                                                 row_len, C.byref(h)))
+        return h.value
+
+    @staticmethod
+    def fused_items_shape(max_rows: int, world: int) -> Tuple[int, int]:
+        """(n_blocks, span) of the items form's build for the largest rank's row count: one workgroup per
+        ~8 K rows, at most 512 spans over all ranks (phase B's bound), spans of ceil(rows / blocks) + 640
+        u32 (multiples of 4)."""
+        nb = max(1, min(512 // max(world, 1), -(-max_rows // 8192)))
+        span = (-(-max_rows // nb) + 4 * 160 + 3) // 4 * 4
+        return nb, span
+
+    def fused_items_build(self, handle: int, build_key: DeviceColumn, group_key: DeviceColumn, n_blocks: int,
+                          span: int, items_ptr: int, offs_ptr: int) -> None:
+        """qeh_fused_items_build: this rank's build rows grouped by slice in n_blocks spans
+        (items[n_blocks * span]; offs[n_blocks * 322]: run starts, then run rows, per span)."""
+        abi.check(self.lib.qeh_fused_items_build(self.h, handle, C.byref(build_key.c), C.byref(group_key.c), n_blocks,
+                                                 span, items_ptr, offs_ptr))
+
+    def fused_items_finish(self, handle: int, items_ptr: int, span: int, offs_ptr: int, n_regions: int,
+                           n_groups: int, lanes_ptr: int) -> None:
+        """qeh_fused_items_finish: phase B over the gathered spans (n_regions) + the lanes (status last)."""
+        abi.check(self.lib.qeh_fused_items_finish(self.h, handle, items_ptr, span, offs_ptr, n_regions, n_groups,
+                                                  lanes_ptr))
+
+    def fused_items_check(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                          predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]]) -> bool:
+        """qeh_fused_items_check: whether this rank's probe shard fits the items form (nothing queued)."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        s = self.lib.qeh_fused_items_check(self.h, cp, len(probe_cols), probe_key_idx,
+                                           C.byref(e) if e is not None else None, ca, len(aggs))
+        if s == abi.QEH_E_UNSUPPORTED:
+            return False
+        abi.check(s)
+        return True
+
+    def fused_items_abort(self, handle: int) -> None:
+        abi.check(self.lib.qeh_fused_items_abort(self.h, handle))
 
     def join_filter_aggregate_prelaunch_stats(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                                               predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],

@@ -527,6 +527,11 @@ class DistributedExecutor:
         probe_flags = [1 if probe_cols[c].c.validity else 0 for _, c in aggs]
         probe_nullable = None
         self.last_build = "replicated"
+        if build_sharded and not os.environ.get("QEH_NO_ITEMS_BCAST"):
+            out = self._broadcast_items(probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs)
+            if out is not None:
+                self.last_build = "items"
+                return out
         if build_sharded:
             st = self._build_stats(build_key, build_group_keys, probe_flags,
                                    probe=(probe_cols, probe_key_idx, predicate, aggs))
@@ -630,6 +635,98 @@ class DistributedExecutor:
             out["krange"] = [int(live[:, 1].min()), int(live[:, 2].max()), total]
             out["grange"] = [int(live[:, 3].min()), int(live[:, 4].max()), total]
         return out
+
+    ITEMS_SLICES = 160       # slices an item buffer holds (the library's kSliceMaxF)
+    ITEMS_STATE_WORDS = 3584  # group slots x value slots the fused pipeline's phase B keeps in LDS
+    ITEMS_MIN_TABLE_BYTES = 6 << 20  # smaller key ranges take the single fused pass (the library's rule)
+
+    def _broadcast_items(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs):
+        """The items form of the broadcast join (include/qeh.h qeh_fused_items_*; the fused pipeline of
+        N = 1 with its build side sharded): every rank groups ITS dimension shard by 2^16-key slice into
+        4-B items, one all-gather moves the items (4 B per dimension row, one region per rank and
+        slice), and phase B builds each slice's LDS entries from every rank's region -- no 2-B-per-key
+        table, no table all-reduce and no table reads in phase B, and phase A is the fused pipeline's
+        kernel.  Phase A is queued (planned on the device from the gathered stats rows) before the host
+        reads the rows.  Whether the form runs is decided from gathered values only -- each rank's
+        shape check travels in its stats row -- so every rank issues the same collectives; a plan the
+        device declines, a region overflow or a key on two ranks come back in the status lane of the
+        lanes' all-reduce, and every rank then returns None (the caller takes the table / all-gather
+        form).  Returns the dense final ([keys], aggs, groups) or None."""
+        if (self.device != "cuda" or len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
+                or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32)
+                or any(f not in (AF.Count, AF.Sum) for f, _ in aggs)):
+            return None
+        gkc = build_group_keys[0]
+        local_ok = 1 if self.ctx.fused_items_check(probe_cols, probe_key_idx, predicate, aggs) else 0
+        bitmap = 1 if (build_key.c.validity or gkc.c.validity) else 0
+        row_len = 7  # [rows, key min, max, group key min, max, has-bitmap, shape ok]
+        row = torch.empty(row_len, dtype=torch.int64, device="cuda")
+        self._sync_torch()
+        self.ctx.broadcast_stats(build_key, gkc, [bitmap, local_ok], row.data_ptr())
+        self._sync()
+        if self.world > 1:
+            out = torch.empty(self.world * row_len, dtype=torch.int64, device="cuda")
+            dist.all_gather_into_tensor(out, row, group=self.group)
+            row = out
+        pinned = getattr(self, "_items_pinned", None)
+        if pinned is None or pinned.numel() != row.numel():
+            pinned = self._items_pinned = torch.empty(row.numel(), dtype=torch.int64, pin_memory=True)
+        pinned.copy_(row, non_blocking=True)  # queued ahead of phase A (a copy behind it would wait for it)
+        copied = torch.cuda.Event()
+        copied.record()
+        handle = None
+        if local_ok:  # phase A planned on the device from the gathered rows, while the host reads them
+            self._sync_torch()
+            handle = self.ctx.fused_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(), self.world,
+                                                row_len)
+        copied.synchronize()
+        M = pinned.numpy().reshape(self.world, row_len).copy()
+        live = M[M[:, 0] > 0]
+        total = int(M[:, 0].sum())
+        n_sum = sum(1 for f, _ in aggs if f == AF.Sum)
+        ok = bool(M[:, 6].min() == 1 and M[:, 5].max() == 0 and total > 0)
+        if ok:
+            kmin, kmax = int(live[:, 1].min()), int(live[:, 2].max())
+            gmin, gmax = int(live[:, 3].min()), int(live[:, 4].max())
+            R, G = kmax - kmin + 1, gmax - gmin + 1
+            F = (R + (1 << 16) - 1) >> 16
+            ok = (1 <= F <= self.ITEMS_SLICES and G * (1 + n_sum) <= self.ITEMS_STATE_WORDS
+                  and 2 * R >= self.ITEMS_MIN_TABLE_BYTES)
+        if not ok:
+            if handle is not None:
+                self.ctx.fused_items_abort(handle)
+            return None
+        # this rank's build rows grouped by slice (spans of ~8 K rows, one run per slice each), all-gathered:
+        # 4 B per dimension row (+ the runs' padding to 16 B); every rank uses the same shape
+        nb, span = self.ctx.fused_items_shape(int(M[:, 0].max()), self.world)
+        OW = 2 * (self.ITEMS_SLICES + 1)
+        items = torch.empty(nb * span, dtype=torch.int32, device="cuda")
+        offs = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        self._sync_torch()
+        self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
+        self._sync()
+        if self.world > 1:
+            gi = torch.empty(self.world * nb * span, dtype=torch.int32, device="cuda")
+            go = torch.empty(self.world * nb * OW, dtype=torch.int32, device="cuda")
+            dist.all_gather_into_tensor(gi, items, group=self.group)
+            dist.all_gather_into_tensor(go, offs, group=self.group)
+            items, offs = gi, go
+        nl = (1 + len(aggs)) * G + 1  # + the status lane
+        lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
+        self._sync_torch()
+        self.ctx.fused_items_finish(handle, items.data_ptr(), span, offs.data_ptr(), self.world * nb, G,
+                                    lanes.data_ptr())
+        self._sync()
+        if self.world > 1:
+            dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+        self._sync_torch()
+        got, ov, g, bad = self.ctx.dense_states_take_status(
+            lanes.data_ptr(), len(aggs), gmin, G, self.world, self.rank, gkc.dtype,
+            [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
+        if bad != 0.0:  # declined, overflowed or a repeated key on some rank (the same lane on every rank)
+            return None
+        self.last_final = "dense"
+        return [got], ov, g
 
     def _broadcast_table(self, st, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs,
                          probe_nullable):

@@ -420,24 +420,32 @@ def mode_gpu_devtensors(rank, world):
     b = np.linspace(0, nd, world + 1).astype(int)
     pred = binop(col(0), BinaryOp.Greater, lit(49))
     aggs = [(AF.Sum, 2), (AF.Count, 2)]
-    ctx.timing(True)
-    ctx.timing_reset()
-    keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
-        [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
-        [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
-    launches = ctx.kernel_time("slice_partition")[1]
-    ctx.timing(False)
-    assert dx.last_final == "dense"
-    assert dx.last_build == "table", dx.last_build  # each rank inserted its shard, the tables were summed
-    assert launches == 1, launches  # the prelaunched phase A was adopted (not re-run)
-    res = dx.gather_to_root(keys + aggs_out)
     if rank == 0:
         X = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 1, n * world, 100)
         KK = ob.generate(abi_gen("UNIFORM_MOD"), 0x5EED, 2, n * world, nd)
         VV = ob.generate(abi_gen("UNIT_F64"), 0x5EED, 3, n * world)
         wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KK), ob.HostCol(VV)], 1, pred,
                                               ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
-        assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    # the items form (default): every rank groups its dim shard by slice, the items are all-gathered,
+    # phase A runs once; then the table form (QEH_NO_ITEMS_BCAST): shard tables summed, the
+    # prelaunched phase A adopted
+    for form in ("items", "table"):
+        if form == "table":
+            os.environ["QEH_NO_ITEMS_BCAST"] = "1"
+        ctx.timing(True)
+        ctx.timing_reset()
+        keys, aggs_out, ng = dx.join_filter_aggregate_broadcast(
+            [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)], 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+            [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs, build_sharded=True)
+        launches = ctx.kernel_time("slice_partition")[1]
+        ctx.timing(False)
+        os.environ.pop("QEH_NO_ITEMS_BCAST", None)
+        assert dx.last_final == "dense"
+        assert dx.last_build == form, (dx.last_build, form)
+        assert launches == 1, launches  # one phase A (the table form: the prelaunch adopted, not re-run)
+        res = dx.gather_to_root(keys + aggs_out)
+        if rank == 0:
+            assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
     fact = [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)]
     # a build key held by two ranks (rank 0 and the last rank) with SUM + COUNT: the no-wait table
     # form sums the two entries to one above G (both group slots >= G / 2), which the table check

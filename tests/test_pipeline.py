@@ -781,3 +781,69 @@ def test_prelaunch_from_device_stats(ctx, case):
     assert launches == (2 if case == "other_probe" else 1)
     assert g == wg
     assert_grouped_equal([c.to_numpy() for c in gk], [c.to_numpy() for c in ga], wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,dup", [(1, False), (3, False), (8, False), (3, True)])
+def test_items_form_vs_oracle(ctx, ranks, dup):
+    """The items form of the distributed broadcast join (qeh_fused_items_*) with `ranks` simulated on
+    one device: every rank's fact and dim shard through begin (phase A planned from the gathered
+    stats rows) and build (its dim rows grouped by slice), the rank-major concatenation of every
+    rank's item buffers standing in for the all-gather, finish per rank, the lanes summed (the
+    all-reduce's stand-in) and taken -- the union over ranks equals the oracle's join + filter +
+    group-by.  A build key on two ranks comes back as the status lane (every rank falls back)."""
+    import torch
+    n_fact, n_dim = 3_000_000, 4_000_000  # (a key range of >= 6 MB of u16 entries: the slice pipeline's)
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 1000)
+    if dup:
+        dk[-3] = dk[2]  # rank 0 and the last rank hold the same key
+    fb = np.linspace(0, n_fact, ranks + 1).astype(int)
+    db = np.linspace(0, n_dim, ranks + 1).astype(int)
+    S, row_len = 160, 7
+    rows = []
+    for r in range(ranks):
+        row = torch.empty(row_len, dtype=torch.int64, device="cuda")
+        ctx.broadcast_stats(ctx.upload(dk[db[r]:db[r + 1]]), ctx.upload(dg[db[r]:db[r + 1]]), [0, 1], row.data_ptr())
+        rows.append(row)
+    ctx.sync()
+    M = torch.cat(rows)
+    gmin, gmax = int(dg.min()), int(dg.max())
+    G = gmax - gmin + 1
+    nb, span = ctx.fused_items_shape(int(np.diff(db).max()), ranks)
+    OW = 2 * (S + 1)
+    handles, facts, items, offs = [], [], [], []
+    for r in range(ranks):
+        fact = [ctx.upload(x[fb[r]:fb[r + 1]]), ctx.upload(k[fb[r]:fb[r + 1]]), ctx.upload(v[fb[r]:fb[r + 1]])]
+        assert ctx.fused_items_check(fact, 1, PRED, AGGS)
+        h = ctx.fused_items_begin(fact, 1, PRED, AGGS, M.data_ptr(), ranks, row_len)
+        it = torch.empty(nb * span, dtype=torch.int32, device="cuda")
+        of = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        ctx.fused_items_build(h, ctx.upload(dk[db[r]:db[r + 1]]), ctx.upload(dg[db[r]:db[r + 1]]), nb, span,
+                              it.data_ptr(), of.data_ptr())
+        handles.append(h), facts.append(fact), items.append(it), offs.append(of)
+    ctx.sync()
+    gi, go = torch.cat(items), torch.cat(offs)
+    nl = (1 + len(AGGS)) * G + 1
+    total = torch.zeros(nl, dtype=torch.float64, device="cuda")
+    for r in range(ranks):
+        lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
+        ctx.fused_items_finish(handles[r], gi.data_ptr(), span, go.data_ptr(), ranks * nb, G, lanes.data_ptr())
+        ctx.sync()
+        total += lanes
+    torch.cuda.synchronize()
+    if dup:
+        assert float(total[nl - 1]) != 0.0  # the repeated key is flagged: every rank falls back
+        return
+    assert float(total[nl - 1]) == 0.0
+    got_k, got_a = [], []
+    for r in range(ranks):
+        ok, ov, g = ctx.dense_states_take(total.data_ptr(), len(AGGS), gmin, G, ranks, r, abi.DT_INT64,
+                                          [abi.DT_FLOAT64, abi.DT_INT64])
+        got_k.append(ok.to_numpy()[0])
+        got_a.append([c.to_numpy()[0] for c in ov])
+    gk = [(np.concatenate(got_k), None)]
+    ga = [(np.concatenate([a[j] for a in got_a]), None) for j in range(len(AGGS))]
+    wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(dk),
+                                          [ob.HostCol(dg)], AGGS)
+    assert len(gk[0][0]) == wg
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])

@@ -21,4 +21,37 @@ run_tests $O/tests.txt tests/test_employees_departments.py tests/test_config4.py
     "tests/test_distributed.py::test_device_tensor_collectives_several_ranks_on_one_gpu" tests/test_pipeline.py
 }
 
+r5b() {
+# phase-A cycle stamps (diagnostic builds): flush late (default) and the round-4 order
+O=gpurun_out/r5b; mkdir -p $O
+timeout -k 10 300 python3 tools/exp/pa_stamps.py libqeh_stamps.so libqeh_stamps0.so > $O/stamps.txt 2>&1 \
+    || { echo stamps failed; cat $O/stamps.txt; exit 1; }
+cat $O/stamps.txt
+}
+
+r5c() {
+# items form of the distributed broadcast join: parity on one device (simulated ranks) and over gloo
+# device tensors (world 2 / 3 / 8), then the rank-share rehearsal of an N = 8 step (1.10 ms in r04)
+O=gpurun_out/r5c; mkdir -p $O
+run_tests $O/tests.txt "tests/test_pipeline.py::test_items_form_vs_oracle" \
+    "tests/test_distributed.py::test_device_tensor_collectives_several_ranks_on_one_gpu" \
+    "tests/test_distributed.py::test_rccl_world_size_one" || exit 1
+for r in 0 3; do
+  QEH_BENCH_RANK_OF=$r/8 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --cpu-sample 0 > $O/rank${r}of8.json 2> $O/rank${r}of8.err \
+      || { tail -20 $O/rank${r}of8.err; exit 1; }
+  tail -1 $O/rank${r}of8.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("dist_build"), d.get("dist_final"))'
+done
+QEH_NO_ITEMS_BCAST=1 QEH_BENCH_RANK_OF=0/8 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --cpu-sample 0 > $O/rank0of8_table.json 2> $O/rank0of8_table.err \
+    || { tail -20 $O/rank0of8_table.err; exit 1; }
+tail -1 $O/rank0of8_table.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("table form", d["ms_per_step"], d.get("dist_build"))'
+}
+
+r5d() {
+# kernel trace of the rank-share rehearsal step (items form) and of the N = 1 metric step
+O=gpurun_out/r5d; mkdir -p $O
+QEH_BENCH_RANK_OF=0/8 bash tools/trace_bench.sh r5d_rank0 || exit 1
+f=$(ls gpurun_out/tb_r5d_rank0/*/kt_kernel_trace.csv 2>/dev/null | head -1); [ -z "$f" ] && f=$(find gpurun_out/tb_r5d_rank0 -name '*kernel_trace.csv' | head -1)
+python3 tools/trace_step.py "$f" k_slice_probe > $O/rank0_step_trace.txt; cat $O/rank0_step_trace.txt
+}
+
 "$@"
