@@ -354,6 +354,15 @@ def check_metric_plans(rank, world, dx, ctx):
             res = dx.gather_to_root(keys + aggs_out)
             if rank == 0:
                 assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=floats), name
+    # a non-null key: the shuffle's probe side takes the fused id + histogram pass (k_ids_hist_pred)
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
+    want = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(K), ob.HostCol(V)], 1, pred, ob.HostCol(DK),
+                                    [ob.HostCol(DG)], aggs)
+    keys, aggs_out, ng = dx.join_filter_aggregate_shuffle([ctx.upload(x), ctx.upload(k), ctx.upload(v)], 1, pred,
+                                                          ctx.upload(dk), [ctx.upload(dg)], aggs)
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=[0])
 
 
 def mode_gpu_cfg4(rank, world):

@@ -28,17 +28,18 @@
     } while (0)
 
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
-constexpr int kBlock = 1024, TILE = 8192, DIG = 1024, RUN = TILE / DIG;  // 8 rows per digit per tile
+constexpr int kBlock = 1024, TILE = 8192;
 
 __global__ void k_fill(int64_t *a, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         a[i] = (int64_t)(i * 0x9E3779B97F4A7C15ull);
 }
 
-template <int W>
+template <int W, int DIG = 1024>
 __global__ __launch_bounds__(kBlock) void k_wpat(const int64_t *__restrict__ K, const int64_t *__restrict__ V,
                                                  int64_t tiles_per_wg, uint64_t *__restrict__ okey, uint16_t *__restrict__ okl,
                                                  uint8_t *__restrict__ orec, int64_t *__restrict__ sink) {
+    constexpr int RUN = TILE / DIG;  // rows per digit per tile
     const int tid = threadIdx.x;
     const int64_t wg = blockIdx.x, G = gridDim.x;
     // digit d's region for this workgroup: RUN items per tile, tiles_per_wg tiles (+ 8 slack, + an
@@ -113,7 +114,7 @@ int main(int argc, char **argv) {
     uint64_t *okey;
     uint16_t *okl;
     uint8_t *orec;
-    const uint64_t per = (uint64_t)tiles_per_wg * RUN + 16, items = per * DIG * G;
+    const uint64_t per = (uint64_t)tiles_per_wg * 8 + 16, items = per * 1024 * G;
     CK(hipMalloc(&K, rows * 8));
     CK(hipMalloc(&V, rows * 8));
     CK(hipMalloc(&sink, 64));
@@ -127,7 +128,9 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const char *names[] = {"W0 loads only", "W1 runs, any alignment (pass 1)", "W2 runs, 64-B aligned",
-                           "W3 2-tile chunks, 128-B aligned", "W4 80-B records", "W5 sequential", "W6 4-tile chunks, 256-B aligned"};
+                           "W3 2-tile chunks, 128-B aligned", "W4 80-B records", "W5 sequential", "W6 4-tile chunks, 256-B aligned",
+                           "W7 runs of 16 (512 digits), any alignment", "W8 runs of 32 (256 digits), any alignment",
+                           "W9 runs of 64 (128 digits), any alignment"};
     auto run = [&](int w) {
         auto go = [&]() {
             switch (w) {
@@ -137,6 +140,9 @@ int main(int argc, char **argv) {
                 case 3: hipLaunchKernelGGL(k_wpat<3>, dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
                 case 4: hipLaunchKernelGGL(k_wpat<4>, dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
                 case 6: hipLaunchKernelGGL(k_wpat<6>, dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
+                case 7: hipLaunchKernelGGL((k_wpat<1, 512>), dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
+                case 8: hipLaunchKernelGGL((k_wpat<1, 256>), dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
+                case 9: hipLaunchKernelGGL((k_wpat<1, 128>), dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
                 default: hipLaunchKernelGGL(k_wpat<5>, dim3(G), dim3(kBlock), 0, 0, K, V, tiles_per_wg, okey, okl, orec, sink); break;
             }
         };
@@ -155,6 +161,6 @@ int main(int argc, char **argv) {
         const double gb = rows * (w ? 26.0 : 16.0) / 1e9;
         std::printf("%-36s %8.3f ms  %6.1f GB  %5.2f TB/s\n", names[w], best, gb, gb / best);
     };
-    for (int w = 0; w < 7; ++w) run(w);
+    for (int w = 0; w < 10; ++w) run(w);
     return 0;
 }
