@@ -294,7 +294,7 @@ constexpr int kSliceMaxF = 160;                  // slices: key range <= 160 * 6
 constexpr int kSliceBlock = 1024;                // one workgroup per CU in both phases
 constexpr int kSliceTile = kSliceBlock * kFastR;  // 8192 probe rows per phase-A iteration
 constexpr int kSliceChunk = 32;                  // items per flushed chunk
-constexpr int kMaxSliceGrid = 512;               // phase-A workgroups of the fused pipeline (one or two per CU)
+constexpr int kMaxSliceGrid = 512;               // phase-A workgroups / build regions (items form) phase B walks
 constexpr int kSliceStateWords = 3584;           // phase-B LDS aggregate states (n_slots * G)
 // Group-range slices (G too large for LDS states): phase A looks the group id up and partitions
 // by gid >> kGidSliceBits; phase B aggregates one range of 2^kGidSliceBits groups in LDS.
@@ -464,20 +464,10 @@ struct __attribute__((aligned(16))) SliceChunk {
 #ifndef QEH_EARLY_CHUNK
 #define QEH_EARLY_CHUNK 64
 #endif
-// NTH = 512 (fused pipeline, QEH_FUSED_2WG): two co-resident 512-thread workgroups per CU, each with
-// 1024-row tiles and 32-item chunks (72 KB of LDS), so one workgroup's rank / scan / stage phases run
-// while the other's loads stream.
-#ifndef QEH_EARLY2_PAIRS
-#define QEH_EARLY2_PAIRS 1
-#endif
-#ifndef QEH_EARLY2_CHUNK
-#define QEH_EARLY2_CHUNK 32
-#endif
 template <int NACOL, bool EARLY = false, int NTH = kSliceBlock>
 struct SliceShape {
-    static constexpr bool HALF = EARLY && NTH < kSliceBlock;
-    static constexpr int P = NACOL > 1 ? 2 : (HALF ? QEH_EARLY2_PAIRS : EARLY ? QEH_EARLY_PAIRS : kFastPairs);
-    static constexpr int CH = NACOL > 1 ? 16 : (HALF ? QEH_EARLY2_CHUNK : EARLY ? QEH_EARLY_CHUNK : kSliceChunk);
+    static constexpr int P = NACOL > 1 ? 2 : (EARLY ? QEH_EARLY_PAIRS : kFastPairs);
+    static constexpr int CH = NACOL > 1 ? 16 : (EARLY ? QEH_EARLY_CHUNK : kSliceChunk);
     static constexpr int TILE = NTH * 2 * P;
 };
 
@@ -867,158 +857,6 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
         const uint64_t n = (uint64_t)pos[b] + cn[b];
         rg.count[region0 + b] = (uint32_t)((n < cap ? n : cap) - hd[b]);
     }
-}
-
-// Phase A of the fused pipeline without staging (QEH_FUSED_RING=1): every selected row takes its
-// position in its slice's region from one LDS atomic on the slice's item count (no order inside a
-// region is needed), and is written straight into the slice's LDS rings -- keys into a 128-entry ring
-// flushed in 64-key (128-B) chunks, values into a 64-entry ring flushed in 32-value (256-B) chunks.
-// After a barrier the waves flush every whole chunk of their own slices (a quarter-wave per slice),
-// then a second barrier frees the ring slots: two barriers per tile, no scan, no staging copy, no
-// carry pass.  A row whose ring slot is still taken (more rows for one slice in one tile than the
-// ring has free, i.e. skewed keys) is stored straight to its region position instead; the chunk it
-// shares with ring items is then written from the ring past that direct prefix (dk / dv: where the
-// ring part of the window's first chunk starts).
-constexpr int kRingK = 128, kRingKC = 64, kRingV = 64, kRingVC = 32;
-#ifndef QEH_RING_PAIRS
-#define QEH_RING_PAIRS 4
-#endif
-constexpr int kRingPairs = QEH_RING_PAIRS;  // row pairs per lane: 8192-row tiles
-// Measured against the staged kernel (profiles/r04/ab_ring_vs_staged.txt, A/B x3 on one box): equal
-// within the box's drift (phase A 5.06-5.38 vs 5.05-5.36 ms; 4096-row tiles 0.05-0.1 ms slower), i.e.
-// the staging, carry and scan work is hidden under the stream and phase A sits at the mixed
-// read/write rate of its 29 GB; kept as an option, the staged kernel stays the default.
-template <int NTERMS, int NACOL, bool NT, int P>
-__global__ __launch_bounds__(kSliceBlock) void k_slice_ring(FastIn in, PredTerms terms, int64_t n_tiles, SliceRegions rg,
-                                                            const SlicePlan *__restrict__ dplan, int64_t tail_rows,
-                                                            FusedPro fp) {
-    static_assert(NACOL <= 1, "one value column");
-    constexpr int R = 2 * P, TILE = kSliceBlock * R, MAXF = kSliceMaxF;
-    const SlicePlan pl = *dplan;
-    if (!pl.ok) return;
-    const int64_t kmin = pl.kmin;
-    const uint64_t range = pl.range, cap = pl.cap;
-    const int F = pl.F;
-    __shared__ uint32_t head[MAXF], fk[MAXF], fv[MAXF], dk[MAXF], dv[MAXF];
-    __shared__ uint16_t ring_k[MAXF * kRingK];
-    __shared__ int64_t ring_v[NACOL ? MAXF * kRingV : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t region0 = (uint64_t)blockIdx.x * F;
-    {
-        __shared__ uint32_t dcnt[MAXF];
-        fused_prologue<kSliceBlock>(fp, F, kmin, dcnt);
-    }
-    for (int i = tid; i < MAXF; i += kSliceBlock) head[i] = 0, fk[i] = 0, fv[i] = 0, dk[i] = 0, dv[i] = 0;
-    __syncthreads();
-    bool ovf = false;
-    FastTile<NTERMS, NACOL, NT, P> ft;
-    const int64_t n_all = n_tiles + (tail_rows > 0 ? 1 : 0), lim = n_tiles * TILE + tail_rows;
-    auto issue_tile = [&](int64_t tl) {
-        const int64_t b = tl * TILE + (int64_t)wave * (64 * R) + 2 * lane;
-        if (tl < n_tiles) ft.issue(in, b);
-        else ft.issue_tail(in, b, lim);
-    };
-    // whole chunks of slice b below its count h, from the ring window [f, f + RS) (chunks past the
-    // window were stored directly); items below d were stored directly too
-    const int q16 = lane & 15;
-    auto flush_slice = [&](int b) {
-        const uint32_t h = head[b];
-        const uint64_t base = (region0 + b) * cap;
-        {
-            const uint32_t f = fk[b], d = dk[b];
-            uint32_t c0 = f;
-            for (; c0 + kRingKC <= h && c0 < f + kRingK; c0 += kRingKC) {
-                const uint32_t r0 = c0 + 4 * q16;
-                if (r0 + 4 > cap) { ovf = true; continue; }
-                const uint16_t *src = ring_k + b * kRingK + (r0 & (kRingK - 1));
-                if (r0 >= d) {
-                    *(uint2 *)(rg.key + base + r0) = *(const uint2 *)src;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (r0 + j >= d) rg.key[base + r0 + j] = src[j];
-                }
-            }
-            const uint32_t fn = h / kRingKC * kRingKC;
-            if (fn != f) {
-                // the new window's first chunk [fn, h): stored directly when it lay past the old window
-                const uint32_t dn = fn >= f + kRingK ? h : fn;
-                if (q16 == 0) fk[b] = fn, dk[b] = dn;
-            }
-        }
-        if constexpr (NACOL > 0) {
-            const uint32_t f = fv[b], d = dv[b];
-            uint32_t c0 = f;
-            for (; c0 + kRingVC <= h && c0 < f + kRingV; c0 += kRingVC) {
-                const uint32_t r0 = c0 + 2 * q16;
-                if (r0 + 2 > cap) { ovf = true; continue; }
-                const int64_t *src = ring_v + b * kRingV + (r0 & (kRingV - 1));
-                if (r0 >= d) {
-                    __builtin_nontemporal_store(*(const v2i64 *)src, (v2i64 *)(rg.val + base + r0));
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        if (r0 + j >= d) __builtin_nontemporal_store(src[j], rg.val + base + r0 + j);
-                }
-            }
-            const uint32_t fn = h / kRingVC * kRingVC;
-            if (fn != f) {
-                const uint32_t dn = fn >= f + kRingV ? h : fn;
-                if (q16 == 0) fv[b] = fn, dv[b] = dn;
-            }
-        }
-    };
-    int64_t tile = blockIdx.x;
-    if (tile < n_all) issue_tile(tile);
-    for (; tile < n_all; tile += gridDim.x) {
-        ft.eval(in, terms);
-        uint32_t sel = ft.sel;
-        if (tile >= n_tiles) sel &= decltype(ft)::tail_mask(tile * TILE + (int64_t)wave * (64 * R) + 2 * lane, lim);
-        uint32_t off[R], pos[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint64_t o = (uint64_t)ft.k(r) - (uint64_t)kmin;  // out of range -> huge, dropped
-            off[r] = (uint32_t)o;
-            pos[r] = 0;
-            if (((sel >> r) & 1) && o < range) pos[r] = atomicAdd(&head[(uint32_t)o >> kSliceBits], 1u);
-            else sel &= ~(1u << r);
-        }
-        int64_t vcur[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) vcur[r] = NACOL ? ft.a(0, r) : 0;
-        if (tile + gridDim.x < n_all) issue_tile(tile + gridDim.x);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!((sel >> r) & 1)) continue;
-            const uint32_t b = off[r] >> kSliceBits, ps = pos[r];
-            if (ps >= cap) { ovf = true; continue; }
-            const uint16_t kv = (uint16_t)(off[r] & (kSliceKeys - 1));
-            if (ps < fk[b] + kRingK) ring_k[b * kRingK + (ps & (kRingK - 1))] = kv;
-            else rg.key[(region0 + b) * cap + ps] = kv;
-            if constexpr (NACOL > 0) {
-                if (ps < fv[b] + kRingV) ring_v[b * kRingV + (ps & (kRingV - 1))] = vcur[r];
-                else __builtin_nontemporal_store(vcur[r], rg.val + (region0 + b) * cap + ps);
-            }
-        }
-        lds_barrier();  // B1: this tile's items are in the rings
-        for (int b = wave * 4 + (lane >> 4); b < F; b += kSliceBlock / 16) flush_slice(b);
-        lds_barrier();  // B2: whole chunks written, windows moved
-    }
-    // the partial last chunks: ring items at and past d
-    for (int p = tid; p < F * kRingK; p += kSliceBlock) {
-        const int b = p / kRingK, x = p % kRingK;
-        const uint32_t h = head[b], r = fk[b] + x;
-        if (r < h && r >= dk[b] && r < cap) rg.key[(region0 + b) * cap + r] = ring_k[b * kRingK + (r & (kRingK - 1))];
-    }
-    if constexpr (NACOL > 0) {
-        for (int p = tid; p < F * kRingV; p += kSliceBlock) {
-            const int b = p / kRingV, x = p % kRingV;
-            const uint32_t h = head[b], r = fv[b] + x;
-            if (r < h && r >= dv[b] && r < cap) rg.val[(region0 + b) * cap + r] = ring_v[b * kRingV + (r & (kRingV - 1))];
-        }
-    }
-    if (ovf) *rg.overflow = 1u;
-    for (int b = tid; b < F; b += kSliceBlock) rg.count[region0 + b] = (uint32_t)(head[b] < cap ? head[b] : cap);
 }
 
 // Phase B.  Region slots are enumerated slice-major (slot = b * nreg + r);
@@ -4127,50 +3965,24 @@ constexpr int kFusedNotEligible = -4;
 
 static void launch_slice_partition_early(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol,
                                          int64_t n_tiles, int64_t tail_rows, int grid, const SliceRegions &rg,
-                                         const SlicePlan *dplan, const FusedPro &fp, bool two, bool ring) {
+                                         const SlicePlan *dplan, const FusedPro &fp) {
     const bool nt = fast_nt_mode() == 1;
     KernelTimer kta(ctx, "slice_partition");
     const HashTable t{};
-    if (ring) {
-#define QEH_SR(NTV, NAV, NTB)                                                                                            \
-    hipLaunchKernelGGL((k_slice_ring<NTV, NAV, NTB, kRingPairs>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,     \
-                       pp.terms, n_tiles, rg, dplan, tail_rows, fp)
-#define QEH_SR_NA(NTV, NTB)                 \
-    if (nacol == 0) { QEH_SR(NTV, 0, NTB); } \
-    else { QEH_SR(NTV, 1, NTB); }
-#define QEH_SR_NT(NTB)                         \
-    if (nterms == 0) { QEH_SR_NA(0, NTB) }     \
-    else if (nterms == 1) { QEH_SR_NA(1, NTB) } \
-    else { QEH_SR_NA(2, NTB) }
-        if (nt) { QEH_SR_NT(true) } else { QEH_SR_NT(false) }
-#undef QEH_SR_NT
-#undef QEH_SR_NA
-#undef QEH_SR
-        return;
-    }
 #define QEH_SE(NTV, NAV, NTB)                                                                                            \
-    if (two)                                                                                                              \
-        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true, kSliceBlock / 2>), dim3(grid), dim3(kSliceBlock / 2), \
-                           0, ctx->stream, in, pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp);                       \
-    else                                                                                                                  \
-        hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in, \
-                           pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
-// two aggregate columns (18-B items: half tiles, 16-item chunks), one 1024-thread workgroup per CU
-#define QEH_SE2(NTV, NTB)                                                                                                 \
-    hipLaunchKernelGGL((k_slice_partition<NTV, 2, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,     \
+    hipLaunchKernelGGL((k_slice_partition<NTV, NAV, NTB, 0, true>), dim3(grid), dim3(kSliceBlock), 0, ctx->stream, in,   \
                        pp.terms, 0, 0, n_tiles, rg, t, dplan, tail_rows, fp)
-#define QEH_SE_NA(NTV, NTB)                 \
-    if (nacol == 0) { QEH_SE(NTV, 0, NTB); } \
+#define QEH_SE_NA(NTV, NTB)                      \
+    if (nacol == 0) { QEH_SE(NTV, 0, NTB); }      \
     else if (nacol == 1) { QEH_SE(NTV, 1, NTB); } \
-    else { QEH_SE2(NTV, NTB); }
-#define QEH_SE_NT(NTB)                         \
-    if (nterms == 0) { QEH_SE_NA(0, NTB) }     \
+    else { QEH_SE(NTV, 2, NTB); }
+#define QEH_SE_NT(NTB)                          \
+    if (nterms == 0) { QEH_SE_NA(0, NTB) }      \
     else if (nterms == 1) { QEH_SE_NA(1, NTB) } \
     else { QEH_SE_NA(2, NTB) }
     if (nt) { QEH_SE_NT(true) } else { QEH_SE_NT(false) }
 #undef QEH_SE_NT
 #undef QEH_SE_NA
-#undef QEH_SE2
 #undef QEH_SE
 }
 
@@ -4189,20 +4001,10 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     if (!fast_cols_eligible(cols, pp, key_col, specs_in, &in, &nterms, &nacol) || nacol > 2 ||
         (nacol == 2 && std::getenv("QEH_NO_FUSED_AGG2")))
         return kFusedNotEligible;
-    // phase A: the staged kernel with one 1024-thread or two 512-thread workgroups per CU
-    // (QEH_FUSED_2WG=1), or the ring kernel (QEH_FUSED_RING=1); two aggregate columns take the staged
-    // kernel with 18-B items
-    const bool ring = nacol < 2 && std::getenv("QEH_FUSED_RING") && std::atoi(std::getenv("QEH_FUSED_RING")) == 1;
-    const bool two = nacol < 2 && !ring && std::getenv("QEH_FUSED_2WG") && std::atoi(std::getenv("QEH_FUSED_2WG")) == 1;
-    constexpr int H = kSliceBlock / 2;
-    const int64_t tile_rows = ring ? (int64_t)kSliceBlock * 2 * kRingPairs
-                              : nacol == 2 ? (int64_t)SliceShape<2, true>::TILE
-                              : two ? (nacol ? SliceShape<1, true, H>::TILE : SliceShape<0, true, H>::TILE)
-                                    : (nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE);
-    const int chunk = ring ? kRingKC
-                      : nacol == 2 ? SliceShape<2, true>::CH
-                      : two ? (nacol ? SliceShape<1, true, H>::CH : SliceShape<0, true, H>::CH)
-                            : (nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH);
+    // phase A: one 1024-thread workgroup per CU (two aggregate columns: 18-B items, half tiles)
+    const int64_t tile_rows = nacol == 2 ? (int64_t)SliceShape<2, true>::TILE
+                                         : (nacol ? SliceShape<1, true>::TILE : SliceShape<0, true>::TILE);
+    const int chunk = nacol == 2 ? SliceShape<2, true>::CH : (nacol ? SliceShape<1, true>::CH : SliceShape<0, true>::CH);
     const int64_t n_tiles = n / tile_rows, tail = n - n_tiles * tile_rows;
     if (n_tiles == 0) return kFusedNotEligible;
     AggSpecs specs = specs_in;
@@ -4215,7 +4017,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     if (std::getenv("QEH_FUSED_SHARDS"))
         while (specs.shards < 64 && (size_t)specs.n_slots * Gs * 8 * specs.shards * 2 <= (8u << 20)) specs.shards *= 2;
     const int64_t n_all = n_tiles + (tail ? 1 : 0);
-    const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount * (two ? 2 : 1), n_all,
+    const int grid = (int)std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all,
                                              (int64_t)kMaxSliceGrid});
     const uint64_t tiles_per_wg = (uint64_t)((n_all + grid - 1) / grid);
 
@@ -4277,7 +4079,7 @@ static int fused_join_filter_aggregate(qeh_ctx *ctx, const ColSet &cols, int64_t
     fp.G = Gs;
     fp.as32 = gk.dtype == QEH_DT_INT32 ? 1 : 0;
     fp.plan = dplan;
-    launch_slice_partition_early(ctx, in, pp, nterms, nacol, n_tiles, tail, grid, rg, &dplan->sp, fp, two, ring);
+    launch_slice_partition_early(ctx, in, pp, nterms, nacol, n_tiles, tail, grid, rg, &dplan->sp, fp);
     {
         KernelTimer ktb(ctx, "slice_probe");
         DimSlices dim{ditems.as<uint32_t>(), dcount.as<uint32_t>(), st + 4, dplan};
@@ -4589,8 +4391,7 @@ static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_p
     fp.status = st;
     fp.plan = dplan;
     if (n_tiles > 0 || tail > 0)
-        launch_slice_partition_early(ctx, fi->in, pp, nterms, fi->nacol, n_tiles, tail, fi->grid, fi->rg, &dplan->sp, fp,
-                                     false, false);
+        launch_slice_partition_early(ctx, fi->in, pp, nterms, fi->nacol, n_tiles, tail, fi->grid, fi->rg, &dplan->sp, fp);
     QEH_HIP(hipGetLastError());
     *handle = fi.release();
     return QEH_OK;

@@ -260,14 +260,11 @@ def test_fused_pipeline_fallbacks_and_shapes(ctx, monkeypatch, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["QEH_FUSED_RING", "QEH_FUSED_2WG"])
 @pytest.mark.parametrize("skew", [False, True])
-def test_fused_phase_a_variants(ctx, monkeypatch, variant, skew):
-    """The fused pipeline's optional phase-A kernels (the ring kernel without staging, and the staged
-    kernel as two 512-thread workgroups per CU) against the oracle, with uniform keys and with 30 %
-    of the probe rows on one slice (the ring kernel's direct stores past a full ring)."""
+def test_fused_phase_a_skewed_slices(ctx, monkeypatch, skew):
+    """The fused pipeline against the oracle with uniform keys and with 30 % of the probe rows on one
+    slice (one slice's carries and chunks far above the others')."""
     monkeypatch.setenv("QEH_SLICE_MIN_BYTES", "0")
-    monkeypatch.setenv(variant, "1")
     n_fact, n_dim, groups = 1_000_003, 400_000, 600
     x, k, v, dk, dg = metric_data(n_fact, n_dim, groups)
     if skew:

@@ -8,7 +8,7 @@ bytes of a 16-B-per-lane coalesced stream -> doubled here; WRITE_SIZE is
 exact for 16-B streaming stores.  Units of both counters are KiB.
 Writes <dir>/traffic.json and prints a table.  With --emit FILE --rows N it
 also writes the bench-readable per-step HBM bytes of the metric query's probe
-pipeline (k_slice_partition or k_slice_ring + k_slice_probe, or the single-pass
+pipeline (k_slice_partition + k_slice_probe, or the single-pass
 k_join_agg_fast, plus the ragged-tail k_agg_rows) to FILE."""
 import csv
 import glob
@@ -57,7 +57,7 @@ def main(d):
     return summary, stats
 
 
-PIPELINE = ("k_slice_partition", "k_slice_ring", "k_slice_probe", "k_join_agg_fast", "k_agg_rows<1")
+PIPELINE = ("k_slice_partition", "k_slice_probe", "k_join_agg_fast", "k_agg_rows<1")
 
 
 def emit(summary, stats, path, rows, source):
