@@ -54,4 +54,31 @@ f=$(ls gpurun_out/tb_r5d_rank0/*/kt_kernel_trace.csv 2>/dev/null | head -1); [ -
 python3 tools/trace_step.py "$f" k_slice_probe > $O/rank0_step_trace.txt; cat $O/rank0_step_trace.txt
 }
 
+r5h() {
+# config 5 (ROW_NUMBER over 1e9 rows): kernel trace and per-kernel HBM bytes (FETCH_SIZE, WRITE_SIZE, one
+# pass each), the window path's first traffic record
+O=$PWD/gpurun_out/r5h; mkdir -p $O
+R=$PWD
+cd /tmp && export TMPDIR=/tmp
+B=(python3 "$R/tools/bench_configs.py" --only cfg5)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- "${B[@]}" > "$O/kt.log" 2>&1 || { tail -20 "$O/kt.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o fetch -- "${B[@]}" > "$O/fetch.log" 2>&1 || { tail -20 "$O/fetch.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o write -- "${B[@]}" > "$O/write.log" 2>&1 || { tail -20 "$O/write.log"; exit 1; }
+python3 "$R/tools/pmc_traffic.py" "$O" > "$O/summary.txt" 2>&1 || { cat "$O/summary.txt"; exit 1; }
+cat "$O/summary.txt"
+grep -h cfg5 "$O/kt.log" | tail -2
+}
+
+r5i() {
+# one box, three views of phase A: the traffic floor (no LDS work), the metric step, and the stamped
+# phase A (diagnostic build) -- run on several boxes to see which phases grow on a slow one
+O=gpurun_out/r5i_$(date +%H%M%S); mkdir -p $O
+rocm-smi --showclocks > $O/clocks.txt 2>&1 || true
+timeout -k 10 180 tools/ubench/floor_ubench 1000000000 5 > $O/floor.txt 2>&1 || { echo floor failed; cat $O/floor.txt; exit 1; }
+timeout -k 10 300 python3 tools/exp_slice.py --rounds 2 libqeh.so > $O/step.txt 2>&1 || { cat $O/step.txt; exit 1; }
+timeout -k 10 200 python3 tools/exp/pa_stamps.py libqeh_stamps.so > $O/stamps.txt 2>&1 || { cat $O/stamps.txt; exit 1; }
+rocm-smi --showclocks >> $O/clocks.txt 2>&1 || true
+cat $O/floor.txt $O/step.txt; grep -v amdgpu.ids $O/stamps.txt | cut -c1-400
+}
+
 "$@"
