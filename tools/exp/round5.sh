@@ -81,4 +81,13 @@ rocm-smi --showclocks >> $O/clocks.txt 2>&1 || true
 cat $O/floor.txt $O/step.txt; grep -v amdgpu.ids $O/stamps.txt | cut -c1-400
 }
 
+r5j() {
+# phase-A time over a long run (clock / power ramp?), with the SMU's view before and after
+O=gpurun_out/r5j_$(date +%H%M%S); mkdir -p $O
+rocm-smi --showclocks --showpower > $O/smi_before.txt 2>&1 || true
+timeout -k 10 300 python3 -u tools/exp/ramp.py 400 > $O/ramp.txt 2>&1 || { cat $O/ramp.txt; exit 1; }
+rocm-smi --showclocks --showpower > $O/smi_after.txt 2>&1 || true
+grep -v amdgpu.ids $O/ramp.txt; grep -i "mclk\|fclk\|sclk\|socclk\|Power" $O/smi_before.txt $O/smi_after.txt | head -20
+}
+
 "$@"
