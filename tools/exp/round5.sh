@@ -90,4 +90,13 @@ rocm-smi --showclocks --showpower > $O/smi_after.txt 2>&1 || true
 grep -v amdgpu.ids $O/ramp.txt; grep -i "mclk\|fclk\|sclk\|socclk\|Power" $O/smi_before.txt $O/smi_after.txt | head -20
 }
 
+r5k() {
+# config 5's partition / inverse passes with one LDS word per staged row (pass 1) and the run bases
+# folded into one array (pass 1, inverse passes): A/B against the previous build, then window parity
+O=gpurun_out/r5k; mkdir -p $O
+timeout -k 10 400 python3 tools/exp/win_ab.py --rounds 2 libqeh_wbase.so libqeh.so > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
+run_tests $O/tests.txt tests/test_window_msd.py
+}
+
 "$@"
