@@ -390,6 +390,37 @@ int qeh_fused_items_build(qeh_ctx *ctx, void *handle, const qeh_column *build_ke
 int qeh_fused_items_finish(qeh_ctx *ctx, void *handle, const uint32_t *items, uint64_t span, const uint32_t *offs,
                            int n_regions, int64_t n_groups, double *lanes);
 int qeh_fused_items_abort(qeh_ctx *ctx, void *handle);
+/* The items form of the shuffle join (BASELINE config 4, hash-partitioned join + aggregate; replaces
+ * the two-pass filter + exchange and the receiving rank's own pipeline over (key, value) rows for the
+ * shapes qeh_fused_items_check accepts).  The partition function: a fact or dimension row with join
+ * key k goes to rank ((k - kmin) >> 16) % world, kmin = the job-wide dimension key minimum -- a
+ * modulo hash of the key's 2^16-key slice, so both sides of every key meet on one rank.
+ *   qeh_shuffle_items_begin: as qeh_fused_items_begin (plan from the gathered stats rows, phase A
+ *     queued over this rank's fact shard, no host wait), with the regions laid out per destination.
+ *   qeh_fused_items_build: this rank's dimension items, all-gathered by the caller as for the
+ *     broadcast items form (phase B takes each of its slices' rows from every rank's spans).
+ *   qeh_shuffle_items_pack: waits for phase A; *ok = 0 (nothing allocated) when the plan declined, a
+ *     region filled up or a kernel failed -- every rank must then learn it (the caller gathers the flag)
+ *     and take the two-pass path.  Else packs each destination q's regions into one block: keys
+ *     (*keys)[q * blockcap ..] and values (*vals)[q * blockcap ..], totals[q] items (region counts
+ *     rounded up to 2), and the block's region counts (*counts)[q * block_regions .. + block_regions],
+ *     all library-owned until qeh_shuffle_items_finish returns.
+ *   (caller: all-to-all of the totals[q] keys and values of block q to rank q, source-major on the
+ *   receiver; all-to-all of the block_regions counts)
+ *   qeh_shuffle_items_finish: phase B over the received blocks (keys / vals / counts as the
+ *     all-to-all left them, source q's items from src_offsets[q], world entries, host memory) with
+ *     this rank's slices built from the gathered dimension items (n_regions spans of `span`, as
+ *     qeh_fused_items_finish), then the dense final stage's lanes ((1 + n_aggs) * n_groups + 1
+ *     doubles, the last = the status lane: a key on two ranks, an overflow); frees the handle.
+ *   qeh_fused_items_abort frees a handle that does not finish. */
+int qeh_shuffle_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                            const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev,
+                            int world, int rank, int row_len, void **handle);
+int qeh_shuffle_items_pack(qeh_ctx *ctx, void *handle, uint16_t **keys, int64_t **vals, uint32_t **counts,
+                           uint64_t *blockcap, int64_t *block_regions, int64_t *totals, int *ok);
+int qeh_shuffle_items_finish(qeh_ctx *ctx, void *handle, const uint16_t *keys, const int64_t *vals,
+                             const uint32_t *counts, const int64_t *src_offsets, const uint32_t *items, uint64_t span,
+                             const uint32_t *offs, int n_regions, int64_t n_groups, double *lanes);
 /* qeh_dense_states_take that also returns the status lane after the (1 + n_vals) * range lanes (the
  * no-wait forms' flag) in *status, from the same host read as the group count. */
 int qeh_dense_states_take_status(qeh_ctx *ctx, const double *in, int n_vals, int64_t key_min, int64_t range,

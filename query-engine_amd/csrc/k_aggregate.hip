@@ -316,7 +316,19 @@ struct SliceRegions {
     // exact layout (materialising join): region (workgroup r, slice b) starts at
     // rbase[b * grid + r] (slice-major, no gaps) instead of (r * F + b) * cap
     const uint64_t *rbase;
+    // partitioned layout (the shuffle join's items form, pw > 0 ranks). Phase A: region (w, b) is number
+    // part_region(b, w), slice-major with the slices of one destination rank (b % pw) together -- rank q's
+    // regions are one contiguous block. Phase B: the packed regions received from pw ranks, local slice
+    // j (global slice j * pw + prank) region (q, w) numbered (q * S + j) * pgrid + w, at rbase[number].
+    int32_t pw;
+    int32_t prank;
+    int32_t pgrid;
 };
+// the partitioned layout's slices per rank and a region's number (phase A, pw > 0)
+__host__ __device__ __forceinline__ int part_slices(int F, int pw) { return (F + pw - 1) / pw; }
+__host__ __device__ __forceinline__ uint64_t part_region(int b, int w, int F, int pw, int grid) {
+    return ((uint64_t)(b % pw) * part_slices(F, pw) + (uint64_t)(b / pw)) * grid + w;
+}
 
 
 // Phase A's shape when it is planned on the device (the prelaunch ahead of the build reads the build
@@ -339,6 +351,7 @@ struct SlicePlanIn {
     int32_t n_slots;
     int32_t sparse_ok;     // direct_table_ok's sparse rule enabled
     int32_t chunk;         // items per flushed chunk (regions are whole chunks); 0 = kSliceChunk
+    int32_t world;         // > 1: the partitioned layout's regions (F rounded up to a multiple of world)
 };
 __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t kmn, int64_t kmx, int64_t kcnt, int64_t gmn,
                                                  int64_t gmx, int64_t gcnt) {
@@ -359,7 +372,8 @@ __host__ __device__ inline SlicePlan plan_slices(const SlicePlanIn &pi, int64_t 
     p.range = range;
     p.F = (int32_t)F;
     const uint64_t ch = pi.chunk > 0 ? (uint64_t)pi.chunk : (uint64_t)kSliceChunk;
-    p.cap = pi.alloc_items / ((uint64_t)pi.grid * F) / ch * ch;
+    const uint64_t Fr = pi.world > 1 ? (F + pi.world - 1) / pi.world * pi.world : F;  // regions' slices
+    p.cap = pi.alloc_items / ((uint64_t)pi.grid * Fr) / ch * ch;
     p.ok = p.cap >= ch;
     return p;
 }
@@ -586,7 +600,9 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
             // exact layout: regions start anywhere; chunks stay aligned to absolute multiples
             // of CH items by starting each region h = start % CH placeholder items early (never
             // written) -- whole 64-B key / 256-B value chunks, as with the capacity layout
-            const uint64_t st = rg.rbase ? rg.rbase[(uint64_t)i * gridDim.x + blockIdx.x] : (region0 + i) * cap;
+            const uint64_t st = rg.rbase ? rg.rbase[(uint64_t)i * gridDim.x + blockIdx.x]
+                                : rg.pw ? part_region(i, blockIdx.x, F, rg.pw, gridDim.x) * cap
+                                        : (region0 + i) * cap;
             hd[i] = (uint32_t)(st % CH);
             abase[i] = st - hd[i];
         }
@@ -855,7 +871,8 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
     if (ovf) *rg.overflow = 1u;
     for (int b = tid; b < F; b += NTH) {
         const uint64_t n = (uint64_t)pos[b] + cn[b];
-        rg.count[region0 + b] = (uint32_t)((n < cap ? n : cap) - hd[b]);
+        rg.count[rg.pw ? part_region(b, blockIdx.x, F, rg.pw, gridDim.x) : region0 + b] =
+            (uint32_t)((n < cap ? n : cap) - hd[b]);
     }
 }
 
@@ -913,10 +930,12 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
     __shared__ uint32_t rbase[DIM ? kMaxSliceGrid : 1];  // DIM: where they start (items, < 2^32)
     uint32_t *lcnt = (uint32_t *)lst;
     uint64_t dcap = 0;
+    int Fg = 0;  // DIM: the plan's slices (the partitioned layout's local slices are fewer)
     if constexpr (DIM) {
         const FusedPlan pl = *dim.plan;
         if (!pl.sp.ok) return;
-        rg.F = pl.sp.F, rg.cap = pl.sp.cap;
+        Fg = pl.sp.F;
+        rg.F = rg.pw ? part_slices(pl.sp.F, rg.pw) : pl.sp.F, rg.cap = pl.sp.cap;
         dcap = pl.dcap;
     }
     uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
@@ -959,11 +978,14 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
             for (int i = tid; i < kSliceKeys / 2; i += kSliceBlock) tw[i] = 0u;
             // build-row regions of the slice: one per phase-A workgroup, or (items form) one per rank
             const int dn = dim.nreg ? dim.nreg : nreg;
+            const int bg = rg.pw ? b * rg.pw + rg.prank : b;  // the slice's number in the plan
             for (int r = tid; r < dn; r += kSliceBlock) {
-                if (dim.nreg) {
+                if (bg >= Fg) {
+                    rcnt[r] = 0u, rbase[r] = 0u;  // (a local slice past the plan's last: no rows)
+                } else if (dim.nreg) {
                     const uint32_t *o = dim.offs + (uint64_t)r * 2 * (kSliceMaxF + 1);
-                    rcnt[r] = o[kSliceMaxF + 1 + b];
-                    rbase[r] = (uint32_t)((uint64_t)r * dim.rstride + o[b]);
+                    rcnt[r] = o[kSliceMaxF + 1 + bg];
+                    rbase[r] = (uint32_t)((uint64_t)r * dim.rstride + o[bg]);
                 } else {
                     rcnt[r] = dim.count[(uint64_t)r * F + b];
                     rbase[r] = (uint32_t)(((uint64_t)r * F + b) * dcap);
@@ -1025,11 +1047,19 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
         }
         __syncthreads();
         for (int64_t s = sb + wave; s < se; s += W) {
-            const uint64_t reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
+            uint64_t reg, rb;
+            if (rg.pw) {  // packed regions received from the ranks: (source q, workgroup w) of local slice b
+                const int64_t r = s - (int64_t)b * nreg, q = r / rg.pgrid;
+                reg = ((uint64_t)q * F + b) * rg.pgrid + (uint64_t)(r - q * rg.pgrid);
+                rb = rg.rbase[reg];
+            } else {
+                reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
+                rb = reg * rg.cap;
+            }
             const uint32_t n_r = rg.count[reg];
-            const uint16_t *kp = rg.key + reg * rg.cap;
-            const int64_t *vp = VC ? rg.val + reg * rg.cap : nullptr;
-            const int64_t *vp2 = NACOL > 1 ? rg.val2 + reg * rg.cap : nullptr;
+            const uint16_t *kp = rg.key + rb;
+            const int64_t *vp = VC ? rg.val + rb : nullptr;
+            const int64_t *vp2 = NACOL > 1 ? rg.val2 + rb : nullptr;
             uint32_t en[8];
             int64_t vn[8], vn2[NACOL > 1 ? 8 : 1];
             // item of register j (the masks below use the same map)
@@ -4318,12 +4348,16 @@ struct FusedItems {
     AggSpecs specs{};
     int nacol = 0, grid = 0;
     int64_t Gs = 0;
+    // the shuffle join's items form (pw > 0): phase A in the partitioned layout, the packed send blocks
+    int pw = 0, prank = 0, S = 0;
+    uint64_t blockcap = 0;
+    DevBuf pkey, pval, pcnt, prb, ptot, rrb, roff;
 };
 
 // begin's checks (check_only: nothing allocated or launched -- the caller's agreement flag)
 static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
                              const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev,
-                             int world, int row_len, void **handle, bool check_only) {
+                             int world, int row_len, void **handle, bool check_only, int pw = 0, int prank = 0) {
     if (!ctx || (!check_only && (!handle || !stats_dev || world < 1 || row_len < 6)) || n_aggs < 1 || n_probe_cols < 1 ||
         probe_key_idx < 0 || probe_key_idx >= n_probe_cols)
         return fail(QEH_E_INVALID, "qeh_fused_items_begin: bad argument");
@@ -4366,7 +4400,10 @@ static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_p
     pi.sparse_ok = direct_sparse_allowed() ? 1 : 0;
     pi.chunk = chunk;
     pi.alloc_items = tiles_per_wg * fi->grid * (uint64_t)tile_rows * 5 / 4 + (uint64_t)fi->grid * kSliceMaxF * (256 + 2 * chunk);
-    const uint64_t nreg_max = (uint64_t)fi->grid * kSliceMaxF;
+    pi.world = pw;
+    const uint64_t nreg_max = (uint64_t)fi->grid * (kSliceMaxF + (pw > 1 ? pw : 0));
+    fi->pw = pw, fi->prank = prank;
+    fi->rg.pw = pw, fi->rg.prank = prank;
     QEH_TRY(fi->plan.alloc(ctx, sizeof(FusedPlan)));
     QEH_TRY(fi->kbuf.alloc(ctx, pi.alloc_items * 2 + 64));
     if (fi->nacol) QEH_TRY(fi->vbuf.alloc(ctx, pi.alloc_items * 8 + 64));
@@ -4473,6 +4510,181 @@ extern "C" int qeh_fused_items_abort(qeh_ctx *ctx, void *handle) {
     DeviceGuard dg(ctx->device);
     std::unique_ptr<FusedItems> fi((FusedItems *)handle);
     QEH_HIP(hipStreamSynchronize(ctx->stream));  // its phase A may still be running
+    return QEH_OK;
+}
+
+// ---- the items form of the shuffle join (BASELINE config 4: hash-partitioned join + aggregate) ----
+// Each rank runs the fused pipeline's phase A over ITS fact shard in the partitioned layout -- the
+// join key's slice b = (k - kmin) >> 16 decides the rank, b % world (the partition function: a modulo
+// hash of the key's slice, so every key's fact and dimension rows meet on one rank) -- packs each
+// destination's regions (10-B items: 16-bit key offset + value) into one block, and the all-to-all moves
+// the blocks; the receiving rank runs phase B over what every rank sent it, with its slices' LDS
+// entries built from the all-gathered dimension items (qeh_fused_items_build), and writes the dense
+// final stage's lanes.  Per fact row: phase A's 24 B read + 10 B per selected row written, the pack's
+// 10 + 10 B, phase B's 10 B read -- instead of the two-pass exchange (42 B) plus a local pipeline over
+// the received (key, value) rows (16 B read, 10 + 10 B of its own items).
+
+// Exclusive scan of each block's region counts (rounded up to 2: phase B's pair loads), written as
+// absolute region starts base(q) + prefix; base(q) = bases[q], or q * blockcap without bases.  With
+// F > 0 (the sender), counts of slices past the plan's last (j * pw + q >= F: never written by phase A)
+// are taken as 0 and the cleaned counts go to cnt_out; totals[q] = the block's items.
+__global__ __launch_bounds__(1024) void k_region_scan(const uint32_t *__restrict__ cnt, int64_t E, const int64_t *bases,
+                                                      uint64_t blockcap, int F, int pw, int grid,
+                                                      uint64_t *__restrict__ rbase, uint32_t *__restrict__ cnt_out,
+                                                      int64_t *__restrict__ totals) {
+    __shared__ uint64_t wsum[16];
+    const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t base = bases ? (uint64_t)bases[q] : (uint64_t)q * blockcap;
+    const int64_t per = (E + 1023) / 1024, e0 = (int64_t)t * per, e1 = e0 + per < E ? e0 + per : E;
+    auto count = [&](int64_t e) -> uint32_t {
+        if (F > 0 && (int64_t)(e / grid) * pw + q >= F) return 0u;
+        return cnt[(uint64_t)q * E + e];
+    };
+    uint64_t tot = 0;
+    for (int64_t e = e0; e < e1; ++e) tot += (count(e) + 1u) & ~1u;
+    uint64_t incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t a = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += a;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t run = incl - tot;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    for (int64_t e = e0; e < e1; ++e) {
+        const uint32_t c = count(e);
+        rbase[(uint64_t)q * E + e] = base + run;
+        if (cnt_out) cnt_out[(uint64_t)q * E + e] = c;
+        run += (c + 1u) & ~1u;
+    }
+    if (totals && t == 1023) totals[q] = (int64_t)run;  // (the last thread's run ends the block)
+}
+
+// Region r's items (count cnt[r], padded to 2) from the phase-A layout (r * cap) to rbase[r]: one
+// workgroup per region, key pairs as 4-B words, value pairs as 16-B words.
+__global__ __launch_bounds__(256) void k_region_pack(const uint16_t *__restrict__ kin, const int64_t *__restrict__ vin,
+                                                     const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ rbase,
+                                                     uint64_t cap, uint16_t *__restrict__ kout, int64_t *__restrict__ vout) {
+    const uint64_t r = blockIdx.x;
+    const uint32_t c2 = (cnt[r] + 1u) >> 1;  // item pairs
+    const uint32_t *ks = (const uint32_t *)(kin + r * cap);
+    uint32_t *kd = (uint32_t *)(kout + rbase[r]);
+    const v2i64 *vs = (const v2i64 *)(vin + r * cap);
+    v2i64 *vd = (v2i64 *)(vout + rbase[r]);
+    for (uint32_t i = threadIdx.x; i < c2; i += 256) {
+        __builtin_nontemporal_store(__builtin_nontemporal_load(ks + i), kd + i);
+        if (vin) __builtin_nontemporal_store(__builtin_nontemporal_load(vs + i), vd + i);
+    }
+}
+
+extern "C" int qeh_shuffle_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_probe_cols, int probe_key_idx,
+                                       const qeh_expr *predicate, const qeh_agg *aggs, int n_aggs, const int64_t *stats_dev,
+                                       int world, int rank, int row_len, void **handle) {
+    if (world < 2 || world > 64 || rank < 0 || rank >= world)
+        return fail(QEH_E_INVALID, "qeh_shuffle_items_begin: bad argument (2..64 ranks)");
+    return fused_items_begin(ctx, probe_cols, n_probe_cols, probe_key_idx, predicate, aggs, n_aggs, stats_dev, world, row_len,
+                             handle, false, world, rank);
+}
+
+extern "C" int qeh_shuffle_items_pack(qeh_ctx *ctx, void *handle, uint16_t **keys, int64_t **vals, uint32_t **counts,
+                                      uint64_t *blockcap, int64_t *block_regions, int64_t *totals, int *ok) {
+    if (!ctx || !handle || !keys || !vals || !counts || !blockcap || !block_regions || !totals || !ok)
+        return fail(QEH_E_INVALID, "qeh_shuffle_items_pack: bad argument");
+    FusedItems *fi = (FusedItems *)handle;
+    if (fi->pw < 2) return fail(QEH_E_INVALID, "qeh_shuffle_items_pack: not a shuffle handle");
+    DeviceGuard dg(ctx->device);
+    *ok = 0;
+    FusedPlan pl;
+    uint32_t sw[8];
+    QEH_TRY(read_small(ctx, &pl, fi->plan.p, sizeof(FusedPlan)));  // (waits for phase A)
+    QEH_TRY(read_small(ctx, sw, fi->errw.p, 32));
+    for (int q = 0; q < fi->pw; ++q) totals[q] = 0;
+    *keys = nullptr, *vals = nullptr, *counts = nullptr, *blockcap = 0, *block_regions = 0;
+    if (!pl.sp.ok || sw[0] || sw[1]) return QEH_OK;  // declined plan, kernel error or a full region: *ok = 0
+    const int pw = fi->pw, grid = fi->grid;
+    fi->S = part_slices(pl.sp.F, pw);
+    const int64_t E = (int64_t)fi->S * grid, P = E * pw;
+    fi->blockcap = (uint64_t)E * pl.sp.cap;
+    QEH_TRY(fi->pkey.alloc(ctx, (fi->blockcap * pw + 4) * 2));
+    if (fi->nacol) QEH_TRY(fi->pval.alloc(ctx, (fi->blockcap * pw + 4) * 8));
+    QEH_TRY(fi->pcnt.alloc(ctx, (size_t)P * 4));
+    QEH_TRY(fi->prb.alloc(ctx, (size_t)P * 8));
+    QEH_TRY(fi->ptot.alloc(ctx, (size_t)pw * 8));
+    {
+        KernelTimer kt(ctx, "shuffle_pack");
+        hipLaunchKernelGGL(k_region_scan, dim3(pw), dim3(1024), 0, ctx->stream, fi->cbuf.as<uint32_t>(), E,
+                           (const int64_t *)nullptr, fi->blockcap, pl.sp.F, pw, grid, fi->prb.as<uint64_t>(),
+                           fi->pcnt.as<uint32_t>(), fi->ptot.as<int64_t>());
+        hipLaunchKernelGGL(k_region_pack, dim3((unsigned)P), dim3(256), 0, ctx->stream, fi->kbuf.as<uint16_t>(),
+                           fi->nacol ? fi->vbuf.as<int64_t>() : nullptr, fi->pcnt.as<uint32_t>(), fi->prb.as<uint64_t>(),
+                           pl.sp.cap, fi->pkey.as<uint16_t>(), fi->nacol ? fi->pval.as<int64_t>() : nullptr);
+    }
+    QEH_HIP(hipGetLastError());
+    QEH_TRY(read_small(ctx, totals, fi->ptot.p, (size_t)pw * 8));
+    *keys = fi->pkey.as<uint16_t>();
+    *vals = fi->nacol ? fi->pval.as<int64_t>() : nullptr;
+    *counts = fi->pcnt.as<uint32_t>();
+    *blockcap = fi->blockcap;
+    *block_regions = E;
+    *ok = 1;
+    return QEH_OK;
+}
+
+extern "C" int qeh_shuffle_items_finish(qeh_ctx *ctx, void *handle, const uint16_t *keys, const int64_t *vals,
+                                        const uint32_t *counts, const int64_t *src_offsets, const uint32_t *items,
+                                        uint64_t span, const uint32_t *offs, int n_regions, int64_t n_groups,
+                                        double *lanes) {
+    if (!ctx || !handle || !keys || !counts || !src_offsets || !items || !offs || !lanes || n_regions < 1 ||
+        n_regions > kMaxSliceGrid || n_groups < 1 || (span & 3) || (uint64_t)n_regions * span >= (1ull << 32))
+        return fail(QEH_E_INVALID, "qeh_shuffle_items_finish: bad argument");
+    std::unique_ptr<FusedItems> fi((FusedItems *)handle);  // freed here: its buffers' users are queued ahead
+    DeviceGuard dg(ctx->device);
+    if (fi->pw < 2 || fi->S < 1) return fail(QEH_E_INVALID, "qeh_shuffle_items_finish: pack did not run");
+    if (n_groups > fi->Gs) return fail(QEH_E_UNSUPPORTED, "qeh_shuffle_items_finish: more groups than the states hold");
+    if (fi->nacol && !vals) return fail(QEH_E_INVALID, "qeh_shuffle_items_finish: the values are missing");
+    const int pw = fi->pw, grid = fi->grid;
+    const int64_t E = (int64_t)fi->S * grid, P = E * pw;
+    uint32_t *st = fi->errw.as<uint32_t>();
+    QEH_TRY(fi->roff.alloc(ctx, (size_t)pw * 8));
+    QEH_TRY(fi->rrb.alloc(ctx, (size_t)P * 8));
+    QEH_HIP(hipMemcpyAsync(fi->roff.p, src_offsets, (size_t)pw * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_region_scan, dim3(pw), dim3(1024), 0, ctx->stream, counts, E, fi->roff.as<int64_t>(), (uint64_t)0,
+                       0, pw, grid, fi->rrb.as<uint64_t>(), (uint32_t *)nullptr, (int64_t *)nullptr);
+    SliceRegions rg{};
+    rg.key = (uint16_t *)keys;
+    rg.val = (int64_t *)vals;
+    rg.count = (uint32_t *)counts;
+    rg.overflow = st + 1;
+    rg.rbase = fi->rrb.as<uint64_t>();
+    rg.pw = pw, rg.prank = fi->prank, rg.pgrid = grid;
+    {
+        KernelTimer ktb(ctx, "slice_probe");
+        DimSlices dim{items, nullptr, st + 4, fi->plan.as<FusedPlan>(), n_regions, 0, span, offs};
+        const int gridB = ctx->props.multiProcessorCount;
+        const HashTable t{};
+        const bool pf = slice_probe_prefetch();
+        const int nreg = pw * grid;
+        if (fi->nacol == 0) {
+            if (pf) hipLaunchKernelGGL((k_slice_probe<0, false, true, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                       rg, nreg, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+            else hipLaunchKernelGGL((k_slice_probe<0, false, false, false, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                    rg, nreg, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+        } else {
+            if (pf) hipLaunchKernelGGL((k_slice_probe<1, false, true, true, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                       rg, nreg, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+            else hipLaunchKernelGGL((k_slice_probe<1, false, false, true, true>), dim3(gridB), dim3(kSliceBlock), 0, ctx->stream,
+                                    rg, nreg, 0, t, fi->in, fi->specs, fi->Gs, fi->states.as<uint64_t>(), dim);
+        }
+    }
+    QEH_HIP(hipGetLastError());
+    const int64_t ne = (int64_t)(1 + fi->specs.n) * n_groups;
+    hipLaunchKernelGGL(k_states_lanes, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, ctx->stream,
+                       (const uint64_t *)fi->states.as<uint64_t>(), fi->Gs, n_groups, fi->specs, lanes, (const uint32_t *)st, 1);
+    QEH_HIP(hipGetLastError());
+    // the handle's buffers (phase A's regions, the packed blocks) are freed when this returns: the
+    // caller's collectives that read the packed blocks were issued before this call on its stream
+    QEH_HIP(hipStreamSynchronize(ctx->stream));
     return QEH_OK;
 }
 

@@ -103,6 +103,10 @@ SIGNATURES = {
     "qeh_fused_items_build": (I, [P, P, COLP, COLP, I, U64, P, P]),
     "qeh_fused_items_finish": (I, [P, P, P, U64, P, I, I64, P]),
     "qeh_fused_items_abort": (I, [P, P]),
+    "qeh_shuffle_items_begin": (I, [P, COLP, I, I, EXPRP, AGGP, I, P, I, I, I, C.POINTER(P)]),
+    "qeh_shuffle_items_pack": (I, [P, P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(U64), C.POINTER(I64),
+                                   C.POINTER(I64), C.POINTER(I)]),
+    "qeh_shuffle_items_finish": (I, [P, P, P, P, P, C.POINTER(I64), P, U64, P, I, I64, P]),
     "qeh_fused_items_check": (I, [P, COLP, I, I, EXPRP, AGGP, I]),
     "qeh_join_filter_aggregate_prelaunch_stats": (I, [P, COLP, I, I, EXPRP, AGGP, I, P, I, I]),
     "qeh_sort_indices": (I, [P, COLP, I, C.POINTER(C.c_int8), COLP]),

@@ -550,6 +550,42 @@ class Context:
     def fused_items_abort(self, handle: int) -> None:
         abi.check(self.lib.qeh_fused_items_abort(self.h, handle))
 
+    def shuffle_items_begin(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
+                            predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]], stats_ptr: int,
+                            world: int, rank: int, row_len: int) -> int:
+        """qeh_shuffle_items_begin: the shuffle join's items form -- plan from the gathered stats rows and
+        phase A over this rank's fact shard in the per-destination layout, queued; returns the handle."""
+        cp = self._cols(probe_cols)
+        ca = (abi.QehAgg * max(len(aggs), 1))(*[abi.QehAgg(f, c) for f, c in aggs])
+        e = keep = None
+        if predicate is not None:
+            e, keep = predicate.to_c()
+        h = C.c_void_p()
+        abi.check(self.lib.qeh_shuffle_items_begin(self.h, cp, len(probe_cols), probe_key_idx,
+                                                   C.byref(e) if e is not None else None, ca, len(aggs), stats_ptr,
+                                                   world, rank, row_len, C.byref(h)))
+        return h.value
+
+    def shuffle_items_pack(self, handle: int, world: int):
+        """qeh_shuffle_items_pack: (ok, keys_ptr, vals_ptr, counts_ptr, blockcap, block_regions, totals[world])
+        -- each destination's packed block (library-owned until shuffle_items_finish)."""
+        kp, vp, cp = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        bc, br, ok = C.c_uint64(), C.c_int64(), C.c_int()
+        tot = (C.c_int64 * world)()
+        abi.check(self.lib.qeh_shuffle_items_pack(self.h, handle, C.byref(kp), C.byref(vp), C.byref(cp), C.byref(bc),
+                                                  C.byref(br), tot, C.byref(ok)))
+        return (bool(ok.value), kp.value or 0, vp.value or 0, cp.value or 0, bc.value, br.value,
+                np.array(tot[:], np.int64))
+
+    def shuffle_items_finish(self, handle: int, keys_ptr: int, vals_ptr: int, counts_ptr: int, src_offsets,
+                             items_ptr: int, span: int, offs_ptr: int, n_regions: int, n_groups: int,
+                             lanes_ptr: int) -> None:
+        """qeh_shuffle_items_finish: phase B over the received blocks (source q's items from
+        src_offsets[q]) with the gathered dimension spans, then the lanes (status last)."""
+        so = (C.c_int64 * len(src_offsets))(*[int(x) for x in src_offsets])
+        abi.check(self.lib.qeh_shuffle_items_finish(self.h, handle, keys_ptr, vals_ptr or None, counts_ptr, so,
+                                                    items_ptr, span, offs_ptr, n_regions, n_groups, lanes_ptr))
+
     def join_filter_aggregate_prelaunch_stats(self, probe_cols: Sequence[DeviceColumn], probe_key_idx: int,
                                               predicate: Optional[PhysicalExpr], aggs: Sequence[Tuple[int, int]],
                                               stats_ptr: int, world: int, row_len: int) -> None:

@@ -122,9 +122,13 @@ def _a2a_rounds(pin: Sequence[int], pout: Sequence[int], me: int, row_bytes: int
     return rounds
 
 
-def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], peak: int, group=None) -> torch.Tensor:
+def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], peak: int, group=None,
+                istarts: Optional[Sequence[int]] = None, pad: int = 0) -> torch.Tensor:
     """Variable all-to-all of one partition-major payload: pin[r] leading rows go to rank r,
-    pout[r] rows arrive from rank r; peak = _peak_remote of the job-wide split matrix.  The local partition never goes through the collective
+    pout[r] rows arrive from rank r; peak = _peak_remote of the job-wide split matrix.  With
+    `istarts`, rank r's rows are p[istarts[r] : istarts[r] + pin[r]] instead (per-destination blocks
+    at fixed places, as qeh_shuffle_items_pack leaves them); `pad` rows of slack after the received
+    rows (world > 1).  The local partition never goes through the collective
     (one copy, or the input itself at world size 1); the remote partitions move in the rounds of
     _a2a_rounds (at most A2A_CHUNK_BYTES per peer each).  Only the collective of a round depends on
     the backend: under "nccl" grouped send/recv of the views (dist.all_to_all over views,
@@ -133,11 +137,14 @@ def _all_to_all(p: torch.Tensor, pin: Sequence[int], pout: Sequence[int], peak: 
     world = len(pin)
     me = dist.get_rank(group)
     if world == 1:
+        if istarts is not None:
+            p = p[int(istarts[0]):int(istarts[0]) + int(pin[0])]
         return p if p.is_contiguous() else p.contiguous()
     p = p.contiguous()
     shape = tuple(p.shape[1:])
-    out = torch.empty((sum(pout),) + shape, dtype=p.dtype, device=p.device)
-    ioff = np.concatenate([[0], np.cumsum(pin)]).astype(np.int64)
+    out = torch.empty((sum(pout) + pad,) + shape, dtype=p.dtype, device=p.device)
+    ioff = np.concatenate([[0], np.cumsum(pin)]).astype(np.int64) if istarts is None else \
+        np.asarray([int(x) for x in istarts], np.int64)
     ooff = np.concatenate([[0], np.cumsum(pout)]).astype(np.int64)
     if pin[me]:
         out[ooff[me]:ooff[me] + pout[me]].copy_(p[ioff[me]:ioff[me] + pin[me]])
@@ -984,6 +991,12 @@ class DistributedExecutor:
             if g == 0:
                 pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
             return self._final(pk, pa_, aggs)
+        if self.device == "cuda" and len(build_group_keys) == 1 and not os.environ.get("QEH_NO_ITEMS_SHUFFLE"):
+            out = self._shuffle_items(probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs)
+            if out is not None:
+                self.last_shuffle = "items"
+                return out
+        self.last_shuffle = "two_pass"
         need = sorted({probe_key_idx} | {c for _, c in aggs})
         remap = {c: i for i, c in enumerate(need)}
         pcounts = None
@@ -1012,6 +1025,111 @@ class DistributedExecutor:
         if g == 0:
             pk, pa_ = self._empty_partials(build_group_keys, probe_cols, aggs)
         return self._final(pk, pa_, aggs)
+
+    def _shuffle_items(self, probe_cols, probe_key_idx, predicate, build_key, build_group_keys, aggs):
+        """The items form of the shuffle join (include/qeh.h qeh_shuffle_items_*): every rank runs the fused
+        pipeline's phase A over its fact shard with the regions laid out per destination rank -- the
+        partition function is ((k - kmin) >> 16) % world, a modulo hash of the join key's 2^16-key slice --
+        packs each destination's regions into one block of 10-B items (16-bit key offset, value), and one
+        all-to-all per payload moves the blocks; each rank's phase B aggregates what it received against
+        its slices' dimension rows (all-gathered as 4-B items, as the broadcast items form does) into the
+        dense final stage's lanes.  The receiving rank needs no pipeline of its own over (key, value)
+        rows, and the wire carries 10 B per selected fact row instead of 16.  Decided from gathered
+        values only; a declined plan or an overflow on any rank (gathered with the block totals), or a
+        key on two ranks (the status lane), returns None on every rank (the two-pass form follows)."""
+        if (len(build_group_keys) != 1 or build_key.dtype != abi.DT_INT64
+                or build_group_keys[0].dtype not in (abi.DT_INT64, abi.DT_INT32)
+                or any(f not in (AF.Count, AF.Sum) for f, _ in aggs)):
+            return None
+        gkc = build_group_keys[0]
+        W, me = self.world, self.rank
+        local_ok = 1 if self.ctx.fused_items_check(probe_cols, probe_key_idx, predicate, aggs) else 0
+        bitmap = 1 if (build_key.c.validity or gkc.c.validity) else 0
+        row_len = 7  # [rows, key min, max, group key min, max, has-bitmap, shape ok]
+        row = torch.empty(row_len, dtype=torch.int64, device="cuda")
+        self._sync_torch()
+        self.ctx.broadcast_stats(build_key, gkc, [bitmap, local_ok], row.data_ptr())
+        self._sync()
+        out = torch.empty(W * row_len, dtype=torch.int64, device="cuda")
+        dist.all_gather_into_tensor(out, row, group=self.group)
+        row = out
+        pinned = getattr(self, "_shuffle_pinned", None)
+        if pinned is None or pinned.numel() != row.numel():
+            pinned = self._shuffle_pinned = torch.empty(row.numel(), dtype=torch.int64, pin_memory=True)
+        pinned.copy_(row, non_blocking=True)  # queued ahead of phase A
+        copied = torch.cuda.Event()
+        copied.record()
+        handle = None
+        if local_ok:
+            self._sync_torch()
+            handle = self.ctx.shuffle_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(), W, me,
+                                                  row_len)
+        copied.synchronize()
+        M = pinned.numpy().reshape(W, row_len).copy()
+        live = M[M[:, 0] > 0]
+        n_sum = sum(1 for f, _ in aggs if f == AF.Sum)
+        ok = bool(M[:, 6].min() == 1 and M[:, 5].max() == 0 and int(M[:, 0].sum()) > 0)
+        if ok:
+            kmin, kmax = int(live[:, 1].min()), int(live[:, 2].max())
+            gmin, gmax = int(live[:, 3].min()), int(live[:, 4].max())
+            R, G = kmax - kmin + 1, gmax - gmin + 1
+            F = (R + (1 << 16) - 1) >> 16
+            ok = (1 <= F <= self.ITEMS_SLICES and G * (1 + n_sum) <= self.ITEMS_STATE_WORDS
+                  and 2 * R >= self.ITEMS_MIN_TABLE_BYTES)
+        if not ok:
+            if handle is not None:
+                self.ctx.fused_items_abort(handle)
+            return None
+        # this rank's dimension rows grouped by slice, all-gathered (every rank builds only its own slices)
+        nb, span = self.ctx.fused_items_shape(int(M[:, 0].max()), W)
+        OW = 2 * (self.ITEMS_SLICES + 1)
+        items = torch.empty(nb * span, dtype=torch.int32, device="cuda")
+        offs = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        self._sync_torch()
+        self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
+        # phase A's regions packed per destination (waits for phase A); the flag and the block totals of
+        # every rank in one all-gather
+        pk_ok, kp, vp, cp, blockcap, E, totals = self.ctx.shuffle_items_pack(handle, W)
+        meta = torch.tensor(list(totals) + [1 if pk_ok else 0], dtype=torch.int64, device="cuda")
+        Mt = _allgather_meta_t(meta, W, self.group)
+        if int(Mt[:, W].min()) == 0:
+            self.ctx.fused_items_abort(handle)
+            return None
+        gi = torch.empty(W * nb * span, dtype=torch.int32, device="cuda")
+        go = torch.empty(W * nb * OW, dtype=torch.int32, device="cuda")
+        dist.all_gather_into_tensor(gi, items, group=self.group)
+        dist.all_gather_into_tensor(go, offs, group=self.group)
+        pin, pout = [int(x) for x in Mt[me, :W]], [int(x) for x in Mt[:, me]]
+        peak = _peak_remote(Mt[:, :W])
+        starts = [q * blockcap for q in range(W)]
+        nacol = vp != 0
+        # (received keys / values with slack: phase B's pair loads may read one item past a count; the
+        # 16-bit keys travel as 32-bit pairs -- every block and total is even -- which gloo also carries)
+        keys_t = torch.as_tensor(_DeviceView(kp, W * blockcap // 2, "<i4", handle))
+        rk = _all_to_all(keys_t, [c // 2 for c in pin], [c // 2 for c in pout], peak // 2, self.group,
+                         [x // 2 for x in starts], pad=2)
+        rv = None
+        if nacol:
+            vals_t = torch.as_tensor(_DeviceView(vp, W * blockcap, "<i8", handle))
+            rv = _all_to_all(vals_t, pin, pout, peak, self.group, starts, pad=4)
+        cnt_t = torch.as_tensor(_DeviceView(cp, W * E, "<i4", handle))
+        rc = _all_to_all(cnt_t, [E] * W, [E] * W, E, self.group)
+        src_off = np.concatenate([[0], np.cumsum(pout)[:-1]]).astype(np.int64)
+        nl = (1 + len(aggs)) * G + 1
+        lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
+        self._sync_torch()
+        self.ctx.shuffle_items_finish(handle, rk.data_ptr(), rv.data_ptr() if rv is not None else 0, rc.data_ptr(),
+                                      src_off, gi.data_ptr(), span, go.data_ptr(), W * nb, G, lanes.data_ptr())
+        self._sync()
+        dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
+        self._sync_torch()
+        got, ov, g, bad = self.ctx.dense_states_take_status(
+            lanes.data_ptr(), len(aggs), gmin, G, W, me, gkc.dtype,
+            [abi.DT_INT64 if f == AF.Count else abi.DT_FLOAT64 for f, _ in aggs])
+        if bad != 0.0:
+            return None
+        self.last_final = "dense"
+        return [got], ov, g
 
     def _moved_shuffle_ok(self, part_keys, cols) -> bool:
         """The fused window shuffle applies: one non-null 16-B aligned Int64 PARTITION BY key, every

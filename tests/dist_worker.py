@@ -360,6 +360,9 @@ def check_metric_plans(rank, world, dx, ctx):
                                     [ob.HostCol(DG)], aggs)
     keys, aggs_out, ng = dx.join_filter_aggregate_shuffle([ctx.upload(x), ctx.upload(k), ctx.upload(v)], 1, pred,
                                                           ctx.upload(dk), [ctx.upload(dg)], aggs)
+    if world > 1 and dx.device == "cuda":
+        # the dimension repeats a key (dk_all[11] == dk_all[12]): the items form sees it and falls back
+        assert dx.last_shuffle == "two_pass", dx.last_shuffle
     res = dx.gather_to_root(keys + aggs_out)
     if rank == 0:
         assert_grouped_equal(res[:1], res[1:], want[0], want[1], float_aggs=[0])
@@ -456,6 +459,19 @@ def mode_gpu_devtensors(rank, world):
         if rank == 0:
             assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
     fact = [ctx.upload(x), ctx.upload(kk), ctx.upload(vv)]
+    # config 4's shape: the shuffle join's items form -- phase A per destination on every rank, the packed
+    # blocks exchanged (all-to-all of keys, values and region counts), phase B on the receiving rank --
+    # then the two-pass exchange (QEH_NO_ITEMS_SHUFFLE), both vs the oracle
+    for form in ("items", "two_pass"):
+        if form == "two_pass":
+            os.environ["QEH_NO_ITEMS_SHUFFLE"] = "1"
+        keys, aggs_out, ng = dx.join_filter_aggregate_shuffle(fact, 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+                                                              [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs)
+        os.environ.pop("QEH_NO_ITEMS_SHUFFLE", None)
+        assert dx.last_shuffle == form, (dx.last_shuffle, form)
+        res = dx.gather_to_root(keys + aggs_out)
+        if rank == 0:
+            assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
     # a build key held by two ranks (rank 0 and the last rank) with SUM + COUNT: the no-wait table
     # form sums the two entries to one above G (both group slots >= G / 2), which the table check
     # clears before the probe reads it; the non-empty count then falls short on every rank and every

@@ -844,3 +844,92 @@ def test_items_form_vs_oracle(ctx, ranks, dup):
                                           [ob.HostCol(dg)], AGGS)
     assert len(gk[0][0]) == wg
     assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,dup", [(2, False), (3, False), (8, False), (3, True)])
+def test_shuffle_items_form_vs_oracle(ctx, ranks, dup):
+    """The items form of the shuffle join (qeh_shuffle_items_*, BASELINE config 4) with `ranks` simulated
+    on one device: every rank's phase A over its fact shard in the per-destination layout, its dim items
+    (all-gathered by concatenation), its packed blocks; the all-to-all's stand-in takes block q of every
+    source (source-major) and the region counts to rank q; finish per rank, the lanes summed and taken --
+    the union over ranks equals the oracle's join + filter + group-by.  A build key on two ranks comes
+    back in the status lane."""
+    import torch
+    from qe_hip.distributed import _DeviceView
+    n_fact, n_dim = 3_000_000, 4_000_000
+    x, k, v, dk, dg = metric_data(n_fact, n_dim, 1000)
+    if dup:
+        dk[-3] = dk[2]
+    fb = np.linspace(0, n_fact, ranks + 1).astype(int)
+    db = np.linspace(0, n_dim, ranks + 1).astype(int)
+    S, row_len = 160, 7
+    rows = []
+    for r in range(ranks):
+        row = torch.empty(row_len, dtype=torch.int64, device="cuda")
+        ctx.broadcast_stats(ctx.upload(dk[db[r]:db[r + 1]]), ctx.upload(dg[db[r]:db[r + 1]]), [0, 1], row.data_ptr())
+        rows.append(row)
+    ctx.sync()
+    M = torch.cat(rows)
+    gmin, gmax = int(dg.min()), int(dg.max())
+    G = gmax - gmin + 1
+    nb, span = ctx.fused_items_shape(int(np.diff(db).max()), ranks)
+    OW = 2 * (S + 1)
+    handles, facts, items, offs, packs = [], [], [], [], []
+    for r in range(ranks):
+        fact = [ctx.upload(x[fb[r]:fb[r + 1]]), ctx.upload(k[fb[r]:fb[r + 1]]), ctx.upload(v[fb[r]:fb[r + 1]])]
+        h = ctx.shuffle_items_begin(fact, 1, PRED, AGGS, M.data_ptr(), ranks, r, row_len)
+        it = torch.empty(nb * span, dtype=torch.int32, device="cuda")
+        of = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        ctx.fused_items_build(h, ctx.upload(dk[db[r]:db[r + 1]]), ctx.upload(dg[db[r]:db[r + 1]]), nb, span,
+                              it.data_ptr(), of.data_ptr())
+        ok, kp, vp, cp, bc, E, tot = ctx.shuffle_items_pack(h, ranks)
+        assert ok
+        assert tot.sum() >= 0 and (tot % 2 == 0).all()
+        packs.append((kp, vp, cp, bc, E, tot))
+        handles.append(h), facts.append(fact), items.append(it), offs.append(of)
+    ctx.sync()
+    # the all-to-all's stand-in: block q of every source, source-major (copies: finish frees the handles)
+    recv = []
+    for q in range(ranks):
+        ks, vs, cs, so, off = [], [], [], [], 0
+        for (kp, vp, cp, bc, E, tot) in packs:
+            kt = torch.as_tensor(_DeviceView(kp, ranks * bc, "<i2", None))
+            vt = torch.as_tensor(_DeviceView(vp, ranks * bc, "<i8", None))
+            ct = torch.as_tensor(_DeviceView(cp, ranks * E, "<i4", None))
+            ks.append(kt[q * bc:q * bc + tot[q]].clone())
+            vs.append(vt[q * bc:q * bc + tot[q]].clone())
+            cs.append(ct[q * E:(q + 1) * E].clone())
+            so.append(off)
+            off += int(tot[q])
+        pad16, pad64 = torch.zeros(4, dtype=torch.int16, device="cuda"), torch.zeros(4, dtype=torch.int64, device="cuda")
+        recv.append((torch.cat(ks + [pad16]), torch.cat(vs + [pad64]), torch.cat(cs), so))
+        assert sum(int(c.sum()) for c in cs) <= off
+    torch.cuda.synchronize()
+    gi, go = torch.cat(items), torch.cat(offs)
+    nl = (1 + len(AGGS)) * G + 1
+    total = torch.zeros(nl, dtype=torch.float64, device="cuda")
+    for r in range(ranks):
+        rk, rv, rc, so = recv[r]
+        lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
+        ctx.shuffle_items_finish(handles[r], rk.data_ptr(), rv.data_ptr(), rc.data_ptr(), so, gi.data_ptr(), span,
+                                 go.data_ptr(), ranks * nb, G, lanes.data_ptr())
+        ctx.sync()
+        total += lanes
+    torch.cuda.synchronize()
+    if dup:
+        assert float(total[nl - 1]) != 0.0
+        return
+    assert float(total[nl - 1]) == 0.0
+    got_k, got_a = [], []
+    for r in range(ranks):
+        okc, ov, g = ctx.dense_states_take(total.data_ptr(), len(AGGS), gmin, G, ranks, r, abi.DT_INT64,
+                                           [abi.DT_FLOAT64, abi.DT_INT64])
+        got_k.append(okc.to_numpy()[0])
+        got_a.append([c.to_numpy()[0] for c in ov])
+    gk = [(np.concatenate(got_k), None)]
+    ga = [(np.concatenate([a[j] for a in got_a]), None) for j in range(len(AGGS))]
+    wk, wa, wg = ob.join_filter_aggregate([ob.HostCol(x), ob.HostCol(k), ob.HostCol(v)], 1, PRED, ob.HostCol(dk),
+                                          [ob.HostCol(dg)], AGGS)
+    assert len(gk[0][0]) == wg
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=[0])

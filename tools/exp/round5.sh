@@ -99,4 +99,14 @@ grep -v amdgpu.ids $O/ab.txt
 run_tests $O/tests.txt tests/test_window_msd.py
 }
 
+r5l() {
+# the shuffle join's items form (config 4): simulated ranks on one device, then gloo device-tensor
+# ranks (world 2 / 3 / 8) through DistributedExecutor, then the per-rank leg
+O=gpurun_out/r5l; mkdir -p $O
+run_tests $O/tests.txt "tests/test_pipeline.py::test_shuffle_items_form_vs_oracle" \
+    "tests/test_pipeline.py::test_items_form_vs_oracle" \
+    "tests/test_distributed.py::test_device_tensor_collectives_several_ranks_on_one_gpu" \
+    "tests/test_distributed.py::test_config4_shuffle_join_two_ranks_on_one_gpu" || exit 1
+}
+
 "$@"
