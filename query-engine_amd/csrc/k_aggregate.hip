@@ -4572,9 +4572,26 @@ __global__ __launch_bounds__(256) void k_region_pack(const uint16_t *__restrict_
     uint32_t *kd = (uint32_t *)(kout + rbase[r]);
     const v2i64 *vs = (const v2i64 *)(vin + r * cap);
     v2i64 *vd = (v2i64 *)(vout + rbase[r]);
-    for (uint32_t i = threadIdx.x; i < c2; i += 256) {
-        __builtin_nontemporal_store(__builtin_nontemporal_load(ks + i), kd + i);
-        if (vin) __builtin_nontemporal_store(__builtin_nontemporal_load(vs + i), vd + i);
+    constexpr int U = 4;  // pairs in flight per thread
+    for (uint32_t i0 = 0; i0 < c2; i0 += 256 * U) {
+        uint32_t kk[U];
+        v2i64 vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * 256 + threadIdx.x;
+            if (i < c2) {
+                kk[u] = __builtin_nontemporal_load(ks + i);
+                if (vin) vv[u] = __builtin_nontemporal_load(vs + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * 256 + threadIdx.x;
+            if (i < c2) {
+                __builtin_nontemporal_store(kk[u], kd + i);
+                if (vin) __builtin_nontemporal_store(vv[u], vd + i);
+            }
+        }
     }
 }
 

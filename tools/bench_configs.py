@@ -469,6 +469,92 @@ def cfg4_leg(ctx, scale, world=8):
                         "wall = sum of the legs"})
 
 
+def cfg4_items_leg(ctx, scale, world=8, rank=5):
+    """BASELINE config 4's per-rank device leg at N = 8 in the shuffle join's items form
+    (DistributedExecutor._shuffle_items, include/qeh.h qeh_shuffle_items_*), on one GPU: rank `rank`'s
+    phase A over its 1e9 fact rows with the regions laid out per destination, its 1/8 of the dimension
+    grouped by slice (k_dim_items), the per-destination packing, and phase B over what it receives --
+    stood in for by its own block for itself from each of the 8 sources (uniform keys send every rank
+    the same share) -- against its slices, built from the whole dimension's items (the all-gather's
+    result).  RCCL time excluded (8-GPU runs are the driver's).  Algorithmic bytes as cfg4leg."""
+    import torch
+    from qe_hip.distributed import _DeviceView
+    n, nd = int(1e9 * scale), 10_000_000
+    x = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 1, n, 100)
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    v = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    full_dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    full_dg = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 5, nd, 1024)
+    b = np.linspace(0, nd, world + 1).astype(int)
+    shards = [(ctx.slice(full_dk, int(b[r]), int(b[r + 1] - b[r])), ctx.slice(full_dg, int(b[r]), int(b[r + 1] - b[r])))
+              for r in range(world)]
+    pred = binop(col(0), BinaryOp.Greater, lit(49))
+    aggs = [(AF.Sum, 2), (AF.Count, 2)]
+    row_len = 7
+    rows = []
+    for dk, dg in shards:
+        row = torch.empty(row_len, dtype=torch.int64, device="cuda")
+        ctx.broadcast_stats(dk, dg, [0, 1], row.data_ptr())
+        rows.append(row)
+    M = torch.cat(rows)
+    ctx.sync()
+    G = 1024
+    nb, span = ctx.fused_items_shape(int(np.diff(b).max()), world)
+    OW = 2 * 161
+    # every shard's dimension items once (the all-gather's result), from throwaway handles
+    gi = torch.empty(world * nb * span, dtype=torch.int32, device="cuda")
+    go = torch.empty(world * nb * OW, dtype=torch.int32, device="cuda")
+    tiny = [ctx.slice(x, 0, 8192), ctx.slice(k, 0, 8192), ctx.slice(v, 0, 8192)]
+    for r, (dk, dg) in enumerate(shards):
+        h = ctx.shuffle_items_begin(tiny, 1, pred, aggs, M.data_ptr(), world, r, row_len)
+        ctx.fused_items_build(h, dk, dg, nb, span, gi.data_ptr() + r * nb * span * 4, go.data_ptr() + r * nb * OW * 4)
+        ctx.fused_items_abort(h)
+    ctx.sync()
+    names = ["slice_partition", "shuffle_pack", "slice_probe", "fused_build"]
+    nl = (1 + len(aggs)) * G + 1
+    lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
+    best = None
+    for rep in range(4):
+        ctx.timing(True)
+        ctx.timing_reset()
+        t0 = time.perf_counter()
+        h = ctx.shuffle_items_begin([x, k, v], 1, pred, aggs, M.data_ptr(), world, rank, row_len)
+        it = torch.empty(nb * span, dtype=torch.int32, device="cuda")
+        of = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        dk, dg = shards[rank]
+        ctx.fused_items_build(h, dk, dg, nb, span, it.data_ptr(), of.data_ptr())
+        ok, kp, vp, cp, bc, E, tot = ctx.shuffle_items_pack(h, world)
+        assert ok
+        # the receive buffers' stand-in: block `rank` of this rank's own pack, once per source
+        kt = torch.as_tensor(_DeviceView(kp, world * bc, "<i2", None))
+        vt = torch.as_tensor(_DeviceView(vp, world * bc, "<i8", None))
+        ct = torch.as_tensor(_DeviceView(cp, world * E, "<i4", None))
+        t_own = int(tot[rank])
+        rk = torch.cat([kt[rank * bc:rank * bc + t_own]] * world + [torch.zeros(4, dtype=torch.int16, device="cuda")])
+        rv = torch.cat([vt[rank * bc:rank * bc + t_own]] * world + [torch.zeros(4, dtype=torch.int64, device="cuda")])
+        rc = torch.cat([ct[rank * E:(rank + 1) * E]] * world)
+        so = [q * t_own for q in range(world)]
+        ctx.shuffle_items_finish(h, rk.data_ptr(), rv.data_ptr(), rc.data_ptr(), so, gi.data_ptr(), span, go.data_ptr(),
+                                 world * nb, G, lanes.data_ptr())
+        ctx.sync()
+        wall = time.perf_counter() - t0
+        kt_ = {nm: ctx.kernel_time(nm)[0] for nm in names}
+        ctx.timing(False)
+        if rep and (best is None or sum(kt_.values()) < sum(best[1].values())):
+            best = (wall, kt_, int(tot.sum()), t_own * world)
+        del rk, rv, rc
+    wall, kt_, sent, recv = best
+    kms = sum(kt_.values())
+    alg = 24.0 * n + 16.0 * nd
+    line(f"cfg4 per-rank device leg at N={world}, items form (1e9 fact rows + 1/{world} dim per rank)", n, wall, alg, kms,
+         "k_slice_partition (per-destination layout) + k_region_pack + k_slice_probe (received regions)", None,
+         {"kernel_split_ms": kt_, "items_packed": sent, "items_received": recv,
+          "xgmi_bytes_per_rank": 10.0 * (sent - sent // world),
+          "note": "frac on SURVEY §8(d)'s 24 B / fact row + 16 B / dim row; the receive side stood in by this "
+                  "rank's own block x 8 (uniform keys); RCCL all-to-all time excluded; wall includes the "
+                  "stand-in copies"})
+
+
 def cfg5_leg(ctx, scale, world=8):
     """BASELINE config 5's per-rank device leg at N = 8, on one GPU: what one rank of the distributed
     ROW_NUMBER() OVER (PARTITION BY k ORDER BY v) runs besides the two RCCL all-to-alls
@@ -619,7 +705,7 @@ def main():
         {"cfg2": cfg2, "cfg3": cfg3, "cfg5": cfg5, "filter": cfg_filter, "limit": cfg_limit,
          "plan": cfg_plan, "left": lambda c, s: cfg_outer(c, s, 1), "full": lambda c, s: cfg_outer(c, s, 3),
          "merge": cfg_merge, "encode": cfg_encode, "shapes": cfg_metric_shapes, "partition": cfg_partition, "cfg3w": cfg3_wide, "window": cfg_window,
-         "cfg4leg": cfg4_leg, "cfg5leg": cfg5_leg,
+         "cfg4leg": cfg4_leg, "cfg4items": cfg4_items_leg, "cfg5leg": cfg5_leg,
          "window_lsd": cfg_window_lsd}[name](ctx, args.scale)
         ctx.sync()
         abi.check(ctx.lib.qeh_pool_trim(ctx.h))

@@ -109,4 +109,11 @@ run_tests $O/tests.txt "tests/test_pipeline.py::test_shuffle_items_form_vs_oracl
     "tests/test_distributed.py::test_config4_shuffle_join_two_ranks_on_one_gpu" || exit 1
 }
 
+r5m() {
+# config 4's per-rank device leg at N = 8: the two-pass exchange form and the items form, one box
+O=gpurun_out/r5m; mkdir -p $O
+timeout -k 10 400 python3 tools/bench_configs.py --only cfg4leg,cfg4items > $O/cfg4.txt 2>&1 || { tail -30 $O/cfg4.txt; exit 1; }
+grep -v amdgpu.ids $O/cfg4.txt | cut -c1-700
+}
+
 "$@"
