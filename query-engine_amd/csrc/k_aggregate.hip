@@ -636,7 +636,7 @@ __global__ __launch_bounds__(NTH) void k_slice_partition(FastIn in, PredTerms te
             }
             const uint64_t o = d.g + xl;
             if (lo == 0 && hi == (uint32_t)CH) {
-                *(uint32_t *)(rg.key + o) = (uint32_t)kv[0] | ((uint32_t)kv[1] << 16);
+                __builtin_nontemporal_store((uint32_t)kv[0] | ((uint32_t)kv[1] << 16), (uint32_t *)(rg.key + o));
 #pragma unroll
                 for (int u = 0; u < VC; ++u) {
                     v2i64 w;

@@ -116,4 +116,27 @@ timeout -k 10 400 python3 tools/bench_configs.py --only cfg4leg,cfg4items > $O/c
 grep -v amdgpu.ids $O/cfg4.txt | cut -c1-700
 }
 
+r5t() {
+# the whole GPU suite (the driver's round-end tier)
+O=gpurun_out/r5t; mkdir -p $O
+timeout -k 10 1080 python3 -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/tests.txt 2>&1
+rc=$?; tail -15 $O/tests.txt; exit $rc
+}
+
+r5b2() {
+# the bench line (driver contract), then the profile of the same command (kernel trace + PMC passes)
+O=gpurun_out/r5b2; mkdir -p $O
+timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+tail -1 $O/bench.json
+timeout -k 10 900 bash tools/profile.sh r05 > $O/profile.txt 2>&1 || { tail -20 $O/profile.txt; exit 1; }
+tail -25 $O/profile.txt
+}
+
+r5n() {
+# phase A's key stores non-temporal (as the value stores) vs cached, alternating builds
+O=gpurun_out/r5n_$(date +%H%M%S); mkdir -p $O
+timeout -k 10 500 python3 tools/exp_slice.py --rounds 3 libqeh_base.so libqeh.so > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
+}
+
 "$@"
