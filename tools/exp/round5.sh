@@ -139,4 +139,24 @@ timeout -k 10 500 python3 tools/exp_slice.py --rounds 3 libqeh_base.so libqeh.so
 grep -v amdgpu.ids $O/ab.txt
 }
 
+r5o() {
+# config 5: the partition passes' run writes non-temporal (QEH_WM_NTS bit 0 pass 1, bit 1 pass 2) vs cached
+O=gpurun_out/r5o_$(date +%H%M%S); mkdir -p $O
+timeout -k 10 600 python3 tools/exp/win_ab.py --rounds 2 libqeh.so libqeh.so:QEH_WM_NTS=1 libqeh.so:QEH_WM_NTS=2 \
+    libqeh.so:QEH_WM_NTS=3 > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
+}
+
+r5p() {
+# non-temporal result stores of the group sort (QEH_WM_NTS=4) and of the small exchange scatter
+# (QEH_PM_NT=1: config 4's two-pass exchange and the window leg's move) vs cached
+O=gpurun_out/r5p_$(date +%H%M%S); mkdir -p $O
+timeout -k 10 600 python3 tools/exp/win_ab.py --rounds 2 libqeh.so libqeh.so:QEH_WM_NTS=4 > $O/ab_win.txt 2>&1 || { cat $O/ab_win.txt; exit 1; }
+grep -v amdgpu.ids $O/ab_win.txt
+for e in 0 1; do
+  QEH_NO_ITEMS_SHUFFLE=1 QEH_PM_NT=$e timeout -k 10 300 python3 tools/bench_configs.py --only cfg4leg > $O/cfg4_nt$e.txt 2>&1 || { tail -5 $O/cfg4_nt$e.txt; exit 1; }
+  grep -v amdgpu.ids $O/cfg4_nt$e.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print("PM_NT='$e'", d["kernel_ms"], d["legs"]["exchange_pass_fact"]["ms"], d["legs"]["local_join"]["ms"])'
+done
+}
+
 "$@"
