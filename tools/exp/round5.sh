@@ -159,4 +159,34 @@ for e in 0 1; do
 done
 }
 
+r5q() {
+# the configs table of this round (one box), then the N = 8 rank-share rehearsal (items form)
+O=gpurun_out/r5q; mkdir -p $O
+timeout -k 10 1000 python3 -u tools/bench_configs.py --only cfg2,cfg3,filter,limit,left,full,shapes,partition,merge,window,cfg4leg,cfg4items,cfg5leg,cfg5 > $O/configs.jsonl 2>$O/configs.err || { tail $O/configs.err; exit 1; }
+python3 -c 'import json,sys
+for l in open(sys.argv[1]):
+    l=l.strip()
+    if not l.startswith("{"): continue
+    d=json.loads(l); print(str(d["config"])[:70], round(d["kernel_ms"] or 0,3), d["frac_of_8TBs"])' $O/configs.jsonl
+for r in 0 3; do
+  QEH_BENCH_RANK_OF=$r/8 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --cpu-sample 0 > $O/rank${r}of8.json 2> $O/rank${r}of8.err || { tail -20 $O/rank${r}of8.err; exit 1; }
+  tail -1 $O/rank${r}of8.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("rank-share", d["ms_per_step"], d.get("dist_build"), d.get("dist_final"))'
+done
+}
+
+r5r() {
+# non-temporal key stores in the fused pipeline only: cfg3 / g17 / agg2 and the metric, base (cached
+# keys everywhere) vs this build, one box
+O=gpurun_out/r5r; mkdir -p $O
+for lib in libqeh_base.so libqeh.so; do
+  QEH_LIB_PATH=$PWD/query-engine_amd/$lib timeout -k 10 400 python3 -u tools/bench_configs.py --only cfg3,shapes > $O/cfg_$lib.jsonl 2>$O/cfg_$lib.err || { tail $O/cfg_$lib.err; exit 1; }
+  python3 -c 'import json,sys
+for l in open(sys.argv[1]):
+    l=l.strip()
+    if l.startswith("{"): d=json.loads(l); print(sys.argv[2], str(d["config"])[:40], round(d["kernel_ms"] or 0,3))' $O/cfg_$lib.jsonl $lib
+done
+timeout -k 10 500 python3 tools/exp_slice.py --rounds 2 libqeh_base.so libqeh.so > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+grep -v amdgpu.ids $O/ab.txt
+}
+
 "$@"
