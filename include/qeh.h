@@ -404,11 +404,13 @@ int qeh_fused_items_abort(qeh_ctx *ctx, void *handle);
  *     and take the two-pass path.  Else packs each destination q's regions into one block: keys
  *     (*keys)[q * blockcap ..] and values (*vals)[q * blockcap ..], totals[q] items (region counts
  *     rounded up to 2), and the block's region counts (*counts)[q * block_regions .. + block_regions],
- *     all library-owned until qeh_shuffle_items_finish returns.
+ *     all library-owned until qeh_shuffle_items_finish returns.  This rank's own block is not packed
+ *     (its keys / values stay in phase A's regions, read there by finish): totals[rank] is its size.
  *   (caller: all-to-all of the totals[q] keys and values of block q to rank q, source-major on the
- *   receiver; all-to-all of the block_regions counts)
+ *   receiver, nothing to or from itself; all-to-all of the block_regions counts, its own included)
  *   qeh_shuffle_items_finish: phase B over the received blocks (keys / vals / counts as the
- *     all-to-all left them, source q's items from src_offsets[q], world entries, host memory) with
+ *     all-to-all left them, source q's items from src_offsets[q], world entries, host memory; the
+ *     entry of this rank unused) and this rank's own regions in place, with
  *     this rank's slices built from the gathered dimension items (n_regions spans of `span`, as
  *     qeh_fused_items_finish), then the dense final stage's lanes ((1 + n_aggs) * n_groups + 1
  *     doubles, the last = the status lane: a key on two ranks, an overflow); frees the handle.

@@ -323,6 +323,11 @@ struct SliceRegions {
     int32_t pw;
     int32_t prank;
     int32_t pgrid;
+    // phase B of the partitioned layout: this rank's own regions (source prank) read in place from phase
+    // A's layout (region number * ocap) instead of from the packed receive buffers
+    const uint16_t *okey;
+    const int64_t *oval;
+    uint64_t ocap;
 };
 // the partitioned layout's slices per rank and a region's number (phase A, pw > 0)
 __host__ __device__ __forceinline__ int part_slices(int F, int pw) { return (F + pw - 1) / pw; }
@@ -1053,17 +1058,24 @@ __global__ __launch_bounds__(kSliceBlock) void k_slice_probe(SliceRegions rg, in
         __syncthreads();
         for (int64_t s = sb + wave; s < se; s += W) {
             uint64_t reg, rb;
+            const uint16_t *kbase = rg.key;
+            const int64_t *vbase = rg.val;
             if (rg.pw) {  // packed regions received from the ranks: (source q, workgroup w) of local slice b
                 const int64_t r = s - (int64_t)b * nreg, q = r / rg.pgrid;
                 reg = ((uint64_t)q * F + b) * rg.pgrid + (uint64_t)(r - q * rg.pgrid);
-                rb = rg.rbase[reg];
+                if (rg.okey && q == rg.prank) {  // (this rank's own regions, in phase A's layout)
+                    kbase = rg.okey, vbase = rg.oval;
+                    rb = reg * rg.ocap;
+                } else {
+                    rb = rg.rbase[reg];
+                }
             } else {
                 reg = (uint64_t)(s - (int64_t)b * nreg) * F + b;
                 rb = reg * rg.cap;
             }
             const uint32_t n_r = rg.count[reg];
-            const uint16_t *kp = rg.key + rb;
-            const int64_t *vp = VC ? rg.val + rb : nullptr;
+            const uint16_t *kp = kbase + rb;
+            const int64_t *vp = VC ? vbase + rb : nullptr;
             const int64_t *vp2 = NACOL > 1 ? rg.val2 + rb : nullptr;
             uint32_t en[8];
             int64_t vn[8], vn2[NACOL > 1 ? 8 : 1];
@@ -4355,7 +4367,7 @@ struct FusedItems {
     int64_t Gs = 0;
     // the shuffle join's items form (pw > 0): phase A in the partitioned layout, the packed send blocks
     int pw = 0, prank = 0, S = 0;
-    uint64_t blockcap = 0;
+    uint64_t blockcap = 0, cap = 0;
     DevBuf pkey, pval, pcnt, prb, ptot, rrb, roff;
 };
 
@@ -4570,8 +4582,10 @@ __global__ __launch_bounds__(1024) void k_region_scan(const uint32_t *__restrict
 // workgroup per region, key pairs as 4-B words, value pairs as 16-B words.
 __global__ __launch_bounds__(256) void k_region_pack(const uint16_t *__restrict__ kin, const int64_t *__restrict__ vin,
                                                      const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ rbase,
-                                                     uint64_t cap, uint16_t *__restrict__ kout, int64_t *__restrict__ vout) {
+                                                     uint64_t cap, uint16_t *__restrict__ kout, int64_t *__restrict__ vout,
+                                                     int64_t E, int skip) {
     const uint64_t r = blockIdx.x;
+    if ((int64_t)(r / E) == skip) return;  // (this rank's own block: phase B reads it in place)
     const uint32_t c2 = (cnt[r] + 1u) >> 1;  // item pairs
     const uint32_t *ks = (const uint32_t *)(kin + r * cap);
     uint32_t *kd = (uint32_t *)(kout + rbase[r]);
@@ -4628,6 +4642,7 @@ extern "C" int qeh_shuffle_items_pack(qeh_ctx *ctx, void *handle, uint16_t **key
     fi->S = part_slices(pl.sp.F, pw);
     const int64_t E = (int64_t)fi->S * grid, P = E * pw;
     fi->blockcap = (uint64_t)E * pl.sp.cap;
+    fi->cap = pl.sp.cap;
     QEH_TRY(fi->pkey.alloc(ctx, (fi->blockcap * pw + 4) * 2));
     if (fi->nacol) QEH_TRY(fi->pval.alloc(ctx, (fi->blockcap * pw + 4) * 8));
     QEH_TRY(fi->pcnt.alloc(ctx, (size_t)P * 4));
@@ -4640,7 +4655,8 @@ extern "C" int qeh_shuffle_items_pack(qeh_ctx *ctx, void *handle, uint16_t **key
                            fi->pcnt.as<uint32_t>(), fi->ptot.as<int64_t>());
         hipLaunchKernelGGL(k_region_pack, dim3((unsigned)P), dim3(256), 0, ctx->stream, fi->kbuf.as<uint16_t>(),
                            fi->nacol ? fi->vbuf.as<int64_t>() : nullptr, fi->pcnt.as<uint32_t>(), fi->prb.as<uint64_t>(),
-                           pl.sp.cap, fi->pkey.as<uint16_t>(), fi->nacol ? fi->pval.as<int64_t>() : nullptr);
+                           pl.sp.cap, fi->pkey.as<uint16_t>(), fi->nacol ? fi->pval.as<int64_t>() : nullptr, E,
+                           fi->prank);
     }
     QEH_HIP(hipGetLastError());
     QEH_TRY(read_small(ctx, totals, fi->ptot.p, (size_t)pw * 8));
@@ -4680,6 +4696,7 @@ extern "C" int qeh_shuffle_items_finish(qeh_ctx *ctx, void *handle, const uint16
     rg.overflow = st + 1;
     rg.rbase = fi->rrb.as<uint64_t>();
     rg.pw = pw, rg.prank = fi->prank, rg.pgrid = grid;
+    rg.okey = fi->kbuf.as<uint16_t>(), rg.oval = fi->nacol ? fi->vbuf.as<int64_t>() : nullptr, rg.ocap = fi->cap;
     {
         KernelTimer ktb(ctx, "slice_probe");
         DimSlices dim{items, nullptr, st + 4, fi->plan.as<FusedPlan>(), n_regions, 0, span, offs};

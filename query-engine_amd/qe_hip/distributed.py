@@ -1099,7 +1099,9 @@ class DistributedExecutor:
         go = torch.empty(W * nb * OW, dtype=torch.int32, device="cuda")
         dist.all_gather_into_tensor(gi, items, group=self.group)
         dist.all_gather_into_tensor(go, offs, group=self.group)
+        # (this rank's own block stays in phase A's regions: nothing to or from itself)
         pin, pout = [int(x) for x in Mt[me, :W]], [int(x) for x in Mt[:, me]]
+        pin[me] = pout[me] = 0
         peak = _peak_remote(Mt[:, :W])
         starts = [q * blockcap for q in range(W)]
         nacol = vp != 0

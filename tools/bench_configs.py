@@ -525,15 +525,20 @@ def cfg4_items_leg(ctx, scale, world=8, rank=5):
         ctx.fused_items_build(h, dk, dg, nb, span, it.data_ptr(), of.data_ptr())
         ok, kp, vp, cp, bc, E, tot = ctx.shuffle_items_pack(h, world)
         assert ok
-        # the receive buffers' stand-in: block `rank` of this rank's own pack, once per source
+        # the receive buffers' stand-in: a packed block of this rank's (the next rank's, same size under
+        # uniform keys) once per remote source; its own block is read in place by phase B
         kt = torch.as_tensor(_DeviceView(kp, world * bc, "<i2", None))
         vt = torch.as_tensor(_DeviceView(vp, world * bc, "<i8", None))
         ct = torch.as_tensor(_DeviceView(cp, world * E, "<i4", None))
-        t_own = int(tot[rank])
-        rk = torch.cat([kt[rank * bc:rank * bc + t_own]] * world + [torch.zeros(4, dtype=torch.int16, device="cuda")])
-        rv = torch.cat([vt[rank * bc:rank * bc + t_own]] * world + [torch.zeros(4, dtype=torch.int64, device="cuda")])
-        rc = torch.cat([ct[rank * E:(rank + 1) * E]] * world)
-        so = [q * t_own for q in range(world)]
+        q1 = (rank + 1) % world
+        t1 = int(tot[q1])
+        rk = torch.cat([kt[q1 * bc:q1 * bc + t1]] * (world - 1) + [torch.zeros(4, dtype=torch.int16, device="cuda")])
+        rv = torch.cat([vt[q1 * bc:q1 * bc + t1]] * (world - 1) + [torch.zeros(4, dtype=torch.int64, device="cuda")])
+        rc = torch.cat([ct[q1 * E:(q1 + 1) * E] if q != rank else ct[rank * E:(rank + 1) * E] for q in range(world)])
+        so, off = [], 0
+        for q in range(world):
+            so.append(off)
+            off += t1 if q != rank else 0
         ctx.shuffle_items_finish(h, rk.data_ptr(), rv.data_ptr(), rc.data_ptr(), so, gi.data_ptr(), span, go.data_ptr(),
                                  world * nb, G, lanes.data_ptr())
         ctx.sync()
@@ -541,7 +546,7 @@ def cfg4_items_leg(ctx, scale, world=8, rank=5):
         kt_ = {nm: ctx.kernel_time(nm)[0] for nm in names}
         ctx.timing(False)
         if rep and (best is None or sum(kt_.values()) < sum(best[1].values())):
-            best = (wall, kt_, int(tot.sum()), t_own * world)
+            best = (wall, kt_, int(tot.sum()), t1 * (world - 1) + int(tot[rank]))
         del rk, rv, rc
     wall, kt_, sent, recv = best
     kms = sum(kt_.values())

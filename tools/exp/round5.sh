@@ -189,4 +189,13 @@ timeout -k 10 500 python3 tools/exp_slice.py --rounds 2 libqeh_base.so libqeh.so
 grep -v amdgpu.ids $O/ab.txt
 }
 
+r5s() {
+# own block read in place (not packed, not copied): shuffle items-form parity, then the per-rank leg
+O=gpurun_out/r5s; mkdir -p $O
+run_tests $O/tests.txt "tests/test_pipeline.py::test_shuffle_items_form_vs_oracle" \
+    "tests/test_distributed.py::test_device_tensor_collectives_several_ranks_on_one_gpu" || exit 1
+timeout -k 10 300 python3 tools/bench_configs.py --only cfg4items > $O/cfg4.txt 2>&1 || { tail -20 $O/cfg4.txt; exit 1; }
+grep -v amdgpu.ids $O/cfg4.txt | cut -c1-600
+}
+
 "$@"
