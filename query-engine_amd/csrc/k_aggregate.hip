@@ -4406,8 +4406,11 @@ static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_p
     AggSpecs &specs = fi->specs;
     specs.shards = 1;
     fi->Gs = std::min<int64_t>(kSliceStateWords / std::max(specs.n_slots, 1), 0xFFFE);
-    fi->grid = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all,
-                                                            (int64_t)kMaxSliceGrid}));
+    // (the shuffle form: the same grid on every rank whatever its row count -- the receivers address the
+    // regions of every sender as (source, slice, workgroup))
+    fi->grid = pw > 1 ? (int)std::min<int64_t>(ctx->props.multiProcessorCount, kMaxSliceGrid)
+                      : (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)ctx->props.multiProcessorCount, n_all,
+                                                                     (int64_t)kMaxSliceGrid}));
     const uint64_t tiles_per_wg = (uint64_t)((n_all + fi->grid - 1) / fi->grid);
     SlicePlanIn pi{};
     pi.min_bytes = 6ull << 20;
@@ -4446,6 +4449,8 @@ static int fused_items_begin(qeh_ctx *ctx, const qeh_column *probe_cols, int n_p
     fp.plan = dplan;
     if (n_tiles > 0 || tail > 0)
         launch_slice_partition_early(ctx, fi->in, pp, nterms, fi->nacol, n_tiles, tail, fi->grid, fi->rg, &dplan->sp, fp);
+    else  // (no fact rows on this rank: its regions are empty)
+        QEH_HIP(hipMemsetAsync(fi->cbuf.p, 0, nreg_max * 4, ctx->stream));
     QEH_HIP(hipGetLastError());
     *handle = fi.release();
     return QEH_OK;

@@ -472,6 +472,33 @@ def mode_gpu_devtensors(rank, world):
         res = dx.gather_to_root(keys + aggs_out)
         if rank == 0:
             assert_grouped_equal(res[:1], res[1:], wk, wa, float_aggs=[0])
+    # the items shuffle with COUNT only (no value column) and rank 1's fact shard empty; then probe keys
+    # crowded into one slice (a region fills up on every rank: the pack's flag sends every rank to the
+    # two-pass form) -- both vs the oracle
+    cnt_only = [(AF.Count, 2)]
+    empty = rank == 1
+    fx = [ctx.upload(x[:0] if empty else x), ctx.upload(kk[:0] if empty else kk), ctx.upload(vv[:0] if empty else vv)]
+    keys, aggs_out, ng = dx.join_filter_aggregate_shuffle(fx, 1, pred, ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+                                                          [ctx.upload(dg_all[b[rank]:b[rank + 1]])], cnt_only)
+    assert dx.last_shuffle == "items", dx.last_shuffle
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        keep = np.ones(n * world, bool)
+        keep[n:2 * n] = False  # rank 1's rows
+        ck, ca, _ = ob.join_filter_aggregate([ob.HostCol(X[keep]), ob.HostCol(KK[keep]), ob.HostCol(VV[keep])], 1, pred,
+                                             ob.HostCol(dk_all), [ob.HostCol(dg_all)], cnt_only)
+        assert_grouped_equal(res[:1], res[1:], ck, ca)
+    ksk = (kk % 60_000).astype(np.int64)
+    keys, aggs_out, ng = dx.join_filter_aggregate_shuffle([ctx.upload(x), ctx.upload(ksk), ctx.upload(vv)], 1, pred,
+                                                          ctx.upload(dk_all[b[rank]:b[rank + 1]]),
+                                                          [ctx.upload(dg_all[b[rank]:b[rank + 1]])], aggs)
+    assert dx.last_shuffle == "two_pass", dx.last_shuffle
+    res = dx.gather_to_root(keys + aggs_out)
+    if rank == 0:
+        KSK = (KK % 60_000).astype(np.int64)
+        sk_, sa_, _ = ob.join_filter_aggregate([ob.HostCol(X), ob.HostCol(KSK), ob.HostCol(VV)], 1, pred,
+                                               ob.HostCol(dk_all), [ob.HostCol(dg_all)], aggs)
+        assert_grouped_equal(res[:1], res[1:], sk_, sa_, float_aggs=[0])
     # a build key held by two ranks (rank 0 and the last rank) with SUM + COUNT: the no-wait table
     # form sums the two entries to one above G (both group slots >= G / 2), which the table check
     # clears before the probe reads it; the non-empty count then falls short on every rank and every
