@@ -97,9 +97,7 @@ struct WmShape {
     int32_t nb;        // buckets (high digits in use)
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
-    int32_t exp;       // QEH_WM_EXP (experiments only, results wrong): pass 1 / 2 bit 0 no key-bit stores,
-                       // bit 1 no order-key stores, bit 2 no write loop, bit 3 (with 2) no ranking
-    int32_t nts;       // QEH_WM_NTS: bit 0 pass 1, bit 1 pass 2 write their runs with non-temporal stores
+    int32_t exp;       // QEH_WM_EXP != 0 (experiments: time pass 1 alone; the query then fails)
 };
 
 // ---- pass 1: histogram of the high key digit per workgroup row range -------------------------
@@ -426,27 +424,25 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
             ovv[j] = wm_ld<OES>(ord.values, ii);
         }
     };
-    if (r0 < r1) load(r0);
-    for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
+    // One tile: FULL tiles store unconditionally (2 * NJ stores on every path), so waiting for the
+    // next tile's prefetched loads never waits for this tile's run stores: the compiler counts
+    // vmcnt exactly only when the store count between a load and its use is fixed -- a run-time
+    // trip count there made it wait for every store ack (vmcnt(0)) before each tile.
+    auto tile = [&](int64_t t0, auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
         uint32_t d[NJ], kl[NJ], slot[NJ];
         uint64_t ok[NJ];
         bool live[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            live[j] = t0 + woff + j * 64 < r1;
+            live[j] = FULL || t0 + woff + j * 64 < r1;
             const uint64_t kk = ((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) & sh.kmask;
             d[j] = (uint32_t)(kk >> sh.lb);
             kl[j] = (uint32_t)kk & lmask;
             ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
-        uint32_t tcnt = 0;
-        if (sh.exp & 8) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) slot[j] = (uint32_t)(wave * 64 * NJ + j * 64 + lane);
-        } else {
-            tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
-        }
+        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             if (!live[j]) continue;
@@ -455,28 +451,42 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
             st_d[slot[j]] = (uint16_t)d[j];
         }
         wm_barrier();
-        const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
-        if (!(sh.exp & 4)) {
-#pragma unroll 8
+        if constexpr (FULL) {
+#pragma unroll
+            for (int q = 0; q < NJ; ++q) {
+                const int s = tid + q * kWmBlock;
+                const uint32_t dd = st_d[s];
+                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                o_key[p] = st_key[s];
+                o_kl[p] = st_kl[s];
+            }
+        } else {
+            const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
             for (int s = tid; s < m; s += kWmBlock) {
                 const uint32_t dd = st_d[s];
                 const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                if (sh.nts & 1) {
-                    if (!(sh.exp & 2)) __builtin_nontemporal_store(st_key[s], o_key + p);
-                    if (!(sh.exp & 1)) __builtin_nontemporal_store(st_kl[s], o_kl + p);
-                } else {
-                    if (!(sh.exp & 2)) o_key[p] = st_key[s];
-                    if (!(sh.exp & 1)) o_kl[p] = st_kl[s];
-                }
+                o_key[p] = st_key[s];
+                o_kl[p] = st_kl[s];
             }
         }
         wm_barrier();
         lpos[tid] += tcnt;
+    };
+    // the first full tile is peeled, so every path into the loop has a tile's stores after the
+    // prefetch (the loop's waits then count past them)
+    if (r0 < r1) load(r0);
+    if (r1 - r0 >= kWmTile) {
+        tile(r0, std::true_type{});
+        int64_t t0 = r0 + kWmTile;
+        for (; t0 + kWmTile <= r1; t0 += kWmTile) tile(t0, std::true_type{});
+        if (t0 < r1) tile(t0, std::false_type{});
+    } else if (r0 < r1) {
+        tile(r0, std::false_type{});
     }
 }
 
 // pass 2: inside each bucket, stable partition by the low digit; group starts -> pstart
-template <int DB>
+template <int DB, bool KS>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
                                                         uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart,
@@ -518,26 +528,26 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
         __syncthreads();
         uint64_t kx[NJ];
         uint32_t lx[NJ];
+        // one base address, the rows at immediate offsets; a tile may read past the bucket (and past
+        // n: i_key / i_kl carry kWmTile rows of padding) -- those rows are not live
         auto load = [&](int64_t t0) {
+            const uint64_t *pk = i_key + t0 + woff;
+            const uint16_t *pl = i_kl + t0 + woff;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int64_t i = t0 + woff + j * 64;
-                const int64_t ii = i < s1 ? i : s0;
-                kx[j] = i_key[ii];
-                lx[j] = i_kl[ii];
-            }
+            for (int j = 0; j < NJ; ++j) kx[j] = pk[j * 64], lx[j] = pl[j * 64];
         };
-        if (s0 < s1) load(s0);
-        for (int64_t t0 = s0; t0 < s1; t0 += kWmTile) {
+        // FULL tiles store unconditionally (see k_wm2_pass1: exact vmcnt accounting)
+        auto tile = [&](int64_t t0, auto fullc) {
+            constexpr bool FULL = decltype(fullc)::value;
             uint32_t d[NJ], slot[NJ];
             uint64_t keys[NJ];
             bool live[NJ];
             uint32_t ksub[NJ];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                live[j] = t0 + woff + j * 64 < s1;
-                d[j] = lx[j] >> sbits;
-                ksub[j] = lx[j] & ((1u << sbits) - 1u);
+                live[j] = FULL || t0 + woff + j * 64 < s1;
+                d[j] = KS ? lx[j] >> sbits : lx[j];
+                ksub[j] = KS ? lx[j] & ((1u << sbits) - 1u) : 0u;
                 keys[j] = kx[j];
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
@@ -549,17 +559,30 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
                 st_d[slot[j]] = (uint16_t)(d[j] | (ksub[j] << 10));  // digit (10 bits) | sub-key (<= 4 bits)
             }
             wm_barrier();
-            const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
-    #pragma unroll 8
-        for (int s = tid; s < m; s += kWmBlock) {
+            auto put = [&](int s) {
                 const uint32_t dd = st_d[s] & 1023u;
                 const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                if (sh.nts & 2) __builtin_nontemporal_store(st_key[s], o_key + p);
-                else o_key[p] = st_key[s];
-                if (sbits) o_ks[p] = (uint8_t)(st_d[s] >> 10);
+                o_key[p] = st_key[s];
+                if constexpr (KS) o_ks[p] = (uint8_t)(st_d[s] >> 10);
+            };
+            if constexpr (FULL) {
+#pragma unroll
+                for (int q = 0; q < NJ; ++q) put(tid + q * kWmBlock);
+            } else {
+                const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
+                for (int s = tid; s < m; s += kWmBlock) put(s);
             }
             wm_barrier();
             lpos[tid] += tcnt;
+        };
+        if (s0 < s1) load(s0);
+        if (s1 - s0 >= kWmTile) {
+            tile(s0, std::true_type{});
+            int64_t t0 = s0 + kWmTile;
+            for (; t0 + kWmTile <= s1; t0 += kWmTile) tile(t0, std::true_type{});
+            if (t0 < s1) tile(t0, std::false_type{});
+        } else if (s0 < s1) {
+            tile(s0, std::false_type{});
         }
         __syncthreads();
     }
@@ -1223,7 +1246,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
     DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2;
     const int64_t nc1 = (int64_t)kWmDig * g1;
-    if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, n * 8) || kl1.alloc(ctx, n * 2) ||
+    if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, (n + kWmTile) * 8) || kl1.alloc(ctx, (n + kWmTile) * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
         flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)))
         return fail(QEH_E_OOM, "window: out of device memory");
@@ -1254,9 +1277,11 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
 #undef QEH_WM_P1
         if (!sh.exp)  // (experiment runs: pass 1 only)
-        hipLaunchKernelGGL(at ? k_wm2_pass2<kWmAtomicRank> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10> : k_wm2_pass2<-1>, dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+#define QEH_WM_P2(KS) (at ? k_wm2_pass2<kWmAtomicRank, KS> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10, KS> : k_wm2_pass2<-1, KS>)
+        hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
                            bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
                            pst.as<uint64_t>(), ks2.as<uint8_t>());
+#undef QEH_WM_P2
     }
     QEH_HIP(hipGetLastError());
     if (sh.exp) {  // experiment runs stop after the partition passes (their outputs are not valid)
@@ -1455,7 +1480,6 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         sh.nparts = (int64_t)1 << 20;
     }
     if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
-    if (const char *e = std::getenv("QEH_WM_NTS")) sh.nts = std::atoi(e);
     return window_noid(ctx, func, part, order, asc, param, dflt, sh, out, folded ? &pre : nullptr);
 }
 
