@@ -36,6 +36,7 @@ constexpr int kWmBlock = 1024;                // partition passes: one workgroup
 constexpr int kWmTile = 8192;                 // rows per partition-pass tile (8 per thread)
 constexpr int kWmDig = 1024;                  // digits per partition pass
 constexpr int kWmSortBlock = 256;             // group sort: 4 waves
+constexpr int kWmCkTiles = 2;                 // pass 2 tiles per inverse-pass-2 chunk (a checkpoint each)
 
 // Workgroup barrier ordering LDS only: the next tile's global loads stay in flight across it
 // (__syncthreads would also drain vmcnt and serialise the prefetch).
@@ -99,6 +100,11 @@ struct WmShape {
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
     int32_t exp;       // QEH_WM_EXP != 0 (experiments: time pass 1 alone; the query then fails)
 };
+
+// inverse-pass chunks of kWmCkTiles tiles per pass-1 row span (sh.span is a multiple of kWmTile)
+__host__ __device__ __forceinline__ int64_t wm_span_chunks(const WmShape &sh) {
+    return (sh.span / kWmTile + kWmCkTiles - 1) / kWmCkTiles;
+}
 
 // ---- pass 1: histogram of the high key digit per workgroup row range -------------------------
 template <int KES>
@@ -401,7 +407,7 @@ __host__ __device__ __forceinline__ int wm_digit_bits(int64_t ndig) {
 template <int KES, int OES, int DB>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
                                                         const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
-                                                        uint16_t *__restrict__ o_kl) {
+                                                        uint16_t *__restrict__ o_kl, uint32_t *__restrict__ ckpt) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
@@ -442,6 +448,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
             ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
         }
         if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
+        {  // every kWmCkTiles tiles: the run positions, where inverse pass 1 resumes the replay
+            const int64_t ti = (t0 - r0) / kWmTile;
+            if (ti % kWmCkTiles == 0) ckpt[((int64_t)blockIdx.x * wm_span_chunks(sh) + ti / kWmCkTiles) * kWmDig + tid] = lpos[tid];
+        }
         const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -490,7 +500,8 @@ template <int DB, bool KS>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
                                                         uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart,
-                                                        uint8_t *__restrict__ o_ks) {
+                                                        uint8_t *__restrict__ o_ks, const uint32_t *__restrict__ cbase,
+                                                        uint32_t *__restrict__ ckpt) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
@@ -551,6 +562,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
                 keys[j] = kx[j];
             }
             if (t0 + kWmTile < s1) load(t0 + kWmTile);
+            {  // every kWmCkTiles tiles: the run positions, where inverse pass 2 resumes the replay
+                const int64_t ti = (t0 - s0) / kWmTile;
+                if (ti % kWmCkTiles == 0) ckpt[((int64_t)cbase[b] + ti / kWmCkTiles) * kWmDig + tid] = lpos[tid];
+            }
             const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
@@ -1089,12 +1104,29 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
     }
 }
 
+// chunks of kWmCkTiles pass-2 tiles per bucket: cbase[b] = first chunk of bucket b (exclusive scan of
+// the chunk counts, one workgroup: nb <= kWmDig)
+__global__ __launch_bounds__(kWmBlock) void k_wm_chunk_base(const uint64_t *__restrict__ bstart, int nb,
+                                                            uint32_t *__restrict__ cbase) {
+    __shared__ uint32_t wsum[kWmBlock / 64];
+    const int b = threadIdx.x;
+    const int64_t rows = b < nb ? (int64_t)(bstart[b + 1] - bstart[b]) : 0;
+    const uint32_t c = (uint32_t)((rows + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles));
+    const uint32_t ex = block_excl_scan1024(c, wsum);
+    if (b < nb) cbase[b] = ex;
+}
+
 // inverse of pass 2: replay each bucket's tiles, gather the results run by run (group order ->
-// pass-1 order)
+// pass-1 order).  The workgroups of one XCD (blockIdx % 8 -- the dispatcher deals workgroups to the 8
+// XCDs in turn) take the chunks of one bucket together, each resuming pass 2's replay at the chunk's
+// checkpoint: a group's 8-row result runs of consecutive tiles share lines, and the bucket's 2 MB of
+// results is then gathered through that XCD's L2 once instead of once per tile (a workgroup per
+// bucket refetched each line for every tile it spans).
 // VAL (value functions): the value bits move beside the flags (res2v -> res1v, staged in LDS).
 template <int DB, bool VAL = false>
-__global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_t *__restrict__ bstart,
-                                                       const uint64_t *__restrict__ pstart, const uint16_t *__restrict__ i_kl,
+__global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == kWmAtomicRank && !VAL ? 8 : 4))) void k_wm2_inv2(WmShape sh, const uint64_t *__restrict__ bstart,
+                                                       const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ ckpt,
+                                                       const uint16_t *__restrict__ i_kl,
                                                        const uint16_t *__restrict__ res2, uint16_t *__restrict__ res1,
                                                        const uint64_t *__restrict__ res2v, uint64_t *__restrict__ res1v) {
     __shared__ WmRankLds R;
@@ -1103,68 +1135,70 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv2(WmShape sh, const uint64_
     __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    const int64_t L = (int64_t)1 << (sh.lb - sh.sb);
     const int dbits = sh.lb - sh.sb;
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, slot = blockIdx.x >> 3;
+    if (slot >= per) return;  // (a grid that is not a multiple of 8)
+    for (int b = xcd; b < sh.nb; b += 8) {
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
-        {
-            const int64_t part = (int64_t)b * L + tid;
-            lpos[tid] = (tid < L && part < sh.nparts) ? (uint32_t)pstart[part] : 0u;
-        }
-        __syncthreads();
-        uint32_t lx[NJ];
-        auto load = [&](int64_t t0) {
+        const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
+        for (int64_t c = slot; c < nch; c += per) {
+            const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
+            lpos[tid] = ckpt[((int64_t)cbase[b] + c) * kWmDig + tid];
+            __syncthreads();
+            uint32_t lx[NJ];
+            auto load = [&](int64_t t0) {
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int64_t i = t0 + woff + j * 64;
-                lx[j] = __builtin_nontemporal_load(i_kl + (i < s1 ? i : s0));
-            }
-        };
-        if (s0 < s1) load(s0);
-        for (int64_t t0 = s0; t0 < s1; t0 += kWmTile) {
-            uint32_t d[NJ], slot[NJ];
-            bool live[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                live[j] = t0 + woff + j * 64 < s1;
-                d[j] = lx[j] >> sh.sb;
-            }
-            if (t0 + kWmTile < s1) load(t0 + kWmTile);
-            const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
-            wm_barrier();
-            const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
-    #pragma unroll 8
-        for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                st_r[s] = res2[src];
-                if (VAL) st_v[s] = res2v[src];
-            }
-            wm_barrier();
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (live[j]) {
-                    __builtin_nontemporal_store(st_r[slot[j]], res1 + t0 + woff + j * 64);
-                    if (VAL) __builtin_nontemporal_store(st_v[slot[j]], res1v + t0 + woff + j * 64);
+                for (int j = 0; j < NJ; ++j) {
+                    const int64_t i = t0 + woff + j * 64;
+                    lx[j] = __builtin_nontemporal_load(i_kl + (i < c1 ? i : c0));
                 }
-            lpos[tid] += tcnt;
-            wm_barrier();
+            };
+            load(c0);
+            for (int64_t t0 = c0; t0 < c1; t0 += kWmTile) {
+                uint32_t d[NJ], slt[NJ];
+                bool live[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    live[j] = t0 + woff + j * 64 < c1;
+                    d[j] = lx[j] >> sh.sb;
+                }
+                if (t0 + kWmTile < c1) load(t0 + kWmTile);
+                const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slt, R);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    if (live[j]) st_d[slt[j]] = (uint16_t)d[j];
+                wm_barrier();
+                const int m = (int)std::min<int64_t>(kWmTile, c1 - t0);
+#pragma unroll 8
+                for (int s = tid; s < m; s += kWmBlock) {
+                    const uint32_t dd = st_d[s];
+                    const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                    st_r[s] = res2[src];
+                    if (VAL) st_v[s] = res2v[src];
+                }
+                wm_barrier();
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    if (live[j]) {
+                        __builtin_nontemporal_store(st_r[slt[j]], res1 + t0 + woff + j * 64);
+                        if (VAL) __builtin_nontemporal_store(st_v[slt[j]], res1v + t0 + woff + j * 64);
+                    }
+                lpos[tid] += tcnt;
+                wm_barrier();
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
-// inverse of pass 1: replay each workgroup's tiles, gather the results run by run and write them in
-// input order as Int64
+// inverse of pass 1: replay pass 1's tiles span by span, chunk by chunk from pass 1's checkpoints,
+// gather the results run by run and write them in input order as Int64
 // VAL = 0: rank functions, out = Int64 results.  VAL = 4 / 8 (value functions): res1 holds valid
 // flags, res1v the value bits (gathered beside them through LDS), written in VAL bytes (zero when
 // NULL) plus a validity byte.
 template <int KES, int DB, int VAL = 0>
-__global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, const uint64_t *__restrict__ base,
+__global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == kWmAtomicRank && !VAL ? 8 : 4))) void k_wm2_inv1(ColRef key, WmShape sh, int nspans, const uint32_t *__restrict__ ckpt,
                                                        const uint16_t *__restrict__ res1, void *__restrict__ out,
                                                        const uint64_t *__restrict__ res1v, uint8_t *__restrict__ valid8) {
     __shared__ WmRankLds R;
@@ -1173,59 +1207,72 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_inv1(ColRef key, WmShape sh, c
     __shared__ uint64_t st_v[VAL ? kWmTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    lpos[tid] = (uint32_t)base[(int64_t)tid * gridDim.x + blockIdx.x];
-    __syncthreads();
     const int dbits = wm_digit_bits(sh.nb);
-    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    uint64_t kv[NJ];
-    auto load = [&](int64_t t0) {
+    // the workgroups of one XCD take the chunks of one pass-1 span together (see k_wm2_inv2)
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
+    if (wslot >= per) return;  // (a grid that is not a multiple of 8)
+    const int64_t cps = wm_span_chunks(sh);
+    for (int w = xcd; w < nspans; w += 8) {
+        const int64_t r0 = (int64_t)w * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
+        const int64_t nch = (r1 - r0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
+        for (int64_t c = wslot; c < nch; c += per) {
+            const int64_t c0 = r0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(r1, c0 + (int64_t)kWmCkTiles * kWmTile);
+            lpos[tid] = ckpt[((int64_t)w * cps + c) * kWmDig + tid];
+            __syncthreads();
+            // the digit needs only the key's low 32 bits: (k - kmin) < 2^24 here, so its low word is
+            // (low word of k) - (low word of kmin) -- half the registers of the prefetched keys
+            uint32_t kv[NJ];
+            auto load = [&](int64_t t0) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int64_t i = t0 + woff + j * 64;
-            kv[j] = wm_ld_nt<KES>(key.values, i < r1 ? i : r0);
-        }
-    };
-    if (r0 < r1) load(r0);
-    for (int64_t t0 = r0; t0 < r1; t0 += kWmTile) {
-        uint32_t d[NJ], slot[NJ];
-        bool live[NJ];
+                for (int j = 0; j < NJ; ++j) {
+                    const int64_t i = t0 + woff + j * 64;
+                    kv[j] = __builtin_nontemporal_load((const uint32_t *)key.values + (i < c1 ? i : c0) * (KES / 4));
+                }
+            };
+            load(c0);
+            for (int64_t t0 = c0; t0 < c1; t0 += kWmTile) {
+                uint32_t d[NJ], slot[NJ];
+                bool live[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            live[j] = t0 + woff + j * 64 < r1;
-            d[j] = (uint32_t)((((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) & sh.kmask) >> sh.lb);
-        }
-        if (t0 + kWmTile < r1) load(t0 + kWmTile);
-        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
+                for (int j = 0; j < NJ; ++j) {
+                    live[j] = t0 + woff + j * 64 < c1;
+                    d[j] = ((kv[j] - (uint32_t)sh.kmin) & (uint32_t)sh.kmask) >> sh.lb;
+                }
+                if (t0 + kWmTile < c1) load(t0 + kWmTile);
+                const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
-        wm_barrier();
-        const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
+                for (int j = 0; j < NJ; ++j)
+                    if (live[j]) st_d[slot[j]] = (uint16_t)d[j];
+                wm_barrier();
+                const int m = (int)std::min<int64_t>(kWmTile, c1 - t0);
 #pragma unroll 8
-        for (int s = tid; s < m; s += kWmBlock) {
-            const uint32_t dd = st_d[s];
-            const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
-            st_r[s] = res1[src];
-            if (VAL) st_v[s] = res1v[src];
-        }
-        wm_barrier();
+                for (int s = tid; s < m; s += kWmBlock) {
+                    const uint32_t dd = st_d[s];
+                    const uint32_t src = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                    st_r[s] = res1[src];
+                    if (VAL) st_v[s] = res1v[src];
+                }
+                wm_barrier();
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            if (!live[j]) continue;
-            const int64_t i = t0 + woff + j * 64;
-            if constexpr (VAL == 0) {
-                __builtin_nontemporal_store((int64_t)st_r[slot[j]], (int64_t *)out + i);
-            } else {
-                const bool ok = st_r[slot[j]] != 0;
-                const uint64_t v = st_v[slot[j]];
-                if constexpr (VAL == 8) __builtin_nontemporal_store(ok ? v : 0ull, (uint64_t *)out + i);
-                else __builtin_nontemporal_store(ok ? (uint32_t)v : 0u, (uint32_t *)out + i);
-                valid8[i] = ok ? 1 : 0;
+                for (int j = 0; j < NJ; ++j) {
+                    if (!live[j]) continue;
+                    const int64_t i = t0 + woff + j * 64;
+                    if constexpr (VAL == 0) {
+                        __builtin_nontemporal_store((int64_t)st_r[slot[j]], (int64_t *)out + i);
+                    } else {
+                        const bool ok = st_r[slot[j]] != 0;
+                        const uint64_t v = st_v[slot[j]];
+                        if constexpr (VAL == 8) __builtin_nontemporal_store(ok ? v : 0ull, (uint64_t *)out + i);
+                        else __builtin_nontemporal_store(ok ? (uint32_t)v : 0u, (uint32_t *)out + i);
+                        valid8[i] = ok ? 1 : 0;
+                    }
+                }
+                lpos[tid] += tcnt;
+                wm_barrier();
             }
+            __syncthreads();
         }
-        lpos[tid] += tcnt;
-        wm_barrier();
     }
 }
 
@@ -1244,11 +1291,14 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int g1 = (int)((n + sh.span - 1) / sh.span);
     const bool value_fn = func >= QEH_WIN_LAG;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2;
+    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2, cbase, ckpt, ckpt1;
+    // inverse pass 2's chunks: at most n / (kWmCkTiles tiles) whole ones plus one partial per bucket
+    const int64_t nck = n / ((int64_t)kWmTile * kWmCkTiles) + sh.nb + 1;
     const int64_t nc1 = (int64_t)kWmDig * g1;
     if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, (n + kWmTile) * 8) || kl1.alloc(ctx, (n + kWmTile) * 2) ||
         key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
-        flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)))
+        flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)) || cbase.alloc(ctx, ((int64_t)sh.nb + 1) * 4) ||
+        ckpt.alloc(ctx, nck * kWmDig * 4) || ckpt1.alloc(ctx, (int64_t)g1 * wm_span_chunks(sh) * kWmDig * 4))
         return fail(QEH_E_OOM, "window: out of device memory");
     const ColRef kc = make_colref(part), oc = make_colref(order);
     const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
@@ -1270,18 +1320,21 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
                                     : (oes == 4 ? QEH_WM_P1(8, 4) : QEH_WM_P1(8, 8)),
                            dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh,
-                           base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
+                           base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), ckpt1.as<uint32_t>());
         // bucket starts = the scanned bases of workgroup 0 per digit, then n
         QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
 #undef QEH_WM_P1
-        if (!sh.exp)  // (experiment runs: pass 1 only)
+        if (!sh.exp) {  // (experiment runs: pass 1 only)
+            hipLaunchKernelGGL(k_wm_chunk_base, dim3(1), dim3(kWmBlock), 0, ctx->stream, bst.as<uint64_t>(), (int)sh.nb,
+                               cbase.as<uint32_t>());
 #define QEH_WM_P2(KS) (at ? k_wm2_pass2<kWmAtomicRank, KS> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10, KS> : k_wm2_pass2<-1, KS>)
-        hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
-                           bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
-                           pst.as<uint64_t>(), ks2.as<uint8_t>());
+            hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
+                               bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
+                               pst.as<uint64_t>(), ks2.as<uint8_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>());
 #undef QEH_WM_P2
+        }
     }
     QEH_HIP(hipGetLastError());
     if (sh.exp) {  // experiment runs stop after the partition passes (their outputs are not valid)
@@ -1373,17 +1426,20 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     {
         KernelTimer kt(ctx, "window_place");
         const bool d10 = sh.lb - sh.sb == 10;
+        // the inverse passes' workgroups, all resident: two per CU where the kernel fits 64 VGPRs
+        // (atomic ranking, rank functions), else one
+        const int ginv = at && !value_fn ? cus * 2 : cus;
         hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : d10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
                                     : (at ? k_wm2_inv2<kWmAtomicRank, false> : d10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
-                           dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), pst.as<uint64_t>(),
-                           kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(), res2v.as<uint64_t>(),
-                           res1v.as<uint64_t>());
+                           dim3(ginv), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), cbase.as<uint32_t>(),
+                           ckpt.as<uint32_t>(), kl1.as<uint16_t>(), res2.as<uint16_t>(), res1.as<uint16_t>(),
+                           res2v.as<uint64_t>(), res1v.as<uint64_t>());
         const bool d1i = wm_digit_bits(sh.nb) == 10;
 #define QEH_WM_I1(V)                                                                                                     \
     (kes == 4 ? (at ? k_wm2_inv1<4, kWmAtomicRank, V> : d1i ? k_wm2_inv1<4, 10, V> : k_wm2_inv1<4, -1, V>)                 \
               : (at ? k_wm2_inv1<8, kWmAtomicRank, V> : d1i ? k_wm2_inv1<8, 10, V> : k_wm2_inv1<8, -1, V>))
-        hipLaunchKernelGGL(!value_fn ? QEH_WM_I1(0) : esz == 8 ? QEH_WM_I1(8) : QEH_WM_I1(4), dim3(g1), dim3(kWmBlock), 0,
-                           ctx->stream, kc, sh, base1.as<uint64_t>(), res1.as<uint16_t>(), out->values,
+        hipLaunchKernelGGL(!value_fn ? QEH_WM_I1(0) : esz == 8 ? QEH_WM_I1(8) : QEH_WM_I1(4), dim3(ginv), dim3(kWmBlock), 0,
+                           ctx->stream, kc, sh, g1, ckpt1.as<uint32_t>(), res1.as<uint16_t>(), out->values,
                            res1v.as<uint64_t>(), valid8.as<uint8_t>());
 #undef QEH_WM_I1
     }
