@@ -10,13 +10,17 @@
 // number of times with run-contiguous writes and no row ids:
 //   1. k_wm_hist1 + k_wm2_pass1: a stable 1024-way partition of (order key, low key bits) by the
 //      key's high bits (per-workgroup histograms, one scan, ballot-ranked LDS-staged runs);
-//   2. k_wm2_pass2: inside each bucket a stable partition by the key's low bits -- every PARTITION
-//      BY group is now contiguous (in input order), its start in pstart[];
+//   2. k_wm2_chunk_hist + k_wm2_chunk_scan + k_wm2_pass2: inside each bucket a stable partition by
+//      the key's low bits, chunk by chunk (two tiles each, the chunks of one bucket taken together by
+//      one XCD's workgroups) -- every PARTITION BY group is now contiguous (in input order), its
+//      start in pstart[];
 //   3. k_wm2_csort_wg: a workgroup per group ranks its rows by counting sort (exact ties by
 //      position in the group = input order) and writes the function's value at each row's own
 //      position; groups whose keys cluster go to the bitonic network kernel (k_wm2_sort);
 //   4. k_wm2_inv2 / k_wm2_inv1: the two partitions are replayed (the ranking is deterministic) and
-//      the results gathered back run by run, into pass-1 order and then input order.
+//      the results gathered back run by run, into pass-1 order and then input order -- chunk by
+//      chunk from the run positions both passes checkpoint every two tiles, one XCD's workgroups
+//      on neighbouring chunks, so the short result runs are gathered through that XCD's L2.
 // Value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column) carry the value
 // bits beside a valid flag.  Groups above 2048 rows (skew) and shapes outside the limits return
 // kWindowMsdNotEligible and the caller takes the LSD path.
@@ -495,13 +499,72 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
     }
 }
 
-// pass 2: inside each bucket, stable partition by the low digit; group starts -> pstart
+// Pass 2 by chunks of kWmCkTiles tiles (default): the workgroups of one XCD partition consecutive
+// chunks of one bucket together, so a group's runs from neighbouring chunks -- adjacent in the output
+// -- are written into the same L2 at about the same time, and each chunk starts from run positions
+// that k_wm2_chunk_hist + k_wm2_chunk_scan computed ahead (rows per group and chunk, then a scan over
+// the bucket's chunks).  Those positions are also inverse pass 2's checkpoints.
+
+// rows per low digit of each chunk (u16: a chunk holds <= kWmCkTiles * kWmTile = 16384 rows)
+__global__ __launch_bounds__(kWmBlock) void k_wm2_chunk_hist(WmShape sh, const uint64_t *__restrict__ bstart,
+                                                             const uint32_t *__restrict__ cbase,
+                                                             const uint16_t *__restrict__ i_kl, uint16_t *__restrict__ ccnt) {
+    __shared__ uint32_t h[kWmDig];
+    const int tid = threadIdx.x, sbits = sh.sb;
+    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
+        const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
+        const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
+        for (int64_t c = 0; c < nch; ++c) {
+            const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
+            h[tid] = 0;
+            __syncthreads();
+            // 8 digits per 16-B load over the aligned body, single loads at the edges
+            const int64_t a0 = std::min<int64_t>(c1, (c0 + 7) & ~(int64_t)7), a1 = std::max<int64_t>(a0, c1 & ~(int64_t)7);
+            for (int64_t i = c0 + tid; i < a0; i += kWmBlock) atomicAdd(&h[i_kl[i] >> sbits], 1u);
+            for (int64_t i = a1 + tid; i < c1; i += kWmBlock) atomicAdd(&h[i_kl[i] >> sbits], 1u);
+            for (int64_t i = a0 + (int64_t)tid * 8; i < a1; i += (int64_t)kWmBlock * 8) {
+                const v4u32w w = __builtin_nontemporal_load((const v4u32w *)(i_kl + i));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    atomicAdd(&h[(w[q] & 0xFFFFu) >> sbits], 1u);
+                    atomicAdd(&h[(w[q] >> 16) >> sbits], 1u);
+                }
+            }
+            __syncthreads();
+            ccnt[((int64_t)cbase[b] + c) * kWmDig + tid] = (uint16_t)h[tid];
+            __syncthreads();
+        }
+    }
+}
+
+// per bucket (one workgroup each): group starts -> pstart, and every chunk's run positions -> ckpt
+__global__ __launch_bounds__(kWmBlock) void k_wm2_chunk_scan(WmShape sh, const uint64_t *__restrict__ bstart,
+                                                             const uint32_t *__restrict__ cbase,
+                                                             const uint16_t *__restrict__ ccnt, uint32_t *__restrict__ ckpt,
+                                                             uint64_t *__restrict__ pstart) {
+    __shared__ uint32_t wsum[kWmBlock / 64];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const int64_t L = (int64_t)1 << (sh.lb - sh.sb);
+    const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
+    const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
+    const int64_t base = cbase[b];
+    uint32_t tot = 0;
+    for (int64_t c = 0; c < nch; ++c) tot += ccnt[(base + c) * kWmDig + tid];
+    const uint32_t ex = block_excl_scan1024(tot, wsum);
+    const int64_t part = (int64_t)b * L + tid;
+    if (tid < L && part < sh.nparts) pstart[part] = (uint64_t)(s0 + ex);
+    uint32_t pos = (uint32_t)(s0 + ex);
+    for (int64_t c = 0; c < nch; ++c) {
+        ckpt[(base + c) * kWmDig + tid] = pos;
+        pos += ccnt[(base + c) * kWmDig + tid];
+    }
+}
+
 template <int DB, bool KS>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
-                                                        const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
-                                                        uint64_t *__restrict__ o_key, uint64_t *__restrict__ pstart,
-                                                        uint8_t *__restrict__ o_ks, const uint32_t *__restrict__ cbase,
-                                                        uint32_t *__restrict__ ckpt) {
+                                                         const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ ckpt,
+                                                         const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
+                                                         uint64_t *__restrict__ o_key, uint8_t *__restrict__ o_ks) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
@@ -509,97 +572,77 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
     const int sbits = sh.sb;
-    const int64_t L = (int64_t)1 << (sh.lb - sbits);
     const int dbits = sh.lb - sbits;
-    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    for (int b = blockIdx.x; b < sh.nb; b += gridDim.x) {
+    const int woff = wave * 64 * NJ + lane;
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
+    if (wslot >= per) return;  // (a grid that is not a multiple of 8)
+    for (int b = xcd; b < sh.nb; b += 8) {
         const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
-        R.lofs[tid] = 0;
-        __syncthreads();
-        {  // the bucket's low-digit counts: 8 digits per 16-B load, aligned body, scalar edges
-            const int64_t a0 = std::min<int64_t>(s1, (s0 + 7) & ~(int64_t)7), a1 = std::max<int64_t>(a0, s1 & ~(int64_t)7);
-            for (int64_t i = s0 + tid; i < a0; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i] >> sbits], 1u);
-            for (int64_t i = a1 + tid; i < s1; i += kWmBlock) atomicAdd(&R.lofs[i_kl[i] >> sbits], 1u);
-            for (int64_t i = a0 + (int64_t)tid * 8; i < a1; i += (int64_t)kWmBlock * 8) {
-                const v4u32w w = __builtin_nontemporal_load((const v4u32w *)(i_kl + i));
+        const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
+        for (int64_t c = wslot; c < nch; c += per) {
+            const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
+            lpos[tid] = ckpt[((int64_t)cbase[b] + c) * kWmDig + tid];
+            __syncthreads();
+            uint64_t kx[NJ];
+            uint32_t lx[NJ];
+            // one base address, the rows at immediate offsets; a tile may read past the chunk (and past
+            // n: i_key / i_kl carry kWmTile rows of padding) -- those rows are not live
+            auto load = [&](int64_t t0) {
+                const uint64_t *pk = i_key + t0 + woff;
+                const uint16_t *pl = i_kl + t0 + woff;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    atomicAdd(&R.lofs[(w[q] & 0xFFFFu) >> sbits], 1u);
-                    atomicAdd(&R.lofs[(w[q] >> 16) >> sbits], 1u);
-                }
-            }
-        }
-        __syncthreads();
-        {
-            const uint32_t ex = block_excl_scan1024(R.lofs[tid], R.wsum);
-            const int64_t part = (int64_t)b * L + tid;
-            if (tid < L && part < sh.nparts) pstart[part] = (uint64_t)(s0 + ex);
-            lpos[tid] = (uint32_t)(s0 + ex);
-        }
-        __syncthreads();
-        uint64_t kx[NJ];
-        uint32_t lx[NJ];
-        // one base address, the rows at immediate offsets; a tile may read past the bucket (and past
-        // n: i_key / i_kl carry kWmTile rows of padding) -- those rows are not live
-        auto load = [&](int64_t t0) {
-            const uint64_t *pk = i_key + t0 + woff;
-            const uint16_t *pl = i_kl + t0 + woff;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) kx[j] = pk[j * 64], lx[j] = pl[j * 64];
-        };
-        // FULL tiles store unconditionally (see k_wm2_pass1: exact vmcnt accounting)
-        auto tile = [&](int64_t t0, auto fullc) {
-            constexpr bool FULL = decltype(fullc)::value;
-            uint32_t d[NJ], slot[NJ];
-            uint64_t keys[NJ];
-            bool live[NJ];
-            uint32_t ksub[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                live[j] = FULL || t0 + woff + j * 64 < s1;
-                d[j] = KS ? lx[j] >> sbits : lx[j];
-                ksub[j] = KS ? lx[j] & ((1u << sbits) - 1u) : 0u;
-                keys[j] = kx[j];
-            }
-            if (t0 + kWmTile < s1) load(t0 + kWmTile);
-            {  // every kWmCkTiles tiles: the run positions, where inverse pass 2 resumes the replay
-                const int64_t ti = (t0 - s0) / kWmTile;
-                if (ti % kWmCkTiles == 0) ckpt[((int64_t)cbase[b] + ti / kWmCkTiles) * kWmDig + tid] = lpos[tid];
-            }
-            const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                if (!live[j]) continue;
-                st_key[slot[j]] = keys[j];
-                st_d[slot[j]] = (uint16_t)(d[j] | (ksub[j] << 10));  // digit (10 bits) | sub-key (<= 4 bits)
-            }
-            wm_barrier();
-            auto put = [&](int s) {
-                const uint32_t dd = st_d[s] & 1023u;
-                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                o_key[p] = st_key[s];
-                if constexpr (KS) o_ks[p] = (uint8_t)(st_d[s] >> 10);
+                for (int j = 0; j < NJ; ++j) kx[j] = pk[j * 64], lx[j] = pl[j * 64];
             };
-            if constexpr (FULL) {
+            // FULL tiles store unconditionally (see k_wm2_pass1: exact vmcnt accounting)
+            auto tile = [&](int64_t t0, auto fullc) {
+                constexpr bool FULL = decltype(fullc)::value;
+                uint32_t d[NJ], slot[NJ];
+                uint64_t keys[NJ];
+                bool live[NJ];
+                uint32_t ksub[NJ];
 #pragma unroll
-                for (int q = 0; q < NJ; ++q) put(tid + q * kWmBlock);
+                for (int j = 0; j < NJ; ++j) {
+                    live[j] = FULL || woff + j * 64 < (int)(c1 - t0);
+                    d[j] = KS ? lx[j] >> sbits : lx[j];
+                    ksub[j] = KS ? lx[j] & ((1u << sbits) - 1u) : 0u;
+                    keys[j] = kx[j];
+                }
+                if (t0 + kWmTile < c1) load(t0 + kWmTile);
+                const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    if (!live[j]) continue;
+                    st_key[slot[j]] = keys[j];
+                    st_d[slot[j]] = (uint16_t)(d[j] | (ksub[j] << 10));  // digit (10 bits) | sub-key (<= 4 bits)
+                }
+                wm_barrier();
+                auto put = [&](int s) {
+                    const uint32_t dd = st_d[s] & 1023u;
+                    const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                    o_key[p] = st_key[s];
+                    if constexpr (KS) o_ks[p] = (uint8_t)(st_d[s] >> 10);
+                };
+                if constexpr (FULL) {
+#pragma unroll
+                    for (int q = 0; q < NJ; ++q) put(tid + q * kWmBlock);
+                } else {
+                    const int m = (int)std::min<int64_t>(kWmTile, c1 - t0);
+                    for (int s = tid; s < m; s += kWmBlock) put(s);
+                }
+                wm_barrier();
+                lpos[tid] += tcnt;
+            };
+            load(c0);
+            if (c1 - c0 >= kWmTile) {
+                tile(c0, std::true_type{});
+                int64_t t0 = c0 + kWmTile;
+                for (; t0 + kWmTile <= c1; t0 += kWmTile) tile(t0, std::true_type{});
+                if (t0 < c1) tile(t0, std::false_type{});
             } else {
-                const int m = (int)std::min<int64_t>(kWmTile, s1 - t0);
-                for (int s = tid; s < m; s += kWmBlock) put(s);
+                tile(c0, std::false_type{});
             }
-            wm_barrier();
-            lpos[tid] += tcnt;
-        };
-        if (s0 < s1) load(s0);
-        if (s1 - s0 >= kWmTile) {
-            tile(s0, std::true_type{});
-            int64_t t0 = s0 + kWmTile;
-            for (; t0 + kWmTile <= s1; t0 += kWmTile) tile(t0, std::true_type{});
-            if (t0 < s1) tile(t0, std::false_type{});
-        } else if (s0 < s1) {
-            tile(s0, std::false_type{});
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
@@ -1305,9 +1348,6 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int oes = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
     // stable tile ranking by LDS atomics (default) or by ballot matching (QEH_WM_BALLOT=1, A/B)
     const bool at = std::getenv("QEH_WM_BALLOT") == nullptr && lds_atomic_rank_ok(ctx);
-    int gbx = 2;  // bucket workgroups per CU (pass 2 / its inverse)
-    if (const char *e = std::getenv("QEH_WM_GBX")) gbx = std::max(1, std::atoi(e));
-    const int gb = std::min(cus * gbx, sh.nb);
     {
         KernelTimer kt(ctx, "window_partition");
         const uint32_t *counts = pre_counts ? pre_counts->as<uint32_t>() : cnt1.as<uint32_t>();
@@ -1329,11 +1369,19 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         if (!sh.exp) {  // (experiment runs: pass 1 only)
             hipLaunchKernelGGL(k_wm_chunk_base, dim3(1), dim3(kWmBlock), 0, ctx->stream, bst.as<uint64_t>(), (int)sh.nb,
                                cbase.as<uint32_t>());
+            {
+                DevBuf ccnt;
+                QEH_TRY(ccnt.alloc(ctx, nck * kWmDig * 2));
+                hipLaunchKernelGGL(k_wm2_chunk_hist, dim3(sh.nb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(),
+                                   cbase.as<uint32_t>(), kl1.as<uint16_t>(), ccnt.as<uint16_t>());
+                hipLaunchKernelGGL(k_wm2_chunk_scan, dim3(sh.nb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(),
+                                   cbase.as<uint32_t>(), ccnt.as<uint16_t>(), ckpt.as<uint32_t>(), pst.as<uint64_t>());
 #define QEH_WM_P2(KS) (at ? k_wm2_pass2<kWmAtomicRank, KS> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10, KS> : k_wm2_pass2<-1, KS>)
-            hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(gb), dim3(kWmBlock), 0, ctx->stream, sh,
-                               bst.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), key2.as<uint64_t>(),
-                               pst.as<uint64_t>(), ks2.as<uint8_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>());
+                hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(cus), dim3(kWmBlock), 0, ctx->stream,
+                                   sh, bst.as<uint64_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>(), key1.as<uint64_t>(),
+                                   kl1.as<uint16_t>(), key2.as<uint64_t>(), ks2.as<uint8_t>());
 #undef QEH_WM_P2
+            }
         }
     }
     QEH_HIP(hipGetLastError());
