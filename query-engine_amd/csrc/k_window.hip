@@ -505,6 +505,20 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, 
 // that k_wm2_chunk_hist + k_wm2_chunk_scan computed ahead (rows per group and chunk, then a scan over
 // the bucket's chunks).  Those positions are also inverse pass 2's checkpoints.
 
+// Chunk ids are dealt per XCD: XCD x (blockIdx % 8 -- the dispatcher deals workgroups to the XCDs in
+// turn) takes buckets [x nb / 8, (x + 1) nb / 8), whose chunks are consecutive ids, and its
+// workgroups take every per-th id, so neighbouring chunks run side by side in one L2 however many
+// chunks a bucket has.  The bucket of chunk j: the last b with cbase[b] <= j (empty buckets share
+// their successor's base and lose to it).
+__device__ __forceinline__ int wm_chunk_bucket(const uint32_t *__restrict__ cbase, int lo, int hi, int64_t j) {
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int64_t)cbase[mid] <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 // rows per low digit of each chunk (u16: a chunk holds <= kWmCkTiles * kWmTile = 16384 rows)
 __global__ __launch_bounds__(kWmBlock) void k_wm2_chunk_hist(WmShape sh, const uint64_t *__restrict__ bstart,
                                                              const uint32_t *__restrict__ cbase,
@@ -576,12 +590,13 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     const int woff = wave * 64 * NJ + lane;
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
-    for (int b = xcd; b < sh.nb; b += 8) {
-        const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
-        const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
-        for (int64_t c = wslot; c < nch; c += per) {
+    const int b_lo = (int)((int64_t)xcd * sh.nb / 8), b_hi = (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    if (b_lo < b_hi) {
+        for (int64_t jc = (int64_t)cbase[b_lo] + wslot; jc < (int64_t)cbase[b_hi]; jc += per) {
+            const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
+            const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
-            lpos[tid] = ckpt[((int64_t)cbase[b] + c) * kWmDig + tid];
+            lpos[tid] = ckpt[jc * kWmDig + tid];
             __syncthreads();
             uint64_t kx[NJ];
             uint32_t lx[NJ];
@@ -1148,7 +1163,7 @@ __global__ __launch_bounds__(256, E == 4 ? 5 : 2) void k_wm2_csort_wg(WmShape sh
 }
 
 // chunks of kWmCkTiles pass-2 tiles per bucket: cbase[b] = first chunk of bucket b (exclusive scan of
-// the chunk counts, one workgroup: nb <= kWmDig)
+// the chunk counts, one workgroup: nb <= kWmDig), cbase[nb] = all chunks
 __global__ __launch_bounds__(kWmBlock) void k_wm_chunk_base(const uint64_t *__restrict__ bstart, int nb,
                                                             uint32_t *__restrict__ cbase) {
     __shared__ uint32_t wsum[kWmBlock / 64];
@@ -1157,6 +1172,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_chunk_base(const uint64_t *__re
     const uint32_t c = (uint32_t)((rows + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles));
     const uint32_t ex = block_excl_scan1024(c, wsum);
     if (b < nb) cbase[b] = ex;
+    if (b == nb - 1) cbase[nb] = ex + c;
 }
 
 // inverse of pass 2: replay each bucket's tiles, gather the results run by run (group order ->
@@ -1182,12 +1198,13 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, slot = blockIdx.x >> 3;
     if (slot >= per) return;  // (a grid that is not a multiple of 8)
-    for (int b = xcd; b < sh.nb; b += 8) {
-        const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1];
-        const int64_t nch = (s1 - s0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
-        for (int64_t c = slot; c < nch; c += per) {
+    const int b_lo = (int)((int64_t)xcd * sh.nb / 8), b_hi = (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    if (b_lo < b_hi) {
+        for (int64_t jc = (int64_t)cbase[b_lo] + slot; jc < (int64_t)cbase[b_hi]; jc += per) {
+            const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
+            const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
-            lpos[tid] = ckpt[((int64_t)cbase[b] + c) * kWmDig + tid];
+            lpos[tid] = ckpt[jc * kWmDig + tid];
             __syncthreads();
             uint32_t lx[NJ];
             auto load = [&](int64_t t0) {
@@ -1256,12 +1273,15 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
     const int64_t cps = wm_span_chunks(sh);
-    for (int w = xcd; w < nspans; w += 8) {
-        const int64_t r0 = (int64_t)w * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-        const int64_t nch = (r1 - r0 + (int64_t)kWmTile * kWmCkTiles - 1) / ((int64_t)kWmTile * kWmCkTiles);
-        for (int64_t c = wslot; c < nch; c += per) {
+    // XCD x takes spans [x nspans / 8, (x + 1) nspans / 8), chunk ids w * cps + c, every per-th id
+    const int64_t j_lo = (int64_t)xcd * nspans / 8 * cps, j_hi = (int64_t)(xcd + 1) * nspans / 8 * cps;
+    {
+        for (int64_t jc = j_lo + wslot; jc < j_hi; jc += per) {
+            const int64_t w = jc / cps, c = jc - w * cps;
+            const int64_t r0 = w * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
             const int64_t c0 = r0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(r1, c0 + (int64_t)kWmCkTiles * kWmTile);
-            lpos[tid] = ckpt[((int64_t)w * cps + c) * kWmDig + tid];
+            if (c0 >= c1) continue;  // (the last span's unused chunk ids)
+            lpos[tid] = ckpt[jc * kWmDig + tid];
             __syncthreads();
             // the digit needs only the key's low 32 bits: (k - kmin) < 2^24 here, so its low word is
             // (low word of k) - (low word of kmin) -- half the registers of the prefetched keys
