@@ -103,6 +103,7 @@ struct WmShape {
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
     int32_t exp;       // QEH_WM_EXP != 0 (experiments: time pass 1 alone; the query then fails)
+    int32_t spread;    // QEH_WM_SPREAD=1 (A/B): chunked passes take chunk ids round-robin over the grid
 };
 
 // inverse-pass chunks of kWmCkTiles tiles per pass-1 row span (sh.span is a multiple of kWmTile)
@@ -590,9 +591,10 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     const int woff = wave * 64 * NJ + lane;
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
-    const int b_lo = (int)((int64_t)xcd * sh.nb / 8), b_hi = (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    const int b_lo = sh.spread ? 0 : (int)((int64_t)xcd * sh.nb / 8), b_hi = sh.spread ? sh.nb : (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
     if (b_lo < b_hi) {
-        for (int64_t jc = (int64_t)cbase[b_lo] + wslot; jc < (int64_t)cbase[b_hi]; jc += per) {
+        for (int64_t jc = (int64_t)cbase[b_lo] + j0; jc < (int64_t)cbase[b_hi]; jc += js) {
             const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
             const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
@@ -1198,9 +1200,10 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, slot = blockIdx.x >> 3;
     if (slot >= per) return;  // (a grid that is not a multiple of 8)
-    const int b_lo = (int)((int64_t)xcd * sh.nb / 8), b_hi = (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    const int b_lo = sh.spread ? 0 : (int)((int64_t)xcd * sh.nb / 8), b_hi = sh.spread ? sh.nb : (int)((int64_t)(xcd + 1) * sh.nb / 8);
+    const int64_t j0 = sh.spread ? blockIdx.x : slot, js = sh.spread ? gridDim.x : per;
     if (b_lo < b_hi) {
-        for (int64_t jc = (int64_t)cbase[b_lo] + slot; jc < (int64_t)cbase[b_hi]; jc += per) {
+        for (int64_t jc = (int64_t)cbase[b_lo] + j0; jc < (int64_t)cbase[b_hi]; jc += js) {
             const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
             const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
@@ -1274,9 +1277,10 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
     const int64_t cps = wm_span_chunks(sh);
     // XCD x takes spans [x nspans / 8, (x + 1) nspans / 8), chunk ids w * cps + c, every per-th id
-    const int64_t j_lo = (int64_t)xcd * nspans / 8 * cps, j_hi = (int64_t)(xcd + 1) * nspans / 8 * cps;
+    const int64_t j_lo = sh.spread ? 0 : (int64_t)xcd * nspans / 8 * cps, j_hi = sh.spread ? (int64_t)nspans * cps : (int64_t)(xcd + 1) * nspans / 8 * cps;
+    const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
     {
-        for (int64_t jc = j_lo + wslot; jc < j_hi; jc += per) {
+        for (int64_t jc = j_lo + j0; jc < j_hi; jc += js) {
             const int64_t w = jc / cps, c = jc - w * cps;
             const int64_t r0 = w * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
             const int64_t c0 = r0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(r1, c0 + (int64_t)kWmCkTiles * kWmTile);
@@ -1604,6 +1608,7 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         sh.nparts = (int64_t)1 << 20;
     }
     if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
+    sh.spread = std::getenv("QEH_WM_SPREAD") ? 1 : 0;
     return window_noid(ctx, func, part, order, asc, param, dflt, sh, out, folded ? &pre : nullptr);
 }
 
