@@ -1,5 +1,7 @@
 #!/bin/bash
 # pass-1 counters, scattered (EXP=16) vs coalesced (EXP=48) run writes
+# (the coalesced variant, QEH_WM_EXP bit 32, and the workgroup-major layout, bit 64, were experiment-only
+#  kernel paths, removed after this measurement: profiles/r05/cfg5_pass1_counters.txt holds the results)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() { # tag exp counters...

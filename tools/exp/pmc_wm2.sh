@@ -1,5 +1,6 @@
 #!/bin/bash
 # pass-1 translation counters: digit-major (EXP=16) vs workgroup-major (EXP=80) run layout
+# (QEH_WM_EXP bit 64, the workgroup-major layout, was an experiment-only kernel path, since removed)
 set -e
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
