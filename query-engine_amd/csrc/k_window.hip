@@ -106,107 +106,115 @@ struct WmShape {
     int32_t spread;    // QEH_WM_SPREAD=1 (A/B): chunked passes take chunk ids round-robin over the grid
 };
 
-// inverse-pass chunks of kWmCkTiles tiles per pass-1 row span (sh.span is a multiple of kWmTile)
-__host__ __device__ __forceinline__ int64_t wm_span_chunks(const WmShape &sh) {
-    return (sh.span / kWmTile + kWmCkTiles - 1) / kWmCkTiles;
-}
+// Pass 1 and its inverse run by chunks of kWmCkTiles tiles of the input (kWmChunk rows; the histogram
+// spans, sh.span, are whole chunks): per-chunk digit counts -> a scan over the chunks per digit gives
+// every chunk its run positions ahead of pass 1 (and inverse pass 1 its checkpoints).
+constexpr int64_t kWmChunk = (int64_t)kWmTile * kWmCkTiles;
+constexpr int kWmScanB = 256;  // chunks per block of the chunk scan
 
-// ---- pass 1: histogram of the high key digit per workgroup row range -------------------------
-template <int KES>
-__global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, uint32_t *__restrict__ counts) {
+// ---- pass 1: histogram of the high key digit per chunk ------------------------------------------
+// One workgroup per span of whole chunks, the chunks in turn: counts[chunk][digit] (u16, a chunk holds
+// <= kWmChunk = 16384 rows).  MM: also the key's min / max (per-workgroup partials) in the same read:
+// the histogram is then taken on the key mod 2^20 (kmin = 0, kmask = 2^20 - 1, 1024 digits of 10
+// bits), which is pass 1's digit for every key range of 2^19 .. 2^20 keys (config 5's shape) whatever
+// its minimum; other ranges histogram again with their own shape (MM = false).
+struct WmMinMax {
+    int64_t mn, mx;
+};
+template <int KES, bool MM>
+__global__ __launch_bounds__(kWmBlock) void k_wm_hist1(ColRef key, WmShape sh, uint16_t *__restrict__ counts,
+                                                       WmMinMax *__restrict__ part) {
     __shared__ uint32_t h[kWmDig];
-    h[threadIdx.x] = 0;
-    __syncthreads();
+    __shared__ int64_t smn[kWmBlock / 64], smx[kWmBlock / 64];
     const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
     // 16-B loads (KES = 8: two keys, KES = 4: four) over the 16-B-aligned body, scalar edges
     constexpr int PER = 16 / KES, U = 4;  // keys per load, loads in flight per thread
     const char *kp = (const char *)key.values;
-    int64_t a0 = r0;
-    while (a0 < r1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
-    const int64_t body = (r1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
-    auto one = [&](uint64_t raw) {
-        const uint64_t kk = ((uint64_t)wm_key_val(raw, key.dtype) - (uint64_t)sh.kmin) & sh.kmask;
-        atomicAdd(&h[kk >> sh.lb], 1u);
-    };
-    for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
-        v4u32w w[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load((const v4u32w *)(kp + (i + (int64_t)u * kWmBlock * PER) * KES));
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if constexpr (KES == 8) {
-                one((uint64_t)w[u][0] | ((uint64_t)w[u][1] << 32));
-                one((uint64_t)w[u][2] | ((uint64_t)w[u][3] << 32));
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) one((uint64_t)w[u][q]);
-            }
-        }
-    }
-    for (int64_t i = r0 + threadIdx.x; i < a0; i += kWmBlock) one(wm_ld<KES>(key.values, i));
-    for (int64_t i = a0 + body + threadIdx.x; i < r1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
-    __syncthreads();
-    counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
-}
-
-// The key's min / max (per-workgroup partials) and pass 1's histogram in one read of the key: the
-// histogram is taken on the key mod 2^20 (kmin = 0, kmask = 2^20 - 1, 1024 digits of 10 bits), which
-// is pass 1's digit for every key range of 2^19 .. 2^20 keys (config 5's shape) whatever its minimum;
-// other ranges histogram again with their own shape.
-struct WmMinMax {
-    int64_t mn, mx;
-};
-template <int KES>
-__global__ __launch_bounds__(kWmBlock) void k_wm_minmax_hist1(ColRef key, WmShape sh, uint32_t *__restrict__ counts,
-                                                              WmMinMax *__restrict__ part) {
-    __shared__ uint32_t h[kWmDig];
-    __shared__ int64_t smn[kWmBlock / 64], smx[kWmBlock / 64];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-    constexpr int PER = 16 / KES, U = 4;
-    const char *kp = (const char *)key.values;
-    int64_t a0 = r0;
-    while (a0 < r1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
-    const int64_t body = (r1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     auto one = [&](uint64_t raw) {
         const int64_t x = wm_key_val(raw, key.dtype);
-        mn = x < mn ? x : mn;
-        mx = x > mx ? x : mx;
+        if constexpr (MM) {
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
         atomicAdd(&h[(((uint64_t)x - (uint64_t)sh.kmin) & sh.kmask) >> sh.lb], 1u);
     };
-    for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
-        v4u32w w[U];
+    for (int64_t c0 = r0; c0 < r1; c0 += kWmChunk) {
+        const int64_t c1 = std::min<int64_t>(r1, c0 + kWmChunk);
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        int64_t a0 = c0;
+        while (a0 < c1 && (((uintptr_t)(kp + a0 * KES)) & 15)) ++a0;
+        const int64_t body = (c1 - a0) / (PER * U * kWmBlock) * (PER * U * kWmBlock);
+        for (int64_t i = a0 + (int64_t)threadIdx.x * PER; i < a0 + body; i += (int64_t)kWmBlock * PER * U) {
+            v4u32w w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load((const v4u32w *)(kp + (i + (int64_t)u * kWmBlock * PER) * KES));
+            for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load((const v4u32w *)(kp + (i + (int64_t)u * kWmBlock * PER) * KES));
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if constexpr (KES == 8) {
-                one((uint64_t)w[u][0] | ((uint64_t)w[u][1] << 32));
-                one((uint64_t)w[u][2] | ((uint64_t)w[u][3] << 32));
-            } else {
+            for (int u = 0; u < U; ++u) {
+                if constexpr (KES == 8) {
+                    one((uint64_t)w[u][0] | ((uint64_t)w[u][1] << 32));
+                    one((uint64_t)w[u][2] | ((uint64_t)w[u][3] << 32));
+                } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) one((uint64_t)w[u][q]);
+                    for (int q = 0; q < 4; ++q) one((uint64_t)w[u][q]);
+                }
             }
         }
+        for (int64_t i = c0 + threadIdx.x; i < a0; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+        for (int64_t i = a0 + body + threadIdx.x; i < c1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+        __syncthreads();
+        counts[(c0 / kWmChunk) * kWmDig + threadIdx.x] = (uint16_t)h[threadIdx.x];
+        __syncthreads();
     }
-    for (int64_t i = r0 + threadIdx.x; i < a0; i += kWmBlock) one(wm_ld<KES>(key.values, i));
-    for (int64_t i = a0 + body + threadIdx.x; i < r1; i += kWmBlock) one(wm_ld<KES>(key.values, i));
+    if constexpr (MM) {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) smn[wave] = mn, smx[wave] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 0; w < kWmBlock / 64; ++w) mn = smn[w] < mn ? smn[w] : mn, mx = smx[w] > mx ? smx[w] : mx;
+            part[blockIdx.x] = WmMinMax{mn, mx};
+        }
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) smn[wave] = mn, smx[wave] = mx;
-    __syncthreads();
-    counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];  // digit-major
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kWmBlock / 64; ++w) mn = smn[w] < mn ? smn[w] : mn, mx = smx[w] > mx ? smx[w] : mx;
-        mn = smn[0] < mn ? smn[0] : mn, mx = smx[0] > mx ? smx[0] : mx;
-        part[blockIdx.x] = WmMinMax{mn, mx};
+}
+
+// The chunk scan, in three steps over blocks of kWmScanB chunks: (1) per block, rows per digit;
+// (2) one workgroup: per digit the blocks' exclusive prefix and its total, then the digits' starts
+// (bucket starts -> bst); (3) per block, every chunk's run positions -> cpos[chunk][digit].
+__global__ __launch_bounds__(kWmBlock) void k_wm_cscan_blocks(const uint16_t *__restrict__ counts, int64_t nchunk,
+                                                              uint32_t *__restrict__ bsum) {
+    const int64_t c0 = (int64_t)blockIdx.x * kWmScanB, c1 = std::min<int64_t>(nchunk, c0 + kWmScanB);
+    uint32_t t = 0;
+    for (int64_t c = c0; c < c1; ++c) t += counts[c * kWmDig + threadIdx.x];
+    bsum[(int64_t)blockIdx.x * kWmDig + threadIdx.x] = t;
+}
+__global__ __launch_bounds__(kWmBlock) void k_wm_cscan_top(uint32_t *__restrict__ bsum, int nblk, int nb,
+                                                           uint32_t *__restrict__ dstart, uint64_t *__restrict__ bst) {
+    __shared__ uint32_t wsum[kWmBlock / 64];
+    uint32_t run = 0;
+    for (int b = 0; b < nblk; ++b) {
+        const uint32_t v = bsum[(int64_t)b * kWmDig + threadIdx.x];
+        bsum[(int64_t)b * kWmDig + threadIdx.x] = run;  // -> the block's exclusive prefix
+        run += v;
+    }
+    const uint32_t ex = block_excl_scan1024(run, wsum);
+    dstart[threadIdx.x] = ex;
+    if ((int)threadIdx.x < nb) bst[threadIdx.x] = ex;
+}
+__global__ __launch_bounds__(kWmBlock) void k_wm_cscan_pos(const uint16_t *__restrict__ counts, int64_t nchunk,
+                                                           const uint32_t *__restrict__ bsum,
+                                                           const uint32_t *__restrict__ dstart, uint32_t *__restrict__ cpos) {
+    const int64_t c0 = (int64_t)blockIdx.x * kWmScanB, c1 = std::min<int64_t>(nchunk, c0 + kWmScanB);
+    uint32_t pos = dstart[threadIdx.x] + bsum[(int64_t)blockIdx.x * kWmDig + threadIdx.x];
+    for (int64_t c = c0; c < c1; ++c) {
+        cpos[c * kWmDig + threadIdx.x] = pos;
+        pos += counts[c * kWmDig + threadIdx.x];
     }
 }
 
@@ -408,95 +416,135 @@ __host__ __device__ __forceinline__ int wm_digit_bits(int64_t ndig) {
     return b;
 }
 
-// pass 1: stable 2^dbits-way partition of (order key, low key bits) by the high key digit
+// pass 1: stable 2^dbits-way partition of (order key, low key bits) by the high key digit, by chunks
+// of the input, each from its precomputed run positions (cpos).  XCD x (blockIdx % 8) owns chunk ids
+// [x nchunk / 8, (x + 1) nchunk / 8) and its workgroups claim them in order from one counter
+// (claim[x]), so the chunks in flight on an XCD are always a window of consecutive ones: a digit's
+// runs from neighbouring chunks are adjacent in the output and reach that XCD's L2 close in time.
+// (Static striding let the workgroups drift thousands of chunks apart.)
 template <int KES, int OES, int DB>
-__global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, int asc, WmShape sh,
-                                                        const uint64_t *__restrict__ base, uint64_t *__restrict__ o_key,
-                                                        uint16_t *__restrict__ o_kl, uint32_t *__restrict__ ckpt) {
+__global__ __launch_bounds__(kWmBlock) void k_wm2_pass1(ColRef key, ColRef ord, int asc, WmShape sh, int64_t nchunk,
+                                                        const uint32_t *__restrict__ cpos, uint32_t *__restrict__ claim,
+                                                        uint64_t *__restrict__ o_key, uint16_t *__restrict__ o_kl) {
     __shared__ WmRankLds R;
     __shared__ uint32_t lpos[kWmDig];  // run positions (< n < 2^32: window_msd's bound)
     __shared__ uint64_t st_key[kWmTile];
     __shared__ uint16_t st_kl[kWmTile], st_d[kWmTile];
+    __shared__ uint32_t s_next;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int NJ = kWmTile / kWmBlock;
-    lpos[tid] = (uint32_t)base[(int64_t)tid * gridDim.x + blockIdx.x];
-    __syncthreads();
     const int dbits = wm_digit_bits(sh.nb);
     const uint32_t lmask = (1u << sh.lb) - 1u;
-    const int64_t r0 = (int64_t)blockIdx.x * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-    const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    uint64_t kv[NJ], ovv[NJ];
-    auto load = [&](int64_t t0) {
+    const int woff = wave * 64 * NJ + lane;
+    static_assert(kWmCkTiles == 2, "a whole chunk is two tiles below");
+    const int xcd = blockIdx.x & 7;
+    const int64_t j_lo = (int64_t)xcd * nchunk / 8, cnt = (int64_t)(xcd + 1) * nchunk / 8 - j_lo;
+    if (tid == 0) s_next = atomicAdd(&claim[xcd], 1u);
+    __syncthreads();
+    int64_t jc = (int64_t)__builtin_amdgcn_readfirstlane(s_next);
+    if (jc >= cnt) return;
+    jc += j_lo;
+    // the digits need only the key's low 32 bits ((k - kmin) < 2^24: see k_wm2_inv1)
+    uint32_t kv[NJ];
+    uint64_t ovv[NJ];
+    // rows of [t0, t0 + kWmTile) inside [lo, hi) (the rest read row lo, not live)
+    auto load = [&](int64_t t0, int64_t lo, int64_t hi) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int64_t i = t0 + woff + j * 64;
-            const int64_t ii = i < r1 ? i : r0;
-            kv[j] = wm_ld<KES>(key.values, ii);
+            const int64_t ii = i < hi ? i : lo;
+            kv[j] = ((const uint32_t *)key.values)[ii * (KES / 4)];
             ovv[j] = wm_ld<OES>(ord.values, ii);
         }
     };
-    // One tile: FULL tiles store unconditionally (2 * NJ stores on every path), so waiting for the
-    // next tile's prefetched loads never waits for this tile's run stores: the compiler counts
-    // vmcnt exactly only when the store count between a load and its use is fixed -- a run-time
-    // trip count there made it wait for every store ack (vmcnt(0)) before each tile.
-    auto tile = [&](int64_t t0, auto fullc) {
-        constexpr bool FULL = decltype(fullc)::value;
-        uint32_t d[NJ], kl[NJ], slot[NJ];
-        uint64_t ok[NJ];
-        bool live[NJ];
+    int64_t c0 = jc * kWmChunk, c1 = std::min<int64_t>(sh.n, c0 + kWmChunk);
+    uint32_t lp = cpos[jc * kWmDig + tid];
+    load(c0, c0, c1);
+    for (;;) {
+        // claim the chunk after this one now: the chunk's last tile prefetches its first rows
+        uint32_t nx = 0;
+        if (tid == 0) nx = atomicAdd(&claim[xcd], 1u);
+        lpos[tid] = lp;  // (own entry: every read of the previous chunk's run positions is behind a barrier)
+        bool more = false;
+        int64_t nj = 0, n0 = 0, n1 = 0;
+        // One tile: FULL tiles store unconditionally (2 * NJ stores on every path), so waiting for the
+        // next tile's prefetched loads never waits for this tile's run stores: the compiler counts
+        // vmcnt exactly only when the store count between a load and its use is fixed -- a run-time
+        // trip count there made it wait for every store ack (vmcnt(0)) before each tile.
+        // LAST: the chunk's last tile (the claimed next chunk is known by then).
+        auto tile = [&](int64_t t0, auto fullc, auto lastc) {
+            constexpr bool FULL = decltype(fullc)::value, last = decltype(lastc)::value;
+            uint32_t d[NJ], kl[NJ], slot[NJ];
+            uint64_t ok[NJ];
+            bool live[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            live[j] = FULL || t0 + woff + j * 64 < r1;
-            const uint64_t kk = ((uint64_t)wm_key_val(kv[j], key.dtype) - (uint64_t)sh.kmin) & sh.kmask;
-            d[j] = (uint32_t)(kk >> sh.lb);
-            kl[j] = (uint32_t)kk & lmask;
-            ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
-        }
-        if (t0 + kWmTile < r1) load(t0 + kWmTile);  // in flight across the LDS phases below
-        {  // every kWmCkTiles tiles: the run positions, where inverse pass 1 resumes the replay
-            const int64_t ti = (t0 - r0) / kWmTile;
-            if (ti % kWmCkTiles == 0) ckpt[((int64_t)blockIdx.x * wm_span_chunks(sh) + ti / kWmCkTiles) * kWmDig + tid] = lpos[tid];
-        }
-        const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            if (!live[j]) continue;
-            st_key[slot[j]] = ok[j];
-            st_kl[slot[j]] = (uint16_t)kl[j];
-            st_d[slot[j]] = (uint16_t)d[j];
-        }
-        wm_barrier();
-        if constexpr (FULL) {
-#pragma unroll
-            for (int q = 0; q < NJ; ++q) {
-                const int s = tid + q * kWmBlock;
-                const uint32_t dd = st_d[s];
-                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                o_key[p] = st_key[s];
-                o_kl[p] = st_kl[s];
+            for (int j = 0; j < NJ; ++j) {
+                live[j] = FULL || woff + j * 64 < (int)(c1 - t0);
+                const uint32_t kk = (kv[j] - (uint32_t)sh.kmin) & (uint32_t)sh.kmask;
+                d[j] = kk >> sh.lb;
+                kl[j] = kk & lmask;
+                ok[j] = wm_order_bits(ovv[j], ord.dtype, asc);
             }
+            // in flight across the LDS phases below: the chunk's next tile, or the next chunk's first
+            if constexpr (!last) load(t0 + kWmTile, c0, c1);
+            else if (more) load(n0, n0, n1);
+            const uint32_t tcnt = wm_stable_rank<NJ, DB>(d, live, dbits, slot, R);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                if (!live[j]) continue;
+                st_key[slot[j]] = ok[j];
+                st_kl[slot[j]] = (uint16_t)kl[j];
+                st_d[slot[j]] = (uint16_t)d[j];
+            }
+            wm_barrier();
+            if constexpr (FULL) {
+#pragma unroll
+                for (int q = 0; q < NJ; ++q) {
+                    const int s = tid + q * kWmBlock;
+                    const uint32_t dd = st_d[s];
+                    const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                    o_key[p] = st_key[s];
+                    o_kl[p] = st_kl[s];
+                }
+            } else {
+                const int m = (int)std::min<int64_t>(kWmTile, c1 - t0);
+                for (int s = tid; s < m; s += kWmBlock) {
+                    const uint32_t dd = st_d[s];
+                    const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
+                    o_key[p] = st_key[s];
+                    o_kl[p] = st_kl[s];
+                }
+            }
+            if constexpr (!last) {
+                if (tid == 0) s_next = nx;
+            }
+            wm_barrier();
+            lpos[tid] += tcnt;
+        };
+        auto next_known = [&]() {  // after a barrier behind the s_next store (uniform: kept scalar)
+            const int64_t q = (int64_t)__builtin_amdgcn_readfirstlane(s_next);
+            more = q < cnt;
+            nj = j_lo + q;
+            n0 = nj * kWmChunk;
+            n1 = more ? std::min<int64_t>(sh.n, n0 + kWmChunk) : 0;
+        };
+        const int ntl = (int)((c1 - c0 + kWmTile - 1) / kWmTile);
+        if (c1 - c0 == kWmChunk) {
+            tile(c0, std::true_type{}, std::false_type{});
+            next_known();
+            if (more) lp = cpos[nj * kWmDig + tid];
+            tile(c0 + kWmTile, std::true_type{}, std::true_type{});
         } else {
-            const int m = (int)std::min<int64_t>(kWmTile, r1 - t0);
-            for (int s = tid; s < m; s += kWmBlock) {
-                const uint32_t dd = st_d[s];
-                const uint32_t p = lpos[dd] + (uint32_t)s - R.lofs[dd];
-                o_key[p] = st_key[s];
-                o_kl[p] = st_kl[s];
+            // the input's last, partial chunk (the last id of the last XCD's range: nothing follows it),
+            // its second tile loaded after the first
+            tile(c0, std::false_type{}, std::true_type{});
+            if (ntl > 1) {
+                load(c0 + kWmTile, c0, c1);
+                tile(c0 + kWmTile, std::false_type{}, std::true_type{});
             }
         }
-        wm_barrier();
-        lpos[tid] += tcnt;
-    };
-    // the first full tile is peeled, so every path into the loop has a tile's stores after the
-    // prefetch (the loop's waits then count past them)
-    if (r0 < r1) load(r0);
-    if (r1 - r0 >= kWmTile) {
-        tile(r0, std::true_type{});
-        int64_t t0 = r0 + kWmTile;
-        for (; t0 + kWmTile <= r1; t0 += kWmTile) tile(t0, std::true_type{});
-        if (t0 < r1) tile(t0, std::false_type{});
-    } else if (r0 < r1) {
-        tile(r0, std::false_type{});
+        if (!more) break;
+        jc = nj, c0 = n0, c1 = n1;
     }
 }
 
@@ -1255,13 +1303,13 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     }
 }
 
-// inverse of pass 1: replay pass 1's tiles span by span, chunk by chunk from pass 1's checkpoints,
-// gather the results run by run and write them in input order as Int64
+// inverse of pass 1: replay pass 1's tiles chunk by chunk from its run positions, gather the results
+// run by run and write them in input order as Int64
 // VAL = 0: rank functions, out = Int64 results.  VAL = 4 / 8 (value functions): res1 holds valid
 // flags, res1v the value bits (gathered beside them through LDS), written in VAL bytes (zero when
 // NULL) plus a validity byte.
 template <int KES, int DB, int VAL = 0>
-__global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == kWmAtomicRank && !VAL ? 8 : 4))) void k_wm2_inv1(ColRef key, WmShape sh, int nspans, const uint32_t *__restrict__ ckpt,
+__global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == kWmAtomicRank && !VAL ? 8 : 4))) void k_wm2_inv1(ColRef key, WmShape sh, int64_t nchunk, const uint32_t *__restrict__ ckpt,
                                                        const uint16_t *__restrict__ res1, void *__restrict__ out,
                                                        const uint64_t *__restrict__ res1v, uint8_t *__restrict__ valid8) {
     __shared__ WmRankLds R;
@@ -1272,19 +1320,14 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     constexpr int NJ = kWmTile / kWmBlock;
     const int dbits = wm_digit_bits(sh.nb);
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
-    // the workgroups of one XCD take the chunks of one pass-1 span together (see k_wm2_inv2)
+    // chunk ids dealt per XCD range, every per-th id (see k_wm2_inv2)
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
-    const int64_t cps = wm_span_chunks(sh);
-    // XCD x takes spans [x nspans / 8, (x + 1) nspans / 8), chunk ids w * cps + c, every per-th id
-    const int64_t j_lo = sh.spread ? 0 : (int64_t)xcd * nspans / 8 * cps, j_hi = sh.spread ? (int64_t)nspans * cps : (int64_t)(xcd + 1) * nspans / 8 * cps;
+    const int64_t j_lo = sh.spread ? 0 : (int64_t)xcd * nchunk / 8, j_hi = sh.spread ? nchunk : (int64_t)(xcd + 1) * nchunk / 8;
     const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
     {
         for (int64_t jc = j_lo + j0; jc < j_hi; jc += js) {
-            const int64_t w = jc / cps, c = jc - w * cps;
-            const int64_t r0 = w * sh.span, r1 = std::min<int64_t>(sh.n, r0 + sh.span);
-            const int64_t c0 = r0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(r1, c0 + (int64_t)kWmCkTiles * kWmTile);
-            if (c0 >= c1) continue;  // (the last span's unused chunk ids)
+            const int64_t c0 = jc * kWmChunk, c1 = std::min<int64_t>(sh.n, c0 + kWmChunk);
             lpos[tid] = ckpt[jc * kWmDig + tid];
             __syncthreads();
             // the digit needs only the key's low 32 bits: (k - kmin) < 2^24 here, so its low word is
@@ -1358,14 +1401,16 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const int g1 = (int)((n + sh.span - 1) / sh.span);
     const bool value_fn = func >= QEH_WIN_LAG;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
-    DevBuf cnt1, base1, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2, cbase, ckpt, ckpt1;
-    // inverse pass 2's chunks: at most n / (kWmCkTiles tiles) whole ones plus one partial per bucket
-    const int64_t nck = n / ((int64_t)kWmTile * kWmCkTiles) + sh.nb + 1;
-    const int64_t nc1 = (int64_t)kWmDig * g1;
-    if ((!pre_counts && cnt1.alloc(ctx, nc1 * 4)) || base1.alloc(ctx, (nc1 + 1) * 8) || key1.alloc(ctx, (n + kWmTile) * 8) || kl1.alloc(ctx, (n + kWmTile) * 2) ||
-        key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) || bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) ||
-        flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)) || cbase.alloc(ctx, ((int64_t)sh.nb + 1) * 4) ||
-        ckpt.alloc(ctx, nck * kWmDig * 4) || ckpt1.alloc(ctx, (int64_t)g1 * wm_span_chunks(sh) * kWmDig * 4))
+    DevBuf cnt1, bsum, dst, claim, key1, kl1, key2, pst, bst, res2, res1, flag, res2v, res1v, valid8, ks2, cbase, ckpt, ckpt1;
+    // pass 1's chunks of the input, and the blocks of its chunk scan
+    const int64_t nchunk = (n + kWmChunk - 1) / kWmChunk, nblk = (nchunk + kWmScanB - 1) / kWmScanB;
+    // pass 2's chunks: at most n / kWmChunk whole ones plus one partial per bucket
+    const int64_t nck = n / kWmChunk + sh.nb + 1;
+    if ((!pre_counts && cnt1.alloc(ctx, nchunk * kWmDig * 2)) || bsum.alloc(ctx, nblk * kWmDig * 4) ||
+        dst.alloc(ctx, kWmDig * 4) || claim.alloc(ctx, 8 * 4) || key1.alloc(ctx, (n + kWmTile) * 8) ||
+        kl1.alloc(ctx, (n + kWmTile) * 2) || key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) ||
+        bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) || flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)) ||
+        cbase.alloc(ctx, ((int64_t)sh.nb + 1) * 4) || ckpt.alloc(ctx, nck * kWmDig * 4) || ckpt1.alloc(ctx, nchunk * kWmDig * 4))
         return fail(QEH_E_OOM, "window: out of device memory");
     const ColRef kc = make_colref(part), oc = make_colref(order);
     const int kes = part.dtype == QEH_DT_INT32 ? 4 : 8;
@@ -1374,19 +1419,24 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     const bool at = std::getenv("QEH_WM_BALLOT") == nullptr && lds_atomic_rank_ok(ctx);
     {
         KernelTimer kt(ctx, "window_partition");
-        const uint32_t *counts = pre_counts ? pre_counts->as<uint32_t>() : cnt1.as<uint32_t>();
+        const uint16_t *counts = pre_counts ? pre_counts->as<uint16_t>() : cnt1.as<uint16_t>();
         if (!pre_counts)
-            hipLaunchKernelGGL(kes == 4 ? k_wm_hist1<4> : k_wm_hist1<8>, dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, sh,
-                               cnt1.as<uint32_t>());
-        QEH_TRY(exclusive_scan_u32(ctx, counts, base1.as<uint64_t>(), nc1, nullptr));
+            hipLaunchKernelGGL((kes == 4 ? k_wm_hist1<4, false> : k_wm_hist1<8, false>), dim3(g1), dim3(kWmBlock), 0, ctx->stream,
+                               kc, sh, cnt1.as<uint16_t>(), nullptr);
+        // run positions of every chunk (-> ckpt1) and the bucket starts (-> bst)
+        hipLaunchKernelGGL(k_wm_cscan_blocks, dim3((unsigned)nblk), dim3(kWmBlock), 0, ctx->stream, counts, nchunk,
+                           bsum.as<uint32_t>());
+        hipLaunchKernelGGL(k_wm_cscan_top, dim3(1), dim3(kWmBlock), 0, ctx->stream, bsum.as<uint32_t>(), (int)nblk, (int)sh.nb,
+                           dst.as<uint32_t>(), bst.as<uint64_t>());
+        hipLaunchKernelGGL(k_wm_cscan_pos, dim3((unsigned)nblk), dim3(kWmBlock), 0, ctx->stream, counts, nchunk,
+                           bsum.as<uint32_t>(), dst.as<uint32_t>(), ckpt1.as<uint32_t>());
+        QEH_HIP(hipMemsetAsync(claim.p, 0, 8 * 4, ctx->stream));
         const bool d1 = wm_digit_bits(sh.nb) == 10;
 #define QEH_WM_P1(K, O) (at ? k_wm2_pass1<K, O, kWmAtomicRank> : d1 ? k_wm2_pass1<K, O, 10> : k_wm2_pass1<K, O, -1>)
         hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
                                     : (oes == 4 ? QEH_WM_P1(8, 4) : QEH_WM_P1(8, 8)),
-                           dim3(g1), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh,
-                           base1.as<uint64_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>(), ckpt1.as<uint32_t>());
-        // bucket starts = the scanned bases of workgroup 0 per digit, then n
-        QEH_HIP(hipMemcpy2DAsync(bst.p, 8, base1.p, (size_t)g1 * 8, 8, sh.nb, hipMemcpyDeviceToDevice, ctx->stream));
+                           dim3(cus), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, nchunk,
+                           ckpt1.as<uint32_t>(), claim.as<uint32_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
 #undef QEH_WM_P1
@@ -1511,7 +1561,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     (kes == 4 ? (at ? k_wm2_inv1<4, kWmAtomicRank, V> : d1i ? k_wm2_inv1<4, 10, V> : k_wm2_inv1<4, -1, V>)                 \
               : (at ? k_wm2_inv1<8, kWmAtomicRank, V> : d1i ? k_wm2_inv1<8, 10, V> : k_wm2_inv1<8, -1, V>))
         hipLaunchKernelGGL(!value_fn ? QEH_WM_I1(0) : esz == 8 ? QEH_WM_I1(8) : QEH_WM_I1(4), dim3(ginv), dim3(kWmBlock), 0,
-                           ctx->stream, kc, sh, g1, ckpt1.as<uint32_t>(), res1.as<uint16_t>(), out->values,
+                           ctx->stream, kc, sh, nchunk, ckpt1.as<uint32_t>(), res1.as<uint16_t>(), out->values,
                            res1v.as<uint64_t>(), valid8.as<uint8_t>());
 #undef QEH_WM_I1
     }
@@ -1560,9 +1610,9 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     int g1x = 2;
     if (const char *e = std::getenv("QEH_WM_G1X")) g1x = std::max(1, std::atoi(e));
     const int g1w = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * g1x, (n + kWmTile - 1) / kWmTile));
-    const int64_t span = ((n + g1w - 1) / g1w + kWmTile - 1) / kWmTile * kWmTile;
+    const int64_t span = ((n + g1w - 1) / g1w + kWmChunk - 1) / kWmChunk * kWmChunk;  // whole chunks
     const int g1 = (int)((n + span - 1) / span);  // window_noid's pass-1 grid (histogram layout)
-    // the key's min / max and the 20-bit shape's pass-1 histogram in one read (k_wm_minmax_hist1)
+    // the key's min / max and the 20-bit shape's pass-1 histogram in one read (k_wm_hist1<KES, true>)
     WmShape sh{};
     sh.n = n;
     sh.span = span;
@@ -1570,12 +1620,12 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
     sh.kmask = (1ull << 20) - 1;
     sh.lb = 10;
     DevBuf pre, mmp;
-    QEH_TRY(pre.alloc(ctx, (size_t)kWmDig * g1 * 4));
+    QEH_TRY(pre.alloc(ctx, (size_t)kWmDig * ((n + kWmChunk - 1) / kWmChunk) * 2));
     QEH_TRY(mmp.alloc(ctx, sizeof(WmMinMax) * (size_t)g1));
     {
         KernelTimer kt(ctx, "window_partition");
-        hipLaunchKernelGGL(part.dtype == QEH_DT_INT32 ? k_wm_minmax_hist1<4> : k_wm_minmax_hist1<8>, dim3(g1), dim3(kWmBlock), 0,
-                           ctx->stream, make_colref(part), sh, pre.as<uint32_t>(), mmp.as<WmMinMax>());
+        hipLaunchKernelGGL((part.dtype == QEH_DT_INT32 ? k_wm_hist1<4, true> : k_wm_hist1<8, true>), dim3(g1), dim3(kWmBlock), 0,
+                           ctx->stream, make_colref(part), sh, pre.as<uint16_t>(), mmp.as<WmMinMax>());
         QEH_HIP(hipGetLastError());
     }
     std::vector<WmMinMax> mmh(g1);
