@@ -626,6 +626,7 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_chunk_scan(WmShape sh, const u
 template <int DB, bool KS>
 __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64_t *__restrict__ bstart,
                                                          const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ ckpt,
+                                                         uint32_t *__restrict__ claim,
                                                          const uint64_t *__restrict__ i_key, const uint16_t *__restrict__ i_kl,
                                                          uint64_t *__restrict__ o_key, uint8_t *__restrict__ o_ks) {
     __shared__ WmRankLds R;
@@ -641,8 +642,20 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     if (wslot >= per) return;  // (a grid that is not a multiple of 8)
     const int b_lo = sh.spread ? 0 : (int)((int64_t)xcd * sh.nb / 8), b_hi = sh.spread ? sh.nb : (int)((int64_t)(xcd + 1) * sh.nb / 8);
     const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
+    __shared__ uint32_t s_next;
     if (b_lo < b_hi) {
-        for (int64_t jc = (int64_t)cbase[b_lo] + j0; jc < (int64_t)cbase[b_hi]; jc += js) {
+        // the XCD's workgroups claim its chunk ids in order from one counter (as pass 1: the chunks in
+        // flight stay consecutive); QEH_WM_SPREAD=1 deals them round-robin over the whole grid
+        bool first = true;
+        for (int64_t jc = (int64_t)cbase[b_lo] + j0;; first = false) {
+            if (!sh.spread) {
+                if (tid == 0) s_next = atomicAdd(&claim[xcd], 1u);
+                __syncthreads();
+                jc = (int64_t)cbase[b_lo] + (int64_t)__builtin_amdgcn_readfirstlane(s_next);
+            } else if (!first) {
+                jc += js;
+            }
+            if (jc >= (int64_t)cbase[b_hi]) break;
             const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
             const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
@@ -1407,7 +1420,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     // pass 2's chunks: at most n / kWmChunk whole ones plus one partial per bucket
     const int64_t nck = n / kWmChunk + sh.nb + 1;
     if ((!pre_counts && cnt1.alloc(ctx, nchunk * kWmDig * 2)) || bsum.alloc(ctx, nblk * kWmDig * 4) ||
-        dst.alloc(ctx, kWmDig * 4) || claim.alloc(ctx, 8 * 4) || key1.alloc(ctx, (n + kWmTile) * 8) ||
+        dst.alloc(ctx, kWmDig * 4) || claim.alloc(ctx, 16 * 4) || key1.alloc(ctx, (n + kWmTile) * 8) ||
         kl1.alloc(ctx, (n + kWmTile) * 2) || key2.alloc(ctx, n * 8) || pst.alloc(ctx, (sh.nparts + 1) * 8) ||
         bst.alloc(ctx, ((int64_t)sh.nb + 1) * 8) || flag.alloc(ctx, 8) || (sh.sb && ks2.alloc(ctx, n)) ||
         cbase.alloc(ctx, ((int64_t)sh.nb + 1) * 4) || ckpt.alloc(ctx, nck * kWmDig * 4) || ckpt1.alloc(ctx, nchunk * kWmDig * 4))
@@ -1430,7 +1443,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                            dst.as<uint32_t>(), bst.as<uint64_t>());
         hipLaunchKernelGGL(k_wm_cscan_pos, dim3((unsigned)nblk), dim3(kWmBlock), 0, ctx->stream, counts, nchunk,
                            bsum.as<uint32_t>(), dst.as<uint32_t>(), ckpt1.as<uint32_t>());
-        QEH_HIP(hipMemsetAsync(claim.p, 0, 8 * 4, ctx->stream));
+        QEH_HIP(hipMemsetAsync(claim.p, 0, 16 * 4, ctx->stream));  // pass 1: [0, 8), pass 2: [8, 16)
         const bool d1 = wm_digit_bits(sh.nb) == 10;
 #define QEH_WM_P1(K, O) (at ? k_wm2_pass1<K, O, kWmAtomicRank> : d1 ? k_wm2_pass1<K, O, 10> : k_wm2_pass1<K, O, -1>)
         hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
@@ -1452,7 +1465,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                                    cbase.as<uint32_t>(), ccnt.as<uint16_t>(), ckpt.as<uint32_t>(), pst.as<uint64_t>());
 #define QEH_WM_P2(KS) (at ? k_wm2_pass2<kWmAtomicRank, KS> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10, KS> : k_wm2_pass2<-1, KS>)
                 hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(cus), dim3(kWmBlock), 0, ctx->stream,
-                                   sh, bst.as<uint64_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>(), key1.as<uint64_t>(),
+                                   sh, bst.as<uint64_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>(), claim.as<uint32_t>() + 8, key1.as<uint64_t>(),
                                    kl1.as<uint16_t>(), key2.as<uint64_t>(), ks2.as<uint8_t>());
 #undef QEH_WM_P2
             }
