@@ -13,16 +13,24 @@ the dim hash table, probe + filter + aggregate every fact row, finalize the
 groups, and for N>1 the RCCL exchanges.
 
 Default workload (the metric, strong scaling): 1e9 fact rows in total, split
-across the N GPUs (torchrun, one rank per GPU); the dim is sharded too.  Inside
-the step (broadcast join, DistributedExecutor.join_filter_aggregate_broadcast):
-each rank inserts its dim shard into a DIRECT u16 table over the job-wide key
-range and one RCCL all-reduce sums the tables (the table form; phase A of the
-probe runs meanwhile), the fused probe runs against the summed table, and the
-partial per-group states (1024 bounded integer group keys) are merged by one
-dense RCCL all-reduce, each rank keeping the groups it owns (the reference's
-partial/final aggregate stage shape, crates/query-distributed/src/planner.rs:
-200-249).  Shapes outside the table form all-gather the dim shards instead;
-group keys outside the dense bound shuffle their partial states by all-to-all.
+across the N GPUs (one rank per GPU); the dim is sharded too.  Inside the step
+(broadcast join, DistributedExecutor.join_filter_aggregate_broadcast, the items
+form first): one small all-gather of every shard's stats row, phase A of the
+fused probe launched from the device-side plan over this rank's fact rows,
+every rank's dim shard grouped by key slice into 4-B items and all-gathered
+over RCCL, phase B builds each slice's LDS entries from every rank's items and
+aggregates, and the per-group partial states (1024 bounded integer group keys)
+are merged by one dense RCCL all-reduce of f64 lanes, each rank keeping the
+groups it owns (the reference's partial/final aggregate stage shape,
+crates/query-distributed/src/planner.rs:200-249).  Shapes outside the items
+form take the table form (shard tables summed by an all-reduce) or all-gather
+the dim shards; the line's "dist_build" names the form that ran.
+
+Launch: the driver starts N > 1 under torch.distributed.run (WORLD_SIZE = N).
+Run directly with --gpus N > 1, bench.py starts that launcher itself as a child
+process before anything touches the GPU and exits with its code; a --gpus that
+disagrees with a WORLD_SIZE already set is an error (exit 2), never a silent
+N = 1 run.
 
 --workload cfg4 (BASELINE config 4, weak scaling): 1e9 fact rows per GPU; both
 sides hash-partitioned by the join key and exchanged over RCCL all-to-all
@@ -168,9 +176,41 @@ def free_port() -> int:
     return p
 
 
+def launch_plan(gpus: int, env) -> str:
+    """How this invocation runs: "run" (this process is the job's rank, or N = 1), "spawn" (--gpus N > 1
+    outside a launcher: start torch.distributed.run with N ranks as a child) or "mismatch" (a launcher
+    set WORLD_SIZE and --gpus disagrees with it)."""
+    ws = env.get("WORLD_SIZE")
+    if gpus < 1:
+        return "mismatch"
+    if ws is None:
+        return "spawn" if gpus > 1 else "run"
+    return "run" if int(ws) == gpus else "mismatch"
+
+
+def spawn_command(argv, gpus: int, port: int):
+    """The launcher command for --gpus N outside torchrun (the driver's own form of the N > 1 run)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     args = parse()
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "mismatch":
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')} -- launch N > 1 as "
+              "`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`, or run bench.py --gpus N "
+              "directly and it starts that launcher itself", file=sys.stderr)
+        sys.exit(2)
+    if plan == "spawn":  # (nothing has touched the GPU yet: the ranks are children, not an exec)
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.run(spawn_command(sys.argv[1:], args.gpus, free_port()), env=env).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("QEH_BENCH_LAUNCH_PROBE"):  # (tests/test_bench_launch.py: the rank's view, no GPU work)
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("QEH_BENCH_SHARE_GPU"):  # rehearsal only: several ranks on one GPU
@@ -360,14 +400,19 @@ def main():
         else:
             workload = ("filter->hash-join->group-by (BASELINE metric query): SELECT d.g, SUM(f.v), COUNT(f.v) "
                         "FROM fact f JOIN dim d ON f.k = d.k WHERE f.x > 49 GROUP BY d.g")
+            form = getattr(dx, "last_build", None) if dx is not None else None
+            how = {"items": "every rank's dim shard grouped by key slice into 4-B items and all-gathered over RCCL "
+                            "(broadcast join, items form)",
+                   "table": "shard tables summed by RCCL all-reduce (broadcast join, table form)",
+                   "allgather": "dim shards all-gathered over RCCL (broadcast join)",
+                   "replicated": "dim replicated on every rank"}.get(form, f"broadcast join ({form})")
             par = (f"fact {args.rows} rows split x{world} (strong scaling)"
-                   + (f", dim sharded x{world}: shard tables summed by RCCL all-reduce inside the step (broadcast join, "
-                      "table form), partial states merged by a dense RCCL all-reduce, final aggregate per owner rank"
-                      if dist else ""))
+                   + (f", dim sharded x{world}: {how} inside the step, partial states merged by a dense RCCL "
+                      "all-reduce, final aggregate per owner rank" if dist else ""))
         if rehearse:
             par = (f"rehearsal of rank {rr} of {ww} at world size 1: fact rows [{row0}, {row0 + n}), dim rows "
-                   f"[{d0}, {d0 + dn}) through the broadcast join's table form (the RCCL all-reduce of the shard "
-                   "tables has one member: its xGMI time is not in the step)")
+                   f"[{d0}, {d0 + dn}) through the broadcast join ({form} form; its RCCL collectives have one "
+                   "member: their xGMI time is not in the step)")
         line = {
             "metric": "rows/sec filter->hash-join->group-by, 1B rows, 1/2/4/8 GPUs; % HBM roofline",
             "value": value,
