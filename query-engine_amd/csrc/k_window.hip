@@ -1617,6 +1617,10 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         order.dtype != QEH_DT_FLOAT32)
         return kWindowMsdNotEligible;
     if ((part.validity && part.null_count != 0) || (order.validity && order.null_count != 0)) return kWindowMsdNotEligible;
+    if (!value_fn) {  // the three-level pipeline first (k_window3.hip); it declines shapes it cannot take
+        const int s = window_w3(ctx, func, part, order, asc, param, out);
+        if (s != kWindowMsdNotEligible) return s;
+    }
     const int cus = ctx->props.multiProcessorCount;
     // pass-1 workgroups (row spans): two per CU by default, so the replaying inverse pass (80 KB of
     // LDS) runs two per CU and one's barrier phases overlap the other's memory phases

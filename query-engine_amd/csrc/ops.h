@@ -158,6 +158,10 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
 // ranges multiplied) takes window_msd when the product of the ranges is within its key bound.
 int window_msd_keys(qeh_ctx *ctx, int func, const qeh_column *parts, int n_part, const qeh_column &order, bool asc,
                     int64_t param, const qeh_column *arg, const int64_t *dflt, qeh_column *out);
+// ROW_NUMBER / RANK / NTILE over a key range of <= 2^20 by three 512-way levels with whole-chunk
+// writes (k_window3.hip); window_msd tries it first.
+int window_w3(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
+              qeh_column *out);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);

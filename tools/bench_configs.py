@@ -194,7 +194,8 @@ def cfg5(ctx, scale):
     def fn():
         rn = ctx.row_number([k], [v], [True])
         rn.release()
-    wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "row_number", "window_partition", "window_sort", "window_place"])
+    wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "row_number", "window_partition", "window_sort", "window_place",
+                                    "w3_partition", "w3_sort", "w3_place"])
     m = 5_000_000
     hk = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 7, m, 2 ** 20)
     hv = ob.generate(abi.GEN_UNIFORM_MOD, SEED, 8, m, 2 ** 62, lo=-(2 ** 61))
@@ -218,7 +219,7 @@ def cfg_window(ctx, scale):
     for name, func, arg, alg in [("RANK", W.Rank, None, 24.0), ("LAG(v,1)", W.Lag, v, 24.0)]:
         def fn():
             ctx.window(func, [k], [v], [True], arg=arg, param=1).release()
-        wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "window", "window_partition", "window_sort", "window_place"])
+        wall, kt, _ = timed(ctx, fn, 2, ["radix_pass", "sort_encode", "window", "window_partition", "window_sort", "window_place", "w3_partition", "w3_sort", "w3_place"])
         t0 = time.perf_counter()
         ob.window(func, [ob.HostCol(hk)], [ob.HostCol(hv)], [True], arg=ob.HostCol(hv) if arg is not None else None,
                   param=1)
@@ -237,7 +238,8 @@ def cfg_window_lsd(ctx, scale):
     n = int(1e9 * scale)
     k = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 7, n, 2 ** 24)
     v = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 8, n, 2 ** 62, lo=-(2 ** 61))
-    names = ["radix_pass", "sort_encode", "row_number", "window", "window_partition", "window_sort", "window_place", "gather"]
+    names = ["radix_pass", "sort_encode", "row_number", "window", "window_partition", "window_sort", "window_place", "gather",
+             "w3_partition", "w3_sort", "w3_place"]
     for label, fn, alg in [
             ("ROW_NUMBER, k over 2^24", lambda: ctx.row_number([k], [v], [True]).release(), 24.0),
             ("RANK, k over 2^24", lambda: ctx.window(W.Rank, [k], [v], [True]).release(), 24.0)]:
@@ -607,7 +609,7 @@ def cfg5_leg(ctx, scale, world=8):
         for q in out:
             q.release()
     names = ["partition_move", "radix_pass", "sort_encode", "row_number", "window_partition", "window_sort",
-             "window_place"]
+             "window_place", "w3_partition", "w3_sort", "w3_place"]
     w1, k1, _ = timed(ctx, leg1, 5, names)
     w2, k2, _ = timed(ctx, leg2, 3, names)
     w3, k3, _ = timed(ctx, leg3, 5, names)
