@@ -29,7 +29,8 @@ __host__ __device__ __forceinline__ uint32_t cmp_truth_table(int op) {
         case D_LT: return 1u;
         case D_LE: return 3u;
         case D_GT: return 4u;
-        default: return 6u;  // D_GE
+        case D_GE: return 6u;
+        default: return 0u;  // (not a comparison: plan_predicate admits only compare ops to the fast tiles)
     }
 }
 

@@ -167,15 +167,18 @@ struct MatIn {
     int64_t n;
 };
 
+// stride = nb, or nb + 1 with a zeroed matched-flag word after the build columns (FULL joins)
 __global__ void k_embed_build(ColRef key, int64_t n, int64_t kmin, const int64_t *b0, const int64_t *b1,
-                              const int64_t *b2, int nb, int64_t *__restrict__ rec, uint32_t *__restrict__ present) {
+                              const int64_t *b2, int nb, int64_t *__restrict__ rec, uint32_t *__restrict__ present,
+                              int stride) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
         const uint64_t off = (uint64_t)load_i64(key, i) - (uint64_t)kmin;
         atomicOr(&present[off >> 5], 1u << (off & 31));
-        rec[off * nb] = b0[i];
-        if (nb > 1) rec[off * nb + 1] = b1[i];
-        if (nb > 2) rec[off * nb + 2] = b2[i];
+        rec[off * stride] = b0[i];
+        if (nb > 1) rec[off * stride + 1] = b1[i];
+        if (nb > 2) rec[off * stride + 2] = b2[i];
+        if (stride > nb) rec[off * stride + nb] = 0;
     }
 }
 
@@ -411,6 +414,133 @@ __global__ __launch_bounds__(kBlock) void k_outer_embed(ColRef key, int64_t n, c
     }
 }
 
+// FULL over a unique DIRECT build (build columns embedded as for LEFT, probe columns non-null 8-byte):
+// one pass writes every output column of the probe rows in probe order -- the probe columns copied
+// beside the key read, the build columns from the embedded records (NULL when unmatched) -- and
+// flags each matched key in its record (a plain store when the record read shows it clear); the build rows no probe row
+// matched are then appended in build-row order (k_full_tail_*).  Replaces the lookup + index arrays +
+// one null-aware gather per output column.
+struct FullEmbedOut {
+    const int64_t *pcol[kMatMaxP];
+    int64_t *pout[kMatMaxP];
+    uint64_t *pvalid[kMatMaxP];
+    int64_t *bout[kMatMaxB];
+    uint64_t *bvalid[kMatMaxB];
+    int32_t np;
+};
+
+template <int NB, int NP>
+__global__ __launch_bounds__(kBlock) void k_full_embed(ColRef key, int64_t n, int64_t *__restrict__ rec,
+                                                       const uint32_t *__restrict__ present, int64_t kmin, int64_t kmax,
+                                                       FullEmbedOut out) {
+    constexpr int S = NB + 1;  // record stride: the values, then the matched flag
+    constexpr int U = 4;  // 64-row groups per wave in flight
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t g0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * U; g0 * 64 < n; g0 += nw * U) {
+        uint64_t off[U];
+        bool hit[U];
+        int64_t pv[U][NP > 0 ? NP : 1];  // the probe columns' values, loaded beside the keys
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pv[u][p] = i < n ? __builtin_nontemporal_load(out.pcol[p] + i) : 0;
+            const bool valid = i < n && col_valid(key, i);
+            const int64_t k = valid ? load_i64(key, i) : 0;
+            const bool in = valid && k >= kmin && k <= kmax;
+            off[u] = in ? (uint64_t)k - (uint64_t)kmin : 0;
+            hit[u] = in && ((present[off[u] >> 5] >> (off[u] & 31)) & 1u);
+        }
+        int64_t v[U][S];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int b = 0; b < S; ++b) v[u][b] = hit[u] ? rec[off[u] * S + b] : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+            const uint64_t mask = __ballot(hit[u]), rows = __ballot(i < n);
+            if (i < n) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) __builtin_nontemporal_store(v[u][b], out.bout[b] + i);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) __builtin_nontemporal_store(pv[u][p], out.pout[p] + i);
+                if (hit[u] && v[u][NB] == 0) rec[off[u] * S + NB] = 1;  // (idempotent: a race stores it twice)
+            }
+            if (lane == 0 && (g0 + u) * 64 < n) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) out.bvalid[b][g0 + u] = mask;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) out.pvalid[p][g0 + u] = rows;
+            }
+        }
+    }
+}
+
+// build rows with no matching probe row (a NULL key never matches), per block of kUmRows rows
+constexpr int kFtRows = kBlock * 8;
+__device__ __forceinline__ bool full_unmatched(const ColRef &bkey, int64_t j, int64_t kmin, const int64_t *rec, int stride) {
+    return !col_valid(bkey, j) || rec[((uint64_t)load_i64(bkey, j) - (uint64_t)kmin) * stride + stride - 1] == 0;
+}
+// (the flag of every build row also goes to um[] -- one byte, in order -- for the emit pass)
+__global__ void k_full_tail_count(ColRef bkey, int64_t nb, int64_t kmin, const int64_t *__restrict__ rec, int stride,
+                                  uint8_t *__restrict__ um, uint32_t *__restrict__ counts) {
+    const int64_t base = (int64_t)blockIdx.x * kFtRows;
+    uint32_t c = 0;
+    for (int r = threadIdx.x; r < kFtRows; r += kBlock) {
+        const int64_t j = base + r;
+        if (j < nb) {
+            const bool u = full_unmatched(bkey, j, kmin, rec, stride);
+            um[j] = u ? 1 : 0;
+            c += u ? 1u : 0u;
+        }
+    }
+    c = (uint32_t)wave_sum_u64(c);
+    __shared__ uint32_t part[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// the unmatched build rows written at n + their rank, in build-row order: build columns (valid), probe
+// columns NULL (their validity words are zero from the allocation)
+__global__ void k_full_tail_emit(const uint8_t *__restrict__ um, int64_t nb, const uint64_t *__restrict__ base_of,
+                                 int64_t n, FullEmbedOut out,
+                                 const int64_t *b0, const int64_t *b1, const int64_t *b2, int nbc) {
+    __shared__ uint32_t wcnt[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kFtRows;
+    uint64_t pos = (uint64_t)n + base_of[blockIdx.x];
+    const int64_t *bc[3] = {b0, b1, b2};
+    for (int step = 0; step < kFtRows; step += kBlock) {
+        const int64_t j = base + step + threadIdx.x;
+        const bool u = j < nb && um[j];
+        const uint64_t bal = __ballot(u);
+        if (lane == 0) wcnt[wave] = (uint32_t)popc64(bal);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            before += w < wave ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (u) {
+            const uint64_t o = pos + before + mbcnt(bal);
+            for (int b = 0; b < nbc; ++b) {
+                out.bout[b][o] = bc[b][j];
+                atomicOr((unsigned long long *)&out.bvalid[b][o >> 6], 1ull << (o & 63));
+            }
+            for (int p = 0; p < out.np; ++p) out.pout[p][o] = 0;
+        }
+        pos += total;
+        __syncthreads();
+    }
+}
+
 __global__ void k_iota_then_null(uint32_t *__restrict__ out, int64_t n, int64_t m) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = i < n ? (uint32_t)i : kNullRow;
@@ -493,7 +623,7 @@ static int join_materialise_fused(qeh_ctx *ctx, const qeh_column &probe_key, con
         hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
                            make_colref(build_key), nbuild, bt.t.kmin, cptr(build_cols[0]),
                            nb > 1 ? cptr(build_cols[1]) : nullptr, nb > 2 ? cptr(build_cols[2]) : nullptr, nb,
-                           rec.as<int64_t>(), present.as<uint32_t>());
+                           rec.as<int64_t>(), present.as<uint32_t>(), nb);
         QEH_HIP(hipGetLastError());
     }
     // outputs sized for every probe row (a unique build emits at most one row per probe row)
@@ -621,6 +751,98 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
     return QEH_OK;
 }
 
+// FULL over a unique DIRECT build: k_full_embed for the probe rows, then the unmatched build rows
+// appended (k_full_tail_count / scan / k_full_tail_emit).  Output columns are allocated for every probe
+// and build row and hold the m rows that result.
+static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column &bk, const BuiltTable &bt,
+                           const qeh_column *pcols, int npc, const qeh_column *bcols, int nbc, qeh_column *pout,
+                           qeh_column *bout, int64_t *out_rows) {
+    const uint64_t range = bt.t.range;
+    const int64_t n = pk.length, nbuild = bk.length, cap = n + nbuild;
+    auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
+    // records of nbc build values + a matched flag word: a probe hit reads its record anyway, so it sets the
+    // flag only when it reads it clear -- about one store per matched key instead of one per matching row
+    DevBuf rec, present;
+    const int stride = nbc + 1;
+    QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * stride, 1) * 8));
+    QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
+    QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+    if (nbuild > 0) {
+        KernelTimer kt(ctx, "join_build");
+        hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                           make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
+                           nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), stride);
+    }
+    int made_p = 0, made_b = 0, s = QEH_OK;
+    FullEmbedOut eo{};
+    eo.np = npc;
+    for (int i = 0; i < npc && s == QEH_OK; ++i) {
+        s = alloc_column(ctx, pcols[i].dtype, cap, true, &pout[i]);
+        if (s != QEH_OK) break;
+        ++made_p;
+        eo.pcol[i] = cptr(pcols[i]);
+        eo.pout[i] = (int64_t *)pout[i].values;
+        eo.pvalid[i] = (uint64_t *)pout[i].validity;
+        s = hipMemsetAsync(pout[i].validity, 0, (size_t)((cap + 63) / 64) * 8, ctx->stream) == hipSuccess
+                ? QEH_OK : fail(QEH_E_HIP, "outer join: memset");
+    }
+    for (int i = 0; i < nbc && s == QEH_OK; ++i) {
+        s = alloc_column(ctx, bcols[i].dtype, cap, true, &bout[i]);
+        if (s != QEH_OK) break;
+        ++made_b;
+        eo.bout[i] = (int64_t *)bout[i].values;
+        eo.bvalid[i] = (uint64_t *)bout[i].validity;
+        s = hipMemsetAsync(bout[i].validity, 0, (size_t)((cap + 63) / 64) * 8, ctx->stream) == hipSuccess
+                ? QEH_OK : fail(QEH_E_HIP, "outer join: memset");
+    }
+    uint64_t extra = 0;
+    if (s == QEH_OK && n > 0) {
+        KernelTimer kt(ctx, "join_probe");
+        const int grid = grid_for(ctx, (n + 255) / 256, kBlock / 64, 8);
+        auto go = [&](auto nbv) {
+            constexpr int NB = decltype(nbv)::value;
+            auto k = npc == 0 ? k_full_embed<NB, 0> : npc == 1 ? k_full_embed<NB, 1> : npc == 2 ? k_full_embed<NB, 2>
+                                                                                         : k_full_embed<NB, 3>;
+            hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n, rec.as<int64_t>(),
+                               present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
+        };
+        if (nbc == 1) go(std::integral_constant<int, 1>{});
+        else if (nbc == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 3>{});
+        if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "outer join: kernel launch failed");
+    }
+    if (s == QEH_OK && nbuild > 0) {
+        KernelTimer kt(ctx, "join_gather");
+        const int64_t nblk = (nbuild + kFtRows - 1) / kFtRows;
+        DevBuf counts, bases, um;
+        s = counts.alloc(ctx, (size_t)nblk * 4);
+        if (s == QEH_OK) s = bases.alloc(ctx, (size_t)nblk * 8);
+        if (s == QEH_OK) s = um.alloc(ctx, (size_t)nbuild);
+        if (s == QEH_OK) {
+            hipLaunchKernelGGL(k_full_tail_count, dim3((unsigned)nblk), dim3(kBlock), 0, ctx->stream, make_colref(bk), nbuild,
+                               bt.t.kmin, rec.as<int64_t>(), stride, um.as<uint8_t>(), counts.as<uint32_t>());
+            s = exclusive_scan_u32(ctx, counts.as<uint32_t>(), bases.as<uint64_t>(), nblk, &extra);
+        }
+        if (s == QEH_OK) {
+            hipLaunchKernelGGL(k_full_tail_emit, dim3((unsigned)nblk), dim3(kBlock), 0, ctx->stream, um.as<uint8_t>(), nbuild,
+                               bases.as<uint64_t>(), n, eo, cptr(bcols[0]),
+                               nbc > 1 ? cptr(bcols[1]) : nullptr, nbc > 2 ? cptr(bcols[2]) : nullptr, nbc);
+            if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "outer join: kernel launch failed");
+        }
+    }
+    if (s == QEH_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(QEH_E_HIP, "outer join: kernel failed");
+    if (s != QEH_OK) {
+        for (int i = 0; i < made_p; ++i) qeh_column_release(ctx, &pout[i]);
+        for (int i = 0; i < made_b; ++i) qeh_column_release(ctx, &bout[i]);
+        return s;
+    }
+    const int64_t m = n + (int64_t)extra;
+    for (int i = 0; i < npc; ++i) pout[i].length = m;
+    for (int i = 0; i < nbc; ++i) bout[i].length = m;
+    *out_rows = m;
+    return QEH_OK;
+}
+
 // LEFT / RIGHT / FULL equi-join (include/qeh.h).  The preserved side probes (LEFT,
 // FULL: left; RIGHT: right) a table built over the other side; unmatched probe rows emit
 // (row, kNullRow), and FULL appends the build rows no probe row matched as (kNullRow, row).  The
@@ -666,9 +888,15 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
     const int nbc = right_outer ? n_left_cols : n_right_cols, npc = right_outer ? n_right_cols : n_left_cols;
     qeh_column *bout = right_outer ? out_left : out_right;
     qeh_column *pout = right_outer ? out_right : out_left;
-    bool embed = in_place && !full && bt.t.kind == TK_DIRECT && nbc >= 1 && nbc <= kMatMaxB && bt.t.range <= (1ull << 31) &&
+    bool embed = in_place && bt.t.kind == TK_DIRECT && nbc >= 1 && nbc <= kMatMaxB && bt.t.range <= (1ull << 31) &&
                  !std::getenv("QEH_NO_FUSED_JOIN");
     for (int i = 0; embed && i < nbc; ++i) embed = mat_col_ok(bcols[i]);
+    // FULL: the probe columns are copied by the same pass (8-byte, non-null, at most kMatMaxP)
+    if (full) {
+        embed = embed && npc <= kMatMaxP;
+        for (int i = 0; embed && i < npc; ++i) embed = mat_col_ok(pcols[i]);
+    }
+    if (embed && full) return full_join_embed(ctx, pk, bk, bt, pcols, npc, bcols, nbc, pout, bout, out_rows);
     if (embed) {
         // LEFT/RIGHT over a unique DIRECT build: build columns embedded by key offset, one fused
         // probe writes them in probe order; the preserved side's columns are returned as views of
@@ -684,7 +912,7 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
             KernelTimer kt(ctx, "join_build");
             hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
                                make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
-                               nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>());
+                               nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), nbc);
         }
         int made = 0, s = QEH_OK;
         OuterEmbedOut eo{};

@@ -102,8 +102,7 @@ struct WmShape {
     int32_t nb;        // buckets (high digits in use)
     int64_t nparts;    // key range = number of PARTITION BY groups (some empty)
     int64_t span;      // rows per workgroup in pass 1 (multiple of kWmTile)
-    int32_t exp;       // QEH_WM_EXP != 0 (experiments: time pass 1 alone; the query then fails)
-    int32_t spread;    // QEH_WM_SPREAD=1 (A/B): chunked passes take chunk ids round-robin over the grid
+    int32_t exp;       // QEH_WM_EXP != 0 (-DQEH_EXPERIMENTS builds only: time pass 1 alone; the query then fails)
 };
 
 // Pass 1 and its inverse run by chunks of kWmCkTiles tiles of the input (kWmChunk rows; the histogram
@@ -229,8 +228,8 @@ __global__ __launch_bounds__(kWmBlock) void k_wm_cscan_pos(const uint16_t *__res
 struct WmFunc {
     int32_t func;      // QEH_WIN_* (ROW_NUMBER .. LAST_VALUE)
     int64_t param;     // NTILE buckets / LAG, LEAD offset
-    int32_t skip_sort; // QEH_WM_SKIP_SORT (experiments: load/emit cost without the network)
-    int32_t no_count;  // QEH_WM_NO_COUNT (experiments: the bitonic network for every group)
+    int32_t skip_sort; // QEH_WM_SKIP_SORT (-DQEH_EXPERIMENTS builds: load/emit cost without the network)
+    int32_t no_count;  // QEH_WM_NO_COUNT (-DQEH_EXPERIMENTS builds: the bitonic network for every group)
     // value functions (LAG / LEAD / FIRST_VALUE / LAST_VALUE of the ORDER BY column itself): the
     // value is decoded from the group's order keys
     int32_t odt;       // order key dtype
@@ -638,25 +637,19 @@ __global__ __launch_bounds__(kWmBlock) void k_wm2_pass2(WmShape sh, const uint64
     const int sbits = sh.sb;
     const int dbits = sh.lb - sbits;
     const int woff = wave * 64 * NJ + lane;
-    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
-    if (wslot >= per) return;  // (a grid that is not a multiple of 8)
-    const int b_lo = sh.spread ? 0 : (int)((int64_t)xcd * sh.nb / 8), b_hi = sh.spread ? sh.nb : (int)((int64_t)(xcd + 1) * sh.nb / 8);
-    const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
+    // XCD x (blockIdx % 8) owns the consecutive chunk ids [x C / 8, (x + 1) C / 8) of all C chunks (an even
+    // share whatever the buckets' sizes) and its workgroups claim them in order from one counter (as pass 1:
+    // the chunks in flight stay consecutive, and adjacent chunk ids are adjacent rows of one bucket)
+    const int xcd = blockIdx.x & 7;
+    const int64_t nck = (int64_t)cbase[sh.nb], c_lo = (int64_t)xcd * nck / 8, c_hi = (int64_t)(xcd + 1) * nck / 8;
     __shared__ uint32_t s_next;
-    if (b_lo < b_hi) {
-        // the XCD's workgroups claim its chunk ids in order from one counter (as pass 1: the chunks in
-        // flight stay consecutive); QEH_WM_SPREAD=1 deals them round-robin over the whole grid
-        bool first = true;
-        for (int64_t jc = (int64_t)cbase[b_lo] + j0;; first = false) {
-            if (!sh.spread) {
-                if (tid == 0) s_next = atomicAdd(&claim[xcd], 1u);
-                __syncthreads();
-                jc = (int64_t)cbase[b_lo] + (int64_t)__builtin_amdgcn_readfirstlane(s_next);
-            } else if (!first) {
-                jc += js;
-            }
-            if (jc >= (int64_t)cbase[b_hi]) break;
-            const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
+    if (c_lo < c_hi) {
+        for (;;) {
+            if (tid == 0) s_next = atomicAdd(&claim[xcd], 1u);
+            __syncthreads();
+            const int64_t jc = c_lo + (int64_t)__builtin_amdgcn_readfirstlane(s_next);
+            if (jc >= c_hi) break;
+            const int b = wm_chunk_bucket(cbase, 0, sh.nb - 1, jc);
             const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
             lpos[tid] = ckpt[jc * kWmDig + tid];
@@ -1259,13 +1252,13 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     constexpr int NJ = kWmTile / kWmBlock;
     const int dbits = sh.lb - sh.sb;
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
+    // chunk ids split evenly per XCD as in pass 2, every per-th id of the XCD's range per workgroup (the
+    // launch grid is a multiple of 8: every XCD slot has a workgroup)
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, slot = blockIdx.x >> 3;
-    if (slot >= per) return;  // (a grid that is not a multiple of 8)
-    const int b_lo = sh.spread ? 0 : (int)((int64_t)xcd * sh.nb / 8), b_hi = sh.spread ? sh.nb : (int)((int64_t)(xcd + 1) * sh.nb / 8);
-    const int64_t j0 = sh.spread ? blockIdx.x : slot, js = sh.spread ? gridDim.x : per;
-    if (b_lo < b_hi) {
-        for (int64_t jc = (int64_t)cbase[b_lo] + j0; jc < (int64_t)cbase[b_hi]; jc += js) {
-            const int b = wm_chunk_bucket(cbase, b_lo, b_hi - 1, jc);
+    const int64_t nck = (int64_t)cbase[sh.nb], c_lo = (int64_t)xcd * nck / 8, c_hi = (int64_t)(xcd + 1) * nck / 8;
+    {
+        for (int64_t jc = c_lo + slot; jc < c_hi; jc += per) {
+            const int b = wm_chunk_bucket(cbase, 0, sh.nb - 1, jc);
             const int64_t s0 = (int64_t)bstart[b], s1 = (int64_t)bstart[b + 1], c = jc - (int64_t)cbase[b];
             const int64_t c0 = s0 + c * kWmCkTiles * kWmTile, c1 = std::min<int64_t>(s1, c0 + (int64_t)kWmCkTiles * kWmTile);
             lpos[tid] = ckpt[jc * kWmDig + tid];
@@ -1335,11 +1328,9 @@ __global__ __launch_bounds__(kWmBlock) __attribute__((amdgpu_waves_per_eu(DB == 
     const int64_t woff = (int64_t)wave * 64 * NJ + lane;
     // chunk ids dealt per XCD range, every per-th id (see k_wm2_inv2)
     const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, wslot = blockIdx.x >> 3;
-    if (wslot >= per) return;  // (a grid that is not a multiple of 8)
-    const int64_t j_lo = sh.spread ? 0 : (int64_t)xcd * nchunk / 8, j_hi = sh.spread ? nchunk : (int64_t)(xcd + 1) * nchunk / 8;
-    const int64_t j0 = sh.spread ? blockIdx.x : wslot, js = sh.spread ? gridDim.x : per;
+    const int64_t j_lo = (int64_t)xcd * nchunk / 8, j_hi = (int64_t)(xcd + 1) * nchunk / 8;
     {
-        for (int64_t jc = j_lo + j0; jc < j_hi; jc += js) {
+        for (int64_t jc = j_lo + wslot; jc < j_hi; jc += per) {
             const int64_t c0 = jc * kWmChunk, c1 = std::min<int64_t>(sh.n, c0 + kWmChunk);
             lpos[tid] = ckpt[jc * kWmDig + tid];
             __syncthreads();
@@ -1411,6 +1402,8 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                        const int64_t *dflt, WmShape sh, qeh_column *out, DevBuf *pre_counts = nullptr) {
     const int64_t n = sh.n;
     const int cus = ctx->props.multiProcessorCount;
+    // the chunked passes deal chunk ids to the 8 XCDs by blockIdx % 8: a grid of whole octets, >= 8
+    const int gx = std::max(8, (cus + 7) / 8 * 8);
     const int g1 = (int)((n + sh.span - 1) / sh.span);
     const bool value_fn = func >= QEH_WIN_LAG;
     const int esz = (order.dtype == QEH_DT_INT32 || order.dtype == QEH_DT_FLOAT32) ? 4 : 8;
@@ -1448,7 +1441,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
 #define QEH_WM_P1(K, O) (at ? k_wm2_pass1<K, O, kWmAtomicRank> : d1 ? k_wm2_pass1<K, O, 10> : k_wm2_pass1<K, O, -1>)
         hipLaunchKernelGGL(kes == 4 ? (oes == 4 ? QEH_WM_P1(4, 4) : QEH_WM_P1(4, 8))
                                     : (oes == 4 ? QEH_WM_P1(8, 4) : QEH_WM_P1(8, 8)),
-                           dim3(cus), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, nchunk,
+                           dim3(gx), dim3(kWmBlock), 0, ctx->stream, kc, oc, asc ? 1 : 0, sh, nchunk,
                            ckpt1.as<uint32_t>(), claim.as<uint32_t>(), key1.as<uint64_t>(), kl1.as<uint16_t>());
         hipLaunchKernelGGL(k_wm_set2, dim3(1), dim3(64), 0, ctx->stream, bst.as<uint64_t>() + sh.nb,
                            pst.as<uint64_t>() + sh.nparts, (uint64_t)n);
@@ -1464,7 +1457,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
                 hipLaunchKernelGGL(k_wm2_chunk_scan, dim3(sh.nb), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(),
                                    cbase.as<uint32_t>(), ccnt.as<uint16_t>(), ckpt.as<uint32_t>(), pst.as<uint64_t>());
 #define QEH_WM_P2(KS) (at ? k_wm2_pass2<kWmAtomicRank, KS> : sh.lb - sh.sb == 10 ? k_wm2_pass2<10, KS> : k_wm2_pass2<-1, KS>)
-                hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(cus), dim3(kWmBlock), 0, ctx->stream,
+                hipLaunchKernelGGL(sh.sb ? QEH_WM_P2(true) : QEH_WM_P2(false), dim3(gx), dim3(kWmBlock), 0, ctx->stream,
                                    sh, bst.as<uint64_t>(), cbase.as<uint32_t>(), ckpt.as<uint32_t>(), claim.as<uint32_t>() + 8, key1.as<uint64_t>(),
                                    kl1.as<uint16_t>(), key2.as<uint64_t>(), ks2.as<uint8_t>());
 #undef QEH_WM_P2
@@ -1485,8 +1478,10 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
     WmFunc wf{};
     wf.func = func;
     wf.param = param;
+#ifdef QEH_EXPERIMENTS  // (A/B builds only: the first skips the network and returns wrong row numbers)
     wf.skip_sort = std::getenv("QEH_WM_SKIP_SORT") ? 1 : 0;
     wf.no_count = std::getenv("QEH_WM_NO_COUNT") ? 1 : 0;
+#endif
     wf.odt = order.dtype;
     wf.asc = asc ? 1 : 0;
     wf.has_dflt = dflt != nullptr;
@@ -1563,7 +1558,7 @@ static int window_noid(qeh_ctx *ctx, int func, const qeh_column &part, const qeh
         const bool d10 = sh.lb - sh.sb == 10;
         // the inverse passes' workgroups, all resident: two per CU where the kernel fits 64 VGPRs
         // (atomic ranking, rank functions), else one
-        const int ginv = at && !value_fn ? cus * 2 : cus;
+        const int ginv = at && !value_fn ? gx * 2 : gx;
         hipLaunchKernelGGL(value_fn ? (at ? k_wm2_inv2<kWmAtomicRank, true> : d10 ? k_wm2_inv2<10, true> : k_wm2_inv2<-1, true>)
                                     : (at ? k_wm2_inv2<kWmAtomicRank, false> : d10 ? k_wm2_inv2<10, false> : k_wm2_inv2<-1, false>),
                            dim3(ginv), dim3(kWmBlock), 0, ctx->stream, sh, bst.as<uint64_t>(), cbase.as<uint32_t>(),
@@ -1674,8 +1669,9 @@ int window_msd(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column 
         sh.nb = kWmDig;
         sh.nparts = (int64_t)1 << 20;
     }
+#ifdef QEH_EXPERIMENTS
     if (const char *e = std::getenv("QEH_WM_EXP")) sh.exp = std::atoi(e);
-    sh.spread = std::getenv("QEH_WM_SPREAD") ? 1 : 0;
+#endif
     return window_noid(ctx, func, part, order, asc, param, dflt, sh, out, folded ? &pre : nullptr);
 }
 

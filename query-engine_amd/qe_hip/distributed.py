@@ -684,8 +684,11 @@ class DistributedExecutor:
         handle = None
         if local_ok:  # phase A planned on the device from the gathered rows, while the host reads them
             self._sync_torch()
-            handle = self.ctx.fused_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(), self.world,
-                                                row_len)
+            try:
+                handle = self.ctx.fused_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(),
+                                                    self.world, row_len)
+            except abi.QehError:
+                handle = None  # (an OOM on this rank: it still joins every collective below, see `failed`)
         copied.synchronize()
         M = pinned.numpy().reshape(self.world, row_len).copy()
         live = M[M[:, 0] > 0]
@@ -707,10 +710,19 @@ class DistributedExecutor:
         # 4 B per dimension row (+ the runs' padding to 16 B); every rank uses the same shape
         nb, span = self.ctx.fused_items_shape(int(M[:, 0].max()), self.world)
         OW = 2 * (self.ITEMS_SLICES + 1)
-        items = torch.empty(nb * span, dtype=torch.int32, device="cuda")
-        offs = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
+        # A library error on this rank only (begin / build / finish: e.g. out of memory) must not leave the
+        # other ranks waiting in a collective: this rank sends empty items and a set status lane, so every
+        # rank's lanes come back flagged and every rank returns None together.
+        failed = handle is None
+        items = torch.zeros(nb * span, dtype=torch.int32, device="cuda")
+        offs = torch.zeros(nb * OW, dtype=torch.int32, device="cuda")
         self._sync_torch()
-        self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
+        if not failed:
+            try:
+                self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
+            except abi.QehError:
+                failed = True
+                items.zero_(), offs.zero_()
         self._sync()
         if self.world > 1:
             gi = torch.empty(self.world * nb * span, dtype=torch.int32, device="cuda")
@@ -721,8 +733,18 @@ class DistributedExecutor:
         nl = (1 + len(aggs)) * G + 1  # + the status lane
         lanes = torch.empty(nl, dtype=torch.float64, device="cuda")
         self._sync_torch()
-        self.ctx.fused_items_finish(handle, items.data_ptr(), span, offs.data_ptr(), self.world * nb, G,
-                                    lanes.data_ptr())
+        if not failed:
+            try:
+                self.ctx.fused_items_finish(handle, items.data_ptr(), span, offs.data_ptr(), self.world * nb, G,
+                                            lanes.data_ptr())
+            except abi.QehError:
+                failed = True
+            handle = None  # (finish frees it, also when it fails)
+        if failed:
+            if handle is not None:
+                self.ctx.fused_items_abort(handle)
+            lanes.zero_()
+            lanes[nl - 1] = 1.0
         self._sync()
         if self.world > 1:
             dist.all_reduce(lanes, op=dist.ReduceOp.SUM, group=self.group)
@@ -1062,8 +1084,11 @@ class DistributedExecutor:
         handle = None
         if local_ok:
             self._sync_torch()
-            handle = self.ctx.shuffle_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(), W, me,
-                                                  row_len)
+            try:
+                handle = self.ctx.shuffle_items_begin(probe_cols, probe_key_idx, predicate, aggs, row.data_ptr(), W,
+                                                      me, row_len)
+            except abi.QehError:
+                handle = None  # (this rank still joins the block-totals all-gather below, with ok = 0)
         copied.synchronize()
         M = pinned.numpy().reshape(W, row_len).copy()
         live = M[M[:, 0] > 0]
@@ -1086,14 +1111,23 @@ class DistributedExecutor:
         items = torch.empty(nb * span, dtype=torch.int32, device="cuda")
         offs = torch.empty(nb * OW, dtype=torch.int32, device="cuda")
         self._sync_torch()
-        self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
         # phase A's regions packed per destination (waits for phase A); the flag and the block totals of
-        # every rank in one all-gather
-        pk_ok, kp, vp, cp, blockcap, E, totals = self.ctx.shuffle_items_pack(handle, W)
+        # every rank in one all-gather -- a library error on this rank (e.g. out of memory) sends ok = 0, so
+        # every rank takes the two-pass form together instead of waiting in a collective
+        pk_ok, kp, vp, cp, blockcap, E, totals = False, 0, 0, 0, 0, 0, np.zeros(W, np.int64)
+        if handle is not None:
+            try:
+                self.ctx.fused_items_build(handle, build_key, gkc, nb, span, items.data_ptr(), offs.data_ptr())
+                pk_ok, kp, vp, cp, blockcap, E, totals = self.ctx.shuffle_items_pack(handle, W)
+            except abi.QehError:
+                pk_ok = False
+        if not pk_ok:
+            totals = np.zeros(W, np.int64)
         meta = torch.tensor(list(totals) + [1 if pk_ok else 0], dtype=torch.int64, device="cuda")
         Mt = _allgather_meta_t(meta, W, self.group)
         if int(Mt[:, W].min()) == 0:
-            self.ctx.fused_items_abort(handle)
+            if handle is not None:
+                self.ctx.fused_items_abort(handle)
             return None
         gi = torch.empty(W * nb * span, dtype=torch.int32, device="cuda")
         go = torch.empty(W * nb * OW, dtype=torch.int32, device="cuda")
