@@ -478,10 +478,71 @@ __global__ __launch_bounds__(kBlock) void k_full_embed(ColRef key, int64_t n, in
     }
 }
 
+// One Int64 build column whose values span < 2^31 - 1: 4-B records by key offset, (value - vmin) + 1 in
+// the low 31 bits (0 = no build row: no presence bitmap) and FULL's matched flag in bit 31 -- a quarter of
+// the 8-B records' footprint (plus the bitmap), so more of the random record reads hit an XCD's L2.
+// (R = uint16_t when the values span < 2^15 - 1: 2-B records, flag in bit 15)
+template <typename R>
+__global__ void k_embed_build32(ColRef key, int64_t n, int64_t kmin, const int64_t *__restrict__ b0, int64_t vmin,
+                                R *__restrict__ rec) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        rec[(uint64_t)load_i64(key, i) - (uint64_t)kmin] = (R)((uint64_t)(b0[i] - vmin) + 1u);
+    }
+}
+
+template <bool FULL, int NP, typename R>
+__global__ __launch_bounds__(kBlock) void k_outer_embed32(ColRef key, int64_t n, R *__restrict__ rec, int64_t kmin,
+                                                          int64_t kmax, int64_t vmin, FullEmbedOut out) {
+    constexpr uint32_t FLAG = 1u << (8 * sizeof(R) - 1), VAL = FLAG - 1u;
+    constexpr int U = 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t g0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * U; g0 * 64 < n; g0 += nw * U) {
+        uint64_t off[U];
+        uint32_t r[U];
+        int64_t pv[U][NP > 0 ? NP : 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pv[u][p] = i < n ? __builtin_nontemporal_load(out.pcol[p] + i) : 0;
+            const bool valid = i < n && col_valid(key, i);
+            const int64_t k = valid ? load_i64(key, i) : 0;
+            const bool in = valid && k >= kmin && k <= kmax;
+            off[u] = in ? (uint64_t)k - (uint64_t)kmin : 0;
+            r[u] = in ? (uint32_t)rec[off[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = (g0 + u) * 64 + lane;
+            const bool hit = (r[u] & VAL) != 0;
+            const uint64_t mask = __ballot(hit), rows = __ballot(i < n);
+            if (i < n) {
+                __builtin_nontemporal_store(hit ? vmin + (int64_t)(r[u] & VAL) - 1 : (int64_t)0, out.bout[0] + i);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) __builtin_nontemporal_store(pv[u][p], out.pout[p] + i);
+                if (FULL && hit && !(r[u] & FLAG)) rec[off[u]] = (R)(r[u] | FLAG);  // (idempotent)
+            }
+            if (lane == 0 && (g0 + u) * 64 < n) {
+                out.bvalid[0][g0 + u] = mask;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) out.pvalid[p][g0 + u] = rows;
+            }
+        }
+    }
+}
+
 // build rows with no matching probe row (a NULL key never matches), per block of kUmRows rows
 constexpr int kFtRows = kBlock * 8;
+// stride 0 / -1: 4-B / 2-B records (k_embed_build32, flag in the top bit); else 8-B records of `stride`
+// words, flag last
 __device__ __forceinline__ bool full_unmatched(const ColRef &bkey, int64_t j, int64_t kmin, const int64_t *rec, int stride) {
-    return !col_valid(bkey, j) || rec[((uint64_t)load_i64(bkey, j) - (uint64_t)kmin) * stride + stride - 1] == 0;
+    if (!col_valid(bkey, j)) return true;
+    const uint64_t off = (uint64_t)load_i64(bkey, j) - (uint64_t)kmin;
+    if (stride == 0) return (((const uint32_t *)rec)[off] >> 31) == 0;
+    if (stride < 0) return (((const uint16_t *)rec)[off] >> 15) == 0;
+    return rec[off * stride + stride - 1] == 0;
 }
 // (the flag of every build row also goes to um[] -- one byte, in order -- for the emit pass)
 __global__ void k_full_tail_count(ColRef bkey, int64_t nb, int64_t kmin, const int64_t *__restrict__ rec, int stride,
@@ -751,6 +812,17 @@ extern "C" int qeh_hash_join_inner(qeh_ctx *ctx, const qeh_column *probe_key, co
     return QEH_OK;
 }
 
+// one Int64 build column without NULLs whose values span < 2^31 - 1 (4-B records)
+// Returns the record width (0: not compact, 4, or 2 when the values span < 2^15 - 1).
+static int compact_records_ok(qeh_ctx *ctx, const qeh_column *bcols, int nbc, int64_t *vmin) {
+    if (nbc != 1 || bcols[0].dtype != QEH_DT_INT64 || std::getenv("QEH_NO_COMPACT_RECORDS")) return 0;
+    int64_t mn, mx, cnt;
+    if (column_minmax(ctx, bcols[0], &mn, &mx, &cnt) != QEH_OK || cnt != bcols[0].length) return 0;
+    if (cnt == 0 || (uint64_t)mx - (uint64_t)mn >= 0x7FFFFFFEull) return 0;
+    *vmin = mn;
+    return (uint64_t)mx - (uint64_t)mn < 0x7FFEull ? 2 : 4;
+}
+
 // FULL over a unique DIRECT build: k_full_embed for the probe rows, then the unmatched build rows
 // appended (k_full_tail_count / scan / k_full_tail_emit).  Output columns are allocated for every probe
 // and build row and hold the m rows that result.
@@ -762,16 +834,32 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
     auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
     // records of nbc build values + a matched flag word: a probe hit reads its record anyway, so it sets the
     // flag only when it reads it clear -- about one store per matched key instead of one per matching row
+    // (one Int64 build column of a narrow range: 4-B records, k_embed_build32)
     DevBuf rec, present;
-    const int stride = nbc + 1;
-    QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * stride, 1) * 8));
-    QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
-    QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+    int64_t vmin = 0;
+    const int rw = compact_records_ok(ctx, bcols, nbc, &vmin);
+    const bool r32 = rw != 0;
+    const int stride = rw == 4 ? 0 : rw == 2 ? -1 : nbc + 1;
+    if (r32) {
+        QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range, 1) * rw));
+        QEH_HIP(hipMemsetAsync(rec.p, 0, std::max<uint64_t>(range, 1) * rw, ctx->stream));
+    } else {
+        QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * stride, 1) * 8));
+        QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
+        QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+    }
     if (nbuild > 0) {
         KernelTimer kt(ctx, "join_build");
-        hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
-                           make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
-                           nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), stride);
+        if (rw == 4)
+            hipLaunchKernelGGL(k_embed_build32<uint32_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,
+                               ctx->stream, make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), vmin, rec.as<uint32_t>());
+        else if (rw == 2)
+            hipLaunchKernelGGL(k_embed_build32<uint16_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,
+                               ctx->stream, make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), vmin, rec.as<uint16_t>());
+        else
+            hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                               make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
+                               nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), stride);
     }
     int made_p = 0, made_b = 0, s = QEH_OK;
     FullEmbedOut eo{};
@@ -806,7 +894,16 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
             hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n, rec.as<int64_t>(),
                                present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
         };
-        if (nbc == 1) go(std::integral_constant<int, 1>{});
+        auto go32 = [&](auto rt) {
+            typedef decltype(rt) R;
+            auto k = npc == 0 ? k_outer_embed32<true, 0, R> : npc == 1 ? k_outer_embed32<true, 1, R>
+                   : npc == 2 ? k_outer_embed32<true, 2, R> : k_outer_embed32<true, 3, R>;
+            hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n, rec.as<R>(), bt.t.kmin,
+                               bt.t.kmax, vmin, eo);
+        };
+        if (rw == 4) go32(uint32_t{});
+        else if (rw == 2) go32(uint16_t{});
+        else if (nbc == 1) go(std::integral_constant<int, 1>{});
         else if (nbc == 2) go(std::integral_constant<int, 2>{});
         else go(std::integral_constant<int, 3>{});
         if (hipGetLastError() != hipSuccess) s = fail(QEH_E_HIP, "outer join: kernel launch failed");
@@ -904,15 +1001,30 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         const uint64_t range = bt.t.range;
         const int64_t n = pk.length, nbuild = bk.length;
         DevBuf rec, present;
-        QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * nbc, 1) * 8));
-        QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
-        QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+        int64_t vmin = 0;
+        const int rw = compact_records_ok(ctx, bcols, nbc, &vmin);
+        const bool r32 = rw != 0;
         auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
+        if (r32) {
+            QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range, 1) * rw));
+            QEH_HIP(hipMemsetAsync(rec.p, 0, std::max<uint64_t>(range, 1) * rw, ctx->stream));
+        } else {
+            QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range * nbc, 1) * 8));
+            QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
+            QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
+        }
         if (nbuild > 0) {
             KernelTimer kt(ctx, "join_build");
-            hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
-                               make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
-                               nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), nbc);
+            if (rw == 4)
+                hipLaunchKernelGGL(k_embed_build32<uint32_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,
+                                   ctx->stream, make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), vmin, rec.as<uint32_t>());
+            else if (rw == 2)
+                hipLaunchKernelGGL(k_embed_build32<uint16_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,
+                                   ctx->stream, make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), vmin, rec.as<uint16_t>());
+            else
+                hipLaunchKernelGGL(k_embed_build, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0, ctx->stream,
+                                   make_colref(bk), nbuild, bt.t.kmin, cptr(bcols[0]), nbc > 1 ? cptr(bcols[1]) : nullptr,
+                                   nbc > 2 ? cptr(bcols[2]) : nullptr, nbc, rec.as<int64_t>(), present.as<uint32_t>(), nbc);
         }
         int made = 0, s = QEH_OK;
         OuterEmbedOut eo{};
@@ -927,7 +1039,17 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         if (s == QEH_OK && n > 0) {
             KernelTimer kt(ctx, "join_probe");
             const int grid = grid_for(ctx, (n + 255) / 256, kBlock / 64, 8);
-            if (nbc == 1)
+            if (r32) {
+                FullEmbedOut fo{};
+                fo.bout[0] = eo.bout[0];
+                fo.bvalid[0] = eo.bvalid[0];
+                if (rw == 4)
+                    hipLaunchKernelGGL((k_outer_embed32<false, 0, uint32_t>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                                       make_colref(pk), n, rec.as<uint32_t>(), bt.t.kmin, bt.t.kmax, vmin, fo);
+                else
+                    hipLaunchKernelGGL((k_outer_embed32<false, 0, uint16_t>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                                       make_colref(pk), n, rec.as<uint16_t>(), bt.t.kmin, bt.t.kmax, vmin, fo);
+            } else if (nbc == 1)
                 hipLaunchKernelGGL(k_outer_embed<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n,
                                    rec.as<int64_t>(), present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
             else if (nbc == 2)

@@ -467,6 +467,33 @@ def test_outer_join_embedded_build_path(ctx, jt, nb):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bkind", ["int_narrow", "int_mid", "float", "two_cols", "int_wide"])
+@pytest.mark.parametrize("npc,nprobe", [(0, 1), (1, 64), (2, 300_007), (3, 131_072)])
+def test_full_join_fused_paths(ctx, bkind, npc, nprobe):
+    """FULL over a unique DIRECT build (k_full_embed / k_outer_embed32 + the appended unmatched build rows):
+    NULL probe keys, build keys never probed, probe columns copied (0-3, non-null 8-byte), the build columns
+    as 2-B / 4-B records (one narrow Int64 column) or 8-B records with the flag word; every row vs the oracle."""
+    r = np.random.default_rng(npc * 7 + nprobe + len(bkind))
+    nbuild = 40_000
+    bk = (r.permutation(90_000)[:nbuild] + 500).astype(np.int64)
+    pk = r.integers(0, 91_000, nprobe).astype(np.int64)
+    pkv = r.random(nprobe) > 0.03
+    if bkind == "int_narrow":
+        bcols = [(r.integers(-700, 700, nbuild).astype(np.int64), None)]
+    elif bkind == "int_mid":  # 4-B records
+        bcols = [(r.integers(-(1 << 20), 1 << 20, nbuild).astype(np.int64), None)]
+    elif bkind == "int_wide":
+        bcols = [(r.integers(-(2 ** 62), 2 ** 62, nbuild).astype(np.int64), None)]
+    elif bkind == "float":
+        bcols = [(r.random(nbuild), None)]
+    else:
+        bcols = [(r.random(nbuild), None), (bk * 3, None)]
+    pcols = [(pk, None), (r.random(nprobe), None), (r.integers(-5, 5, nprobe).astype(np.int64), None)][:npc]
+    got, want = outer_both(ctx, "full", (pk, pkv), pcols, (bk, None), bcols)
+    assert sorted_rows(got) == sorted_rows(want)
+
+
+@pytest.mark.gpu
 def test_row_number_windowed_scatter_path(ctx, monkeypatch):
     """n > 2^22: the direct scatter and the experimental windowed scatter (QEH_RN_WINDOWED:
     (destination, rn) pairs grouped by output window by one radix pass) both match the oracle."""
