@@ -164,6 +164,23 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
         gid = e - 1u;
         return e != 0;
     }
+    if (t.kind == TK_BUCKET) {
+        const int S = bucket_slots(t.pbits);
+        uint64_t b = bucket_home(t, (uint64_t)key);
+        for (uint64_t step = 0; step < t.nbkt; ++step) {
+            uint64_t w[8];
+            bucket_load(t, b, w);
+            const uint32_t cnt = (uint32_t)(w[7] >> 32);
+            for (int s = 0; s < S; ++s)
+                if (s < (int)cnt && (int64_t)w[s] == key) {
+                    gid = bucket_payload(w, s, t.pbits) - 1u;
+                    return true;
+                }
+            if (cnt <= (uint32_t)S) return false;
+            b = b + 1 == t.nbkt ? 0 : b + 1;
+        }
+        return false;
+    }
     uint64_t h = hash64((uint64_t)key) & t.mask;
     if (t.kind == TK_WIDE) {
         for (uint64_t i = 0; i <= t.mask; ++i) {
@@ -2336,6 +2353,7 @@ static bool try_fast_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
 static uint64_t table_bytes(const HashTable &t) {
     if (t.kind == TK_DIRECT) return t.range * (t.payload16 ? 2 : 4);
     if (t.kind == TK_PACKED) return (t.mask + 1) * 8;
+    if (t.kind == TK_BUCKET) return t.nbkt * 64;
     return (t.mask + 1) * 16;
 }
 

@@ -311,7 +311,31 @@ __global__ void k_insert_wide(ColRef key, int64_t n, RowPayload row_payload, Has
     }
 }
 
-// Duplicate detection for WIDE tables (separate launch: all slots are final).
+// BUCKET: one returning atomic on the bucket's count word claims slot s; a full bucket sends the key on
+// to the next one (the count keeps rising there, which tells probes to follow).  Payload halves and the
+// count share bytes of one word: byte-granular stores beside a 4-B atomic on the other bytes.
+__global__ void k_insert_bucket(ColRef key, int64_t n, RowPayload row_payload, HashTable t) {
+    const int S = bucket_slots(t.pbits);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!col_valid(key, i)) continue;
+        const int64_t k = load_i64(key, i);
+        const uint32_t e = payload_of(row_payload, i) + 1u;
+        uint64_t b = bucket_home(t, (uint64_t)k);
+        for (uint64_t step = 0; step < t.nbkt; ++step) {
+            uint64_t *line = t.slots + b * 8;
+            const uint32_t s = atomicAdd((uint32_t *)(line + 7) + 1, 1u);
+            if (s < (uint32_t)S) {
+                line[s] = (uint64_t)k;
+                if (t.pbits == 16) ((uint16_t *)(line + S))[s] = (uint16_t)e;
+                else ((uint32_t *)(line + S))[s] = e;
+                break;
+            }
+            b = b + 1 == t.nbkt ? 0 : b + 1;
+        }
+    }
+}
+
+// Duplicate detection for WIDE / BUCKET tables (separate launch: all slots are final).
 __global__ void k_wide_dups(ColRef key, int64_t n, HashTable t, uint32_t *dup) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (!col_valid(key, i)) continue;
@@ -584,6 +608,12 @@ static int bits_for(uint64_t v) {  // bits to represent values 0..v
     return b;
 }
 
+// BUCKET payload width for a build's largest payload: 16 or 32 bits, 0 = too wide (QEH_NO_BUCKET=1: never)
+static int bucket_pbits(uint64_t payload_max) {
+    if (std::getenv("QEH_NO_BUCKET")) return 0;
+    return payload_max < 0xFFFFull ? 16 : payload_max < 0xFFFFFFFFull ? 32 : 0;
+}
+
 int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_payload, uint64_t payload_max,
                      BuiltTable *out, int force_kind) {
     QEH_TRY(check_column(key, "join key"));
@@ -619,7 +649,8 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
     const bool packed_ok = kbits + pbits <= 64;
     if (kind == TK_DIRECT && !direct_ok) kind = -1;
     if (kind == TK_PACKED && !packed_ok) kind = -1;
-    if (kind < 0) kind = direct_ok ? TK_DIRECT : (packed_ok ? TK_PACKED : TK_WIDE);
+    if (kind < 0) kind = direct_ok ? TK_DIRECT : (packed_ok ? TK_PACKED : bucket_pbits(payload_max) ? TK_BUCKET : TK_WIDE);
+    if (kind == TK_BUCKET && !bucket_pbits(payload_max)) kind = TK_WIDE;
 
     DevBuf flag;
     QEH_TRY(flag.alloc(ctx, 8));
@@ -694,8 +725,34 @@ int build_join_table(qeh_ctx *ctx, const qeh_column &key, const RowPayload &row_
         // duplicate build keys: a perfect-hash slot holds one row; rebuild hashed
         out->payload.reset();
         QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
-        kind = packed_ok ? TK_PACKED : TK_WIDE;
+        kind = packed_ok ? TK_PACKED : bucket_pbits(payload_max) ? TK_BUCKET : TK_WIDE;
         if (force_kind == TK_DIRECT) force_kind = -1;
+    }
+
+    if (kind == TK_BUCKET) {
+        t.kind = TK_BUCKET;
+        t.pbits = bucket_pbits(payload_max);
+        t.nbkt = std::max<uint64_t>(64, (nv * 10 + 6 * bucket_slots(t.pbits) - 1) / (6 * bucket_slots(t.pbits)));  // 60 % load
+        QEH_TRY(out->slots.alloc(ctx, t.nbkt * 64));
+        t.slots = out->slots.as<uint64_t>();
+        {
+            KernelTimer kt(ctx, "join_build");
+            QEH_HIP(hipMemsetAsync(t.slots, 0, t.nbkt * 64, ctx->stream));
+            hipLaunchKernelGGL(k_insert_bucket, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, row_payload, t);
+            t.unique = 0;
+            hipLaunchKernelGGL(k_wide_dups, dim3(grid), dim3(kBlock), 0, ctx->stream, kr, n, t, flag.as<uint32_t>());
+        }
+        QEH_HIP(hipGetLastError());
+        QEH_TRY(read_small(ctx, &dup, flag.p, 4));
+        if (!dup) {
+            t.unique = 1;
+            return QEH_OK;
+        }
+        // repeated build keys: the WIDE layout (multi-match probing over 16-B slots)
+        out->slots.reset();
+        t.slots = nullptr;
+        QEH_HIP(hipMemsetAsync(flag.p, 0, 8, ctx->stream));
+        kind = TK_WIDE;
     }
 
     const uint64_t cap = std::max<uint64_t>(1024, next_pow2((nv * 5 + 2) / 3));

@@ -67,6 +67,7 @@ int forced_table_kind() {
     if (!std::strcmp(e, "direct")) return TK_DIRECT;
     if (!std::strcmp(e, "packed")) return TK_PACKED;
     if (!std::strcmp(e, "wide")) return TK_WIDE;
+    if (!std::strcmp(e, "bucket")) return TK_BUCKET;
     return -1;
 }
 

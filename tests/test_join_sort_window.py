@@ -51,7 +51,30 @@ def test_join_duplicates_nulls_int32_keys(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["direct", "packed", "wide"])
+@pytest.mark.parametrize("nbuild", [1, 7, 5_000, 300_000])
+@pytest.mark.parametrize("payload", ["rows", "rows_null_keys", "dup_keys"])
+def test_bucket_table_sparse_keys(ctx, monkeypatch, nbuild, payload):
+    """The BUCKET layout (64-B buckets of 5-6 keys, chained by insert counts) for sparse 64-bit keys: the
+    INNER / LEFT join's build-row payloads are 32-bit for large builds, 16-bit below 65535 rows; a repeated
+    build key falls back to WIDE; NULL keys never match; keys absent from the build miss."""
+    monkeypatch.setenv("QEH_FORCE_TABLE", "bucket")
+    r = np.random.default_rng(nbuild + len(payload))
+    bk = r.integers(-(2 ** 62), 2 ** 62, nbuild, dtype=np.int64)
+    bkv = None
+    if payload == "dup_keys" and nbuild > 1:
+        bk[-1] = bk[0]
+    if payload == "rows_null_keys":
+        bkv = r.random(nbuild) > 0.1
+    pk = np.concatenate([bk[r.integers(0, nbuild, 200_000)], r.integers(-(2 ** 62), 2 ** 62, 50_000, dtype=np.int64)])
+    pv = r.random(len(pk))
+    got, want = join_both(ctx, (pk, None), [(pk, None), (pv, None)], (bk, bkv), [(bk, bkv)])
+    assert sorted_rows(got) == sorted_rows(want)
+    got, want = outer_both(ctx, "left", (pk, None), [(pk, None), (pv, None)], (bk, bkv), [(bk, bkv)])
+    assert sorted_rows(got) == sorted_rows(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("table", ["direct", "packed", "wide", "bucket"])
 def test_join_table_layouts(ctx, monkeypatch, table):
     monkeypatch.setenv("QEH_FORCE_TABLE", table)
     r = np.random.default_rng(2)

@@ -64,7 +64,7 @@ def test_metric_shape(ctx, n_fact, n_dim, groups):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["direct", "packed", "wide"])
+@pytest.mark.parametrize("table", ["direct", "packed", "wide", "bucket"])
 def test_forced_table_layouts(ctx, monkeypatch, table):
     monkeypatch.setenv("QEH_FORCE_TABLE", table)
     x, k, v, dk, dg = metric_data(300_000, 30_000, 512)
