@@ -169,14 +169,41 @@ extern "C" int qeh_merge_sorted(qeh_ctx *ctx, const qeh_column *parts, int n_par
     for (int k = 0; k < n_keys; ++k)
         if (key_idx[k] < 0 || key_idx[k] >= n_cols) return fail(QEH_E_INVALID, "qeh_merge_sorted: sort column out of range");
     DeviceGuard dg(ctx->device);
+    if (n_keys == 1 && n_cols == 2 && n_parts <= 16) {
+        // one key and one 8-byte payload: the payload rides through the radix passes (no gathers), and the
+        // first pass reads the partitions in place -- the concatenation (operators.rs:206-216) is never
+        // materialised
+        const int kj = key_idx[0], vj = 1 - key_idx[0];
+        std::vector<qeh_column> kp(n_parts), vp(n_parts);
+        bool ok = true;
+        for (int p = 0; p < n_parts; ++p) {
+            kp[p] = parts[(size_t)p * n_cols + kj];
+            vp[p] = parts[(size_t)p * n_cols + vj];
+            ok = ok && check_column(kp[p], "merge key") == QEH_OK && check_column(vp[p], "merge column") == QEH_OK;
+        }
+        qeh_column ok_{}, ov{};
+        const int ps = ok ? sort_pairs_payload_parts(ctx, kp.data(), vp.data(), n_parts, ascending ? ascending[0] != 0 : true,
+                                                     nulls_first ? nulls_first[0] != 0 : true, &ok_, &ov)
+                          : kPayloadSortNotEligible;
+        if (ps != kPayloadSortNotEligible) {
+            QEH_TRY(ps);
+            out[kj] = ok_;
+            out[vj] = ov;
+            *out_rows = ok_.length;
+            return QEH_OK;
+        }
+    }
     // concat_batches (operators.rs:206-216): parts is [n_parts][n_cols], row-major by partition
     std::vector<qeh_column> cat(n_cols);
     int made = 0, s = QEH_OK;
-    for (int j = 0; j < n_cols && s == QEH_OK; ++j) {
-        std::vector<const qeh_column *> pp(n_parts);
-        for (int p = 0; p < n_parts; ++p) pp[p] = &parts[(size_t)p * n_cols + j];
-        s = concat_columns(ctx, pp.data(), n_parts, &cat[j]);
-        if (s == QEH_OK) ++made;
+    {
+        KernelTimer kt(ctx, "merge_concat");  // (part of Merge::sorted's device time: tools/bench_configs.py cfg_merge)
+        for (int j = 0; j < n_cols && s == QEH_OK; ++j) {
+            std::vector<const qeh_column *> pp(n_parts);
+            for (int p = 0; p < n_parts; ++p) pp[p] = &parts[(size_t)p * n_cols + j];
+            s = concat_columns(ctx, pp.data(), n_parts, &cat[j]);
+            if (s == QEH_OK) ++made;
+        }
     }
     auto release_cat = [&]() {
         for (int j = 0; j < made; ++j) qeh_column_release(ctx, &cat[j]);

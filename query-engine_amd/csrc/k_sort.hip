@@ -45,14 +45,18 @@ __device__ __forceinline__ int64_t ordered_key(const ColRef &c, int64_t row) {
     return x;
 }
 
-__global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t n, KeyStats *out) {
+constexpr int kRsMaxSegs = 16;  // Merge::sorted partitions read in place (RsEncode, KeySegs)
+
+// (block bid of nb over the rows: k_key_stats runs it for one column, k_key_stats_segs for one segment each)
+__device__ __forceinline__ void key_stats_body(const ColRef &c, const uint32_t *__restrict__ perm, int64_t n, KeyStats *out,
+                                               int64_t bid, int64_t nb) {
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     if (!perm && !c.validity && c.dtype == QEH_DT_INT64 && ((uintptr_t)c.values & 15) == 0) {
         // plain int64 column: 16-B loads, four in flight per thread
         typedef long long v2 __attribute__((ext_vector_type(2)));
         const v2 *kv = (const v2 *)c.values;
-        const int64_t pairs = n / 2, stride = (int64_t)gridDim.x * blockDim.x;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pairs; i += 4 * stride) {
+        const int64_t pairs = n / 2, stride = nb * blockDim.x;
+        for (int64_t i = bid * blockDim.x + threadIdx.x; i < pairs; i += 4 * stride) {
             v2 q[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) q[u] = kv[i + u * stride < pairs ? i + u * stride : i];
@@ -64,7 +68,7 @@ __global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t
                 mx = q[u].y > mx ? q[u].y : mx;
             }
         }
-        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        if ((n & 1) && bid == 0 && threadIdx.x == 0) {
             const int64_t k = ((const int64_t *)c.values)[n - 1];
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
@@ -74,8 +78,8 @@ __global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t
         // (one validity byte, four 16-B loads), rows of NULLs skipped by mask
         typedef long long v2 __attribute__((ext_vector_type(2)));
         const uint8_t *vb = c.validity + (c.vbit0 >> 3);
-        const int64_t groups = n / 8, stride = (int64_t)gridDim.x * blockDim.x;
-        for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
+        const int64_t groups = n / 8, stride = nb * blockDim.x;
+        for (int64_t g = bid * blockDim.x + threadIdx.x; g < groups; g += stride) {
             const uint32_t m = vb[g];
             const v2 *kv = (const v2 *)c.values + g * 4;
             v2 q[4];
@@ -87,14 +91,14 @@ __global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t
                 if ((m >> (2 * u + 1)) & 1u) mn = q[u].y < mn ? q[u].y : mn, mx = q[u].y > mx ? q[u].y : mx;
             }
         }
-        for (int64_t i = groups * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        for (int64_t i = groups * 8 + bid * blockDim.x + threadIdx.x; i < n; i += stride) {
             if (!col_valid(c, i)) continue;
             const int64_t k = ((const int64_t *)c.values)[i];
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
         }
     } else {
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        for (int64_t i = bid * blockDim.x + threadIdx.x; i < n; i += nb * blockDim.x) {
             const int64_t r = perm ? perm[i] : i;
             if (!col_valid(c, r)) continue;
             const int64_t k = ordered_key(c, r);
@@ -112,6 +116,21 @@ __global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t
         atomicMin((long long *)&out->mn, (long long)mn);
         atomicMax((long long *)&out->mx, (long long)mx);
     }
+}
+
+__global__ void k_key_stats(ColRef c, const uint32_t *__restrict__ perm, int64_t n, KeyStats *out) {
+    key_stats_body(c, perm, n, out, blockIdx.x, gridDim.x);
+}
+
+// one launch over up to kRsMaxSegs columns (Merge::sorted's partitions): gps blocks per segment
+struct KeySegs {
+    int32_t ns, gps;
+    ColRef c[kRsMaxSegs];
+    int64_t n[kRsMaxSegs];
+};
+__global__ void k_key_stats_segs(KeySegs ks, KeyStats *out) {
+    const int seg = blockIdx.x / ks.gps;
+    key_stats_body(ks.c[seg], nullptr, ks.n[seg], out, blockIdx.x % ks.gps, ks.gps);
 }
 
 __global__ void k_stats_init(KeyStats *s) {
@@ -181,23 +200,73 @@ __device__ __forceinline__ uint32_t tile_rank(uint32_t *wc, uint32_t dg, bool li
 
 // The payload sort's first pass reads the raw key column and encodes on load (KES = 4 / 8: Int32 /
 // Int64 values) instead of a separate encode pass; KES = 0 reads the codes.
+// ns > 0: the first pass reads the key and payload in place from ns row segments (qeh_merge_sorted's
+// partitions: rows [start[s], start[s + 1]) are segment s's rows 0..) instead of one column -- no
+// concatenation copy ahead of the sort (kRsMaxSegs: at the top of the file)
 struct RsEncode {
     ColRef c;
     int64_t mn, mx;
     uint64_t bias, null_code;
     int32_t asc;
+    int32_t ns;
+    int64_t start[kRsMaxSegs + 1];
+    ColRef sk[kRsMaxSegs];
+    const uint64_t *sv[kRsMaxSegs];
 };
 
+// the segment of row i (branch-free count of the segment starts at or below i)
+__device__ __forceinline__ int rs_seg(const RsEncode &e, int64_t i) {
+    int s = 0;
+#pragma unroll
+    for (int q = 1; q < kRsMaxSegs; ++q) s += (q < e.ns && i >= e.start[q]) ? 1 : 0;
+    return s;
+}
+
+// the segment of a tile's rows [a, b] when they share one (wave-uniform: a scalar index into the kernel
+// arguments), else -1 (rows straddle a partition boundary: looked up per row)
+__device__ __forceinline__ int rs_tile_seg(const RsEncode &e, int64_t a, int64_t b) {
+    if (!e.ns) return 0;
+    const int sa = rs_seg(e, a), sb = rs_seg(e, b);
+    return __builtin_amdgcn_readfirstlane(sa == sb ? sa : -1);
+}
+
+template <int KES>
+__device__ __forceinline__ uint64_t rs_code(const RsEncode &e, const ColRef &c, int64_t i) {
+    const int64_t x = KES == 4 ? (int64_t)__builtin_nontemporal_load((const int32_t *)c.values + i)
+                               : __builtin_nontemporal_load((const int64_t *)c.values + i);
+    const uint64_t code = e.asc ? (uint64_t)x - (uint64_t)e.mn + e.bias : (uint64_t)e.mx - (uint64_t)x + e.bias;
+    return col_valid(c, i) ? code : e.null_code;
+}
+
+// (segments are only ever indexed by a wave-uniform value: a per-lane index into the kernel arguments
+// would copy the whole RsEncode to scratch)
 template <int KES, typename KeyT>
-__device__ __forceinline__ KeyT rs_load_key(const KeyT *__restrict__ keys, const RsEncode &e, int64_t i) {
+__device__ __forceinline__ KeyT rs_load_key(const KeyT *__restrict__ keys, const RsEncode &e, int64_t i, int ts = 0) {
     if constexpr (KES == 0) {
         return __builtin_nontemporal_load(&keys[i]);
     } else {
-        const int64_t x = KES == 4 ? (int64_t)__builtin_nontemporal_load((const int32_t *)e.c.values + i)
-                                   : __builtin_nontemporal_load((const int64_t *)e.c.values + i);
-        const uint64_t code = e.asc ? (uint64_t)x - (uint64_t)e.mn + e.bias : (uint64_t)e.mx - (uint64_t)x + e.bias;
-        return (KeyT)(col_valid(e.c, i) ? code : e.null_code);
+        if (!e.ns) return (KeyT)rs_code<KES>(e, e.c, i);
+        if (ts >= 0) return (KeyT)rs_code<KES>(e, e.sk[ts], i - e.start[ts]);
+        uint64_t code = 0;
+        for (int s = 0; s < e.ns; ++s)  // (a tile across a partition boundary)
+            if (i >= e.start[s] && i < e.start[s + 1]) code = rs_code<KES>(e, e.sk[s], i - e.start[s]);
+        return (KeyT)code;
     }
+}
+
+// the first pass's payload of row i (in place from the segments when ns > 0)
+template <int KES, typename ValT>
+__device__ __forceinline__ ValT rs_load_val(const ValT *__restrict__ vals, const RsEncode &e, int64_t i, int ts = 0) {
+    if constexpr (KES != 0 && sizeof(ValT) == 8) {
+        if (e.ns) {
+            if (ts >= 0) return (ValT)__builtin_nontemporal_load(e.sv[ts] + (i - e.start[ts]));
+            ValT v = 0;
+            for (int s = 0; s < e.ns; ++s)
+                if (i >= e.start[s] && i < e.start[s + 1]) v = (ValT)__builtin_nontemporal_load(e.sv[s] + (i - e.start[s]));
+            return v;
+        }
+    }
+    return __builtin_nontemporal_load(&vals[i]);
 }
 
 template <typename KeyT, int KES = 0>
@@ -211,11 +280,12 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t c0 = lo; c0 < hi; c0 += kRsSTile) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
+        const int ts = KES != 0 ? rs_tile_seg(enc, c0, (c0 + kRsSTile < hi ? c0 + kRsSTile : hi) - 1) : 0;
         KeyT k[kRsIpt];
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
-            k[j] = rs_load_key<KES>(keys, enc, i < hi ? i : hi - 1);
+            k[j] = rs_load_key<KES>(keys, enc, i < hi ? i : hi - 1, ts);
         }
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
@@ -332,12 +402,13 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const KeyT *__restric
     // stays in flight across the ranking of the current tile
     auto load_tile = [&](int64_t c0, KeyT *kk, ValT *vv) {
         const int64_t base = c0 + (int64_t)wave * 64 * kRsIpt + lane;
+        const int ts = KES != 0 ? rs_tile_seg(enc, c0, (c0 + kRsSTile < hi ? c0 + kRsSTile : hi) - 1) : 0;
 #pragma unroll
         for (int j = 0; j < kRsIpt; ++j) {
             const int64_t i = base + j * 64;
             const int64_t ii = i < hi ? i : hi - 1;
-            kk[j] = rs_load_key<KES>(keys, enc, ii);
-            vv[j] = __builtin_nontemporal_load(&vals[ii]);
+            kk[j] = rs_load_key<KES>(keys, enc, ii, ts);
+            vv[j] = rs_load_val<KES>(vals, enc, ii, ts);
         }
     };
     if (lo < hi) load_tile(lo, k, v);
@@ -1792,12 +1863,28 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
 
 int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_column &val, bool asc, bool nulls_first,
                             qeh_column *out_key, qeh_column *out_val) {
-    const int64_t n = key.length;
-    if (std::getenv("QEH_NO_PAYLOAD_SORT") || n <= 1 || n >= ((int64_t)1 << 32) || val.length != n) return kPayloadSortNotEligible;
+    return sort_pairs_payload_parts(ctx, &key, &val, 1, asc, nulls_first, out_key, out_val);
+}
+
+// The key / payload as nparts row segments (Merge::sorted's partitions, concatenated in order): the first
+// pass reads them in place (RsEncode.ns); every later pass works on the sort's own buffers.
+int qeh::sort_pairs_payload_parts(qeh_ctx *ctx, const qeh_column *keys, const qeh_column *vals, int nparts, bool asc,
+                                  bool nulls_first, qeh_column *out_key, qeh_column *out_val) {
+    if (nparts < 1 || nparts > kRsMaxSegs) return kPayloadSortNotEligible;
+    const qeh_column &key = keys[0], &val = vals[0];
+    int64_t n = 0;
+    bool nullable = false;
+    for (int p = 0; p < nparts; ++p) {
+        if (keys[p].dtype != key.dtype || vals[p].dtype != val.dtype || vals[p].length != keys[p].length)
+            return kPayloadSortNotEligible;
+        if (vals[p].validity && vals[p].null_count != 0) return kPayloadSortNotEligible;
+        nullable = nullable || (keys[p].validity && keys[p].null_count != 0);
+        n += keys[p].length;
+    }
+    if (std::getenv("QEH_NO_PAYLOAD_SORT") || n <= 1 || n >= ((int64_t)1 << 32)) return kPayloadSortNotEligible;
     if (key.dtype != QEH_DT_INT64 && key.dtype != QEH_DT_INT32) return kPayloadSortNotEligible;
     if (rs_ballot(ctx)) return kPayloadSortNotEligible;  // its passes rank by LDS atomics only
-    if ((val.dtype != QEH_DT_INT64 && val.dtype != QEH_DT_FLOAT64) || (val.validity && val.null_count != 0))
-        return kPayloadSortNotEligible;
+    if (val.dtype != QEH_DT_INT64 && val.dtype != QEH_DT_FLOAT64) return kPayloadSortNotEligible;
     const ColRef kc = make_colref(key);
     DevBuf st;
     QEH_TRY(st.alloc(ctx, sizeof(KeyStats)));
@@ -1805,14 +1892,21 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     {
         KernelTimer kt(ctx, "sort_encode");
         hipLaunchKernelGGL(k_stats_init, dim3(1), dim3(1), 0, ctx->stream, st.as<KeyStats>());
-        hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kc, nullptr, n,
-                           st.as<KeyStats>());
+        if (nparts == 1) {
+            hipLaunchKernelGGL(k_key_stats, dim3(grid_for(ctx, n, kBlock * 8, 1)), dim3(kBlock), 0, ctx->stream, kc, nullptr,
+                               n, st.as<KeyStats>());
+        } else {  // every partition in one launch
+            KeySegs kss{};
+            kss.ns = nparts;
+            kss.gps = std::max(1, grid_for(ctx, n, kBlock * 8, 1) / nparts);
+            for (int p = 0; p < nparts; ++p) kss.c[p] = make_colref(keys[p]), kss.n[p] = keys[p].length;
+            hipLaunchKernelGGL(k_key_stats_segs, dim3(nparts * kss.gps), dim3(kBlock), 0, ctx->stream, kss, st.as<KeyStats>());
+        }
     }
     QEH_TRY(read_small(ctx, &ks, st.p, sizeof ks));
     const bool any_valid = ks.mn <= ks.mx;
     const int64_t mn = any_valid ? ks.mn : 0, mx = any_valid ? ks.mx : 0;
     const uint64_t range = (uint64_t)mx - (uint64_t)mn;  // value codes 0 .. range (+ bias)
-    const bool nullable = key.validity && key.null_count != 0;
     const uint64_t bias = nullable && nulls_first ? 1 : 0;
     const uint64_t null_code = nullable && nulls_first ? 0 : range + 1;  // (no NULLs: never produced)
     // the largest code: range (+ 1 for the NULL code when nullable); a nullable key spanning the
@@ -1843,7 +1937,20 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     vb[npass % 2] = (uint64_t *)out_val->values;
     vb[(npass + 1) % 2] = vtmp.as<uint64_t>();
     // pass 0 encodes the key column on load (histogram and scatter), the last pass decodes on store
-    const RsEncode enc{kc, mn, mx, bias, null_code, asc ? 1 : 0};
+    RsEncode enc{kc, mn, mx, bias, null_code, asc ? 1 : 0};
+    auto segs = [&](RsEncode &e) {
+        if (nparts == 1) return;
+        e.ns = nparts;
+        int64_t at = 0;
+        for (int p = 0; p < nparts; ++p) {
+            e.start[p] = at;
+            e.sk[p] = make_colref(keys[p]);
+            e.sv[p] = (const uint64_t *)((const char *)vals[p].values + (size_t)vals[p].offset * 8);
+            at += keys[p].length;
+        }
+        e.start[nparts] = at;
+    };
+    segs(enc);
     const RsDecode dec{mn, mx, bias, null_code, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
     const bool k32 = key.dtype == QEH_DT_INT32;
     // codes of 24..45 bits over many rows: the MSD passes (three passes over the rows); a sub-bucket
@@ -1867,7 +1974,8 @@ int qeh::sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_colum
     }
     bool done = false;
     if (mbits) {
-        const RsEncode encm{kc, mn, mx, mbias, mnull, asc ? 1 : 0};
+        RsEncode encm{kc, mn, mx, mbias, mnull, asc ? 1 : 0};
+        segs(encm);
         const RsDecode decm{mn, mx, mbias, mnull, asc ? 1 : 0, key.dtype, out_key->values, nullable ? validb.as<uint8_t>() : nullptr};
         const int r = msd_payload_passes(ctx, key, vsrc, n, mbits, encm, decm, kb[0].as<uint64_t>(), kb[1].as<uint64_t>(),
                                          vtmp.as<uint64_t>(), (uint64_t *)out_val->values);

@@ -76,6 +76,8 @@ int columns_minmax_collect(qeh_ctx *ctx, const qeh_column *cols, int n, const Mi
 // the radix passes (no gather): the sorted key and payload columns.  kPayloadSortNotEligible when
 // the shapes do not fit (nothing allocated).
 constexpr int kPayloadSortNotEligible = -3;
+int sort_pairs_payload_parts(qeh_ctx *ctx, const qeh_column *keys, const qeh_column *vals, int nparts, bool asc,
+                             bool nulls_first, qeh_column *out_key, qeh_column *out_val);
 int sort_pairs_payload(qeh_ctx *ctx, const qeh_column &key, const qeh_column &val, bool asc, bool nulls_first,
                        qeh_column *out_key, qeh_column *out_val);
 // min / max / valid count of an integer column (one synchronous read).

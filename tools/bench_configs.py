@@ -306,7 +306,7 @@ def cfg_merge(ctx, scale):
         for c in cols:
             c.release()
         return rows
-    wall, kt, rows = timed(ctx, fn, 3, ["radix_pass", "sort_encode", "gather"])
+    wall, kt, rows = timed(ctx, fn, 3, ["merge_concat", "radix_pass", "sort_encode", "gather"])
     hk = [p[0].to_numpy() for p in parts]
     m = 4_000_000
     hkk = np.concatenate([a for a, _ in hk])[:m]
