@@ -729,6 +729,92 @@ def test_inner_join_full_size_properties(ctx):
     assert int((a_out * lo_out).sum()) == int((a_in * lo_in).sum())
 
 
+_FP = (0x1E3779B97F4A7C15, 0x42B2AE3D27D4EB4F, 0x3F58476D1CE4E5B9)
+
+
+def _pair_fingerprint(vb, a):
+    """Order-independent fingerprint of the (v bits, a) pairs: Σ of a 64-bit mix per pair, wrapping.
+    The same int64 expression runs in numpy (host) and torch (device): products and sums wrap, >> is
+    arithmetic in both."""
+    h = vb * _FP[0] + a * _FP[1]
+    h = h ^ (h >> 31)
+    h = h * _FP[2]
+    h = h ^ (h >> 29)
+    return h.sum()
+
+
+def test_pair_fingerprint_numpy_matches_torch():
+    """The fingerprint config 3's full-size test compares: numpy and torch give the same wrapped int64,
+    it ignores row order, and it sees one swapped pairing."""
+    import torch
+    rng = np.random.default_rng(5)
+    vb = rng.integers(-2 ** 63, 2 ** 63 - 1, 100_000, dtype=np.int64)
+    a = rng.integers(0, 1000, 100_000, dtype=np.int64)
+    with np.errstate(over="ignore"):
+        h = int(_pair_fingerprint(vb, a))
+        perm = rng.permutation(len(vb))
+        assert int(_pair_fingerprint(vb[perm], a[perm])) == h
+        a2 = a.copy()
+        a2[[0, 1]] = a2[[1, 0]] + np.array([1, 0])
+        assert int(_pair_fingerprint(vb, a2)) != h
+    assert int(_pair_fingerprint(torch.from_numpy(vb), torch.from_numpy(a))) == h
+
+
+@pytest.mark.gpu
+def test_config3_full_size_vs_oracle(ctx):
+    """BASELINE config 3 at its full size (INNER join of 1e9 fact rows x 1e7 dim rows materialising
+    (f.v, d.a)) against the oracle's own join (qo_hash_join_inner, the intended-semantics restatement
+    of executor.rs:500-540) over the same counter-based columns generated on the host.  The device
+    emits rows in slice order and the oracle in probe order, so the two outputs are compared as
+    multisets, exactly on what does not depend on order: the row count, the histogram of a (1000
+    values), and a 64-bit mix summed over every (bits(v), a) pair.  The oracle runs per probe-row
+    chunk (an inner join is row-wise in the probe side, so the chunks' outputs concatenate to the
+    whole), the chunks on a thread pool (ctypes drops the GIL)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from qe_hip.distributed import TYPESTR, _DeviceView
+    n, nd, na = 1_000_000_000, 10_000_000, 1000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 2, n, nd)
+    fv = ctx.generate(abi.GEN_UNIT_F64, SEED, 3, n)
+    dk = ctx.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, na)
+    p, b, rows = ctx.hash_join_inner(fk, [fv], dk, [da])
+
+    def view(col, dt=None):
+        return torch.as_tensor(_DeviceView(col.c.values, len(col), TYPESTR[dt or col.dtype], col), device="cuda")
+
+    vb_dev, a_dev = view(p[0], abi.DT_INT64), view(b[0])
+    got_fp, got_hist = 0, torch.zeros(na, dtype=torch.int64, device="cuda")
+    step = 100_000_000
+    for s in range(0, rows, step):
+        got_fp += int(_pair_fingerprint(vb_dev[s:s + step], a_dev[s:s + step]))
+        got_hist += torch.bincount(a_dev[s:s + step], minlength=na)
+    got_fp = (got_fp + 2 ** 63) % 2 ** 64 - 2 ** 63
+    got_hist = got_hist.cpu().numpy()
+    del p, b, fk, fv, dk, da, vb_dev, a_dev
+
+    hdk = ob.HostCol(ob.generate(abi.GEN_PERMUTATION, SEED, 0, nd, nd))
+    hda = ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, SEED, 6, nd, na))
+    chunk = 31_250_000
+
+    def oracle_chunk(r0):
+        m = min(chunk, n - r0)
+        k = ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, SEED, 2, m, nd, row0=r0))
+        v = ob.HostCol(ob.generate(abi.GEN_UNIT_F64, SEED, 3, m, row0=r0))
+        op, obc, r = ob.hash_join_inner(k, [v], hdk, [hda])
+        vb, a = op[0][0].view(np.int64), obc[0][0]
+        return r, int(_pair_fingerprint(vb, a)), np.bincount(a, minlength=na)
+
+    with np.errstate(over="ignore"), ThreadPoolExecutor(max_workers=min(16, _host_threads())) as pool:
+        parts = list(pool.map(oracle_chunk, range(0, n, chunk)))
+    want_rows = sum(r for r, _, _ in parts)
+    want_fp = (sum(f for _, f, _ in parts) + 2 ** 63) % 2 ** 64 - 2 ** 63
+    want_hist = sum(h for _, _, h in parts)
+    assert rows == want_rows == n
+    assert np.array_equal(got_hist, want_hist)
+    assert got_fp == want_fp
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["table_lanes", "plain_call", "other_probe", "bitmap_flag", "two_rank_rows"])
 def test_prelaunch_from_device_stats(ctx, case):
