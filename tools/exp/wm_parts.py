@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""(Needs an experiments build: make -C query-engine_amd EXTRA=-DQEH_EXPERIMENTS.)
+"""(Needs the experiments build: make -C query-engine_amd experiments, then QEH_LIB_PATH=.../libqeh_exp.so.)
 Config 5's partition passes per setting (QEH_WM_EXP=16: pass 1 alone, the query then fails;
 QEH_WM_LB: the digit split; QEH_WM_G1W / G1X: pass-1 workgroups): the window timers (partition =
 min/max + histogram + scan + pass 1 [+ pass 2]), best of `reps`, alternating settings over rounds.
