@@ -884,6 +884,7 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
                 ? QEH_OK : fail(QEH_E_HIP, "outer join: memset");
     }
     uint64_t extra = 0;
+    bool rw_done = false;  // the slice probe ran (k_outer_slice.hip)
     if (s == QEH_OK && n > 0) {
         KernelTimer kt(ctx, "join_probe");
         const int grid = grid_for(ctx, (n + 255) / 256, kBlock / 64, 8);
@@ -894,6 +895,14 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
             hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n, rec.as<int64_t>(),
                                present.as<uint32_t>(), bt.t.kmin, bt.t.kmax, eo);
         };
+        int st = kOuterSliceNotEligible;
+        if (r32)
+            st = outer_slice_probe(ctx, pk, rec.p, rw, bt.t.kmin, range, vmin, true, npc, eo.pcol, eo.pout, eo.pvalid,
+                                   eo.bout[0], eo.bvalid[0]);
+        if (st != kOuterSliceNotEligible) {
+            s = st;
+            rw_done = true;
+        }
         auto go32 = [&](auto rt) {
             typedef decltype(rt) R;
             auto k = npc == 0 ? k_outer_embed32<true, 0, R> : npc == 1 ? k_outer_embed32<true, 1, R>
@@ -901,7 +910,8 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
             hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(pk), n, rec.as<R>(), bt.t.kmin,
                                bt.t.kmax, vmin, eo);
         };
-        if (rw == 4) go32(uint32_t{});
+        if (rw_done) {
+        } else if (rw == 4) go32(uint32_t{});
         else if (rw == 2) go32(uint16_t{});
         else if (nbc == 1) go(std::integral_constant<int, 1>{});
         else if (nbc == 2) go(std::integral_constant<int, 2>{});
@@ -1039,7 +1049,12 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         if (s == QEH_OK && n > 0) {
             KernelTimer kt(ctx, "join_probe");
             const int grid = grid_for(ctx, (n + 255) / 256, kBlock / 64, 8);
-            if (r32) {
+            const int st = r32 ? outer_slice_probe(ctx, pk, rec.p, rw, bt.t.kmin, range, vmin, false, 0, nullptr, nullptr,
+                                                   nullptr, eo.bout[0], eo.bvalid[0])
+                               : kOuterSliceNotEligible;
+            if (st != kOuterSliceNotEligible) {
+                s = st;
+            } else if (r32) {
                 FullEmbedOut fo{};
                 fo.bout[0] = eo.bout[0];
                 fo.bvalid[0] = eo.bvalid[0];

@@ -165,6 +165,15 @@ int window_msd_keys(qeh_ctx *ctx, int func, const qeh_column *parts, int n_part,
 int window_w3(qeh_ctx *ctx, int func, const qeh_column &part, const qeh_column &order, bool asc, int64_t param,
               qeh_column *out);
 
+// Order-preserving LDS-slice probe of an outer join over compact embedded records (k_outer_slice.hip):
+// writes the build column (vmin + record - 1, validity) of every probe row in probe order and, for
+// FULL, copies np probe columns and sets the records' matched flags.  kOuterSliceNotEligible (nothing
+// launched) when the shape does not fit.
+constexpr int kOuterSliceNotEligible = -1;
+int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int64_t kmin, uint64_t range, int64_t vmin,
+                      bool full, int np, const int64_t *const *pcol, int64_t *const *pout, uint64_t *const *pvalid,
+                      int64_t *bout, uint64_t *bvalid);
+
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
 

@@ -517,6 +517,57 @@ def test_full_join_fused_paths(ctx, bkind, npc, nprobe):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "right", "full"])
+@pytest.mark.parametrize("rec", ["u16", "u32"])
+@pytest.mark.parametrize("shape", ["uniform", "one_slice", "ragged_int32", "big"])
+def test_outer_slice_probe(ctx, monkeypatch, jt, rec, shape):
+    """The order-preserving slice probe (k_outer_slice.hip, forced below its size threshold): phase A
+    partitions the probe rows' key offsets by table slice with a replayable ranking, phase B looks them up
+    in LDS (FULL: matched flags), phase C restores probe order.  Every output row equals the oracle's in
+    order (the preserved side's rows come first, in probe order; FULL's unmatched build rows after them,
+    compared as a multiset): NULL probe keys, keys below / above the build range, 2-B and 4-B records,
+    one slice taking every row (many chunks per tile), Int32 keys and a ragged last tile."""
+    monkeypatch.setenv("QEH_OUTER_SLICE", "1")
+    r = np.random.default_rng(len(jt) * 31 + len(rec) * 7 + len(shape))
+    nbuild, span, nprobe, kdt = 60_000, 300_000, 700_001, np.int64
+    if shape == "big":
+        nbuild, span, nprobe = 1_500_000, 6_000_000, 6_000_000
+    elif shape == "ragged_int32":
+        nprobe, kdt = 123_457, np.int32
+    bk = (r.permutation(span)[:nbuild] + 1000).astype(kdt)
+    if shape == "one_slice":
+        pk = r.integers(1000, 1000 + 30_000, nprobe).astype(kdt)
+    else:
+        pk = r.integers(0, span + 3000, nprobe).astype(kdt)
+    pkv = r.random(nprobe) > 0.05
+    lo, hi = (-700, 700) if rec == "u16" else (-(1 << 24), 1 << 24)
+    bcol = (r.integers(lo, hi, nbuild).astype(np.int64), None)
+    pcols = [(r.random(nprobe), None), (pk.astype(np.int64), None)] if jt == "full" else [(r.random(nprobe), None)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        if jt == "right":
+            got, want = outer_both(ctx, jt, (bk, None), [bcol], (pk, pkv), pcols)
+        else:
+            got, want = outer_both(ctx, jt, (pk, pkv), pcols, (bk, None), [bcol])
+        ran = ctx.kernel_time("outer_slice")[1]
+    finally:
+        ctx.timing(False)
+    assert ran == 1
+    # probe-order rows: exact, position by position (values compared where valid)
+    for (gv, gm), (wv, wm) in zip(got, want):
+        gm = np.ones(len(gv), bool) if gm is None else gm
+        wm = np.ones(len(wv), bool) if wm is None else wm
+        assert len(gv) == len(wv)
+        m = min(len(gv), nprobe)
+        assert np.array_equal(gm[:m], wm[:m])
+        assert np.array_equal(gv[:m][gm[:m]], wv[:m][wm[:m]])
+    if jt == "full":
+        tail = lambda cols: sorted_rows([(v[nprobe:], None if m is None else m[nprobe:]) for v, m in cols])
+        assert tail(got) == tail(want)
+
+
+@pytest.mark.gpu
 def test_row_number_windowed_scatter_path(ctx, monkeypatch):
     """n > 2^22: the direct scatter and the experimental windowed scatter (QEH_RN_WINDOWED:
     (destination, rn) pairs grouped by output window by one radix pass) both match the oracle."""
