@@ -39,6 +39,9 @@ constexpr int kOsWaves = kOsBlock / 64;
 #ifndef QEH_OS_R
 #define QEH_OS_R 8
 #endif
+#ifndef QEH_OS_EXP  // timing ablations (experiment builds only: 1 no item stores, 2 no ranking, 3 no gather)
+#define QEH_OS_EXP 0
+#endif
 constexpr int kOsR = QEH_OS_R;               // rows per thread per tile
 constexpr int kOsTile = kOsBlock * kOsR;     // 4096 probe rows per tile
 constexpr int kOsChunk = 256;                // items per pool chunk
@@ -70,7 +73,7 @@ struct OsLds {
     os_u4 ss[kOsMaxF];
     uint32_t wtot[4];
     uint32_t nxt;                     // next free chunk of the workgroup's pool
-    uint32_t stage[kOsTile];          // A: item destinations; C: destinations, then results
+    alignas(16) uint32_t stage[kOsTile];  // A: item destinations; C: destinations, then results
 };
 
 // LDS barrier that keeps global loads in flight (the next tile's keys)
@@ -103,7 +106,11 @@ __device__ __forceinline__ void os_rank(OsLds &L, const OsShape &sh, int wave, c
         const bool in = ((vm >> q) & 1u) && d < sh.range;
         s[q] = in ? (int)(d >> sh.sbits) : -1;
         o[q] = (uint32_t)d & omask;
+#if QEH_OS_EXP == 2
+        r[q] = 0u;
+#else
         r[q] = in ? atomicAdd(&L.cnt[wave][s[q]], 1u) : 0u;
+#endif
     }
 }
 
@@ -189,7 +196,7 @@ template <int KES>
 __global__ __launch_bounds__(kOsBlock) void k_os_part(ColRef key, OsShape sh, uint16_t *__restrict__ items,
                                                       uint16_t *__restrict__ tag, uint16_t *__restrict__ ccnt) {
     __shared__ OsLds L;
-    __shared__ uint16_t sval[kOsTile];
+    __shared__ __attribute__((aligned(16))) uint16_t sval[kOsTile];
     const int tid = threadIdx.x, wave = tid >> 6;
     const int64_t ntiles = (sh.n + kOsTile - 1) / kOsTile;
     const int64_t t_lo = (int64_t)blockIdx.x * sh.tpw, t_hi = std::min<int64_t>(ntiles, t_lo + sh.tpw);
@@ -224,7 +231,19 @@ __global__ __launch_bounds__(kOsBlock) void k_os_part(ColRef key, OsShape sh, ui
             }
         os_barrier();
         const uint32_t tot = os_tile_total(L);
-        for (uint32_t p = tid; p < tot; p += kOsBlock) items[L.stage[p]] = sval[p];
+#if QEH_OS_EXP != 1
+        // staged items in pairs: two neighbours of one run at an even place leave as one 4-B store
+        for (uint32_t p = 2 * tid; p < tot; p += 2 * kOsBlock) {
+            const uint2 d = *(const uint2 *)&L.stage[p];
+            const uint32_t v = *(const uint32_t *)&sval[p];
+            if (p + 1 < tot && d.y == d.x + 1 && !(d.x & 1u)) {
+                *(uint32_t *)(items + d.x) = v;
+            } else {
+                items[d.x] = (uint16_t)v;
+                if (p + 1 < tot) items[d.y] = (uint16_t)(v >> 16);
+            }
+        }
+#endif
         os_advance(L, tid, sh.F, my_pos, my_cur, tc, abase);
         os_barrier();
     }
@@ -232,6 +251,7 @@ __global__ __launch_bounds__(kOsBlock) void k_os_part(ColRef key, OsShape sh, ui
 }
 
 // ---- chunk lists: the pool's chunks grouped by slice (phase B reads its slice's list) ---------------
+// (an entry is the chunk id (< 2^24: the pool holds < 2^32 items) | its item count - 1 << 24)
 __global__ __launch_bounds__(kOsLBlock) void k_os_list_count(const uint16_t *__restrict__ tag, uint64_t nchunks, int F,
                                                            uint32_t *__restrict__ wg_hist, uint32_t *__restrict__ scount) {
     __shared__ uint32_t h[kOsMaxF];
@@ -253,7 +273,7 @@ __global__ __launch_bounds__(kOsLBlock) void k_os_list_count(const uint16_t *__r
 __global__ __launch_bounds__(kOsLBlock) void k_os_list_fill(const uint16_t *__restrict__ tag, uint64_t nchunks, int F,
                                                           const uint32_t *__restrict__ wg_hist,
                                                           const uint32_t *__restrict__ scount, uint32_t *__restrict__ sbase,
-                                                          uint32_t *__restrict__ list) {
+                                                          const uint16_t *__restrict__ ccnt, uint32_t *__restrict__ list) {
     __shared__ uint32_t cur[kOsMaxF];
     const int tid = threadIdx.x;
     for (int s = tid; s < F; s += kOsLBlock) {
@@ -270,16 +290,15 @@ __global__ __launch_bounds__(kOsLBlock) void k_os_list_fill(const uint16_t *__re
     const uint64_t lo = nchunks * blockIdx.x / gridDim.x, hi = nchunks * (blockIdx.x + 1) / gridDim.x;
     for (uint64_t c = lo + tid; c < hi; c += kOsLBlock) {
         const uint32_t t = tag[c];
-        if (t < (uint32_t)F) list[atomicAdd(&cur[t], 1u)] = (uint32_t)c;
+        if (t < (uint32_t)F) list[atomicAdd(&cur[t], 1u)] = (uint32_t)c | ((uint32_t)(ccnt[c] - 1u) << 24);
     }
 }
 
 // ---- phase B ----------------------------------------------------------------------------------------
 template <typename R, bool FULL>
 __global__ __launch_bounds__(kOsPBlock) void k_os_probe(OsShape sh, int H, const uint32_t *__restrict__ sbase,
-                                                        const uint32_t *__restrict__ list, const uint16_t *__restrict__ ccnt,
-                                                        uint16_t *__restrict__ items, uint32_t *__restrict__ res32,
-                                                        R *__restrict__ rec) {
+                                                        const uint32_t *__restrict__ list, uint16_t *__restrict__ items,
+                                                        uint32_t *__restrict__ res32, R *__restrict__ rec) {
     constexpr int NK = kOsSliceBytes / (int)sizeof(R);
     constexpr uint32_t FLAG = 1u << (8 * sizeof(R) - 1), VAL = FLAG - 1u;
     __shared__ __attribute__((aligned(16))) R tab[NK];
@@ -299,19 +318,28 @@ __global__ __launch_bounds__(kOsPBlock) void k_os_probe(OsShape sh, int H, const
         for (int i = tid; i < NK; i += kOsPBlock) tab[i] = (uint64_t)i < have ? rec[kb + i] : (R)0;
     }
     __syncthreads();
-    // a wave per chunk, 4 items per lane, kOsPU chunks in flight per wave
+    // a wave per chunk, 4 items per lane, kOsPU chunks in flight per wave; the next batch's list entries
+    // are read while this batch is looked up
+    uint32_t ent[kOsPU];
+#pragma unroll
+    for (int u = 0; u < kOsPU; ++u) {
+        const uint32_t e = lo + wave + u * kOsPWaves;
+        ent[u] = e < hi ? list[e] : 0xFFFFFFFFu;
+    }
     for (uint32_t e0 = lo + wave; e0 < hi; e0 += kOsPWaves * kOsPU) {
         uint32_t cid[kOsPU], cn[kOsPU];
         uint64_t it[kOsPU];
 #pragma unroll
         for (int u = 0; u < kOsPU; ++u) {
-            const uint32_t e = e0 + u * kOsPWaves;
-            cid[u] = e < hi ? list[e] : 0u;
-            cn[u] = e < hi ? (uint32_t)ccnt[cid[u]] : 0u;
+            cid[u] = ent[u] & 0xFFFFFFu;
+            cn[u] = ent[u] == 0xFFFFFFFFu ? 0u : (ent[u] >> 24) + 1u;
+            it[u] = cn[u] ? *(const uint64_t *)(items + (uint64_t)cid[u] * kOsChunk + lane * 4) : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < kOsPU; ++u)
-            it[u] = cn[u] ? *(const uint64_t *)(items + (uint64_t)cid[u] * kOsChunk + lane * 4) : 0ull;
+        for (int u = 0; u < kOsPU; ++u) {
+            const uint32_t e = e0 + (uint32_t)(kOsPWaves * kOsPU) + u * kOsPWaves;
+            ent[u] = e < hi ? list[e] : 0xFFFFFFFFu;
+        }
 #pragma unroll
         for (int u = 0; u < kOsPU; ++u) {
             if (!cn[u]) continue;
@@ -405,9 +433,17 @@ __global__ __launch_bounds__(kOsBlock) void k_os_emit(ColRef key, OsShape sh, co
         os_barrier();
         // the tile's results, run by run, into its staged positions
         const uint32_t tot = os_tile_total(L);
-        for (uint32_t i = tid; i < tot; i += kOsBlock) {
-            const uint32_t d = L.stage[i];
-            L.stage[i] = sizeof(R) == 2 ? (uint32_t)res16[d] : res32[d];
+        for (uint32_t i = 2 * tid; i < tot; i += 2 * kOsBlock) {
+            const uint2 d = *(const uint2 *)&L.stage[i];
+            uint2 v;
+            if (sizeof(R) == 2 && i + 1 < tot && d.y == d.x + 1 && !(d.x & 1u)) {
+                const uint32_t w = *(const uint32_t *)(res16 + d.x);  // two neighbours of one run in one load
+                v = make_uint2(w & 0xFFFFu, w >> 16);
+            } else {
+                v.x = sizeof(R) == 2 ? (uint32_t)res16[d.x] : res32[d.x];
+                v.y = i + 1 < tot ? (sizeof(R) == 2 ? (uint32_t)res16[d.y] : res32[d.y]) : 0u;
+            }
+            *(uint2 *)&L.stage[i] = v;
         }
         os_advance(L, tid, sh.F, my_pos, my_cur, tc, abase);
         os_barrier();
@@ -475,7 +511,7 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
     hipLaunchKernelGGL(k_os_list_count, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag.as<uint16_t>(), nchunks,
                        (int)F, wg_hist, scount);
     hipLaunchKernelGGL(k_os_list_fill, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag.as<uint16_t>(), nchunks,
-                       (int)F, wg_hist, scount, sbase, list.as<uint32_t>());
+                       (int)F, wg_hist, scount, sbase, ccnt.as<uint16_t>(), list.as<uint32_t>());
     // phase B: about three rounds of workgroups (one per CU: the slice takes 128 KB of LDS) over the slices,
     // each slice's chunk list split evenly among its H workgroups
     const int H = (int)std::max<int64_t>(1, 3 * (int64_t)cus / (int64_t)F);
@@ -483,7 +519,7 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
         typedef decltype(rt) R;
         auto kern = full ? k_os_probe<R, true> : k_os_probe<R, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)(F * H)), dim3(kOsPBlock), 0, ctx->stream, sh, H, sbase,
-                           list.as<uint32_t>(), ccnt.as<uint16_t>(), items.as<uint16_t>(), res32.as<uint32_t>(), (R *)rec);
+                           list.as<uint32_t>(), items.as<uint16_t>(), res32.as<uint32_t>(), (R *)rec);
     };
     if (rw == 2) probe(uint16_t{});
     else probe(uint32_t{});
