@@ -290,6 +290,222 @@ __global__ __launch_bounds__(kBlock) void k_join_agg_fast(FastIn in, PredTerms t
     }
 }
 
+// ---- bucket-range partitioned probe (BUCKET tables: sparse 64-bit keys; opt-in, see try_bucket_parts) --
+// A BUCKET table of 1e7 sparse keys is 178 MB: the single fused pass (k_join_agg_fast) reads one 64-B
+// bucket line per selected probe row from the Infinity Cache.  Here the probe rows are first split by
+// the high bits of the key's hash -- the home bucket is monotone in the hash, so each of the 64
+// partitions owns a contiguous 1/64 of the table (2.8 MB at 1e7 keys) -- and each partition is then
+// probed by the workgroups of one XCD together, so its part of the table stays in that XCD's 4 MB L2.
+//   P1 k_bp_part: FastTile loads + predicate; the selected rows' (key, aggregate input) are staged in
+//      LDS by partition and appended to the workgroup's open 256-item chunk per partition (chunks from
+//      one global counter, tagged with their partition; runs of ~32 rows per partition per tile).
+//   P2 k_bp_probe: XCD x (blockIdx % 8) takes partitions x, x + 8, ...; its workgroups split each
+//      partition's chunk list (chunk_lists), probe the table (L2 hits) and aggregate in LDS states.
+// HBM bytes per probe row: 24 read (x, k, v) + 16 written and read back per selected row; the table
+// once per partition.  A key stored past its partition's last bucket (linear probing by buckets) is
+// still found: the probe reads the real table.
+constexpr int kBpBlock = 512;
+constexpr int kBpWaves = kBpBlock / 64;
+constexpr int kBpTile = kBpBlock * kFastR;  // 4096 probe rows per P1 iteration
+constexpr int kBpPBits = 6;
+constexpr int kBpP = 1 << kBpPBits;         // partitions
+constexpr int kBpChunk = 256;
+
+// LDS-only workgroup barrier: the next tile's loads stay in flight across it
+__device__ __forceinline__ void bp_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NTERMS, int NACOL, bool NT>
+__global__ __launch_bounds__(kBpBlock) void k_bp_part(FastIn in, PredTerms terms, int64_t n, int acs,
+                                                      uint64_t *__restrict__ okey, uint64_t *__restrict__ oval,
+                                                      uint16_t *__restrict__ tag, uint16_t *__restrict__ ccnt,
+                                                      uint32_t *__restrict__ nchunk) {
+    __shared__ uint32_t pc[kBpP], tstart[kBpP], fillp[kBpP], curc[kBpP], cbase[kBpP];
+    __shared__ uint64_t skey[kBpTile];
+    __shared__ uint64_t sval[NACOL > 0 ? kBpTile : 1];
+    __shared__ uint32_t sdst[kBpTile];
+    __shared__ uint32_t tot_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kBpP) pc[tid] = 0, fillp[tid] = kBpChunk, curc[tid] = 0;  // fill 256: no open chunk
+    __syncthreads();
+    const int64_t n_tiles = (n + kBpTile - 1) / kBpTile;
+    const int64_t woff = (int64_t)wave * (64 * kFastR) + 2 * lane;
+    // the next tile's loads are issued before this tile's LDS phases (full tiles; the ragged last tile
+    // is loaded on its own)
+    FastTile<NTERMS, NACOL, NT> nx;
+    if ((int64_t)blockIdx.x < n_tiles && ((int64_t)blockIdx.x + 1) * kBpTile <= n) nx.issue(in, (int64_t)blockIdx.x * kBpTile + woff);
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t base = tile * kBpTile + woff;
+        FastTile<NTERMS, NACOL, NT> ft;
+        if ((tile + 1) * kBpTile <= n) {
+            ft = nx;
+            ft.eval(in, terms);
+            const int64_t t2 = tile + gridDim.x;
+            if (t2 < n_tiles && (t2 + 1) * kBpTile <= n) nx.issue(in, t2 * kBpTile + woff);
+        } else {
+            ft.issue_tail(in, base, n);
+            ft.eval(in, terms);
+            ft.sel &= FastTile<NTERMS, NACOL, NT>::tail_mask(base, n);
+        }
+        uint32_t part[kFastR], rk[kFastR];
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            part[r] = (uint32_t)(hash64((uint64_t)ft.k(r)) >> (64 - kBpPBits));
+            rk[r] = ((ft.sel >> r) & 1u) ? atomicAdd(&pc[part[r]], 1u) : 0u;
+        }
+        bp_barrier();
+        if (tid < kBpP) {  // wave 0: the tile's starts, and the chunks each partition opens
+            const uint32_t c = pc[tid];
+            const uint32_t incl = wave_incl_scan(c);
+            tstart[tid] = incl - c;
+            if (tid == kBpP - 1) tot_s = incl;
+            const uint32_t room = kBpChunk - fillp[tid];
+            const uint32_t spill = c > room ? c - room : 0u;
+            const uint32_t nnew = (spill + kBpChunk - 1) / kBpChunk;
+            uint32_t b = 0;
+            if (nnew) {
+                b = atomicAdd(nchunk, nnew);
+                for (uint32_t i = 0; i < nnew; ++i) tag[b + i] = (uint16_t)tid, ccnt[b + i] = (uint16_t)kBpChunk;
+            }
+            cbase[tid] = b;
+        }
+        bp_barrier();
+#pragma unroll
+        for (int r = 0; r < kFastR; ++r) {
+            if (!((ft.sel >> r) & 1u)) continue;
+            const uint32_t p = part[r], f = fillp[p], room = kBpChunk - f;
+            uint32_t dst;
+            if (rk[r] < room) {
+                dst = curc[p] * kBpChunk + f + rk[r];
+            } else {
+                const uint32_t q = rk[r] - room;
+                dst = (cbase[p] + q / kBpChunk) * kBpChunk + q % kBpChunk;
+            }
+            const uint32_t st = tstart[p] + rk[r];
+            skey[st] = (uint64_t)ft.k(r);
+            if (NACOL > 0) sval[st] = (uint64_t)ft.a(acs, r);
+            sdst[st] = dst;
+        }
+        bp_barrier();
+        const uint32_t tot = tot_s;
+        for (uint32_t i = tid; i < tot; i += kBpBlock) {
+            const uint32_t d = sdst[i];
+            okey[d] = skey[i];
+            if (NACOL > 0) oval[d] = sval[i];
+        }
+        if (tid < kBpP) {
+            const uint32_t c = pc[tid], f = fillp[tid], room = kBpChunk - f;
+            if (c <= room) {
+                fillp[tid] = f + c;
+            } else {
+                const uint32_t q = c - room;
+                curc[tid] = cbase[tid] + (q - 1) / kBpChunk;
+                fillp[tid] = (q - 1) % kBpChunk + 1;
+            }
+            pc[tid] = 0;
+        }
+        bp_barrier();
+    }
+    if (tid < kBpP && fillp[tid] < kBpChunk) ccnt[curc[tid]] = (uint16_t)fillp[tid];
+}
+
+template <int NACOL>
+__global__ __launch_bounds__(kBpBlock) void k_bp_probe(AggSpecs specs, FastIn in, HashTable t, int64_t G,
+                                                       const uint32_t *__restrict__ sbase, const uint32_t *__restrict__ list,
+                                                       const uint64_t *__restrict__ ikey, const uint64_t *__restrict__ ival,
+                                                       uint64_t *__restrict__ gstates_all) {
+    uint64_t *__restrict__ gstates = shard_states(gstates_all, specs, G);
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    {
+        const int64_t words = (int64_t)specs.n_slots * G;
+        for (int64_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = 0;
+        __syncthreads();
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind == AK_MIN || sp.kind == AK_MAX)
+                for (int64_t g = threadIdx.x; g < G; g += blockDim.x) lds[(int64_t)sp.val_slot * G + g] = (uint64_t)agg_init_value(sp.kind);
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x & 7;
+    const uint32_t wi = blockIdx.x >> 3, nwg = gridDim.x >> 3;
+    constexpr int U = 2;  // chunks per wave in flight (8 probes per lane)
+    for (int p = x; p < kBpP; p += 8) {
+        const uint32_t lo = sbase[p], hi = sbase[p + 1];
+        const uint32_t stride = nwg * kBpWaves * U;
+        uint32_t ent[U];  // this iteration's list entries (the next ones are read while it probes)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t e = lo + (wi * kBpWaves + wave) * U + u;
+            ent[u] = e < hi ? list[e] : 0xFFFFFFFFu;
+        }
+        for (uint32_t e0 = lo + (wi * kBpWaves + wave) * U; e0 < hi; e0 += stride) {
+            int64_t key[U][4], val[U][4];
+            uint32_t cn[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cn[u] = ent[u] == 0xFFFFFFFFu ? 0u : (ent[u] >> 24) + 1u;
+                const uint64_t at = (uint64_t)(ent[u] & 0xFFFFFFu) * kBpChunk + lane * 4;
+                if (cn[u]) {
+                    const v2i64 k0 = __builtin_nontemporal_load((const v2i64 *)(ikey + at));
+                    const v2i64 k1 = __builtin_nontemporal_load((const v2i64 *)(ikey + at + 2));
+                    key[u][0] = k0[0], key[u][1] = k0[1], key[u][2] = k1[0], key[u][3] = k1[1];
+                    if (NACOL > 0) {
+                        const v2i64 v0 = __builtin_nontemporal_load((const v2i64 *)(ival + at));
+                        const v2i64 v1 = __builtin_nontemporal_load((const v2i64 *)(ival + at + 2));
+                        val[u][0] = v0[0], val[u][1] = v0[1], val[u][2] = v1[0], val[u][3] = v1[1];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t e = e0 + stride + u;
+                ent[u] = e < hi ? list[e] : 0xFFFFFFFFu;
+            }
+            uint32_t gid[U][4];
+            uint32_t hit = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    gid[u][q] = 0;
+                    if ((uint32_t)(lane * 4 + q) < cn[u] && probe_unique(t, key[u][q], gid[u][q])) hit |= 1u << (u * 4 + q);
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if ((hit >> (u * 4 + q)) & 1u) atomicAdd((unsigned long long *)&lds[gid[u][q]], 1ull);
+            for (int a = 0; a < specs.n; ++a) {
+                const AggSpec sp = specs.a[a];
+                if (sp.kind == AK_COUNT || in.agg_colslot[a] < 0) continue;
+                uint64_t *st = lds + (int64_t)sp.val_slot * G;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if ((hit >> (u * 4 + q)) & 1u) {
+                            const int64_t v = NACOL > 0 ? val[u][q] : 0;
+                            if (sp.kind == AK_SUM_F) atomicAdd((double *)&st[gid[u][q]], as_f64(v));
+                            else if (sp.kind == AK_SUM_I) atomicAdd((unsigned long long *)&st[gid[u][q]], (unsigned long long)v);
+                            else agg_apply<true>(sp.kind, &st[gid[u][q]], agg_input(sp.kind, sp.in_type, v));
+                        }
+            }
+        }
+    }
+    __syncthreads();
+    for (int64_t g = threadIdx.x; g < G; g += blockDim.x) {
+        uint64_t rows = lds[g];
+        if (!rows) continue;
+        atomicAdd((unsigned long long *)&gstates[g], (unsigned long long)rows);
+        for (int a = 0; a < specs.n; ++a) {
+            const AggSpec sp = specs.a[a];
+            if (sp.kind != AK_COUNT)
+                agg_merge_global(sp.kind, &gstates[(int64_t)sp.val_slot * G + g], lds[(int64_t)sp.val_slot * G + g]);
+        }
+    }
+}
+
 // ---- LDS-slice partitioned probe (direct u16 tables larger than L2) ----------------
 // A single fused pass pays one L2 miss (a 64-B Infinity-Cache request) per
 // probe once the table outgrows an XCD's 4 MiB L2; at the BASELINE shape
@@ -2319,6 +2535,62 @@ static void launch_tail(qeh_ctx *ctx, const ColSet &cols, int64_t n, int64_t don
                              err);
 }
 
+static uint64_t table_bytes(const HashTable &t);
+
+// The bucket-range partitioned probe (k_bp_part + chunk_lists + k_bp_probe) for a BUCKET table past
+// the Infinity Cache's comfortable share; false when it does not apply (nothing launched).
+static bool try_bucket_parts(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp, int nterms, int nacol,
+                             const AggSpecs &specs, const HashTable &t, int64_t G, int64_t n, uint64_t *states,
+                             size_t lds_bytes) {
+    // opt-in (QEH_BUCKET_PARTS=1): measured slower than the single pass at the sparse metric shape
+    // (P1 7.5-7.9 ms + P2 8.9 ms against 13.2 ms; profiles/r06/bucket_parts.txt) -- the probes hit the
+    // XCD's L2 (4.7e8 TCC hits, 1.1e8 misses) and still run at the single pass's ~56 G probes/s
+    if (t.kind != TK_BUCKET || nacol > 1 || !std::getenv("QEH_BUCKET_PARTS")) return false;
+    if (lds_bytes > 64 * 1024) return false;
+    const int cus = ctx->props.multiProcessorCount;
+    const int64_t n_tiles = (n + kBpTile - 1) / kBpTile;
+    const int grid1 = (int)std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)cus, n_tiles));
+    const uint64_t max_chunks = (uint64_t)(n + kBpChunk - 1) / kBpChunk + (uint64_t)grid1 * kBpP;
+    if (max_chunks >= (1ull << 24)) return false;
+    DevBuf keys, vals, tags, cnts, lists, ctr;
+    if (keys.alloc(ctx, max_chunks * kBpChunk * 8) != QEH_OK || (nacol && vals.alloc(ctx, max_chunks * kBpChunk * 8) != QEH_OK) ||
+        tags.alloc(ctx, max_chunks * 2) != QEH_OK || cnts.alloc(ctx, max_chunks * 2) != QEH_OK ||
+        lists.alloc(ctx, max_chunks * 4 + (kBpP + 1) * 4) != QEH_OK || ctr.alloc(ctx, 4) != QEH_OK)
+        return false;
+    if (hipMemsetAsync(tags.p, 0xFF, max_chunks * 2, ctx->stream) != hipSuccess ||
+        hipMemsetAsync(ctr.p, 0, 4, ctx->stream) != hipSuccess)
+        return false;
+    const int acs = nacol ? 0 : -1;
+    KernelTimer kt(ctx, "bucket_parts");
+    const bool nt = fast_nt_mode() == 1;
+#define QEH_BP(NTV, NAV, NTB)                                                                                            \
+    hipLaunchKernelGGL((k_bp_part<NTV, NAV, NTB>), dim3(grid1), dim3(kBpBlock), 0, ctx->stream, in, pp.terms, n, acs,   \
+                       keys.as<uint64_t>(), vals.as<uint64_t>(), tags.as<uint16_t>(), cnts.as<uint16_t>(), ctr.as<uint32_t>())
+#define QEH_BP_NA(NTV, NTB)                  \
+    if (nacol == 0) QEH_BP(NTV, 0, NTB);     \
+    else QEH_BP(NTV, 1, NTB);
+#define QEH_BP_NT(NTB)                           \
+    if (nterms == 0) { QEH_BP_NA(0, NTB) }       \
+    else if (nterms == 1) { QEH_BP_NA(1, NTB) }  \
+    else { QEH_BP_NA(2, NTB) }
+    if (nt) { QEH_BP_NT(true) } else { QEH_BP_NT(false) }
+#undef QEH_BP_NT
+#undef QEH_BP_NA
+#undef QEH_BP
+    uint32_t *sbase = lists.as<uint32_t>() + max_chunks;
+    if (chunk_lists(ctx, tags.as<uint16_t>(), cnts.as<uint16_t>(), max_chunks, kBpP, sbase, lists.as<uint32_t>()) != QEH_OK)
+        return false;
+    const int grid2 = std::max(8, (2 * cus + 7) / 8 * 8);  // a multiple of 8: every XCD the same count
+    if (nacol)
+        hipLaunchKernelGGL(k_bp_probe<1>, dim3(grid2), dim3(kBpBlock), lds_bytes, ctx->stream, specs, in, t, G, sbase,
+                           lists.as<uint32_t>(), keys.as<uint64_t>(), vals.as<uint64_t>(), states);
+    else
+        hipLaunchKernelGGL(k_bp_probe<0>, dim3(grid2), dim3(kBpBlock), lds_bytes, ctx->stream, specs, in, t, G, sbase,
+                           lists.as<uint32_t>(), keys.as<uint64_t>(), vals.as<uint64_t>(), states);
+    // the pool buffers above must outlive the kernels
+    return hipStreamSynchronize(ctx->stream) == hipSuccess;
+}
+
 static bool try_fast_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const PredPlan &pp, const GidSource &src,
                           const AggSpecs &specs, int64_t G, uint64_t *states, uint32_t *err, size_t lds_bytes,
                           int per_cu) {
@@ -2326,6 +2598,7 @@ static bool try_fast_join(qeh_ctx *ctx, const ColSet &cols, int64_t n, const Pre
     FastIn in;
     int nterms, nacol;
     if (!fast_eligible(cols, pp, src, specs, &in, &nterms, &nacol)) return false;
+    if (try_bucket_parts(ctx, in, pp, nterms, nacol, specs, src.jt, G, n, states, lds_bytes)) return true;
     const int64_t n_tiles = n / kFastTile;
     if (n_tiles > 0) {
         const int grid = grid_for(ctx, n_tiles * kFastTile, kFastTile, per_cu);

@@ -470,6 +470,23 @@ __global__ __launch_bounds__(kOsBlock) void k_os_emit(ColRef key, OsShape sh, co
 }
 
 // ---- host --------------------------------------------------------------------------------------------
+// The chunks of a pool grouped by tag (k_os_list_count + k_os_list_fill): sbase[0..F] the tags' list
+// ranges, list[] entries chunk id | (item count - 1) << 24.  Chunk ids < 2^24, F <= kOsMaxF.
+int chunk_lists(qeh_ctx *ctx, const uint16_t *tag, const uint16_t *ccnt, uint64_t nchunks, int F, uint32_t *sbase,
+                uint32_t *list) {
+    if (F <= 0 || F > kOsMaxF || nchunks >= (1ull << 24)) return fail(QEH_E_INVALID, "chunk_lists: shape");
+    DevBuf lwork;
+    QEH_TRY(lwork.alloc(ctx, ((size_t)kOsLGrid * F + F) * 4));
+    uint32_t *wg_hist = lwork.as<uint32_t>(), *scount = wg_hist + (size_t)kOsLGrid * F;
+    QEH_HIP(hipMemsetAsync(scount, 0, F * 4, ctx->stream));
+    hipLaunchKernelGGL(k_os_list_count, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag, nchunks, F, wg_hist, scount);
+    hipLaunchKernelGGL(k_os_list_fill, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag, nchunks, F, wg_hist, scount,
+                       sbase, ccnt, list);
+    QEH_HIP(hipGetLastError());
+    // (lwork goes back to the pool behind the two kernels on the same queue)
+    return QEH_OK;
+}
+
 int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int64_t kmin, uint64_t range, int64_t vmin,
                       bool full, int np, const int64_t *const *pcol, int64_t *const *pout, uint64_t *const *pvalid,
                       int64_t *bout, uint64_t *bvalid) {

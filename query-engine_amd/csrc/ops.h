@@ -174,6 +174,11 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
                       bool full, int np, const int64_t *const *pcol, int64_t *const *pout, uint64_t *const *pvalid,
                       int64_t *bout, uint64_t *bvalid);
 
+// The chunks of a pool grouped by their tag (k_outer_slice.hip): list ranges sbase[0..F], entries
+// chunk id | (item count - 1) << 24 (chunk ids < 2^24; unused chunks carry a tag >= F).
+int chunk_lists(qeh_ctx *ctx, const uint16_t *tag, const uint16_t *ccnt, uint64_t nchunks, int F, uint32_t *sbase,
+                uint32_t *list);
+
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
 

@@ -700,6 +700,36 @@ def test_prelaunch_adopted_only_when_the_hint_matches(ctx, hint):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("aggs", [[(AF.Sum, 2), (AF.Count, 2)], [(AF.Min, 2), (AF.Max, 2), (AF.Count, 2)],
+                                  [(AF.Count, 2)], [(AF.Sum, 0), (AF.Avg, 0)]])
+@pytest.mark.parametrize("n_fact", [3_000_001, 4096])
+def test_bucket_parts_join_aggregate(ctx, monkeypatch, aggs, n_fact):
+    """Sparse 64-bit dimension keys (a BUCKET table) through the bucket-range partitioned probe
+    (k_bp_part + k_bp_probe, forced below its size threshold): the probe rows are split by the high bits
+    of the key's hash, each partition probed by one XCD's workgroups.  Keys absent from the dimension
+    miss, the ragged last tile is masked, and every aggregate kind (float / int SUM, COUNT, MIN, MAX,
+    AVG; COUNT alone stages no values) equals the oracle's."""
+    monkeypatch.setenv("QEH_BUCKET_PARTS", "1")
+    r = np.random.default_rng(n_fact + len(aggs))
+    nd = 150_000
+    dk = r.integers(-(2 ** 62), 2 ** 62, nd, dtype=np.int64)
+    dg = r.integers(0, 1000, nd).astype(np.int64)
+    k = np.where(r.random(n_fact) < 0.9, dk[r.integers(0, nd, n_fact)], r.integers(-(2 ** 62), 2 ** 62, n_fact))
+    x = r.integers(0, 100, n_fact).astype(np.int64)
+    v = r.random(n_fact) * 100 - 50
+    probe = [(x, None), (k.astype(np.int64), None), (v, None)]
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        gk, ga, wk, wa = run_both(ctx, probe, 1, PRED, (dk, None), [(dg, None)], aggs)
+        ran = ctx.kernel_time("bucket_parts")[1]
+    finally:
+        ctx.timing(False)
+    assert ran == 1
+    assert_grouped_equal(gk, ga, wk, wa, float_aggs=float_idx(aggs, probe))
+
+
+@pytest.mark.gpu
 def test_inner_join_full_size_properties(ctx):
     """BASELINE config 3 at its full size (INNER join of 1e9 fact rows x 1e7 dim rows materialising
     (f.v, d.a), generated in HBM; the slice path, rows in slice order), against independent torch
