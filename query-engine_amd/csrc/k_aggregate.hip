@@ -2555,7 +2555,8 @@ static bool try_bucket_parts(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp,
     DevBuf keys, vals, tags, cnts, lists, ctr;
     if (keys.alloc(ctx, max_chunks * kBpChunk * 8) != QEH_OK || (nacol && vals.alloc(ctx, max_chunks * kBpChunk * 8) != QEH_OK) ||
         tags.alloc(ctx, max_chunks * 2) != QEH_OK || cnts.alloc(ctx, max_chunks * 2) != QEH_OK ||
-        lists.alloc(ctx, max_chunks * 4 + (kBpP + 1) * 4) != QEH_OK || ctr.alloc(ctx, 4) != QEH_OK)
+        lists.alloc(ctx, max_chunks * 4 + (kBpP + 1) * 4 + chunk_lists_work_words(kBpP) * 4) != QEH_OK ||
+        ctr.alloc(ctx, 4) != QEH_OK)
         return false;
     if (hipMemsetAsync(tags.p, 0xFF, max_chunks * 2, ctx->stream) != hipSuccess ||
         hipMemsetAsync(ctr.p, 0, 4, ctx->stream) != hipSuccess)
@@ -2578,7 +2579,8 @@ static bool try_bucket_parts(qeh_ctx *ctx, const FastIn &in, const PredPlan &pp,
 #undef QEH_BP_NA
 #undef QEH_BP
     uint32_t *sbase = lists.as<uint32_t>() + max_chunks;
-    if (chunk_lists(ctx, tags.as<uint16_t>(), cnts.as<uint16_t>(), max_chunks, kBpP, sbase, lists.as<uint32_t>()) != QEH_OK)
+    if (chunk_lists(ctx, tags.as<uint16_t>(), cnts.as<uint16_t>(), max_chunks, kBpP, sbase, lists.as<uint32_t>(),
+                    sbase + kBpP + 1) != QEH_OK)
         return false;
     const int grid2 = std::max(8, (2 * cus + 7) / 8 * 8);  // a multiple of 8: every XCD the same count
     if (nacol)

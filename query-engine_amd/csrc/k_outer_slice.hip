@@ -472,18 +472,17 @@ __global__ __launch_bounds__(kOsBlock) void k_os_emit(ColRef key, OsShape sh, co
 // ---- host --------------------------------------------------------------------------------------------
 // The chunks of a pool grouped by tag (k_os_list_count + k_os_list_fill): sbase[0..F] the tags' list
 // ranges, list[] entries chunk id | (item count - 1) << 24.  Chunk ids < 2^24, F <= kOsMaxF.
+size_t chunk_lists_work_words(int F) { return (size_t)kOsLGrid * F + F; }
+
 int chunk_lists(qeh_ctx *ctx, const uint16_t *tag, const uint16_t *ccnt, uint64_t nchunks, int F, uint32_t *sbase,
-                uint32_t *list) {
+                uint32_t *list, uint32_t *work) {
     if (F <= 0 || F > kOsMaxF || nchunks >= (1ull << 24)) return fail(QEH_E_INVALID, "chunk_lists: shape");
-    DevBuf lwork;
-    QEH_TRY(lwork.alloc(ctx, ((size_t)kOsLGrid * F + F) * 4));
-    uint32_t *wg_hist = lwork.as<uint32_t>(), *scount = wg_hist + (size_t)kOsLGrid * F;
+    uint32_t *wg_hist = work, *scount = wg_hist + (size_t)kOsLGrid * F;
     QEH_HIP(hipMemsetAsync(scount, 0, F * 4, ctx->stream));
     hipLaunchKernelGGL(k_os_list_count, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag, nchunks, F, wg_hist, scount);
     hipLaunchKernelGGL(k_os_list_fill, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag, nchunks, F, wg_hist, scount,
                        sbase, ccnt, list);
     QEH_HIP(hipGetLastError());
-    // (lwork goes back to the pool behind the two kernels on the same queue)
     return QEH_OK;
 }
 
@@ -510,14 +509,13 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
     if (nchunks * kOsChunk >= (1ull << 32)) return kOuterSliceNotEligible;
     DevBuf items, res32, tag, ccnt, list, lwork;
     // (no room for the pool: the single-pass probe needs none)
-    const size_t lw_words = (size_t)kOsLGrid * F + 2 * F + 1;  // per-block histograms, slice counts, slice bases
+    const size_t lw_words = chunk_lists_work_words((int)F) + F + 1;  // the list passes' scratch, slice bases
     if (items.alloc(ctx, nchunks * kOsChunk * 2) != QEH_OK || tag.alloc(ctx, nchunks * 2 + 16) != QEH_OK ||
         ccnt.alloc(ctx, nchunks * 2 + 16) != QEH_OK || list.alloc(ctx, nchunks * 4) != QEH_OK ||
         lwork.alloc(ctx, lw_words * 4) != QEH_OK ||
         (rw == 4 && res32.alloc(ctx, nchunks * kOsChunk * 4) != QEH_OK))
         return kOuterSliceNotEligible;
-    uint32_t *wg_hist = lwork.as<uint32_t>(), *scount = wg_hist + (size_t)kOsLGrid * F, *sbase = scount + F;
-    QEH_HIP(hipMemsetAsync(scount, 0, F * 4, ctx->stream));
+    uint32_t *sbase = lwork.as<uint32_t>() + chunk_lists_work_words((int)F);
     QEH_HIP(hipMemsetAsync(tag.p, 0xFF, nchunks * 2 + 16, ctx->stream));
     KernelTimer kt(ctx, "outer_slice");
     OsShape sh{n, kmin, range, sbits, (int32_t)F, tpw, (uint32_t)pool};
@@ -525,10 +523,8 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
     const bool k8 = pk.dtype == QEH_DT_INT64;
     hipLaunchKernelGGL(k8 ? k_os_part<8> : k_os_part<4>, dim3(grid), dim3(kOsBlock), 0, ctx->stream, kr, sh,
                        items.as<uint16_t>(), tag.as<uint16_t>(), ccnt.as<uint16_t>());
-    hipLaunchKernelGGL(k_os_list_count, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag.as<uint16_t>(), nchunks,
-                       (int)F, wg_hist, scount);
-    hipLaunchKernelGGL(k_os_list_fill, dim3(kOsLGrid), dim3(kOsLBlock), 0, ctx->stream, tag.as<uint16_t>(), nchunks,
-                       (int)F, wg_hist, scount, sbase, ccnt.as<uint16_t>(), list.as<uint32_t>());
+    QEH_TRY(chunk_lists(ctx, tag.as<uint16_t>(), ccnt.as<uint16_t>(), nchunks, (int)F, sbase, list.as<uint32_t>(),
+                        lwork.as<uint32_t>()));
     // phase B: about three rounds of workgroups (one per CU: the slice takes 128 KB of LDS) over the slices,
     // each slice's chunk list split evenly among its H workgroups
     const int H = (int)std::max<int64_t>(1, 3 * (int64_t)cus / (int64_t)F);

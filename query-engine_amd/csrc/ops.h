@@ -175,9 +175,11 @@ int outer_slice_probe(qeh_ctx *ctx, const qeh_column &pk, void *rec, int rw, int
                       int64_t *bout, uint64_t *bvalid);
 
 // The chunks of a pool grouped by their tag (k_outer_slice.hip): list ranges sbase[0..F], entries
-// chunk id | (item count - 1) << 24 (chunk ids < 2^24; unused chunks carry a tag >= F).
+// chunk id | (item count - 1) << 24 (chunk ids < 2^24; unused chunks carry a tag >= F).  `work`: the
+// caller's device scratch of chunk_lists_work_words(F) words, alive until the two kernels have run.
+size_t chunk_lists_work_words(int F);
 int chunk_lists(qeh_ctx *ctx, const uint16_t *tag, const uint16_t *ccnt, uint64_t nchunks, int F, uint32_t *sbase,
-                uint32_t *list);
+                uint32_t *list, uint32_t *work);
 
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
