@@ -568,6 +568,64 @@ def test_outer_slice_probe(ctx, monkeypatch, jt, rec, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("jt", ["left", "full"])
+def test_outer_join_full_size_vs_oracle(ctx, jt):
+    """The outer-join bench shape at its full size (2e8 probe rows with keys over twice the build's
+    range, 1e7 build rows, 2-B records: the order-preserving slice probe) against the oracle's
+    qo_hash_join_outer: the probe rows' part of the output in probe order, chunk by chunk (a LEFT /
+    FULL join is row-wise in the probe side), values and validity exact; FULL's unmatched build rows
+    after them as a multiset."""
+    from qe_hip import abi
+    seed, n, nd = 0x5EED, 200_000_000, 10_000_000
+    fk = ctx.generate(abi.GEN_UNIFORM_MOD, seed, 2, n, 2 * nd)
+    fv = ctx.generate(abi.GEN_UNIFORM_MOD, seed, 3, n, 1 << 40)
+    dk = ctx.generate(abi.GEN_PERMUTATION, seed, 0, nd, nd)
+    da = ctx.generate(abi.GEN_UNIFORM_MOD, seed, 6, nd, 1000)
+    ctx.timing(True)
+    ctx.timing_reset()
+    try:
+        lo, ro, rows = ctx.hash_join_outer(JT[jt], fk, [fv], dk, [da])
+        ran = ctx.kernel_time("outer_slice")[1]
+    finally:
+        ctx.timing(False)
+    assert ran == 1
+    gv, gm = lo[0].to_numpy()
+    ga, gam = ro[0].to_numpy()
+    del lo, ro, fk, fv, dk, da
+    hdk = ob.HostCol(ob.generate(abi.GEN_PERMUTATION, seed, 0, nd, nd))
+    hda = ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, seed, 6, nd, 1000))
+    step = 25_000_000
+    for r0 in range(0, n, step):
+        m = min(step, n - r0)
+        hk = ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, seed, 2, m, 2 * nd, row0=r0))
+        hv = ob.HostCol(ob.generate(abi.GEN_UNIFORM_MOD, seed, 3, m, 1 << 40, row0=r0))
+        wl, wr, wrows = ob.hash_join_outer(JT["left"], hk, [hv], hdk, [hda])
+        assert wrows == m  # unique build keys: one row per probe row
+        (wv, _), (wa, wam) = wl[0], wr[0]
+        assert np.array_equal(gv[r0:r0 + m], wv)
+        want_m = np.ones(m, bool) if wam is None else wam
+        got_m = np.ones(m, bool) if gam is None else gam[r0:r0 + m]
+        assert np.array_equal(got_m, want_m)
+        assert np.array_equal(ga[r0:r0 + m][got_m], wa[want_m])
+    if jt == "full":
+        # the build rows no probe key matched, after the probe rows, with the probe side NULL
+        tail = ga[n:]
+        assert gm is not None and not gm[n:].any()
+        hit = np.zeros(nd, bool)
+        for r0 in range(0, n, step):
+            m = min(step, n - r0)
+            hk = ob.generate(abi.GEN_UNIFORM_MOD, seed, 2, m, 2 * nd, row0=r0)
+            hit[hk[hk < nd]] = True
+        dkh = ob.generate(abi.GEN_PERMUTATION, seed, 0, nd, nd)
+        dah = ob.generate(abi.GEN_UNIFORM_MOD, seed, 6, nd, 1000)
+        want_tail = np.sort(dah[~hit[dkh]])
+        assert rows == n + len(want_tail)
+        assert np.array_equal(np.sort(tail), want_tail)
+    else:
+        assert rows == n
+
+
+@pytest.mark.gpu
 def test_row_number_windowed_scatter_path(ctx, monkeypatch):
     """n > 2^22: the direct scatter and the experimental windowed scatter (QEH_RN_WINDOWED:
     (destination, rn) pairs grouped by output window by one radix pass) both match the oracle."""

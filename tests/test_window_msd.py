@@ -261,6 +261,39 @@ def test_row_number_full_size_properties(ctx):
 
 
 @pytest.mark.gpu
+def test_row_number_full_size_vs_oracle_sample(ctx):
+    """BASELINE config 5 at its full size (1e9 rows, k in [0, 2^20)) against the oracle itself on 1024
+    sampled PARTITION BY groups (~1e6 rows): a group's row numbers depend only on its own rows in input
+    order, so the oracle's ROW_NUMBER over the sampled groups' rows (regenerated on the host by chunks,
+    input order kept) must equal the device's numbers at those rows exactly."""
+    import torch
+    from qe_hip import abi
+    from qe_hip.distributed import TYPESTR, _DeviceView
+    n, parts = 1_000_000_000, 1 << 20
+    k = ctx.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 7, n, parts)
+    v = ctx.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 8, n, 2 ** 62, lo=-(2 ** 61))
+    rn = ctx.row_number([k], [v], [True])
+    tr = torch.as_tensor(_DeviceView(rn.c.values, len(rn), TYPESTR[rn.dtype], rn), device="cuda")
+    sample = np.sort(np.random.default_rng(9).choice(parts, 1024, replace=False))
+    rows, ks, vs = [], [], []
+    step = 100_000_000
+    for r0 in range(0, n, step):
+        m = min(step, n - r0)
+        hk = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 7, m, parts, row0=r0)
+        sel = np.nonzero(np.isin(hk, sample, assume_unique=False))[0]
+        hv = ob.generate(abi.GEN_UNIFORM_MOD, 0x5EED, 8, m, 2 ** 62, lo=-(2 ** 61), row0=r0)
+        rows.append(sel + r0)
+        ks.append(hk[sel])
+        vs.append(hv[sel])
+        del hk, hv
+    rows, ks, vs = np.concatenate(rows), np.concatenate(ks), np.concatenate(vs)
+    want = ob.row_number([ob.HostCol(ks)], [ob.HostCol(vs)], [True])
+    got = tr[torch.as_tensor(rows, device="cuda")].cpu().numpy()
+    assert len(rows) > 500_000
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("func,param", [(W.RowNumber, 0), (W.Rank, 0), (W.Ntile, 3)])
 @pytest.mark.parametrize("n,parts,k0", [(300_001, (1 << 20) + 5, -7), (2_000_000, 1 << 22, 1 << 40), (1_500_000, 1 << 24, -(1 << 30))])
 @pytest.mark.parametrize("asc", [True, False])
