@@ -462,6 +462,24 @@ extern "C" int qeh_broadcast_stats(qeh_ctx *ctx, const qeh_column *build_key, co
     return QEH_OK;
 }
 
+// Non-zero entries of a device table of n entries of `bytes` (2 or 4) bytes (one synchronous read).
+int count_nonzero_entries(qeh_ctx *ctx, const void *table, uint64_t n, int bytes, uint64_t *out) {
+    *out = 0;
+    if (n == 0) return QEH_OK;
+    if (bytes != 2 && bytes != 4) return fail(QEH_E_INVALID, "count_nonzero_entries: entry width");
+    DevBuf c;
+    QEH_TRY(c.alloc(ctx, 8));
+    QEH_HIP(hipMemsetAsync(c.p, 0, 8, ctx->stream));
+    const int gc = grid_for(ctx, (int64_t)(n * bytes / 16 + 1), kBlock * 4, 1);
+    hipLaunchKernelGGL(k_count_nonzero, dim3(gc), dim3(kBlock), 0, ctx->stream, (void *)table, n, bytes,
+                       c.as<unsigned long long>(), 0u);
+    QEH_HIP(hipGetLastError());
+    unsigned long long v = 0;
+    QEH_TRY(read_small(ctx, &v, c.p, 8));
+    *out = (uint64_t)v;
+    return QEH_OK;
+}
+
 extern "C" int qeh_u16_count_nonzero(qeh_ctx *ctx, const uint16_t *table, uint64_t n, int64_t *out) {
     if (!ctx || !out || (n > 0 && !table)) return fail(QEH_E_INVALID, "qeh_u16_count_nonzero: bad argument");
     DeviceGuard dg(ctx->device);

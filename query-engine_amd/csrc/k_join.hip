@@ -823,24 +823,79 @@ static int compact_records_ok(qeh_ctx *ctx, const qeh_column *bcols, int nbc, in
     return (uint64_t)mx - (uint64_t)mn < 0x7FFEull ? 2 : 4;
 }
 
+// One narrow Int64 build column embedded as 2-B / 4-B records straight from the build rows, the key's
+// uniqueness read off the filled records (a repeated key leaves fewer non-zero records than keys) --
+// instead of a DIRECT join table built only to learn that.  built = false: take the general path.
+struct PreRecords {
+    DevBuf rec;
+    int rw = 0;
+    int64_t vmin = 0;
+    bool built = false;
+};
+static bool prebuild_records(qeh_ctx *ctx, const qeh_column &bk, const qeh_column *bcols, int nbc, BuiltTable *bt,
+                             PreRecords *pr) {
+    if (nbc != 1 || !mat_col_ok(bcols[0])) return false;
+    int64_t vmin = 0;
+    const int rw = compact_records_ok(ctx, bcols, nbc, &vmin);
+    if (!rw) return false;
+    int64_t mn, mx, cnt;
+    if (column_minmax(ctx, bk, &mn, &mx, &cnt) != QEH_OK || cnt <= 0) return false;
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1ull;
+    // the DIRECT rule build_join_table applies (row-id payloads), and the embed path's range bound
+    if (range == 0 || range > (1ull << 31) || !direct_table_ok(range, (uint64_t)cnt, (uint64_t)std::max<int64_t>(bk.length - 1, 0)))
+        return false;
+    if (pr->rec.alloc(ctx, range * rw) != QEH_OK || hipMemsetAsync(pr->rec.p, 0, range * rw, ctx->stream) != hipSuccess)
+        return false;
+    {
+        KernelTimer kt(ctx, "join_build");
+        const int grid = grid_for(ctx, bk.length, kBlock * 4, 8);
+        const int64_t *b0 = (const int64_t *)bcols[0].values + bcols[0].offset;
+        if (rw == 4)
+            hipLaunchKernelGGL(k_embed_build32<uint32_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(bk),
+                               bk.length, mn, b0, vmin, pr->rec.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_embed_build32<uint16_t>, dim3(grid), dim3(kBlock), 0, ctx->stream, make_colref(bk),
+                               bk.length, mn, b0, vmin, pr->rec.as<uint16_t>());
+    }
+    uint64_t filled = 0;
+    if (hipGetLastError() != hipSuccess || count_nonzero_entries(ctx, pr->rec.p, range, rw, &filled) != QEH_OK ||
+        filled != (uint64_t)cnt) {
+        pr->rec.reset();
+        return false;
+    }
+    bt->t = HashTable{};
+    bt->t.kind = TK_DIRECT;
+    bt->t.kmin = mn;
+    bt->t.kmax = mx;
+    bt->t.range = range;
+    bt->t.unique = 1;
+    bt->n_inserted = cnt;
+    pr->rw = rw;
+    pr->vmin = vmin;
+    pr->built = true;
+    return true;
+}
+
 // FULL over a unique DIRECT build: k_full_embed for the probe rows, then the unmatched build rows
 // appended (k_full_tail_count / scan / k_full_tail_emit).  Output columns are allocated for every probe
 // and build row and hold the m rows that result.
 static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column &bk, const BuiltTable &bt,
                            const qeh_column *pcols, int npc, const qeh_column *bcols, int nbc, qeh_column *pout,
-                           qeh_column *bout, int64_t *out_rows) {
+                           qeh_column *bout, int64_t *out_rows, PreRecords *pre) {
     const uint64_t range = bt.t.range;
     const int64_t n = pk.length, nbuild = bk.length, cap = n + nbuild;
     auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
     // records of nbc build values + a matched flag word: a probe hit reads its record anyway, so it sets the
     // flag only when it reads it clear -- about one store per matched key instead of one per matching row
     // (one Int64 build column of a narrow range: 4-B records, k_embed_build32)
-    DevBuf rec, present;
-    int64_t vmin = 0;
-    const int rw = compact_records_ok(ctx, bcols, nbc, &vmin);
+    DevBuf own_rec, present;
+    int64_t vmin = pre->built ? pre->vmin : 0;
+    const int rw = pre->built ? pre->rw : compact_records_ok(ctx, bcols, nbc, &vmin);
     const bool r32 = rw != 0;
     const int stride = rw == 4 ? 0 : rw == 2 ? -1 : nbc + 1;
-    if (r32) {
+    DevBuf &rec = pre->built ? pre->rec : own_rec;
+    if (pre->built) {
+    } else if (r32) {
         QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range, 1) * rw));
         QEH_HIP(hipMemsetAsync(rec.p, 0, std::max<uint64_t>(range, 1) * rw, ctx->stream));
     } else {
@@ -848,7 +903,7 @@ static int full_join_embed(qeh_ctx *ctx, const qeh_column &pk, const qeh_column 
         QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
         QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
     }
-    if (nbuild > 0) {
+    if (nbuild > 0 && !pre->built) {
         KernelTimer kt(ctx, "join_build");
         if (rw == 4)
             hipLaunchKernelGGL(k_embed_build32<uint32_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,
@@ -980,8 +1035,19 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
     const qeh_column &bk = right_outer ? *left_key : *right_key;
     if (pk.length >= (int64_t)kNullRow || bk.length >= (int64_t)kNullRow)
         return fail(QEH_E_UNSUPPORTED, "join inputs beyond 2^32 - 1 rows");
+    const qeh_column *bcols = right_outer ? left_cols : right_cols;
+    const qeh_column *pcols = right_outer ? right_cols : left_cols;
+    const int nbc = right_outer ? n_left_cols : n_right_cols, npc = right_outer ? n_right_cols : n_left_cols;
     BuiltTable bt;
-    QEH_TRY(build_join_table(ctx, bk, nullptr, (uint64_t)std::max<int64_t>(bk.length - 1, 0), &bt));
+    PreRecords pre;
+    bool want_pre = !std::getenv("QEH_OUTER_COMPACT") && !std::getenv("QEH_NO_FUSED_JOIN") && nbc == 1 &&
+                    !std::getenv("QEH_NO_PREBUILD") && forced_table_kind() < 0;
+    if (full) {
+        want_pre = want_pre && npc <= kMatMaxP;
+        for (int i = 0; want_pre && i < npc; ++i) want_pre = mat_col_ok(pcols[i]);
+    }
+    if (!(want_pre && prebuild_records(ctx, bk, bcols, nbc, &bt, &pre)))
+        QEH_TRY(build_join_table(ctx, bk, nullptr, (uint64_t)std::max<int64_t>(bk.length - 1, 0), &bt));
     DevBuf matched, pidx, bidx;
     if (full) {
         QEH_TRY(matched.alloc(ctx, (size_t)std::max<int64_t>(bk.length, 1)));
@@ -990,9 +1056,6 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
     int64_t m = 0;
     // unique build keys: every probe row yields exactly one row, at its own position
     const bool in_place = bt.t.unique && !std::getenv("QEH_OUTER_COMPACT");
-    const qeh_column *bcols = right_outer ? left_cols : right_cols;
-    const qeh_column *pcols = right_outer ? right_cols : left_cols;
-    const int nbc = right_outer ? n_left_cols : n_right_cols, npc = right_outer ? n_right_cols : n_left_cols;
     qeh_column *bout = right_outer ? out_left : out_right;
     qeh_column *pout = right_outer ? out_right : out_left;
     bool embed = in_place && bt.t.kind == TK_DIRECT && nbc >= 1 && nbc <= kMatMaxB && bt.t.range <= (1ull << 31) &&
@@ -1003,19 +1066,21 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
         embed = embed && npc <= kMatMaxP;
         for (int i = 0; embed && i < npc; ++i) embed = mat_col_ok(pcols[i]);
     }
-    if (embed && full) return full_join_embed(ctx, pk, bk, bt, pcols, npc, bcols, nbc, pout, bout, out_rows);
+    if (embed && full) return full_join_embed(ctx, pk, bk, bt, pcols, npc, bcols, nbc, pout, bout, out_rows, &pre);
     if (embed) {
         // LEFT/RIGHT over a unique DIRECT build: build columns embedded by key offset, one fused
         // probe writes them in probe order; the preserved side's columns are returned as views of
         // the inputs (owned = 0, a RecordBatch column clone)
         const uint64_t range = bt.t.range;
         const int64_t n = pk.length, nbuild = bk.length;
-        DevBuf rec, present;
-        int64_t vmin = 0;
-        const int rw = compact_records_ok(ctx, bcols, nbc, &vmin);
+        DevBuf own_rec, present;
+        int64_t vmin = pre.built ? pre.vmin : 0;
+        const int rw = pre.built ? pre.rw : compact_records_ok(ctx, bcols, nbc, &vmin);
         const bool r32 = rw != 0;
+        DevBuf &rec = pre.built ? pre.rec : own_rec;
         auto cptr = [](const qeh_column &c) { return (const int64_t *)c.values + c.offset; };
-        if (r32) {
+        if (pre.built) {
+        } else if (r32) {
             QEH_TRY(rec.alloc(ctx, std::max<uint64_t>(range, 1) * rw));
             QEH_HIP(hipMemsetAsync(rec.p, 0, std::max<uint64_t>(range, 1) * rw, ctx->stream));
         } else {
@@ -1023,7 +1088,7 @@ extern "C" int qeh_hash_join_outer(qeh_ctx *ctx, int join_type, const qeh_column
             QEH_TRY(present.alloc(ctx, ((range + 31) / 32 + 1) * 4));
             QEH_HIP(hipMemsetAsync(present.p, 0, ((range + 31) / 32 + 1) * 4, ctx->stream));
         }
-        if (nbuild > 0) {
+        if (nbuild > 0 && !pre.built) {
             KernelTimer kt(ctx, "join_build");
             if (rw == 4)
                 hipLaunchKernelGGL(k_embed_build32<uint32_t>, dim3(grid_for(ctx, nbuild, kBlock * 4, 8)), dim3(kBlock), 0,

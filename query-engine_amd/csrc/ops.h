@@ -181,6 +181,9 @@ size_t chunk_lists_work_words(int F);
 int chunk_lists(qeh_ctx *ctx, const uint16_t *tag, const uint16_t *ccnt, uint64_t nchunks, int F, uint32_t *sbase,
                 uint32_t *list, uint32_t *work);
 
+// Non-zero entries of a device table of n 2-B or 4-B entries (k_build.hip; one synchronous read).
+int count_nonzero_entries(qeh_ctx *ctx, const void *table, uint64_t n, int bytes, uint64_t *out);
+
 // Error word -> status.
 int kernel_error_status(uint32_t err, const char *op);
 
