@@ -8,7 +8,7 @@
 // that request rate bounds it (1.9 ms for 2e8 probe rows, 1e8 of them in range).  Here the lookups
 // run in LDS, as in the metric's slice pipeline (k_aggregate.hip), and probe order comes back by
 // replaying a deterministic partition instead of carrying row ids:
-//   A  k_os_part: workgroup w walks its own contiguous range of 8192-row tiles.  A tile's rows are
+//   A  k_os_part: workgroup w walks its own contiguous range of 4096-row tiles.  A tile's rows are
 //      ranked per table slice (2^16 keys of 2-B records or 2^15 of 4-B: 128 KB either way) with
 //      returning LDS atomics on per-wave counters -- the lanes of one instruction are served in lane
 //      order (lds_atomic_rank_ok) and the instructions in program order, so a row's rank is a function
@@ -16,8 +16,8 @@
 //      256-item chunks taken in a fixed order from w's own pool (no global atomics: chunk ids are a
 //      function of the keys as well).  The tile's items are staged in LDS in (slice, rank) order and
 //      stored run by run; each chunk is tagged with its slice and its item count.
-//   B  k_os_probe: a workgroup per (slice, part of the chunk pool) loads the slice's records into LDS,
-//      collects the chunks tagged with its slice, and overwrites each item with its record's value
+//   B  chunk_lists groups the chunks by slice tag; k_os_probe, a workgroup per (slice, part of its
+//      list), loads the slice's records into LDS and overwrites each item with its record's value
 //      (FULL: sets the matched flag in the LDS copy and ORs the flags back into the table at the end).
 //   C  k_os_emit: the same workgroups walk the same tiles, replay A's ranking and chunk choice, gather
 //      each tile's results run by run into LDS, and write the build column (+ validity) in probe
@@ -39,7 +39,7 @@ constexpr int kOsWaves = kOsBlock / 64;
 #ifndef QEH_OS_R
 #define QEH_OS_R 8
 #endif
-#ifndef QEH_OS_EXP  // timing ablations (experiment builds only: 1 no item stores, 2 no ranking, 3 no gather)
+#ifndef QEH_OS_EXP  // timing ablations (experiment builds only, wrong results: 1 no item stores, 2 no ranking)
 #define QEH_OS_EXP 0
 #endif
 constexpr int kOsR = QEH_OS_R;               // rows per thread per tile
@@ -60,7 +60,7 @@ struct OsShape {
     int32_t sbits;    // key bits per slice: 16 (2-B records) or 15 (4-B)
     int32_t F;        // slices
     int64_t tpw;      // tiles per workgroup (phases A and C)
-    uint32_t pool;    // chunks per workgroup pool: tpw * 32 + F bounds what one workgroup can open
+    uint32_t pool;    // chunks per workgroup pool: tpw * (kOsTile / kOsChunk) + F bounds what one workgroup opens
 };
 
 typedef unsigned int os_u4 __attribute__((ext_vector_type(4)));
