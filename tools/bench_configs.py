@@ -286,7 +286,7 @@ def cfg_outer(ctx, scale, jt=1):
     # key is read and the build column (+ validity) written; FULL gathers every output column
     alg = 16.0 * n + n / 8 if jt == 1 else 16.0 * n + 24.0 * rows
     line(f"{name} outer join 2e8 x 1e7 (50% unmatched)", n, wall, alg, kms,
-         "k_outer_lookup + copies / null-aware gathers", cpu, {"output_rows": rows, "kernel_split_ms": kt})
+         "order-preserving slice probe k_os_part + k_os_probe + k_os_emit (FULL: + unmatched build rows)", cpu, {"output_rows": rows, "kernel_split_ms": kt})
 
 
 def cfg_merge(ctx, scale):
