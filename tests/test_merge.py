@@ -175,13 +175,15 @@ def test_merge_sorted_payload_full_range_keys(ctx, asc, nf, nulls):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["bench_shape", "ties_25_bits", "skew_redo", "constant_big", "int32_full", "asc_nulls_first",
-                                  "45_bits"])
+                                  "45_bits", "repeats_40", "half_repeats"])
 def test_merge_sorted_msd_payload_vs_oracle(ctx, monkeypatch, case):
     """The MSD payload sort (codes of 24..48 bits over >= 2^20 rows: two global 256-way passes on the top
     16 bits, then an LDS sort per sub-bucket): equal to the oracle's stable sort and to the LSD passes
     (QEH_NO_MSD_SORT=1) -- the Merge::sorted bench shape, many ties, a sub-bucket too large for LDS
     (the LSD redo), a large sub-bucket of one repeated key (copied through), Int32 keys over their
-    whole range, NULLs first, 45-bit codes (the widest the LDS sort packs)."""
+    whole range, NULLs first, 45-bit codes (the widest the LDS sort packs), every key 40 times and half
+    the keys 40 times (sub-buckets whose counting-sort bucket overflows go to the radix LDS passes).
+    Also equal to the radix LDS passes for every sub-bucket (QEH_MSD_RADIX_LDS=1)."""
     r = np.random.default_rng(23)
     n = (1 << 20) + 12_345
     dt, asc, nf, nulls = np.int64, False, False, True
@@ -203,15 +205,20 @@ def test_merge_sorted_msd_payload_vs_oracle(ctx, monkeypatch, case):
     elif case == "45_bits":
         k = r.integers(-(2 ** 43), 2 ** 43, n, dtype=np.int64)
         nulls = False
+    elif case == "repeats_40":
+        k = r.permutation(np.repeat(r.integers(0, 2 ** 40, n // 40 + 1, dtype=np.int64), 40)[:n])
+    elif case == "half_repeats":
+        rep = r.permutation(np.repeat(r.integers(0, 2 ** 39, n // 80 + 1, dtype=np.int64), 40)[:n // 2])
+        k = np.concatenate([rep, r.integers(2 ** 39, 2 ** 40, n - rep.size, dtype=np.int64)])[r.permutation(n)]
     kv = r.random(n) > 0.05 if nulls else np.ones(n, bool)
     v = r.random(n)
     cuts = [0, n // 3, n // 3 + 7, n]
     parts = [[ctx.upload(k[a:b], kv[a:b]) if nulls else ctx.upload(k[a:b]), ctx.upload(v[a:b])] for a, b in zip(cuts[:-1], cuts[1:])]
     perm = ob.sort_indices_nulls([ob.HostCol(k.astype(np.int64), kv)], [asc], [nf])
     outs = []
-    for env in (None, "1"):
+    for env in (None, "QEH_MSD_RADIX_LDS", "QEH_NO_MSD_SORT"):
         if env:
-            monkeypatch.setenv("QEH_NO_MSD_SORT", env)
+            monkeypatch.setenv(env, "1")
         cols, rows = ctx.merge_sorted(parts, [0], [asc], [nf])
         assert rows == n
         gk, gm = host(cols[0])
@@ -221,4 +228,4 @@ def test_merge_sorted_msd_payload_vs_oracle(ctx, monkeypatch, case):
         assert np.array_equal(gv, v[perm])
         assert cols[0].dtype == (abi.DT_INT32 if dt == np.int32 else abi.DT_INT64)
         outs.append(gv)
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
