@@ -212,6 +212,10 @@ struct RsEncode {
     int64_t start[kRsMaxSegs + 1];
     ColRef sk[kRsMaxSegs];
     const uint64_t *sv[kRsMaxSegs];
+    // KES = 1 (the MSD payload sort's second pass): the keys are the low 32 code bits, and the byte
+    // stream nd holds code bits [nd_shift, nd_shift + 8) -- all the pass reads of a code
+    const uint8_t *nd;
+    int32_t nd_shift;
 };
 
 // the segment of row i (branch-free count of the segment starts at or below i)
@@ -244,6 +248,9 @@ template <int KES, typename KeyT>
 __device__ __forceinline__ KeyT rs_load_key(const KeyT *__restrict__ keys, const RsEncode &e, int64_t i, int ts = 0) {
     if constexpr (KES == 0) {
         return __builtin_nontemporal_load(&keys[i]);
+    } else if constexpr (KES == 1) {
+        const uint32_t lo = __builtin_nontemporal_load((const uint32_t *)keys + i);
+        return ((KeyT)e.nd[i] << e.nd_shift) | (KeyT)(lo & ((1u << e.nd_shift) - 1u));
     } else {
         if (!e.ns) return (KeyT)rs_code<KES>(e, e.c, i);
         if (ts >= 0) return (KeyT)rs_code<KES>(e, e.sk[ts], i - e.start[ts]);
@@ -257,7 +264,7 @@ __device__ __forceinline__ KeyT rs_load_key(const KeyT *__restrict__ keys, const
 // the first pass's payload of row i (in place from the segments when ns > 0)
 template <int KES, typename ValT>
 __device__ __forceinline__ ValT rs_load_val(const ValT *__restrict__ vals, const RsEncode &e, int64_t i, int ts = 0) {
-    if constexpr (KES != 0 && sizeof(ValT) == 8) {
+    if constexpr (KES >= 4 && sizeof(ValT) == 8) {
         if (e.ns) {
             if (ts >= 0) return (ValT)__builtin_nontemporal_load(e.sv[ts] + (i - e.start[ts]));
             ValT v = 0;
@@ -1923,9 +1930,11 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
         auto hk = k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
         hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, n, seg, shift1, hist.as<uint32_t>(), nblocks, enc);
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
-        auto sk = k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4> : k_rs_scatter<uint64_t, true, uint64_t, false, 8>;
+        // the codes leave as their low 32 bits (the second pass takes its digit from the byte stream nd)
+        auto sk = k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4, false, uint32_t>
+                      : k_rs_scatter<uint64_t, true, uint64_t, false, 8, false, uint32_t>;
         hipLaunchKernelGGL(sk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, vsrc, n, seg, shift1, offs.as<uint64_t>(),
-                           nblocks, kb1, vtmp, nd.as<uint8_t>(), shift2, dec, enc, nullptr);
+                           nblocks, (uint32_t *)kb1, vtmp, nd.as<uint8_t>(), shift2, dec, enc, nullptr);
         QEH_HIP(hipGetLastError());
     }
     // the buckets' starts (the scanned offsets of block 0), then blocks of <= S rows inside each bucket
@@ -1965,9 +1974,12 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
                            hist2.as<uint32_t>());
         QEH_TRY(exclusive_scan_u32(ctx, hist2.as<uint32_t>(), offs2.as<uint64_t>(), (int64_t)kRadix * B, nullptr));
         uint32_t *codes2 = (uint32_t *)kb0;  // the low 32 code bits: all the LDS sort needs (lbits <= 29)
-        hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t, false, 0, true, uint32_t>), dim3((unsigned)B), dim3(kRsThreads), 0,
+        RsEncode enc2{};  // codes = (nd << shift2) | low shift2 bits of the first pass's 32-bit codes
+        enc2.nd = nd.as<uint8_t>();
+        enc2.nd_shift = shift2;
+        hipLaunchKernelGGL((k_rs_scatter<uint64_t, true, uint64_t, false, 1, true, uint32_t>), dim3((unsigned)B), dim3(kRsThreads), 0,
                            ctx->stream, kb1, vtmp, n, 0, shift2, offs2.as<uint64_t>(), (int)B, codes2, vtmp2.as<uint64_t>(), nullptr, 0,
-                           dec, enc, tabd.as<int64_t>());
+                           dec, enc2, tabd.as<int64_t>());
         hipLaunchKernelGGL(k_msd_sbstart, dim3((kRadix * kRadix + 256) / 256), dim3(256), 0, ctx->stream, offs2.as<uint64_t>(),
                            btabd.as<int64_t>(), n, sbd.as<uint64_t>());
         QEH_HIP(hipMemsetAsync(flag.p, 0, 16, ctx->stream));
