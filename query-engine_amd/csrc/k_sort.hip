@@ -1777,13 +1777,15 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
 // Merge::sorted shape against 4.09 ms for the radix passes, sorted-order stores 3.93 ms.
 // A sub-bucket with a bucket above kCsCap rows (clustered or repeated codes) is queued in fb for
 // k_msd_lds_sort (list mode); one above kMsdCap rows goes to k_msd_big as before.
+// 12 bits measured best: 10 / 11 / 13 / 14 bits 3.96 / 3.85 / 4.05 / 5.06 ms vs 3.76 (ab_merge_csort.txt)
 constexpr int kCsBits = 12, kCsCap = 24;
 static_assert(kMsdCap <= 4096 && (kMsdCap & (kMsdCap - 1)) == 0, "row index packs into the low 12 bits");
+template <int CB>
 __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__restrict__ codes, const uint64_t *__restrict__ vin,
                                                            const uint64_t *__restrict__ sb, int lbits, RsDecode dec,
                                                            uint64_t *__restrict__ vout, uint32_t *__restrict__ flag,
                                                            uint32_t *__restrict__ big, uint32_t *__restrict__ fb) {
-    constexpr int W = kMsdThreads / 64, J = kMsdCap / kMsdThreads, NB = 1 << kCsBits, BPT = NB / kMsdThreads;
+    constexpr int W = kMsdThreads / 64, J = kMsdCap / kMsdThreads, NB = 1 << CB, BPT = NB / kMsdThreads;
     __shared__ uint32_t cnt[NB];   // counts, then starts
     __shared__ uint64_t ce[kMsdCap];  // by slot: code << 12 | row
     __shared__ uint32_t wsum[W], wmax[W];
@@ -1802,7 +1804,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
     const int mm = (int)m;
     const uint64_t hi_code = (uint64_t)blockIdx.x << lbits;
     const uint32_t lmask = lbits >= 32 ? 0xFFFFFFFFu : ((1u << lbits) - 1u);
-    const int bshift = lbits > kCsBits ? lbits - kCsBits : 0;
+    const int bshift = lbits > CB ? lbits - CB : 0;
     for (int i = t; i < NB; i += kMsdThreads) cnt[i] = 0;
     uint32_t c[J], arr[J];
 #pragma unroll
@@ -1991,7 +1993,7 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
         } else {
             // one counting pass per sub-bucket; the ones with a crowded bucket queued for the radix passes
             QEH_HIP(hipMemsetAsync(fbl.p, 0, 4, ctx->stream));
-            hipLaunchKernelGGL(k_msd_csort, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2, vtmp2.as<uint64_t>(),
+            hipLaunchKernelGGL(k_msd_csort<kCsBits>, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2, vtmp2.as<uint64_t>(),
                                sbd.as<uint64_t>(), shift2, dec, vout, flag.as<uint32_t>(), bigl, fbl.as<uint32_t>());
             hipLaunchKernelGGL(k_msd_lds_sort, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2,
                                vtmp2.as<uint64_t>(), sbd.as<uint64_t>(), shift2, dec, vout, flag.as<uint32_t>(), bigl,
