@@ -14,13 +14,74 @@
 // Utf8 offsets re-based) and then copied into the host stream.
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ops.h"
 
 namespace qeh {
 namespace {
+
+// Pinned host buffers handed out by the IPC entry points (freed by qeh_host_free).  Pinning a few
+// hundred MB costs more than the copy into them (hipHostMalloc locks and maps every page), so a freed
+// buffer is kept (up to kPinKeep bytes in all) and handed out again to a request it fits within 2x.
+struct PinCache {
+    std::mutex mu;
+    std::unordered_map<void *, size_t> live;      // handed out: size
+    std::vector<std::pair<void *, size_t>> idle;  // freed and kept, oldest first
+    size_t idle_bytes = 0;
+};
+PinCache &pins() {
+    static PinCache *c = new PinCache;  // never destroyed: a buffer may be freed during interpreter exit
+    return *c;
+}
+constexpr size_t kPinKeep = (size_t)1 << 30;
+
+void *pinned_get(size_t n) {
+    PinCache &c = pins();
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        for (size_t i = 0; i < c.idle.size(); ++i) {
+            const auto e = c.idle[i];
+            if (e.second >= n && e.second <= 2 * n + ((size_t)1 << 20)) {
+                c.idle.erase(c.idle.begin() + (std::ptrdiff_t)i);
+                c.idle_bytes -= e.second;
+                c.live[e.first] = e.second;
+                return e.first;
+            }
+        }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p) return nullptr;
+    std::lock_guard<std::mutex> g(c.mu);
+    c.live[p] = n;
+    return p;
+}
+
+void pinned_put(void *p) {
+    PinCache &c = pins();
+    std::vector<void *> drop;
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        auto it = c.live.find(p);
+        if (it == c.live.end() || it->second > kPinKeep) {
+            drop.push_back(p);
+            if (it != c.live.end()) c.live.erase(it);
+        } else {
+            c.idle.push_back({p, it->second});
+            c.idle_bytes += it->second;
+            c.live.erase(it);
+            while (c.idle_bytes > kPinKeep) {
+                drop.push_back(c.idle.front().first);
+                c.idle_bytes -= c.idle.front().second;
+                c.idle.erase(c.idle.begin());
+            }
+        }
+    }
+    for (void *q : drop) (void)hipHostFree(q);
+}
 
 class FbWriter {
   public:
@@ -425,8 +486,8 @@ extern "C" int qeh_encode_arrow_ipc(qeh_ctx *ctx, const qeh_column *cols, const 
     // one host allocation: metadata, the body copied straight from HBM, end-of-stream marker
     const size_t total = head.size() + (size_t)body + 8;
     // pinned: the body leaves HBM at the DMA rate instead of through pageable staging
-    uint8_t *p = nullptr;
-    if (hipHostMalloc((void **)&p, total, hipHostMallocDefault) != hipSuccess || !p) {
+    uint8_t *p = (uint8_t *)pinned_get(total);
+    if (!p) {
         release();
         return fail(QEH_E_OOM, "ipc: host allocation");
     }
@@ -445,7 +506,7 @@ extern "C" int qeh_encode_arrow_ipc(qeh_ctx *ctx, const qeh_column *cols, const 
     if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
     release();
     if (he != hipSuccess) {
-        (void)hipHostFree(p);
+        pinned_put(p);
         return fail(QEH_E_HIP, std::string("ipc: ") + hipGetErrorString(he));
     }
     const uint32_t eos[2] = {0xFFFFFFFFu, 0u};
@@ -455,9 +516,9 @@ extern "C" int qeh_encode_arrow_ipc(qeh_ctx *ctx, const qeh_column *cols, const 
     return QEH_OK;
 }
 
-// buffers returned by the IPC entry points are pinned host memory
+// buffers returned by the IPC entry points are pinned host memory (kept for reuse, pinned_put)
 extern "C" void qeh_host_free(void *p) {
-    if (p) (void)hipHostFree(p);
+    if (p) pinned_put(p);
 }
 
 extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t size, qeh_column *out_cols, int max_cols,
@@ -601,8 +662,8 @@ extern "C" int qeh_decode_arrow_ipc(qeh_ctx *ctx, const uint8_t *bytes, int64_t 
         return s;
     }
     if (out_names) {
-        char *p = nullptr;
-        if (hipHostMalloc((void **)&p, std::max<size_t>(names.size(), 1), hipHostMallocDefault) != hipSuccess || !p) {
+        char *p = (char *)pinned_get(std::max<size_t>(names.size(), 1));
+        if (!p) {
             for (int i = 0; i < made; ++i) qeh_column_release(ctx, &out_cols[i]);
             return fail(QEH_E_OOM, "ipc: host allocation");
         }

@@ -156,6 +156,27 @@ def test_arrow_ipc_stream_round_trips_through_pyarrow(ctx, n):
 
 
 @pytest.mark.gpu
+def test_arrow_ipc_reused_pinned_buffers(ctx):
+    """The encoder's pinned host buffers are kept after qeh_host_free and handed out again: a stream
+    still held is never overwritten by a later encode, and a reused buffer carries the new stream whole."""
+    import gc
+    import pyarrow as pa
+    r = np.random.default_rng(5)
+    batches = [r.integers(-(2 ** 62), 2 ** 62, m).astype(np.int64) for m in (200_000, 190_000, 200_000, 120_000)]
+    held = []
+    for i, v in enumerate(batches):
+        data = ctx.encode_arrow_ipc([ctx.upload(v)], ["x"])
+        held.append((i, data))
+        if i == 1:  # free the first two streams: the next encodes may take their buffers
+            held.clear()
+            gc.collect()
+        got = pa.ipc.open_stream(pa.py_buffer(data)).read_all().column(0).to_numpy()
+        assert np.array_equal(got, v)
+    for i, data in held:
+        assert np.array_equal(pa.ipc.open_stream(pa.py_buffer(data)).read_all().column(0).to_numpy(), batches[i])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [0, 5, 65_537])
 def test_arrow_ipc_decode_pyarrow_streams_and_round_trip(ctx, n):
     """qeh_decode_arrow_ipc (SerializedBatch::to_batch, network.rs:75-90) reads a stream written by
