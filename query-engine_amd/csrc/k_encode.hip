@@ -90,11 +90,13 @@ __device__ inline void pg_write_row(const EncCols &cols, int64_t r, char *p, uin
 // One workgroup per 256 rows: the rows are rendered into LDS at their relative offsets, then the
 // workgroup's contiguous byte range leaves with coalesced 4-byte stores (a row-per-thread direct
 // write would scatter ~50-byte pieces).  Ranges larger than the LDS stage are written directly.
-constexpr int kEncLds = 48 * 1024;
-
+// LDS = the stage's bytes: 16 KB (rows averaging <= 56 B: more workgroups per CU for the formatting
+// work; a workgroup whose rows overflow it writes directly) or 48 KB.
+template <int LDS>
 __global__ __launch_bounds__(kBlock) void k_pg_row_write(EncCols cols, int64_t n, const uint64_t *__restrict__ at,
                                                          const uint32_t *__restrict__ len, char *__restrict__ out,
                                                          int32_t *__restrict__ out_offs, uint64_t total) {
+    constexpr int kEncLds = LDS;
     __shared__ __attribute__((aligned(16))) char stage[kEncLds + 8];
     for (int64_t b0 = (int64_t)blockIdx.x * kBlock; b0 < n; b0 += (int64_t)gridDim.x * kBlock) {
         const int64_t r = b0 + threadIdx.x;
@@ -178,7 +180,10 @@ extern "C" int qeh_encode_pg_datarows(qeh_ctx *ctx, const qeh_column *cols, int 
     if (n == 0) QEH_HIP(hipMemsetAsync(o, 0, 4, ctx->stream));
     else {
         KernelTimer kt(ctx, "encode_write");
-        hipLaunchKernelGGL(k_pg_row_write, dim3(grid), dim3(kBlock), 0, ctx->stream, ec, n, at.as<uint64_t>(),
+        const char *ek = std::getenv("QEH_ENC_LDS_KB");  // (A/B)
+        const bool small = ek ? atoi(ek) == 16 : total <= (uint64_t)n * 56;
+        auto wk = small ? k_pg_row_write<16 * 1024> : k_pg_row_write<48 * 1024>;
+        hipLaunchKernelGGL(wk, dim3(grid), dim3(kBlock), 0, ctx->stream, ec, n, at.as<uint64_t>(),
                            len.as<uint32_t>(), (char *)d, (int32_t *)o, total);
     }
     QEH_HIP(hipGetLastError());
