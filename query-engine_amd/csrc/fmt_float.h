@@ -88,23 +88,40 @@ __device__ inline int fmt_put(char *out, int n, const char *s) {
     return n + i;
 }
 
+__device__ const uint64_t kFmtPow10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                          100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
+                                          1000000000000ull, 10000000000000ull, 100000000000000ull,
+                                          1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
+                                          1000000000000000000ull, 10000000000000000000ull};
+
+// number of decimal digits: log10 from the bit length (1233 / 4096 ~ log10 2), one table compare
 __device__ inline int fmt_u64_digits(uint64_t v) {
-    int d = 1;
-    while (v >= 10) {
-        v /= 10;
-        ++d;
-    }
-    return d;
+    const int bl = 64 - __builtin_clzll(v | 1);
+    const int t = (bl * 1233) >> 12;
+    return t + 1 - (v < kFmtPow10[t] && t > 0 ? 1 : 0);  // (v = 0: one digit)
 }
 
-// decimal digits of v at out[n .. n + digits)
+// decimal digits of v at out[n .. n + digits), from the back: 8-digit pieces split off with one 64-bit
+// division each, their digits in 32-bit arithmetic
 __device__ inline int fmt_u64(char *out, int n, uint64_t v) {
     const int d = fmt_u64_digits(v);
-    if (out)
-        for (int i = d - 1; i >= 0; --i) {
-            out[n + i] = (char)('0' + v % 10);
-            v /= 10;
+    if (out) {
+        int i = d;
+        while (v >= 100000000ull) {
+            const uint64_t q = v / 100000000ull;
+            uint32_t r = (uint32_t)(v - q * 100000000ull);
+            for (int j = 0; j < 8; ++j) {
+                out[n + --i] = (char)('0' + r % 10u);
+                r /= 10u;
+            }
+            v = q;
         }
+        uint32_t r = (uint32_t)v;
+        while (i > 0) {
+            out[n + --i] = (char)('0' + r % 10u);
+            r /= 10u;
+        }
+    }
     return n + d;
 }
 
@@ -140,15 +157,12 @@ __device__ inline int fmt_positional(char *out, int n, FmtDec d) {
             if (out) out[n + i] = '0';
         return n + (pt - nd);
     }
-    // digits[0, pt) "." digits[pt, nd)
-    uint64_t v = d.f;
-    if (out)
-        for (int i = nd; i > 0; --i) {
-            const int pos = n + i - 1 + (i - 1 >= pt ? 1 : 0);
-            out[pos] = (char)('0' + v % 10);
-            v /= 10;
-        }
-    if (out) out[n + pt] = '.';
+    // digits[0, pt) "." digits[pt, nd): all digits, then the fraction moved one place right
+    if (out) {
+        fmt_u64(out, n, d.f);
+        for (int i = nd - 1; i >= pt; --i) out[n + i + 1] = out[n + i];
+        out[n + pt] = '.';
+    }
     return n + nd + 1;
 }
 

@@ -51,6 +51,22 @@ def test_known_answers_rust_display(fmt):
     assert i64(-(2 ** 63)) == str(-(2 ** 63)) and i64(0) == "0" and i64(2 ** 63 - 1) == str(2 ** 63 - 1)
 
 
+def test_i64_digit_boundaries_and_random(fmt):
+    """Integer text: every power-of-ten boundary (the digit count comes from the bit length and one
+    table compare; 8-digit pieces), both signs, and random values of every bit length."""
+    _, _, i64 = fmt
+    vals = [0, 1, -1, 2 ** 63 - 1, -(2 ** 63)]
+    for k in range(19):
+        for d in (-1, 0, 1):
+            x = 10 ** k + d
+            if x < 2 ** 63:
+                vals += [x, -x]
+    r = random.Random(7)
+    vals += [r.getrandbits(b) * r.choice((1, -1)) for b in range(1, 64) for _ in range(40)]
+    for x in vals:
+        assert i64(x) == str(x), x
+
+
 def test_f64_edges_and_random_bits(fmt):
     f64 = fmt[0]
     for v in EDGE:
