@@ -93,7 +93,7 @@ __device__ inline void pg_write_row(const EncCols &cols, int64_t r, char *p, uin
 // LDS = the stage's bytes: 16 KB (rows averaging <= 56 B: more workgroups per CU for the formatting
 // work; a workgroup whose rows overflow it writes directly) or 48 KB.
 template <int LDS>
-__global__ __launch_bounds__(kBlock) void k_pg_row_write(EncCols cols, int64_t n, const uint64_t *__restrict__ at,
+__global__ __launch_bounds__(kBlock, 6) void k_pg_row_write(EncCols cols, int64_t n, const uint64_t *__restrict__ at,
                                                          const uint32_t *__restrict__ len, char *__restrict__ out,
                                                          int32_t *__restrict__ out_offs, uint64_t total) {
     constexpr int kEncLds = LDS;
