@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_pg_row_write(EncCols cols, int64_
                                                          const uint32_t *__restrict__ len, char *__restrict__ out,
                                                          int32_t *__restrict__ out_offs, uint64_t total) {
     constexpr int kEncLds = LDS;
-    __shared__ __attribute__((aligned(16))) char stage[kEncLds + 8];
+    __shared__ __attribute__((aligned(16))) char stage[kEncLds + 16];
     for (int64_t b0 = (int64_t)blockIdx.x * kBlock; b0 < n; b0 += (int64_t)gridDim.x * kBlock) {
         const int64_t r = b0 + threadIdx.x;
         const uint64_t base = at[b0];
@@ -109,18 +109,19 @@ __global__ __launch_bounds__(kBlock, 6) void k_pg_row_write(EncCols cols, int64_
             if (r < n) pg_write_row(cols, r, out + at[r], len[r]);
             continue;
         }
-        // stage at the destination's alignment so that whole dwords can be stored
-        const uint32_t lead = (uint32_t)(base & 3);
+        // stage at the destination's 16-B alignment so that whole 16-B pieces can be stored
+        const uint32_t lead = (uint32_t)(base & 15);
         if (r < n) pg_write_row(cols, r, stage + lead + (at[r] - base), len[r]);
         __syncthreads();
-        const uint32_t head = lead ? 4 - lead : 0;  // bytes before the first aligned dword
+        const uint32_t head = lead ? 16 - lead : 0;  // bytes before the first aligned 16-B piece
         const uint32_t h = (uint32_t)(head < span ? head : span);
         if (threadIdx.x < h) out[base + threadIdx.x] = stage[lead + threadIdx.x];
-        const uint32_t body = (uint32_t)(span - h) / 4;
-        uint32_t *dst = (uint32_t *)(out + base + h);
-        const uint32_t *src = (const uint32_t *)(stage + lead + h);
+        const uint32_t body = (uint32_t)(span - h) / 16;
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        v4u *dst = (v4u *)(out + base + h);
+        const v4u *src = (const v4u *)(stage + lead + h);
         for (uint32_t i = threadIdx.x; i < body; i += kBlock) dst[i] = src[i];
-        for (uint32_t i = h + body * 4 + threadIdx.x; i < span; i += kBlock) out[base + i] = stage[lead + i];
+        for (uint32_t i = h + body * 16 + threadIdx.x; i < span; i += kBlock) out[base + i] = stage[lead + i];
         __syncthreads();
     }
 }
