@@ -41,7 +41,8 @@ __device__ __forceinline__ bool cmp_i64(int op, int64_t a, int64_t b) {
         case D_LT: return a < b;
         case D_LE: return a <= b;
         case D_GT: return a > b;
-        default: return a >= b;
+        case D_GE: return a >= b;
+        default: return false;  // (not a comparison: the host admits only compare ops here)
     }
 }
 
