@@ -229,3 +229,40 @@ def test_merge_sorted_msd_payload_vs_oracle(ctx, monkeypatch, case):
         assert cols[0].dtype == (abi.DT_INT32 if dt == np.int32 else abi.DT_INT64)
         outs.append(gv)
     assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+
+
+@pytest.mark.gpu
+def test_merge_sorted_full_size_vs_oracle(ctx):
+    """The Merge::sorted bench configuration at its full size (tools/bench_configs.py cfg_merge: 8
+    partitions x 1.25e7 rows, k Int64 over 2^40 with 5 % NULLs, v Float64, ORDER BY k DESC NULLS LAST)
+    against the oracle's stable sort of the concatenation: keys, validity and payloads bit-exact (the
+    payload order pins stability: ties keep partition-major input order).  Runs the default MSD path
+    (two global passes, the counting sort per sub-bucket, radix LDS passes for crowded ones)."""
+    seed, per = 0x5EED, 12_500_000
+    parts, hk, hv, hm = [], [], [], []
+    for p in range(8):
+        k = ctx.generate(abi.GEN_UNIFORM_MOD, seed + p, 7, per, 2 ** 40)
+        kv, _ = k.to_numpy()
+        valid = np.random.default_rng(p).random(per) > 0.05
+        v = ctx.generate(abi.GEN_UNIT_F64, seed + p, 8, per)
+        parts.append([ctx.upload(kv, valid), v])
+        hk.append(kv)
+        hm.append(valid)
+        hv.append(v.to_numpy()[0])
+        k.release()
+    cols, rows = ctx.merge_sorted(parts, [0], [False], [False])
+    n = 8 * per
+    assert rows == n
+    k, m, v = np.concatenate(hk), np.concatenate(hm), np.concatenate(hv)
+    del hk, hm, hv
+    perm = ob.sort_indices_nulls([ob.HostCol(k, m)], [False], [False])
+    gk, gm = host(cols[0])
+    assert np.array_equal(gm, m[perm])
+    assert np.array_equal(gk[gm], k[perm][m[perm]])
+    gv, _ = host(cols[1])
+    assert np.array_equal(gv.view(np.uint64), v[perm].view(np.uint64))
+    for c in cols:
+        c.release()
+    for a, b in parts:
+        a.release()
+        b.release()
