@@ -78,18 +78,26 @@ __device__ __forceinline__ void key_stats_body(const ColRef &c, const uint32_t *
         // (one validity byte, four 16-B loads), rows of NULLs skipped by mask
         typedef long long v2 __attribute__((ext_vector_type(2)));
         const uint8_t *vb = c.validity + (c.vbit0 >> 3);
+        // (four groups per iteration: 16 loads in flight per thread, the grid is one workgroup per CU)
         const int64_t groups = n / 8, stride = nb * blockDim.x;
-        for (int64_t g = bid * blockDim.x + threadIdx.x; g < groups; g += stride) {
-            const uint32_t m = vb[g];
-            const v2 *kv = (const v2 *)c.values + g * 4;
-            v2 q[4];
+        for (int64_t g0 = bid * blockDim.x + threadIdx.x; g0 < groups; g0 += 4 * stride) {
+            uint32_t m[4];
+            v2 q[4][4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) q[u] = kv[u];
+            for (int w = 0; w < 4; ++w) {
+                const int64_t g = g0 + w * stride < groups ? g0 + w * stride : g0;
+                m[w] = g0 + w * stride < groups ? vb[g] : 0u;  // (a clamped repeat counts nothing)
+                const v2 *kv = (const v2 *)c.values + g * 4;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if ((m >> (2 * u)) & 1u) mn = q[u].x < mn ? q[u].x : mn, mx = q[u].x > mx ? q[u].x : mx;
-                if ((m >> (2 * u + 1)) & 1u) mn = q[u].y < mn ? q[u].y : mn, mx = q[u].y > mx ? q[u].y : mx;
+                for (int u = 0; u < 4; ++u) q[w][u] = kv[u];
             }
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if ((m[w] >> (2 * u)) & 1u) mn = q[w][u].x < mn ? q[w][u].x : mn, mx = q[w][u].x > mx ? q[w][u].x : mx;
+                    if ((m[w] >> (2 * u + 1)) & 1u) mn = q[w][u].y < mn ? q[w][u].y : mn, mx = q[w][u].y > mx ? q[w][u].y : mx;
+                }
         }
         for (int64_t i = groups * 8 + bid * blockDim.x + threadIdx.x; i < n; i += stride) {
             if (!col_valid(c, i)) continue;
