@@ -318,6 +318,83 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const KeyT *__restrict__
     }
 }
 
+// The payload sort's first histogram (KES = 8 / 4: Int64 / Int32 keys, encoded as rs_code does): a
+// lane reads 8 consecutive rows of a partition with 16-B loads and their validity byte at once (row
+// order does not matter to a histogram), four such groups in flight; a segment's head and tail rows,
+// and columns whose values or validity do not line up, one row at a time.  Same block row ranges
+// [b * seg, (b + 1) * seg) and hist layout as k_rs_hist<KeyT, KES>.
+template <int KES>
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist_enc(int64_t n, int64_t seg, int shift, uint32_t *__restrict__ hist,
+                                                            int nblocks, RsEncode enc) {
+    constexpr int W = kRsThreads / 64;
+    constexpr int NL = KES / 2;  // 16-B loads per 8-row group
+    typedef long long v2 __attribute__((ext_vector_type(2)));
+    __shared__ uint32_t h[W][kRadix];
+    for (int i = threadIdx.x; i < W * kRadix; i += kRsThreads) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
+    auto count = [&](int64_t x, bool ok) {
+        const uint64_t code = ok ? (enc.asc ? (uint64_t)x - (uint64_t)enc.mn + enc.bias : (uint64_t)enc.mx - (uint64_t)x + enc.bias)
+                                 : enc.null_code;
+        atomicAdd(&h[wave][(uint32_t)(code >> shift) & (kRadix - 1)], 1u);
+    };
+    const int ns = enc.ns ? enc.ns : 1;
+    for (int sg = 0; sg < ns; ++sg) {  // (uniform: segments indexed by a scalar)
+        const ColRef c = enc.ns ? enc.sk[sg] : enc.c;
+        const int64_t st = enc.ns ? enc.start[sg] : 0, en = enc.ns ? enc.start[sg + 1] : n;
+        const int64_t a = (lo > st ? lo : st) - st, e = (hi < en ? hi : en) - st;  // local rows [a, e)
+        if (a >= e) continue;
+        auto row = [&](int64_t i) {
+            const int64_t x = KES == 4 ? (int64_t)__builtin_nontemporal_load((const int32_t *)c.values + i)
+                                       : __builtin_nontemporal_load((const int64_t *)c.values + i);
+            count(x, col_valid(c, i));
+        };
+        const bool vec = ((uintptr_t)c.values & 15) == 0 && (!c.validity || (c.vbit0 & 7) == 0);
+        int64_t ga = (a + 7) / 8, gb = e / 8;  // whole 8-row groups [ga, gb)
+        if (!vec || ga >= gb) ga = gb = 0;
+        const int64_t h0 = ga < gb ? ga * 8 : e, t0 = ga < gb ? gb * 8 : e;
+        for (int64_t i = a + threadIdx.x; i < h0; i += kRsThreads) row(i);
+        for (int64_t i = (t0 > a ? t0 : a) + threadIdx.x; i < e; i += kRsThreads) row(i);
+        const uint8_t *vb = c.validity ? c.validity + (c.vbit0 >> 3) : nullptr;
+        for (int64_t g0 = ga + threadIdx.x; g0 < gb; g0 += 4 * kRsThreads) {
+            uint32_t m[4];
+            v2 q[4][NL];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const bool live = g0 + w * kRsThreads < gb;
+                const int64_t g = live ? g0 + w * kRsThreads : g0;
+                m[w] = live ? (vb ? (uint32_t)vb[g] : 0xFFu) : 0u;
+                const v2 *kv = (const v2 *)((const char *)c.values + g * 8 * KES);
+#pragma unroll
+                for (int u = 0; u < NL; ++u) q[w][u] = __builtin_nontemporal_load(kv + u);
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                if (g0 + w * kRsThreads >= gb) continue;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    int64_t x;
+                    if constexpr (KES == 8) {
+                        x = (r & 1) ? q[w][r >> 1].y : q[w][r >> 1].x;
+                    } else {
+                        const long long wd = (r & 2) ? q[w][r >> 2].y : q[w][r >> 2].x;
+                        x = (int64_t)(int32_t)(uint32_t)((r & 1) ? ((unsigned long long)wd >> 32) : (unsigned long long)wd);
+                    }
+                    count(x, (m[w] >> r) & 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kRadix) {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) cnt += h[w][threadIdx.x];
+        hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt;
+    }
+}
+
 // Histogram of a pass whose digits the previous scatter wrote as a byte stream
 // (nd_out): 1 B per element instead of the 8-B key, 16 digits per 16-B load,
 // per-wave LDS counters (no cross-wave atomics on hot digits).
@@ -1937,8 +2014,14 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
     QEH_TRY(fbl.alloc(ctx, 4 * ((size_t)kRadix * kRadix + 1)));
     {
         KernelTimer kt(ctx, "radix_pass");
-        auto hk = k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
-        hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, n, seg, shift1, hist.as<uint32_t>(), nblocks, enc);
+        if (std::getenv("QEH_RS_HIST_LANE")) {  // (A/B: the lane-strided histogram of the scatter's layout)
+            auto hk = k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
+            hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb0, n, seg, shift1, hist.as<uint32_t>(), nblocks,
+                               enc);
+        } else {
+            auto hk = k32 ? k_rs_hist_enc<4> : k_rs_hist_enc<8>;
+            hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, n, seg, shift1, hist.as<uint32_t>(), nblocks, enc);
+        }
         QEH_TRY(exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr));
         // the codes leave as their low 32 bits (the second pass takes its digit from the byte stream nd)
         auto sk = k32 ? k_rs_scatter<uint64_t, true, uint64_t, false, 4, false, uint32_t>
@@ -2141,9 +2224,13 @@ int qeh::sort_pairs_payload_parts(qeh_ctx *ctx, const qeh_column *keys, const qe
         KernelTimer kt(ctx, "radix_pass");
         const int c = p & 1, shift = p * kRadixBits;
         const bool first = p == 0, last = p + 1 == npass;
-        auto hk = !first ? k_rs_hist<uint64_t, 0> : k32 ? k_rs_hist<uint64_t, 4> : k_rs_hist<uint64_t, 8>;
-        hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), n, seg, shift,
-                           hist.as<uint32_t>(), nblocks, enc);
+        if (first) {  // the key columns themselves, encoded on load
+            auto hk = k32 ? k_rs_hist_enc<4> : k_rs_hist_enc<8>;
+            hipLaunchKernelGGL(hk, dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, n, seg, shift, hist.as<uint32_t>(), nblocks, enc);
+        } else {
+            hipLaunchKernelGGL((k_rs_hist<uint64_t, 0>), dim3(nblocks), dim3(kRsThreads), 0, ctx->stream, kb[c].as<uint64_t>(), n, seg,
+                               shift, hist.as<uint32_t>(), nblocks, enc);
+        }
         s = exclusive_scan_u32(ctx, hist.as<uint32_t>(), offs.as<uint64_t>(), (int64_t)kRadix * nblocks, nullptr);
         if (s != QEH_OK) break;
         const uint64_t *vin = first ? vsrc : vb[c];
