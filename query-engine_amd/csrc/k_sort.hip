@@ -1862,7 +1862,8 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
 // Merge::sorted shape against 4.09 ms for the radix passes, sorted-order stores 3.93 ms.
 // A sub-bucket with a bucket above kCsCap rows (clustered or repeated codes) is queued in fb for
 // k_msd_lds_sort (list mode); one above kMsdCap rows goes to k_msd_big as before.
-// 12 bits measured best: 10 / 11 / 13 / 14 bits 3.96 / 3.85 / 4.05 / 5.06 ms vs 3.76 (ab_merge_csort.txt)
+// 12 bits measured best: 10 / 11 / 13 / 14 bits 3.96 / 3.85 / 4.05 / 5.06 ms vs 3.76, and 13 bits again
+// with 32-bit rank words 3.71 vs 3.62 (ab_merge_csort.txt)
 constexpr int kCsBits = 12, kCsCap = 24;
 static_assert(kMsdCap <= 4096 && (kMsdCap & (kMsdCap - 1)) == 0, "row index packs into the low 12 bits");
 template <int CB>
@@ -1871,8 +1872,9 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
                                                            uint64_t *__restrict__ vout, uint32_t *__restrict__ flag,
                                                            uint32_t *__restrict__ big, uint32_t *__restrict__ fb) {
     constexpr int W = kMsdThreads / 64, J = kMsdCap / kMsdThreads, NB = 1 << CB, BPT = NB / kMsdThreads;
-    __shared__ uint32_t cnt[NB];   // counts, then starts
-    __shared__ uint64_t ce[kMsdCap];  // by slot: code << 12 | row
+    static_assert(NB >= kMsdCap, "cnt holds the sorted codes at the end");
+    __shared__ uint32_t cnt[NB];      // counts, then starts; at the end the codes in sorted order
+    __shared__ uint32_t ce[kMsdCap];  // by slot: the code bits below the bucket's << 12 | row; then rows in sorted order
     __shared__ uint32_t wsum[W], wmax[W];
     const int64_t s0 = (int64_t)sb[blockIdx.x], s1 = (int64_t)sb[blockIdx.x + 1];
     const int64_t m = s1 - s0;
@@ -1890,6 +1892,8 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
     const uint64_t hi_code = (uint64_t)blockIdx.x << lbits;
     const uint32_t lmask = lbits >= 32 ? 0xFFFFFFFFu : ((1u << lbits) - 1u);
     const int bshift = lbits > CB ? lbits - CB : 0;
+    const uint32_t lowm = (1u << bshift) - 1u;  // bshift <= kMsdMaxLow - CB: the rank words fit 32 bits
+    static_assert(kMsdMaxLow - CB + 12 <= 32, "rank words: low code bits + 12-bit row");
     for (int i = t; i < NB; i += kMsdThreads) cnt[i] = 0;
     uint32_t c[J], arr[J];
 #pragma unroll
@@ -1941,7 +1945,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
         slot[j] = 0;
         if (e < mm) {
             slot[j] = cnt[c[j] >> bshift] + arr[j];
-            ce[slot[j]] = ((uint64_t)c[j] << 12) | (uint32_t)e;
+            ce[slot[j]] = ((c[j] & lowm) << 12) | (uint32_t)e;
         }
     }
     __syncthreads();
@@ -1953,7 +1957,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
         if (e >= mm) continue;
         const uint32_t b = c[j] >> bshift;
         const uint32_t st = cnt[b], en = b + 1 < (uint32_t)NB ? cnt[b + 1] : (uint32_t)mm;
-        const uint64_t me = ((uint64_t)c[j] << 12) | (uint32_t)e;
+        const uint32_t me = ((c[j] & lowm) << 12) | (uint32_t)e;  // (a bucket shares the bits above)
         uint32_t rk = st;
         for (uint32_t x = st; x < en; ++x) rk += ce[x] < me ? 1u : 0u;
         rank[j] = rk;
@@ -1962,14 +1966,14 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_csort(const uint32_t *__res
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const int e = j * kMsdThreads + t;
-        if (e < mm) ce[rank[j]] = ((uint64_t)c[j] << 12) | (uint32_t)e;
+        if (e < mm) {
+            ce[rank[j]] = (uint32_t)e;
+            cnt[rank[j]] = c[j];
+        }
     }
     __syncthreads();
     // written in sorted order (coalesced), the payload gathered from its row
-    for (int p = t; p < mm; p += kMsdThreads) {
-        const uint64_t x = ce[p];
-        msd_emit(dec, vout, s0 + p, hi_code | (uint32_t)(x >> 12), vin[s0 + (x & (kMsdCap - 1))]);
-    }
+    for (int p = t; p < mm; p += kMsdThreads) msd_emit(dec, vout, s0 + p, hi_code | cnt[p], vin[s0 + ce[p]]);
 }
 
 // The sub-buckets above kMsdCap rows (big[0] of them, ids in big[1..]), every workgroup of the grid on
