@@ -1771,11 +1771,13 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
     __shared__ uint32_t buf[2][kMsdCap];
     __shared__ uint32_t wc[W][ND];
     __shared__ uint32_t loc[ND], wsum[W];
-    if (list && blockIdx.x >= list[0]) return;
-    const uint32_t id = list ? list[1 + blockIdx.x] : blockIdx.x;
+    const uint32_t nlist = list ? list[0] : 0u;
+    // list mode: the grid strides over the queued sub-buckets; else sub-bucket blockIdx.x
+    for (uint32_t it = blockIdx.x; list ? it < nlist : it == blockIdx.x; it += gridDim.x) {
+    const uint32_t id = list ? list[1 + it] : it;
     const int64_t s0 = (int64_t)sb[id], s1 = (int64_t)sb[id + 1];
     const int64_t m = s1 - s0;
-    if (m <= 0) return;
+    if (m <= 0) continue;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     if (m > kMsdCap) {  // k_msd_big takes it, with the whole grid
         if (t == 0) {
@@ -1783,7 +1785,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
             if (q < kMsdMaxBig) big[1 + q] = id;
             else atomicOr(flag, 1u);
         }
-        return;
+        continue;
     }
     const int mm = (int)m;
     const uint64_t hi_code = (uint64_t)id << lbits;
@@ -1850,6 +1852,8 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_lds_sort(const uint32_t *__
     for (int e = t; e < mm; e += kMsdThreads) {
         const uint32_t r = buf[cur][e] & (kMsdCap - 1);
         msd_emit(dec, vout, s0 + e, hi_code | (codes[s0 + r] & lmask), vin[s0 + r]);
+    }
+    __syncthreads();  // (list mode: buf is read before the next sub-bucket overwrites it)
     }
 }
 
@@ -2090,7 +2094,7 @@ static int msd_payload_passes(qeh_ctx *ctx, const qeh_column &key, const uint64_
             QEH_HIP(hipMemsetAsync(fbl.p, 0, 4, ctx->stream));
             hipLaunchKernelGGL(k_msd_csort<kCsBits>, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2, vtmp2.as<uint64_t>(),
                                sbd.as<uint64_t>(), shift2, dec, vout, flag.as<uint32_t>(), bigl, fbl.as<uint32_t>());
-            hipLaunchKernelGGL(k_msd_lds_sort, dim3(kRadix * kRadix), dim3(kMsdThreads), 0, ctx->stream, codes2,
+            hipLaunchKernelGGL(k_msd_lds_sort, dim3(cus * 4), dim3(kMsdThreads), 0, ctx->stream, codes2,
                                vtmp2.as<uint64_t>(), sbd.as<uint64_t>(), shift2, dec, vout, flag.as<uint32_t>(), bigl,
                                (const uint32_t *)fbl.as<uint32_t>());
         }
