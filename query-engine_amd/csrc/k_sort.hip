@@ -334,18 +334,22 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist_enc(int64_t n, int64_t s
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     const int64_t lo = (int64_t)blockIdx.x * seg, hi = lo + seg < n ? lo + seg : n;
-    auto count = [&](int64_t x, bool ok) {
-        const uint64_t code = ok ? (enc.asc ? (uint64_t)x - (uint64_t)enc.mn + enc.bias : (uint64_t)enc.mx - (uint64_t)x + enc.bias)
-                                 : enc.null_code;
-        atomicAdd(&h[wave][(uint32_t)(code >> shift) & (kRadix - 1)], 1u);
+    const bool asc = enc.asc != 0;
+    const uint64_t emn = (uint64_t)enc.mn, emx = (uint64_t)enc.mx, bias = enc.bias, null_code = enc.null_code;
+    uint32_t *hw = &h[wave][0];
+    auto count = [=](int64_t x, bool ok) {
+        const uint64_t code = ok ? (asc ? (uint64_t)x - emn + bias : emx - (uint64_t)x + bias) : null_code;
+        atomicAdd(&hw[(uint32_t)(code >> shift) & (kRadix - 1)], 1u);
     };
     const int ns = enc.ns ? enc.ns : 1;
-    for (int sg = 0; sg < ns; ++sg) {  // (uniform: segments indexed by a scalar)
+    for (int sg0 = 0; sg0 < ns; ++sg0) {
+        // a scalar index into the kernel arguments (else the compiler copies RsEncode to scratch)
+        const int sg = __builtin_amdgcn_readfirstlane(sg0);
         const ColRef c = enc.ns ? enc.sk[sg] : enc.c;
         const int64_t st = enc.ns ? enc.start[sg] : 0, en = enc.ns ? enc.start[sg + 1] : n;
         const int64_t a = (lo > st ? lo : st) - st, e = (hi < en ? hi : en) - st;  // local rows [a, e)
         if (a >= e) continue;
-        auto row = [&](int64_t i) {
+        auto row = [=](int64_t i) {
             const int64_t x = KES == 4 ? (int64_t)__builtin_nontemporal_load((const int32_t *)c.values + i)
                                        : __builtin_nontemporal_load((const int64_t *)c.values + i);
             count(x, col_valid(c, i));
