@@ -112,8 +112,13 @@ struct FastTile {
     }
     __device__ __forceinline__ int64_t k(int r) const { return key[r >> 1][r & 1]; }
     // value of row r for aggregate input slot `cs` (0 or 1)
+    // (a masked blend of the two registers: a select between two elements of ac became a select
+    // between two addresses, which spilled ac to scratch every tile)
     __device__ __forceinline__ int64_t a(int cs, int r) const {
-        return (NACOL > 1 && cs == 1) ? ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1] : ac[0][r >> 1][r & 1];
+        const int64_t v0 = ac[0][r >> 1][r & 1];
+        if constexpr (NACOL < 2) return v0;
+        const int64_t v1 = ac[NACOL > 1 ? 1 : 0][r >> 1][r & 1];
+        return v0 ^ ((v0 ^ v1) & -(int64_t)(cs == 1));
     }
 };
 
