@@ -171,11 +171,20 @@ __device__ __forceinline__ bool probe_unique(const HashTable &t, int64_t key, ui
             uint64_t w[8];
             bucket_load(t, b, w);
             const uint32_t cnt = (uint32_t)(w[7] >> 32);
-            for (int s = 0; s < S; ++s)
-                if (s < (int)cnt && (int64_t)w[s] == key) {
-                    gid = bucket_payload(w, s, t.pbits) - 1u;
-                    return true;
-                }
+            // every slot compared with constant register indices (a runtime slot index into w
+            // costs a chain of selects per access), the payload picked the same way
+            uint32_t hit = 0;
+#pragma unroll
+            for (int s = 0; s < 6; ++s) hit |= (s < S && s < (int)cnt && (int64_t)w[s] == key) ? 1u << s : 0u;
+            if (hit) {
+                const int s0 = __builtin_ctz(hit);
+                uint32_t pl = 0;
+#pragma unroll
+                for (int s = 0; s < 6; ++s)
+                    if (s == s0) pl = bucket_payload(w, s, t.pbits);
+                gid = pl - 1u;
+                return true;
+            }
             if (cnt <= (uint32_t)S) return false;
             b = b + 1 == t.nbkt ? 0 : b + 1;
         }
