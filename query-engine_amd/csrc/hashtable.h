@@ -85,8 +85,9 @@ __device__ __forceinline__ int table_probe(const HashTable &t, int64_t key, F &&
             uint64_t w[8];
             bucket_load(t, b, w);
             const uint32_t cnt = (uint32_t)(w[7] >> 32);
-            for (int s = 0; s < S && s < (int)cnt; ++s)
-                if ((int64_t)w[s] == key) {
+#pragma unroll
+            for (int s = 0; s < 6; ++s)  // (constant register indices into w)
+                if (s < S && s < (int)cnt && (int64_t)w[s] == key) {
                     f(bucket_payload(w, s, t.pbits) - 1u);
                     ++found;
                     if (t.unique) return found;
